@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Graphalytics PageRank edges/s on MI355X (BASELINE.json configs[1]).
+
+Workload: PageRank, d = 0.85, 10 iterations, fp64, on SYN-7_5 -- the
+seeded stand-in for datagen-7_5-fb (no network for the real dataset): undirected R-MAT
+(a,b,c,d) = (0.57,0.19,0.19,0.05), scale 20, edgefactor 32, seed 75, duplicates and
+self-loops removed, vertex ids randomly permuted.  One "step" = one complete PageRank run
+(init + 10 pull iterations) with the graph resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL): the pull matrix is
+row-partitioned by nnz and the rank vector is all-gathered every iteration (strong scaling
+on the same graph).  Rank 0 prints ONE JSON line.
+
+value    = (stored entries * iterations * K) / max-over-ranks wall time of the K steps
+roofline = k_pr_pull: algorithmic bytes per launch (4 nnz + 8 (n+1) + 8 n + 8 n, SURVEY.md
+           8d) / mean launch duration from hipEvents on the launch stream during the timed
+           steps; peak 8.0 TB/s (MI355X HBM3E); traffic from the committed rocprofv3 PMC pass.
+cpu_baseline = the oracle's OpenMP PageRank (oracle/gx_oracle.c, "port" -- SuiteSparse is not
+           installed) timed on this host on the same graph, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "edges/sec (GTEPS) per algorithm at 1/2/4/8 GPUs; % HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scale", type=int, default=20)
+    ap.add_argument("--edgefactor", type=int, default=32)
+    ap.add_argument("--seed", type=int, default=75)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--damping", type=float, default=0.85)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def pmc_traffic(workload: str):
+    """Per-launch HBM bytes of k_pr_pull from the committed rocprofv3 PMC pass, if present."""
+    p = ROOT / "profiles" / "pmc_pr_pull.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
+    from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import GpuStep, PartitionedPageRank, local_rows
+
+    workload = f"PageRank SYN-7_5 (R-MAT scale {args.scale}, ef {args.edgefactor}, seed {args.seed}, undirected)"
+    t_gen = time.time()
+    csr = rmat(args.scale, args.edgefactor, args.seed, undirected=True)
+    t_gen = time.time() - t_gen
+    n, nnz = csr.n, csr.nnz
+    lr = local_rows(csr, directed=False, nranks=world, rank=rank)
+
+    ctx = Context(local_rank)
+    dev_name, cus = ctx.info()
+    stepper = GpuStep(ctx, n, world, lr, args.damping)
+    # a real (non-null) stream: libgx launches on it and RCCL orders against it
+    stream = torch.cuda.Stream(device)
+    torch.cuda.set_stream(stream)
+    gather = (lambda out, inp: dist.all_gather_into_tensor(out, inp)) if dist else None
+    pr = PartitionedPageRank(stepper, world, lr.rows, device, all_gather=gather,
+                             stream_handle=lambda: stream.cuda_stream)
+
+    def barrier():
+        torch.cuda.synchronize(device)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    for _ in range(args.warmup):
+        pr.run(args.iters)
+    barrier()
+    ctx.reset_kernel_stats()
+    ctx.set_kernel_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pr.run(args.iters)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_kernel_timing(False)
+    launches, pull_ms = ctx.kernel_stats("pr_pull")
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # result of the last step (for the parity check on rank 0)
+    local_rank_out = pr.rank_out[:lr.rows].detach().cpu().numpy()
+    if dist:
+        parts = [None] * world
+        dist.all_gather_object(parts, local_rank_out)
+        result = np.concatenate(parts)
+    else:
+        result = local_rank_out
+
+    edges_total = nnz * args.iters * args.steps
+    value = edges_total / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # roofline of k_pr_pull on this rank (per launch)
+    bytes_per_launch = 4 * lr.nnz + 8 * (lr.rows + 1) + 8 * lr.rows + 8 * lr.rows
+    mean_launch_s = (pull_ms / launches) / 1e3 if launches else float("nan")
+    achieved = bytes_per_launch / mean_launch_s / 1e9
+    traffic = pmc_traffic(workload) if world == 1 else None
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        threads = min(16, os.cpu_count() or 1)
+        # bounded sample: whole PageRank runs on the same graph until the budget is spent
+        runs, t_cpu, ref = 0, 0.0, None
+        while runs == 0 or (t_cpu < args.cpu_seconds and runs < 5):
+            t1 = time.perf_counter()
+            ref = O.pagerank(csr, False, args.damping, args.iters, nthreads=threads)
+            t_cpu += time.perf_counter() - t1
+            runs += 1
+        cpu = {"value": nnz * args.iters * runs / t_cpu, "unit": "edges/s", "cores": threads, "kind": "port",
+               "sample": f"{runs} full PageRank run(s) ({args.iters} iterations) on the same SYN-7_5 graph, "
+                         f"OpenMP pull restatement (oracle/gx_oracle.c), {t_cpu:.2f} s"}
+        parity = float(np.max(np.abs(result - ref) / np.abs(ref)))
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded R-MAT stand-in for datagen-7_5-fb; no network for the real dataset)",
+            "config": {
+                "workload": workload,
+                "algorithm": "pagerank",
+                "graph": "SYN-7_5",
+                "n": n,
+                "nnz": nnz,
+                "iterations": args.iters,
+                "damping": args.damping,
+                "parallelism": f"row{world}",
+                "device": dev_name,
+                "cus": cus,
+            },
+            "roofline": {
+                "kernel": "k_pr_pull",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "bytes_per_launch": bytes_per_launch,
+                "mean_launch_us": mean_launch_s * 1e6,
+                "launches": launches,
+            },
+            "cpu_baseline": cpu,
+            "parity_max_rel_err_vs_oracle": parity,
+            "graph_gen_s": t_gen,
+        }
+        print(json.dumps(line), flush=True)
+    stepper.close()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

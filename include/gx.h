@@ -1,0 +1,185 @@
+/*
+ * gx.h -- C ABI of the MI355X-native GraphBLAS execution layer (libgx.so).
+ *
+ * Drop-in boundary for the LDBC Graphalytics algorithm hot path of the reference
+ * platform driver.  The reference wrapper executables (src/main/c/src/algorithms/<alg>.cpp)
+ * load `graph.grb` + `graph.vtb`, call ONE LAGraph function between the
+ * "Processing starts/ends at" markers and serialise the result.  libgx replaces that
+ * LAGraph/SuiteSparse:GraphBLAS call with hand-written HIP kernels for gfx950; the
+ * executables under bin/exe keep the CLI and file contract (execute-job.sh:68-145).
+ *
+ * Conventions
+ *   - Every entry point returns an int status with GrB_Info numbering: 0 = success,
+ *     < 0 = error (GX_* below mirror GrB_NULL_POINTER, GrB_INVALID_VALUE, ...).  The
+ *     executables keep the reference's OK()-throws convention on top (utils.h:45-55).
+ *     gx_last_error() returns a message for the last failure on that thread.
+ *   - Host arrays are owned by the caller; libgx copies them to HBM.  Outputs are
+ *     caller-allocated host arrays of length n.  Device memory is owned by libgx until
+ *     gx_graph_free / gx_free.
+ *   - Vertex ids are internal 0-based indices (the .grb row order = .vtb order); the
+ *     caller maps them to original ids exactly as the reference serialisers do.
+ *   - One gx_ctx per device per process; calls on one ctx come from one host thread.
+ *   - There is no CPU fallback: if no gfx950 device is usable gx_init fails.
+ */
+#ifndef GX_H
+#define GX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (GrB_Info numbering) */
+#define GX_SUCCESS 0
+#define GX_NO_VALUE 1
+#define GX_UNINITIALIZED_OBJECT (-1)
+#define GX_NULL_POINTER (-2)
+#define GX_INVALID_VALUE (-3)
+#define GX_INVALID_INDEX (-4)
+#define GX_NOT_IMPLEMENTED (-101)
+#define GX_OUT_OF_MEMORY (-102)
+#define GX_INVALID_OBJECT (-104)
+#define GX_PANIC (-103)
+#define GX_IO_ERROR (-1001)       /* LAGRAPH_IO_ERROR / binread FREAD CATCH(-1001), graphio.h:43-49 */
+#define GX_DEVICE_ERROR (-2000)   /* HIP runtime error */
+
+typedef struct gx_ctx gx_ctx;
+typedef struct gx_graph gx_graph;
+
+/* ---------------------------------------------------------------------------------
+ * Host CSR exactly as the `.grb` file provides it (graphio.h:88-137, binread).
+ * rowptr[n+1], colidx[nnz] are GrB_Index (uint64); vals is NULL for iso/boolean
+ * (unweighted) graphs, else nnz fp64 weights.  Row i = out-edges of vertex i.
+ * ------------------------------------------------------------------------------- */
+typedef struct gx_csr {
+    uint64_t n;
+    uint64_t nnz;
+    uint64_t *rowptr;
+    uint64_t *colidx;
+    double *vals;
+} gx_csr;
+
+/* ---- runtime ---------------------------------------------------------------- */
+
+/* Replaces LAGraph_Init + GxB_Global_Option_set(GxB_GLOBAL_NTHREADS) (bfs.cpp:88-89). */
+int gx_init(int device, gx_ctx **ctx);
+int gx_free(gx_ctx *ctx);
+const char *gx_last_error(void);
+int gx_device_count(int *count);
+/* Device name / CU count of the context's device (for logs and bench metadata). */
+int gx_device_info(gx_ctx *ctx, char *name, size_t name_len, int *num_cus);
+
+/* ---- graph I/O (host, no SuiteSparse) --------------------------------------- */
+
+/* Replaces ReadMatrixMarket -> binread (graphio.cpp:10-15, graphio.h:49-285).
+ * Reads sparse / hypersparse, CSR or CSC, any GrB type; bool/integer values are
+ * treated as structure (iso), FP32/FP64 values become fp64 weights.  Output arrays
+ * are allocated by libgx; release with gx_csr_release. */
+int gx_read_grb(const char *path, gx_csr *out);
+/* Replaces binwrite (graphio.h:310-615): writes a SuiteSparse-compatible sparse CSR
+ * `.grb` (BOOL iso when vals == NULL, else FP64). */
+int gx_write_grb(const char *path, const gx_csr *csr);
+/* Replaces ReadMapping for `.vtb` (graphio.cpp:39-49): raw uint64 original ids. */
+int gx_read_vtb(const char *path, uint64_t **ids, uint64_t *count);
+int gx_write_vtb(const char *path, const uint64_t *ids, uint64_t count);
+/* Replaces LAGraph_MMRead (graphio.cpp:16-24; converter.cpp:38): Matrix Market
+ * coordinate file as written by relabel.py:64-79 (integer|real|pattern,
+ * general|symmetric; the `%%GraphBLAS <type>` line is honoured).  Symmetric files are
+ * expanded to both directions; rows come out sorted; duplicate entries keep the last. */
+int gx_read_mtx(const char *path, gx_csr *out);
+/* Replaces ReadMapping for `.vtx` (graphio.cpp:50-57): one original id per line. */
+int gx_read_vtx(const char *path, uint64_t **ids, uint64_t *count);
+void gx_csr_release(gx_csr *csr);
+void gx_host_free(void *p);
+
+/* Synthetic inputs (bench / tests): R-MAT edge list with probabilities
+ * (a,b,c, d=1-a-b-c), 2^scale vertices, edgefactor*2^scale generated edges, seeded and
+ * independent of thread count; self-loops and duplicates removed; vertex ids permuted by
+ * a seeded permutation; `undirected` stores both directions.  weighted != 0 attaches
+ * U(0,1] fp64 weights (symmetric for undirected graphs).  Result is a sorted CSR. */
+int gx_rmat_csr(int scale, int edgefactor, double a, double b, double c, uint64_t seed,
+                int undirected, int weighted, gx_csr *out);
+
+/* ---- device graph ------------------------------------------------------------ */
+
+/* Uploads A to HBM (int64 row pointers, int32 column indices when n < 2^31).
+ * Replaces LAGraph_New(&G, &A, kind) (bfs.cpp:78). */
+int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **g);
+int gx_graph_free(gx_graph *g);
+int gx_graph_info(gx_graph *g, uint64_t *n, uint64_t *nnz, int *directed, int *weighted);
+
+/* ---- algorithm-level entry points (one per reference executable) -------------- */
+
+/* LAGr_BreadthFirstSearch(&level, NULL, G, src) (bfs.cpp:80).  level[v] = hop count
+ * over out-edges, INT64_MAX when unreachable (bfs.cpp:53-61). */
+int gx_bfs(gx_graph *g, uint64_t src, int64_t *level);
+
+/* LAGr_PageRankGX(&r, &iters, G, damping, itermax) incl. LAGraph_Cached_OutDegree /
+ * LAGraph_Cached_AT (pr.cpp:58-61).  Graphalytics PR with dangling redistribution,
+ * exactly `iters` iterations, fp64. */
+int gx_pagerank(gx_graph *g, double damping, int iters, double *rank);
+
+/* Diagonal fill + LAGraph_Cached_EMin + LAGr_SingleSourceShortestPath(Delta = 2.5)
+ * (sssp.cpp:53-81).  dist[v] fp64, +INFINITY when unreachable (printed `infinity`,
+ * sssp.cpp:44-46).  Requires a weighted graph. */
+int gx_sssp(gx_graph *g, uint64_t src, double *dist);
+
+/* A LOR A' (directed) + LAGr_ConnectedComponents (wcc.cpp:39-66).  comp[v] = the
+ * smallest internal vertex index of v's weakly connected component. */
+int gx_wcc(gx_graph *g, uint64_t *comp);
+
+/* LAGraph_cdlp / CUDA_CDLP::LAGraph_cdlp_gpu (cdlp.cpp:54-81; cdlp_cuda.cu:118-251).
+ * labels[v] = internal index of v's community label after at most `iters` synchronous
+ * min-mode iterations (in + out neighbours for directed graphs). */
+int gx_cdlp(gx_graph *g, int iters, uint64_t *labels);
+
+/* LAGraph_lcc(&d, A, symmetric = !directed) (lcc.cpp:61-71). */
+int gx_lcc(gx_graph *g, double *lcc);
+
+/* ---- timing ---------------------------------------------------------------------
+ * Kernel-level timing with hipEvents on the stream the kernels run on.  When enabled,
+ * every launch of a named hot kernel is bracketed by events; gx_kernel_stats reports
+ * the number of launches and the summed device time since the last reset. */
+int gx_set_kernel_timing(gx_ctx *ctx, int enable);
+int gx_kernel_stats(gx_ctx *ctx, const char *kernel, uint64_t *launches, double *total_ms);
+int gx_reset_kernel_stats(gx_ctx *ctx);
+/* Device time (ms) of the last algorithm call, from hipEvents around its device work
+ * (excludes the host->device upload of the graph and the device->host result copy). */
+int gx_last_device_ms(gx_ctx *ctx, double *ms);
+
+/* ---- PageRank row partition (1-D row blocks, one process per GPU) ----------------
+ * The pull matrix (A' for directed graphs, A for undirected) is split into row blocks;
+ * each rank owns rows [row_begin, row_end).  Rank vectors are exchanged in a padded
+ * layout of `nranks` chunks of `chunk` doubles: rows of rank k occupy
+ * [k*chunk, k*chunk + rows_k) and the rank's dangling-score sum sits at
+ * k*chunk + chunk - 1.  The caller all-gathers the local chunk each iteration
+ * (RCCL over xGMI); libgx only touches device memory on the context's stream.
+ *
+ *   gx_pr_part_create   : local pull rows (global column ids, sorted), global out-degree
+ *                         of every local row, and the row ranges of all ranks.
+ *   gx_pr_part_chunk    : doubles per chunk (buffers are nranks*chunk long).
+ *   gx_pr_part_init     : writes the iteration-0 local chunk into x_local (device).
+ *   gx_pr_part_step     : one iteration: reads the gathered x_full (device), writes the
+ *                         next local chunk into x_local (device); if rank_out (device,
+ *                         rows_local long) is non-NULL also writes the scores.
+ *   stream              : hipStream_t to launch on (NULL = the context's stream).
+ * ------------------------------------------------------------------------------- */
+typedef struct gx_pr_part gx_pr_part;
+int gx_pr_part_create(gx_ctx *ctx, uint64_t n_global, int nranks, int rank,
+                      const uint64_t *row_ranges /* nranks+1 */,
+                      const uint64_t *rowptr_local /* rows_local+1, starting at 0 */,
+                      const uint64_t *colidx_local, const uint64_t *outdeg_local,
+                      double damping, gx_pr_part **part);
+int gx_pr_part_chunk(gx_pr_part *part, uint64_t *chunk);
+int gx_pr_part_init(gx_pr_part *part, double *x_local, void *stream);
+int gx_pr_part_step(gx_pr_part *part, const double *x_full, double *x_local,
+                    double *rank_out, void *stream);
+int gx_pr_part_free(gx_pr_part *part);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GX_H */

@@ -1,0 +1,278 @@
+// gx_cdlp.hip -- community detection by synchronous label propagation (Graphalytics CDLP).
+//
+// Replaces LAGraph_cdlp (cdlp.cpp:54-67; semantics LAGraph_cdlp.c:37-121) and the fork's
+// CUDA_CDLP::LAGraph_cdlp_gpu (cdlp_cuda.cu:118-251, kernels cdlp_kernel.cu:449-1140).
+// Every iteration each vertex takes min(argmax_l #neighbour labels == l) over its
+// out-neighbours and, for directed graphs, its in-neighbours too (a reciprocal edge counts
+// twice, LAGraph_cdlp.c:47-50).  A vertex without neighbours keeps its label.
+// Unlike the reference CUDA kernels this is exact and deterministic: counts are built with
+// atomics that never lose an update (the reference's LDS insert is unlocked,
+// cdlp_kernel.cu:685-694), in-edges are included for directed graphs, and degree-0 vertices
+// are written (cdlp_kernel.cu:108-112, 1060-1063).
+//   deg <= 64        : one wave per vertex, labels in registers, counts by 64 shuffles.
+//   deg <= kLdsHash/2: one wave per vertex, open-addressing hash table in that wave's LDS.
+//   larger           : one workgroup per vertex, hash table in a global-memory segment
+//                      (2*deg rounded up to a power of two slots, cleared per iteration).
+// The winner is the maximum of the 64-bit key (count << 32) | ~label, i.e. the highest
+// count and among equal counts the smallest label.
+#include <algorithm>
+
+#include "gx_device.h"
+
+namespace gx {
+namespace {
+
+constexpr int kCdlpBlock = 256;
+constexpr int kLdsHash = 1024;   // slots per wave (8 KiB per wave of int32 key + int32 count)
+constexpr uint32_t kEmpty = 0xffffffffu;
+
+struct CdlpArgs {
+    const int64_t *rpA;
+    const int32_t *ciA;
+    const int64_t *rpT;   // null for undirected graphs
+    const int32_t *ciT;
+    const int32_t *lab;
+    int32_t *nxt;
+    int64_t n;
+    int *changed;
+};
+
+__device__ __forceinline__ int32_t label_at(const CdlpArgs &a, int64_t ob, int64_t od, int64_t ib,
+                                            int64_t k) {
+    return k < od ? a.lab[a.ciA[ob + k]] : a.lab[a.ciT[ib + (k - od)]];
+}
+
+__device__ __forceinline__ uint32_t hash_slot(uint32_t l, int log2ts) {
+    return (l * 2654435761u) >> (32 - log2ts);
+}
+
+__device__ __forceinline__ unsigned long long pack(uint32_t count, uint32_t label) {
+    return ((unsigned long long)count << 32) | (unsigned long long)(kEmpty - label);
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_xor(v, off, kWave);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a) {
+    __shared__ uint32_t keys[kCdlpBlock / kWave][kLdsHash];
+    __shared__ uint32_t cnts[kCdlpBlock / kWave][kLdsHash];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    uint32_t *K = keys[wv];
+    uint32_t *C = cnts[wv];
+    const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
+    const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
+    bool any = false;
+    for (int64_t v = gw; v < a.n; v += nw) {
+        const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
+        int64_t ib = 0, id = 0;
+        if (a.rpT) {
+            ib = a.rpT[v];
+            id = a.rpT[v + 1] - ib;
+        }
+        const int64_t d = od + id;
+        if (d > kLdsHash / 2) continue;   // heavy vertex: k_cdlp_heavy
+        const int32_t old = a.lab[v];
+        int32_t best;
+        if (d == 0) {
+            best = old;
+        } else if (d <= kWave) {
+            const uint32_t my = lane < d ? (uint32_t)label_at(a, ob, od, ib, lane) : kEmpty;
+            uint32_t c = 0;
+            for (int j = 0; j < d; j++) c += (__shfl(my, j, kWave) == my) ? 1u : 0u;
+            const unsigned long long key = lane < d ? pack(c, my) : 0ull;
+            best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+        } else {
+            int log2ts = 1;
+            while ((1ll << log2ts) < 2 * d) log2ts++;
+            const int ts = 1 << log2ts;
+            for (int s = lane; s < ts; s += kWave) {
+                K[s] = kEmpty;
+                C[s] = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int64_t k = lane; k < d; k += kWave) {
+                const uint32_t l = (uint32_t)label_at(a, ob, od, ib, k);
+                uint32_t h = hash_slot(l, log2ts);
+                for (;;) {
+                    const uint32_t prev = atomicCAS(&K[h], kEmpty, l);
+                    if (prev == kEmpty || prev == l) {
+                        atomicAdd(&C[h], 1u);
+                        break;
+                    }
+                    h = (h + 1) & (ts - 1);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            unsigned long long key = 0;
+            for (int s = lane; s < ts; s += kWave) {
+                const uint32_t c = C[s];
+                if (c) {
+                    const unsigned long long kk = pack(c, K[s]);
+                    key = kk > key ? kk : key;
+                }
+            }
+            best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane == 0) {
+            a.nxt[v] = best;
+            any |= best != old;
+        }
+    }
+    if (any) *a.changed = 1;
+}
+
+__global__ __launch_bounds__(kCdlpBlock) void k_cdlp_heavy(CdlpArgs a, const int32_t *__restrict__ hv,
+                                                           const int64_t *__restrict__ hoff,
+                                                           const int32_t *__restrict__ hlog2,
+                                                           uint32_t *gkeys, uint32_t *gcnts) {
+    __shared__ unsigned long long red[kCdlpBlock / kWave];
+    const int64_t v = hv[blockIdx.x];
+    const int log2ts = hlog2[blockIdx.x];
+    const int64_t ts = 1ll << log2ts;
+    uint32_t *K = gkeys + hoff[blockIdx.x];
+    uint32_t *C = gcnts + hoff[blockIdx.x];
+    for (int64_t s = threadIdx.x; s < ts; s += kCdlpBlock) {
+        __hip_atomic_store(&K[s], kEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&C[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
+    int64_t ib = 0, id = 0;
+    if (a.rpT) {
+        ib = a.rpT[v];
+        id = a.rpT[v + 1] - ib;
+    }
+    const int64_t d = od + id;
+    for (int64_t k = threadIdx.x; k < d; k += kCdlpBlock) {
+        const uint32_t l = (uint32_t)label_at(a, ob, od, ib, k);
+        int64_t h = hash_slot(l, log2ts);
+        for (;;) {
+            const uint32_t prev = atomicCAS(&K[h], kEmpty, l);
+            if (prev == kEmpty || prev == l) {
+                atomicAdd(&C[h], 1u);
+                break;
+            }
+            h = (h + 1) & (ts - 1);
+        }
+    }
+    __syncthreads();
+    unsigned long long key = 0;
+    for (int64_t s = threadIdx.x; s < ts; s += kCdlpBlock) {
+        const uint32_t c = __hip_atomic_load(&C[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c) {
+            const uint32_t l = __hip_atomic_load(&K[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long kk = pack(c, l);
+            key = kk > key ? kk : key;
+        }
+    }
+    key = wave_max_u64(key);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = key;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = red[0];
+        for (int w = 1; w < kCdlpBlock / kWave; w++) m = red[w] > m ? red[w] : m;
+        const int32_t best = (int32_t)(kEmpty - (uint32_t)(m & 0xffffffffu));
+        a.nxt[v] = best;
+        if (best != a.lab[v]) *a.changed = 1;
+    }
+}
+
+__global__ void k_cdlp_iota(int32_t *a, int64_t n) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+         v += (int64_t)gridDim.x * blockDim.x)
+        a[v] = (int32_t)v;
+}
+
+}  // namespace
+}  // namespace gx
+
+using namespace gx;
+
+extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
+    if (!g || !labels) return fail(GX_NULL_POINTER, "gx_cdlp: null argument");
+    if (iters < 0) return fail(GX_INVALID_VALUE, "gx_cdlp: negative iteration count");
+    gx_ctx *ctx = g->ctx;
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int64_t n = (int64_t)g->n;
+    if (n == 0) return GX_SUCCESS;
+    GX_TRY(device_begin(ctx));
+    if (g->directed) GX_TRY(ensure_transpose(g));
+    // heavy vertices and their global hash segments
+    std::vector<int32_t> hv, hl;
+    std::vector<int64_t> hoff;
+    int64_t total = 0;
+    for (int64_t v = 0; v < n; v++) {
+        int64_t d = g->A.h_rp[v + 1] - g->A.h_rp[v];
+        if (g->directed) d += g->AT.h_rp[v + 1] - g->AT.h_rp[v];
+        if (d > kLdsHash / 2) {
+            int l2 = 1;
+            while ((1ll << l2) < 2 * d) l2++;
+            hv.push_back((int32_t)v);
+            hl.push_back(l2);
+            hoff.push_back(total);
+            total += 1ll << l2;
+        }
+    }
+    DBuf<int32_t> la, lb, d_hv, d_hl;
+    DBuf<int64_t> d_hoff;
+    DBuf<uint32_t> gk, gc;
+    DBuf<int> changed;
+    GX_TRY(la.alloc(n));
+    GX_TRY(lb.alloc(n));
+    GX_TRY(changed.alloc(1));
+    if (!hv.empty()) {
+        GX_TRY(d_hv.alloc(hv.size()));
+        GX_TRY(d_hl.alloc(hl.size()));
+        GX_TRY(d_hoff.alloc(hoff.size()));
+        GX_TRY(gk.alloc(total));
+        GX_TRY(gc.alloc(total));
+        GX_HIP_TRY(hipMemcpyAsync(d_hv.p, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(d_hl.p, hl.data(), hl.size() * 4, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(d_hoff.p, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, s));
+    }
+    hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, la.p, n);
+    GX_TRY(check_launch("k_cdlp_iota"));
+    int32_t *cur = la.p, *nxt = lb.p;
+    for (int it = 0; it < iters; it++) {
+        CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr,
+                   g->directed ? g->AT.ci.p : nullptr, cur, nxt, n, changed.p};
+        GX_HIP_TRY(hipMemsetAsync(changed.p, 0, sizeof(int), s));
+        {
+            KTimer kt(ctx, "cdlp_light", s);
+            hipLaunchKernelGGL(k_cdlp_light, dim3(grid_for((uint64_t)n * kWave, kCdlpBlock, 8192)),
+                               dim3(kCdlpBlock), 0, s, a);
+        }
+        GX_TRY(check_launch("k_cdlp_light"));
+        if (!hv.empty()) {
+            KTimer kt(ctx, "cdlp_heavy", s);
+            hipLaunchKernelGGL(k_cdlp_heavy, dim3((unsigned)hv.size()), dim3(kCdlpBlock), 0, s, a, d_hv.p,
+                               d_hoff.p, d_hl.p, gk.p, gc.p);
+            GX_TRY(check_launch("k_cdlp_heavy"));
+        }
+        int h_changed = 0;
+        GX_HIP_TRY(hipMemcpyAsync(&h_changed, changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+        std::swap(cur, nxt);
+        if (!h_changed) break;   // fixed point (LAGraph_cdlp.c:328-332)
+    }
+    GX_TRY(device_end(ctx));
+    std::vector<int32_t> h(n);
+    GX_HIP_TRY(hipMemcpy(h.data(), cur, n * 4, hipMemcpyDeviceToHost));
+    for (int64_t v = 0; v < n; v++) labels[v] = (uint64_t)h[v];
+    return GX_SUCCESS;
+}

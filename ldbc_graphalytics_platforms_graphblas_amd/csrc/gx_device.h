@@ -1,0 +1,195 @@
+// gx_device.h -- device-side internals of libgx (gfx950 / CDNA4, wave64).
+//
+// HBM layout of a graph (gx_graph):
+//   A   : out-edge CSR as stored in the .grb (rows = sources), int64 row pointers,
+//         int32 column indices (n < 2^31), optional fp64 weights.
+//   AT  : in-edge CSR (A transposed), built on the device by a radix sort when a
+//         directed algorithm needs in-edges (PR pull, CDLP in-labels, BFS bottom-up).
+//   S   : undirected closure A U A' without self-loops, sorted rows, one flag byte per
+//         entry (bit0: v->u stored in A, bit1: u->v stored in A); built for LCC.
+// Column-index arrays are allocated with 16 bytes of slack so int4 loads that start at
+// an aligned-down address and run past the last entry stay inside the allocation.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "gx_internal.h"
+
+#define GX_HIP_TRY(expr)                                                              \
+    do {                                                                              \
+        hipError_t _e = (expr);                                                       \
+        if (_e != hipSuccess)                                                         \
+            return ::gx::fail(GX_DEVICE_ERROR, std::string(#expr " failed: ") +       \
+                                                   hipGetErrorString(_e));            \
+    } while (0)
+
+#define GX_TRY(expr)                  \
+    do {                              \
+        int _rc = (expr);             \
+        if (_rc != GX_SUCCESS) return _rc; \
+    } while (0)
+
+namespace gx {
+
+constexpr int kWave = 64;
+
+struct PrPart;
+
+// RAII device allocation (hipMalloc / hipFree); size in elements of T.
+template <typename T>
+struct DBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf &) = delete;
+    DBuf &operator=(const DBuf &) = delete;
+    ~DBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    // `slack_bytes` extra zeroed bytes past the end (for over-reading vector loads)
+    int alloc(size_t count, size_t slack_bytes = 0) {
+        release();
+        size_t bytes = count * sizeof(T) + slack_bytes;
+        if (bytes == 0) bytes = 16;
+        hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(GX_OUT_OF_MEMORY, std::string("hipMalloc(") + std::to_string(bytes) +
+                                              ") failed: " + hipGetErrorString(e));
+        }
+        n = count;
+        if (slack_bytes) {
+            e = hipMemset(reinterpret_cast<char *>(p) + count * sizeof(T), 0, slack_bytes);
+            if (e != hipSuccess) return fail(GX_DEVICE_ERROR, "hipMemset slack failed");
+        }
+        return GX_SUCCESS;
+    }
+};
+
+struct DevCSR {
+    uint64_t n = 0, nnz = 0;
+    DBuf<int64_t> rp;         // n + 1
+    DBuf<int32_t> ci;         // nnz (+16 B slack)
+    DBuf<double> w;           // nnz or empty
+    DBuf<uint8_t> flag;       // nnz or empty (closure only)
+    std::vector<int64_t> h_rp;  // host copy of the row pointers (row-block planning)
+    bool built = false;
+};
+
+}  // namespace gx
+
+struct gx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    struct Pending {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;   // recycled by collect_timings
+    std::map<std::string, std::pair<uint64_t, double>> stats;
+    double last_device_ms = 0.0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string device_name;
+    int num_cus = 0;
+};
+
+struct gx_graph {
+    gx_ctx *ctx = nullptr;
+    uint64_t n = 0, nnz = 0;
+    bool directed = false, weighted = false;
+    gx::DevCSR A, AT, S;
+    gx::DBuf<int32_t> outdeg;   // out-degree of every vertex (PR)
+    gx::PrPart *pr = nullptr;   // cached single-rank PageRank plan
+};
+
+namespace gx {
+
+// Kernel timer: brackets one launch with hipEvents when ctx->timing is on.
+struct KTimer {
+    gx_ctx *ctx;
+    const char *name;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    KTimer(gx_ctx *c, const char *nm, hipStream_t st) : ctx(c), name(nm), s(st) {
+        if (ctx && ctx->timing) {
+            a = take();
+            b = take();
+            (void)hipEventRecord(a, s);
+        }
+    }
+    hipEvent_t take() {
+        hipEvent_t e = nullptr;
+        if (!ctx->event_pool.empty()) {
+            e = ctx->event_pool.back();
+            ctx->event_pool.pop_back();
+        } else {
+            (void)hipEventCreate(&e);
+        }
+        return e;
+    }
+    ~KTimer() {
+        if (a) {
+            (void)hipEventRecord(b, s);
+            ctx->pending.push_back({name, a, b});
+        }
+    }
+};
+
+// Collect elapsed times of finished timed launches into ctx->stats.
+int collect_timings(gx_ctx *ctx);
+
+// Device work bracket for gx_last_device_ms.
+int device_begin(gx_ctx *ctx);
+int device_end(gx_ctx *ctx);
+
+// Lazily build the transposed / closure CSR of a graph on the device.
+int ensure_transpose(gx_graph *g);
+int ensure_closure(gx_graph *g);
+int ensure_outdeg(gx_graph *g);
+
+// Launch-error check after hipLaunchKernelGGL.
+inline int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(GX_DEVICE_ERROR, std::string("launch of ") + what + " failed: " +
+                                         hipGetErrorString(e));
+    return GX_SUCCESS;
+}
+
+inline unsigned grid_for(uint64_t work, int block, unsigned cap = 65535u * 4u) {
+    uint64_t g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+// ---- device helpers -----------------------------------------------------------------
+
+// Last row r with rp[r] <= e (rows with rp[r] == rp[r+1] are skipped): upper_bound - 1.
+__device__ __forceinline__ int64_t row_of_edge(const int64_t *rp, int64_t nrows, int64_t e) {
+    int64_t lo = 0, hi = nrows;   // invariant: rp[lo] <= e < rp[hi]
+    while (hi - lo > 1) {
+        int64_t mid = (lo + hi) >> 1;
+        if (rp[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+}  // namespace gx

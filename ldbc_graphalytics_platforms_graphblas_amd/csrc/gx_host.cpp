@@ -1,0 +1,517 @@
+// gx_host.cpp -- host side of libgx that needs no GPU: `.grb`/`.vtb` I/O without
+// SuiteSparse and the seeded R-MAT generator used by the bench and the tests.
+//
+// .grb layout (reference include/graphio.h:49-285 binread, :310-615 binwrite; format of
+// SuiteSparse:GraphBLAS v7 serialisation as written by LAGraph's binwrite):
+//   char header[512]                       informational ASCII
+//   int32  fmt        GxB_BY_ROW=0 / GxB_BY_COL=1
+//   int32  kind       1 hyper, 2 sparse (0 legacy sparse), 4 bitmap, 8 full; +100 if iso
+//   double hyper      hyper switch
+//   uint64 nrows, ncols
+//   int64  nonempty
+//   uint64 nvec, nvals
+//   int32  typecode   0 BOOL ... 8 UINT64, 9 FP32, 10 FP64
+//   size_t typesize
+//   then Ap[nvec+1], [Ah[nvec]], Ai[nvals] (uint64), Ax[iso ? 1 : nvals] (typesize each)
+#include <algorithm>
+#include <cctype>
+#include <cinttypes>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <vector>
+
+#include <omp.h>
+
+#include "gx_internal.h"
+
+namespace gx {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+int fail(int code, const std::string &msg) {
+    set_error(msg);
+    return code;
+}
+
+}  // namespace gx
+
+using gx::fail;
+
+extern "C" const char *gx_last_error(void) { return gx::g_last_error.c_str(); }
+
+extern "C" void gx_host_free(void *p) { std::free(p); }
+
+extern "C" void gx_csr_release(gx_csr *csr) {
+    if (!csr) return;
+    std::free(csr->rowptr);
+    std::free(csr->colidx);
+    std::free(csr->vals);
+    csr->rowptr = nullptr;
+    csr->colidx = nullptr;
+    csr->vals = nullptr;
+    csr->n = csr->nnz = 0;
+}
+
+namespace {
+
+struct FileCloser {
+    void operator()(FILE *f) const {
+        if (f) std::fclose(f);
+    }
+};
+using FilePtr = std::unique_ptr<FILE, FileCloser>;
+
+template <typename T>
+bool read_n(FILE *f, T *p, size_t n) {
+    return n == 0 || std::fread(p, sizeof(T), n, f) == n;
+}
+
+template <typename T>
+T *xmalloc(size_t n) {
+    return static_cast<T *>(std::malloc(std::max<size_t>(n, 1) * sizeof(T)));
+}
+
+// Convert one stored value of GrB type `typecode` to fp64.
+double value_as_double(const unsigned char *p, int32_t typecode) {
+    switch (typecode) {
+        case 0: return *reinterpret_cast<const bool *>(p) ? 1.0 : 0.0;
+        case 1: return *reinterpret_cast<const int8_t *>(p);
+        case 2: return *reinterpret_cast<const int16_t *>(p);
+        case 3: return *reinterpret_cast<const int32_t *>(p);
+        case 4: return (double)*reinterpret_cast<const int64_t *>(p);
+        case 5: return *reinterpret_cast<const uint8_t *>(p);
+        case 6: return *reinterpret_cast<const uint16_t *>(p);
+        case 7: return *reinterpret_cast<const uint32_t *>(p);
+        case 8: return (double)*reinterpret_cast<const uint64_t *>(p);
+        case 9: return *reinterpret_cast<const float *>(p);
+        case 10: return *reinterpret_cast<const double *>(p);
+        default: return 0.0;
+    }
+}
+
+// Build a row-major CSR (sorted rows) from a column-major one: a counting-sort transpose.
+void csc_to_csr(uint64_t nrows, uint64_t ncols, const uint64_t *cp, const uint64_t *ri,
+                const double *cx, uint64_t *rp, uint64_t *ci, double *rx) {
+    std::fill(rp, rp + nrows + 1, 0);
+    uint64_t nnz = cp[ncols];
+    for (uint64_t k = 0; k < nnz; k++) rp[ri[k] + 1]++;
+    for (uint64_t i = 0; i < nrows; i++) rp[i + 1] += rp[i];
+    std::vector<uint64_t> cur(rp, rp + nrows);
+    for (uint64_t j = 0; j < ncols; j++)
+        for (uint64_t k = cp[j]; k < cp[j + 1]; k++) {
+            uint64_t d = cur[ri[k]]++;
+            ci[d] = j;
+            if (rx) rx[d] = cx[k];
+        }
+}
+
+}  // namespace
+
+extern "C" int gx_read_grb(const char *path, gx_csr *out) {
+    if (!path || !out) return fail(GX_NULL_POINTER, "gx_read_grb: null argument");
+    std::memset(out, 0, sizeof(*out));
+    FilePtr f(std::fopen(path, "rb"));
+    if (!f) return fail(GX_IO_ERROR, std::string("cannot open ") + path);
+    char header[512];
+    int32_t fmt = 0, kind = 0, typecode = 0;
+    double hyper = 0;
+    uint64_t nrows = 0, ncols = 0, nvec = 0, nvals = 0;
+    int64_t nonempty = 0;
+    uint64_t typesize = 0;   // size_t on the LP64 writer
+    FILE *fp = f.get();
+    if (!read_n(fp, header, 512) || !read_n(fp, &fmt, 1) || !read_n(fp, &kind, 1) ||
+        !read_n(fp, &hyper, 1) || !read_n(fp, &nrows, 1) || !read_n(fp, &ncols, 1) ||
+        !read_n(fp, &nonempty, 1) || !read_n(fp, &nvec, 1) || !read_n(fp, &nvals, 1) ||
+        !read_n(fp, &typecode, 1) || !read_n(fp, &typesize, 1))
+        return fail(GX_IO_ERROR, std::string("truncated .grb header: ") + path);
+    bool iso = false;
+    if (kind > 100) {
+        iso = true;
+        kind -= 100;
+    }
+    const bool is_hyper = kind == 1;
+    const bool is_sparse = kind == 0 || kind == 2;
+    if (!is_hyper && !is_sparse)
+        return fail(GX_NOT_IMPLEMENTED, "bitmap/full .grb matrices are not supported");
+    if (typecode < 0 || typecode > 10 || typesize == 0 || typesize > 16)
+        return fail(GX_NOT_IMPLEMENTED, "unsupported .grb value type");
+    if (fmt != 0 && fmt != 1) return fail(GX_INVALID_VALUE, "bad .grb format field");
+    if (nrows != ncols) return fail(GX_INVALID_VALUE, "adjacency matrix must be square");
+    const uint64_t nmajor = fmt == 0 ? nrows : ncols;
+    if (is_sparse && nvec != nmajor) nvec = nmajor;   // sparse: nvec = vdim
+
+    std::vector<uint64_t> Ap(nvec + 1), Ah(is_hyper ? nvec : 0), Ai(nvals);
+    if (!read_n(fp, Ap.data(), nvec + 1)) return fail(GX_IO_ERROR, "truncated Ap");
+    if (is_hyper && !read_n(fp, Ah.data(), nvec)) return fail(GX_IO_ERROR, "truncated Ah");
+    if (!read_n(fp, Ai.data(), nvals)) return fail(GX_IO_ERROR, "truncated Ai");
+    const uint64_t nx = iso ? 1 : nvals;
+    std::vector<unsigned char> Ax(nx * typesize);
+    if (!read_n(fp, Ax.data(), Ax.size())) return fail(GX_IO_ERROR, "truncated Ax");
+    if (Ap[0] != 0 || Ap[nvec] != nvals) return fail(GX_INVALID_VALUE, "corrupt Ap");
+    for (uint64_t k = 0; k < nvals; k++)
+        if (Ai[k] >= nrows) return fail(GX_INVALID_INDEX, "column index out of range");
+
+    // Weighted iff the values are floating point and not iso (relabel.py:11-16 writes
+    // FP64 for weighted graphs and BOOL iso for unweighted ones).
+    const bool weighted = (typecode == 9 || typecode == 10) && !iso;
+
+    // Expand the (hyper)sparse major dimension to a full pointer array.
+    std::vector<uint64_t> P(nmajor + 1, 0);
+    if (is_hyper) {
+        for (uint64_t k = 0; k < nvec; k++) {
+            if (Ah[k] >= nmajor) return fail(GX_INVALID_INDEX, "hyper index out of range");
+            P[Ah[k] + 1] = Ap[k + 1] - Ap[k];
+        }
+        for (uint64_t i = 0; i < nmajor; i++) P[i + 1] += P[i];
+    } else {
+        P.assign(Ap.begin(), Ap.end());
+    }
+    std::vector<double> X;
+    if (weighted) {
+        X.resize(nvals);
+        for (uint64_t k = 0; k < nvals; k++) X[k] = value_as_double(&Ax[k * typesize], typecode);
+    }
+
+    out->n = nrows;
+    out->nnz = nvals;
+    out->rowptr = xmalloc<uint64_t>(nrows + 1);
+    out->colidx = xmalloc<uint64_t>(nvals);
+    out->vals = weighted ? xmalloc<double>(nvals) : nullptr;
+    if (!out->rowptr || !out->colidx || (weighted && !out->vals)) {
+        gx_csr_release(out);
+        return fail(GX_OUT_OF_MEMORY, "gx_read_grb: out of memory");
+    }
+    if (fmt == 0) {
+        std::memcpy(out->rowptr, P.data(), (nrows + 1) * sizeof(uint64_t));
+        std::memcpy(out->colidx, Ai.data(), nvals * sizeof(uint64_t));
+        if (weighted) std::memcpy(out->vals, X.data(), nvals * sizeof(double));
+        // SuiteSparse may leave rows jumbled; sort every row (values follow).
+        #pragma omp parallel for schedule(dynamic, 1024)
+        for (int64_t i = 0; i < (int64_t)nrows; i++) {
+            uint64_t b = out->rowptr[i], e = out->rowptr[i + 1];
+            if (std::is_sorted(out->colidx + b, out->colidx + e)) continue;
+            std::vector<std::pair<uint64_t, double>> row;
+            for (uint64_t k = b; k < e; k++) row.push_back({out->colidx[k], weighted ? out->vals[k] : 0.0});
+            std::sort(row.begin(), row.end());
+            for (uint64_t k = b; k < e; k++) {
+                out->colidx[k] = row[k - b].first;
+                if (weighted) out->vals[k] = row[k - b].second;
+            }
+        }
+    } else {
+        csc_to_csr(nrows, ncols, P.data(), Ai.data(), weighted ? X.data() : nullptr,
+                   out->rowptr, out->colidx, out->vals);
+    }
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_write_grb(const char *path, const gx_csr *csr) {
+    if (!path || !csr || !csr->rowptr || (!csr->colidx && csr->nnz))
+        return fail(GX_NULL_POINTER, "gx_write_grb: null argument");
+    FilePtr f(std::fopen(path, "wb"));
+    if (!f) return fail(GX_IO_ERROR, std::string("cannot create ") + path);
+    const bool weighted = csr->vals != nullptr;
+    const uint64_t n = csr->n, nnz = csr->nnz;
+    int32_t fmt = 0;                              // GxB_BY_ROW
+    int32_t kind = weighted ? 2 : 102;            // sparse (+100 iso)
+    double hyper = 0.0625;                        // GxB_HYPER_DEFAULT
+    int64_t nonempty = -1;
+    uint64_t nvec = n;
+    int32_t typecode = weighted ? 10 : 0;         // GrB_FP64 / GrB_BOOL
+    uint64_t typesize = weighted ? 8 : 1;
+    char header[512];
+    int len = std::snprintf(header, sizeof(header),
+                            "SuiteSparse:GraphBLAS matrix\nv%-25s\n"
+                            "nrows:  %-18" PRIu64 "\nncols:  %-18" PRIu64 "\n"
+                            "nvec:   %-18" PRIu64 "\nnvals:  %-18" PRIu64 "\n"
+                            "format: %-8s\nsize:   %-18" PRIu64 "\ntype:   %-72s\n"
+                            "iso:    %1d\n%-210s\n\n",
+                            "7.4.4 (gx)", n, n, nvec, nnz, "CSR ", typesize,
+                            weighted ? "GrB_FP64  " : "GrB_BOOL  ", weighted ? 0 : 1, "\n");
+    if (len < 0) len = 0;
+    for (int k = len; k < 512; k++) header[k] = ' ';
+    header[511] = '\0';
+    FILE *fp = f.get();
+    bool ok = std::fwrite(header, 1, 512, fp) == 512;
+    ok = ok && std::fwrite(&fmt, 4, 1, fp) == 1 && std::fwrite(&kind, 4, 1, fp) == 1;
+    ok = ok && std::fwrite(&hyper, 8, 1, fp) == 1 && std::fwrite(&n, 8, 1, fp) == 1;
+    ok = ok && std::fwrite(&n, 8, 1, fp) == 1 && std::fwrite(&nonempty, 8, 1, fp) == 1;
+    ok = ok && std::fwrite(&nvec, 8, 1, fp) == 1 && std::fwrite(&nnz, 8, 1, fp) == 1;
+    ok = ok && std::fwrite(&typecode, 4, 1, fp) == 1 && std::fwrite(&typesize, 8, 1, fp) == 1;
+    ok = ok && std::fwrite(csr->rowptr, 8, n + 1, fp) == n + 1;
+    ok = ok && (nnz == 0 || std::fwrite(csr->colidx, 8, nnz, fp) == nnz);
+    if (weighted) {
+        ok = ok && (nnz == 0 || std::fwrite(csr->vals, 8, nnz, fp) == nnz);
+    } else {
+        const bool one = true;
+        ok = ok && std::fwrite(&one, 1, 1, fp) == 1;
+    }
+    if (!ok) return fail(GX_IO_ERROR, std::string("write failed: ") + path);
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_read_vtb(const char *path, uint64_t **ids, uint64_t *count) {
+    if (!path || !ids || !count) return fail(GX_NULL_POINTER, "gx_read_vtb: null argument");
+    FilePtr f(std::fopen(path, "rb"));
+    if (!f) return fail(GX_IO_ERROR, std::string("cannot open ") + path);
+    std::fseek(f.get(), 0, SEEK_END);
+    long bytes = std::ftell(f.get());
+    std::fseek(f.get(), 0, SEEK_SET);
+    if (bytes < 0 || bytes % 8) return fail(GX_IO_ERROR, "bad .vtb size");
+    uint64_t n = (uint64_t)bytes / 8;
+    uint64_t *p = xmalloc<uint64_t>(n);
+    if (!p) return fail(GX_OUT_OF_MEMORY, "gx_read_vtb: out of memory");
+    if (!read_n(f.get(), p, n)) {
+        std::free(p);
+        return fail(GX_IO_ERROR, "truncated .vtb");
+    }
+    *ids = p;
+    *count = n;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_write_vtb(const char *path, const uint64_t *ids, uint64_t count) {
+    if (!path || (!ids && count)) return fail(GX_NULL_POINTER, "gx_write_vtb: null argument");
+    FilePtr f(std::fopen(path, "wb"));
+    if (!f) return fail(GX_IO_ERROR, std::string("cannot create ") + path);
+    if (count && std::fwrite(ids, 8, count, f.get()) != count)
+        return fail(GX_IO_ERROR, "write failed");
+    return GX_SUCCESS;
+}
+
+// ------------------------------------------------------------------------------------
+// Seeded R-MAT (SURVEY.md 8d synthetic inputs).  Every random draw is a pure function
+// of (seed, edge index, level), so the graph does not depend on the thread count.
+// ------------------------------------------------------------------------------------
+namespace {
+
+inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+inline double u01(uint64_t h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); }
+
+// U(0,1] weight of the unordered pair {u, v}: symmetric by construction.
+inline double pair_weight(uint64_t seed, uint32_t u, uint32_t v) {
+    uint32_t lo = std::min(u, v), hi = std::max(u, v);
+    uint64_t h = splitmix64(seed ^ 0x5851F42D4C957F2Dull ^ (((uint64_t)lo << 32) | hi));
+    return 1.0 - u01(h);   // in (0, 1]
+}
+
+}  // namespace
+
+extern "C" int gx_rmat_csr(int scale, int edgefactor, double a, double b, double c,
+                           uint64_t seed, int undirected, int weighted, gx_csr *out) {
+    if (!out) return fail(GX_NULL_POINTER, "gx_rmat_csr: null out");
+    std::memset(out, 0, sizeof(*out));
+    if (scale < 1 || scale > 30 || edgefactor < 1)
+        return fail(GX_INVALID_VALUE, "gx_rmat_csr: bad scale/edgefactor");
+    if (a < 0 || b < 0 || c < 0 || a + b + c > 1.0)
+        return fail(GX_INVALID_VALUE, "gx_rmat_csr: bad probabilities");
+    const uint64_t n = 1ull << scale;
+    const uint64_t m = (uint64_t)edgefactor << scale;
+
+    // seeded vertex permutation (Fisher-Yates)
+    std::vector<uint32_t> perm(n);
+    std::iota(perm.begin(), perm.end(), 0u);
+    for (uint64_t i = n - 1; i > 0; i--) {
+        uint64_t j = splitmix64(seed ^ 0xA24BAED4963EE407ull ^ i) % (i + 1);
+        std::swap(perm[i], perm[j]);
+    }
+
+    // edge generation
+    const uint64_t mult = undirected ? 2 : 1;
+    std::vector<uint32_t> src(m * mult), dst(m * mult);
+    const double ab = a + b, abc = a + b + c;
+    #pragma omp parallel for schedule(static)
+    for (int64_t e = 0; e < (int64_t)m; e++) {
+        uint64_t u = 0, v = 0;
+        uint64_t state = splitmix64(seed * 0x100000001B3ull + (uint64_t)e);
+        for (int l = 0; l < scale; l++) {
+            state = splitmix64(state);
+            double r = u01(state);
+            u <<= 1;
+            v <<= 1;
+            if (r < a) {
+            } else if (r < ab) {
+                v |= 1;
+            } else if (r < abc) {
+                u |= 1;
+            } else {
+                u |= 1;
+                v |= 1;
+            }
+        }
+        uint32_t pu = perm[u], pv = perm[v];
+        src[e] = pu;
+        dst[e] = pv;
+        if (undirected) {
+            src[m + e] = pv;
+            dst[m + e] = pu;
+        }
+    }
+    const uint64_t me = m * mult;
+
+    // counting sort by source (self-loops dropped)
+    std::vector<uint64_t> rp(n + 1, 0);
+    for (uint64_t e = 0; e < me; e++)
+        if (src[e] != dst[e]) rp[src[e] + 1]++;
+    for (uint64_t i = 0; i < n; i++) rp[i + 1] += rp[i];
+    std::vector<uint32_t> col(rp[n]);
+    {
+        std::vector<uint64_t> cur(rp.begin(), rp.end() - 1);
+        for (uint64_t e = 0; e < me; e++)
+            if (src[e] != dst[e]) col[cur[src[e]]++] = dst[e];
+    }
+    std::vector<uint32_t>().swap(src);
+    std::vector<uint32_t>().swap(dst);
+
+    // sort + dedup each row
+    std::vector<uint64_t> deg(n);
+    #pragma omp parallel for schedule(dynamic, 4096)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        uint32_t *bgn = col.data() + rp[i], *end = col.data() + rp[i + 1];
+        std::sort(bgn, end);
+        deg[i] = (uint64_t)(std::unique(bgn, end) - bgn);
+    }
+    uint64_t *orp = xmalloc<uint64_t>(n + 1);
+    if (!orp) return fail(GX_OUT_OF_MEMORY, "gx_rmat_csr: out of memory");
+    orp[0] = 0;
+    for (uint64_t i = 0; i < n; i++) orp[i + 1] = orp[i] + deg[i];
+    const uint64_t nnz = orp[n];
+    uint64_t *oci = xmalloc<uint64_t>(nnz);
+    double *ow = weighted ? xmalloc<double>(nnz) : nullptr;
+    if (!oci || (weighted && !ow)) {
+        std::free(orp);
+        std::free(oci);
+        std::free(ow);
+        return fail(GX_OUT_OF_MEMORY, "gx_rmat_csr: out of memory");
+    }
+    #pragma omp parallel for schedule(dynamic, 4096)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        const uint32_t *row = col.data() + rp[i];
+        for (uint64_t k = 0; k < deg[i]; k++) {
+            oci[orp[i] + k] = row[k];
+            if (weighted) ow[orp[i] + k] = pair_weight(seed, (uint32_t)i, row[k]);
+        }
+    }
+    out->n = n;
+    out->nnz = nnz;
+    out->rowptr = orp;
+    out->colidx = oci;
+    out->vals = ow;
+    return GX_SUCCESS;
+}
+
+// ------------------------------------------------------------------------------------
+// Text formats written by relabel.py (Matrix Market + one-id-per-line mapping).
+// ------------------------------------------------------------------------------------
+extern "C" int gx_read_vtx(const char *path, uint64_t **ids, uint64_t *count) {
+    if (!path || !ids || !count) return fail(GX_NULL_POINTER, "gx_read_vtx: null argument");
+    FilePtr f(std::fopen(path, "r"));
+    if (!f) return fail(GX_IO_ERROR, std::string("cannot open ") + path);
+    std::vector<uint64_t> v;
+    unsigned long long x;
+    while (std::fscanf(f.get(), "%llu", &x) == 1) v.push_back(x);
+    uint64_t *p = xmalloc<uint64_t>(v.size());
+    if (!p) return fail(GX_OUT_OF_MEMORY, "gx_read_vtx: out of memory");
+    std::memcpy(p, v.data(), v.size() * 8);
+    *ids = p;
+    *count = v.size();
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_read_mtx(const char *path, gx_csr *out) {
+    if (!path || !out) return fail(GX_NULL_POINTER, "gx_read_mtx: null argument");
+    std::memset(out, 0, sizeof(*out));
+    FilePtr f(std::fopen(path, "r"));
+    if (!f) return fail(GX_IO_ERROR, std::string("cannot open Matrix Market file: ") + path);
+    char line[1024];
+    if (!std::fgets(line, sizeof line, f.get())) return fail(GX_IO_ERROR, "empty .mtx");
+    char banner[64] = {0}, object[64] = {0}, format[64] = {0}, field[64] = {0}, symmetry[64] = {0};
+    if (std::sscanf(line, "%63s %63s %63s %63s %63s", banner, object, format, field, symmetry) != 5 ||
+        std::strcmp(banner, "%%MatrixMarket") != 0)
+        return fail(GX_IO_ERROR, "bad Matrix Market banner");
+    auto lower = [](char *s) {
+        for (; *s; s++) *s = (char)std::tolower((unsigned char)*s);
+    };
+    lower(object);
+    lower(format);
+    lower(field);
+    lower(symmetry);
+    if (std::strcmp(object, "matrix") != 0 || std::strcmp(format, "coordinate") != 0)
+        return fail(GX_NOT_IMPLEMENTED, "only coordinate matrices are supported");
+    const bool symmetric = std::strcmp(symmetry, "symmetric") == 0;
+    if (!symmetric && std::strcmp(symmetry, "general") != 0)
+        return fail(GX_NOT_IMPLEMENTED, "only general/symmetric Matrix Market files are supported");
+    const bool pattern = std::strcmp(field, "pattern") == 0;
+    bool weighted = std::strcmp(field, "real") == 0 || std::strcmp(field, "double") == 0;
+    // %%GraphBLAS <type> (relabel.py:68) overrides the Matrix Market field
+    uint64_t nr = 0, nc = 0, ne = 0;
+    for (;;) {
+        if (!std::fgets(line, sizeof line, f.get())) return fail(GX_IO_ERROR, "missing size line");
+        if (line[0] == '%') {
+            char tag[64] = {0}, type[64] = {0};
+            if (std::sscanf(line, "%63s %63s", tag, type) == 2 && std::strcmp(tag, "%%GraphBLAS") == 0)
+                weighted = std::strcmp(type, "GrB_FP64") == 0 || std::strcmp(type, "GrB_FP32") == 0;
+            continue;
+        }
+        unsigned long long a, b, c;
+        if (std::sscanf(line, "%llu %llu %llu", &a, &b, &c) != 3) return fail(GX_IO_ERROR, "bad size line");
+        nr = a;
+        nc = b;
+        ne = c;
+        break;
+    }
+    if (nr != nc) return fail(GX_INVALID_VALUE, "adjacency matrix must be square");
+    struct Ent {
+        uint64_t r, c;
+        double v;
+    };
+    std::vector<Ent> ents;
+    ents.reserve(symmetric ? 2 * ne : ne);
+    for (uint64_t k = 0; k < ne; k++) {
+        unsigned long long i, j;
+        double v = 1.0;
+        int got = pattern ? std::fscanf(f.get(), "%llu %llu", &i, &j)
+                          : std::fscanf(f.get(), "%llu %llu %lf", &i, &j, &v);
+        if (got != (pattern ? 2 : 3)) return fail(GX_IO_ERROR, "truncated Matrix Market entries");
+        if (i < 1 || j < 1 || i > nr || j > nc) return fail(GX_INVALID_INDEX, "entry out of range");
+        ents.push_back({i - 1, j - 1, v});
+        if (symmetric && i != j) ents.push_back({j - 1, i - 1, v});
+    }
+    std::stable_sort(ents.begin(), ents.end(),
+                     [](const Ent &x, const Ent &y) { return x.r != y.r ? x.r < y.r : x.c < y.c; });
+    // duplicates: keep the last occurrence
+    std::vector<Ent> uniq;
+    uniq.reserve(ents.size());
+    for (size_t k = 0; k < ents.size(); k++) {
+        if (!uniq.empty() && uniq.back().r == ents[k].r && uniq.back().c == ents[k].c) uniq.back() = ents[k];
+        else uniq.push_back(ents[k]);
+    }
+    const uint64_t nnz = uniq.size();
+    out->n = nr;
+    out->nnz = nnz;
+    out->rowptr = xmalloc<uint64_t>(nr + 1);
+    out->colidx = xmalloc<uint64_t>(nnz);
+    out->vals = weighted ? xmalloc<double>(nnz) : nullptr;
+    if (!out->rowptr || !out->colidx || (weighted && !out->vals)) {
+        gx_csr_release(out);
+        return fail(GX_OUT_OF_MEMORY, "gx_read_mtx: out of memory");
+    }
+    std::fill(out->rowptr, out->rowptr + nr + 1, 0);
+    for (uint64_t k = 0; k < nnz; k++) {
+        out->rowptr[uniq[k].r + 1]++;
+        out->colidx[k] = uniq[k].c;
+        if (weighted) out->vals[k] = uniq[k].v;
+    }
+    for (uint64_t i = 0; i < nr; i++) out->rowptr[i + 1] += out->rowptr[i];
+    return GX_SUCCESS;
+}

@@ -1,0 +1,68 @@
+// gx_pr.h -- PageRank pull plan (row blocks of the pull matrix of one rank).
+#pragma once
+
+#include "gx_device.h"
+
+namespace gx {
+
+// One workgroup's share of the pull SpMV (the CSR-Adaptive split):
+//   split <  0 : STREAM  -- rows [row_begin, row_end), all of them short, <= kStreamNnz
+//                 entries in total; staged through LDS, reduced per row.
+//   split >= 0 : LONG    -- entries [nz_begin, nz_end) of the single row row_begin;
+//                 rows longer than kSegNnz are cut into several segments whose partial
+//                 sums are combined by the last-arriving workgroup (ticket per row).
+struct RowBlock {
+    int64_t nz_begin;
+    int64_t nz_end;
+    int32_t row_begin;
+    int32_t row_end;
+    int32_t split;      // -1 stream; else index into the per-long-row ticket/partials
+    int32_t seg;        // segment number within the long row
+};
+
+constexpr int kPullBlock = 256;      // 4 waves
+constexpr int kStreamNnz = 2048;     // LDS stage: 16 KiB of fp64 per workgroup
+constexpr int kStreamRows = 256;     // at most one row per lane in stream mode
+constexpr int kSegNnz = 8192;        // entries per LONG segment
+
+struct PrPart {
+    gx_ctx *ctx = nullptr;
+    uint64_t n_global = 0;
+    int nranks = 1, rank = 0;
+    uint64_t rows = 0;       // local rows
+    uint64_t chunk = 0;      // doubles per rank chunk (last one = dangling slot)
+    double damping = 0.85;
+    // pull matrix of the local rows (column ids already in the padded chunk layout)
+    DBuf<int64_t> rp_own;    // when the plan owns its matrix
+    DBuf<int32_t> ci_own;
+    const int64_t *rp = nullptr;
+    const int32_t *ci = nullptr;
+    DBuf<int32_t> outdeg_own;
+    const int32_t *outdeg = nullptr;   // out-degree of each local row's vertex
+    // row blocks
+    DBuf<RowBlock> blocks;
+    uint32_t nblocks = 0;
+    DBuf<int32_t> long_first;  // per long row: index of its first partial
+    DBuf<int32_t> long_nseg;   // per long row: number of segments
+    DBuf<double> long_part;    // per segment partial sum
+    DBuf<uint32_t> long_ticket;
+    uint32_t nlong = 0, nsegs = 0;
+    // dangling rows (out-degree 0) of this rank
+    DBuf<int32_t> dlist;
+    uint64_t nd = 0;
+    uint32_t dgrid = 0;
+    DBuf<double> dpart;
+    DBuf<uint32_t> dticket;
+    // single-GPU driver buffers (gx_pagerank)
+    DBuf<double> xa, xb, rank_out;
+};
+
+// Build the row-block plan and dangling list from a local pull CSR (host row pointers
+// h_rp, device rp/ci) and device out-degrees.  Borrowed device pointers must outlive it.
+int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp,
+            const int32_t *d_ci, const int32_t *d_outdeg, const std::vector<int32_t> &h_outdeg);
+
+int pr_init(PrPart *p, double *x_local, hipStream_t s);
+int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
+
+}  // namespace gx

@@ -1,0 +1,485 @@
+// gx_pr.hip -- PageRank (Graphalytics definition) as one fused pull-SpMV per iteration.
+//
+// Replaces LA_PR -> LAGraph_Cached_OutDegree + LAGraph_Cached_AT + LAGr_PageRankGX
+// (pr.cpp:47-66), whose hot loop is one GrB_mxv PLUS_SECOND over A' per iteration.
+//
+// Per iteration, for every vertex v of the rank's rows:
+//     teleport = (1-d)/n + d/n * sum_k dangling_k           (k over ranks, fixed order)
+//     r(v)     = teleport + sum_{u in in(v)} x(u)
+//     x'(v)    = outdeg(v) > 0 ? r(v) / (outdeg(v)/d) : r(v)
+// where x(u) = r(u)/(outdeg(u)/d) is what the previous iteration stored, and a dangling
+// vertex stores r itself (it has no out-edges, so nobody gathers its slot).  That is the
+// GX arithmetic of the oracle (oracle/gx_oracle.c orc_pagerank) with the division by the
+// out-degree fused into the producer of x instead of a separate GrB_eWiseMult pass.
+//
+// HBM traffic per iteration (algorithmic): 4 B per stored entry (int32 column index),
+// 8 B row pointer + 4 B out-degree + 8 B x write per row, the x gathers (L2 / MALL
+// resident for the graphs we run), and 8 B per row for the scores in the last iteration.
+//
+// k_pr_pull is CSR-Adaptive (Greathouse & Daga): rows are packed into workgroups of at
+// most kStreamNnz entries; a workgroup streams its contiguous column-index range with
+// 16-B loads, gathers x into LDS, then reduces each row with a power-of-two lane group.
+// Rows longer than kStreamNnz get whole workgroups (split into kSegNnz segments, combined
+// by the last-arriving segment through an agent-scope release/acquire ticket), and are
+// dispatched first so they overlap the stream blocks.
+#include <algorithm>
+#include <numeric>
+
+#include "gx_pr.h"
+
+namespace gx {
+namespace {
+
+struct PullArgs {
+    const RowBlock *blocks;
+    const int64_t *rp;
+    const int32_t *ci;
+    const int32_t *outdeg;
+    const double *x_in;
+    double *x_out;
+    double *rank_out;
+    int64_t chunk;
+    int nranks;
+    int zero_slot;
+    double teleport0, damping_over_n, damping;
+    const int32_t *long_first;
+    const int32_t *long_nseg;
+    double *long_part;
+    uint32_t *long_ticket;
+};
+
+__device__ __forceinline__ void pr_epilogue(const PullArgs &a, int32_t row, double s,
+                                            double teleport) {
+    const double r = teleport + s;
+    if (a.rank_out) a.rank_out[row] = r;
+    const int32_t deg = a.outdeg[row];
+    a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+}
+
+__global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
+    __shared__ double vals[kStreamNnz];
+    __shared__ int32_t rofs[kStreamRows + 1];
+    __shared__ double wred[kPullBlock / kWave];
+
+    const RowBlock b = a.blocks[blockIdx.x];
+    const int tid = threadIdx.x;
+
+    double dsum = 0.0;
+    for (int k = 0; k < a.nranks; k++) dsum += a.x_in[(int64_t)k * a.chunk + a.chunk - 1];
+    const double teleport = a.teleport0 + a.damping_over_n * dsum;
+    if (a.zero_slot && blockIdx.x == 0 && tid == 0) a.x_out[a.chunk - 1] = 0.0;
+
+    if (b.split < 0) {
+        // ---------------- STREAM: short rows staged through LDS ----------------
+        const int64_t z0 = b.nz_begin, z1 = b.nz_end;
+        const int32_t r0 = b.row_begin;
+        const int nrows = b.row_end - b.row_begin;
+        for (int i = tid; i <= nrows; i += kPullBlock) rofs[i] = (int32_t)(a.rp[r0 + i] - z0);
+        const int64_t base = z0 & ~(int64_t)3;
+        const int nq = (int)((z1 - base + 3) >> 2);
+        const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
+        constexpr int NQ = (kStreamNnz / 4 + kPullBlock) / kPullBlock;
+        int4 c[NQ];
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + j * kPullBlock;
+            if (q < nq) c[j] = ci4[q];
+            else c[j] = make_int4(0, 0, 0, 0);
+        }
+        double v[NQ][4];
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int64_t e = base + 4 * (int64_t)(tid + j * kPullBlock);
+            const int cc[4] = {c[j].x, c[j].y, c[j].z, c[j].w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool ok = (e + k >= z0) && (e + k < z1);
+                v[j][k] = ok ? a.x_in[cc[k]] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int64_t e = base + 4 * (int64_t)(tid + j * kPullBlock);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if ((e + k >= z0) && (e + k < z1)) vals[e + k - z0] = v[j][k];
+        }
+        __syncthreads();
+        int L = kWave;
+        while (L > 1 && L * nrows > kPullBlock) L >>= 1;
+        const int row = tid / L, lane = tid & (L - 1);
+        double s = 0.0;
+        if (row < nrows) {
+            const int kb = rofs[row], ke = rofs[row + 1];
+            for (int k = kb + lane; k < ke; k += L) s += vals[k];
+        }
+        for (int off = L >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+        if (row < nrows && lane == 0) pr_epilogue(a, r0 + row, s, teleport);
+        return;
+    }
+
+    // ---------------- LONG: one segment of one long row ----------------
+    const int64_t zb = b.nz_begin, ze = b.nz_end;
+    const int64_t base = zb & ~(int64_t)3;
+    const int64_t nq = (ze - base + 3) >> 2;
+    const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
+    double s0 = 0.0, s1 = 0.0;
+    for (int64_t q = tid; q < nq; q += 2 * kPullBlock) {
+        const int64_t q1 = q + kPullBlock;
+        const int4 c0 = ci4[q];
+        const int4 c1 = q1 < nq ? ci4[q1] : make_int4(0, 0, 0, 0);
+        const int64_t e0 = base + 4 * q, e1 = base + 4 * q1;
+        const int a0[4] = {c0.x, c0.y, c0.z, c0.w};
+        const int a1[4] = {c1.x, c1.y, c1.z, c1.w};
+        double g0[4], g1[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            g0[k] = (e0 + k >= zb && e0 + k < ze) ? a.x_in[a0[k]] : 0.0;
+            g1[k] = (e1 + k >= zb && e1 + k < ze) ? a.x_in[a1[k]] : 0.0;
+        }
+        s0 += (g0[0] + g0[1]) + (g0[2] + g0[3]);
+        s1 += (g1[0] + g1[1]) + (g1[2] + g1[3]);
+    }
+    double s = wave_sum(s0 + s1);
+    if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = s;
+    __syncthreads();
+    if (tid != 0) return;
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < kPullBlock / kWave; w++) tot += wred[w];
+    const int32_t sp = b.split;
+    const int32_t nseg = a.long_nseg[sp];
+    if (nseg == 1) {
+        pr_epilogue(a, b.row_begin, tot, teleport);
+        return;
+    }
+    const int32_t first = a.long_first[sp];
+    // publish the partial (agent scope), then take a ticket; the last arriver combines
+    __hip_atomic_store(&a.long_part[first + b.seg], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(&a.long_ticket[sp], 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    if (t != (uint32_t)(nseg - 1)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double all = 0.0;
+    for (int j = 0; j < nseg; j++)
+        all += __hip_atomic_load(&a.long_part[first + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.long_ticket[sp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pr_epilogue(a, b.row_begin, all, teleport);
+}
+
+// Sum of the scores of this rank's dangling vertices into the chunk's last slot.
+// Workgroup partials are combined in workgroup order by the last arriver.
+__global__ __launch_bounds__(256) void k_pr_dangling(const int32_t *__restrict__ dlist, int64_t nd,
+                                                     int64_t per, double *x, int64_t slot,
+                                                     double *part, uint32_t *ticket) {
+    __shared__ double wred[256 / kWave];
+    const int tid = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(b0 + per, nd);
+    double s = 0.0;
+    for (int64_t i = b0 + tid; i < b1; i += 256) s += x[dlist[i]];
+    s = wave_sum(s);
+    if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = s;
+    __syncthreads();
+    if (tid != 0) return;
+    const double tot = (wred[0] + wred[1]) + (wred[2] + wred[3]);
+    const uint32_t G = gridDim.x;
+    if (G == 1) {
+        x[slot] = tot;
+        return;
+    }
+    __hip_atomic_store(&part[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t != G - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double all = 0.0;
+    for (uint32_t j = 0; j < G; j++)
+        all += __hip_atomic_load(&part[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x[slot] = all;
+}
+
+__global__ void k_pr_init(const int32_t *__restrict__ outdeg, int64_t rows, double inv_n,
+                          double damping, double *x, int64_t slot, int zero_slot) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t deg = outdeg[i];
+        x[i] = deg > 0 ? inv_n / ((double)deg / damping) : inv_n;
+    }
+    if (zero_slot && blockIdx.x == 0 && threadIdx.x == 0) x[slot] = 0.0;
+}
+
+}  // namespace
+
+int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, const int32_t *d_ci,
+            const int32_t *d_outdeg, const std::vector<int32_t> &h_outdeg) {
+    const int64_t rows = (int64_t)h_rp.size() - 1;
+    p->rows = (uint64_t)rows;
+    p->rp = d_rp;
+    p->ci = d_ci;
+    p->outdeg = d_outdeg;
+    std::vector<RowBlock> longb, streamb;
+    std::vector<int32_t> lfirst, lnseg;
+    int32_t nsegs = 0;
+    std::vector<std::pair<int64_t, int32_t>> longrows;   // (length, row)
+    int64_t r = 0;
+    while (r < rows) {
+        const int64_t len = h_rp[r + 1] - h_rp[r];
+        if (len > kStreamNnz) {
+            longrows.push_back({len, (int32_t)r});
+            r++;
+            continue;
+        }
+        const int64_t start = r;
+        int64_t nz = 0;
+        while (r < rows && r - start < kStreamRows) {
+            const int64_t l = h_rp[r + 1] - h_rp[r];
+            if (l > kStreamNnz || nz + l > kStreamNnz) break;
+            nz += l;
+            r++;
+        }
+        streamb.push_back({h_rp[start], h_rp[r], (int32_t)start, (int32_t)r, -1, 0});
+    }
+    // longest rows first: they are the tail of the launch otherwise
+    std::stable_sort(longrows.begin(), longrows.end(),
+                     [](const auto &x, const auto &y) { return x.first > y.first; });
+    for (const auto &lr : longrows) {
+        const int32_t row = lr.second;
+        const int64_t len = lr.first;
+        const int32_t nseg = (int32_t)((len + kSegNnz - 1) / kSegNnz);
+        const int32_t sp = (int32_t)lfirst.size();
+        lfirst.push_back(nsegs);
+        lnseg.push_back(nseg);
+        for (int32_t s = 0; s < nseg; s++) {
+            const int64_t zb = h_rp[row] + (int64_t)s * kSegNnz;
+            const int64_t ze = std::min(zb + kSegNnz, h_rp[row + 1]);
+            longb.push_back({zb, ze, row, row + 1, sp, s});
+        }
+        nsegs += nseg;
+    }
+    std::vector<RowBlock> all;
+    all.reserve(longb.size() + streamb.size());
+    all.insert(all.end(), longb.begin(), longb.end());
+    all.insert(all.end(), streamb.begin(), streamb.end());
+    p->nblocks = (uint32_t)all.size();
+    p->nlong = (uint32_t)lfirst.size();
+    p->nsegs = (uint32_t)nsegs;
+    GX_TRY(p->blocks.alloc(std::max<size_t>(all.size(), 1)));
+    GX_TRY(p->long_first.alloc(std::max<size_t>(lfirst.size(), 1)));
+    GX_TRY(p->long_nseg.alloc(std::max<size_t>(lnseg.size(), 1)));
+    GX_TRY(p->long_part.alloc(std::max<size_t>(nsegs, 1)));
+    GX_TRY(p->long_ticket.alloc(std::max<size_t>(lfirst.size(), 1)));
+    if (!all.empty())
+        GX_HIP_TRY(hipMemcpy(p->blocks.p, all.data(), all.size() * sizeof(RowBlock), hipMemcpyHostToDevice));
+    if (!lfirst.empty()) {
+        GX_HIP_TRY(hipMemcpy(p->long_first.p, lfirst.data(), lfirst.size() * 4, hipMemcpyHostToDevice));
+        GX_HIP_TRY(hipMemcpy(p->long_nseg.p, lnseg.data(), lnseg.size() * 4, hipMemcpyHostToDevice));
+    }
+    GX_HIP_TRY(hipMemset(p->long_ticket.p, 0, p->long_ticket.n * 4));
+    // dangling rows
+    std::vector<int32_t> dl;
+    for (int64_t i = 0; i < rows; i++)
+        if (h_outdeg[i] == 0) dl.push_back((int32_t)i);
+    p->nd = dl.size();
+    GX_TRY(p->dlist.alloc(std::max<size_t>(dl.size(), 1)));
+    if (!dl.empty())
+        GX_HIP_TRY(hipMemcpy(p->dlist.p, dl.data(), dl.size() * 4, hipMemcpyHostToDevice));
+    p->dgrid = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(1, (p->nd + 4095) / 4096));
+    GX_TRY(p->dpart.alloc(p->dgrid));
+    GX_TRY(p->dticket.alloc(1));
+    GX_HIP_TRY(hipMemset(p->dticket.p, 0, 4));
+    return GX_SUCCESS;
+}
+
+static int pr_dangling(PrPart *p, double *x_local, hipStream_t s) {
+    if (p->nd == 0) return GX_SUCCESS;
+    const int64_t per = (int64_t)((p->nd + p->dgrid - 1) / p->dgrid);
+    hipLaunchKernelGGL(k_pr_dangling, dim3(p->dgrid), dim3(256), 0, s, p->dlist.p, (int64_t)p->nd, per,
+                       x_local, (int64_t)p->chunk - 1, p->dpart.p, p->dticket.p);
+    return check_launch("k_pr_dangling");
+}
+
+int pr_init(PrPart *p, double *x_local, hipStream_t s) {
+    const double inv_n = 1.0 / (double)p->n_global;
+    hipLaunchKernelGGL(k_pr_init, dim3(grid_for(p->rows, 256, 8192)), dim3(256), 0, s, p->outdeg,
+                       (int64_t)p->rows, inv_n, p->damping, x_local, (int64_t)p->chunk - 1,
+                       p->nd == 0 ? 1 : 0);
+    GX_TRY(check_launch("k_pr_init"));
+    return pr_dangling(p, x_local, s);
+}
+
+int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s) {
+    const double dn = (double)p->n_global;
+    PullArgs a;
+    a.blocks = p->blocks.p;
+    a.rp = p->rp;
+    a.ci = p->ci;
+    a.outdeg = p->outdeg;
+    a.x_in = x_full;
+    a.x_out = x_local;
+    a.rank_out = rank_out;
+    a.chunk = (int64_t)p->chunk;
+    a.nranks = p->nranks;
+    a.zero_slot = p->nd == 0 ? 1 : 0;
+    a.teleport0 = (1.0 - p->damping) / dn;
+    a.damping_over_n = p->damping / dn;
+    a.damping = p->damping;
+    a.long_first = p->long_first.p;
+    a.long_nseg = p->long_nseg.p;
+    a.long_part = p->long_part.p;
+    a.long_ticket = p->long_ticket.p;
+    if (p->nblocks) {
+        KTimer kt(p->ctx, "pr_pull", s);
+        hipLaunchKernelGGL(k_pr_pull, dim3(p->nblocks), dim3(kPullBlock), 0, s, a);
+    }
+    GX_TRY(check_launch("k_pr_pull"));
+    return pr_dangling(p, x_local, s);
+}
+
+}  // namespace gx
+
+using namespace gx;
+
+static uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank) {
+    if (!g || !rank) return fail(GX_NULL_POINTER, "gx_pagerank: null argument");
+    if (iters < 0) return fail(GX_INVALID_VALUE, "gx_pagerank: negative iteration count");
+    const uint64_t n = g->n;
+    if (n == 0) return GX_SUCCESS;
+    gx_ctx *ctx = g->ctx;
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    GX_TRY(device_begin(ctx));
+    GX_TRY(ensure_outdeg(g));
+    if (g->directed) GX_TRY(ensure_transpose(g));
+    if (!g->pr) {
+        DevCSR &P = g->directed ? g->AT : g->A;
+        auto *p = new PrPart();
+        p->ctx = ctx;
+        p->n_global = n;
+        p->nranks = 1;
+        p->rank = 0;
+        p->chunk = round_up(n + 1, 32);
+        std::vector<int32_t> h_outdeg(n);
+        for (uint64_t v = 0; v < n; v++) h_outdeg[v] = (int32_t)(g->A.h_rp[v + 1] - g->A.h_rp[v]);
+        int rc = pr_plan(p, P.h_rp, P.rp.p, P.ci.p, g->outdeg.p, h_outdeg);
+        if (rc == GX_SUCCESS) rc = p->xa.alloc(p->chunk);
+        if (rc == GX_SUCCESS) rc = p->xb.alloc(p->chunk);
+        if (rc == GX_SUCCESS) rc = p->rank_out.alloc(n);
+        if (rc != GX_SUCCESS) {
+            delete p;
+            return rc;
+        }
+        g->pr = p;
+    }
+    PrPart *p = g->pr;
+    p->damping = damping;
+    double *cur = p->xa.p, *nxt = p->xb.p;
+    GX_TRY(pr_init(p, cur, s));
+    for (int it = 0; it < iters; it++) {
+        GX_TRY(pr_step(p, cur, nxt, it == iters - 1 ? p->rank_out.p : nullptr, s));
+        std::swap(cur, nxt);
+    }
+    GX_TRY(device_end(ctx));
+    if (iters == 0) {
+        for (uint64_t v = 0; v < n; v++) rank[v] = 1.0 / (double)n;
+        return GX_SUCCESS;
+    }
+    GX_HIP_TRY(hipMemcpyAsync(rank, p->rank_out.p, n * 8, hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    return GX_SUCCESS;
+}
+
+// ---------------------------------------------------------------- row partition API
+
+extern "C" int gx_pr_part_create(gx_ctx *ctx, uint64_t n_global, int nranks, int rank,
+                                 const uint64_t *row_ranges, const uint64_t *rowptr_local,
+                                 const uint64_t *colidx_local, const uint64_t *outdeg_local,
+                                 double damping, gx_pr_part **out) {
+    if (!ctx || !row_ranges || !rowptr_local || !outdeg_local || !out)
+        return fail(GX_NULL_POINTER, "gx_pr_part_create: null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GX_INVALID_VALUE, "bad rank/nranks");
+    if (row_ranges[0] != 0 || row_ranges[nranks] != n_global)
+        return fail(GX_INVALID_VALUE, "row_ranges must cover [0, n)");
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    uint64_t maxrows = 0;
+    for (int k = 0; k < nranks; k++) {
+        if (row_ranges[k + 1] < row_ranges[k]) return fail(GX_INVALID_VALUE, "row_ranges not monotone");
+        maxrows = std::max(maxrows, row_ranges[k + 1] - row_ranges[k]);
+    }
+    const uint64_t chunk = round_up(maxrows + 1, 32);
+    if (chunk * (uint64_t)nranks >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "partition too large");
+    const uint64_t rows = row_ranges[rank + 1] - row_ranges[rank];
+    const uint64_t nnz = rowptr_local[rows];
+    if (nnz && !colidx_local) return fail(GX_NULL_POINTER, "null colidx");
+    std::vector<int64_t> h_rp(rows + 1);
+    for (uint64_t i = 0; i <= rows; i++) h_rp[i] = (int64_t)rowptr_local[i];
+    std::vector<int32_t> ci(nnz);
+    for (uint64_t k = 0; k < nnz; k++) {
+        const uint64_t c = colidx_local[k];
+        if (c >= n_global) return fail(GX_INVALID_INDEX, "column out of range");
+        const int owner = (int)(std::upper_bound(row_ranges, row_ranges + nranks + 1, c) - row_ranges) - 1;
+        ci[k] = (int32_t)((uint64_t)owner * chunk + (c - row_ranges[owner]));
+    }
+    std::vector<int32_t> h_outdeg(rows);
+    for (uint64_t i = 0; i < rows; i++) h_outdeg[i] = (int32_t)outdeg_local[i];
+    auto *p = new PrPart();
+    p->ctx = ctx;
+    p->n_global = n_global;
+    p->nranks = nranks;
+    p->rank = rank;
+    p->chunk = chunk;
+    p->damping = damping;
+    int rc = p->rp_own.alloc(rows + 1);
+    if (rc == GX_SUCCESS) rc = p->ci_own.alloc(nnz, 16);
+    if (rc == GX_SUCCESS) rc = p->outdeg_own.alloc(std::max<uint64_t>(rows, 1));
+    hipError_t e = hipSuccess;
+    if (rc == GX_SUCCESS) e = hipMemcpy(p->rp_own.p, h_rp.data(), (rows + 1) * 8, hipMemcpyHostToDevice);
+    if (rc == GX_SUCCESS && e == hipSuccess && nnz)
+        e = hipMemcpy(p->ci_own.p, ci.data(), nnz * 4, hipMemcpyHostToDevice);
+    if (rc == GX_SUCCESS && e == hipSuccess && rows)
+        e = hipMemcpy(p->outdeg_own.p, h_outdeg.data(), rows * 4, hipMemcpyHostToDevice);
+    if (rc == GX_SUCCESS && e != hipSuccess)
+        rc = fail(GX_DEVICE_ERROR, std::string("gx_pr_part_create upload: ") + hipGetErrorString(e));
+    if (rc == GX_SUCCESS) rc = pr_plan(p, h_rp, p->rp_own.p, p->ci_own.p, p->outdeg_own.p, h_outdeg);
+    if (rc != GX_SUCCESS) {
+        delete p;
+        return rc;
+    }
+    *out = reinterpret_cast<gx_pr_part *>(p);
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_pr_part_chunk(gx_pr_part *part, uint64_t *chunk) {
+    if (!part || !chunk) return fail(GX_NULL_POINTER, "null argument");
+    *chunk = reinterpret_cast<PrPart *>(part)->chunk;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_pr_part_init(gx_pr_part *part, double *x_local, void *stream) {
+    if (!part || !x_local) return fail(GX_NULL_POINTER, "null argument");
+    PrPart *p = reinterpret_cast<PrPart *>(part);
+    GX_HIP_TRY(hipSetDevice(p->ctx->device));
+    return pr_init(p, x_local, stream ? (hipStream_t)stream : p->ctx->stream);
+}
+
+extern "C" int gx_pr_part_step(gx_pr_part *part, const double *x_full, double *x_local,
+                               double *rank_out, void *stream) {
+    if (!part || !x_full || !x_local) return fail(GX_NULL_POINTER, "null argument");
+    PrPart *p = reinterpret_cast<PrPart *>(part);
+    GX_HIP_TRY(hipSetDevice(p->ctx->device));
+    return pr_step(p, x_full, x_local, rank_out, stream ? (hipStream_t)stream : p->ctx->stream);
+}
+
+extern "C" int gx_pr_part_free(gx_pr_part *part) {
+    if (!part) return GX_SUCCESS;
+    PrPart *p = reinterpret_cast<PrPart *>(part);
+    (void)hipSetDevice(p->ctx->device);
+    (void)hipDeviceSynchronize();
+    delete p;
+    return GX_SUCCESS;
+}

@@ -1,0 +1,409 @@
+// gx_runtime.hip -- context, device graph upload and on-device graph transforms.
+//
+// Replaces LAGraph_Init / LAGraph_New / LAGraph_Cached_AT / the A LOR A' symmetrisation
+// the reference runs inside SuiteSparse (pr.cpp:58-60, wcc.cpp:53-55, lcc.cpp:68).
+// The transforms run on the device with rocPRIM radix sorts over packed 64-bit
+// (row << 32 | col) keys, so their rows come out sorted by column.
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <cstring>
+
+#include "gx_device.h"
+#include "gx_pr.h"
+
+using namespace gx;
+
+// ----------------------------------------------------------------------------- ctx
+
+extern "C" int gx_device_count(int *count) {
+    if (!count) return fail(GX_NULL_POINTER, "gx_device_count: null");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    *count = c;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_init(int device, gx_ctx **out) {
+    if (!out) return fail(GX_NULL_POINTER, "gx_init: null ctx");
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0)
+        return fail(GX_DEVICE_ERROR, "gx_init: no HIP device visible (libgx has no CPU fallback)");
+    if (device < 0 || device >= count) return fail(GX_INVALID_VALUE, "gx_init: bad device index");
+    GX_HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    GX_HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(GX_DEVICE_ERROR, std::string("gx_init: libgx is built for gfx950, device is ") +
+                                         prop.gcnArchName);
+    gx_ctx *ctx = new gx_ctx();
+    ctx->device = device;
+    ctx->device_name = prop.name;
+    ctx->num_cus = prop.multiProcessorCount;
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(GX_DEVICE_ERROR, std::string("gx_init: ") + hipGetErrorString(e));
+    }
+    *out = ctx;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_free(gx_ctx *ctx) {
+    if (!ctx) return GX_SUCCESS;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto &p : ctx->pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_device_info(gx_ctx *ctx, char *name, size_t name_len, int *num_cus) {
+    if (!ctx) return fail(GX_NULL_POINTER, "gx_device_info: null ctx");
+    if (name && name_len) {
+        std::strncpy(name, ctx->device_name.c_str(), name_len - 1);
+        name[name_len - 1] = '\0';
+    }
+    if (num_cus) *num_cus = ctx->num_cus;
+    return GX_SUCCESS;
+}
+
+// -------------------------------------------------------------------------- timing
+
+namespace gx {
+
+int collect_timings(gx_ctx *ctx) {
+    if (ctx->pending.empty()) return GX_SUCCESS;
+    GX_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (auto &p : ctx->pending) {
+        (void)hipEventSynchronize(p.b);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            auto &s = ctx->stats[p.name];
+            s.first += 1;
+            s.second += ms;
+        }
+        ctx->event_pool.push_back(p.a);
+        ctx->event_pool.push_back(p.b);
+    }
+    ctx->pending.clear();
+    return GX_SUCCESS;
+}
+
+int device_begin(gx_ctx *ctx) {
+    GX_HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    return GX_SUCCESS;
+}
+
+int device_end(gx_ctx *ctx) {
+    GX_HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    GX_HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float ms = 0.f;
+    GX_HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last_device_ms = ms;
+    return GX_SUCCESS;
+}
+
+}  // namespace gx
+
+extern "C" int gx_set_kernel_timing(gx_ctx *ctx, int enable) {
+    if (!ctx) return fail(GX_NULL_POINTER, "null ctx");
+    ctx->timing = enable != 0;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_kernel_stats(gx_ctx *ctx, const char *kernel, uint64_t *launches,
+                               double *total_ms) {
+    if (!ctx || !kernel) return fail(GX_NULL_POINTER, "null argument");
+    GX_TRY(collect_timings(ctx));
+    auto it = ctx->stats.find(kernel);
+    if (launches) *launches = it == ctx->stats.end() ? 0 : it->second.first;
+    if (total_ms) *total_ms = it == ctx->stats.end() ? 0.0 : it->second.second;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_reset_kernel_stats(gx_ctx *ctx) {
+    if (!ctx) return fail(GX_NULL_POINTER, "null ctx");
+    GX_TRY(collect_timings(ctx));
+    ctx->stats.clear();
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_last_device_ms(gx_ctx *ctx, double *ms) {
+    if (!ctx || !ms) return fail(GX_NULL_POINTER, "null argument");
+    *ms = ctx->last_device_ms;
+    return GX_SUCCESS;
+}
+
+// --------------------------------------------------------------------------- graph
+
+extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **out) {
+    if (!ctx || !A || !out) return fail(GX_NULL_POINTER, "gx_graph_create: null argument");
+    *out = nullptr;
+    if (!A->rowptr || (A->nnz && !A->colidx))
+        return fail(GX_NULL_POINTER, "gx_graph_create: null CSR arrays");
+    if (A->n >= (1ull << 31) - 64)
+        return fail(GX_NOT_IMPLEMENTED, "gx_graph_create: n >= 2^31 needs 64-bit column indices");
+    if (A->rowptr[0] != 0 || A->rowptr[A->n] != A->nnz)
+        return fail(GX_INVALID_VALUE, "gx_graph_create: inconsistent row pointers");
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    const uint64_t n = A->n, nnz = A->nnz;
+    std::vector<int32_t> ci(nnz);
+    for (uint64_t i = 0; i < n; i++) {
+        if (A->rowptr[i + 1] < A->rowptr[i])
+            return fail(GX_INVALID_VALUE, "gx_graph_create: row pointers not monotone");
+    }
+    for (uint64_t k = 0; k < nnz; k++) {
+        if (A->colidx[k] >= n) return fail(GX_INVALID_INDEX, "gx_graph_create: column out of range");
+        ci[k] = (int32_t)A->colidx[k];
+    }
+    gx_graph *g = new gx_graph();
+    g->ctx = ctx;
+    g->n = n;
+    g->nnz = nnz;
+    g->directed = directed != 0;
+    g->weighted = A->vals != nullptr;
+    g->A.n = n;
+    g->A.nnz = nnz;
+    g->A.h_rp.assign(A->rowptr, A->rowptr + n + 1);
+    int rc = g->A.rp.alloc(n + 1);
+    if (rc == GX_SUCCESS) rc = g->A.ci.alloc(nnz, 16);
+    if (rc == GX_SUCCESS && g->weighted) rc = g->A.w.alloc(nnz);
+    if (rc != GX_SUCCESS) {
+        delete g;
+        return rc;
+    }
+    hipError_t e = hipMemcpy(g->A.rp.p, g->A.h_rp.data(), (n + 1) * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz) e = hipMemcpy(g->A.ci.p, ci.data(), nnz * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && g->weighted && nnz)
+        e = hipMemcpy(g->A.w.p, A->vals, nnz * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        delete g;
+        return fail(GX_DEVICE_ERROR, std::string("gx_graph_create: upload failed: ") + hipGetErrorString(e));
+    }
+    g->A.built = true;
+    *out = g;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_graph_free(gx_graph *g) {
+    if (!g) return GX_SUCCESS;
+    (void)hipSetDevice(g->ctx->device);
+    (void)hipStreamSynchronize(g->ctx->stream);
+    delete g->pr;
+    delete g;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_graph_info(gx_graph *g, uint64_t *n, uint64_t *nnz, int *directed, int *weighted) {
+    if (!g) return fail(GX_NULL_POINTER, "gx_graph_info: null graph");
+    if (n) *n = g->n;
+    if (nnz) *nnz = g->nnz;
+    if (directed) *directed = g->directed;
+    if (weighted) *weighted = g->weighted;
+    return GX_SUCCESS;
+}
+
+// ------------------------------------------------------------------ device transforms
+
+namespace {
+
+constexpr int kBuildBlock = 256;
+constexpr int kEdgesPerThread = 16;
+
+// keys[k] = (col << 32) | row for every edge k of A (one chunk of edges per thread).
+__global__ void k_transpose_keys(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                 int64_t n, int64_t nnz, uint64_t *__restrict__ keys) {
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t e0 = t * kEdgesPerThread;
+    if (e0 >= nnz) return;
+    int64_t e1 = min(e0 + kEdgesPerThread, nnz);
+    int64_t r = row_of_edge(rp, n, e0);
+    for (int64_t e = e0; e < e1; e++) {
+        while (rp[r + 1] <= e) r++;
+        keys[e] = ((uint64_t)(uint32_t)ci[e] << 32) | (uint32_t)r;
+    }
+}
+
+// Closure keys: both orientations of every non-loop edge, flag 1 (stored v->u) / 2 (u->v).
+__global__ void k_closure_keys(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                               int64_t n, int64_t nnz, uint64_t *__restrict__ keys,
+                               uint8_t *__restrict__ flags) {
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t e0 = t * kEdgesPerThread;
+    if (e0 >= nnz) return;
+    int64_t e1 = min(e0 + kEdgesPerThread, nnz);
+    int64_t r = row_of_edge(rp, n, e0);
+    for (int64_t e = e0; e < e1; e++) {
+        while (rp[r + 1] <= e) r++;
+        uint32_t u = (uint32_t)r, v = (uint32_t)ci[e];
+        if (u == v) {   // self-loop: sorts to the very end, dropped by count
+            keys[2 * e] = keys[2 * e + 1] = ~0ull;
+            flags[2 * e] = flags[2 * e + 1] = 0;
+        } else {
+            keys[2 * e] = ((uint64_t)u << 32) | v;
+            flags[2 * e] = 1;
+            keys[2 * e + 1] = ((uint64_t)v << 32) | u;
+            flags[2 * e + 1] = 2;
+        }
+    }
+}
+
+// rp[r] = lower_bound(keys, r << 32) for r in [0, n]; ci[k] = low word of keys[k].
+__global__ void k_keys_to_csr(const uint64_t *__restrict__ keys, int64_t m, int64_t n,
+                              int64_t *__restrict__ rp, int32_t *__restrict__ ci) {
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t <= n) {
+        uint64_t target = (uint64_t)t << 32;
+        int64_t lo = 0, hi = m;
+        while (lo < hi) {
+            int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < target) lo = mid + 1;
+            else hi = mid;
+        }
+        rp[t] = lo;
+    }
+    for (int64_t k = t; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        ci[k] = (int32_t)(uint32_t)(keys[k] & 0xffffffffu);
+}
+
+__global__ void k_outdeg(const int64_t *__restrict__ rp, int64_t n, int32_t *__restrict__ deg) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+         v += (int64_t)gridDim.x * blockDim.x)
+        deg[v] = (int32_t)(rp[v + 1] - rp[v]);
+}
+
+struct BitOr {
+    __device__ __host__ uint8_t operator()(uint8_t a, uint8_t b) const { return a | b; }
+};
+
+int key_bits(uint64_t n) {
+    int b = 1;
+    while ((1ull << b) < n) b++;
+    return 32 + b;   // (row << 32) | col with row < n
+}
+
+}  // namespace
+
+namespace gx {
+
+int ensure_outdeg(gx_graph *g) {
+    if (g->outdeg.p) return GX_SUCCESS;
+    GX_TRY(g->outdeg.alloc(g->n));
+    hipLaunchKernelGGL(k_outdeg, dim3(grid_for(g->n, 256, 4096)), dim3(256), 0, g->ctx->stream,
+                       g->A.rp.p, (int64_t)g->n, g->outdeg.p);
+    return check_launch("k_outdeg");
+}
+
+int ensure_transpose(gx_graph *g) {
+    if (g->AT.built) return GX_SUCCESS;
+    hipStream_t s = g->ctx->stream;
+    const uint64_t n = g->n, nnz = g->nnz;
+    DBuf<uint64_t> k0, k1;
+    DBuf<double> w1;
+    GX_TRY(k0.alloc(nnz));
+    GX_TRY(k1.alloc(nnz));
+    GX_TRY(g->AT.rp.alloc(n + 1));
+    GX_TRY(g->AT.ci.alloc(nnz, 16));
+    if (g->weighted) GX_TRY(g->AT.w.alloc(nnz));
+    if (nnz) {
+        unsigned grid = grid_for((nnz + kEdgesPerThread - 1) / kEdgesPerThread, kBuildBlock, 1u << 30);
+        hipLaunchKernelGGL(k_transpose_keys, dim3(grid), dim3(kBuildBlock), 0, s, g->A.rp.p,
+                           g->A.ci.p, (int64_t)n, (int64_t)nnz, k0.p);
+        GX_TRY(check_launch("k_transpose_keys"));
+        size_t tmp_bytes = 0;
+        const int bits = key_bits(n);
+        if (g->weighted) {
+            GX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, k0.p, k1.p, g->A.w.p, g->AT.w.p,
+                                                 (size_t)nnz, 0, bits, s));
+        } else {
+            GX_HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, k0.p, k1.p, (size_t)nnz, 0, bits, s));
+        }
+        DBuf<char> tmp;
+        GX_TRY(tmp.alloc(tmp_bytes));
+        if (g->weighted) {
+            GX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_bytes, k0.p, k1.p, g->A.w.p, g->AT.w.p,
+                                                 (size_t)nnz, 0, bits, s));
+        } else {
+            GX_HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, k0.p, k1.p, (size_t)nnz, 0, bits, s));
+        }
+    }
+    hipLaunchKernelGGL(k_keys_to_csr, dim3(grid_for(n + 1, 256, 1u << 30)), dim3(256), 0, s, k1.p,
+                       (int64_t)nnz, (int64_t)n, g->AT.rp.p, g->AT.ci.p);
+    GX_TRY(check_launch("k_keys_to_csr"));
+    g->AT.n = n;
+    g->AT.nnz = nnz;
+    g->AT.h_rp.resize(n + 1);
+    GX_HIP_TRY(hipMemcpyAsync(g->AT.h_rp.data(), g->AT.rp.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    g->AT.built = true;
+    return GX_SUCCESS;
+}
+
+int ensure_closure(gx_graph *g) {
+    if (g->S.built) return GX_SUCCESS;
+    hipStream_t s = g->ctx->stream;
+    const uint64_t n = g->n, nnz = g->nnz, m2 = 2 * nnz;
+    DBuf<uint64_t> k0, k1, uk;
+    DBuf<uint8_t> f0, f1;
+    DBuf<uint64_t> count;
+    GX_TRY(k0.alloc(m2));
+    GX_TRY(k1.alloc(m2));
+    GX_TRY(f0.alloc(m2));
+    GX_TRY(f1.alloc(m2));
+    GX_TRY(uk.alloc(m2));
+    GX_TRY(count.alloc(1));
+    GX_TRY(g->S.rp.alloc(n + 1));
+    uint64_t m = 0;
+    if (nnz) {
+        unsigned grid = grid_for((nnz + kEdgesPerThread - 1) / kEdgesPerThread, kBuildBlock, 1u << 30);
+        hipLaunchKernelGGL(k_closure_keys, dim3(grid), dim3(kBuildBlock), 0, s, g->A.rp.p, g->A.ci.p,
+                           (int64_t)n, (int64_t)nnz, k0.p, f0.p);
+        GX_TRY(check_launch("k_closure_keys"));
+        size_t tmp_sort = 0, tmp_red = 0;
+        GX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_sort, k0.p, k1.p, f0.p, f1.p, (size_t)m2, 0, 64, s));
+        GX_HIP_TRY(rocprim::reduce_by_key(nullptr, tmp_red, k1.p, f1.p, (size_t)m2, uk.p, f0.p, count.p,
+                                          BitOr(), rocprim::equal_to<uint64_t>(), s));
+        DBuf<char> tmp;
+        GX_TRY(tmp.alloc(std::max(tmp_sort, tmp_red)));
+        GX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_sort, k0.p, k1.p, f0.p, f1.p, (size_t)m2, 0, 64, s));
+        GX_HIP_TRY(rocprim::reduce_by_key(tmp.p, tmp_red, k1.p, f1.p, (size_t)m2, uk.p, f0.p, count.p,
+                                          BitOr(), rocprim::equal_to<uint64_t>(), s));
+        GX_HIP_TRY(hipMemcpyAsync(&m, count.p, 8, hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+        // a trailing ~0 key collects every self-loop
+        if (m > 0) {
+            uint64_t last = 0;
+            GX_HIP_TRY(hipMemcpy(&last, uk.p + (m - 1), 8, hipMemcpyDeviceToHost));
+            if (last == ~0ull) m--;
+        }
+    }
+    GX_TRY(g->S.ci.alloc(m, 16));
+    GX_TRY(g->S.flag.alloc(m));
+    hipLaunchKernelGGL(k_keys_to_csr, dim3(grid_for(n + 1, 256, 1u << 30)), dim3(256), 0, s, uk.p,
+                       (int64_t)m, (int64_t)n, g->S.rp.p, g->S.ci.p);
+    GX_TRY(check_launch("k_keys_to_csr"));
+    if (m) GX_HIP_TRY(hipMemcpyAsync(g->S.flag.p, f0.p, m, hipMemcpyDeviceToDevice, s));
+    g->S.n = n;
+    g->S.nnz = m;
+    g->S.h_rp.resize(n + 1);
+    GX_HIP_TRY(hipMemcpyAsync(g->S.h_rp.data(), g->S.rp.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    g->S.built = true;
+    return GX_SUCCESS;
+}
+
+}  // namespace gx

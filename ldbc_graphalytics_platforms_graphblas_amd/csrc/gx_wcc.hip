@@ -1,0 +1,117 @@
+// gx_wcc.hip -- weakly connected components by min-label hooking + pointer jumping.
+//
+// Replaces WeaklyConnectedComponents -> GrB_eWiseAdd(A, LOR, A, A') + LAGr_ConnectedComponents
+// (wcc.cpp:39-66).  Hooking treats every stored edge (u, v) as undirected, so the explicit
+// symmetrisation the reference performs inside processing time is not needed.
+//   hook     : edge-balanced (one chunk of kEdgesPerThread entries per thread); the roots
+//              ru, rv of both endpoints are found by following parent pointers and the larger
+//              root is hooked below the smaller one with atomicMin.
+//   compress : pointer jumping until every vertex points at its root.
+// parent[v] <= v always holds, so the root of each final tree is the smallest vertex index
+// of the component: comp[v] is canonical and equals the oracle's union-find labels exactly.
+#include "gx_device.h"
+
+namespace gx {
+namespace {
+
+constexpr int kWccBlock = 256;
+constexpr int kWccEdgesPerThread = 16;
+
+__device__ __forceinline__ int32_t find_root(const int32_t *parent, int32_t v) {
+    int32_t p = parent[v];
+    while (p != v) {
+        v = p;
+        p = parent[v];
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kWccBlock) void k_wcc_hook(const int64_t *__restrict__ rp,
+                                                        const int32_t *__restrict__ ci, int64_t n,
+                                                        int64_t nnz, int32_t *parent, int *changed) {
+    const int64_t t = (int64_t)blockIdx.x * kWccBlock + threadIdx.x;
+    const int64_t e0 = t * kWccEdgesPerThread;
+    bool any = false;
+    if (e0 < nnz) {
+        const int64_t e1 = min(e0 + kWccEdgesPerThread, nnz);
+        int64_t r = row_of_edge(rp, n, e0);
+        for (int64_t e = e0; e < e1; e++) {
+            while (rp[r + 1] <= e) r++;
+            int32_t ru = find_root(parent, (int32_t)r);
+            int32_t rv = find_root(parent, ci[e]);
+            if (ru != rv) {
+                const int32_t hi = max(ru, rv), lo = min(ru, rv);
+                atomicMin(&parent[hi], lo);
+                any = true;
+            }
+        }
+    }
+    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) *changed = 1;
+}
+
+__global__ __launch_bounds__(kWccBlock) void k_wcc_compress(int32_t *parent, int64_t n) {
+    for (int64_t v = (int64_t)blockIdx.x * kWccBlock + threadIdx.x; v < n;
+         v += (int64_t)gridDim.x * kWccBlock) {
+        int32_t p = parent[v];
+        int32_t pp = parent[p];
+        while (p != pp) {
+            p = pp;
+            pp = parent[p];
+        }
+        parent[v] = p;
+    }
+}
+
+__global__ void k_iota(int32_t *a, int64_t n) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+         v += (int64_t)gridDim.x * blockDim.x)
+        a[v] = (int32_t)v;
+}
+
+}  // namespace
+}  // namespace gx
+
+using namespace gx;
+
+extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
+    if (!g || !comp) return fail(GX_NULL_POINTER, "gx_wcc: null argument");
+    gx_ctx *ctx = g->ctx;
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int64_t n = (int64_t)g->n, nnz = (int64_t)g->nnz;
+    if (n == 0) return GX_SUCCESS;
+    DBuf<int32_t> parent;
+    DBuf<int> changed;
+    GX_TRY(parent.alloc(n));
+    GX_TRY(changed.alloc(1));
+    GX_TRY(device_begin(ctx));
+    hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, parent.p, n);
+    GX_TRY(check_launch("k_iota"));
+    const unsigned hook_grid =
+        grid_for((uint64_t)((nnz + kWccEdgesPerThread - 1) / kWccEdgesPerThread), kWccBlock, 1u << 30);
+    for (int round = 0;; round++) {
+        int h_changed = 0;
+        GX_HIP_TRY(hipMemsetAsync(changed.p, 0, sizeof(int), s));
+        if (nnz) {
+            KTimer kt(ctx, "wcc_hook", s);
+            hipLaunchKernelGGL(k_wcc_hook, dim3(hook_grid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
+                               nnz, parent.p, changed.p);
+        }
+        GX_TRY(check_launch("k_wcc_hook"));
+        {
+            KTimer kt(ctx, "wcc_compress", s);
+            hipLaunchKernelGGL(k_wcc_compress, dim3(grid_for(n, kWccBlock, 8192)), dim3(kWccBlock), 0, s,
+                               parent.p, n);
+        }
+        GX_TRY(check_launch("k_wcc_compress"));
+        GX_HIP_TRY(hipMemcpyAsync(&h_changed, changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+        if (!h_changed) break;
+        if (round > 100000) return fail(GX_PANIC, "gx_wcc: hooking did not converge");
+    }
+    GX_TRY(device_end(ctx));
+    std::vector<int32_t> h(n);
+    GX_HIP_TRY(hipMemcpy(h.data(), parent.p, n * 4, hipMemcpyDeviceToHost));
+    for (int64_t v = 0; v < n; v++) comp[v] = (uint64_t)h[v];
+    return GX_SUCCESS;
+}

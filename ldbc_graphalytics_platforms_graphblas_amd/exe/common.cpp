@@ -1,0 +1,194 @@
+// common.cpp -- shared driver of the Graphalytics executables (see common.h).
+#include "common.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cinttypes>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <memory>
+
+#include <omp.h>
+
+namespace gxexe {
+
+BenchmarkParameters ParseBenchmarkParameters(int argc, char **argv) {
+    BenchmarkParameters p;
+    for (int i = 0; i + 1 < argc; i++) {
+        const char *key = argv[i];
+        const char *value = argv[i + 1];
+        if (std::strcmp(key, "--binary") == 0) p.binary = std::strcmp(value, "true") == 0;
+        else if (std::strcmp(key, "--input-dir") == 0) p.input_dir = value;
+        else if (std::strcmp(key, "--directed") == 0) p.directed = std::strcmp(value, "true") == 0;
+        else if (std::strcmp(key, "--source-vertex") == 0) p.source_vertex = std::stoul(value);
+        else if (std::strcmp(key, "--damping-factor") == 0) p.damping_factor = std::stod(value);
+        else if (std::strcmp(key, "--max-iteration") == 0) p.max_iteration = std::stoi(value);
+        else if (std::strcmp(key, "--output-file") == 0) p.output_file = value;
+        else if (std::strcmp(key, "--threadnum") == 0) p.thread_num = std::stoul(value);
+    }
+    return p;
+}
+
+long long GetCurrentMilliseconds() {
+    using namespace std::chrono;
+    return duration_cast<milliseconds>(system_clock::now().time_since_epoch()).count();
+}
+
+void OK(int info, const char *what) {
+    if (info != GX_SUCCESS)
+        throw std::runtime_error(std::string("GraphBLAS error [") + std::to_string(info) + "]  " + what +
+                                 ": " + gx_last_error());
+}
+
+namespace {
+
+struct CsrHolder {
+    gx_csr csr{};
+    ~CsrHolder() { gx_csr_release(&csr); }
+};
+
+struct IdsHolder {
+    uint64_t *ids = nullptr;
+    uint64_t n = 0;
+    ~IdsHolder() { gx_host_free(ids); }
+};
+
+struct CtxHolder {
+    gx_ctx *ctx = nullptr;
+    gx_graph *g = nullptr;
+    ~CtxHolder() {
+        gx_graph_free(g);
+        gx_free(ctx);
+    }
+};
+
+// ReadMatrixMarket (graphio.cpp:4-32) without SuiteSparse
+void ReadMatrix(const BenchmarkParameters &p, gx_csr *out) {
+    if (p.binary) OK(gx_read_grb((p.input_dir + "/graph.grb").c_str(), out), "reading graph.grb");
+    else OK(gx_read_mtx((p.input_dir + "/graph.mtx").c_str(), out), "reading graph.mtx");
+}
+
+// ReadMapping (graphio.cpp:34-60)
+void ReadMapping(const BenchmarkParameters &p, IdsHolder *m) {
+    if (p.binary) OK(gx_read_vtb((p.input_dir + "/graph.vtb").c_str(), &m->ids, &m->n), "reading graph.vtb");
+    else OK(gx_read_vtx((p.input_dir + "/graph.vtx").c_str(), &m->ids, &m->n), "reading graph.vtx");
+}
+
+struct OutFile {
+    FILE *f = nullptr;
+    std::vector<char> buf;
+    explicit OutFile(const std::string &path) : buf(1 << 22) {
+        f = std::fopen(path.c_str(), "w");
+        if (!f) {
+            std::cerr << "Output file " << path << " does not exists" << std::endl;
+            std::exit(-1);
+        }
+        std::setvbuf(f, buf.data(), _IOFBF, buf.size());
+    }
+    ~OutFile() {
+        if (f) std::fclose(f);
+    }
+};
+
+// "%.16e" == ostream precision(16) + std::scientific (pr.cpp:26-27)
+void PutDouble(FILE *f, uint64_t id, double x) { std::fprintf(f, "%" PRIu64 " %.16e\n", id, x); }
+
+}  // namespace
+
+int Main(int argc, char **argv, Algorithm alg) {
+    try {
+        BenchmarkParameters p = ParseBenchmarkParameters(argc, argv);
+        if (p.thread_num > 0) omp_set_num_threads((int)p.thread_num);
+        int device = 0;
+        if (const char *d = std::getenv("GX_DEVICE")) device = std::atoi(d);
+
+        CsrHolder A;
+        ReadMatrix(p, &A.csr);
+        IdsHolder mapping;
+        ReadMapping(p, &mapping);
+        const uint64_t n = mapping.n;
+        if (A.csr.n != n) throw std::runtime_error("graph and mapping sizes differ");
+
+        uint64_t src = 0;
+        if (alg == Algorithm::BFS || alg == Algorithm::SSSP) {
+            // linear search of the original id, as bfs.cpp:94-103 / sssp.cpp:93-102
+            const uint64_t *it = std::find(mapping.ids, mapping.ids + n, (uint64_t)p.source_vertex);
+            if (it == mapping.ids + n) {
+                std::cout << "Source vertex not found in mapping" << std::endl;
+                return -1;
+            }
+            src = (uint64_t)(it - mapping.ids);
+        }
+
+        CtxHolder H;
+        OK(gx_init(device, &H.ctx), "gx_init");
+        std::vector<int64_t> level;
+        std::vector<double> vals;
+        std::vector<uint64_t> labels;
+
+        std::cout << "Processing starts at: " << GetCurrentMilliseconds() << std::endl;
+        OK(gx_graph_create(H.ctx, &A.csr, p.directed ? 1 : 0, &H.g), "gx_graph_create");
+        switch (alg) {
+            case Algorithm::BFS:
+                level.resize(n);
+                OK(gx_bfs(H.g, src, level.data()), "gx_bfs");
+                break;
+            case Algorithm::PR:
+                vals.resize(n);
+                OK(gx_pagerank(H.g, p.damping_factor, p.max_iteration, vals.data()), "gx_pagerank");
+                break;
+            case Algorithm::SSSP:
+                vals.resize(n);
+                OK(gx_sssp(H.g, src, vals.data()), "gx_sssp");
+                break;
+            case Algorithm::WCC:
+                labels.resize(n);
+                OK(gx_wcc(H.g, labels.data()), "gx_wcc");
+                break;
+            case Algorithm::CDLP:
+                labels.resize(n);
+                OK(gx_cdlp(H.g, p.max_iteration, labels.data()), "gx_cdlp");
+                break;
+            case Algorithm::LCC:
+                vals.resize(n);
+                OK(gx_lcc(H.g, vals.data()), "gx_lcc");
+                break;
+        }
+        std::cout << "Processing ends at: " << GetCurrentMilliseconds() << std::endl;
+        double dev_ms = 0;
+        gx_last_device_ms(H.ctx, &dev_ms);
+        std::cout << "Device time: " << dev_ms << " ms" << std::endl;
+
+        OutFile out(p.output_file);
+        const uint64_t *ids = mapping.ids;
+        switch (alg) {
+            case Algorithm::BFS:   // SerializeBFSResult (bfs.cpp:11-68)
+                for (uint64_t v = 0; v < n; v++) std::fprintf(out.f, "%" PRIu64 " %" PRId64 "\n", ids[v], level[v]);
+                break;
+            case Algorithm::PR:    // SerializePageRankResult (pr.cpp:17-45)
+            case Algorithm::LCC:   // SerializeLCCResult (lcc.cpp:17-59)
+                for (uint64_t v = 0; v < n; v++) PutDouble(out.f, ids[v], vals[v]);
+                break;
+            case Algorithm::SSSP:  // SerializeSSSPResult (sssp.cpp:11-51)
+                for (uint64_t v = 0; v < n; v++) {
+                    if (std::isinf(vals[v])) std::fprintf(out.f, "%" PRIu64 " infinity\n", ids[v]);
+                    else PutDouble(out.f, ids[v], vals[v]);
+                }
+                break;
+            case Algorithm::WCC:   // SerializeWCCResult (wcc.cpp:11-37), label -> original id
+            case Algorithm::CDLP:  // SerializeCDLPResult (cdlp.cpp:21-52): mapping[label]
+                for (uint64_t v = 0; v < n; v++)
+                    std::fprintf(out.f, "%" PRIu64 " %" PRIu64 "\n", ids[v], ids[labels[v]]);
+                break;
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        std::cerr << e.what() << std::endl;
+        return 1;
+    }
+}
+
+}  // namespace gxexe

@@ -1,0 +1,160 @@
+"""HIP path vs the oracle and vs the Graphalytics validation outputs (runs on the MI355X).
+
+Bars: bit-exact for BFS levels, WCC labels, CDLP labels, SSSP distances and
+LCC values (integer counts + one fp64 division); PageRank within 1e-12 relative of the fp64
+oracle (the GPU sums each row in a different order) and 1e-4 of the validation files.
+"""
+import numpy as np
+import pytest
+
+from conftest import VALIDATION, FIXTURES, alg_params, check_against_validation, internal_index, \
+    read_validation, split_validation
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+PR_RTOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def gpu_run(ctx, g, alg, **p):
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    G = A.Graph(ctx, g.csr if not isinstance(g, tuple) else g[0], g.directed if not isinstance(g, tuple) else g[1])
+    try:
+        if alg == "BFS":
+            return A.LA_BFS(G, p["source"])
+        if alg == "SSSP":
+            return A.LA_SSSP(G, p["source"])
+        if alg == "PR":
+            return A.LA_PR(G, p["damping"], p["iters"])
+        if alg == "WCC":
+            return A.WeaklyConnectedComponents(G)
+        if alg == "CDLP":
+            return A.LA_CDLP(G, p["iters"])
+        if alg == "LCC":
+            return A.LA_LCC(G)
+    finally:
+        G.close()
+    raise AssertionError(alg)
+
+
+@pytest.mark.parametrize("name", VALIDATION)
+def test_gpu_matches_validation(ctx, name, fixture_graphs):
+    graph, alg = split_validation(name)
+    g = fixture_graphs(graph)
+    p = alg_params(g, alg)
+    if "source" in p:
+        p["source"] = internal_index(g.mapping, p["source"])
+    got = gpu_run(ctx, g, alg, **p)
+    check_against_validation(alg, g.mapping, got, read_validation(FIXTURES / name))
+
+
+class _G:
+    def __init__(self, csr, directed):
+        self.csr = csr
+        self.directed = directed
+
+
+def _rmat(scale, ef, seed, undirected=True, weighted=False):
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
+    return _G(rmat(scale, ef, seed, undirected=undirected, weighted=weighted), not undirected)
+
+
+SYNTH = [
+    # (scale, edgefactor, seed, undirected)
+    (10, 8, 1, True),
+    (12, 16, 2, True),
+    (11, 8, 3, False),
+    (14, 16, 4, True),
+]
+
+
+def _src(g):
+    deg = np.diff(g.csr.rowptr.astype(np.int64))
+    return int(np.argmax(deg))
+
+
+@pytest.mark.parametrize("spec", SYNTH)
+def test_bfs_synthetic(ctx, spec):
+    g = _rmat(*spec)
+    s = _src(g)
+    np.testing.assert_array_equal(gpu_run(ctx, g, "BFS", source=s), O.bfs(g.csr, s))
+
+
+@pytest.mark.parametrize("spec", SYNTH)
+def test_pagerank_synthetic(ctx, spec):
+    g = _rmat(*spec)
+    want = O.pagerank(g.csr, g.directed, 0.85, 10)
+    got = gpu_run(ctx, g, "PR", damping=0.85, iters=10)
+    np.testing.assert_allclose(got, want, rtol=PR_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("spec", SYNTH)
+def test_wcc_synthetic(ctx, spec):
+    g = _rmat(*spec)
+    np.testing.assert_array_equal(gpu_run(ctx, g, "WCC"), O.wcc(g.csr))
+
+
+@pytest.mark.parametrize("spec", SYNTH)
+def test_cdlp_synthetic(ctx, spec):
+    g = _rmat(*spec)
+    np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=10), O.cdlp(g.csr, g.directed, 10))
+
+
+@pytest.mark.parametrize("spec", SYNTH)
+def test_lcc_synthetic(ctx, spec):
+    g = _rmat(*spec)
+    np.testing.assert_array_equal(gpu_run(ctx, g, "LCC"), O.lcc(g.csr, g.directed))
+
+
+@pytest.mark.parametrize("spec", SYNTH)
+def test_sssp_synthetic(ctx, spec):
+    scale, ef, seed, und = spec
+    g = _rmat(scale, ef, seed, undirected=und, weighted=True)
+    s = _src(g)
+    np.testing.assert_array_equal(gpu_run(ctx, g, "SSSP", source=s), O.sssp(g.csr, s))
+
+
+def test_long_rows_pagerank(ctx):
+    """A star plus a clique: rows far longer than the stream block (split segments)."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    n = 40000
+    hub = np.zeros(n - 1, dtype=np.int64)
+    leaves = np.arange(1, n, dtype=np.int64)
+    src = np.concatenate([hub, leaves[:100]])
+    dst = np.concatenate([leaves, leaves[100:200]])
+    csr = csr_from_edges(n, src, dst, None, symmetric=True)
+    g = _G(csr, False)
+    want = O.pagerank(csr, False, 0.85, 5)
+    got = gpu_run(ctx, g, "PR", damping=0.85, iters=5)
+    np.testing.assert_allclose(got, want, rtol=PR_RTOL, atol=0)
+    gd = _G(csr_from_edges(n, src, dst, None, symmetric=False), True)
+    want = O.pagerank(gd.csr, True, 0.85, 5)
+    got = gpu_run(ctx, gd, "PR", damping=0.85, iters=5)
+    np.testing.assert_allclose(got, want, rtol=PR_RTOL, atol=0)
+
+
+def test_empty_and_isolated(ctx):
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    csr = csr_from_edges(5, np.array([0]), np.array([1]), np.array([0.5]), symmetric=False)
+    g = _G(csr, True)
+    np.testing.assert_array_equal(gpu_run(ctx, g, "BFS", source=0), O.bfs(csr, 0))
+    np.testing.assert_array_equal(gpu_run(ctx, g, "WCC"), O.wcc(csr))
+    np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=3), O.cdlp(csr, True, 3))
+    np.testing.assert_array_equal(gpu_run(ctx, g, "LCC"), O.lcc(csr, True))
+    np.testing.assert_array_equal(gpu_run(ctx, g, "SSSP", source=0), O.sssp(csr, 0))
+    np.testing.assert_allclose(gpu_run(ctx, g, "PR", damping=0.85, iters=3),
+                               O.pagerank(csr, True, 0.85, 3), rtol=PR_RTOL)
+    e = csr_from_edges(4, np.zeros(0, np.int64), np.zeros(0, np.int64), None, symmetric=True)
+    ge = _G(e, False)
+    np.testing.assert_allclose(gpu_run(ctx, ge, "PR", damping=0.85, iters=4),
+                               O.pagerank(e, False, 0.85, 4), rtol=PR_RTOL)
+    np.testing.assert_array_equal(gpu_run(ctx, ge, "CDLP", iters=2), O.cdlp(e, False, 2))
+    np.testing.assert_array_equal(gpu_run(ctx, ge, "WCC"), O.wcc(e))
