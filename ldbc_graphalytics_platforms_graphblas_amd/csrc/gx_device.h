@@ -186,6 +186,14 @@ __device__ __forceinline__ int64_t row_of_edge(const int64_t *rp, int64_t nrows,
     return lo;
 }
 
+typedef int gx_v4i __attribute__((ext_vector_type(4)));
+
+// 16-byte non-temporal load (read-once streams: keep L2 for the gathered vectors).
+__device__ __forceinline__ int4 load_nt(const int4 *p) {
+    const gx_v4i v = __builtin_nontemporal_load(reinterpret_cast<const gx_v4i *>(p));
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

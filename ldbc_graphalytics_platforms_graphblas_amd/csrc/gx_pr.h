@@ -48,13 +48,16 @@ struct PrPart {
     DBuf<uint32_t> long_ticket;
     uint32_t nlong = 0, nsegs = 0;
     // dangling rows (out-degree 0) of this rank
-    DBuf<int32_t> dlist;
+    DBuf<int32_t> dlist;      // only when the dangling rows are not one contiguous range
     uint64_t nd = 0;
+    bool d_range = false;
+    int64_t d0 = 0;
     uint32_t dgrid = 0;
     DBuf<double> dpart;
     DBuf<uint32_t> dticket;
-    // single-GPU driver buffers (gx_pagerank)
-    DBuf<double> xa, xb, rank_out;
+    // single-GPU driver buffers (gx_pagerank): vertices relabelled hub-first
+    DBuf<double> xa, xb, rank_out, result;
+    DBuf<int32_t> perm;        // old vertex id -> position in the hub-first order
 };
 
 // Build the row-block plan and dangling list from a local pull CSR (host row pointers

@@ -79,23 +79,22 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
         const int nq = (int)((z1 - base + 3) >> 2);
         const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
         constexpr int NQ = (kStreamNnz / 4 + kPullBlock) / kPullBlock;
+        // Column indices: 16 B per lane, non-temporal (read once; keep L2 for x).  Every
+        // index read here is a valid x offset (neighbouring rows' entries, or the zeroed
+        // slack past the end), so all gathers below are issued unconditionally.
         int4 c[NQ];
 #pragma unroll
         for (int j = 0; j < NQ; j++) {
             const int q = tid + j * kPullBlock;
-            if (q < nq) c[j] = ci4[q];
-            else c[j] = make_int4(0, 0, 0, 0);
+            c[j] = q < nq ? load_nt(ci4 + q) : make_int4(0, 0, 0, 0);
         }
         double v[NQ][4];
 #pragma unroll
         for (int j = 0; j < NQ; j++) {
-            const int64_t e = base + 4 * (int64_t)(tid + j * kPullBlock);
-            const int cc[4] = {c[j].x, c[j].y, c[j].z, c[j].w};
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool ok = (e + k >= z0) && (e + k < z1);
-                v[j][k] = ok ? a.x_in[cc[k]] : 0.0;
-            }
+            v[j][0] = a.x_in[c[j].x];
+            v[j][1] = a.x_in[c[j].y];
+            v[j][2] = a.x_in[c[j].z];
+            v[j][3] = a.x_in[c[j].w];
         }
 #pragma unroll
         for (int j = 0; j < NQ; j++) {
@@ -126,16 +125,21 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
     double s0 = 0.0, s1 = 0.0;
     for (int64_t q = tid; q < nq; q += 2 * kPullBlock) {
         const int64_t q1 = q + kPullBlock;
-        const int4 c0 = ci4[q];
-        const int4 c1 = q1 < nq ? ci4[q1] : make_int4(0, 0, 0, 0);
+        const int4 c0 = load_nt(ci4 + q);
+        const int4 c1 = q1 < nq ? load_nt(ci4 + q1) : make_int4(0, 0, 0, 0);
         const int64_t e0 = base + 4 * q, e1 = base + 4 * q1;
         const int a0[4] = {c0.x, c0.y, c0.z, c0.w};
         const int a1[4] = {c1.x, c1.y, c1.z, c1.w};
         double g0[4], g1[4];
 #pragma unroll
+        for (int k = 0; k < 4; k++) {   // unconditional gathers, masked adds
+            g0[k] = a.x_in[a0[k]];
+            g1[k] = a.x_in[a1[k]];
+        }
+#pragma unroll
         for (int k = 0; k < 4; k++) {
-            g0[k] = (e0 + k >= zb && e0 + k < ze) ? a.x_in[a0[k]] : 0.0;
-            g1[k] = (e1 + k >= zb && e1 + k < ze) ? a.x_in[a1[k]] : 0.0;
+            if (!(e0 + k >= zb && e0 + k < ze)) g0[k] = 0.0;
+            if (!(e1 + k >= zb && e1 + k < ze)) g1[k] = 0.0;
         }
         s0 += (g0[0] + g0[1]) + (g0[2] + g0[3]);
         s1 += (g1[0] + g1[1]) + (g1[2] + g1[3]);
@@ -170,15 +174,21 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
 }
 
 // Sum of the scores of this rank's dangling vertices into the chunk's last slot.
-// Workgroup partials are combined in workgroup order by the last arriver.
-__global__ __launch_bounds__(256) void k_pr_dangling(const int32_t *__restrict__ dlist, int64_t nd,
-                                                     int64_t per, double *x, int64_t slot,
+// dlist == nullptr: the dangling rows are the contiguous range [d0, d0 + nd) (hub-first
+// order puts every out-degree-0 vertex last), read coalesced.  Workgroup partials are
+// combined in workgroup order by the last arriver (deterministic).
+__global__ __launch_bounds__(256) void k_pr_dangling(const int32_t *__restrict__ dlist, int64_t d0,
+                                                     int64_t nd, int64_t per, double *x, int64_t slot,
                                                      double *part, uint32_t *ticket) {
     __shared__ double wred[256 / kWave];
     const int tid = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(b0 + per, nd);
     double s = 0.0;
-    for (int64_t i = b0 + tid; i < b1; i += 256) s += x[dlist[i]];
+    if (dlist) {
+        for (int64_t i = b0 + tid; i < b1; i += 256) s += x[dlist[i]];
+    } else {
+        for (int64_t i = b0 + tid; i < b1; i += 256) s += x[d0 + i];
+    }
     s = wave_sum(s);
     if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = s;
     __syncthreads();
@@ -284,10 +294,14 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     for (int64_t i = 0; i < rows; i++)
         if (h_outdeg[i] == 0) dl.push_back((int32_t)i);
     p->nd = dl.size();
-    GX_TRY(p->dlist.alloc(std::max<size_t>(dl.size(), 1)));
-    if (!dl.empty())
-        GX_HIP_TRY(hipMemcpy(p->dlist.p, dl.data(), dl.size() * 4, hipMemcpyHostToDevice));
-    p->dgrid = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(1, (p->nd + 4095) / 4096));
+    p->d_range = !dl.empty() && (int64_t)dl.back() - dl.front() + 1 == (int64_t)dl.size();
+    p->d0 = dl.empty() ? 0 : dl.front();
+    if (!p->d_range) {
+        GX_TRY(p->dlist.alloc(std::max<size_t>(dl.size(), 1)));
+        if (!dl.empty())
+            GX_HIP_TRY(hipMemcpy(p->dlist.p, dl.data(), dl.size() * 4, hipMemcpyHostToDevice));
+    }
+    p->dgrid = (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(1, (p->nd + 2047) / 2048));
     GX_TRY(p->dpart.alloc(p->dgrid));
     GX_TRY(p->dticket.alloc(1));
     GX_HIP_TRY(hipMemset(p->dticket.p, 0, 4));
@@ -297,7 +311,8 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
 static int pr_dangling(PrPart *p, double *x_local, hipStream_t s) {
     if (p->nd == 0) return GX_SUCCESS;
     const int64_t per = (int64_t)((p->nd + p->dgrid - 1) / p->dgrid);
-    hipLaunchKernelGGL(k_pr_dangling, dim3(p->dgrid), dim3(256), 0, s, p->dlist.p, (int64_t)p->nd, per,
+    hipLaunchKernelGGL(k_pr_dangling, dim3(p->dgrid), dim3(256), 0, s, p->d_range ? nullptr : p->dlist.p,
+                       (int64_t)p->d0, (int64_t)p->nd, per,
                        x_local, (int64_t)p->chunk - 1, p->dpart.p, p->dticket.p);
     return check_launch("k_pr_dangling");
 }
@@ -345,6 +360,107 @@ using namespace gx;
 
 static uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
+namespace {
+
+// Relabel a CSR by `perm` (old vertex -> new position): row perm[r] of the result holds the
+// entries of row r with every column c renamed perm[c].  Edge-balanced, no sort.
+__global__ void k_permute_csr(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci, int64_t n,
+                              int64_t nnz, const int32_t *__restrict__ perm, const int64_t *__restrict__ nrp,
+                              int32_t *__restrict__ nci) {
+    constexpr int kPer = 16;
+    const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPer;
+    if (e0 >= nnz) return;
+    const int64_t e1 = min(e0 + kPer, nnz);
+    int64_t r = row_of_edge(rp, n, e0);
+    for (int64_t e = e0; e < e1; e++) {
+        while (rp[r + 1] <= e) r++;
+        nci[nrp[perm[r]] + (e - rp[r])] = perm[ci[e]];
+    }
+}
+
+// out[v] = in[perm[v]]: back from the hub-first order to the caller's vertex order.
+__global__ void k_gather_perm(const double *__restrict__ in, const int32_t *__restrict__ perm, int64_t n,
+                              double *__restrict__ out) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+         v += (int64_t)gridDim.x * blockDim.x)
+        out[v] = in[perm[v]];
+}
+
+// Hub-first order: vertices by out-degree descending, ties by id (stable counting sort).
+// The pull SpMV gathers x(u) once per out-edge of u, so this packs the most gathered
+// entries of x into its first few MiB, which stay resident in each XCD's 4 MiB L2.
+void hub_order(const std::vector<int32_t> &outdeg, std::vector<int32_t> &order, std::vector<int32_t> &perm) {
+    const size_t n = outdeg.size();
+    int32_t maxd = 0;
+    for (int32_t d : outdeg) maxd = std::max(maxd, d);
+    std::vector<int64_t> start((size_t)maxd + 2, 0);
+    for (int32_t d : outdeg) start[(size_t)(maxd - d) + 1]++;
+    for (size_t k = 1; k < start.size(); k++) start[k] += start[k - 1];
+    order.assign(n, 0);
+    perm.assign(n, 0);
+    for (size_t v = 0; v < n; v++) {
+        const int64_t pos = start[(size_t)(maxd - outdeg[v])]++;
+        order[pos] = (int32_t)v;
+        perm[v] = (int32_t)pos;
+    }
+}
+
+int pr_single_plan(gx_graph *g, PrPart **out) {
+    const uint64_t n = g->n;
+    gx_ctx *ctx = g->ctx;
+    hipStream_t s = ctx->stream;
+    DevCSR &P = g->directed ? g->AT : g->A;
+    std::vector<int32_t> h_outdeg(n), order, perm;
+    for (uint64_t v = 0; v < n; v++) h_outdeg[v] = (int32_t)(g->A.h_rp[v + 1] - g->A.h_rp[v]);
+    hub_order(h_outdeg, order, perm);
+    std::vector<int64_t> nrp(n + 1, 0);
+    std::vector<int32_t> nout(n);
+    for (uint64_t i = 0; i < n; i++) {
+        const int32_t v = order[i];
+        nrp[i + 1] = nrp[i] + (P.h_rp[v + 1] - P.h_rp[v]);
+        nout[i] = h_outdeg[v];
+    }
+    auto *p = new PrPart();
+    p->ctx = ctx;
+    p->n_global = n;
+    p->nranks = 1;
+    p->rank = 0;
+    p->chunk = round_up(n + 1, 32);
+    int rc = p->perm.alloc(n);
+    if (rc == GX_SUCCESS) rc = p->rp_own.alloc(n + 1);
+    if (rc == GX_SUCCESS) rc = p->ci_own.alloc(P.nnz, 16);
+    if (rc == GX_SUCCESS) rc = p->outdeg_own.alloc(n);
+    if (rc == GX_SUCCESS) rc = p->xa.alloc(p->chunk);
+    if (rc == GX_SUCCESS) rc = p->xb.alloc(p->chunk);
+    if (rc == GX_SUCCESS) rc = p->rank_out.alloc(n);
+    if (rc == GX_SUCCESS) rc = p->result.alloc(n);
+    hipError_t e = hipSuccess;
+    if (rc == GX_SUCCESS) e = hipMemcpyAsync(p->perm.p, perm.data(), n * 4, hipMemcpyHostToDevice, s);
+    if (rc == GX_SUCCESS && e == hipSuccess)
+        e = hipMemcpyAsync(p->rp_own.p, nrp.data(), (n + 1) * 8, hipMemcpyHostToDevice, s);
+    if (rc == GX_SUCCESS && e == hipSuccess)
+        e = hipMemcpyAsync(p->outdeg_own.p, nout.data(), n * 4, hipMemcpyHostToDevice, s);
+    if (rc == GX_SUCCESS && e != hipSuccess) rc = fail(GX_DEVICE_ERROR, hipGetErrorString(e));
+    if (rc == GX_SUCCESS && P.nnz) {
+        hipLaunchKernelGGL(k_permute_csr, dim3(grid_for((P.nnz + 15) / 16, 256, 1u << 30)), dim3(256), 0, s,
+                           P.rp.p, P.ci.p, (int64_t)n, (int64_t)P.nnz, p->perm.p, p->rp_own.p, p->ci_own.p);
+        rc = check_launch("k_permute_csr");
+    }
+    if (rc == GX_SUCCESS) rc = pr_plan(p, nrp, p->rp_own.p, p->ci_own.p, p->outdeg_own.p, nout);
+    if (rc == GX_SUCCESS) {
+        e = hipStreamSynchronize(s);   // host vectors above die at return
+        if (e != hipSuccess) rc = fail(GX_DEVICE_ERROR, hipGetErrorString(e));
+    }
+    if (rc != GX_SUCCESS) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return GX_SUCCESS;
+}
+
+}  // namespace
+
 extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank) {
     if (!g || !rank) return fail(GX_NULL_POINTER, "gx_pagerank: null argument");
     if (iters < 0) return fail(GX_INVALID_VALUE, "gx_pagerank: negative iteration count");
@@ -354,28 +470,8 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     GX_TRY(device_begin(ctx));
-    GX_TRY(ensure_outdeg(g));
     if (g->directed) GX_TRY(ensure_transpose(g));
-    if (!g->pr) {
-        DevCSR &P = g->directed ? g->AT : g->A;
-        auto *p = new PrPart();
-        p->ctx = ctx;
-        p->n_global = n;
-        p->nranks = 1;
-        p->rank = 0;
-        p->chunk = round_up(n + 1, 32);
-        std::vector<int32_t> h_outdeg(n);
-        for (uint64_t v = 0; v < n; v++) h_outdeg[v] = (int32_t)(g->A.h_rp[v + 1] - g->A.h_rp[v]);
-        int rc = pr_plan(p, P.h_rp, P.rp.p, P.ci.p, g->outdeg.p, h_outdeg);
-        if (rc == GX_SUCCESS) rc = p->xa.alloc(p->chunk);
-        if (rc == GX_SUCCESS) rc = p->xb.alloc(p->chunk);
-        if (rc == GX_SUCCESS) rc = p->rank_out.alloc(n);
-        if (rc != GX_SUCCESS) {
-            delete p;
-            return rc;
-        }
-        g->pr = p;
-    }
+    if (!g->pr) GX_TRY(pr_single_plan(g, &g->pr));
     PrPart *p = g->pr;
     p->damping = damping;
     double *cur = p->xa.p, *nxt = p->xb.p;
@@ -384,12 +480,17 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
         GX_TRY(pr_step(p, cur, nxt, it == iters - 1 ? p->rank_out.p : nullptr, s));
         std::swap(cur, nxt);
     }
+    if (iters > 0) {
+        hipLaunchKernelGGL(k_gather_perm, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, p->rank_out.p,
+                           p->perm.p, (int64_t)n, p->result.p);
+        GX_TRY(check_launch("k_gather_perm"));
+    }
     GX_TRY(device_end(ctx));
     if (iters == 0) {
         for (uint64_t v = 0; v < n; v++) rank[v] = 1.0 / (double)n;
         return GX_SUCCESS;
     }
-    GX_HIP_TRY(hipMemcpyAsync(rank, p->rank_out.p, n * 8, hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipMemcpyAsync(rank, p->result.p, n * 8, hipMemcpyDeviceToHost, s));
     GX_HIP_TRY(hipStreamSynchronize(s));
     return GX_SUCCESS;
 }

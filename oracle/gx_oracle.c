@@ -132,6 +132,17 @@ int orc_bfs(int64_t n, const int64_t *rp, const int64_t *ci, int64_t src, int64_
  * OpenMP over rows; the per-row sum order (ascending column) does not depend on the
  * thread count, so the result is bitwise independent of nthreads.
  * ---------------------------------------------------------------------------------- */
+static double dangling_sum(const int64_t *rp, const double *x, int64_t lo, int64_t hi) {
+    if (hi - lo <= 1024) {
+        double s = 0.0;
+        for (int64_t i = lo; i < hi; i++)
+            if (rp[i + 1] == rp[i]) s += x[i];
+        return s;
+    }
+    const int64_t mid = lo + (hi - lo) / 2;
+    return dangling_sum(rp, x, lo, mid) + dangling_sum(rp, x, mid, hi);
+}
+
 int orc_pagerank(int64_t n, const int64_t *rp, const int64_t *ci, int directed,
                  double damping, int iters, double *rank, int nthreads) {
     if (n <= 0) return ORC_OK;
@@ -162,10 +173,9 @@ int orc_pagerank(int64_t n, const int64_t *rp, const int64_t *ci, int directed,
     const double damping_over_n = damping / dn;
     for (int it = 0; it < iters; it++) {
         double *tmp = prev; prev = cur; cur = tmp;   /* prev = previous scores */
-        double dangling = 0.0;
-        /* sequential, ascending vertex order: deterministic sum of sink scores */
-        for (int64_t i = 0; i < n; i++)
-            if (rp[i + 1] == rp[i]) dangling += prev[i];
+        /* sum of sink scores: blocked pairwise reduction (GrB_reduce of SuiteSparse is a
+         * blocked parallel reduction, not a left-to-right sum); deterministic */
+        const double dangling = dangling_sum(rp, prev, 0, n);
         const double teleport = teleport0 + damping_over_n * dangling;
         #pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < n; i++) w[i] = (rp[i + 1] > rp[i]) ? prev[i] / dsc[i] : 0.0;
