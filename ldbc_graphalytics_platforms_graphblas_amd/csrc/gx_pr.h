@@ -42,6 +42,9 @@ struct PrPart {
     // row blocks
     DBuf<RowBlock> blocks;
     uint32_t nblocks = 0;
+    uint32_t nlong_blocks = 0;   // LONG blocks come first in `blocks`
+    int stream_nnz = kStreamNnz; // LDS stage of a STREAM block: 1024, 2048 or 4096 entries
+    int only = 0;                // tuning/debug: 1 = launch LONG blocks only, 2 = STREAM only
     DBuf<int32_t> long_first;  // per long row: index of its first partial
     DBuf<int32_t> long_nseg;   // per long row: number of segments
     DBuf<double> long_part;    // per segment partial sum

@@ -23,6 +23,8 @@
 // by the last-arriving segment through an agent-scope release/acquire ticket), and are
 // dispatched first so they overlap the stream blocks.
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <numeric>
 
 #include "gx_pr.h"
@@ -37,6 +39,7 @@ struct PullArgs {
     const int32_t *outdeg;
     const double *x_in;
     double *x_out;
+    int64_t block_offset;
     double *rank_out;
     int64_t chunk;
     int nranks;
@@ -56,12 +59,13 @@ __device__ __forceinline__ void pr_epilogue(const PullArgs &a, int32_t row, doub
     a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
 }
 
+template <int NB>
 __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
-    __shared__ double vals[kStreamNnz];
+    __shared__ __attribute__((aligned(16))) double vals[NB + 4];
     __shared__ int32_t rofs[kStreamRows + 1];
     __shared__ double wred[kPullBlock / kWave];
 
-    const RowBlock b = a.blocks[blockIdx.x];
+    const RowBlock b = a.blocks[a.block_offset + blockIdx.x];
     const int tid = threadIdx.x;
 
     double dsum = 0.0;
@@ -74,11 +78,19 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
         const int64_t z0 = b.nz_begin, z1 = b.nz_end;
         const int32_t r0 = b.row_begin;
         const int nrows = b.row_end - b.row_begin;
-        for (int i = tid; i <= nrows; i += kPullBlock) rofs[i] = (int32_t)(a.rp[r0 + i] - z0);
+        // LDS is indexed from the 16-B aligned `base`, so every lane stores its four values
+        // as two aligned 16-B words; the reduction only reads [rofs[r], rofs[r+1]).
         const int64_t base = z0 & ~(int64_t)3;
+        for (int i = tid; i <= nrows; i += kPullBlock) rofs[i] = (int32_t)(a.rp[r0 + i] - base);
         const int nq = (int)((z1 - base + 3) >> 2);
         const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
-        constexpr int NQ = (kStreamNnz / 4 + kPullBlock) / kPullBlock;
+        // lane group per row, fixed for the block; the epilogue's out-degree is fetched early
+        int L = kWave;
+        while (L > 1 && L * nrows > kPullBlock) L >>= 1;
+        const int row = tid / L, lane = tid & (L - 1);
+        const bool writer = row < nrows && lane == 0;
+        const int32_t deg = writer ? a.outdeg[r0 + row] : 0;
+        constexpr int NQ = (NB / 4 + kPullBlock) / kPullBlock;
         // Column indices: 16 B per lane, non-temporal (read once; keep L2 for x).  Every
         // index read here is a valid x offset (neighbouring rows' entries, or the zeroed
         // slack past the end), so all gathers below are issued unconditionally.
@@ -98,22 +110,25 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < NQ; j++) {
-            const int64_t e = base + 4 * (int64_t)(tid + j * kPullBlock);
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if ((e + k >= z0) && (e + k < z1)) vals[e + k - z0] = v[j][k];
+            const int q = tid + j * kPullBlock;
+            if (q < nq) {
+                double2 *d = reinterpret_cast<double2 *>(&vals[4 * q]);
+                d[0] = make_double2(v[j][0], v[j][1]);
+                d[1] = make_double2(v[j][2], v[j][3]);
+            }
         }
         __syncthreads();
-        int L = kWave;
-        while (L > 1 && L * nrows > kPullBlock) L >>= 1;
-        const int row = tid / L, lane = tid & (L - 1);
         double s = 0.0;
         if (row < nrows) {
             const int kb = rofs[row], ke = rofs[row + 1];
             for (int k = kb + lane; k < ke; k += L) s += vals[k];
         }
         for (int off = L >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
-        if (row < nrows && lane == 0) pr_epilogue(a, r0 + row, s, teleport);
+        if (writer) {
+            const double r = teleport + s;
+            if (a.rank_out) a.rank_out[r0 + row] = r;
+            a.x_out[r0 + row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+        }
         return;
     }
 
@@ -228,6 +243,13 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
             const int32_t *d_outdeg, const std::vector<int32_t> &h_outdeg) {
     const int64_t rows = (int64_t)h_rp.size() - 1;
     p->rows = (uint64_t)rows;
+    // tuning knobs (plan time): GX_PR_STREAM_NNZ = 1024 | 2048 | 4096, GX_PR_ONLY = long | stream
+    if (const char *e = std::getenv("GX_PR_STREAM_NNZ")) {
+        const int v = std::atoi(e);
+        if (v == 1024 || v == 2048 || v == 4096) p->stream_nnz = v;
+    }
+    if (const char *e = std::getenv("GX_PR_ONLY")) p->only = std::strcmp(e, "long") == 0 ? 1 : std::strcmp(e, "stream") == 0 ? 2 : 0;
+    const int64_t NB = p->stream_nnz;
     p->rp = d_rp;
     p->ci = d_ci;
     p->outdeg = d_outdeg;
@@ -238,7 +260,7 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     int64_t r = 0;
     while (r < rows) {
         const int64_t len = h_rp[r + 1] - h_rp[r];
-        if (len > kStreamNnz) {
+        if (len > NB) {
             longrows.push_back({len, (int32_t)r});
             r++;
             continue;
@@ -247,7 +269,7 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
         int64_t nz = 0;
         while (r < rows && r - start < kStreamRows) {
             const int64_t l = h_rp[r + 1] - h_rp[r];
-            if (l > kStreamNnz || nz + l > kStreamNnz) break;
+            if (l > NB || nz + l > NB) break;
             nz += l;
             r++;
         }
@@ -275,6 +297,7 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     all.insert(all.end(), longb.begin(), longb.end());
     all.insert(all.end(), streamb.begin(), streamb.end());
     p->nblocks = (uint32_t)all.size();
+    p->nlong_blocks = (uint32_t)longb.size();
     p->nlong = (uint32_t)lfirst.size();
     p->nsegs = (uint32_t)nsegs;
     GX_TRY(p->blocks.alloc(std::max<size_t>(all.size(), 1)));
@@ -346,9 +369,21 @@ int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, 
     a.long_nseg = p->long_nseg.p;
     a.long_part = p->long_part.p;
     a.long_ticket = p->long_ticket.p;
-    if (p->nblocks) {
+    uint32_t nb = p->nblocks;
+    a.block_offset = 0;
+    if (p->only == 1) nb = p->nlong_blocks;
+    if (p->only == 2) {
+        a.block_offset = p->nlong_blocks;
+        nb = p->nblocks - p->nlong_blocks;
+    }
+    if (nb) {
         KTimer kt(p->ctx, "pr_pull", s);
-        hipLaunchKernelGGL(k_pr_pull, dim3(p->nblocks), dim3(kPullBlock), 0, s, a);
+        if (p->stream_nnz == 1024)
+            hipLaunchKernelGGL(k_pr_pull<1024>, dim3(nb), dim3(kPullBlock), 0, s, a);
+        else if (p->stream_nnz == 4096)
+            hipLaunchKernelGGL(k_pr_pull<4096>, dim3(nb), dim3(kPullBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_pr_pull<2048>, dim3(nb), dim3(kPullBlock), 0, s, a);
     }
     GX_TRY(check_launch("k_pr_pull"));
     return pr_dangling(p, x_local, s);
