@@ -20,6 +20,27 @@ struct RowBlock {
     int32_t seg;        // segment number within the long row
 };
 
+// One wave's share of the hub-cached pull SpMV (k_pr_pull_hub):
+//   split <  0 : rows [row_begin, row_end) of similar length (hub-first order), `lanes`
+//                lanes per row, 64 / lanes rows in flight per pass.
+//   split >= 0 : entries [nz_begin, nz_end) of the long row row_begin (all 64 lanes);
+//                partial sums of a row's segments are combined by the last arriver.
+struct WaveItem {
+    int64_t nz_begin;
+    int64_t nz_end;
+    int32_t row_begin;
+    int32_t row_end;
+    int32_t split;
+    int32_t seg;
+    int32_t lanes;
+    int32_t pad;
+};
+
+constexpr int kHubBlock = 1024;       // one 16-wave workgroup per CU
+constexpr int kItemNnz = 2048;        // entries per wave item
+constexpr int kItemRows = 512;        // rows per wave item
+constexpr int kHubSegNnz = 4096;      // entries per long-row segment item
+
 constexpr int kPullBlock = 256;      // 4 waves
 constexpr int kStreamNnz = 2048;     // LDS stage: 16 KiB of fp64 per workgroup
 constexpr int kStreamRows = 256;     // at most one row per lane in stream mode
@@ -58,6 +79,17 @@ struct PrPart {
     uint32_t dgrid = 0;
     DBuf<double> dpart;
     DBuf<uint32_t> dticket;
+    // hub-cached kernel (default): wave items, LDS hub prefix, fused dangling reduction
+    int kernel = 0;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive)
+    DBuf<WaveItem> items;
+    uint32_t nitems = 0;
+    DBuf<int32_t> hlong_first, hlong_nseg;
+    DBuf<double> hlong_part;
+    DBuf<uint32_t> hlong_ticket;
+    uint32_t hub_grid = 0;       // workgroups (one per CU)
+    int64_t hub_entries = 0;     // x prefix cached in LDS
+    DBuf<double> gpart;          // per-workgroup dangling partial
+    DBuf<uint32_t> gticket;
     // single-GPU driver buffers (gx_pagerank): vertices relabelled hub-first
     DBuf<double> xa, xb, rank_out, result;
     DBuf<int32_t> perm;        // old vertex id -> position in the hub-first order
@@ -67,6 +99,11 @@ struct PrPart {
 // h_rp, device rp/ci) and device out-degrees.  Borrowed device pointers must outlive it.
 int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp,
             const int32_t *d_ci, const int32_t *d_outdeg, const std::vector<int32_t> &h_outdeg);
+
+// Wave-item plan of the hub-cached kernel (called by pr_plan).
+int pr_plan_hub(PrPart *p, const std::vector<int64_t> &h_rp);
+// One iteration with k_pr_pull_hub (pull + fused dangling sum).
+int pr_step_hub(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 
 int pr_init(PrPart *p, double *x_local, hipStream_t s);
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);

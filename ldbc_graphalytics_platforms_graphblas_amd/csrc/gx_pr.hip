@@ -328,6 +328,9 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     GX_TRY(p->dpart.alloc(p->dgrid));
     GX_TRY(p->dticket.alloc(1));
     GX_HIP_TRY(hipMemset(p->dticket.p, 0, 4));
+    // kernel choice: GX_PR_KERNEL = hub (default) | adaptive
+    if (const char *e = std::getenv("GX_PR_KERNEL")) p->kernel = std::strcmp(e, "adaptive") == 0 ? 1 : 0;
+    if (p->kernel == 0) GX_TRY(pr_plan_hub(p, h_rp));
     return GX_SUCCESS;
 }
 
@@ -350,6 +353,7 @@ int pr_init(PrPart *p, double *x_local, hipStream_t s) {
 }
 
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s) {
+    if (p->kernel == 0) return pr_step_hub(p, x_full, x_local, rank_out, s);
     const double dn = (double)p->n_global;
     PullArgs a;
     a.blocks = p->blocks.p;

@@ -20,11 +20,11 @@ except Exception as e:
 EOF
     return $rc
 }
-for nb in 1024 2048 4096; do
-    run nb$nb GX_PR_STREAM_NNZ=$nb || exit 1
+run hub_default X=1 || exit 1
+for h in 0 4096 12288; do
+    run hub_$h GX_PR_HUB_ENTRIES=$h || exit 1
 done
-run only_long GX_PR_ONLY=long || exit 1
-run only_stream GX_PR_ONLY=stream || exit 1
+run adaptive GX_PR_KERNEL=adaptive || exit 1
 rocprofv3 -L > "$OUT/counters.txt" 2>&1
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS" \
            "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum" \
