@@ -1,20 +1,23 @@
 // gx_pr_hub.hip -- hub-cached pull SpMV for PageRank (default k_pr_pull variant).
 //
-// Profile of the CSR-Adaptive kernel (profiles/README.md, round 1): with the hub-first
-// vertex order the gathers hit L2 94% of the time, but every 8-byte gather is still one
-// L1 access and one L2 request, and 64% of wave cycles are issue stalls on the vector
-// memory pipe -- the kernel is bound by gather REQUESTS, not HBM bytes.  This kernel takes
-// requests off that pipe:
-//   * one 1024-thread workgroup per CU copies the hottest prefix of x (hub-first order, up
-//     to 158 KiB = the most gathered ~20K vertices) into LDS once per launch; gathers of
-//     those columns are ds_read_b64, the rest go to L2 / MALL;
-//   * waves work independently on equal-size items (statically interleaved over the
-//     grid), L lanes per row where all rows of an item have nearly the same length;
-//     column indices stream with non-temporal loads;
-//   * the dangling-score sum of the rank is reduced in the same launch (per-lane sums ->
-//     per-workgroup sum -> last-arriving workgroup adds the 256 partials in order), so an
-//     iteration is one launch.
-// Results are deterministic: the static item assignment fixes every summation order.
+// Profile of the CSR-Adaptive kernel (profiles/README.md): with the hub-first vertex
+// order the gathers hit L2 94% of the time, but every 8-byte gather is one L1 access and
+// one L2 request, and 64% of wave cycles are issue stalls on the vector memory pipe -- the
+// kernel is bound by gather REQUESTS, not HBM bytes.  This kernel takes requests off that
+// pipe and keeps many of them in flight:
+//   * one 1024-thread workgroup per CU copies the hottest prefix of x (hub-first order:
+//     the ~12K most gathered vertices, 95 KiB) into LDS once per launch; gathers of those
+//     columns are ds_read_b64, the rest go to L2 / MALL;
+//   * every wave owns a private 4 KiB LDS stage and works through equal-size items,
+//     statically interleaved over the grid: a STREAM item is <= 508 consecutive entries
+//     of <= 63 whole rows (two 16-B index loads + eight gathers per lane, staged, then
+//     reduced by lane groups of 64 / rows); a LONG item is <= 4096 entries of one row;
+//   * while the gathers of item i are in flight the wave already issues the index, row-
+//     pointer and out-degree loads of item i + 1 (software pipeline, one gather round trip
+//     exposed per item);
+//   * the rank's dangling-score sum is reduced in the same launch (lanes -> wave ->
+//     workgroup -> the last-arriving workgroup adds the per-workgroup partials in order).
+// Static item assignment fixes every summation order: results are deterministic.
 #include <algorithm>
 
 #include "gx_pr.h"
@@ -22,7 +25,12 @@
 namespace gx {
 namespace {
 
-constexpr int kHubMax = 20224;   // doubles of x cached in LDS (158 KiB)
+constexpr int kWaves = kHubBlock / kWave;   // 16
+constexpr int kStage = 512;                 // doubles per wave stage
+constexpr int kStreamMax = 508;             // entries per STREAM item (2 x 64 int4 incl. alignment)
+constexpr int kStreamRowsMax = 63;          // rows per STREAM item (row offsets in one lane each)
+constexpr int kLongSeg = 4096;              // entries per LONG item
+constexpr int kHubMax = 12224;              // doubles of x cached in LDS (95.5 KiB)
 
 struct HubArgs {
     const WaveItem *items;
@@ -35,7 +43,7 @@ struct HubArgs {
     double *rank_out;
     int64_t chunk;
     int nranks;
-    int64_t hub_entries;
+    int32_t hub_entries;
     double teleport0, damping_over_n, damping;
     const int32_t *long_first;
     const int32_t *long_nseg;
@@ -45,35 +53,43 @@ struct HubArgs {
     uint32_t *gticket;
 };
 
-// sum of x over entries [b, e) taken by this lane (stride L, 4 loads in flight).
-// Index loads are clamped to the row (always valid, no branches); the LDS read is issued
-// for every lane and the global read only for non-hub columns -- written so that the two
-// cannot be folded into one flat load (which would send the hub reads down the vector
-// memory pipe again).
-__device__ __forceinline__ double row_sum(const HubArgs &a, const double *hub, int64_t b, int64_t e,
-                                          int L, int gl) {
-    double s = 0.0;
-    const int32_t H = (int32_t)a.hub_entries;
-    for (int64_t k0 = b + gl; k0 < e; k0 += 4 * (int64_t)L) {
-        int32_t c[4];
+// x[c]: from the LDS hub when c < H, else from global memory.  Both reads are issued
+// unconditionally so the compiler can count outstanding loads exactly (no vmcnt(0) behind
+// branches): hub lanes point their global read at x[0] -- one shared cache line per wave
+// instruction -- and non-hub lanes read hub[0].
+__device__ __forceinline__ void gather4(const HubArgs &a, const double *hub, const int4 c, double v[4]) {
+    const int32_t H = a.hub_entries;
+    const int cc[4] = {c.x, c.y, c.z, c.w};
+    double hv[4], gv[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int64_t k = min(k0 + (int64_t)u * L, e - 1);
-            c[u] = __builtin_nontemporal_load(a.ci + k);
-        }
-        double hv[4], gv[4];
+    for (int k = 0; k < 4; k++) hv[k] = hub[cc[k] < H ? cc[k] : 0];
 #pragma unroll
-        for (int u = 0; u < 4; u++) hv[u] = hub[c[u] < H ? c[u] : 0];
+    for (int k = 0; k < 4; k++) gv[k] = a.x_in[cc[k] < H ? 0 : cc[k]];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            gv[u] = 0.0;
-            if (c[u] >= H) gv[u] = a.x_in[c[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (k0 + (int64_t)u * L < e) s += c[u] < H ? hv[u] : gv[u];
-    }
-    return s;
+    for (int k = 0; k < 4; k++) v[k] = cc[k] < H ? hv[k] : gv[k];
+}
+
+// Operands of one STREAM item, loaded ahead of its gathers.  All loads are unconditional
+// (addresses clamped into the item) and nothing is computed from them here, so issuing
+// them never waits on the gathers already in flight.
+struct StreamOps {
+    int4 c0, c1;      // column indices of entries base + 4*lane .. and base + 4*(lane+64) ..
+    int64_t rp;       // row pointer of row min(lane, nrows)
+    int32_t deg;      // out-degree of row min(lane, nrows - 1)
+};
+
+__device__ __forceinline__ StreamOps load_stream(const HubArgs &a, const WaveItem &w, int lane) {
+    StreamOps o;
+    const int64_t base = w.nz_begin & ~(int64_t)3;
+    const int nq = (int)((w.nz_end - base + 3) >> 2);
+    const int qmax = nq > 0 ? nq - 1 : 0;
+    const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
+    o.c0 = load_nt(ci4 + min(lane, qmax));
+    o.c1 = load_nt(ci4 + min(lane + kWave, qmax));
+    const int nrows = w.row_end - w.row_begin;
+    o.rp = a.rp[w.row_begin + min(lane, nrows)];
+    o.deg = a.outdeg[w.row_begin + min(lane, nrows - 1)];
+    return o;
 }
 
 __device__ __forceinline__ double finish_row(const HubArgs &a, int32_t row, double s, double teleport,
@@ -84,26 +100,56 @@ __device__ __forceinline__ double finish_row(const HubArgs &a, int32_t row, doub
     return deg == 0 ? r : 0.0;   // contribution to the dangling sum
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LONG item: entries [zb, ze) of one row; returns this lane's partial sum.
+__device__ __forceinline__ double long_sum(const HubArgs &a, const double *hub, int64_t zb, int64_t ze,
+                                           int lane) {
+    const int64_t base = zb & ~(int64_t)3;
+    const int nq = (int)((ze - base + 3) >> 2);
+    const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
+    double s = 0.0;
+    for (int q0 = 0; q0 < nq; q0 += 4 * kWave) {
+        int4 c[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) c[j] = load_nt(ci4 + min(q0 + lane + j * kWave, nq - 1));
+        double v[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) gather4(a, hub, c[j], v[j]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t e = base + 4 * (int64_t)(q0 + lane + j * kWave);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (e + k >= zb && e + k < ze) s += v[j][k];
+        }
+    }
+    return s;
+}
+
 __global__ __launch_bounds__(kHubBlock) void k_pr_pull_hub(HubArgs a) {
     __shared__ __attribute__((aligned(16))) double hub[kHubMax];
-    __shared__ double wsum[kHubBlock / kWave];
+    __shared__ __attribute__((aligned(16))) double stage[kWaves][kStage];
+    __shared__ double wsum[kWaves];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     {
-        // all loads first, then all LDS stores (one round trip, not one per 16 KiB)
+        // all loads first, then all LDS stores (one round trip for the whole fill)
         constexpr int kFill = (kHubMax / 2 + kHubBlock - 1) / kHubBlock;
         const double2 *src = reinterpret_cast<const double2 *>(a.x_in);
         double2 *dst = reinterpret_cast<double2 *>(hub);
-        const int npair = (int)(a.hub_entries / 2);
-        double2 t[kFill];
+        const int npair = a.hub_entries / 2;
+        if (npair > 0) {
+            // clamped loads AND stores: lanes past the end rewrite the last pair with its
+            // own value, so there is no branch between the loads and the LDS stores
+            double2 t[kFill];
 #pragma unroll
-        for (int j = 0; j < kFill; j++) {
-            const int i = tid + j * kHubBlock;
-            t[j] = i < npair ? src[i] : make_double2(0.0, 0.0);
-        }
+            for (int j = 0; j < kFill; j++) t[j] = src[min(tid + j * kHubBlock, npair - 1)];
 #pragma unroll
-        for (int j = 0; j < kFill; j++) {
-            const int i = tid + j * kHubBlock;
-            if (i < npair) dst[i] = t[j];
+            for (int j = 0; j < kFill; j++) dst[min(tid + j * kHubBlock, npair - 1)] = t[j];
         }
         if ((a.hub_entries & 1) && tid == 0) hub[a.hub_entries - 1] = a.x_in[a.hub_entries - 1];
     }
@@ -112,53 +158,91 @@ __global__ __launch_bounds__(kHubBlock) void k_pr_pull_hub(HubArgs a) {
     const double teleport = a.teleport0 + a.damping_over_n * dsum;
     __syncthreads();
 
+    double *st = stage[wv];
     double dang = 0.0;
-    const uint32_t nw = gridDim.x * (kHubBlock / kWave);
-    for (uint32_t i = (uint32_t)wv * gridDim.x + blockIdx.x; i < a.nitems; i += nw) {
-        const WaveItem w = a.items[i];
-        if (w.split >= 0) {
-            // one segment of a long row: all 64 lanes
-            double s = wave_sum(row_sum(a, hub, w.nz_begin, w.nz_end, kWave, lane));
+    const uint32_t nw = gridDim.x * kWaves;
+    uint32_t i = (uint32_t)wv * gridDim.x + blockIdx.x;
+    bool have = i < a.nitems;
+    WaveItem cur{};
+    StreamOps ops{};
+    if (have) {
+        cur = a.items[i];
+        if (cur.split < 0) ops = load_stream(a, cur, lane);
+    }
+    while (have) {
+        const uint32_t ni = i + nw;
+        const bool nhave = ni < a.nitems;
+        WaveItem nxt{};
+        if (nhave) nxt = a.items[ni];
+        if (cur.split >= 0) {
+            // ---- LONG item: one segment of one row
+            const double s = wave_sum(long_sum(a, hub, cur.nz_begin, cur.nz_end, lane));
             if (lane == 0) {
-                const int32_t nseg = a.long_nseg[w.split];
-                const int32_t row = w.row_begin;
+                const int32_t nseg = a.long_nseg[cur.split];
+                const int32_t row = cur.row_begin;
                 if (nseg == 1) {
                     dang += finish_row(a, row, s, teleport, a.outdeg[row]);
                 } else {
-                    const int32_t first = a.long_first[w.split];
-                    __hip_atomic_store(&a.long_part[first + w.seg], s, __ATOMIC_RELAXED,
+                    const int32_t first = a.long_first[cur.split];
+                    __hip_atomic_store(&a.long_part[first + cur.seg], s, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    const uint32_t t = __hip_atomic_fetch_add(&a.long_ticket[w.split], 1u, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t t = __hip_atomic_fetch_add(&a.long_ticket[cur.split], 1u,
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (t == (uint32_t)(nseg - 1)) {
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                         double all = 0.0;
                         for (int j = 0; j < nseg; j++)
                             all += __hip_atomic_load(&a.long_part[first + j], __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(&a.long_ticket[w.split], 0u, __ATOMIC_RELAXED,
+                        __hip_atomic_store(&a.long_ticket[cur.split], 0u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                         dang += finish_row(a, row, all, teleport, a.outdeg[row]);
                     }
                 }
             }
-            continue;
-        }
-        // rows of similar length: L lanes per row, G rows per pass
-        const int L = w.lanes;
-        const int G = kWave / L;
-        const int grp = lane / L, gl = lane & (L - 1);
-        for (int32_t r0 = w.row_begin; r0 < w.row_end; r0 += G) {
-            const int32_t row = r0 + grp;
-            const bool valid = row < w.row_end;
-            const int32_t deg = (valid && gl == 0) ? a.outdeg[row] : 0;
+            if (nhave && nxt.split < 0) ops = load_stream(a, nxt, lane);
+        } else {
+            // ---- STREAM item: gathers of this item, then the next item's operands
+            double v0[4], v1[4];
+            gather4(a, hub, ops.c0, v0);
+            gather4(a, hub, ops.c1, v1);
+            StreamOps nops{};
+            if (nhave && nxt.split < 0) nops = load_stream(a, nxt, lane);
+            const int64_t base = cur.nz_begin & ~(int64_t)3;
+            const int nq = (int)((cur.nz_end - base + 3) >> 2);
+            if (lane < nq) {
+                double2 *d = reinterpret_cast<double2 *>(st + 4 * lane);
+                d[0] = make_double2(v0[0], v0[1]);
+                d[1] = make_double2(v0[2], v0[3]);
+            }
+            if (lane + kWave < nq) {
+                double2 *d = reinterpret_cast<double2 *>(st + 4 * (lane + kWave));
+                d[0] = make_double2(v1[0], v1[1]);
+                d[1] = make_double2(v1[2], v1[3]);
+            }
+            wave_sync_lds();
+            const int nrows = cur.row_end - cur.row_begin;
+            int P = 1;
+            while (P < nrows) P <<= 1;
+            const int L = kWave / P;
+            const int row = lane / L, gl = lane & (L - 1);
+            const int rpv = (int)(ops.rp - base);
+            const int kb = __shfl(rpv, row, kWave);
+            const int ke = __shfl(rpv, row + 1 < kWave ? row + 1 : 0, kWave);
+            const int32_t deg = __shfl(ops.deg, row, kWave);
             double s = 0.0;
-            if (valid) s = row_sum(a, hub, a.rp[row], a.rp[row + 1], L, gl);
+            if (row < nrows)
+                for (int k = kb + gl; k < ke; k += L) s += st[k];
             for (int off = L >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
-            if (valid && gl == 0) dang += finish_row(a, row, s, teleport, deg);
+            if (row < nrows && gl == 0) dang += finish_row(a, cur.row_begin + row, s, teleport, deg);
+            wave_sync_lds();
+            ops = nops;
         }
+        cur = nxt;
+        i = ni;
+        have = nhave;
     }
 
     // dangling sum of the rank: lanes -> wave -> workgroup -> last-arriving workgroup
@@ -168,7 +252,7 @@ __global__ __launch_bounds__(kHubBlock) void k_pr_pull_hub(HubArgs a) {
     if (tid != 0) return;
     double bs = 0.0;
 #pragma unroll
-    for (int w = 0; w < kHubBlock / kWave; w++) bs += wsum[w];
+    for (int w = 0; w < kWaves; w++) bs += wsum[w];
     __hip_atomic_store(&a.gpart[blockIdx.x], bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -182,12 +266,6 @@ __global__ __launch_bounds__(kHubBlock) void k_pr_pull_hub(HubArgs a) {
     a.x_out[a.chunk - 1] = all;
 }
 
-int pow2_floor(int64_t v) {
-    int p = 1;
-    while ((int64_t)p * 2 <= v) p *= 2;
-    return p;
-}
-
 }  // namespace
 
 int pr_plan_hub(PrPart *p, const std::vector<int64_t> &h_rp) {
@@ -199,39 +277,34 @@ int pr_plan_hub(PrPart *p, const std::vector<int64_t> &h_rp) {
     int64_t r = 0;
     while (r < rows) {
         const int64_t len = h_rp[r + 1] - h_rp[r];
-        if (len > kHubSegNnz) {
+        if (len > kStreamMax) {
             longrows.push_back({len, (int32_t)r});
             r++;
             continue;
         }
         const int64_t start = r;
         int64_t nz = 0;
-        while (r < rows && r - start < kItemRows) {
+        while (r < rows && r - start < kStreamRowsMax) {
             const int64_t l = h_rp[r + 1] - h_rp[r];
-            if (l > kHubSegNnz) break;
-            if (r > start && nz + l > kItemNnz) break;
+            if (l > kStreamMax || nz + l > kStreamMax) break;
             nz += l;
             r++;
         }
-        const int64_t nrows = r - start;
-        // lanes per row: about half the mean row length, so a row takes ~2+ passes of its
-        // group; rows of one item have nearly the same length in hub-first order
-        int L = pow2_floor(std::max<int64_t>(1, nz / std::max<int64_t>(1, nrows) / 2));
-        L = std::min(L, kWave);
-        streami.push_back({h_rp[start], h_rp[r], (int32_t)start, (int32_t)r, -1, 0, L, 0});
+        streami.push_back({h_rp[start], h_rp[r], (int32_t)start, (int32_t)r, -1, 0, 0, 0});
     }
+    // longest rows first: their items are the heaviest
     std::stable_sort(longrows.begin(), longrows.end(),
                      [](const auto &x, const auto &y) { return x.first > y.first; });
     for (const auto &lr : longrows) {
         const int32_t row = lr.second;
-        const int32_t nseg = (int32_t)((lr.first + kHubSegNnz - 1) / kHubSegNnz);
+        const int32_t nseg = (int32_t)((lr.first + kLongSeg - 1) / kLongSeg);
         const int32_t sp = (int32_t)lfirst.size();
         lfirst.push_back(nsegs);
         lnseg.push_back(nseg);
         for (int32_t s = 0; s < nseg; s++) {
-            const int64_t zb = h_rp[row] + (int64_t)s * kHubSegNnz;
-            const int64_t ze = std::min<int64_t>(zb + kHubSegNnz, h_rp[row + 1]);
-            longi.push_back({zb, ze, row, row + 1, sp, s, kWave, 0});
+            const int64_t zb = h_rp[row] + (int64_t)s * kLongSeg;
+            const int64_t ze = std::min<int64_t>(zb + kLongSeg, h_rp[row + 1]);
+            longi.push_back({zb, ze, row, row + 1, sp, s, 0, 0});
         }
         nsegs += nseg;
     }
@@ -275,7 +348,7 @@ int pr_step_hub(PrPart *p, const double *x_full, double *x_local, double *rank_o
     a.rank_out = rank_out;
     a.chunk = (int64_t)p->chunk;
     a.nranks = p->nranks;
-    a.hub_entries = p->hub_entries;
+    a.hub_entries = (int32_t)p->hub_entries;
     a.teleport0 = (1.0 - p->damping) / dn;
     a.damping_over_n = p->damping / dn;
     a.damping = p->damping;
