@@ -44,6 +44,7 @@ struct HubArgs {
     int64_t chunk;
     int nranks;
     int32_t hub_entries;
+    uint32_t x_bytes;
     double teleport0, damping_over_n, damping;
     const int32_t *long_first;
     const int32_t *long_nseg;
@@ -53,20 +54,37 @@ struct HubArgs {
     uint32_t *gticket;
 };
 
-// x[c]: from the LDS hub when c < H, else from global memory.  Both reads are issued
-// unconditionally so the compiler can count outstanding loads exactly (no vmcnt(0) behind
-// branches): hub lanes point their global read at x[0] -- one shared cache line per wave
-// instruction -- and non-hub lanes read hub[0].
-__device__ __forceinline__ void gather4(const HubArgs &a, const double *hub, const int4 c, double v[4]) {
-    const int32_t H = a.hub_entries;
+// Buffer resource of a global array (stride 0, raw byte offsets, range-checked).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+constexpr uint32_t kOob = 0x80000000u;   // offset past every record: the lane is dropped
+
+// x[c]: from the LDS hub when c < H, else from global memory through a range-checked buffer
+// load.  Hub lanes get an out-of-range offset, so the hardware drops them (no cache access,
+// value 0) without a branch: the compiler keeps exact vmcnt counts and the next item's
+// loads stay in flight.  (Exec-masking via branches forced vmcnt(0); pointing hub lanes at
+// one shared line still cost one vector-L1 access per lane -- both measured.)
+__device__ __forceinline__ void gather4(const double *hub, int32_t H, __amdgpu_buffer_rsrc_t xr, const int4 c,
+                                        double v[4]) {
     const int cc[4] = {c.x, c.y, c.z, c.w};
     double hv[4], gv[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) hv[k] = hub[cc[k] < H ? cc[k] : 0];
 #pragma unroll
-    for (int k = 0; k < 4; k++) gv[k] = a.x_in[cc[k] < H ? 0 : cc[k]];
+    for (int k = 0; k < 4; k++)
+        gv[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                               xr, cc[k] < H ? kOob : (uint32_t)cc[k] * 8u, 0, 0));
 #pragma unroll
     for (int k = 0; k < 4; k++) v[k] = cc[k] < H ? hv[k] : gv[k];
+}
+
+// 16 column indices (int4) at entry offset q*4 of a per-item descriptor; lanes past the
+// item's records read zeros (no access).  aux 2 = non-temporal (read-once stream).
+__device__ __forceinline__ int4 load_idx4(__amdgpu_buffer_rsrc_t r, int q) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)q * 16u, 0, 2);
+    return make_int4((int)v[0], (int)v[1], (int)v[2], (int)v[3]);
 }
 
 // Operands of one STREAM item, loaded ahead of its gathers.  All loads are unconditional
@@ -83,9 +101,10 @@ __device__ __forceinline__ StreamOps load_stream(const HubArgs &a, const WaveIte
     const int64_t base = w.nz_begin & ~(int64_t)3;
     const int nq = (int)((w.nz_end - base + 3) >> 2);
     const int qmax = nq > 0 ? nq - 1 : 0;
-    const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
-    o.c0 = load_nt(ci4 + min(lane, qmax));
-    o.c1 = load_nt(ci4 + min(lane + kWave, qmax));
+    const __amdgpu_buffer_rsrc_t cr = rsrc_of(a.ci + base, (uint32_t)nq * 16u);
+    (void)qmax;
+    o.c0 = load_idx4(cr, lane);
+    o.c1 = load_idx4(cr, lane + kWave);
     const int nrows = w.row_end - w.row_begin;
     o.rp = a.rp[w.row_begin + min(lane, nrows)];
     o.deg = a.outdeg[w.row_begin + min(lane, nrows - 1)];
@@ -107,19 +126,19 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 // LONG item: entries [zb, ze) of one row; returns this lane's partial sum.
-__device__ __forceinline__ double long_sum(const HubArgs &a, const double *hub, int64_t zb, int64_t ze,
-                                           int lane) {
+__device__ __forceinline__ double long_sum(const HubArgs &a, const double *hub, __amdgpu_buffer_rsrc_t xr,
+                                           int64_t zb, int64_t ze, int lane) {
     const int64_t base = zb & ~(int64_t)3;
     const int nq = (int)((ze - base + 3) >> 2);
-    const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
+    const __amdgpu_buffer_rsrc_t cr = rsrc_of(a.ci + base, (uint32_t)nq * 16u);
     double s = 0.0;
     for (int q0 = 0; q0 < nq; q0 += 4 * kWave) {
         int4 c[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) c[j] = load_nt(ci4 + min(q0 + lane + j * kWave, nq - 1));
+        for (int j = 0; j < 4; j++) c[j] = load_idx4(cr, q0 + lane + j * kWave);
         double v[4][4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) gather4(a, hub, c[j], v[j]);
+        for (int j = 0; j < 4; j++) gather4(hub, a.hub_entries, xr, c[j], v[j]);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int64_t e = base + 4 * (int64_t)(q0 + lane + j * kWave);
@@ -159,6 +178,7 @@ __global__ __launch_bounds__(kHubBlock) void k_pr_pull_hub(HubArgs a) {
     __syncthreads();
 
     double *st = stage[wv];
+    const __amdgpu_buffer_rsrc_t xr = rsrc_of(a.x_in, a.x_bytes);
     double dang = 0.0;
     const uint32_t nw = gridDim.x * kWaves;
     uint32_t i = (uint32_t)wv * gridDim.x + blockIdx.x;
@@ -176,7 +196,7 @@ __global__ __launch_bounds__(kHubBlock) void k_pr_pull_hub(HubArgs a) {
         if (nhave) nxt = a.items[ni];
         if (cur.split >= 0) {
             // ---- LONG item: one segment of one row
-            const double s = wave_sum(long_sum(a, hub, cur.nz_begin, cur.nz_end, lane));
+            const double s = wave_sum(long_sum(a, hub, xr, cur.nz_begin, cur.nz_end, lane));
             if (lane == 0) {
                 const int32_t nseg = a.long_nseg[cur.split];
                 const int32_t row = cur.row_begin;
@@ -206,8 +226,8 @@ __global__ __launch_bounds__(kHubBlock) void k_pr_pull_hub(HubArgs a) {
         } else {
             // ---- STREAM item: gathers of this item, then the next item's operands
             double v0[4], v1[4];
-            gather4(a, hub, ops.c0, v0);
-            gather4(a, hub, ops.c1, v1);
+            gather4(hub, a.hub_entries, xr, ops.c0, v0);
+            gather4(hub, a.hub_entries, xr, ops.c1, v1);
             StreamOps nops{};
             if (nhave && nxt.split < 0) nops = load_stream(a, nxt, lane);
             const int64_t base = cur.nz_begin & ~(int64_t)3;
@@ -349,6 +369,7 @@ int pr_step_hub(PrPart *p, const double *x_full, double *x_local, double *rank_o
     a.chunk = (int64_t)p->chunk;
     a.nranks = p->nranks;
     a.hub_entries = (int32_t)p->hub_entries;
+    a.x_bytes = (uint32_t)(p->chunk * (uint64_t)p->nranks * 8u);
     a.teleport0 = (1.0 - p->damping) / dn;
     a.damping_over_n = p->damping / dn;
     a.damping = p->damping;

@@ -21,7 +21,7 @@ EOF
     return $rc
 }
 run hub_default X=1 || exit 1
-for h in 0 4096 12288; do
+for h in 0 6144; do
     run hub_$h GX_PR_HUB_ENTRIES=$h || exit 1
 done
 run adaptive GX_PR_KERNEL=adaptive || exit 1
