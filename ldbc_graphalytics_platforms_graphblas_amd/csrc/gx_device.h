@@ -152,6 +152,12 @@ int collect_timings(gx_ctx *ctx);
 int device_begin(gx_ctx *ctx);
 int device_end(gx_ctx *ctx);
 
+// Sort packed (row << 32 | col) keys (rows < n) in place (k1 = scratch of the same size)
+// and build row pointers / column indices from them.  rp must hold n + 1 entries and ci
+// m entries; keys end up sorted in *keys.
+int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,
+                     int32_t *ci, hipStream_t s);
+
 // Lazily build the transposed / closure CSR of a graph on the device.
 int ensure_transpose(gx_graph *g);
 int ensure_closure(gx_graph *g);

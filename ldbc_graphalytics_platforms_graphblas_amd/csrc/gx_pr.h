@@ -80,7 +80,8 @@ struct PrPart {
     DBuf<double> dpart;
     DBuf<uint32_t> dticket;
     // hub-cached kernel (default): wave items, LDS hub prefix, fused dangling reduction
-    int kernel = 0;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive)
+    int kernel = 1;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive, default)
+    bool int4_loads = false;     // k_pr_pull: 16-B index loads (lane stride 4) instead of lane-consecutive
     DBuf<WaveItem> items;
     uint32_t nitems = 0;
     DBuf<int32_t> hlong_first, hlong_nseg;

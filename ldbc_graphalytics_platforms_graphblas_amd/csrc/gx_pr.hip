@@ -59,7 +59,7 @@ __device__ __forceinline__ void pr_epilogue(const PullArgs &a, int32_t row, doub
     a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
 }
 
-template <int NB>
+template <int NB, bool STRIDE1>
 __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
     __shared__ __attribute__((aligned(16))) double vals[NB + 4];
     __shared__ int32_t rofs[kStreamRows + 1];
@@ -90,6 +90,26 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
         const int row = tid / L, lane = tid & (L - 1);
         const bool writer = row < nrows && lane == 0;
         const int32_t deg = writer ? a.outdeg[r0 + row] : 0;
+        if (STRIDE1) {
+            // Lane-consecutive entries: gather instruction j of a wave covers 64 consecutive
+            // entries, so with every row sorted by (hub-first) column id neighbouring lanes
+            // often hit the same x cache line -- one L1 miss serves several gathers.  The
+            // L1-miss count is what bounds this kernel (~70 misses in flight per CU).
+            constexpr int NE = (NB + 3 + kPullBlock - 1) / kPullBlock;
+            const int64_t last = z1 > base ? z1 - 1 : base;   // clamp: index loads stay valid
+            int32_t c[NE];
+#pragma unroll
+            for (int j = 0; j < NE; j++)
+                c[j] = __builtin_nontemporal_load(a.ci + min(base + tid + (int64_t)j * kPullBlock, last));
+            double v[NE];
+#pragma unroll
+            for (int j = 0; j < NE; j++) v[j] = a.x_in[c[j]];
+#pragma unroll
+            for (int j = 0; j < NE; j++) {
+                const int e = tid + j * kPullBlock;
+                if (base + e < z1) vals[e] = v[j];
+            }
+        } else {
         constexpr int NQ = (NB / 4 + kPullBlock) / kPullBlock;
         // Column indices: 16 B per lane, non-temporal (read once; keep L2 for x).  Every
         // index read here is a valid x offset (neighbouring rows' entries, or the zeroed
@@ -117,6 +137,7 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
                 d[1] = make_double2(v[j][2], v[j][3]);
             }
         }
+        }
         __syncthreads();
         double s = 0.0;
         if (row < nrows) {
@@ -134,10 +155,26 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
 
     // ---------------- LONG: one segment of one long row ----------------
     const int64_t zb = b.nz_begin, ze = b.nz_end;
-    const int64_t base = zb & ~(int64_t)3;
-    const int64_t nq = (ze - base + 3) >> 2;
-    const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
     double s0 = 0.0, s1 = 0.0;
+    if (STRIDE1) {
+        // lane-consecutive entries, 8 loads in flight per lane, clamped (always valid)
+        constexpr int U = 8;
+        for (int64_t k0 = zb + tid; k0 < ze; k0 += (int64_t)U * kPullBlock) {
+            int32_t c[U];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                c[u] = __builtin_nontemporal_load(a.ci + min(k0 + (int64_t)u * kPullBlock, ze - 1));
+            double g[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (k0 + (int64_t)u * kPullBlock < ze) ((u & 1) ? s1 : s0) += g[u];
+        }
+    }
+    const int64_t base = zb & ~(int64_t)3;
+    const int64_t nq = STRIDE1 ? 0 : (ze - base + 3) >> 2;
+    const int4 *ci4 = reinterpret_cast<const int4 *>(a.ci) + (base >> 2);
     for (int64_t q = tid; q < nq; q += 2 * kPullBlock) {
         const int64_t q1 = q + kPullBlock;
         const int4 c0 = load_nt(ci4 + q);
@@ -329,7 +366,8 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     GX_TRY(p->dticket.alloc(1));
     GX_HIP_TRY(hipMemset(p->dticket.p, 0, 4));
     // kernel choice: GX_PR_KERNEL = hub (default) | adaptive
-    if (const char *e = std::getenv("GX_PR_KERNEL")) p->kernel = std::strcmp(e, "adaptive") == 0 ? 1 : 0;
+    if (const char *e = std::getenv("GX_PR_KERNEL")) p->kernel = std::strcmp(e, "hub") == 0 ? 0 : 1;
+    if (const char *e = std::getenv("GX_PR_INT4")) p->int4_loads = std::atoi(e) != 0;
     if (p->kernel == 0) GX_TRY(pr_plan_hub(p, h_rp));
     return GX_SUCCESS;
 }
@@ -382,12 +420,15 @@ int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, 
     }
     if (nb) {
         KTimer kt(p->ctx, "pr_pull", s);
-        if (p->stream_nnz == 1024)
-            hipLaunchKernelGGL(k_pr_pull<1024>, dim3(nb), dim3(kPullBlock), 0, s, a);
-        else if (p->stream_nnz == 4096)
-            hipLaunchKernelGGL(k_pr_pull<4096>, dim3(nb), dim3(kPullBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_pr_pull<2048>, dim3(nb), dim3(kPullBlock), 0, s, a);
+        if (p->int4_loads) {
+            hipLaunchKernelGGL((k_pr_pull<2048, false>), dim3(nb), dim3(kPullBlock), 0, s, a);
+        } else if (p->stream_nnz == 1024) {
+            hipLaunchKernelGGL((k_pr_pull<1024, true>), dim3(nb), dim3(kPullBlock), 0, s, a);
+        } else if (p->stream_nnz == 4096) {
+            hipLaunchKernelGGL((k_pr_pull<4096, true>), dim3(nb), dim3(kPullBlock), 0, s, a);
+        } else {
+            hipLaunchKernelGGL((k_pr_pull<2048, true>), dim3(nb), dim3(kPullBlock), 0, s, a);
+        }
     }
     GX_TRY(check_launch("k_pr_pull"));
     return pr_dangling(p, x_local, s);
@@ -403,9 +444,10 @@ namespace {
 
 // Relabel a CSR by `perm` (old vertex -> new position): row perm[r] of the result holds the
 // entries of row r with every column c renamed perm[c].  Edge-balanced, no sort.
-__global__ void k_permute_csr(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci, int64_t n,
-                              int64_t nnz, const int32_t *__restrict__ perm, const int64_t *__restrict__ nrp,
-                              int32_t *__restrict__ nci) {
+// keys[e] = (perm[row] << 32) | perm[col] for every entry: sorted, they give the relabelled
+// CSR with every row sorted by new column id.  Edge-balanced.
+__global__ void k_permute_keys(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci, int64_t n,
+                               int64_t nnz, const int32_t *__restrict__ perm, uint64_t *__restrict__ keys) {
     constexpr int kPer = 16;
     const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPer;
     if (e0 >= nnz) return;
@@ -413,7 +455,7 @@ __global__ void k_permute_csr(const int64_t *__restrict__ rp, const int32_t *__r
     int64_t r = row_of_edge(rp, n, e0);
     for (int64_t e = e0; e < e1; e++) {
         while (rp[r + 1] <= e) r++;
-        nci[nrp[perm[r]] + (e - rp[r])] = perm[ci[e]];
+        keys[e] = ((uint64_t)(uint32_t)perm[r] << 32) | (uint32_t)perm[ci[e]];
     }
 }
 
@@ -481,9 +523,19 @@ int pr_single_plan(gx_graph *g, PrPart **out) {
         e = hipMemcpyAsync(p->outdeg_own.p, nout.data(), n * 4, hipMemcpyHostToDevice, s);
     if (rc == GX_SUCCESS && e != hipSuccess) rc = fail(GX_DEVICE_ERROR, hipGetErrorString(e));
     if (rc == GX_SUCCESS && P.nnz) {
-        hipLaunchKernelGGL(k_permute_csr, dim3(grid_for((P.nnz + 15) / 16, 256, 1u << 30)), dim3(256), 0, s,
-                           P.rp.p, P.ci.p, (int64_t)n, (int64_t)P.nnz, p->perm.p, p->rp_own.p, p->ci_own.p);
-        rc = check_launch("k_permute_csr");
+        DBuf<uint64_t> keys, scratch;
+        rc = keys.alloc(P.nnz);
+        if (rc == GX_SUCCESS) rc = scratch.alloc(P.nnz);
+        if (rc == GX_SUCCESS) {
+            hipLaunchKernelGGL(k_permute_keys, dim3(grid_for((P.nnz + 15) / 16, 256, 1u << 30)), dim3(256), 0, s,
+                               P.rp.p, P.ci.p, (int64_t)n, (int64_t)P.nnz, p->perm.p, keys.p);
+            rc = check_launch("k_permute_keys");
+        }
+        if (rc == GX_SUCCESS) rc = sort_keys_to_csr(keys, scratch, P.nnz, (int64_t)n, p->rp_own.p, p->ci_own.p, s);
+        if (rc == GX_SUCCESS) {
+            e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = fail(GX_DEVICE_ERROR, hipGetErrorString(e));
+        }
     }
     if (rc == GX_SUCCESS) rc = pr_plan(p, nrp, p->rp_own.p, p->ci_own.p, p->outdeg_own.p, nout);
     if (rc == GX_SUCCESS) {

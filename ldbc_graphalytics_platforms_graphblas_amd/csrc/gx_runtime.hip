@@ -300,6 +300,23 @@ int key_bits(uint64_t n) {
 
 namespace gx {
 
+int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,
+                     int32_t *ci, hipStream_t s) {
+    if (m) {
+        const int bits = key_bits((uint64_t)n);
+        size_t tmp_bytes = 0;
+        GX_HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, keys.p, scratch.p, m, 0, bits, s));
+        DBuf<char> tmp;
+        GX_TRY(tmp.alloc(tmp_bytes));
+        GX_HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, keys.p, scratch.p, m, 0, bits, s));
+        GX_HIP_TRY(hipMemcpyAsync(keys.p, scratch.p, m * 8, hipMemcpyDeviceToDevice, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+    }
+    hipLaunchKernelGGL(k_keys_to_csr, dim3(grid_for((uint64_t)n + 1, 256, 1u << 30)), dim3(256), 0, s, keys.p,
+                       (int64_t)m, n, rp, ci);
+    return check_launch("k_keys_to_csr");
+}
+
 int ensure_outdeg(gx_graph *g) {
     if (g->outdeg.p) return GX_SUCCESS;
     GX_TRY(g->outdeg.alloc(g->n));

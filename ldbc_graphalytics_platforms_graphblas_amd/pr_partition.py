@@ -39,9 +39,19 @@ def hub_relabel(csr: CSR):
     nrp = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(new_deg, out=nrp[1:])
     idx = np.repeat(csr.rowptr.astype(np.int64)[order] - nrp[:-1], new_deg) + np.arange(int(nrp[-1]))
-    nci = perm[csr.colidx.astype(np.int64)[idx]].astype(np.uint64)
-    vals = None if csr.vals is None else np.ascontiguousarray(csr.vals[idx])
-    return perm, CSR(n, nrp.astype(np.uint64), nci, vals)
+    nci = perm[csr.colidx.astype(np.int64)[idx]]
+    # every row sorted by new column id: neighbouring lanes of a gather then often share
+    # an x cache line (hub columns cluster at the start of each row)
+    rows = np.repeat(np.arange(n, dtype=np.int64), new_deg)
+    if csr.vals is None:
+        key = np.sort(rows * n + nci)
+        nci = (key - rows * n).astype(np.uint64)
+        vals = None
+    else:
+        o = np.argsort(rows * n + nci, kind="stable")
+        nci = nci[o].astype(np.uint64)
+        vals = np.ascontiguousarray(csr.vals[idx][o])
+    return perm, CSR(n, nrp.astype(np.uint64), np.ascontiguousarray(nci), vals)
 
 
 def partition_rows(rowptr: np.ndarray, nranks: int) -> np.ndarray:

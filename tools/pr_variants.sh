@@ -20,11 +20,11 @@ except Exception as e:
 EOF
     return $rc
 }
-run hub_default X=1 || exit 1
-for h in 0 6144; do
-    run hub_$h GX_PR_HUB_ENTRIES=$h || exit 1
-done
-run adaptive GX_PR_KERNEL=adaptive || exit 1
+run stride1_nb2048 X=1 || exit 1
+run stride1_nb1024 GX_PR_STREAM_NNZ=1024 || exit 1
+run stride1_nb4096 GX_PR_STREAM_NNZ=4096 || exit 1
+run int4 GX_PR_INT4=1 || exit 1
+run hub GX_PR_KERNEL=hub || exit 1
 rocprofv3 -L > "$OUT/counters.txt" 2>&1
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS" \
            "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum" \
