@@ -1,0 +1,164 @@
+"""Row-partitioned PageRank across ranks (the bench's N > 1 path).
+
+CPU (gloo, world_size 2): the same orchestration bench.py runs over RCCL --
+partition_rows / local_rows / hub_relabel / PartitionedPageRank with one
+all_gather_into_tensor per iteration -- driven by a numpy stepper that restates the
+gx_pr_part_* contract (padded chunk layout, dangling slot), checked against the oracle.
+GPU: gx_pr_part_* itself with two ranks simulated on one device.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT  # noqa: F401  (sys.path)
+from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
+from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import (PartitionedPageRank, hub_relabel, local_rows,
+                                                                    partition_rows)
+from oracle import oracle as O
+
+
+class CpuStep:
+    """numpy restatement of gx_pr_part_create/init/step (test-only stand-in for the GPU)."""
+
+    def __init__(self, n_global, nranks, lr, damping):
+        rr = lr.row_ranges.astype(np.int64)
+        self.chunk = int(((rr[1:] - rr[:-1]).max() + 1 + 31) // 32 * 32)
+        owner = np.searchsorted(rr, lr.colidx.astype(np.int64), side="right") - 1
+        self.cols = owner * self.chunk + (lr.colidx.astype(np.int64) - rr[owner])
+        self.rp = lr.rowptr.astype(np.int64)
+        self.deg = lr.outdeg.astype(np.int64)
+        self.rows = lr.rows
+        self.n = n_global
+        self.nranks = nranks
+        self.d = damping
+
+    def init(self, x_local, stream):
+        inv_n = 1.0 / self.n
+        x = np.where(self.deg > 0, inv_n / (self.deg / self.d), inv_n)
+        x_local[:self.rows] = torch.from_numpy(x)
+        x_local[self.chunk - 1] = float(np.sum(np.where(self.deg == 0, inv_n, 0.0)))
+
+    def step(self, x_full, x_local, rank_out, stream):
+        xf = x_full.numpy()
+        dsum = sum(xf[k * self.chunk + self.chunk - 1] for k in range(self.nranks))
+        tele = (1.0 - self.d) / self.n + self.d / self.n * dsum
+        s = np.add.reduceat(np.append(xf[self.cols], 0.0), self.rp[:-1]) if len(self.cols) else np.zeros(self.rows)
+        s = np.where(np.diff(self.rp) > 0, s, 0.0)
+        r = tele + s
+        x_local[:self.rows] = torch.from_numpy(np.where(self.deg > 0, r / (self.deg / self.d), r))
+        x_local[self.chunk - 1] = float(np.sum(np.where(self.deg == 0, r, 0.0)))
+        if rank_out is not None:
+            rank_out[:self.rows] = torch.from_numpy(r)
+
+
+def _gloo_gather(out, inp):
+    parts = list(out.chunk(dist.get_world_size()))
+    dist.all_gather(parts, inp)
+    if parts[0].data_ptr() != out.data_ptr():
+        out.copy_(torch.cat(parts))
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        csr = rmat(11, 8, 5)
+        perm, hub = hub_relabel(csr)
+        lr = local_rows(hub, directed=False, nranks=world, rank=rank)
+        pr = PartitionedPageRank(CpuStep(csr.n, world, lr, 0.85), world, lr.rows, "cpu", all_gather=_gloo_gather)
+        out = pr.run(7).numpy().copy()
+        parts = [None] * world
+        dist.all_gather_object(parts, out)
+        if rank == 0:
+            q.put(np.concatenate(parts)[perm])
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_partition_rows_balanced():
+    csr = rmat(12, 16, 9)
+    rp = csr.rowptr.astype(np.int64)
+    for k in (1, 2, 3, 8):
+        b = partition_rows(rp, k).astype(np.int64)
+        assert b[0] == 0 and b[-1] == csr.n and (np.diff(b) >= 0).all()
+        loads = rp[b[1:]] - rp[b[:-1]]
+        assert loads.sum() == csr.nnz
+        assert loads.max() <= csr.nnz / k + np.diff(rp).max() + 1
+
+
+def test_hub_relabel_is_isomorphic():
+    csr = rmat(10, 8, 2)
+    perm, hub = hub_relabel(csr)
+    deg_new = np.diff(hub.rowptr.astype(np.int64))
+    assert (np.diff(deg_new) <= 0).all()                    # hub-first
+    for v in range(0, csr.n, 97):
+        old = np.sort(perm[csr.colidx[csr.rowptr[v]:csr.rowptr[v + 1]].astype(np.int64)])
+        row = hub.colidx[hub.rowptr[perm[v]]:hub.rowptr[perm[v] + 1]].astype(np.int64)
+        assert (np.diff(row) > 0).all()                     # rows sorted
+        assert (old == row).all()
+    # PageRank is invariant under relabelling
+    a = O.pagerank(csr, False, 0.85, 5)
+    b = O.pagerank(hub, False, 0.85, 5)[perm]
+    np.testing.assert_allclose(a, b, rtol=1e-12)
+
+
+def test_gloo_world2_matches_oracle():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    csr = rmat(11, 8, 5)
+    np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, 7), rtol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [1, 2, 3])
+def test_gpu_partition_api_simulated_ranks(nranks):
+    """gx_pr_part_* with `nranks` parts on one device; the exchange is a device concat."""
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import GpuStep
+    csr = rmat(13, 16, 11)
+    perm, hub = hub_relabel(csr)
+    ctx = Context(0)
+    dev = torch.device("cuda", 0)
+    steps, lrs = [], []
+    for r in range(nranks):
+        lr = local_rows(hub, directed=False, nranks=nranks, rank=r)
+        lrs.append(lr)
+        steps.append(GpuStep(ctx, csr.n, nranks, lr, 0.85))
+    chunk = steps[0].chunk
+    xl = [torch.zeros(chunk, dtype=torch.float64, device=dev) for _ in range(nranks)]
+    xf = torch.zeros(chunk * nranks, dtype=torch.float64, device=dev)
+    ro = [torch.zeros(max(lr.rows, 1), dtype=torch.float64, device=dev) for lr in lrs]
+    iters = 6
+    for r in range(nranks):
+        steps[r].init(xl[r], 0)
+    torch.cuda.synchronize()
+    xf.copy_(torch.cat(xl))
+    for it in range(iters):
+        for r in range(nranks):
+            steps[r].step(xf, xl[r], ro[r] if it == iters - 1 else None, 0)
+        torch.cuda.synchronize()
+        xf.copy_(torch.cat(xl))
+    got = np.concatenate([ro[r][:lrs[r].rows].cpu().numpy() for r in range(nranks)])[perm]
+    for s in steps:
+        s.close()
+    ctx.close()
+    np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, iters), rtol=1e-12)
