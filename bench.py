@@ -50,7 +50,135 @@ def parse():
     ap.add_argument("--damping", type=float, default=0.85)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--algorithm", default="pr", choices=["pr", "bfs", "wcc", "sssp", "cdlp", "lcc"],
+                    help="pr = the headline (BASELINE configs[1]); the others measure configs 3-5 on 1 GPU")
+    ap.add_argument("--graph", default=None, choices=sorted(PRESETS), help="synthetic stand-in (SURVEY.md 8d)")
     return ap.parse_args()
+
+
+# SURVEY.md 8d synthetic stand-ins (no network for the Graphalytics datasets)
+PRESETS = {
+    "SYN-7_5": dict(scale=20, ef=32, seed=75, undirected=True, weighted=False, stands_for="datagen-7_5-fb"),
+    "SYN-g500-22": dict(scale=22, ef=16, seed=22, undirected=True, weighted=False, stands_for="graph500-22"),
+    "SYN-8_5": dict(scale=23, ef=40, seed=85, undirected=True, weighted=True, stands_for="datagen-8_5-fb"),
+    "SYN-cit": dict(scale=22, ef=4, seed=3, undirected=False, weighted=False, stands_for="cit-Patents"),
+}
+DEFAULT_GRAPH = {"pr": "SYN-7_5", "cdlp": "SYN-7_5", "bfs": "SYN-g500-22", "wcc": "SYN-g500-22",
+                 "sssp": "SYN-8_5", "lcc": "SYN-cit"}
+DOMINANT = {"bfs": "bfs_topdown", "wcc": "wcc_hook", "sssp": "sssp_relax", "cdlp": "cdlp_light",
+            "lcc": "lcc_triangles"}
+
+
+def run_algorithm(args):
+    """One GPU, one algorithm on its BASELINE config (3-5); prints one JSON line.
+    value = work units / device time of a warm call (graph resident in HBM; the transpose /
+    closure built by the first call is cached and reported separately as first_call_ms)."""
+    import torch  # noqa: F401  (device init like the PR path)
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
+    alg = args.algorithm
+    gname = args.graph or DEFAULT_GRAPH[alg]
+    P = PRESETS[gname]
+    t_gen = time.time()
+    csr = rmat(P["scale"], P["ef"], P["seed"], undirected=P["undirected"], weighted=(alg == "sssp"))
+    t_gen = time.time() - t_gen
+    directed = not P["undirected"]
+    n, nnz = csr.n, csr.nnz
+    deg = np.diff(csr.rowptr.astype(np.int64))
+    src = int(np.argmax(deg))
+    ctx = A.Context(0)
+    dev_name, cus = ctx.info()
+    G = A.Graph(ctx, csr, directed)
+    iters = args.iters
+
+    def call():
+        if alg == "bfs":
+            return A.LA_BFS(G, src)
+        if alg == "wcc":
+            return A.WeaklyConnectedComponents(G)
+        if alg == "sssp":
+            return A.LA_SSSP(G, src)
+        if alg == "cdlp":
+            return A.LA_CDLP(G, iters)
+        return A.LA_LCC(G)
+
+    t1 = time.perf_counter()
+    out = call()
+    first_ms = (time.perf_counter() - t1) * 1e3
+    for _ in range(max(0, args.warmup - 1)):
+        call()
+    ctx.reset_kernel_stats()
+    ctx.set_kernel_timing(True)
+    dev_ms = []
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        out = call()
+        dev_ms.append(ctx.last_device_ms())
+    wall = time.perf_counter() - t1
+    ctx.set_kernel_timing(False)
+    kl, kms = ctx.kernel_stats(DOMINANT[alg])
+    t_dev = float(np.median(dev_ms)) / 1e3
+    # work units and algorithmic bytes (SURVEY.md 8d / BASELINE.md)
+    nnz_eff = nnz * (2 if (alg == "cdlp" and directed) else 1)
+    if alg == "bfs":
+        reached = out != np.iinfo(np.int64).max
+        work = int(deg[reached].sum()) // (1 if directed else 2)   # Graph500 TEPS: input edges reached
+        nbytes = 4 * nnz + 16 * n + 8
+        unit = "TEPS"
+    elif alg == "wcc":
+        work, nbytes, unit = nnz, 4 * nnz + 16 * n + 8, "edges/s"
+    elif alg == "sssp":
+        work, nbytes, unit = nnz, 12 * nnz + 16 * n + 8, "edges/s"
+    elif alg == "cdlp":
+        work = nnz_eff * iters
+        nbytes = (4 * nnz_eff + 8 * (n + 1) * (2 if directed else 1) + 16 * n) * iters
+        unit = "edges/s"
+    else:
+        from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+        rows = np.repeat(np.arange(n, dtype=np.int64), deg)
+        cl = csr_from_edges(n, rows, csr.colidx.astype(np.int64), None, symmetric=True)
+        sdeg = np.diff(cl.rowptr.astype(np.int64))
+        work = cl.nnz
+        nbytes = 4 * int((sdeg.astype(np.float64) ** 2).sum()) + 4 * cl.nnz + 8 * (n + 1)
+        unit = "edges/s"
+    cpu = None
+    parity = None
+    if not args.no_cpu_baseline:
+        from oracle import oracle as O
+        threads = min(16, os.cpu_count() or 1)
+        t1 = time.perf_counter()
+        if alg == "bfs":
+            ref, cores = O.bfs(csr, src), 1
+        elif alg == "wcc":
+            ref, cores = O.wcc(csr), 1
+        elif alg == "sssp":
+            ref, cores = O.sssp(csr, src), 1
+        elif alg == "cdlp":
+            ref, cores = O.cdlp(csr, directed, iters, nthreads=threads), threads
+        else:
+            ref, cores = O.lcc(csr, directed, nthreads=threads), threads
+        t_cpu = time.perf_counter() - t1
+        cpu = {"value": work / t_cpu, "unit": unit, "cores": cores, "kind": "port",
+               "sample": f"one full {alg} run on the same {gname} graph (oracle/gx_oracle.c), {t_cpu:.2f} s"}
+        parity = "bit-exact" if np.array_equal(out, ref) else f"MISMATCH ({int((out != ref).sum())} vertices)"
+    line = {
+        "metric": METRIC, "value": work / t_dev, "unit": unit, "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": t_dev * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": {"sssp": "f64", "lcc": "int64+f64"}.get(alg, "int32"),
+        "data": f"synthetic (seeded R-MAT stand-in for {P['stands_for']}; no network for the real dataset)",
+        "config": {"workload": f"{alg.upper()} {gname}", "algorithm": alg, "graph": gname, "n": n, "nnz": nnz,
+                   "directed": directed, "iterations": iters if alg == "cdlp" else None, "source": src,
+                   "parallelism": "single", "device": dev_name, "cus": cus},
+        "roofline": {"kernel": f"{alg} (whole device time)", "dominant_kernel": DOMINANT[alg], "bound": "hbm",
+                     "achieved": nbytes / t_dev / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": nbytes / t_dev / 1e9 / HBM_PEAK_GBS, "traffic": None, "bytes_per_run": nbytes,
+                     "dominant_kernel_ms_per_run": kms / max(1, args.steps), "dominant_launches": kl},
+        "cpu_baseline": cpu, "parity_vs_oracle": parity, "first_call_ms": first_ms,
+        "wall_ms_per_call_incl_d2h": wall * 1e3 / args.steps, "graph_gen_s": t_gen,
+    }
+    print(json.dumps(line), flush=True)
+    G.close()
+    ctx.close()
 
 
 def pmc_traffic(workload: str):
@@ -71,6 +199,14 @@ def main():
     args = parse()
     import torch
 
+    if args.algorithm != "pr":
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1:
+            raise SystemExit(f"--algorithm {args.algorithm} runs on one GPU (replicas only)")
+        return run_algorithm(args)
+    if args.graph and args.graph != "SYN-7_5":
+        P = PRESETS[args.graph]
+        args.scale, args.edgefactor, args.seed = P["scale"], P["ef"], P["seed"]
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -90,7 +226,8 @@ def main():
     from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import GpuStep, PartitionedPageRank, hub_relabel, \
         local_rows
 
-    workload = f"PageRank SYN-7_5 (R-MAT scale {args.scale}, ef {args.edgefactor}, seed {args.seed}, undirected)"
+    gname = args.graph or "SYN-7_5"
+    workload = f"PageRank {gname} (R-MAT scale {args.scale}, ef {args.edgefactor}, seed {args.seed}, undirected)"
     t_gen = time.time()
     csr = rmat(args.scale, args.edgefactor, args.seed, undirected=True)
     t_gen = time.time() - t_gen
@@ -165,7 +302,7 @@ def main():
             t_cpu += time.perf_counter() - t1
             runs += 1
         cpu = {"value": nnz * args.iters * runs / t_cpu, "unit": "edges/s", "cores": threads, "kind": "port",
-               "sample": f"{runs} full PageRank run(s) ({args.iters} iterations) on the same SYN-7_5 graph, "
+               "sample": f"{runs} full PageRank run(s) ({args.iters} iterations) on the same {gname} graph, "
                          f"OpenMP pull restatement (oracle/gx_oracle.c), {t_cpu:.2f} s"}
         parity = float(np.max(np.abs(result - ref) / np.abs(ref)))
 
@@ -182,11 +319,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded R-MAT stand-in for datagen-7_5-fb; no network for the real dataset)",
+            "data": f"synthetic (seeded R-MAT stand-in for {PRESETS[gname]['stands_for']}; no network for the real dataset)",
             "config": {
                 "workload": workload,
                 "algorithm": "pagerank",
-                "graph": "SYN-7_5",
+                "graph": gname,
                 "n": n,
                 "nnz": nnz,
                 "iterations": args.iters,
