@@ -16,27 +16,40 @@ namespace gx {
 namespace {
 
 constexpr int kBfsBlock = 256;
+constexpr int kChunk = 256;   // edges per top-down work item (4 per lane)
 
-__device__ __forceinline__ void wave_append(bool take, int32_t v, int32_t *queue, uint32_t *qcount) {
-    const uint64_t mask = __ballot(take);
-    if (mask == 0) return;
+// Frontier work items: (vertex << 32) | chunk, one item per kChunk out-edges, so a hub's
+// adjacency is spread over many waves.  Appends are wave-aggregated: an inclusive scan of
+// the lanes' item counts, one atomicAdd per wave.
+__device__ __forceinline__ void wave_append(bool take, int32_t v, uint32_t nch, uint64_t *queue,
+                                            uint32_t *qcount) {
     const int lane = threadIdx.x & (kWave - 1);
-    const int leader = __ffsll((unsigned long long)mask) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(qcount, (uint32_t)__popcll(mask));
-    base = __shfl(base, leader, kWave);
-    if (take) {
-        const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1));
-        queue[base + rank] = v;
+    const uint32_t k = take ? nch : 0u;
+    uint32_t x = k;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, kWave);
+        if (lane >= off) x += y;
     }
+    const uint32_t total = __shfl(x, kWave - 1, kWave);
+    if (total == 0) return;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(qcount, total);
+    base = __shfl(base, 0, kWave);
+    const uint32_t excl = x - k;
+    for (uint32_t j = 0; j < k; j++) queue[base + excl + j] = ((uint64_t)(uint32_t)v << 32) | j;
 }
 
-// top-down: one wave per frontier vertex
+__device__ __forceinline__ uint32_t chunks_of(int64_t deg) {
+    return (uint32_t)((deg + kChunk - 1) / kChunk);
+}
+
+// top-down: one wave per work item (<= kChunk edges of one frontier vertex)
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown(const int64_t *__restrict__ rp,
                                                            const int32_t *__restrict__ ci,
-                                                           const int32_t *__restrict__ qin,
+                                                           const uint64_t *__restrict__ qin,
                                                            uint32_t qsize, int32_t *level,
-                                                           int32_t depth, int32_t *qout,
+                                                           int32_t depth, uint64_t *qout,
                                                            uint32_t *qcount,
                                                            unsigned long long *next_edges) {
     const int lane = threadIdx.x & (kWave - 1);
@@ -44,20 +57,26 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown(const int64_t *__rest
     const uint32_t nwaves = gridDim.x * (kBfsBlock / kWave);
     unsigned long long edges = 0;
     for (uint32_t f = wave; f < qsize; f += nwaves) {
-        const int32_t u = qin[f];
-        const int64_t b = rp[u], e = rp[u + 1];
-        for (int64_t k0 = b; k0 < e; k0 += kWave) {
-            const int64_t k = k0 + lane;
+        const uint64_t item = qin[f];
+        const int32_t u = (int32_t)(item >> 32);
+        const int64_t e = rp[u + 1];
+        const int64_t b = rp[u] + (int64_t)(uint32_t)item * kChunk;
+        const int64_t end = min(e, b + kChunk);
+#pragma unroll
+        for (int i = 0; i < kChunk / kWave; i++) {
+            const int64_t k = b + lane + (int64_t)i * kWave;
             bool take = false;
             int32_t v = 0;
-            if (k < e) {
+            int64_t dv = 0;
+            if (k < end) {
                 v = ci[k];
                 if (level[v] < 0 && atomicCAS(&level[v], -1, depth + 1) == -1) {
                     take = true;
-                    edges += (unsigned long long)(rp[v + 1] - rp[v]);
+                    dv = rp[v + 1] - rp[v];
+                    edges += (unsigned long long)dv;
                 }
             }
-            wave_append(take, v, qout, qcount);
+            wave_append(take, v, chunks_of(dv), qout, qcount);
         }
     }
     // one atomic per wave for the next frontier's edge count (direction heuristic)
@@ -70,7 +89,7 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__res
                                                             const int32_t *__restrict__ cii,
                                                             const int64_t *__restrict__ rpo,
                                                             int64_t n, int32_t *level, int32_t depth,
-                                                            int32_t *qout, uint32_t *qcount,
+                                                            uint64_t *qout, uint32_t *qcount,
                                                             unsigned long long *next_edges) {
     unsigned long long edges = 0;
     const int64_t stride = (int64_t)gridDim.x * kBfsBlock;
@@ -78,6 +97,7 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__res
     for (int64_t r = 0; r < nround; r++) {
         const int64_t v = r * stride + (int64_t)blockIdx.x * kBfsBlock + threadIdx.x;
         bool take = false;
+        int64_t dv = 0;
         if (v < n && level[v] < 0) {
             for (int64_t k = rpi[v]; k < rpi[v + 1]; k++) {
                 if (level[cii[k]] == depth) {
@@ -87,18 +107,22 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__res
             }
             if (take) {
                 level[v] = depth + 1;
-                edges += (unsigned long long)(rpo[v + 1] - rpo[v]);
+                dv = rpo[v + 1] - rpo[v];
+                edges += (unsigned long long)dv;
             }
         }
-        wave_append(take, (int32_t)v, qout, qcount);
+        wave_append(take, (int32_t)v, chunks_of(dv), qout, qcount);
     }
     for (int off = 32; off > 0; off >>= 1) edges += __shfl_xor(edges, off, kWave);
     if ((threadIdx.x & (kWave - 1)) == 0 && edges) atomicAdd(next_edges, edges);
 }
 
-__global__ void k_bfs_seed(int32_t *level, int32_t *queue, int32_t src) {
+__global__ void k_bfs_seed(const int64_t *__restrict__ rp, int32_t *level, uint64_t *queue, uint32_t *qcount,
+                           int32_t src) {
     level[src] = 0;
-    queue[0] = src;
+    const uint32_t nch = chunks_of(rp[src + 1] - rp[src]);
+    for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x) queue[j] = ((uint64_t)(uint32_t)src << 32) | j;
+    if (threadIdx.x == 0) *qcount = nch;
 }
 
 }  // namespace
@@ -113,21 +137,26 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const int64_t n = (int64_t)g->n;
-    DBuf<int32_t> level, q0, q1;
+    DBuf<int32_t> level;
+    DBuf<uint64_t> q0, q1;
     DBuf<uint32_t> qcount;
     DBuf<unsigned long long> nedges;
+    const uint64_t qcap = (uint64_t)n + g->nnz / kChunk + 64;   // sum over vertices of ceil(deg / kChunk)
     GX_TRY(level.alloc(n));
-    GX_TRY(q0.alloc(n));
-    GX_TRY(q1.alloc(n));
+    GX_TRY(q0.alloc(qcap));
+    GX_TRY(q1.alloc(qcap));
     GX_TRY(qcount.alloc(1));
     GX_TRY(nedges.alloc(1));
     GX_TRY(device_begin(ctx));
     // in-edges: the graph itself when undirected, the transpose when already resident
     const DevCSR *in = g->directed ? (g->AT.built ? &g->AT : nullptr) : &g->A;
     GX_HIP_TRY(hipMemsetAsync(level.p, 0xff, n * 4, s));
-    hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(1), 0, s, level.p, q0.p, (int32_t)src);
+    hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, qcount.p, (int32_t)src);
     GX_TRY(check_launch("k_bfs_seed"));
-    uint32_t qsize = 1;
+    uint32_t qsize = 0;
+    GX_HIP_TRY(hipMemcpyAsync(&qsize, qcount.p, 4, hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    uint32_t nfront = 1;   // frontier vertices (direction heuristic)
     unsigned long long mf = (unsigned long long)(g->A.h_rp[src + 1] - g->A.h_rp[src]);
     unsigned long long mu = g->nnz;
     bool bottom_up = false;

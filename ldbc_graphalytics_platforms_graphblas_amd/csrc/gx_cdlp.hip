@@ -11,6 +11,8 @@
 // are written (cdlp_kernel.cu:108-112, 1060-1063).
 //   deg <= 64        : one wave per vertex, labels in registers, counts by 64 shuffles.
 //   deg <= kLdsHash/2: one wave per vertex, open-addressing hash table in that wave's LDS.
+//   deg <= 8192      : one 1024-thread workgroup per vertex, 16K-slot hash table in LDS
+//                      (workgroups loop over the medium-vertex list, one per CU).
 //   larger           : one workgroup per vertex, hash table in a global-memory segment
 //                      (2*deg rounded up to a power of two slots, cleared per iteration).
 // The winner is the maximum of the 64-bit key (count << 32) | ~label, i.e. the highest
@@ -191,6 +193,72 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_heavy(CdlpArgs a, const int
     }
 }
 
+// Medium vertices (kLdsHash/2 < deg <= kMidMax): one 1024-thread workgroup per vertex with a
+// 16K-slot hash table in LDS (128 KiB, one workgroup per CU); workgroups loop over the
+// medium-vertex list so the table is reused without a relaunch.
+constexpr int kMidBlock = 1024;
+constexpr int kMidSlots = 16384;
+constexpr int64_t kMidMax = kMidSlots / 2;
+
+__global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_t *__restrict__ mv, int32_t nmid) {
+    __shared__ uint32_t K[kMidSlots];
+    __shared__ uint32_t C[kMidSlots];
+    __shared__ unsigned long long red[kMidBlock / kWave];
+    const int tid = threadIdx.x;
+    bool any = false;
+    for (int32_t i = blockIdx.x; i < nmid; i += gridDim.x) {
+        const int64_t v = mv[i];
+        const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
+        int64_t ib = 0, id = 0;
+        if (a.rpT) {
+            ib = a.rpT[v];
+            id = a.rpT[v + 1] - ib;
+        }
+        const int64_t d = od + id;
+        int log2ts = 1;
+        while ((1ll << log2ts) < 2 * d) log2ts++;
+        const int ts = 1 << log2ts;
+        for (int s = tid; s < ts; s += kMidBlock) {
+            K[s] = kEmpty;
+            C[s] = 0;
+        }
+        __syncthreads();
+        for (int64_t k = tid; k < d; k += kMidBlock) {
+            const uint32_t l = (uint32_t)label_at(a, ob, od, ib, k);
+            uint32_t h = hash_slot(l, log2ts);
+            for (;;) {
+                const uint32_t prev = atomicCAS(&K[h], kEmpty, l);
+                if (prev == kEmpty || prev == l) {
+                    atomicAdd(&C[h], 1u);
+                    break;
+                }
+                h = (h + 1) & (ts - 1);
+            }
+        }
+        __syncthreads();
+        unsigned long long key = 0;
+        for (int s = tid; s < ts; s += kMidBlock) {
+            const uint32_t c = C[s];
+            if (c) {
+                const unsigned long long kk = pack(c, K[s]);
+                key = kk > key ? kk : key;
+            }
+        }
+        key = wave_max_u64(key);
+        if ((tid & (kWave - 1)) == 0) red[tid / kWave] = key;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long m = red[0];
+            for (int w = 1; w < kMidBlock / kWave; w++) m = red[w] > m ? red[w] : m;
+            const int32_t best = (int32_t)(kEmpty - (uint32_t)(m & 0xffffffffu));
+            a.nxt[v] = best;
+            any |= best != a.lab[v];
+        }
+        __syncthreads();   // the table is cleared for the next vertex
+    }
+    if (any) *a.changed = 1;
+}
+
 __global__ void k_cdlp_iota(int32_t *a, int64_t n) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
          v += (int64_t)gridDim.x * blockDim.x)
@@ -212,14 +280,16 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     if (n == 0) return GX_SUCCESS;
     GX_TRY(device_begin(ctx));
     if (g->directed) GX_TRY(ensure_transpose(g));
-    // heavy vertices and their global hash segments
-    std::vector<int32_t> hv, hl;
+    // medium vertices (LDS table per workgroup) and huge ones (global hash segments)
+    std::vector<int32_t> hv, hl, mv;
     std::vector<int64_t> hoff;
     int64_t total = 0;
     for (int64_t v = 0; v < n; v++) {
         int64_t d = g->A.h_rp[v + 1] - g->A.h_rp[v];
         if (g->directed) d += g->AT.h_rp[v + 1] - g->AT.h_rp[v];
-        if (d > kLdsHash / 2) {
+        if (d > kLdsHash / 2 && d <= kMidMax) {
+            mv.push_back((int32_t)v);
+        } else if (d > kMidMax) {
             int l2 = 1;
             while ((1ll << l2) < 2 * d) l2++;
             hv.push_back((int32_t)v);
@@ -228,7 +298,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             total += 1ll << l2;
         }
     }
-    DBuf<int32_t> la, lb, d_hv, d_hl;
+    DBuf<int32_t> la, lb, d_hv, d_hl, d_mv;
     DBuf<int64_t> d_hoff;
     DBuf<uint32_t> gk, gc;
     DBuf<int> changed;
@@ -245,6 +315,11 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         GX_HIP_TRY(hipMemcpyAsync(d_hl.p, hl.data(), hl.size() * 4, hipMemcpyHostToDevice, s));
         GX_HIP_TRY(hipMemcpyAsync(d_hoff.p, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, s));
     }
+    if (!mv.empty()) {
+        GX_TRY(d_mv.alloc(mv.size()));
+        GX_HIP_TRY(hipMemcpyAsync(d_mv.p, mv.data(), mv.size() * 4, hipMemcpyHostToDevice, s));
+    }
+    const unsigned mid_grid = (unsigned)std::min<size_t>(mv.size(), (size_t)std::max(1, ctx->num_cus));
     hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, la.p, n);
     GX_TRY(check_launch("k_cdlp_iota"));
     int32_t *cur = la.p, *nxt = lb.p;
@@ -258,6 +333,11 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                                dim3(kCdlpBlock), 0, s, a);
         }
         GX_TRY(check_launch("k_cdlp_light"));
+        if (!mv.empty()) {
+            KTimer kt(ctx, "cdlp_mid", s);
+            hipLaunchKernelGGL(k_cdlp_mid, dim3(mid_grid), dim3(kMidBlock), 0, s, a, d_mv.p, (int32_t)mv.size());
+            GX_TRY(check_launch("k_cdlp_mid"));
+        }
         if (!hv.empty()) {
             KTimer kt(ctx, "cdlp_heavy", s);
             hipLaunchKernelGGL(k_cdlp_heavy, dim3((unsigned)hv.size()), dim3(kCdlpBlock), 0, s, a, d_hv.p,
