@@ -67,6 +67,9 @@ DEFAULT_GRAPH = {"pr": "SYN-7_5", "cdlp": "SYN-7_5", "bfs": "SYN-g500-22", "wcc"
                  "sssp": "SYN-8_5", "lcc": "SYN-cit"}
 DOMINANT = {"bfs": "bfs_topdown", "wcc": "wcc_hook", "sssp": "sssp_relax", "cdlp": "cdlp_light",
             "lcc": "lcc_triangles"}
+KERNELS = {"bfs": ["bfs_topdown", "bfs_bottomup"], "wcc": ["wcc_hook", "wcc_compress"],
+           "sssp": ["sssp_relax"], "cdlp": ["cdlp_light", "cdlp_mid", "cdlp_heavy"],
+           "lcc": ["lcc_triangles"]}
 
 
 def run_algorithm(args):
@@ -117,6 +120,8 @@ def run_algorithm(args):
     wall = time.perf_counter() - t1
     ctx.set_kernel_timing(False)
     kl, kms = ctx.kernel_stats(DOMINANT[alg])
+    per_kernel = {k: dict(zip(("launches", "ms_per_run"), (lambda t: (t[0], t[1] / max(1, args.steps)))(
+        ctx.kernel_stats(k)))) for k in KERNELS[alg]}
     t_dev = float(np.median(dev_ms)) / 1e3
     # work units and algorithmic bytes (SURVEY.md 8d / BASELINE.md)
     nnz_eff = nnz * (2 if (alg == "cdlp" and directed) else 1)
@@ -172,7 +177,8 @@ def run_algorithm(args):
         "roofline": {"kernel": f"{alg} (whole device time)", "dominant_kernel": DOMINANT[alg], "bound": "hbm",
                      "achieved": nbytes / t_dev / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": nbytes / t_dev / 1e9 / HBM_PEAK_GBS, "traffic": None, "bytes_per_run": nbytes,
-                     "dominant_kernel_ms_per_run": kms / max(1, args.steps), "dominant_launches": kl},
+                     "dominant_kernel_ms_per_run": kms / max(1, args.steps), "dominant_launches": kl,
+                     "kernels": per_kernel},
         "cpu_baseline": cpu, "parity_vs_oracle": parity, "first_call_ms": first_ms,
         "wall_ms_per_call_incl_d2h": wall * 1e3 / args.steps, "graph_gen_s": t_gen,
     }

@@ -156,7 +156,6 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     uint32_t qsize = 0;
     GX_HIP_TRY(hipMemcpyAsync(&qsize, qcount.p, 4, hipMemcpyDeviceToHost, s));
     GX_HIP_TRY(hipStreamSynchronize(s));
-    uint32_t nfront = 1;   // frontier vertices (direction heuristic)
     unsigned long long mf = (unsigned long long)(g->A.h_rp[src + 1] - g->A.h_rp[src]);
     unsigned long long mu = g->nnz;
     bool bottom_up = false;
