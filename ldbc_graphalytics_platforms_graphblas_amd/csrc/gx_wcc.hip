@@ -9,6 +9,8 @@
 //   compress : pointer jumping until every vertex points at its root.
 // parent[v] <= v always holds, so the root of each final tree is the smallest vertex index
 // of the component: comp[v] is canonical and equals the oracle's union-find labels exactly.
+#include <algorithm>
+
 #include "gx_device.h"
 
 namespace gx {
@@ -62,6 +64,54 @@ __global__ __launch_bounds__(kWccBlock) void k_wcc_compress(int32_t *parent, int
     }
 }
 
+// Afforest link (Sutton et al., IPDPS'18): hook the higher of the two roots below the lower
+// one with a CAS; parent[x] <= x is kept, so roots stay component minima.
+__device__ __forceinline__ void link(int32_t *parent, int32_t u, int32_t v) {
+    int32_t p1 = __hip_atomic_load(&parent[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int32_t p2 = __hip_atomic_load(&parent[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (p1 != p2) {
+        const int32_t high = max(p1, p2), low = min(p1, p2);
+        const int32_t ph = __hip_atomic_load(&parent[high], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ph == low) break;
+        if (ph == high && atomicCAS(&parent[high], high, low) == high) break;
+        p1 = __hip_atomic_load(&parent[ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        p2 = __hip_atomic_load(&parent[low], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Afforest sampling round r: link every vertex with its r-th neighbour.
+__global__ __launch_bounds__(kWccBlock) void k_afforest_sample(const int64_t *__restrict__ rp,
+                                                               const int32_t *__restrict__ ci, int64_t n,
+                                                               int r, int32_t *parent) {
+    for (int64_t v = (int64_t)blockIdx.x * kWccBlock + threadIdx.x; v < n;
+         v += (int64_t)gridDim.x * kWccBlock) {
+        const int64_t k = rp[v] + r;
+        if (k < rp[v + 1]) link(parent, (int32_t)v, ci[k]);
+    }
+}
+
+// Afforest finish: every vertex outside the sampled giant component links all its remaining
+// neighbours (undirected graphs store every edge at both endpoints, so an edge between the
+// giant component and another vertex is seen from the other vertex).  One wave per vertex.
+__global__ __launch_bounds__(kWccBlock) void k_afforest_finish(const int64_t *__restrict__ rp,
+                                                               const int32_t *__restrict__ ci, int64_t n,
+                                                               int skip, int32_t giant, int32_t *parent) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t w0 = ((int64_t)blockIdx.x * kWccBlock + threadIdx.x) / kWave;
+    const int64_t nw = (int64_t)gridDim.x * (kWccBlock / kWave);
+    for (int64_t v = w0; v < n; v += nw) {
+        const int64_t b = rp[v] + skip, e = rp[v + 1];
+        if (b >= e) continue;
+        if (find_root(parent, (int32_t)v) == giant) continue;
+        for (int64_t k = b + lane; k < e; k += kWave) link(parent, (int32_t)v, ci[k]);
+    }
+}
+
+__global__ void k_sample_roots(const int32_t *parent, const int32_t *__restrict__ ids, int m, int32_t *roots) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x)
+        roots[i] = find_root(parent, ids[i]);
+}
+
 __global__ void k_iota(int32_t *a, int64_t n) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
          v += (int64_t)gridDim.x * blockDim.x)
@@ -87,9 +137,66 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
     GX_TRY(device_begin(ctx));
     hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, parent.p, n);
     GX_TRY(check_launch("k_iota"));
+    const unsigned vgrid = grid_for(n, kWccBlock, 8192);
+    if (!g->directed && nnz) {
+        // ---- Afforest: sample two neighbours per vertex, find the giant component from
+        // 1024 sampled roots, then link only the remaining edges of the other vertices.
+        for (int r = 0; r < 2; r++) {
+            {
+                KTimer kt(ctx, "wcc_sample", s);
+                hipLaunchKernelGGL(k_afforest_sample, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, r,
+                                   parent.p);
+            }
+            GX_TRY(check_launch("k_afforest_sample"));
+            {
+                KTimer kt(ctx, "wcc_compress", s);
+                hipLaunchKernelGGL(k_wcc_compress, dim3(vgrid), dim3(kWccBlock), 0, s, parent.p, n);
+            }
+            GX_TRY(check_launch("k_wcc_compress"));
+        }
+        constexpr int kSamples = 1024;
+        std::vector<int32_t> ids(kSamples), roots(kSamples);
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (int i = 0; i < kSamples; i++) {
+            h ^= h >> 31;
+            h *= 0xBF58476D1CE4E5B9ull;
+            h ^= h >> 29;
+            ids[i] = (int32_t)(h % (uint64_t)n);
+        }
+        DBuf<int32_t> d_ids, d_roots;
+        GX_TRY(d_ids.alloc(kSamples));
+        GX_TRY(d_roots.alloc(kSamples));
+        GX_HIP_TRY(hipMemcpyAsync(d_ids.p, ids.data(), kSamples * 4, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_sample_roots, dim3(4), dim3(256), 0, s, parent.p, d_ids.p, kSamples, d_roots.p);
+        GX_TRY(check_launch("k_sample_roots"));
+        GX_HIP_TRY(hipMemcpyAsync(roots.data(), d_roots.p, kSamples * 4, hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+        std::sort(roots.begin(), roots.end());
+        int32_t giant = roots[0];
+        int best = 0;
+        for (int i = 0, j; i < kSamples; i = j) {
+            for (j = i; j < kSamples && roots[j] == roots[i]; j++) {
+            }
+            if (j - i > best) {
+                best = j - i;
+                giant = roots[i];
+            }
+        }
+        {
+            KTimer kt(ctx, "wcc_hook", s);
+            hipLaunchKernelGGL(k_afforest_finish, dim3(grid_for((uint64_t)n * kWave, kWccBlock, 8192)),
+                               dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, 2, giant, parent.p);
+        }
+        GX_TRY(check_launch("k_afforest_finish"));
+        {
+            KTimer kt(ctx, "wcc_compress", s);
+            hipLaunchKernelGGL(k_wcc_compress, dim3(vgrid), dim3(kWccBlock), 0, s, parent.p, n);
+        }
+        GX_TRY(check_launch("k_wcc_compress"));
+    }
     const unsigned hook_grid =
         grid_for((uint64_t)((nnz + kWccEdgesPerThread - 1) / kWccEdgesPerThread), kWccBlock, 1u << 30);
-    for (int round = 0;; round++) {
+    for (int round = 0; g->directed; round++) {
         int h_changed = 0;
         GX_HIP_TRY(hipMemsetAsync(changed.p, 0, sizeof(int), s));
         if (nnz) {
