@@ -13,8 +13,9 @@
 //   deg <= kLdsHash/2: one wave per vertex, open-addressing hash table in that wave's LDS.
 //   deg <= 8192      : one 1024-thread workgroup per vertex, 16K-slot hash table in LDS
 //                      (workgroups loop over the medium-vertex list, one per CU).
-//   larger           : one workgroup per vertex, hash table in a global-memory segment
-//                      (2*deg rounded up to a power of two slots, cleared per iteration).
+//   larger           : 4096-label chunks histogrammed in LDS by separate workgroups, merged
+//                      into a per-vertex global table (2*deg slots, cleared per iteration),
+//                      then one reduce workgroup per vertex.
 // The winner is the maximum of the 64-bit key (count << 32) | ~label, i.e. the highest
 // count and among equal counts the smallest label.
 #include <algorithm>
@@ -137,47 +138,85 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a) {
     if (any) *a.changed = 1;
 }
 
-__global__ __launch_bounds__(kCdlpBlock) void k_cdlp_heavy(CdlpArgs a, const int32_t *__restrict__ hv,
-                                                           const int64_t *__restrict__ hoff,
-                                                           const int32_t *__restrict__ hlog2,
-                                                           uint32_t *gkeys, uint32_t *gcnts) {
-    __shared__ unsigned long long red[kCdlpBlock / kWave];
-    const int64_t v = hv[blockIdx.x];
-    const int log2ts = hlog2[blockIdx.x];
-    const int64_t ts = 1ll << log2ts;
-    uint32_t *K = gkeys + hoff[blockIdx.x];
-    uint32_t *C = gcnts + hoff[blockIdx.x];
-    for (int64_t s = threadIdx.x; s < ts; s += kCdlpBlock) {
-        __hip_atomic_store(&K[s], kEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&C[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
+// Huge vertices (deg > kMidMax): the label multiset is cut into kHugeChunk-label chunks; a
+// 1024-thread workgroup histograms one chunk in a 64 KiB LDS table, then adds each distinct
+// label once into the vertex's global table (device-scope CAS + atomicAdd), so global
+// atomics scale with distinct labels per chunk, not with the degree.
+constexpr int kHugeBlock = 1024;
+constexpr int kHugeChunk = 4096;
+constexpr int kHugeSlots = 2 * kHugeChunk;
+
+__global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, const int32_t *__restrict__ hv,
+                                                                 const int64_t *__restrict__ hoff,
+                                                                 const int32_t *__restrict__ hlog2,
+                                                                 const int32_t *__restrict__ cvert,
+                                                                 const int64_t *__restrict__ cbeg,
+                                                                 uint32_t *gkeys, uint32_t *gcnts) {
+    __shared__ uint32_t K[kHugeSlots];
+    __shared__ uint32_t C[kHugeSlots];
+    constexpr int kLog2 = 13;   // log2(kHugeSlots)
+    const int tid = threadIdx.x;
+    const int32_t hi = cvert[blockIdx.x];
+    const int64_t v = hv[hi];
     const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
     int64_t ib = 0, id = 0;
     if (a.rpT) {
         ib = a.rpT[v];
         id = a.rpT[v + 1] - ib;
     }
-    const int64_t d = od + id;
-    for (int64_t k = threadIdx.x; k < d; k += kCdlpBlock) {
+    const int64_t k0 = cbeg[blockIdx.x], k1 = min(k0 + kHugeChunk, od + id);
+    for (int s = tid; s < kHugeSlots; s += kHugeBlock) {
+        K[s] = kEmpty;
+        C[s] = 0;
+    }
+    __syncthreads();
+    for (int64_t k = k0 + tid; k < k1; k += kHugeBlock) {
         const uint32_t l = (uint32_t)label_at(a, ob, od, ib, k);
-        int64_t h = hash_slot(l, log2ts);
+        uint32_t h = hash_slot(l, kLog2);
         for (;;) {
             const uint32_t prev = atomicCAS(&K[h], kEmpty, l);
             if (prev == kEmpty || prev == l) {
                 atomicAdd(&C[h], 1u);
                 break;
             }
-            h = (h + 1) & (ts - 1);
+            h = (h + 1) & (kHugeSlots - 1);
         }
     }
     __syncthreads();
+    const int log2ts = hlog2[hi];
+    const int64_t ts = 1ll << log2ts;
+    uint32_t *GK = gkeys + hoff[hi];
+    uint32_t *GC = gcnts + hoff[hi];
+    for (int s = tid; s < kHugeSlots; s += kHugeBlock) {
+        const uint32_t c = C[s];
+        if (!c) continue;
+        const uint32_t l = K[s];
+        int64_t h = hash_slot(l, log2ts);
+        for (;;) {
+            const uint32_t prev = atomicCAS(&GK[h], kEmpty, l);
+            if (prev == kEmpty || prev == l) {
+                atomicAdd(&GC[h], c);
+                break;
+            }
+            h = (h + 1) & (ts - 1);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_reduce(CdlpArgs a, const int32_t *__restrict__ hv,
+                                                                 const int64_t *__restrict__ hoff,
+                                                                 const int32_t *__restrict__ hlog2,
+                                                                 const uint32_t *gkeys, const uint32_t *gcnts) {
+    __shared__ unsigned long long red[kHugeBlock / kWave];
+    const int64_t v = hv[blockIdx.x];
+    const int64_t ts = 1ll << hlog2[blockIdx.x];
+    const uint32_t *GK = gkeys + hoff[blockIdx.x];
+    const uint32_t *GC = gcnts + hoff[blockIdx.x];
     unsigned long long key = 0;
-    for (int64_t s = threadIdx.x; s < ts; s += kCdlpBlock) {
-        const uint32_t c = __hip_atomic_load(&C[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int64_t s = threadIdx.x; s < ts; s += kHugeBlock) {
+        const uint32_t c = GC[s];
         if (c) {
-            const uint32_t l = __hip_atomic_load(&K[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long kk = pack(c, l);
+            const unsigned long long kk = pack(c, GK[s]);
             key = kk > key ? kk : key;
         }
     }
@@ -186,7 +225,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_heavy(CdlpArgs a, const int
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long m = red[0];
-        for (int w = 1; w < kCdlpBlock / kWave; w++) m = red[w] > m ? red[w] : m;
+        for (int w = 1; w < kHugeBlock / kWave; w++) m = red[w] > m ? red[w] : m;
         const int32_t best = (int32_t)(kEmpty - (uint32_t)(m & 0xffffffffu));
         a.nxt[v] = best;
         if (best != a.lab[v]) *a.changed = 1;
@@ -282,7 +321,8 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     if (g->directed) GX_TRY(ensure_transpose(g));
     // medium vertices (LDS table per workgroup) and huge ones (global hash segments)
     std::vector<int32_t> hv, hl, mv;
-    std::vector<int64_t> hoff;
+    std::vector<int64_t> hoff, cbeg;
+    std::vector<int32_t> cvert;
     int64_t total = 0;
     for (int64_t v = 0; v < n; v++) {
         int64_t d = g->A.h_rp[v + 1] - g->A.h_rp[v];
@@ -292,6 +332,10 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         } else if (d > kMidMax) {
             int l2 = 1;
             while ((1ll << l2) < 2 * d) l2++;
+            for (int64_t c = 0; c < d; c += kHugeChunk) {
+                cvert.push_back((int32_t)hv.size());
+                cbeg.push_back(c);
+            }
             hv.push_back((int32_t)v);
             hl.push_back(l2);
             hoff.push_back(total);
@@ -299,7 +343,8 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         }
     }
     DBuf<int32_t> la, lb, d_hv, d_hl, d_mv;
-    DBuf<int64_t> d_hoff;
+    DBuf<int64_t> d_hoff, d_cbeg;
+    DBuf<int32_t> d_cvert;
     DBuf<uint32_t> gk, gc;
     DBuf<int> changed;
     GX_TRY(la.alloc(n));
@@ -314,6 +359,10 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         GX_HIP_TRY(hipMemcpyAsync(d_hv.p, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, s));
         GX_HIP_TRY(hipMemcpyAsync(d_hl.p, hl.data(), hl.size() * 4, hipMemcpyHostToDevice, s));
         GX_HIP_TRY(hipMemcpyAsync(d_hoff.p, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, s));
+        GX_TRY(d_cvert.alloc(cvert.size()));
+        GX_TRY(d_cbeg.alloc(cbeg.size()));
+        GX_HIP_TRY(hipMemcpyAsync(d_cvert.p, cvert.data(), cvert.size() * 4, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(d_cbeg.p, cbeg.data(), cbeg.size() * 8, hipMemcpyHostToDevice, s));
     }
     if (!mv.empty()) {
         GX_TRY(d_mv.alloc(mv.size()));
@@ -340,9 +389,14 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         }
         if (!hv.empty()) {
             KTimer kt(ctx, "cdlp_heavy", s);
-            hipLaunchKernelGGL(k_cdlp_heavy, dim3((unsigned)hv.size()), dim3(kCdlpBlock), 0, s, a, d_hv.p,
+            GX_HIP_TRY(hipMemsetAsync(gk.p, 0xff, (size_t)total * 4, s));
+            GX_HIP_TRY(hipMemsetAsync(gc.p, 0, (size_t)total * 4, s));
+            hipLaunchKernelGGL(k_cdlp_huge_insert, dim3((unsigned)cvert.size()), dim3(kHugeBlock), 0, s, a, d_hv.p,
+                               d_hoff.p, d_hl.p, d_cvert.p, d_cbeg.p, gk.p, gc.p);
+            GX_TRY(check_launch("k_cdlp_huge_insert"));
+            hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)hv.size()), dim3(kHugeBlock), 0, s, a, d_hv.p,
                                d_hoff.p, d_hl.p, gk.p, gc.p);
-            GX_TRY(check_launch("k_cdlp_heavy"));
+            GX_TRY(check_launch("k_cdlp_huge_reduce"));
         }
         int h_changed = 0;
         GX_HIP_TRY(hipMemcpyAsync(&h_changed, changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
