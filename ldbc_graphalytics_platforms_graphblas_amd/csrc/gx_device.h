@@ -110,6 +110,7 @@ struct gx_graph {
     gx::DevCSR A, AT, S;
     gx::DBuf<int32_t> outdeg;   // out-degree of every vertex (PR)
     gx::PrPart *pr = nullptr;   // cached single-rank PageRank plan
+    double mean_w = -1.0;       // cached mean edge weight (SSSP bucket width), < 0 = not yet computed
 };
 
 namespace gx {

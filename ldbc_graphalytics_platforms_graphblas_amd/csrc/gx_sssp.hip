@@ -1,15 +1,32 @@
-// gx_sssp.hip -- single-source shortest paths, frontier Bellman-Ford (min.plus relaxations).
+// gx_sssp.hip -- single-source shortest paths by device-scheduled delta-stepping (min.plus).
 //
 // Replaces LA_SSSP -> diagonal fill + LAGraph_Cached_EMin + LAGr_SingleSourceShortestPath
 // with delta = 2.5 (sssp.cpp:53-81).  The zero diagonal the reference inserts cannot change a
 // distance and is not materialised.
 // Distances are non-negative fp64 kept as their IEEE bit patterns, whose unsigned order is
-// the numeric order, so a relaxation is one 64-bit atomicMin.  Every round relaxes the
-// out-edges of the vertices improved in the previous round (one wave per frontier vertex);
-// a per-round stamp puts a vertex into the next frontier once.  The fixed point is the
-// minimum over paths of the left-to-right fp64 path sum -- the same value Dijkstra and
-// delta-stepping produce -- so the result is bitwise equal to the oracle.
+// the numeric order, so a relaxation is one 64-bit atomicMin.  Every improvement re-queues
+// its vertex, so the loop ends at the relaxation fixed point: the minimum over paths of the
+// left-to-right fp64 path sum, the value Dijkstra produces -- bitwise equal to the oracle
+// whatever delta or the relaxation order.
+//
+// Buckets (delta-stepping, Meyer & Sanders; GPU bucket ring after Davidson et al. and ADDS):
+//   bucket(d) = floor(d / delta); `cur` is the bucket being settled.
+//   near    : work items (vertex << 32 | 256-edge chunk) of vertices in buckets <= cur,
+//             one wave per item, ping-ponged between rounds;
+//   ring    : kRing vertex lists for the buckets cur+1 .. win_base+kRing-1 (deduplicated by
+//             a per-vertex bucket stamp);
+//   overflow: vertices beyond the ring window, split into a new window when the ring empties.
+//   relaxed[v] = largest source distance any chunk of v was relaxed with since v was last
+//             queued; a bucket entry whose distance equals it was already relaxed and is
+//             skipped (removes the near/far double processing).
+// Scheduling runs on the device: a one-thread plan kernel reads the queue counts and picks
+// the next action (relax / open the next ring bucket / split the overflow / done), so the
+// host launches plan -> advance -> relax triples in batches and syncs once per batch.
+#include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #include "gx_device.h"
 
@@ -17,58 +34,484 @@ namespace gx {
 namespace {
 
 constexpr int kSsspBlock = 256;
+constexpr int kChunk = 256;
+constexpr int kRing = 32;
+constexpr uint32_t kOob = 0x80000000u;   // buffer offset past every record: the lane is dropped
+constexpr int64_t kMaxBufVertices = (int64_t)(kOob / 8u);   // dist[] must stay below kOob bytes
 
 __device__ __forceinline__ unsigned long long dbits(double d) {
     return (unsigned long long)__double_as_longlong(d);
 }
+__device__ __forceinline__ double bitsd(unsigned long long b) { return __longlong_as_double((long long)b); }
 
-__global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(const int64_t *__restrict__ rp,
-                                                           const int32_t *__restrict__ ci,
-                                                           const double *__restrict__ w,
-                                                           const int32_t *__restrict__ qin,
-                                                           uint32_t qsize, unsigned long long *dist,
-                                                           int32_t *stamp, int32_t round,
-                                                           int32_t *qout, uint32_t *qcount) {
+__device__ __forceinline__ uint32_t chunks_of(int64_t deg) { return (uint32_t)((deg + kChunk - 1) / kChunk); }
+
+__device__ __forceinline__ int64_t bucket_of(double d, double inv_delta) {
+    const double q = d * inv_delta;
+    return q < 4.0e18 ? (int64_t)q : (int64_t)4000000000000000000ll;
+}
+
+struct SsspState {
+    int64_t cur;                  // bucket being settled
+    int64_t win_base;             // ring window [win_base, win_base + kRing)
+    unsigned long long ovf_minb;  // lower bound on the buckets in the overflow
+    int32_t round;                // near queue q[round & 1] is relaxed this step
+    int32_t done;
+    int32_t epoch;                // relaxations append to overflow[epoch & 1]
+    int32_t mode;                 // advance: 0 none, 1 open ring slot, 2 split overflow, 3 heavy items
+    int32_t heavy;                // relax phase: 0 light edges, 1 heavy edges
+    int32_t slot;                 // ring slot opened (mode 1)
+    int32_t consume;              // ring slot to clear at the next plan, -1 none
+    int32_t split_src;            // overflow list being split (mode 2)
+    uint32_t qcnt[2];
+    uint32_t ovf_cnt[2];
+    uint32_t settled_cnt;         // vertices queued in the current bucket
+    uint32_t ring_cnt[kRing];
+};
+
+struct SsspBufs {
+    const int64_t *rp;
+    const int32_t *ci;
+    const double *w;
+    unsigned long long *dist;
+    unsigned long long *relaxed;  // distance all edges of v were last relaxed with
+    int32_t *near_stamp;          // round a vertex was last queued as near
+    int32_t *bstamp;              // bucket a vertex was last put into a ring slot for
+    int32_t *ostamp;              // overflow epoch a vertex was last put on the overflow
+    int32_t *sstamp;              // bucket a vertex was last put on the settled list for
+    uint64_t *q[2];               // near work items
+    int32_t *ring;                // kRing slots of ring_cap vertices
+    int32_t *ovf[2];
+    int32_t *settled;             // vertices of the current bucket (heavy edges pending)
+    uint64_t ring_cap;
+    double delta, inv_delta;
+    SsspState *st;
+    unsigned long long *stats;    // GX_SSSP_VERBOSE work counters, else null
+};
+
+// stats slots: 0 items, 1 edges scanned, 2 relaxations tried, 3 improvements, 4 near pushes,
+// 5 ring pushes, 6 overflow pushes, 7 bucket entries skipped as already relaxed
+__device__ __forceinline__ void wave_count(unsigned long long *stats, int slot, unsigned long long x) {
+    if (!stats) return;
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0 && x) atomicAdd(&stats[slot], x);
+}
+
+// wave-aggregated append of `k` consecutive items (vertex << 32 | j) per lane
+__device__ __forceinline__ void wave_append_items(uint32_t k, int32_t v, uint64_t *queue, uint32_t *qcount) {
     const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = (blockIdx.x * kSsspBlock + threadIdx.x) / kWave;
-    const uint32_t nwaves = gridDim.x * (kSsspBlock / kWave);
-    for (uint32_t f = wave; f < qsize; f += nwaves) {
-        const int32_t u = qin[f];
-        const double du = __longlong_as_double((long long)__hip_atomic_load(
-            &dist[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        const int64_t b = rp[u], e = rp[u + 1];
-        for (int64_t k0 = b; k0 < e; k0 += kWave) {
-            const int64_t k = k0 + lane;
-            bool take = false;
-            int32_t v = 0;
-            if (k < e) {
-                v = ci[k];
-                const unsigned long long nd = dbits(du + w[k]);
-                if (nd < __hip_atomic_load(&dist[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    const unsigned long long old = atomicMin(&dist[v], nd);
-                    if (nd < old && atomicExch(&stamp[v], round) != round) take = true;
-                }
-            }
-            const uint64_t mask = __ballot(take);
-            if (mask) {
-                const int leader = __ffsll((unsigned long long)mask) - 1;
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(qcount, (uint32_t)__popcll(mask));
-                base = __shfl(base, leader, kWave);
-                if (take) qout[base + __popcll(mask & ((1ull << lane) - 1))] = v;
-            }
-        }
+    uint32_t x = k;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, kWave);
+        if (lane >= off) x += y;
+    }
+    const uint32_t total = __shfl(x, kWave - 1, kWave);
+    if (total == 0) return;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(qcount, total);
+    base = __shfl(base, 0, kWave);
+    const uint32_t excl = x - k;
+    for (uint32_t j = 0; j < k; j++) queue[base + excl + j] = ((uint64_t)(uint32_t)v << 32) | j;
+}
+
+__device__ __forceinline__ void wave_append_vertex(bool take, int32_t v, int32_t *list, uint32_t *count) {
+    const uint64_t mask = __ballot(take);
+    if (mask == 0) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader, kWave);
+    if (take) list[base + __popcll(mask & ((1ull << lane) - 1))] = v;
+}
+
+// append v to ring slot `slot`; lanes are grouped by slot, one atomic per distinct slot
+__device__ __forceinline__ void wave_append_ring(bool take, int slot, int32_t v, const SsspBufs &B) {
+    const int lane = threadIdx.x & (kWave - 1);
+    uint64_t pending = __ballot(take);
+    while (pending) {
+        const int leader = __ffsll((unsigned long long)pending) - 1;
+        const int s = __shfl(slot, leader, kWave);
+        const uint64_t grp = __ballot(take && slot == s);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&B.st->ring_cnt[s], (uint32_t)__popcll(grp));
+        base = __shfl(base, leader, kWave);
+        if (take && slot == s) B.ring[(uint64_t)s * B.ring_cap + base + __popcll(grp & ((1ull << lane) - 1))] = v;
+        pending &= ~grp;
     }
 }
 
-__global__ void k_sssp_init(unsigned long long *dist, int32_t *stamp, int64_t n, int32_t src,
-                            int32_t *queue) {
+__device__ __forceinline__ void wave_min_to(unsigned long long m, unsigned long long *dst) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off, kWave);
+        m = o < m ? o : m;
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0 && m != ~0ull) atomicMin(dst, m);
+}
+
+// Per-wave LDS staging of queue pushes.  Improvements are sparse (well under 1% of the
+// relaxations), so pushing them one wave-slot at a time costs one same-address global atomic
+// per push on the few queue counters -- those serialise in one L2 channel and dominated the
+// kernel.  Pushes are staged as (vertex, tag) in LDS and flushed kStage at a time, with one
+// global atomic per queue per flush.
+constexpr int kStage = 512;
+constexpr int kTagNear = kRing, kTagOvf = kRing + 1;   // tags 0..kRing-1 are ring slots
+
+struct Stage {
+    int32_t v[kStage];
+    uint32_t tag[kStage];   // bits 0-6 queue, bit 7 settled-list push, bits 8.. chunk count
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void stage_flush(Stage &sg, uint32_t &n, const SsspBufs &B, uint64_t *near_out,
+                                            uint32_t *near_count, int32_t *ovf, uint32_t *ovf_count) {
+    wave_lds_sync();
+    const int lane = threadIdx.x & (kWave - 1);
+    for (uint32_t base = 0; base < n; base += kWave) {
+        const uint32_t i = base + lane;
+        const bool valid = i < n;
+        const int32_t v = valid ? sg.v[i] : 0;
+        const uint32_t tag = valid ? sg.tag[i] : 0xFFu;
+        const uint32_t q = tag & 0x7Fu;
+        const bool near = valid && q == (uint32_t)kTagNear;
+        wave_append_items(near ? (tag >> 8) : 0u, v, near_out, near_count);
+        wave_append_vertex(near && (tag & 0x80u), v, B.settled, &B.st->settled_cnt);
+        wave_append_vertex(valid && q == (uint32_t)kTagOvf, v, ovf, ovf_count);
+        wave_append_ring(valid && q < (uint32_t)kRing, (int)q, v, B);
+    }
+    wave_lds_sync();
+    n = 0;
+}
+
+// One thread: choose this step's action from the queue counts.
+//   near non-empty           -> relax it (current phase)
+//   light phase drained      -> heavy phase: relax the heavy edges of the bucket's vertices
+//   heavy phase drained      -> open the next non-empty ring bucket, else split the overflow,
+//                               else done
+__global__ void k_sssp_plan(SsspState *st) {
+    if (st->done) {
+        st->mode = 0;
+        return;
+    }
+    const int32_t r = ++st->round;
+    if (st->consume >= 0) {
+        st->ring_cnt[st->consume] = 0;
+        st->consume = -1;
+    }
+    const int qin = r & 1;
+    st->qcnt[qin ^ 1] = 0;
+    st->mode = 0;
+    if (st->qcnt[qin] > 0) return;
+    if (!st->heavy && st->settled_cnt > 0) {
+        st->heavy = 1;
+        st->mode = 3;
+        return;
+    }
+    st->heavy = 0;
+    st->settled_cnt = 0;
+    const int64_t lim = st->win_base + kRing;
+    for (int64_t b = st->cur + 1; b < lim; b++) {
+        const int s = (int)(b % kRing);
+        if (st->ring_cnt[s] > 0) {
+            st->cur = b;
+            st->mode = 1;
+            st->slot = s;
+            st->consume = s;
+            return;
+        }
+    }
+    const int src = st->epoch & 1;
+    if (st->ovf_cnt[src] > 0) {
+        st->split_src = src;
+        st->epoch++;
+        st->ovf_cnt[st->epoch & 1] = 0;
+        const int64_t mb = (int64_t)min(st->ovf_minb, 4000000000000000000ull);
+        st->win_base = max(st->cur + 1, mb);
+        st->cur = st->win_base - 1;
+        st->ovf_minb = ~0ull;
+        st->mode = 2;
+        return;
+    }
+    st->done = 1;
+}
+
+// Mode 1: turn the opened ring bucket into near items (and settled-list entries);
+// mode 2: split the overflow into the new ring window;
+// mode 3: emit heavy-phase items for the bucket's settled list and record the distance
+//         their edges are relaxed with.
+// Ring / overflow entries whose edges were all relaxed at their current distance are dropped.
+__global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
+    const SsspState *st = B.st;
+    const int mode = st->mode;
+    if (mode == 0) return;
+    const int32_t r = st->round;
+    const int qin = r & 1;
+    const int32_t *list;
+    uint32_t count;
+    if (mode == 1) {
+        list = B.ring + (uint64_t)st->slot * B.ring_cap;
+        count = st->ring_cnt[st->slot];
+    } else if (mode == 2) {
+        list = B.ovf[st->split_src];
+        count = st->ovf_cnt[st->split_src];
+    } else {
+        list = B.settled;
+        count = st->settled_cnt;
+    }
+    const int64_t cur = st->cur, win_base = st->win_base, lim = win_base + kRing;
+    const int32_t epoch = st->epoch;
+    unsigned long long mymin = ~0ull, n_skip = 0;
+    const uint32_t stride = gridDim.x * kSsspBlock;
+    const uint32_t nround = (count + stride - 1) / stride;
+    for (uint32_t it = 0; it < nround; it++) {
+        const uint32_t f = it * stride + blockIdx.x * kSsspBlock + threadIdx.x;
+        bool to_near = false, to_ring = false, to_ovf = false, to_set = false;
+        int32_t v = 0;
+        int slot = 0;
+        uint32_t nch = 0;
+        if (f < count) {
+            v = list[f];
+            const unsigned long long db = B.dist[v];
+            if (mode == 3) {
+                B.relaxed[v] = db;   // heavy edges now, light edges already relaxed at db
+                to_near = true;
+                nch = chunks_of(B.rp[v + 1] - B.rp[v]);
+            } else if (db == B.relaxed[v]) {
+                n_skip++;
+            } else if (mode == 1) {
+                // entries are unique within a slot: plain stores
+                B.near_stamp[v] = r;
+                B.sstamp[v] = (int32_t)cur;
+                to_near = to_set = true;
+                nch = chunks_of(B.rp[v + 1] - B.rp[v]);
+            } else {
+                const int64_t b = max(bucket_of(bitsd(db), B.inv_delta), win_base);
+                if (b < lim) {
+                    B.bstamp[v] = (int32_t)b;
+                    slot = (int)(b % kRing);
+                    to_ring = true;
+                } else {
+                    B.ostamp[v] = epoch;
+                    to_ovf = true;
+                    mymin = min(mymin, (unsigned long long)b);
+                }
+            }
+        }
+        if (mode != 2) {
+            wave_append_items(to_near ? nch : 0u, v, B.q[qin], &B.st->qcnt[qin]);
+            if (mode == 1) wave_append_vertex(to_set, v, B.settled, &B.st->settled_cnt);
+        } else {
+            wave_append_ring(to_ring, slot, v, B);
+            wave_append_vertex(to_ovf, v, B.ovf[epoch & 1], &B.st->ovf_cnt[epoch & 1]);
+        }
+    }
+    if (mode == 2) wave_min_to(mymin, &B.st->ovf_minb);
+    wave_count(B.stats, 7, n_skip);
+}
+
+// Relax the light (w < delta) or, in the heavy phase, the heavy out-edges of every near item;
+// improved targets go to the next near queue, a ring slot or the overflow by their new bucket.
+// Heavy relaxations always land past the current bucket (forced there if rounding says
+// otherwise), so the heavy phase is a single round per bucket.
+// Load-balanced waves: a wave takes 64 items (one per lane), scans their edge counts and then
+// walks the concatenated edge range 64 x kSlots edges at a time, every lane finding the item
+// that owns its edge by a 6-step binary search over the scanned counts.  All lanes stay busy
+// whatever the degrees, and each lane keeps kSlots independent gather chains in flight.
+__global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
+    constexpr int kSlots = 4;
+    const SsspState *st = B.st;
+    const int32_t r = st->round;
+    const int qin = r & 1;
+    const uint32_t count = st->qcnt[qin];
+    if (count == 0) return;
+    const bool heavy = st->heavy != 0;
+    const int64_t cur = st->cur, lim = st->win_base + kRing;
+    const int32_t epoch = st->epoch, rn = r + 1, cur32 = (int32_t)cur;
+    const double delta = B.delta;
+    const uint64_t *near_in = B.q[qin];
+    uint64_t *near_out = B.q[qin ^ 1];
+    uint32_t *near_count = &B.st->qcnt[qin ^ 1];
+    int32_t *ovf = B.ovf[epoch & 1];
+    uint32_t *ovf_count = &B.st->ovf_cnt[epoch & 1];
+    const __amdgpu_buffer_rsrc_t dist_r =
+        __builtin_amdgcn_make_buffer_rsrc(B.dist, (short)0, (int)(B.ring_cap * 8u), 0x00020000);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = (blockIdx.x * kSsspBlock + threadIdx.x) / kWave;
+    const uint32_t nwaves = gridDim.x * (kSsspBlock / kWave);
+    __shared__ Stage stages[kSsspBlock / kWave];
+    Stage &sg = stages[threadIdx.x / kWave];
+    uint32_t staged = 0;
+    unsigned long long mymin = ~0ull, c_items = 0, c_edges = 0, c_try = 0, c_impr = 0, c_near = 0, c_ring = 0,
+                       c_ovf = 0;
+    for (uint64_t base = (uint64_t)wave * kWave; base < count; base += (uint64_t)nwaves * kWave) {
+        const uint64_t idx = base + lane;
+        int64_t rs = 0;
+        int32_t sz = 0;
+        double du = 0.0;
+        if (idx < count) {
+            const uint64_t item = near_in[idx];
+            const int32_t u = (int32_t)(item >> 32);
+            rs = B.rp[u] + (int64_t)(uint32_t)item * kChunk;
+            sz = (int32_t)min(B.rp[u + 1] - rs, (int64_t)kChunk);
+            du = bitsd(__hip_atomic_load(&B.dist[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            c_items++;
+        }
+        int32_t incl = sz;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int32_t y = __shfl_up(incl, off, kWave);
+            if (lane >= off) incl += y;
+        }
+        const int32_t total = __shfl(incl, kWave - 1, kWave);
+        const int32_t excl = incl - sz;
+        for (int32_t e0 = 0; e0 < total; e0 += kWave * kSlots) {
+            int64_t k[kSlots];
+            double dsrc[kSlots], wk[kSlots];
+            int32_t v[kSlots];
+            unsigned long long cd[kSlots];
+            bool act[kSlots];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) {
+                const int32_t e_raw = e0 + q * kWave + lane;
+                act[q] = e_raw < total;
+                const int32_t e = act[q] ? e_raw : total - 1;   // keep the loads in range
+                int o = 0;
+#pragma unroll
+                for (int step = kWave / 2; step > 0; step >>= 1)
+                    if (__shfl(incl, o + step - 1, kWave) <= e) o += step;
+                k[q] = __shfl(rs, o, kWave) + (e - __shfl(excl, o, kWave));
+                dsrc[q] = __shfl(du, o, kWave);
+            }
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) wk[q] = B.w[k[q]];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) v[q] = B.ci[k[q]];
+            // edges of the other weight class (and idle slots) get an out-of-range offset: the
+            // buffer load drops them without a memory access or a branch.  A stale value only
+            // costs an extra atomicMin, it is never below the true distance.
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) {
+                const bool in_class = act[q] && (wk[q] >= delta) == heavy;
+                cd[q] = __builtin_bit_cast(unsigned long long,
+                                           __builtin_amdgcn_raw_buffer_load_b64(
+                                               dist_r, in_class ? (uint32_t)v[q] * 8u : kOob, 0, 0));
+            }
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) {
+                bool to_near = false, to_ring = false, to_ovf = false, to_set = false;
+                int slot = 0;
+                uint32_t nch = 0;
+                c_edges += act[q];
+                if (act[q] && (wk[q] >= delta) == heavy) {
+                    c_try++;
+                    const double nd = dsrc[q] + wk[q];
+                    const unsigned long long ndb = dbits(nd);
+                    if (ndb < cd[q]) {
+                        const unsigned long long old = atomicMin(&B.dist[v[q]], ndb);
+                        if (ndb < old) {
+                            c_impr++;
+                            int64_t b = bucket_of(nd, B.inv_delta);
+                            if (heavy && b <= cur) b = cur + 1;
+                            if (b <= cur) {
+                                if (atomicExch(&B.near_stamp[v[q]], rn) != rn) {
+                                    to_near = true;
+                                    nch = chunks_of(B.rp[v[q] + 1] - B.rp[v[q]]);
+                                    to_set = atomicExch(&B.sstamp[v[q]], cur32) != cur32;
+                                }
+                            } else if (b < lim) {
+                                if (atomicExch(&B.bstamp[v[q]], (int32_t)b) != (int32_t)b) {
+                                    to_ring = true;
+                                    slot = (int)(b % kRing);
+                                }
+                            } else {
+                                if (atomicExch(&B.ostamp[v[q]], epoch) != epoch) to_ovf = true;
+                                mymin = min(mymin, (unsigned long long)b);
+                            }
+                        }
+                    }
+                }
+                c_near += to_near;
+                c_ring += to_ring;
+                c_ovf += to_ovf;
+                const bool take = to_near | to_ring | to_ovf;
+                const uint64_t mask = __ballot(take);
+                if (mask == 0) continue;
+                if (take) {
+                    const uint32_t pos = staged + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
+                    sg.v[pos] = v[q];
+                    sg.tag[pos] = to_near ? ((uint32_t)kTagNear | (to_set ? 0x80u : 0u) | (nch << 8))
+                                          : (to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot);
+                }
+                staged += (uint32_t)__popcll(mask);
+                if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
+            }
+        }
+    }
+    if (staged) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
+    wave_min_to(mymin, &B.st->ovf_minb);
+    if (B.stats) {
+        wave_count(B.stats, 0, c_items);
+        wave_count(B.stats, 1, c_edges);
+        wave_count(B.stats, 2, c_try);
+        wave_count(B.stats, 3, c_impr);
+        wave_count(B.stats, 4, c_near);
+        wave_count(B.stats, 5, c_ring);
+        wave_count(B.stats, 6, c_ovf);
+    }
+}
+
+__global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxed, int32_t *near_stamp,
+                            int32_t *bstamp, int32_t *ostamp, int32_t *sstamp, int64_t n) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
          v += (int64_t)gridDim.x * blockDim.x) {
-        dist[v] = v == src ? 0ull : 0x7FF0000000000000ull;   // +infinity
-        stamp[v] = 0;
+        dist[v] = 0x7FF0000000000000ull;   // +infinity
+        relaxed[v] = ~0ull;                // never equal to a distance
+        near_stamp[v] = -1;
+        bstamp[v] = -1;
+        ostamp[v] = 0;
+        sstamp[v] = -1;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) queue[0] = src;
+}
+
+__global__ void k_sssp_seed(SsspBufs B, int32_t src) {
+    SsspState *st = B.st;
+    const uint32_t nch = chunks_of(B.rp[src + 1] - B.rp[src]);
+    for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x) B.q[0][j] = ((uint64_t)(uint32_t)src << 32) | j;
+    if (threadIdx.x < kRing) st->ring_cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        B.dist[src] = 0ull;
+        B.near_stamp[src] = 0;
+        B.sstamp[src] = 0;
+        B.settled[0] = src;
+        st->settled_cnt = 1;
+        st->cur = 0;
+        st->win_base = 0;
+        st->ovf_minb = ~0ull;
+        st->round = -1;   // the first plan makes it 0
+        st->done = 0;
+        st->epoch = 1;
+        st->mode = 0;
+        st->heavy = 0;
+        st->slot = 0;
+        st->consume = -1;
+        st->split_src = 0;
+        st->qcnt[0] = nch;
+        st->qcnt[1] = 0;
+        st->ovf_cnt[0] = st->ovf_cnt[1] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sum_weights(const double *__restrict__ w, int64_t m, double *sum) {
+    double acc = 0.0;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < m; k += (int64_t)gridDim.x * 256) acc += w[k];
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) atomicAdd(sum, acc);
 }
 
 }  // namespace
@@ -80,37 +523,111 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     if (!g || !dist_out) return fail(GX_NULL_POINTER, "gx_sssp: null argument");
     if (!g->weighted) return fail(GX_INVALID_VALUE, "gx_sssp: graph has no edge weights");
     if (src >= g->n) return fail(GX_INVALID_INDEX, "gx_sssp: source out of range");
+    if ((int64_t)g->n >= kMaxBufVertices)
+        return fail(GX_NOT_IMPLEMENTED, "gx_sssp: more than 2^28 vertices (buffer-load offsets are 31-bit)");
     gx_ctx *ctx = g->ctx;
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const int64_t n = (int64_t)g->n;
-    DBuf<unsigned long long> dist;
-    DBuf<int32_t> stamp, q0, q1;
-    DBuf<uint32_t> qcount;
+    const uint64_t qcap = (uint64_t)n + g->nnz / kChunk + 64;
+    DBuf<unsigned long long> dist, relaxed;
+    DBuf<int32_t> nstamp, bstamp, ostamp, sstamp, ring, ovf0, ovf1, settled;
+    DBuf<uint64_t> q0, q1;
+    DBuf<SsspState> st;
     GX_TRY(dist.alloc(n));
-    GX_TRY(stamp.alloc(n));
-    GX_TRY(q0.alloc(n));
-    GX_TRY(q1.alloc(n));
-    GX_TRY(qcount.alloc(1));
+    GX_TRY(relaxed.alloc(n));
+    GX_TRY(nstamp.alloc(n));
+    GX_TRY(bstamp.alloc(n));
+    GX_TRY(ostamp.alloc(n));
+    GX_TRY(sstamp.alloc(n));
+    GX_TRY(settled.alloc(n));
+    GX_TRY(ring.alloc((uint64_t)n * kRing));
+    GX_TRY(ovf0.alloc(n));
+    GX_TRY(ovf1.alloc(n));
+    GX_TRY(q0.alloc(qcap));
+    GX_TRY(q1.alloc(qcap));
+    GX_TRY(st.alloc(1));
+
+    // bucket width delta = scale * mean weight / mean degree (GX_SSSP_DELTA overrides); any
+    // positive value gives the same distances, it only trades rounds for re-relaxations
+    if (g->mean_w < 0.0) {
+        double mean = 1.0;
+        if (g->nnz) {
+            DBuf<double> sum;
+            GX_TRY(sum.alloc(1));
+            GX_HIP_TRY(hipMemsetAsync(sum.p, 0, sizeof(double), s));
+            hipLaunchKernelGGL(k_sum_weights, dim3(grid_for(g->nnz, 256, 4096)), dim3(256), 0, s, g->A.w.p,
+                               (int64_t)g->nnz, sum.p);
+            GX_TRY(check_launch("k_sum_weights"));
+            double h = 0.0;
+            GX_HIP_TRY(hipMemcpyAsync(&h, sum.p, sizeof(double), hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            mean = h / (double)g->nnz;
+        }
+        g->mean_w = mean;
+    }
+    double delta = 0.0, scale = 20.0;
+    if (const char *e = std::getenv("GX_SSSP_DELTA")) delta = std::atof(e);
+    if (const char *e = std::getenv("GX_SSSP_DSCALE")) scale = std::atof(e);
+    if (!(delta > 0.0)) {
+        const double avg_deg = g->nnz ? (double)g->nnz / (double)n : 1.0;
+        delta = scale * g->mean_w / std::max(1.0, avg_deg);
+        if (!(delta > 0.0) || !std::isfinite(delta)) delta = 1.0;
+    }
+    const double inv_delta = 1.0 / delta;
+    const bool verbose = std::getenv("GX_SSSP_VERBOSE") != nullptr;
+    DBuf<unsigned long long> stats;
+    if (verbose) {
+        GX_TRY(stats.alloc(8));
+        GX_HIP_TRY(hipMemsetAsync(stats.p, 0, 64, s));
+    }
+    SsspBufs B{g->A.rp.p,   g->A.ci.p,    g->A.w.p,      dist.p,     relaxed.p,   nstamp.p,
+               bstamp.p,    ostamp.p,     sstamp.p,      {q0.p, q1.p}, ring.p,    {ovf0.p, ovf1.p},
+               settled.p,   (uint64_t)n,  delta,         inv_delta,  st.p,        stats.p};
+
     GX_TRY(device_begin(ctx));
-    hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, stamp.p, n,
-                       (int32_t)src, q0.p);
+    hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nstamp.p,
+                       bstamp.p, ostamp.p, sstamp.p, n);
     GX_TRY(check_launch("k_sssp_init"));
-    uint32_t qsize = 1;
-    for (int32_t round = 1; qsize > 0; round++) {
-        GX_HIP_TRY(hipMemsetAsync(qcount.p, 0, 4, s));
-        {
-            KTimer kt(ctx, "sssp_relax", s);
-            hipLaunchKernelGGL(k_sssp_relax, dim3(grid_for((uint64_t)qsize * kWave, kSsspBlock, 8192)),
-                               dim3(kSsspBlock), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, q0.p, qsize, dist.p,
-                               stamp.p, round, q1.p, qcount.p);
+    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src);
+    GX_TRY(check_launch("k_sssp_seed"));
+    const unsigned grid = (unsigned)std::max(1, ctx->num_cus) * 8;
+    // a bound every correct run stays far below: each step settles a vertex or a bucket
+    const uint64_t max_steps = 8ull * (uint64_t)n + 4ull * (uint64_t)g->nnz + 1000000ull;
+    uint64_t steps = 0;
+    int batch = 4;
+    int32_t done = 0;
+    while (!done) {
+        for (int i = 0; i < batch; i++) {
+            hipLaunchKernelGGL(k_sssp_plan, dim3(1), dim3(1), 0, s, st.p);
+            {
+                KTimer kt(ctx, "sssp_advance", s);
+                hipLaunchKernelGGL(k_sssp_advance, dim3(grid), dim3(kSsspBlock), 0, s, B);
+            }
+            {
+                KTimer kt(ctx, "sssp_relax", s);
+                hipLaunchKernelGGL(k_sssp_relax, dim3(grid), dim3(kSsspBlock), 0, s, B);
+            }
         }
         GX_TRY(check_launch("k_sssp_relax"));
-        GX_HIP_TRY(hipMemcpyAsync(&qsize, qcount.p, 4, hipMemcpyDeviceToHost, s));
+        steps += batch;
+        GX_HIP_TRY(hipMemcpyAsync(&done, &st.p->done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
         GX_HIP_TRY(hipStreamSynchronize(s));
-        std::swap(q0.p, q1.p);
+        if (steps > max_steps) return fail(GX_PANIC, "gx_sssp: delta-stepping did not converge");
+        batch = std::min(batch * 2, 32);
     }
     GX_TRY(device_end(ctx));
+    if (verbose) {
+        SsspState h;
+        GX_HIP_TRY(hipMemcpy(&h, st.p, sizeof(h), hipMemcpyDeviceToHost));
+        unsigned long long c[8];
+        GX_HIP_TRY(hipMemcpy(c, stats.p, 64, hipMemcpyDeviceToHost));
+        std::fprintf(stderr,
+                     "gx_sssp: delta %g rounds %d last bucket %lld epochs %d launched steps %llu | items %llu edges "
+                     "%llu tried %llu improved %llu near %llu ring %llu ovf %llu skipped %llu\n",
+                     delta, h.round, (long long)h.cur, h.epoch, (unsigned long long)steps, c[0], c[1], c[2], c[3],
+                     c[4], c[5], c[6], c[7]);
+    }
     GX_HIP_TRY(hipMemcpy(dist_out, dist.p, n * 8, hipMemcpyDeviceToHost));
     return GX_SUCCESS;
 }
