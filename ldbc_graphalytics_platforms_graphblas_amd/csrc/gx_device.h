@@ -103,6 +103,17 @@ struct gx_ctx {
     int num_cus = 0;
 };
 
+namespace gx {
+// SSSP edge layout: every row of A split into its light (w < delta) edges, then its heavy
+// ones; built once per graph and delta by gx_sssp.
+struct SsspLayout {
+    double delta = 0.0;
+    DBuf<int32_t> ci;
+    DBuf<double> w;
+    DBuf<int64_t> lend;   // end of the light part of row v (absolute entry index)
+};
+}  // namespace gx
+
 struct gx_graph {
     gx_ctx *ctx = nullptr;
     uint64_t n = 0, nnz = 0;
@@ -111,6 +122,7 @@ struct gx_graph {
     gx::DBuf<int32_t> outdeg;   // out-degree of every vertex (PR)
     gx::PrPart *pr = nullptr;   // cached single-rank PageRank plan
     double mean_w = -1.0;       // cached mean edge weight (SSSP bucket width), < 0 = not yet computed
+    gx::SsspLayout *sssp = nullptr;   // cached light/heavy edge layout
 };
 
 namespace gx {

@@ -204,6 +204,7 @@ extern "C" int gx_graph_free(gx_graph *g) {
     (void)hipSetDevice(g->ctx->device);
     (void)hipStreamSynchronize(g->ctx->stream);
     delete g->pr;
+    delete g->sssp;
     delete g;
     return GX_SUCCESS;
 }

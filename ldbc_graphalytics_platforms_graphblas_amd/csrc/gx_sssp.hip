@@ -28,6 +28,10 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <memory>
+
+#include <rocprim/rocprim.hpp>
+
 #include "gx_device.h"
 
 namespace gx {
@@ -71,7 +75,8 @@ struct SsspState {
 
 struct SsspBufs {
     const int64_t *rp;
-    const int32_t *ci;
+    const int64_t *lend;          // light part of row v: [rp[v], lend[v]), heavy: [lend[v], rp[v+1])
+    const int32_t *ci;            // light/heavy-partitioned rows (SsspLayout)
     const double *w;
     unsigned long long *dist;
     unsigned long long *relaxed;  // distance all edges of v were last relaxed with
@@ -88,6 +93,11 @@ struct SsspBufs {
     SsspState *st;
     unsigned long long *stats;    // GX_SSSP_VERBOSE work counters, else null
 };
+
+// First push of v under `tag`: a plain load filters repeats, the exchange settles races.
+__device__ __forceinline__ bool claim(int32_t *stamp, int32_t tag) {
+    return __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag && atomicExch(stamp, tag) != tag;
+}
 
 // stats slots: 0 items, 1 edges scanned, 2 relaxations tried, 3 improvements, 4 near pushes,
 // 5 ring pushes, 6 overflow pushes, 7 bucket entries skipped as already relaxed
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
             if (mode == 3) {
                 B.relaxed[v] = db;   // heavy edges now, light edges already relaxed at db
                 to_near = true;
-                nch = chunks_of(B.rp[v + 1] - B.rp[v]);
+                nch = chunks_of(B.rp[v + 1] - B.lend[v]);
             } else if (db == B.relaxed[v]) {
                 n_skip++;
             } else if (mode == 1) {
@@ -289,7 +299,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
                 B.near_stamp[v] = r;
                 B.sstamp[v] = (int32_t)cur;
                 to_near = to_set = true;
-                nch = chunks_of(B.rp[v + 1] - B.rp[v]);
+                nch = chunks_of(B.lend[v] - B.rp[v]);
             } else {
                 const int64_t b = max(bucket_of(bitsd(db), B.inv_delta), win_base);
                 if (b < lim) {
@@ -333,7 +343,6 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
     const bool heavy = st->heavy != 0;
     const int64_t cur = st->cur, lim = st->win_base + kRing;
     const int32_t epoch = st->epoch, rn = r + 1, cur32 = (int32_t)cur;
-    const double delta = B.delta;
     const uint64_t *near_in = B.q[qin];
     uint64_t *near_out = B.q[qin ^ 1];
     uint32_t *near_count = &B.st->qcnt[qin ^ 1];
@@ -357,8 +366,9 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
         if (idx < count) {
             const uint64_t item = near_in[idx];
             const int32_t u = (int32_t)(item >> 32);
-            rs = B.rp[u] + (int64_t)(uint32_t)item * kChunk;
-            sz = (int32_t)min(B.rp[u + 1] - rs, (int64_t)kChunk);
+            const int64_t lo = heavy ? B.lend[u] : B.rp[u], hi = heavy ? B.rp[u + 1] : B.lend[u];
+            rs = lo + (int64_t)(uint32_t)item * kChunk;
+            sz = (int32_t)min(hi - rs, (int64_t)kChunk);
             du = bitsd(__hip_atomic_load(&B.dist[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             c_items++;
         }
@@ -392,12 +402,12 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
             for (int q = 0; q < kSlots; q++) wk[q] = B.w[k[q]];
 #pragma unroll
             for (int q = 0; q < kSlots; q++) v[q] = B.ci[k[q]];
-            // edges of the other weight class (and idle slots) get an out-of-range offset: the
-            // buffer load drops them without a memory access or a branch.  A stale value only
-            // costs an extra atomicMin, it is never below the true distance.
+            // idle slots get an out-of-range offset: the buffer load drops them without a
+            // memory access or a branch.  A stale value only costs an extra atomicMin, it is
+            // never below the true distance.
 #pragma unroll
             for (int q = 0; q < kSlots; q++) {
-                const bool in_class = act[q] && (wk[q] >= delta) == heavy;
+                const bool in_class = act[q];
                 cd[q] = __builtin_bit_cast(unsigned long long,
                                            __builtin_amdgcn_raw_buffer_load_b64(
                                                dist_r, in_class ? (uint32_t)v[q] * 8u : kOob, 0, 0));
@@ -408,31 +418,32 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
                 int slot = 0;
                 uint32_t nch = 0;
                 c_edges += act[q];
-                if (act[q] && (wk[q] >= delta) == heavy) {
+                if (act[q]) {
                     c_try++;
                     const double nd = dsrc[q] + wk[q];
                     const unsigned long long ndb = dbits(nd);
                     if (ndb < cd[q]) {
-                        const unsigned long long old = atomicMin(&B.dist[v[q]], ndb);
-                        if (ndb < old) {
-                            c_impr++;
-                            int64_t b = bucket_of(nd, B.inv_delta);
-                            if (heavy && b <= cur) b = cur + 1;
-                            if (b <= cur) {
-                                if (atomicExch(&B.near_stamp[v[q]], rn) != rn) {
-                                    to_near = true;
-                                    nch = chunks_of(B.rp[v[q] + 1] - B.rp[v[q]]);
-                                    to_set = atomicExch(&B.sstamp[v[q]], cur32) != cur32;
-                                }
-                            } else if (b < lim) {
-                                if (atomicExch(&B.bstamp[v[q]], (int32_t)b) != (int32_t)b) {
-                                    to_ring = true;
-                                    slot = (int)(b % kRing);
-                                }
-                            } else {
-                                if (atomicExch(&B.ostamp[v[q]], epoch) != epoch) to_ovf = true;
-                                mymin = min(mymin, (unsigned long long)b);
+                        // no-return atomicMin: the pre-check decides the push.  If another lane
+                        // lowered dist[v] further meanwhile, it pushes v as well: an extra push,
+                        // never a missed one.
+                        __hip_atomic_fetch_min(&B.dist[v[q]], ndb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        c_impr++;
+                        int64_t b = bucket_of(nd, B.inv_delta);
+                        if (heavy && b <= cur) b = cur + 1;
+                        if (b <= cur) {
+                            if (claim(&B.near_stamp[v[q]], rn)) {
+                                to_near = true;
+                                nch = chunks_of(B.lend[v[q]] - B.rp[v[q]]);
+                                to_set = claim(&B.sstamp[v[q]], cur32);
                             }
+                        } else if (b < lim) {
+                            if (claim(&B.bstamp[v[q]], (int32_t)b)) {
+                                to_ring = true;
+                                slot = (int)(b % kRing);
+                            }
+                        } else {
+                            if (claim(&B.ostamp[v[q]], epoch)) to_ovf = true;
+                            mymin = min(mymin, (unsigned long long)b);
                         }
                     }
                 }
@@ -481,7 +492,7 @@ __global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxe
 
 __global__ void k_sssp_seed(SsspBufs B, int32_t src) {
     SsspState *st = B.st;
-    const uint32_t nch = chunks_of(B.rp[src + 1] - B.rp[src]);
+    const uint32_t nch = chunks_of(B.lend[src] - B.rp[src]);
     for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x) B.q[0][j] = ((uint64_t)(uint32_t)src << 32) | j;
     if (threadIdx.x < kRing) st->ring_cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
@@ -505,6 +516,132 @@ __global__ void k_sssp_seed(SsspBufs B, int32_t src) {
         st->qcnt[1] = 0;
         st->ovf_cnt[0] = st->ovf_cnt[1] = 0;
     }
+}
+
+// ---- light/heavy edge layout (built once per graph and delta, no atomics) ----
+// Entries are taken in 64-entry slabs: one ballot per slab gives its light mask, so the
+// number of light entries before entry e is L(e) = cpre[e/64] + popc(mask[e/64] below e).
+// A row's light entries go to rp[r] + L(e) - L(rp[r]), its heavy ones after lend[r] in order.
+__global__ __launch_bounds__(256) void k_light_masks(const double *__restrict__ w, int64_t nnz, double delta,
+                                                     uint64_t *mask, int32_t *cnt, int64_t nslabs) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
+    for (int64_t sl = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; sl < nslabs; sl += nw) {
+        const int64_t e = sl * kWave + lane;
+        const bool light = e < nnz && w[e] < delta;
+        const uint64_t m = __ballot(light);
+        if (lane == 0) {
+            mask[sl] = m;
+            cnt[sl] = __popcll(m);
+        }
+    }
+}
+
+__device__ __forceinline__ int64_t light_before(const uint64_t *mask, const int64_t *cpre, int64_t e) {
+    const int64_t sl = e / kWave;
+    const int b = (int)(e % kWave);
+    return cpre[sl] + (b ? __popcll(mask[sl] & ((1ull << b) - 1)) : 0);
+}
+
+__global__ __launch_bounds__(256) void k_light_rows(const int64_t *__restrict__ rp, const uint64_t *__restrict__ mask,
+                                                    const int64_t *__restrict__ cpre, int64_t n, int64_t *Ls,
+                                                    int64_t *lend) {
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += (int64_t)gridDim.x * 256) {
+        const int64_t a = light_before(mask, cpre, rp[v]), b = light_before(mask, cpre, rp[v + 1]);
+        Ls[v] = a;
+        lend[v] = rp[v] + (b - a);
+    }
+}
+
+// One wave per slab; lane = entry.  The slab's rows lie in [r0, r1] (two uniform binary
+// searches); when that range is at most 64 rows each lane finds its row by a 6-step shuffle
+// search over rp[r0+1 .. r0+64], else by its own binary search.
+__global__ __launch_bounds__(256) void k_light_scatter(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                       const double *__restrict__ w, const uint64_t *__restrict__ mask,
+                                                       const int64_t *__restrict__ cpre, const int64_t *__restrict__ Ls,
+                                                       const int64_t *__restrict__ lend, int64_t n, int64_t nnz,
+                                                       int64_t nslabs, int32_t *ci2, double *w2) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
+    for (int64_t sl = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; sl < nslabs; sl += nw) {
+        const int64_t e0 = sl * kWave, e_last = min(e0 + kWave, nnz) - 1;
+        const int64_t r0 = row_of_edge(rp, n, e0), r1 = row_of_edge(rp, n, e_last);
+        const int64_t e = e0 + lane;
+        const bool valid = e < nnz;
+        const int64_t ee = valid ? e : e_last;
+        int64_t r;
+        if (r1 - r0 < kWave) {
+            // lane k holds rp[r0 + 1 + k] (clamped); row = r0 + #{k : rp[r0+1+k] <= e}
+            const int64_t rpk = rp[min(r0 + 1 + lane, n)];
+            int o = 0;
+#pragma unroll
+            for (int step = kWave / 2; step > 0; step >>= 1)
+                if (__shfl(rpk, o + step - 1, kWave) <= ee) o += step;
+            r = r0 + o;
+        } else {
+            int64_t lo = r0, hi = r1 + 1;   // rp[lo] <= ee < rp[hi]
+            while (hi - lo > 1) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (rp[mid] <= ee) lo = mid;
+                else hi = mid;
+            }
+            r = lo;
+        }
+        if (valid) {
+            const uint64_t m = mask[sl];
+            const bool light = (m >> lane) & 1ull;
+            const int64_t lin = cpre[sl] + (lane ? __popcll(m & ((1ull << lane) - 1)) : 0) - Ls[r];
+            const int64_t pos = light ? rp[r] + lin : lend[r] + ((e - rp[r]) - lin);
+            ci2[pos] = ci[e];
+            w2[pos] = w[e];
+        }
+    }
+}
+
+int ensure_sssp_layout(gx_graph *g, double delta, hipStream_t s) {
+    if (g->sssp && g->sssp->delta == delta) return GX_SUCCESS;
+    const int64_t n = (int64_t)g->n, nnz = (int64_t)g->nnz;
+    auto L = std::make_unique<SsspLayout>();
+    L->delta = delta;
+    GX_TRY(L->ci.alloc(nnz, 16));
+    GX_TRY(L->w.alloc(nnz, 16));
+    GX_TRY(L->lend.alloc(n));
+    const int64_t nslabs = (nnz + kWave - 1) / kWave;
+    DBuf<uint64_t> mask;
+    DBuf<int32_t> cnt;
+    DBuf<int64_t> cpre, Ls;
+    GX_TRY(mask.alloc(nslabs + 1));
+    GX_TRY(cnt.alloc(nslabs + 1));
+    GX_TRY(cpre.alloc(nslabs + 1));
+    GX_TRY(Ls.alloc(n));
+    GX_HIP_TRY(hipMemsetAsync(cnt.p + nslabs, 0, sizeof(int32_t), s));
+    GX_HIP_TRY(hipMemsetAsync(mask.p + nslabs, 0, sizeof(uint64_t), s));
+    const unsigned wgrid = grid_for((uint64_t)nslabs * kWave, 256, 16384);
+    if (nslabs) {
+        hipLaunchKernelGGL(k_light_masks, dim3(wgrid), dim3(256), 0, s, g->A.w.p, nnz, delta, mask.p, cnt.p, nslabs);
+        GX_TRY(check_launch("k_light_masks"));
+    }
+    size_t tmp_bytes = 0;
+    GX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt.p, cpre.p, (int64_t)0, (size_t)(nslabs + 1),
+                                       rocprim::plus<int64_t>(), s));
+    DBuf<char> tmp;
+    GX_TRY(tmp.alloc(tmp_bytes));
+    GX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tmp_bytes, cnt.p, cpre.p, (int64_t)0, (size_t)(nslabs + 1),
+                                       rocprim::plus<int64_t>(), s));
+    if (n) {
+        hipLaunchKernelGGL(k_light_rows, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, g->A.rp.p, mask.p, cpre.p, n,
+                           Ls.p, L->lend.p);
+        GX_TRY(check_launch("k_light_rows"));
+    }
+    if (nslabs) {
+        hipLaunchKernelGGL(k_light_scatter, dim3(wgrid), dim3(256), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, mask.p,
+                           cpre.p, Ls.p, L->lend.p, n, nnz, nslabs, L->ci.p, L->w.p);
+        GX_TRY(check_launch("k_light_scatter"));
+    }
+    GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries are freed on return
+    delete g->sssp;
+    g->sssp = L.release();
+    return GX_SUCCESS;
 }
 
 __global__ __launch_bounds__(256) void k_sum_weights(const double *__restrict__ w, int64_t m, double *sum) {
@@ -581,11 +718,16 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         GX_TRY(stats.alloc(8));
         GX_HIP_TRY(hipMemsetAsync(stats.p, 0, 64, s));
     }
-    SsspBufs B{g->A.rp.p,   g->A.ci.p,    g->A.w.p,      dist.p,     relaxed.p,   nstamp.p,
+    GX_TRY(device_begin(ctx));
+    {
+        KTimer kt(ctx, "sssp_layout", s);
+        GX_TRY(ensure_sssp_layout(g, delta, s));
+    }
+    const SsspLayout &lay = *g->sssp;
+    SsspBufs B{g->A.rp.p,   lay.lend.p,   lay.ci.p,      lay.w.p,    dist.p,      relaxed.p,   nstamp.p,
                bstamp.p,    ostamp.p,     sstamp.p,      {q0.p, q1.p}, ring.p,    {ovf0.p, ovf1.p},
                settled.p,   (uint64_t)n,  delta,         inv_delta,  st.p,        stats.p};
 
-    GX_TRY(device_begin(ctx));
     hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nstamp.p,
                        bstamp.p, ostamp.p, sstamp.p, n);
     GX_TRY(check_launch("k_sssp_init"));
