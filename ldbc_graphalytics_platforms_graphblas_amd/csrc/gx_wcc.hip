@@ -1,11 +1,18 @@
-// gx_wcc.hip -- weakly connected components by min-label hooking + pointer jumping.
+// gx_wcc.hip -- weakly connected components: Afforest (undirected) / min-label hooking
+// (directed), with pointer jumping.
 //
 // Replaces WeaklyConnectedComponents -> GrB_eWiseAdd(A, LOR, A, A') + LAGr_ConnectedComponents
-// (wcc.cpp:39-66).  Hooking treats every stored edge (u, v) as undirected, so the explicit
+// (wcc.cpp:39-66).  Every stored edge (u, v) is treated as undirected, so the explicit
 // symmetrisation the reference performs inside processing time is not needed.
+// Undirected graphs (every edge stored at both endpoints), Afforest (Sutton et al.):
+//   sample   : two rounds linking each vertex with its r-th neighbour (CAS hooking), each
+//              followed by pointer jumping;
+//   giant    : the most frequent root among 1024 hashed vertices;
+//   finish   : one wave per vertex outside the giant component links its remaining neighbours.
+// Directed graphs (an edge is seen from one endpoint only):
 //   hook     : edge-balanced (one chunk of kEdgesPerThread entries per thread); the roots
 //              ru, rv of both endpoints are found by following parent pointers and the larger
-//              root is hooked below the smaller one with atomicMin.
+//              root is hooked below the smaller one with atomicMin; repeated until no change.
 //   compress : pointer jumping until every vertex points at its root.
 // parent[v] <= v always holds, so the root of each final tree is the smallest vertex index
 // of the component: comp[v] is canonical and equals the oracle's union-find labels exactly.
