@@ -178,6 +178,62 @@ int gx_pr_part_step(gx_pr_part *part, const double *x_full, double *x_local,
                     double *rank_out, void *stream);
 int gx_pr_part_free(gx_pr_part *part);
 
+/* ---------------------------------------------------------------------------------
+ * Multi-GPU steps for the other algorithms.  The graph is replicated on
+ * every rank (gx_graph_create on each device); rank k owns the vertex range
+ * [v0, v1) = [ranges[k], ranges[k+1]).  All array arguments are DEVICE pointers of full
+ * length n (caller-allocated, e.g. torch tensors); the caller runs the collective named
+ * below between steps (torch.distributed / RCCL).  `stream` is the hipStream_t to launch
+ * on; unlike gx_pr_part_*, NULL here means the null (default) stream -- torch's default
+ * stream -- so the steps order with tensors and collectives issued there.
+ * The reference has no distributed path; these replace LA_BFS / LA_CDLP_CPU / LA_LCC /
+ * LA_SSSP / WeaklyConnectedComponents (bfs.cpp:70-83, cdlp.cpp:54-67, lcc.cpp:61-71,
+ * sssp.cpp:53-81, wcc.cpp:39-66) when they run on several GPUs.
+ *
+ * BFS  : init(level); per level cur = 0, 1, ...: zero next (n bytes); expand(owned rows);
+ *        all-reduce MAX(next); zero count; commit -> count = vertices at level cur+1;
+ *        stop when count == 0.  level: INT64_MAX = unreached.
+ * WCC  : init(parent); per round: zero changed; hook(owned rows' edges, then compress);
+ *        all-reduce MIN(parent); compress; all-reduce MAX(changed); stop when 0.
+ *        parent[v] is then the smallest vertex id of v's component.
+ * SSSP : init(dist, prev); per round: zero active; round(owned); all-reduce MIN(dist as
+ *        int64); all-reduce SUM(active); stop when active == 0.  dist holds fp64 bit
+ *        patterns (+inf = unreached).
+ * CDLP : part_create(range) once; part_init(labels); per iteration: zero changed;
+ *        part_step(labels -> next, owned range written); exchange the owned slices of next
+ *        into every rank's labels (all-gather); all-reduce MAX(changed); stop when 0 or
+ *        after `iters`.  labels are int32 vertex ids.
+ * LCC  : part_create once (orientation); part_ranges -> balanced ranges (same on every
+ *        rank); zero tc (n uint64); part_counts(owned range); all-reduce SUM(tc);
+ *        part_finish(tc -> lcc).
+ * ------------------------------------------------------------------------------- */
+int gx_bfs_part_init(gx_graph *g, uint64_t src, int64_t *level, void *stream);
+int gx_bfs_part_expand(gx_graph *g, uint64_t v0, uint64_t v1, const int64_t *level, int64_t cur,
+                       uint8_t *next, void *stream);
+int gx_bfs_part_commit(gx_graph *g, const uint8_t *next, int64_t *level, int64_t cur, uint64_t *count,
+                       void *stream);
+
+int gx_wcc_part_init(gx_graph *g, int32_t *parent, void *stream);
+int gx_wcc_part_hook(gx_graph *g, uint64_t v0, uint64_t v1, int32_t *parent, int *changed, void *stream);
+int gx_wcc_part_compress(gx_graph *g, int32_t *parent, void *stream);
+
+int gx_sssp_part_init(gx_graph *g, uint64_t src, uint64_t *dist, uint64_t *prev, void *stream);
+int gx_sssp_part_round(gx_graph *g, uint64_t v0, uint64_t v1, uint64_t *dist, uint64_t *prev,
+                       uint8_t *flag, uint64_t *active, void *stream);
+
+typedef struct gx_cdlp_part gx_cdlp_part;
+int gx_cdlp_part_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_cdlp_part **part);
+int gx_cdlp_part_init(gx_cdlp_part *part, int32_t *labels, void *stream);
+int gx_cdlp_part_step(gx_cdlp_part *part, const int32_t *labels, int32_t *next, int *changed, void *stream);
+int gx_cdlp_part_free(gx_cdlp_part *part);
+
+typedef struct gx_lcc_part gx_lcc_part;
+int gx_lcc_part_create(gx_graph *g, gx_lcc_part **part);
+int gx_lcc_part_ranges(gx_lcc_part *part, int nranks, uint64_t *ranges /* nranks+1, host */);
+int gx_lcc_part_counts(gx_lcc_part *part, uint64_t v0, uint64_t v1, uint64_t *tc, void *stream);
+int gx_lcc_part_finish(gx_lcc_part *part, const uint64_t *tc, double *lcc, void *stream);
+int gx_lcc_part_free(gx_lcc_part *part);
+
 #ifdef __cplusplus
 }
 #endif

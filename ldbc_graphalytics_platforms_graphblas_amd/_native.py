@@ -75,6 +75,24 @@ SIGNATURES = [
     ("gx_pr_part_init", C.c_int, [_P, _P, _P]),
     ("gx_pr_part_step", C.c_int, [_P, _P, _P, _P, _P]),
     ("gx_pr_part_free", C.c_int, [_P]),
+    # multi-GPU steps (device pointers as c_void_p)
+    ("gx_bfs_part_init", C.c_int, [_P, C.c_uint64, _P, _P]),
+    ("gx_bfs_part_expand", C.c_int, [_P, C.c_uint64, C.c_uint64, _P, C.c_int64, _P, _P]),
+    ("gx_bfs_part_commit", C.c_int, [_P, _P, _P, C.c_int64, _P, _P]),
+    ("gx_wcc_part_init", C.c_int, [_P, _P, _P]),
+    ("gx_wcc_part_hook", C.c_int, [_P, C.c_uint64, C.c_uint64, _P, _P, _P]),
+    ("gx_wcc_part_compress", C.c_int, [_P, _P, _P]),
+    ("gx_sssp_part_init", C.c_int, [_P, C.c_uint64, _P, _P, _P]),
+    ("gx_sssp_part_round", C.c_int, [_P, C.c_uint64, C.c_uint64, _P, _P, _P, _P, _P]),
+    ("gx_cdlp_part_create", C.c_int, [_P, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
+    ("gx_cdlp_part_init", C.c_int, [_P, _P, _P]),
+    ("gx_cdlp_part_step", C.c_int, [_P, _P, _P, _P, _P]),
+    ("gx_cdlp_part_free", C.c_int, [_P]),
+    ("gx_lcc_part_create", C.c_int, [_P, C.POINTER(_P)]),
+    ("gx_lcc_part_ranges", C.c_int, [_P, C.c_int, _U64P]),
+    ("gx_lcc_part_counts", C.c_int, [_P, C.c_uint64, C.c_uint64, _P, _P]),
+    ("gx_lcc_part_finish", C.c_int, [_P, _P, _P, _P]),
+    ("gx_lcc_part_free", C.c_int, [_P]),
 ]
 
 _lib = None

@@ -19,6 +19,8 @@
 // The winner is the maximum of the 64-bit key (count << 32) | ~label, i.e. the highest
 // count and among equal counts the smallest label.
 #include <algorithm>
+#include <memory>
+#include <vector>
 
 #include "gx_device.h"
 
@@ -38,6 +40,7 @@ struct CdlpArgs {
     int32_t *nxt;
     int64_t n;
     int *changed;
+    int64_t v0, v1;       // vertices updated by this call (the whole graph, or one rank's range)
 };
 
 __device__ __forceinline__ int32_t label_at(const CdlpArgs &a, int64_t ob, int64_t od, int64_t ib,
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a) {
     const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
     bool any = false;
-    for (int64_t v = gw; v < a.n; v += nw) {
+    for (int64_t v = a.v0 + gw; v < a.v1; v += nw) {
         const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
         int64_t ib = 0, id = 0;
         if (a.rpT) {
@@ -304,27 +307,22 @@ __global__ void k_cdlp_iota(int32_t *a, int64_t n) {
         a[v] = (int32_t)v;
 }
 
-}  // namespace
-}  // namespace gx
-
-using namespace gx;
-
-extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
-    if (!g || !labels) return fail(GX_NULL_POINTER, "gx_cdlp: null argument");
-    if (iters < 0) return fail(GX_INVALID_VALUE, "gx_cdlp: negative iteration count");
-    gx_ctx *ctx = g->ctx;
-    GX_HIP_TRY(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
-    const int64_t n = (int64_t)g->n;
-    if (n == 0) return GX_SUCCESS;
-    GX_TRY(device_begin(ctx));
-    if (g->directed) GX_TRY(ensure_transpose(g));
-    // medium vertices (LDS table per workgroup) and huge ones (global hash segments)
-    std::vector<int32_t> hv, hl, mv;
-    std::vector<int64_t> hoff, cbeg;
-    std::vector<int32_t> cvert;
+// Tier lists of the vertices in [v0, v1): medium vertices (LDS table per workgroup) and huge
+// ones (chunked global hash segments); light vertices are found by k_cdlp_light itself.
+struct CdlpPlan {
+    int64_t v0 = 0, v1 = 0;
+    size_t n_mid = 0, n_huge = 0, n_chunks = 0;
     int64_t total = 0;
-    for (int64_t v = 0; v < n; v++) {
+    DBuf<int32_t> d_hv, d_hl, d_mv, d_cvert;
+    DBuf<int64_t> d_hoff, d_cbeg;
+    DBuf<uint32_t> gk, gc;
+};
+
+int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
+    std::vector<int32_t> hv, hl, mv, cvert;
+    std::vector<int64_t> hoff, cbeg;
+    int64_t total = 0;
+    for (int64_t v = v0; v < v1; v++) {
         int64_t d = g->A.h_rp[v + 1] - g->A.h_rp[v];
         if (g->directed) d += g->AT.h_rp[v + 1] - g->AT.h_rp[v];
         if (d > kLdsHash / 2 && d <= kMidMax) {
@@ -342,62 +340,95 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             total += 1ll << l2;
         }
     }
-    DBuf<int32_t> la, lb, d_hv, d_hl, d_mv;
-    DBuf<int64_t> d_hoff, d_cbeg;
-    DBuf<int32_t> d_cvert;
-    DBuf<uint32_t> gk, gc;
+    P.v0 = v0;
+    P.v1 = v1;
+    P.n_mid = mv.size();
+    P.n_huge = hv.size();
+    P.n_chunks = cvert.size();
+    P.total = total;
+    if (!hv.empty()) {
+        GX_TRY(P.d_hv.alloc(hv.size()));
+        GX_TRY(P.d_hl.alloc(hl.size()));
+        GX_TRY(P.d_hoff.alloc(hoff.size()));
+        GX_TRY(P.gk.alloc(total));
+        GX_TRY(P.gc.alloc(total));
+        GX_TRY(P.d_cvert.alloc(cvert.size()));
+        GX_TRY(P.d_cbeg.alloc(cbeg.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_hv.p, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_hl.p, hl.data(), hl.size() * 4, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_hoff.p, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_cvert.p, cvert.data(), cvert.size() * 4, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_cbeg.p, cbeg.data(), cbeg.size() * 8, hipMemcpyHostToDevice, s));
+    }
+    if (!mv.empty()) {
+        GX_TRY(P.d_mv.alloc(mv.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_mv.p, mv.data(), mv.size() * 4, hipMemcpyHostToDevice, s));
+    }
+    GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors go out of scope
+    return GX_SUCCESS;
+}
+
+// One synchronous iteration for the plan's vertices: nxt[v] for v in [v0, v1) from cur
+// (the full label array); *changed is set when a label moved (caller zeroes it).
+int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s) {
+    gx_ctx *ctx = g->ctx;
+    const int64_t n = (int64_t)g->n;
+    CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr,
+               cur,       nxt,       n,      changed, P.v0, P.v1};
+    if (P.v1 > P.v0) {
+        KTimer kt(ctx, "cdlp_light", s);
+        hipLaunchKernelGGL(k_cdlp_light, dim3(grid_for((uint64_t)(P.v1 - P.v0) * kWave, kCdlpBlock, 8192)),
+                           dim3(kCdlpBlock), 0, s, a);
+    }
+    GX_TRY(check_launch("k_cdlp_light"));
+    if (P.n_mid) {
+        KTimer kt(ctx, "cdlp_mid", s);
+        const unsigned mid_grid = (unsigned)std::min<size_t>(P.n_mid, (size_t)std::max(1, ctx->num_cus));
+        hipLaunchKernelGGL(k_cdlp_mid, dim3(mid_grid), dim3(kMidBlock), 0, s, a, P.d_mv.p, (int32_t)P.n_mid);
+        GX_TRY(check_launch("k_cdlp_mid"));
+    }
+    if (P.n_huge) {
+        KTimer kt(ctx, "cdlp_heavy", s);
+        GX_HIP_TRY(hipMemsetAsync(P.gk.p, 0xff, (size_t)P.total * 4, s));
+        GX_HIP_TRY(hipMemsetAsync(P.gc.p, 0, (size_t)P.total * 4, s));
+        hipLaunchKernelGGL(k_cdlp_huge_insert, dim3((unsigned)P.n_chunks), dim3(kHugeBlock), 0, s, a, P.d_hv.p,
+                           P.d_hoff.p, P.d_hl.p, P.d_cvert.p, P.d_cbeg.p, P.gk.p, P.gc.p);
+        GX_TRY(check_launch("k_cdlp_huge_insert"));
+        hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)P.n_huge), dim3(kHugeBlock), 0, s, a, P.d_hv.p,
+                           P.d_hoff.p, P.d_hl.p, P.gk.p, P.gc.p);
+        GX_TRY(check_launch("k_cdlp_huge_reduce"));
+    }
+    return GX_SUCCESS;
+}
+
+}  // namespace
+}  // namespace gx
+
+using namespace gx;
+
+extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
+    if (!g || !labels) return fail(GX_NULL_POINTER, "gx_cdlp: null argument");
+    if (iters < 0) return fail(GX_INVALID_VALUE, "gx_cdlp: negative iteration count");
+    gx_ctx *ctx = g->ctx;
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int64_t n = (int64_t)g->n;
+    if (n == 0) return GX_SUCCESS;
+    GX_TRY(device_begin(ctx));
+    if (g->directed) GX_TRY(ensure_transpose(g));
+    CdlpPlan P;
+    GX_TRY(cdlp_plan(g, 0, n, P, s));
+    DBuf<int32_t> la, lb;
     DBuf<int> changed;
     GX_TRY(la.alloc(n));
     GX_TRY(lb.alloc(n));
     GX_TRY(changed.alloc(1));
-    if (!hv.empty()) {
-        GX_TRY(d_hv.alloc(hv.size()));
-        GX_TRY(d_hl.alloc(hl.size()));
-        GX_TRY(d_hoff.alloc(hoff.size()));
-        GX_TRY(gk.alloc(total));
-        GX_TRY(gc.alloc(total));
-        GX_HIP_TRY(hipMemcpyAsync(d_hv.p, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, s));
-        GX_HIP_TRY(hipMemcpyAsync(d_hl.p, hl.data(), hl.size() * 4, hipMemcpyHostToDevice, s));
-        GX_HIP_TRY(hipMemcpyAsync(d_hoff.p, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, s));
-        GX_TRY(d_cvert.alloc(cvert.size()));
-        GX_TRY(d_cbeg.alloc(cbeg.size()));
-        GX_HIP_TRY(hipMemcpyAsync(d_cvert.p, cvert.data(), cvert.size() * 4, hipMemcpyHostToDevice, s));
-        GX_HIP_TRY(hipMemcpyAsync(d_cbeg.p, cbeg.data(), cbeg.size() * 8, hipMemcpyHostToDevice, s));
-    }
-    if (!mv.empty()) {
-        GX_TRY(d_mv.alloc(mv.size()));
-        GX_HIP_TRY(hipMemcpyAsync(d_mv.p, mv.data(), mv.size() * 4, hipMemcpyHostToDevice, s));
-    }
-    const unsigned mid_grid = (unsigned)std::min<size_t>(mv.size(), (size_t)std::max(1, ctx->num_cus));
     hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, la.p, n);
     GX_TRY(check_launch("k_cdlp_iota"));
     int32_t *cur = la.p, *nxt = lb.p;
     for (int it = 0; it < iters; it++) {
-        CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr,
-                   g->directed ? g->AT.ci.p : nullptr, cur, nxt, n, changed.p};
         GX_HIP_TRY(hipMemsetAsync(changed.p, 0, sizeof(int), s));
-        {
-            KTimer kt(ctx, "cdlp_light", s);
-            hipLaunchKernelGGL(k_cdlp_light, dim3(grid_for((uint64_t)n * kWave, kCdlpBlock, 8192)),
-                               dim3(kCdlpBlock), 0, s, a);
-        }
-        GX_TRY(check_launch("k_cdlp_light"));
-        if (!mv.empty()) {
-            KTimer kt(ctx, "cdlp_mid", s);
-            hipLaunchKernelGGL(k_cdlp_mid, dim3(mid_grid), dim3(kMidBlock), 0, s, a, d_mv.p, (int32_t)mv.size());
-            GX_TRY(check_launch("k_cdlp_mid"));
-        }
-        if (!hv.empty()) {
-            KTimer kt(ctx, "cdlp_heavy", s);
-            GX_HIP_TRY(hipMemsetAsync(gk.p, 0xff, (size_t)total * 4, s));
-            GX_HIP_TRY(hipMemsetAsync(gc.p, 0, (size_t)total * 4, s));
-            hipLaunchKernelGGL(k_cdlp_huge_insert, dim3((unsigned)cvert.size()), dim3(kHugeBlock), 0, s, a, d_hv.p,
-                               d_hoff.p, d_hl.p, d_cvert.p, d_cbeg.p, gk.p, gc.p);
-            GX_TRY(check_launch("k_cdlp_huge_insert"));
-            hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)hv.size()), dim3(kHugeBlock), 0, s, a, d_hv.p,
-                               d_hoff.p, d_hl.p, gk.p, gc.p);
-            GX_TRY(check_launch("k_cdlp_huge_reduce"));
-        }
+        GX_TRY(cdlp_iteration(g, P, cur, nxt, changed.p, s));
         int h_changed = 0;
         GX_HIP_TRY(hipMemcpyAsync(&h_changed, changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
         GX_HIP_TRY(hipStreamSynchronize(s));
@@ -408,5 +439,49 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     std::vector<int32_t> h(n);
     GX_HIP_TRY(hipMemcpy(h.data(), cur, n * 4, hipMemcpyDeviceToHost));
     for (int64_t v = 0; v < n; v++) labels[v] = (uint64_t)h[v];
+    return GX_SUCCESS;
+}
+
+// ---- partitioned CDLP (one rank's vertex range; the caller exchanges labels) ----
+struct gx_cdlp_part {
+    gx_graph *g = nullptr;
+    gx::CdlpPlan plan;
+};
+
+extern "C" int gx_cdlp_part_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_cdlp_part **part) {
+    if (!g || !part) return fail(GX_NULL_POINTER, "gx_cdlp_part_create: null argument");
+    if (v0 > v1 || v1 > g->n) return fail(GX_INVALID_INDEX, "gx_cdlp_part_create: bad vertex range");
+    GX_HIP_TRY(hipSetDevice(g->ctx->device));
+    if (g->directed) GX_TRY(ensure_transpose(g));
+    auto p = std::make_unique<gx_cdlp_part>();
+    p->g = g;
+    GX_TRY(cdlp_plan(g, (int64_t)v0, (int64_t)v1, p->plan, g->ctx->stream));
+    *part = p.release();
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_cdlp_part_init(gx_cdlp_part *part, int32_t *labels, void *stream) {
+    if (!part || !labels) return fail(GX_NULL_POINTER, "gx_cdlp_part_init: null argument");
+    gx_graph *g = part->g;
+    GX_HIP_TRY(hipSetDevice(g->ctx->device));
+    hipStream_t s = (hipStream_t)stream;   // NULL = the null stream (torch's default)
+    if (g->n) {
+        hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(g->n, 256, 8192)), dim3(256), 0, s, labels, (int64_t)g->n);
+        GX_TRY(check_launch("k_cdlp_iota"));
+    }
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_cdlp_part_step(gx_cdlp_part *part, const int32_t *labels, int32_t *next, int *changed,
+                                 void *stream) {
+    if (!part || !labels || !next || !changed) return fail(GX_NULL_POINTER, "gx_cdlp_part_step: null argument");
+    gx_graph *g = part->g;
+    GX_HIP_TRY(hipSetDevice(g->ctx->device));
+    hipStream_t s = (hipStream_t)stream;   // NULL = the null stream (torch's default)
+    return cdlp_iteration(g, part->plan, labels, next, changed, s);
+}
+
+extern "C" int gx_cdlp_part_free(gx_cdlp_part *part) {
+    delete part;
     return GX_SUCCESS;
 }

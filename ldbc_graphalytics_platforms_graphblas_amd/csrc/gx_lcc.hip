@@ -21,6 +21,7 @@
 // Counts are exact integers, so the result is deterministic and equal to the oracle bit for
 // bit (one fp64 division per vertex).
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include <rocprim/rocprim.hpp>
@@ -126,14 +127,15 @@ __global__ __launch_bounds__(kLccBlock) void k_orient_scatter(const int32_t *__r
 }
 
 // ---- vertex tiers ----
-__global__ void k_lcc_classify(const int64_t *__restrict__ orp, int64_t n, int32_t *wave_list, uint32_t *wave_cnt,
-                               int32_t *block_list, uint32_t *block_cnt, int32_t *big_list, uint32_t *big_cnt) {
+__global__ void k_lcc_classify(const int64_t *__restrict__ orp, int64_t v0, int64_t v1, int32_t *wave_list,
+                               uint32_t *wave_cnt, int32_t *block_list, uint32_t *block_cnt, int32_t *big_list,
+                               uint32_t *big_cnt) {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t nround = (n + stride - 1) / stride;
+    const int64_t nround = (v1 - v0 + stride - 1) / stride;
     for (int64_t it = 0; it < nround; it++) {
-        const int64_t v = it * stride + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        const int64_t d = v < n ? orp[v + 1] - orp[v] : 0;
+        const int64_t v = v0 + it * stride + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int64_t d = v < v1 ? orp[v + 1] - orp[v] : 0;
         const bool tw = d > 0 && d <= kWaveMax, tb = d > kWaveMax && d <= kBlockMax, tg = d > kBlockMax;
         const uint64_t mw = __ballot(tw), mb = __ballot(tb), mg = __ballot(tg);
         const uint64_t lt = (1ull << lane) - 1;
@@ -332,6 +334,19 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_merge_row(const int64_t *__re
     }
 }
 
+// Work estimate of vertex v for balancing ranks: |O(v)| + sum over u in O(v) of |O(u)|.
+__global__ void k_lcc_work(const int64_t *__restrict__ orp, const int32_t *__restrict__ oci, int64_t n,
+                           uint64_t *work) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t w = 1;
+        for (int64_t k = orp[v]; k < orp[v + 1]; k++) {
+            const int32_t u = oci[k];
+            w += 1 + (uint64_t)(orp[u + 1] - orp[u]);
+        }
+        work[v] = w;
+    }
+}
+
 __global__ void k_lcc_final(const int64_t *__restrict__ srp, const unsigned long long *__restrict__ tc,
                             int64_t n, double *__restrict__ out) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
@@ -339,6 +354,100 @@ __global__ void k_lcc_final(const int64_t *__restrict__ srp, const unsigned long
         const int64_t k = srp[v + 1] - srp[v];
         out[v] = k < 2 ? 0.0 : (double)tc[v] / ((double)k * (double)(k - 1));
     }
+}
+
+// Degree-ordered orientation O of the closure S (CSR: orp, oci, ofl).
+struct LccOrient {
+    int64_t m = 0;
+    DBuf<int64_t> orp;
+    DBuf<int32_t> oci;
+    DBuf<uint8_t> ofl;
+};
+
+int lcc_orient(gx_graph *g, LccOrient &O, hipStream_t s) {
+    gx_ctx *ctx = g->ctx;
+    const int64_t n = (int64_t)g->n;
+    const DevCSR &S = g->S;
+    const int64_t nnz = (int64_t)S.h_rp[n];
+    const int64_t nslabs = (nnz + kWave - 1) / kWave;
+    DBuf<uint64_t> mask;
+    DBuf<int32_t> cnt;
+    DBuf<int64_t> cpre;
+    GX_TRY(mask.alloc(nslabs + 1));
+    GX_TRY(cnt.alloc(nslabs + 1));
+    GX_TRY(cpre.alloc(nslabs + 1));
+    GX_TRY(O.orp.alloc(n + 1));
+    GX_HIP_TRY(hipMemsetAsync(cnt.p + nslabs, 0, sizeof(int32_t), s));
+    GX_HIP_TRY(hipMemsetAsync(mask.p + nslabs, 0, sizeof(uint64_t), s));
+    KTimer kt(ctx, "lcc_orient", s);
+    if (nslabs)
+        hipLaunchKernelGGL(k_orient_masks, dim3(grid_for((uint64_t)nslabs * kWave, kLccBlock, 16384)), dim3(kLccBlock),
+                           0, s, S.rp.p, S.ci.p, n, nnz, nslabs, mask.p, cnt.p);
+    GX_TRY(check_launch("k_orient_masks"));
+    size_t tmp_bytes = 0;
+    GX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt.p, cpre.p, (int64_t)0, (size_t)(nslabs + 1),
+                                       rocprim::plus<int64_t>(), s));
+    DBuf<char> tmp;
+    GX_TRY(tmp.alloc(tmp_bytes));
+    GX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tmp_bytes, cnt.p, cpre.p, (int64_t)0, (size_t)(nslabs + 1),
+                                       rocprim::plus<int64_t>(), s));
+    hipLaunchKernelGGL(k_orient_rows, dim3(grid_for(n + 1, 256, 16384)), dim3(256), 0, s, S.rp.p, mask.p, cpre.p, n,
+                       O.orp.p);
+    GX_TRY(check_launch("k_orient_rows"));
+    GX_HIP_TRY(hipMemcpyAsync(&O.m, O.orp.p + n, 8, hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    GX_TRY(O.oci.alloc(O.m));
+    GX_TRY(O.ofl.alloc(O.m));
+    if (nnz)
+        hipLaunchKernelGGL(k_orient_scatter, dim3(grid_for(nnz, kLccBlock, 16384)), dim3(kLccBlock), 0, s, S.ci.p,
+                           S.flag.p, nnz, mask.p, cpre.p, O.oci.p, O.ofl.p);
+    GX_TRY(check_launch("k_orient_scatter"));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries are freed on return
+    return GX_SUCCESS;
+}
+
+// Adds the triangle contributions of every triangle whose lowest-ranked vertex (the
+// orientation source) lies in [v0, v1) into tc (n counters).
+int lcc_count_range(gx_graph *g, const LccOrient &O, int64_t v0, int64_t v1, unsigned long long *tc,
+                    hipStream_t s) {
+    gx_ctx *ctx = g->ctx;
+    const int64_t n = (int64_t)g->n, nv = v1 - v0;
+    if (nv <= 0 || O.m == 0) return GX_SUCCESS;
+    DBuf<int32_t> lists;
+    DBuf<uint32_t> counts;
+    GX_TRY(lists.alloc(3 * (uint64_t)nv));
+    GX_TRY(counts.alloc(3));
+    GX_HIP_TRY(hipMemsetAsync(counts.p, 0, 12, s));
+    hipLaunchKernelGGL(k_lcc_classify, dim3(grid_for(nv, 256, 4096)), dim3(256), 0, s, O.orp.p, v0, v1, lists.p,
+                       counts.p, lists.p + nv, counts.p + 1, lists.p + 2 * nv, counts.p + 2);
+    GX_TRY(check_launch("k_lcc_classify"));
+    uint32_t hc[3] = {0, 0, 0};
+    GX_HIP_TRY(hipMemcpyAsync(hc, counts.p, 12, hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    {
+        KTimer kt(ctx, "lcc_triangles", s);
+        if (hc[0])
+            hipLaunchKernelGGL(k_lcc_wave, dim3(grid_for((uint64_t)hc[0] * kWave, kLccBlock, 8192)), dim3(kLccBlock),
+                               0, s, O.orp.p, O.oci.p, O.ofl.p, lists.p, hc[0], tc);
+        GX_TRY(check_launch("k_lcc_wave"));
+        if (hc[1])
+            hipLaunchKernelGGL(k_lcc_block, dim3(std::min<uint32_t>(hc[1], 4096)), dim3(kLccBlock), 0, s, O.orp.p,
+                               O.oci.p, O.ofl.p, lists.p + nv, hc[1], tc);
+        GX_TRY(check_launch("k_lcc_block"));
+        if (hc[2]) {
+            std::vector<int32_t> big(hc[2]);
+            GX_HIP_TRY(hipMemcpyAsync(big.data(), lists.p + 2 * nv, hc[2] * 4, hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            for (int32_t v : big) {
+                hipLaunchKernelGGL(k_lcc_merge_row, dim3(64), dim3(kLccBlock), 0, s, O.orp.p, O.oci.p, O.ofl.p, v,
+                                   tc);
+                GX_TRY(check_launch("k_lcc_merge_row"));
+            }
+        }
+    }
+    GX_HIP_TRY(hipStreamSynchronize(s));   // lists are freed on return
+    (void)n;
+    return GX_SUCCESS;
 }
 
 }  // namespace
@@ -355,87 +464,92 @@ extern "C" int gx_lcc(gx_graph *g, double *lcc) {
     if (n == 0) return GX_SUCCESS;
     GX_TRY(device_begin(ctx));
     GX_TRY(ensure_closure(g));
-    const DevCSR &S = g->S;
-    const int64_t nnz = (int64_t)S.h_rp[n];
-    const int64_t nslabs = (nnz + kWave - 1) / kWave;
-    DBuf<uint64_t> mask;
-    DBuf<int32_t> cnt;
-    DBuf<int64_t> cpre, orp;
-    GX_TRY(mask.alloc(nslabs + 1));
-    GX_TRY(cnt.alloc(nslabs + 1));
-    GX_TRY(cpre.alloc(nslabs + 1));
-    GX_TRY(orp.alloc(n + 1));
-    GX_HIP_TRY(hipMemsetAsync(cnt.p + nslabs, 0, sizeof(int32_t), s));
-    GX_HIP_TRY(hipMemsetAsync(mask.p + nslabs, 0, sizeof(uint64_t), s));
-    {
-        KTimer kt(ctx, "lcc_orient", s);
-        if (nslabs)
-            hipLaunchKernelGGL(k_orient_masks, dim3(grid_for((uint64_t)nslabs * kWave, kLccBlock, 16384)),
-                               dim3(kLccBlock), 0, s, S.rp.p, S.ci.p, n, nnz, nslabs, mask.p, cnt.p);
-        GX_TRY(check_launch("k_orient_masks"));
-        size_t tmp_bytes = 0;
-        GX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt.p, cpre.p, (int64_t)0, (size_t)(nslabs + 1),
-                                           rocprim::plus<int64_t>(), s));
-        DBuf<char> tmp;
-        GX_TRY(tmp.alloc(tmp_bytes));
-        GX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tmp_bytes, cnt.p, cpre.p, (int64_t)0, (size_t)(nslabs + 1),
-                                           rocprim::plus<int64_t>(), s));
-        hipLaunchKernelGGL(k_orient_rows, dim3(grid_for(n + 1, 256, 16384)), dim3(256), 0, s, S.rp.p, mask.p, cpre.p,
-                           n, orp.p);
-        GX_TRY(check_launch("k_orient_rows"));
-    }
-    int64_t m = 0;
-    GX_HIP_TRY(hipMemcpyAsync(&m, orp.p + n, 8, hipMemcpyDeviceToHost, s));
-    GX_HIP_TRY(hipStreamSynchronize(s));
-    DBuf<int32_t> oci, lists;
-    DBuf<uint8_t> ofl;
-    DBuf<uint32_t> counts;
+    LccOrient O;
+    GX_TRY(lcc_orient(g, O, s));
     DBuf<unsigned long long> tc;
     DBuf<double> out;
-    GX_TRY(oci.alloc(m));
-    GX_TRY(ofl.alloc(m));
-    GX_TRY(lists.alloc(3 * (uint64_t)n));
-    GX_TRY(counts.alloc(3));
     GX_TRY(tc.alloc(n));
     GX_TRY(out.alloc(n));
     GX_HIP_TRY(hipMemsetAsync(tc.p, 0, n * 8, s));
-    GX_HIP_TRY(hipMemsetAsync(counts.p, 0, 12, s));
-    {
-        KTimer kt(ctx, "lcc_orient", s);
-        if (nnz)
-            hipLaunchKernelGGL(k_orient_scatter, dim3(grid_for(nnz, kLccBlock, 16384)), dim3(kLccBlock), 0, s, S.ci.p,
-                               S.flag.p, nnz, mask.p, cpre.p, oci.p, ofl.p);
-        GX_TRY(check_launch("k_orient_scatter"));
-        hipLaunchKernelGGL(k_lcc_classify, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, orp.p, n, lists.p,
-                           counts.p, lists.p + n, counts.p + 1, lists.p + 2 * n, counts.p + 2);
-        GX_TRY(check_launch("k_lcc_classify"));
-    }
-    uint32_t hc[3] = {0, 0, 0};
-    GX_HIP_TRY(hipMemcpyAsync(hc, counts.p, 12, hipMemcpyDeviceToHost, s));
-    GX_HIP_TRY(hipStreamSynchronize(s));
-    {
-        KTimer kt(ctx, "lcc_triangles", s);
-        if (hc[0])
-            hipLaunchKernelGGL(k_lcc_wave, dim3(grid_for((uint64_t)hc[0] * kWave, kLccBlock, 8192)), dim3(kLccBlock),
-                               0, s, orp.p, oci.p, ofl.p, lists.p, hc[0], tc.p);
-        GX_TRY(check_launch("k_lcc_wave"));
-        if (hc[1])
-            hipLaunchKernelGGL(k_lcc_block, dim3(std::min<uint32_t>(hc[1], 4096)), dim3(kLccBlock), 0, s, orp.p,
-                               oci.p, ofl.p, lists.p + n, hc[1], tc.p);
-        GX_TRY(check_launch("k_lcc_block"));
-        if (hc[2]) {
-            std::vector<int32_t> big(hc[2]);
-            GX_HIP_TRY(hipMemcpyAsync(big.data(), lists.p + 2 * n, hc[2] * 4, hipMemcpyDeviceToHost, s));
-            GX_HIP_TRY(hipStreamSynchronize(s));
-            for (int32_t v : big) {
-                hipLaunchKernelGGL(k_lcc_merge_row, dim3(64), dim3(kLccBlock), 0, s, orp.p, oci.p, ofl.p, v, tc.p);
-                GX_TRY(check_launch("k_lcc_merge_row"));
-            }
-        }
-    }
-    hipLaunchKernelGGL(k_lcc_final, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, S.rp.p, tc.p, n, out.p);
+    GX_TRY(lcc_count_range(g, O, 0, n, tc.p, s));
+    hipLaunchKernelGGL(k_lcc_final, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->S.rp.p, tc.p, n, out.p);
     GX_TRY(check_launch("k_lcc_final"));
     GX_TRY(device_end(ctx));
     GX_HIP_TRY(hipMemcpy(lcc, out.p, n * 8, hipMemcpyDeviceToHost));
+    return GX_SUCCESS;
+}
+
+// ---- partitioned LCC: the graph is replicated, ranks split the orientation sources; the
+// caller sums the n counters of all ranks (one all-reduce) and finishes locally ----
+struct gx_lcc_part {
+    gx_graph *g = nullptr;
+    gx::LccOrient orient;
+};
+
+extern "C" int gx_lcc_part_create(gx_graph *g, gx_lcc_part **part) {
+    if (!g || !part) return fail(GX_NULL_POINTER, "gx_lcc_part_create: null argument");
+    GX_HIP_TRY(hipSetDevice(g->ctx->device));
+    GX_TRY(ensure_closure(g));
+    auto p = std::make_unique<gx_lcc_part>();
+    p->g = g;
+    if (g->n) GX_TRY(lcc_orient(g, p->orient, g->ctx->stream));
+    *part = p.release();
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_lcc_part_ranges(gx_lcc_part *part, int nranks, uint64_t *ranges) {
+    if (!part || !ranges) return fail(GX_NULL_POINTER, "gx_lcc_part_ranges: null argument");
+    if (nranks < 1) return fail(GX_INVALID_VALUE, "gx_lcc_part_ranges: nranks < 1");
+    gx_graph *g = part->g;
+    const int64_t n = (int64_t)g->n;
+    hipStream_t s = g->ctx->stream;
+    std::vector<uint64_t> w(n);
+    if (n) {
+        DBuf<uint64_t> work;
+        GX_TRY(work.alloc(n));
+        hipLaunchKernelGGL(k_lcc_work, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, part->orient.orp.p,
+                           part->orient.oci.p, n, work.p);
+        GX_TRY(check_launch("k_lcc_work"));
+        GX_HIP_TRY(hipMemcpyAsync(w.data(), work.p, n * 8, hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+    }
+    uint64_t total = 0;
+    for (uint64_t x : w) total += x;
+    ranges[0] = 0;
+    uint64_t acc = 0;
+    int64_t v = 0;
+    for (int k = 1; k < nranks; k++) {
+        const uint64_t target = (uint64_t)((long double)total * k / nranks);
+        while (v < n && acc + w[v] <= target) acc += w[v++];
+        ranges[k] = (uint64_t)v;
+    }
+    ranges[nranks] = (uint64_t)n;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_lcc_part_counts(gx_lcc_part *part, uint64_t v0, uint64_t v1, uint64_t *tc, void *stream) {
+    if (!part || !tc) return fail(GX_NULL_POINTER, "gx_lcc_part_counts: null argument");
+    gx_graph *g = part->g;
+    if (v0 > v1 || v1 > g->n) return fail(GX_INVALID_INDEX, "gx_lcc_part_counts: bad vertex range");
+    GX_HIP_TRY(hipSetDevice(g->ctx->device));
+    hipStream_t s = (hipStream_t)stream;   // NULL = the null stream (torch's default)
+    return lcc_count_range(g, part->orient, (int64_t)v0, (int64_t)v1, (unsigned long long *)tc, s);
+}
+
+extern "C" int gx_lcc_part_finish(gx_lcc_part *part, const uint64_t *tc, double *lcc, void *stream) {
+    if (!part || !tc || !lcc) return fail(GX_NULL_POINTER, "gx_lcc_part_finish: null argument");
+    gx_graph *g = part->g;
+    GX_HIP_TRY(hipSetDevice(g->ctx->device));
+    hipStream_t s = (hipStream_t)stream;   // NULL = the null stream (torch's default)
+    if (g->n) {
+        hipLaunchKernelGGL(k_lcc_final, dim3(grid_for(g->n, 256, 8192)), dim3(256), 0, s, g->S.rp.p,
+                           (const unsigned long long *)tc, (int64_t)g->n, lcc);
+        GX_TRY(check_launch("k_lcc_final"));
+    }
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_lcc_part_free(gx_lcc_part *part) {
+    delete part;
     return GX_SUCCESS;
 }

@@ -1,0 +1,325 @@
+"""Multi-GPU BFS, WCC, SSSP, CDLP and LCC: one process per GPU, the graph
+replicated on every rank, ranks owning contiguous vertex ranges, one RCCL collective per
+round.  (PageRank, whose exchange is the rank vector, lives in pr_partition.py.)
+
+The drivers below run a list of *local ranks* in lock step against a `Comm`:
+
+* TorchComm -- one local rank per process; collectives are torch.distributed (backend
+  "nccl" = RCCL over xGMI on MI355X, or gloo on CPU).
+* LocalComm -- all ranks in this process; a collective combines the per-rank tensors.
+  Used to run the partitioned GPU path with 1..k simulated ranks on one device.
+
+A backend supplies the per-rank device steps; GpuBackend binds the gx_*_part_* entry
+points of libgx (include/gx.h).  Every state array is full length on every rank:
+
+    BFS  : expand owned frontier rows -> next (uint8)   all-reduce MAX, commit levels
+    WCC  : hook owned rows' edges     -> parent (int32) all-reduce MIN, compress
+    SSSP : relax owned dropped rows   -> dist (int64 bit patterns of fp64) all-reduce MIN
+    CDLP : new labels of owned rows   -> all-gather of the owned slices
+    LCC  : triangle counts of owned orientation sources -> all-reduce SUM, finish
+
+Results are the single-GPU results (BFS levels, canonical WCC labels, the SSSP fixed point,
+the CDLP labels, exact LCC counts).  The reference has no distributed path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Sequence
+
+import numpy as np
+
+from .pr_partition import partition_rows
+
+INF_LEVEL = np.iinfo(np.int64).max
+
+
+# ---------------------------------------------------------------------------- comms
+class LocalComm:
+    """All ranks live in this process: combine the per-rank tensors elementwise."""
+
+    world_size = None   # = the number of local ranks
+
+    def all_reduce(self, ts: Sequence, op: str) -> None:
+        import torch
+        r = ts[0].clone()
+        for t in ts[1:]:
+            if op == "min":
+                r = torch.minimum(r, t)
+            elif op == "max":
+                r = torch.maximum(r, t)
+            elif op == "sum":
+                r = r + t
+            else:
+                raise ValueError(op)
+        for t in ts:
+            t.copy_(r)
+
+    def all_gather(self, outs: Sequence, ins: Sequence) -> None:
+        import torch
+        cat = torch.cat(list(ins))
+        for o in outs:
+            o.copy_(cat)
+
+
+class TorchComm:
+    """One local rank per process; torch.distributed collectives (RCCL or gloo)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world_size = dist.get_world_size(group)
+        self.ops = {"min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX, "sum": dist.ReduceOp.SUM}
+
+    def all_reduce(self, ts: Sequence, op: str) -> None:
+        for t in ts:
+            self.dist.all_reduce(t, op=self.ops[op], group=self.group)
+
+    def all_gather(self, outs: Sequence, ins: Sequence) -> None:
+        gloo = self.dist.get_backend(self.group) == "gloo"
+        for o, i in zip(outs, ins):
+            if gloo:   # gloo has no all_gather_into_tensor
+                parts = list(o.chunk(self.world_size))
+                self.dist.all_gather(parts, i, group=self.group)
+            else:
+                self.dist.all_gather_into_tensor(o, i, group=self.group)
+
+
+# ------------------------------------------------------------------------- backend
+class GpuBackend:
+    """gx_*_part_* of libgx on one device for one rank; tensors are torch CUDA tensors.
+    Steps launch on torch's current stream by default, so they are ordered with the
+    tensor initialisation and the collectives torch issues on that stream."""
+
+    def __init__(self, graph, stream_handle=None):
+        from . import _native as N
+        self.N = N
+        self.lib = N.lib()
+        self.g = graph.handle
+        if stream_handle is None:
+            import torch
+            stream_handle = lambda: torch.cuda.current_stream().cuda_stream   # noqa: E731
+        self.stream = stream_handle
+
+    @staticmethod
+    def _p(t):
+        return C.c_void_p(t.data_ptr())
+
+    def _s(self):
+        return C.c_void_p(self.stream())
+
+    def bfs_init(self, src, level):
+        self.N.check(self.lib.gx_bfs_part_init(self.g, src, self._p(level), self._s()), "gx_bfs_part_init")
+
+    def bfs_expand(self, v0, v1, level, cur, nxt):
+        self.N.check(self.lib.gx_bfs_part_expand(self.g, v0, v1, self._p(level), cur, self._p(nxt), self._s()),
+                     "gx_bfs_part_expand")
+
+    def bfs_commit(self, nxt, level, cur, count):
+        self.N.check(self.lib.gx_bfs_part_commit(self.g, self._p(nxt), self._p(level), cur, self._p(count),
+                                                 self._s()), "gx_bfs_part_commit")
+
+    def wcc_init(self, parent):
+        self.N.check(self.lib.gx_wcc_part_init(self.g, self._p(parent), self._s()), "gx_wcc_part_init")
+
+    def wcc_hook(self, v0, v1, parent, changed):
+        self.N.check(self.lib.gx_wcc_part_hook(self.g, v0, v1, self._p(parent), self._p(changed), self._s()),
+                     "gx_wcc_part_hook")
+
+    def wcc_compress(self, parent):
+        self.N.check(self.lib.gx_wcc_part_compress(self.g, self._p(parent), self._s()), "gx_wcc_part_compress")
+
+    def sssp_init(self, src, dist, prev):
+        self.N.check(self.lib.gx_sssp_part_init(self.g, src, self._p(dist), self._p(prev), self._s()),
+                     "gx_sssp_part_init")
+
+    def sssp_round(self, v0, v1, dist, prev, flag, active):
+        self.N.check(self.lib.gx_sssp_part_round(self.g, v0, v1, self._p(dist), self._p(prev), self._p(flag),
+                                                 self._p(active), self._s()), "gx_sssp_part_round")
+
+    def cdlp_part(self, v0, v1):
+        return _GpuCdlpPart(self, v0, v1)
+
+    def lcc_part(self):
+        return _GpuLccPart(self)
+
+
+class _GpuCdlpPart:
+    def __init__(self, be: GpuBackend, v0: int, v1: int):
+        self.be = be
+        self.h = C.c_void_p()
+        be.N.check(be.lib.gx_cdlp_part_create(be.g, v0, v1, C.byref(self.h)), "gx_cdlp_part_create")
+
+    def init(self, labels):
+        self.be.N.check(self.be.lib.gx_cdlp_part_init(self.h, self.be._p(labels), self.be._s()), "gx_cdlp_part_init")
+
+    def step(self, labels, nxt, changed):
+        self.be.N.check(self.be.lib.gx_cdlp_part_step(self.h, self.be._p(labels), self.be._p(nxt),
+                                                      self.be._p(changed), self.be._s()), "gx_cdlp_part_step")
+
+    def close(self):
+        if self.h:
+            self.be.lib.gx_cdlp_part_free(self.h)
+            self.h = C.c_void_p()
+
+
+class _GpuLccPart:
+    def __init__(self, be: GpuBackend):
+        self.be = be
+        self.h = C.c_void_p()
+        be.N.check(be.lib.gx_lcc_part_create(be.g, C.byref(self.h)), "gx_lcc_part_create")
+
+    def ranges(self, nranks: int) -> np.ndarray:
+        r = np.zeros(nranks + 1, dtype=np.uint64)
+        self.be.N.check(self.be.lib.gx_lcc_part_ranges(self.h, nranks, self.be.N.as_u64p(r)), "gx_lcc_part_ranges")
+        return r
+
+    def counts(self, v0, v1, tc):
+        self.be.N.check(self.be.lib.gx_lcc_part_counts(self.h, v0, v1, self.be._p(tc), self.be._s()),
+                        "gx_lcc_part_counts")
+
+    def finish(self, tc, out):
+        self.be.N.check(self.be.lib.gx_lcc_part_finish(self.h, self.be._p(tc), self.be._p(out), self.be._s()),
+                        "gx_lcc_part_finish")
+
+    def close(self):
+        if self.h:
+            self.be.lib.gx_lcc_part_free(self.h)
+            self.h = C.c_void_p()
+
+
+# -------------------------------------------------------------------------- drivers
+@dataclass
+class LocalRank:
+    backend: object
+    v0: int
+    v1: int
+    device: object
+    rank: int = 0   # global rank (index into the ranges of all ranks)
+
+
+def vertex_ranges(rowptr: np.ndarray, nranks: int) -> np.ndarray:
+    """Contiguous vertex ranges with ~nnz/nranks stored entries each (uint64[nranks+1])."""
+    return partition_rows(rowptr, nranks)
+
+
+def _zeros(rank: LocalRank, n: int, dtype):
+    import torch
+    return torch.zeros(n, dtype=dtype, device=rank.device)
+
+
+def bfs(ranks: List[LocalRank], comm, n: int, src: int):
+    """Level-synchronous top-down BFS; returns rank 0's level tensor (int64, INT64_MAX =
+    unreached)."""
+    import torch
+    level = [_zeros(r, n, torch.int64) for r in ranks]
+    for r, lv in zip(ranks, level):
+        r.backend.bfs_init(src, lv)
+    cur = 0
+    while True:
+        nxt = [_zeros(r, n, torch.uint8) for r in ranks]
+        for r, lv, nx in zip(ranks, level, nxt):
+            r.backend.bfs_expand(r.v0, r.v1, lv, cur, nx)
+        comm.all_reduce(nxt, "max")
+        count = [_zeros(r, 1, torch.int64) for r in ranks]
+        for r, lv, nx, c in zip(ranks, level, nxt, count):
+            r.backend.bfs_commit(nx, lv, cur, c)
+        if int(count[0].item()) == 0:   # identical on every rank (same inputs)
+            break
+        cur += 1
+    return level[0]
+
+
+def wcc(ranks: List[LocalRank], comm, n: int):
+    """Min-root hooking over owned rows + MIN exchange of the forest; returns parent (int32):
+    the smallest vertex id of each component."""
+    import torch
+    parent = [_zeros(r, n, torch.int32) for r in ranks]
+    for r, p in zip(ranks, parent):
+        r.backend.wcc_init(p)
+    while True:
+        changed = [_zeros(r, 1, torch.int32) for r in ranks]
+        for r, p, c in zip(ranks, parent, changed):
+            r.backend.wcc_hook(r.v0, r.v1, p, c)
+        comm.all_reduce(parent, "min")
+        for r, p in zip(ranks, parent):
+            r.backend.wcc_compress(p)
+        comm.all_reduce(changed, "max")
+        if int(changed[0].item()) == 0:
+            break
+    return parent[0]
+
+
+def sssp(ranks: List[LocalRank], comm, n: int, src: int):
+    """Frontier Bellman-Ford over owned rows + MIN exchange of the distance bits; returns the
+    distances (float64, inf = unreached)."""
+    import torch
+    dist = [_zeros(r, n, torch.int64) for r in ranks]
+    prev = [_zeros(r, n, torch.int64) for r in ranks]
+    flag = [_zeros(r, n, torch.uint8) for r in ranks]
+    for r, d, p in zip(ranks, dist, prev):
+        r.backend.sssp_init(src, d, p)
+    while True:
+        active = [_zeros(r, 1, torch.int64) for r in ranks]
+        for r, d, p, f, a in zip(ranks, dist, prev, flag, active):
+            r.backend.sssp_round(r.v0, r.v1, d, p, f, a)
+        comm.all_reduce(dist, "min")
+        comm.all_reduce(active, "sum")
+        if int(active[0].item()) == 0:
+            break
+    return dist[0].view(torch.float64)
+
+
+def cdlp(ranks: List[LocalRank], comm, n: int, iters: int, ranges: np.ndarray):
+    """Synchronous label propagation; each rank updates its range, the owned slices are
+    all-gathered.  `ranges` (uint64[nranks+1]) covers ALL ranks.  Returns labels (int32)."""
+    import torch
+    nranks = len(ranges) - 1
+    sizes = [int(ranges[k + 1] - ranges[k]) for k in range(nranks)]
+    chunk = max(1, max(sizes))
+    parts = [r.backend.cdlp_part(r.v0, r.v1) for r in ranks]
+    try:
+        labels = [_zeros(r, n, torch.int32) for r in ranks]
+        nxt = [_zeros(r, n, torch.int32) for r in ranks]
+        for p, lb in zip(parts, labels):
+            p.init(lb)
+        for _ in range(iters):
+            changed = [_zeros(r, 1, torch.int32) for r in ranks]
+            for p, lb, nx, c in zip(parts, labels, nxt, changed):
+                p.step(lb, nx, c)
+            send = [_zeros(r, chunk, torch.int32) for r in ranks]
+            for r, nx, sd in zip(ranks, nxt, send):
+                sd[:r.v1 - r.v0].copy_(nx[r.v0:r.v1])
+            gathered = [_zeros(r, chunk * nranks, torch.int32) for r in ranks]
+            comm.all_gather(gathered, send)
+            for g, lb in zip(gathered, labels):
+                lb.copy_(torch.cat([g[k * chunk:k * chunk + sizes[k]] for k in range(nranks)]))
+            comm.all_reduce(changed, "max")
+            if int(changed[0].item()) == 0:   # fixed point (LAGraph_cdlp.c:328-332)
+                break
+        return labels[0]
+    finally:
+        for p in parts:
+            p.close()
+
+
+def lcc(ranks: List[LocalRank], comm, n: int):
+    """Triangle counts per owned orientation source + SUM exchange; returns LCC (float64).
+    The ranks' vertex ranges are replaced by the work-balanced ones of gx_lcc_part_ranges."""
+    import torch
+    parts = [r.backend.lcc_part() for r in ranks]
+    try:
+        nranks = getattr(comm, "world_size", None) or len(ranks)
+        rng = parts[0].ranges(nranks)   # identical on every rank (same graph, same estimate)
+        tc = [_zeros(r, n, torch.int64) for r in ranks]
+        for r, p, t in zip(ranks, parts, tc):
+            p.counts(int(rng[r.rank]), int(rng[r.rank + 1]), t)
+        comm.all_reduce(tc, "sum")
+        out = [_zeros(r, n, torch.float64) for r in ranks]
+        for p, t, o in zip(parts, tc, out):
+            p.finish(t, o)
+        return out[0]
+    finally:
+        for p in parts:
+            p.close()
