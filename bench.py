@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--algorithm", default="pr", choices=["pr", "bfs", "wcc", "sssp", "cdlp", "lcc"],
                     help="pr = the headline (BASELINE configs[1]); the others measure configs 3-5 on 1 GPU")
     ap.add_argument("--graph", default=None, choices=sorted(PRESETS), help="synthetic stand-in (SURVEY.md 8d)")
+    ap.add_argument("--partitioned", action="store_true",
+                    help="run --algorithm through the multi-GPU (vertex-range) path even at N=1")
     return ap.parse_args()
 
 
@@ -215,13 +217,115 @@ def pmc_traffic(workload: str):
     return None
 
 
+def run_algorithm_distributed(args):
+    """--algorithm X on N GPUs (one process per GPU, torch.distributed.run): the graph is
+    replicated, ranks own vertex ranges and exchange state once per round over RCCL
+    (distributed.py).  `value` = work units of the whole job / max-over-ranks
+    time per call; scaling is strong (every N runs the same graph)."""
+    import torch
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    from ldbc_graphalytics_platforms_graphblas_amd import distributed as D
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    dist = None
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1 or "MASTER_ADDR" in os.environ:   # under torch.distributed.run: RCCL, even at N=1
+        import torch.distributed as dist
+        dist.init_process_group("nccl")
+    alg = args.algorithm
+    gname = args.graph or DEFAULT_GRAPH[alg]
+    P = PRESETS[gname]
+    csr = rmat(P["scale"], P["ef"], P["seed"], undirected=P["undirected"], weighted=(alg == "sssp"))
+    directed = not P["undirected"]
+    n, nnz = csr.n, csr.nnz
+    deg = np.diff(csr.rowptr.astype(np.int64))
+    src = int(np.argmax(deg))
+    ctx = A.Context(local_rank)
+    dev_name, cus = ctx.info()
+    G = A.Graph(ctx, csr, directed)
+    rng = D.vertex_ranges(csr.rowptr, world)
+    ranks = [D.LocalRank(D.GpuBackend(G), int(rng[rank]), int(rng[rank + 1]), device, rank)]
+    comm = D.TorchComm() if dist else D.LocalComm()
+
+    def call():
+        if alg == "bfs":
+            return D.bfs(ranks, comm, n, src)
+        if alg == "wcc":
+            return D.wcc(ranks, comm, n)
+        if alg == "sssp":
+            return D.sssp(ranks, comm, n, src)
+        if alg == "cdlp":
+            return D.cdlp(ranks, comm, n, args.iters, rng)
+        return D.lcc(ranks, comm, n)
+
+    def barrier():
+        torch.cuda.synchronize(device)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    for _ in range(max(1, args.warmup)):
+        out = call()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = call()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res = out.cpu().numpy()
+    t_call = elapsed / args.steps
+    if alg == "bfs":
+        reached = res != np.iinfo(np.int64).max
+        work, unit = int(deg[reached].sum()) // (1 if directed else 2), "TEPS"
+    elif alg == "cdlp":
+        work, unit = nnz * (2 if directed else 1) * args.iters, "edges/s"
+    else:
+        work, unit = nnz, "edges/s"
+    parity = None
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        threads = min(16, os.cpu_count() or 1)
+        ref = {"bfs": lambda: O.bfs(csr, src), "wcc": lambda: O.wcc(csr), "sssp": lambda: O.sssp(csr, src),
+               "cdlp": lambda: O.cdlp(csr, directed, args.iters, nthreads=threads),
+               "lcc": lambda: O.lcc(csr, directed, nthreads=threads)}[alg]()
+        got = res.astype(ref.dtype) if alg in ("wcc", "cdlp") else res
+        parity = "bit-exact" if np.array_equal(got, ref) else f"MISMATCH ({int((got != ref).sum())} vertices)"
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": work / t_call, "unit": unit, "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": t_call * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": {"sssp": "f64", "lcc": "int64+f64"}.get(alg, "int32"),
+            "data": f"synthetic (seeded R-MAT stand-in for {P['stands_for']}; no network for the real dataset)",
+            "config": {"workload": f"{alg.upper()} {gname} (partitioned)", "algorithm": alg, "graph": gname,
+                       "n": n, "nnz": nnz, "directed": directed, "source": src,
+                       "parallelism": f"replicated graph, {world} vertex ranges, RCCL exchange per round",
+                       "device": dev_name, "cus": cus},
+            "roofline": None, "cpu_baseline": None, "parity_vs_oracle": parity,
+            "note": "wall time per call incl. per-round host syncs; the single-GPU path is bench.py --algorithm X",
+        }
+        print(json.dumps(line), flush=True)
+    G.close()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import torch
 
     if args.algorithm != "pr":
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1:
-            raise SystemExit(f"--algorithm {args.algorithm} runs on one GPU (replicas only)")
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1 or args.partitioned:
+            return run_algorithm_distributed(args)
         return run_algorithm(args)
     if args.graph and args.graph != "SYN-7_5":
         P = PRESETS[args.graph]
