@@ -70,7 +70,7 @@ DEFAULT_GRAPH = {"pr": "SYN-7_5", "cdlp": "SYN-7_5", "bfs": "SYN-g500-22", "wcc"
 DOMINANT = {"bfs": "bfs_topdown", "wcc": "wcc_hook", "sssp": "sssp_relax", "cdlp": "cdlp_light",
             "lcc": "lcc_triangles"}
 KERNELS = {"bfs": ["bfs_topdown", "bfs_bottomup"], "wcc": ["wcc_sample", "wcc_hook", "wcc_compress"],
-           "sssp": ["sssp_relax", "sssp_advance"], "cdlp": ["cdlp_light", "cdlp_mid", "cdlp_heavy"],
+           "sssp": ["sssp_relax", "sssp_advance"], "cdlp": ["cdlp_tiny", "cdlp_small", "cdlp_light", "cdlp_mid2", "cdlp_mid", "cdlp_heavy"],
            "lcc": ["lcc_orient", "lcc_triangles"]}
 
 

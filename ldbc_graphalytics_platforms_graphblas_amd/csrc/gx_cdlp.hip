@@ -9,8 +9,10 @@
 // atomics that never lose an update (the reference's LDS insert is unlocked,
 // cdlp_kernel.cu:685-694), in-edges are included for directed graphs, and degree-0 vertices
 // are written (cdlp_kernel.cu:108-112, 1060-1063).
+//   deg <= 16        : one thread per vertex, labels and counts in registers.
 //   deg <= 64        : one wave per vertex, labels in registers, counts by 64 shuffles.
 //   deg <= kLdsHash/2: one wave per vertex, open-addressing hash table in that wave's LDS.
+//   deg <= 2048      : one 256-thread workgroup per vertex, 4K-slot LDS table (4 per CU).
 //   deg <= 8192      : one 1024-thread workgroup per vertex, 16K-slot hash table in LDS
 //                      (workgroups loop over the medium-vertex list, one per CU).
 //   larger           : 4096-label chunks histogrammed in LDS by separate workgroups, merged
@@ -65,7 +67,82 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     return v;
 }
 
-__global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a) {
+// Tiny vertices (deg <= kTiny, including isolated ones): one THREAD per vertex, labels in
+// registers (clamped loads, all in flight), mode by register compares -- 64 vertices per wave
+// instead of one (two thirds of the vertices of a power-law graph have degree <= 8).
+constexpr int kTiny = 16;
+
+__global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
+    bool any = false;
+    for (int64_t v = a.v0 + (int64_t)blockIdx.x * kCdlpBlock + threadIdx.x; v < a.v1;
+         v += (int64_t)gridDim.x * kCdlpBlock) {
+        const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
+        int64_t ib = 0, id = 0;
+        if (a.rpT) {
+            ib = a.rpT[v];
+            id = a.rpT[v + 1] - ib;
+        }
+        const int64_t d = od + id;
+        if (d > kTiny) continue;
+        const int32_t old = a.lab[v];
+        int32_t best = old;
+        if (d > 0) {
+            uint32_t L[kTiny];
+#pragma unroll
+            for (int k = 0; k < kTiny; k++) L[k] = (uint32_t)label_at(a, ob, od, ib, min((int64_t)k, d - 1));
+            uint32_t bc = 0, bl = kEmpty;
+#pragma unroll
+            for (int i = 0; i < kTiny; i++) {
+                uint32_t c = 0;
+#pragma unroll
+                for (int j = 0; j < kTiny; j++) c += (j < d && L[j] == L[i]) ? 1u : 0u;
+                if (i < d && (c > bc || (c == bc && L[i] < bl))) {
+                    bc = c;
+                    bl = L[i];
+                }
+            }
+            best = (int32_t)bl;
+        }
+        a.nxt[v] = best;
+        any |= best != old;
+    }
+    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) *a.changed = 1;
+}
+
+// Small vertices (kTiny < deg <= 64), from a list: one wave per vertex, labels in registers,
+// counts by shuffles; no LDS, so the kernel runs at full occupancy.
+__global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int32_t *__restrict__ sv,
+                                                           int32_t nsmall) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
+    const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
+    bool any = false;
+    for (int64_t i = gw; i < nsmall; i += nw) {
+        const int64_t v = sv[i];
+        const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
+        int64_t ib = 0, id = 0;
+        if (a.rpT) {
+            ib = a.rpT[v];
+            id = a.rpT[v + 1] - ib;
+        }
+        const int64_t d = od + id;
+        const int32_t old = a.lab[v];
+        const uint32_t my = lane < d ? (uint32_t)label_at(a, ob, od, ib, lane) : kEmpty;
+        uint32_t c = 0;
+        for (int j = 0; j < d; j++) c += (__shfl(my, j, kWave) == my) ? 1u : 0u;
+        const unsigned long long key = lane < d ? pack(c, my) : 0ull;
+        const int32_t best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+        if (lane == 0) {
+            a.nxt[v] = best;
+            any |= best != old;
+        }
+    }
+    if (any) *a.changed = 1;
+}
+
+// Light vertices (64 < deg <= kLdsHash/2), from a list: one wave per vertex.
+__global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int32_t *__restrict__ lv,
+                                                           int32_t nlight) {
     __shared__ uint32_t keys[kCdlpBlock / kWave][kLdsHash];
     __shared__ uint32_t cnts[kCdlpBlock / kWave][kLdsHash];
     const int lane = threadIdx.x & (kWave - 1);
@@ -75,7 +152,8 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a) {
     const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
     bool any = false;
-    for (int64_t v = a.v0 + gw; v < a.v1; v += nw) {
+    for (int64_t i = gw; i < nlight; i += nw) {
+        const int64_t v = lv[i];
         const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
         int64_t ib = 0, id = 0;
         if (a.rpT) {
@@ -83,7 +161,6 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a) {
             id = a.rpT[v + 1] - ib;
         }
         const int64_t d = od + id;
-        if (d > kLdsHash / 2) continue;   // heavy vertex: k_cdlp_heavy
         const int32_t old = a.lab[v];
         int32_t best;
         if (d == 0) {
@@ -238,10 +315,17 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_reduce(CdlpArgs a, con
 // Medium vertices (kLdsHash/2 < deg <= kMidMax): one 1024-thread workgroup per vertex with a
 // 16K-slot hash table in LDS (128 KiB, one workgroup per CU); workgroups loop over the
 // medium-vertex list so the table is reused without a relaunch.
+// Two sizes: 1024 threads / 16K slots (128 KiB, one workgroup per CU) for deg <= 8192, and
+// 256 threads / 4K slots (32 KiB, four workgroups per CU) for deg <= 2048, which keeps four
+// vertices in flight per CU for the many mid vertices near the bottom of the range.
 constexpr int kMidBlock = 1024;
 constexpr int kMidSlots = 16384;
 constexpr int64_t kMidMax = kMidSlots / 2;
+constexpr int kMid2Block = 256;
+constexpr int kMid2Slots = 4096;
+constexpr int64_t kMid2Max = kMid2Slots / 2;
 
+template <int kMidBlock, int kMidSlots>
 __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_t *__restrict__ mv, int32_t nmid) {
     __shared__ uint32_t K[kMidSlots];
     __shared__ uint32_t C[kMidSlots];
@@ -311,23 +395,32 @@ __global__ void k_cdlp_iota(int32_t *a, int64_t n) {
 // ones (chunked global hash segments); light vertices are found by k_cdlp_light itself.
 struct CdlpPlan {
     int64_t v0 = 0, v1 = 0;
-    size_t n_mid = 0, n_huge = 0, n_chunks = 0;
+    size_t n_light = 0, n_mid2 = 0, n_mid = 0, n_huge = 0, n_chunks = 0;
     int64_t total = 0;
-    DBuf<int32_t> d_hv, d_hl, d_mv, d_cvert;
+    DBuf<int32_t> d_hv, d_hl, d_mv, d_cvert, d_lv, d_mv2, d_sv;
+    size_t n_small = 0;
     DBuf<int64_t> d_hoff, d_cbeg;
     DBuf<uint32_t> gk, gc;
 };
 
 int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
-    std::vector<int32_t> hv, hl, mv, cvert;
+    std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv;
     std::vector<int64_t> hoff, cbeg;
     int64_t total = 0;
     for (int64_t v = v0; v < v1; v++) {
         int64_t d = g->A.h_rp[v + 1] - g->A.h_rp[v];
         if (g->directed) d += g->AT.h_rp[v + 1] - g->AT.h_rp[v];
-        if (d > kLdsHash / 2 && d <= kMidMax) {
+        if (d <= kTiny) {
+            // k_cdlp_tiny scans the range itself
+        } else if (d <= kWave) {
+            sv.push_back((int32_t)v);
+        } else if (d <= kLdsHash / 2) {
+            lv.push_back((int32_t)v);
+        } else if (d <= kMid2Max) {
+            mv2.push_back((int32_t)v);
+        } else if (d <= kMidMax) {
             mv.push_back((int32_t)v);
-        } else if (d > kMidMax) {
+        } else {
             int l2 = 1;
             while ((1ll << l2) < 2 * d) l2++;
             for (int64_t c = 0; c < d; c += kHugeChunk) {
@@ -342,6 +435,13 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
     }
     P.v0 = v0;
     P.v1 = v1;
+    P.n_light = lv.size();
+    P.n_small = sv.size();
+    if (!sv.empty()) {
+        GX_TRY(P.d_sv.alloc(sv.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_sv.p, sv.data(), sv.size() * 4, hipMemcpyHostToDevice, s));
+    }
+    P.n_mid2 = mv2.size();
     P.n_mid = mv.size();
     P.n_huge = hv.size();
     P.n_chunks = cvert.size();
@@ -364,6 +464,14 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
         GX_TRY(P.d_mv.alloc(mv.size()));
         GX_HIP_TRY(hipMemcpyAsync(P.d_mv.p, mv.data(), mv.size() * 4, hipMemcpyHostToDevice, s));
     }
+    if (!mv2.empty()) {
+        GX_TRY(P.d_mv2.alloc(mv2.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_mv2.p, mv2.data(), mv2.size() * 4, hipMemcpyHostToDevice, s));
+    }
+    if (!lv.empty()) {
+        GX_TRY(P.d_lv.alloc(lv.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_lv.p, lv.data(), lv.size() * 4, hipMemcpyHostToDevice, s));
+    }
     GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors go out of scope
     return GX_SUCCESS;
 }
@@ -376,15 +484,35 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
     CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr,
                cur,       nxt,       n,      changed, P.v0, P.v1};
     if (P.v1 > P.v0) {
-        KTimer kt(ctx, "cdlp_light", s);
-        hipLaunchKernelGGL(k_cdlp_light, dim3(grid_for((uint64_t)(P.v1 - P.v0) * kWave, kCdlpBlock, 8192)),
-                           dim3(kCdlpBlock), 0, s, a);
+        KTimer kt(ctx, "cdlp_tiny", s);
+        hipLaunchKernelGGL(k_cdlp_tiny, dim3(grid_for((uint64_t)(P.v1 - P.v0), kCdlpBlock, 8192)), dim3(kCdlpBlock),
+                           0, s, a);
     }
-    GX_TRY(check_launch("k_cdlp_light"));
+    GX_TRY(check_launch("k_cdlp_tiny"));
+    if (P.n_small) {
+        KTimer kt(ctx, "cdlp_small", s);
+        hipLaunchKernelGGL(k_cdlp_small, dim3(grid_for((uint64_t)P.n_small * kWave, kCdlpBlock, 8192)),
+                           dim3(kCdlpBlock), 0, s, a, P.d_sv.p, (int32_t)P.n_small);
+        GX_TRY(check_launch("k_cdlp_small"));
+    }
+    if (P.n_light) {
+        KTimer kt(ctx, "cdlp_light", s);
+        hipLaunchKernelGGL(k_cdlp_light, dim3(grid_for((uint64_t)P.n_light * kWave, kCdlpBlock, 8192)),
+                           dim3(kCdlpBlock), 0, s, a, P.d_lv.p, (int32_t)P.n_light);
+        GX_TRY(check_launch("k_cdlp_light"));
+    }
+    if (P.n_mid2) {
+        KTimer kt(ctx, "cdlp_mid2", s);
+        const unsigned grid2 = (unsigned)std::min<size_t>(P.n_mid2, (size_t)std::max(1, ctx->num_cus) * 4);
+        hipLaunchKernelGGL((k_cdlp_mid<kMid2Block, kMid2Slots>), dim3(grid2), dim3(kMid2Block), 0, s, a, P.d_mv2.p,
+                           (int32_t)P.n_mid2);
+        GX_TRY(check_launch("k_cdlp_mid2"));
+    }
     if (P.n_mid) {
         KTimer kt(ctx, "cdlp_mid", s);
         const unsigned mid_grid = (unsigned)std::min<size_t>(P.n_mid, (size_t)std::max(1, ctx->num_cus));
-        hipLaunchKernelGGL(k_cdlp_mid, dim3(mid_grid), dim3(kMidBlock), 0, s, a, P.d_mv.p, (int32_t)P.n_mid);
+        hipLaunchKernelGGL((k_cdlp_mid<kMidBlock, kMidSlots>), dim3(mid_grid), dim3(kMidBlock), 0, s, a, P.d_mv.p,
+                           (int32_t)P.n_mid);
         GX_TRY(check_launch("k_cdlp_mid"));
     }
     if (P.n_huge) {
