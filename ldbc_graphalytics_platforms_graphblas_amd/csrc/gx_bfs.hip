@@ -7,7 +7,8 @@
 //               one wave-aggregated atomic (ballot + mbcnt).
 //   bottom-up : (when the in-edges are resident: undirected graphs, or a directed graph
 //               whose transpose is already built) one thread per unvisited vertex scans its
-//               in-row until it meets a vertex of the current level.
+//               in-row, probing a bitmap of the current level (n/8 bytes, L2-resident) four
+//               neighbours at a time, until it meets a frontier vertex.
 // Direction switching follows Beamer's heuristic (alpha = 14, beta = 24).  Levels are
 // unique, so the result is bit-exact whatever the traversal order.
 #include "gx_device.h"
@@ -85,36 +86,124 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown(const int64_t *__rest
 }
 
 // bottom-up: one thread per vertex; in-edges in (rpi, cii)
-__global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__restrict__ rpi,
-                                                            const int32_t *__restrict__ cii,
-                                                            const int64_t *__restrict__ rpo,
-                                                            int64_t n, int32_t *level, int32_t depth,
-                                                            uint64_t *qout, uint32_t *qcount,
-                                                            unsigned long long *next_edges) {
-    unsigned long long edges = 0;
+// Frontier bitmap for bottom-up steps: bit u set iff level[u] == depth.  One 64-bit word per
+// wave (ballot over 64 consecutive vertices); n/8 bytes, so it stays resident in every XCD's
+// L2 while the bottom-up probes hit it at random (the int32 level array does not).
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_bitmap(const int32_t *__restrict__ level, int64_t n,
+                                                          int32_t depth, uint64_t *fb) {
     const int64_t stride = (int64_t)gridDim.x * kBfsBlock;
     const int64_t nround = (n + stride - 1) / stride;
     for (int64_t r = 0; r < nround; r++) {
         const int64_t v = r * stride + (int64_t)blockIdx.x * kBfsBlock + threadIdx.x;
-        bool take = false;
-        int64_t dv = 0;
-        if (v < n && level[v] < 0) {
-            for (int64_t k = rpi[v]; k < rpi[v + 1]; k++) {
-                if (level[cii[k]] == depth) {
-                    take = true;
-                    break;
-                }
-            }
-            if (take) {
-                level[v] = depth + 1;
-                dv = rpo[v + 1] - rpo[v];
-                edges += (unsigned long long)dv;
-            }
-        }
-        wave_append(take, (int32_t)v, chunks_of(dv), qout, qcount);
+        const uint64_t m = __ballot(v < n && level[v] == depth);
+        if ((threadIdx.x & (kWave - 1)) == 0 && v < n) fb[v >> 6] = m;
     }
-    for (int off = 32; off > 0; off >>= 1) edges += __shfl_xor(edges, off, kWave);
-    if ((threadIdx.x & (kWave - 1)) == 0 && edges) atomicAdd(next_edges, edges);
+}
+
+__device__ __forceinline__ uint32_t in_frontier(const uint64_t *__restrict__ fb, int32_t u) {
+    return (uint32_t)((fb[u >> 6] >> (u & 63)) & 1ull);
+}
+
+// bottom-up: one thread per unvisited vertex scans its in-row, 4 neighbours per step (four
+// independent bitmap probes in flight), until it meets a frontier vertex.  The next frontier
+// is left in `level` (no queue: a queue append per wave is one same-address atomic per wave,
+// ~11 ns each serialised, which dominated); found vertices and their out-edges are summed
+// per workgroup and leave as one atomic each.
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__restrict__ rpi,
+                                                            const int32_t *__restrict__ cii,
+                                                            const int64_t *__restrict__ rpo,
+                                                            const uint64_t *__restrict__ fb, int64_t n,
+                                                            int32_t *level, int32_t depth,
+                                                            unsigned long long *counters /* found, edges */) {
+    __shared__ unsigned long long red[2][kBfsBlock / kWave];
+    unsigned long long edges = 0, found = 0;
+    for (int64_t v = (int64_t)blockIdx.x * kBfsBlock + threadIdx.x; v < n; v += (int64_t)gridDim.x * kBfsBlock) {
+        if (level[v] >= 0) continue;
+        const int64_t b = rpi[v], e = rpi[v + 1];
+        bool take = false;
+        for (int64_t k = b; k < e && !take; k += 4) {
+            const int32_t u0 = cii[k];
+            const int32_t u1 = cii[min(k + 1, e - 1)];
+            const int32_t u2 = cii[min(k + 2, e - 1)];
+            const int32_t u3 = cii[min(k + 3, e - 1)];
+            // all four probes issue (no short-circuit), then one test
+            take = (in_frontier(fb, u0) | in_frontier(fb, u1) | in_frontier(fb, u2) | in_frontier(fb, u3)) != 0;
+        }
+        if (take) {
+            level[v] = depth + 1;
+            edges += (unsigned long long)(rpo[v + 1] - rpo[v]);
+            found++;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        edges += __shfl_xor(edges, off, kWave);
+        found += __shfl_xor(found, off, kWave);
+    }
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        red[0][w] = found;
+        red[1][w] = edges;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long f = 0, ed = 0;
+        for (int i = 0; i < kBfsBlock / kWave; i++) {
+            f += red[0][i];
+            ed += red[1][i];
+        }
+        if (f) atomicAdd(&counters[0], f);
+        if (ed) atomicAdd(&counters[1], ed);
+    }
+}
+
+// Top-down queue of the vertices at `depth` (after bottom-up steps), built per tile of
+// kQTile consecutive vertices: count the tile's items, one atomicAdd for its base, write.
+constexpr int64_t kQTile = 4096;
+
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue(const int64_t *__restrict__ rp,
+                                                               const int32_t *__restrict__ level, int64_t n,
+                                                               int32_t depth, uint64_t *queue, uint32_t *qcount) {
+    __shared__ uint32_t wsum[kBfsBlock / kWave];
+    __shared__ uint32_t tile_base;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    for (int64_t t0 = (int64_t)blockIdx.x * kQTile; t0 < n; t0 += (int64_t)gridDim.x * kQTile) {
+        const int64_t t1 = min(t0 + kQTile, n);
+        uint32_t mine = 0;
+        for (int64_t v = t0 + threadIdx.x; v < t1; v += kBfsBlock)
+            if (level[v] == depth) mine += chunks_of(rp[v + 1] - rp[v]);
+        for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off, kWave);
+        if (lane == 0) wsum[w] = mine;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (int i = 0; i < kBfsBlock / kWave; i++) tot += wsum[i];
+            tile_base = tot ? atomicAdd(qcount, tot) : 0u;
+        }
+        __syncthreads();
+        // second pass: ordered positions inside the tile, one 256-vertex step at a time
+        uint32_t base = tile_base;
+        for (int64_t v0 = t0; v0 < t1; v0 += kBfsBlock) {
+            const int64_t v = v0 + threadIdx.x;
+            const uint32_t k = (v < t1 && level[v] == depth) ? chunks_of(rp[v + 1] - rp[v]) : 0u;
+            uint32_t x = k;   // inclusive scan over the workgroup: waves, then wave totals
+#pragma unroll
+            for (int off = 1; off < kWave; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off, kWave);
+                if (lane >= off) x += y;
+            }
+            if (lane == kWave - 1) wsum[w] = x;
+            __syncthreads();
+            uint32_t before = 0, step = 0;
+            for (int i = 0; i < kBfsBlock / kWave; i++) {
+                if (i < w) before += wsum[i];
+                step += wsum[i];
+            }
+            const uint32_t pos = base + before + x - k;
+            for (uint32_t j = 0; j < k; j++) queue[pos + j] = ((uint64_t)(uint32_t)v << 32) | j;
+            base += step;
+            __syncthreads();
+        }
+    }
 }
 
 __global__ void k_bfs_seed(const int64_t *__restrict__ rp, int32_t *level, uint64_t *queue, uint32_t *qcount,
@@ -141,6 +230,10 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     DBuf<uint64_t> q0, q1;
     DBuf<uint32_t> qcount;
     DBuf<unsigned long long> nedges;
+    DBuf<uint64_t> fbits;
+    DBuf<unsigned long long> bucnt;
+    GX_TRY(fbits.alloc((n + 63) / 64));
+    GX_TRY(bucnt.alloc(2));
     const uint64_t qcap = (uint64_t)n + g->nnz / kChunk + 64;   // sum over vertices of ceil(deg / kChunk)
     GX_TRY(level.alloc(n));
     GX_TRY(q0.alloc(qcap));
@@ -165,36 +258,63 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         uint32_t pad;
         unsigned long long e;
     };
-    while (qsize > 0) {
+    // frontier: qsize vertices (top-down steps keep them as work items in q0; after a
+    // bottom-up step they are only in `level` until a top-down step needs the queue)
+    bool have_queue = true;
+    uint64_t fsize = qsize;
+    const unsigned bu_grid = (unsigned)std::min<int64_t>(grid_for(n, kBfsBlock, 8192), 1024);
+    while (fsize > 0) {
         // Beamer switch: TD -> BU when the frontier's edges exceed the unexplored ones / 14;
         // BU -> TD when the frontier shrinks below n / 24.
         if (in) {
             if (!bottom_up && mf > mu / 14) bottom_up = true;
-            else if (bottom_up && (int64_t)qsize < n / 24) bottom_up = false;
+            else if (bottom_up && (int64_t)fsize < n / 24) bottom_up = false;
         }
-        GX_HIP_TRY(hipMemsetAsync(qcount.p, 0, 4, s));
-        GX_HIP_TRY(hipMemsetAsync(nedges.p, 0, 8, s));
+        unsigned long long next_edges = 0;
+        uint64_t next_size = 0;
         if (bottom_up) {
             KTimer kt(ctx, "bfs_bottomup", s);
-            hipLaunchKernelGGL(k_bfs_bottomup, dim3(grid_for(n, kBfsBlock, 8192)), dim3(kBfsBlock), 0, s,
-                               in->rp.p, in->ci.p, g->A.rp.p, n, level.p, depth, q1.p, qcount.p,
-                               nedges.p);
+            GX_HIP_TRY(hipMemsetAsync(bucnt.p, 0, 16, s));
+            hipLaunchKernelGGL(k_bfs_bitmap, dim3(grid_for(n, kBfsBlock, 8192)), dim3(kBfsBlock), 0, s, level.p, n,
+                               depth, fbits.p);
+            hipLaunchKernelGGL(k_bfs_bottomup, dim3(bu_grid), dim3(kBfsBlock), 0, s, in->rp.p, in->ci.p, g->A.rp.p,
+                               fbits.p, n, level.p, depth, bucnt.p);
+            GX_TRY(check_launch("k_bfs_bottomup"));
+            unsigned long long c[2] = {0, 0};
+            GX_HIP_TRY(hipMemcpyAsync(c, bucnt.p, 16, hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            next_size = c[0];
+            next_edges = c[1];
+            have_queue = false;
         } else {
             KTimer kt(ctx, "bfs_topdown", s);
-            const uint64_t waves = qsize;
-            hipLaunchKernelGGL(k_bfs_topdown, dim3(grid_for(waves * kWave, kBfsBlock, 8192)),
-                               dim3(kBfsBlock), 0, s, g->A.rp.p, g->A.ci.p, q0.p, qsize, level.p, depth,
-                               q1.p, qcount.p, nedges.p);
+            if (!have_queue) {
+                GX_HIP_TRY(hipMemsetAsync(qcount.p, 0, 4, s));
+                hipLaunchKernelGGL(k_bfs_level_queue, dim3((unsigned)std::min<int64_t>((n + kQTile - 1) / kQTile, 2048)),
+                                   dim3(kBfsBlock), 0, s, g->A.rp.p, level.p, n, depth, q0.p, qcount.p);
+                GX_TRY(check_launch("k_bfs_level_queue"));
+                GX_HIP_TRY(hipMemcpyAsync(&qsize, qcount.p, 4, hipMemcpyDeviceToHost, s));
+                GX_HIP_TRY(hipStreamSynchronize(s));
+                have_queue = true;
+            }
+            GX_HIP_TRY(hipMemsetAsync(qcount.p, 0, 4, s));
+            GX_HIP_TRY(hipMemsetAsync(nedges.p, 0, 8, s));
+            hipLaunchKernelGGL(k_bfs_topdown, dim3(grid_for((uint64_t)qsize * kWave, kBfsBlock, 8192)),
+                               dim3(kBfsBlock), 0, s, g->A.rp.p, g->A.ci.p, q0.p, qsize, level.p, depth, q1.p,
+                               qcount.p, nedges.p);
+            GX_TRY(check_launch("k_bfs_topdown"));
+            Counters c{};
+            GX_HIP_TRY(hipMemcpyAsync(&c.q, qcount.p, 4, hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipMemcpyAsync(&c.e, nedges.p, 8, hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            qsize = c.q;
+            next_size = c.q;   // work items (~ vertices; a hub counts once per 256 edges)
+            next_edges = c.e;
+            std::swap(q0.p, q1.p);
         }
-        GX_TRY(check_launch("bfs step"));
-        Counters c{};
-        GX_HIP_TRY(hipMemcpyAsync(&c.q, qcount.p, 4, hipMemcpyDeviceToHost, s));
-        GX_HIP_TRY(hipMemcpyAsync(&c.e, nedges.p, 8, hipMemcpyDeviceToHost, s));
-        GX_HIP_TRY(hipStreamSynchronize(s));
         mu = mu > mf ? mu - mf : 0;
-        mf = c.e;
-        qsize = c.q;
-        std::swap(q0.p, q1.p);
+        mf = next_edges;
+        fsize = next_size;
         depth++;
     }
     GX_TRY(device_end(ctx));

@@ -13,6 +13,7 @@
 //   deg <= 64        : one wave per vertex, labels in registers, counts by 64 shuffles.
 //   deg <= kLdsHash/2: one wave per vertex, open-addressing hash table in that wave's LDS.
 //   deg <= 2048      : one 256-thread workgroup per vertex, 4K-slot LDS table (4 per CU).
+//   deg <= 4096      : one 512-thread workgroup per vertex, 8K-slot LDS table (2 per CU).
 //   deg <= 8192      : one 1024-thread workgroup per vertex, 16K-slot hash table in LDS
 //                      (workgroups loop over the medium-vertex list, one per CU).
 //   larger           : 4096-label chunks histogrammed in LDS by separate workgroups, merged
@@ -283,21 +284,30 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
     }
 }
 
-__global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_reduce(CdlpArgs a, const int32_t *__restrict__ hv,
+// Reduce of the huge vertices' global tables, one workgroup per kHugeSeg-slot segment: the
+// segment's best (count << 32 | ~label) goes to the vertex's key by a 64-bit atomicMax, and
+// every slot read is reset, so the tables are clean for the next iteration without a memset.
+constexpr int64_t kHugeSeg = 16384;
+
+__global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_reduce(const int32_t *__restrict__ sv,
+                                                                 const int64_t *__restrict__ sbeg,
                                                                  const int64_t *__restrict__ hoff,
-                                                                 const int32_t *__restrict__ hlog2,
-                                                                 const uint32_t *gkeys, const uint32_t *gcnts) {
+                                                                 const int32_t *__restrict__ hlog2, uint32_t *gkeys,
+                                                                 uint32_t *gcnts, unsigned long long *vkey) {
     __shared__ unsigned long long red[kHugeBlock / kWave];
-    const int64_t v = hv[blockIdx.x];
-    const int64_t ts = 1ll << hlog2[blockIdx.x];
-    const uint32_t *GK = gkeys + hoff[blockIdx.x];
-    const uint32_t *GC = gcnts + hoff[blockIdx.x];
+    const int32_t hi = sv[blockIdx.x];
+    const int64_t ts = 1ll << hlog2[hi];
+    const int64_t s0 = sbeg[blockIdx.x], s1 = min(s0 + kHugeSeg, ts);
+    uint32_t *GK = gkeys + hoff[hi];
+    uint32_t *GC = gcnts + hoff[hi];
     unsigned long long key = 0;
-    for (int64_t s = threadIdx.x; s < ts; s += kHugeBlock) {
+    for (int64_t s = s0 + threadIdx.x; s < s1; s += kHugeBlock) {
         const uint32_t c = GC[s];
         if (c) {
             const unsigned long long kk = pack(c, GK[s]);
             key = kk > key ? kk : key;
+            GC[s] = 0;
+            GK[s] = kEmpty;
         }
     }
     key = wave_max_u64(key);
@@ -306,10 +316,24 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_reduce(CdlpArgs a, con
     if (threadIdx.x == 0) {
         unsigned long long m = red[0];
         for (int w = 1; w < kHugeBlock / kWave; w++) m = red[w] > m ? red[w] : m;
-        const int32_t best = (int32_t)(kEmpty - (uint32_t)(m & 0xffffffffu));
+        if (m) atomicMax(&vkey[hi], m);
+    }
+}
+
+__global__ void k_cdlp_huge_final(CdlpArgs a, const int32_t *__restrict__ hv, int32_t nhuge,
+                                  unsigned long long *vkey) {
+    for (int32_t hi = blockIdx.x * blockDim.x + threadIdx.x; hi < nhuge; hi += gridDim.x * blockDim.x) {
+        const int64_t v = hv[hi];
+        const int32_t best = (int32_t)(kEmpty - (uint32_t)(vkey[hi] & 0xffffffffu));
+        vkey[hi] = 0;   // clean for the next iteration
         a.nxt[v] = best;
         if (best != a.lab[v]) *a.changed = 1;
     }
+}
+
+__global__ void k_cdlp_fill_u32(uint32_t *p, uint32_t v, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = v;
 }
 
 // Medium vertices (kLdsHash/2 < deg <= kMidMax): one 1024-thread workgroup per vertex with a
@@ -324,6 +348,9 @@ constexpr int64_t kMidMax = kMidSlots / 2;
 constexpr int kMid2Block = 256;
 constexpr int kMid2Slots = 4096;
 constexpr int64_t kMid2Max = kMid2Slots / 2;
+constexpr int kMid4Block = 512;   // deg <= 4096: 8K slots (64 KiB), two workgroups per CU
+constexpr int kMid4Slots = 8192;
+constexpr int64_t kMid4Max = kMid4Slots / 2;
 
 template <int kMidBlock, int kMidSlots>
 __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_t *__restrict__ mv, int32_t nmid) {
@@ -397,14 +424,18 @@ struct CdlpPlan {
     int64_t v0 = 0, v1 = 0;
     size_t n_light = 0, n_mid2 = 0, n_mid = 0, n_huge = 0, n_chunks = 0;
     int64_t total = 0;
-    DBuf<int32_t> d_hv, d_hl, d_mv, d_cvert, d_lv, d_mv2, d_sv;
-    size_t n_small = 0;
+    DBuf<int32_t> d_hv, d_hl, d_mv, d_cvert, d_lv, d_mv2, d_sv, d_mv4;
+    size_t n_small = 0, n_mid4 = 0;
     DBuf<int64_t> d_hoff, d_cbeg;
     DBuf<uint32_t> gk, gc;
+    DBuf<unsigned long long> vkey;      // per huge vertex best key (zero between iterations)
+    DBuf<int32_t> d_segv;               // huge-table segments: vertex index, first slot
+    DBuf<int64_t> d_segb;
+    size_t n_seg = 0;
 };
 
 int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
-    std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv;
+    std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv, mv4;
     std::vector<int64_t> hoff, cbeg;
     int64_t total = 0;
     for (int64_t v = v0; v < v1; v++) {
@@ -418,6 +449,8 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
             lv.push_back((int32_t)v);
         } else if (d <= kMid2Max) {
             mv2.push_back((int32_t)v);
+        } else if (d <= kMid4Max) {
+            mv4.push_back((int32_t)v);
         } else if (d <= kMidMax) {
             mv.push_back((int32_t)v);
         } else {
@@ -437,6 +470,11 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
     P.v1 = v1;
     P.n_light = lv.size();
     P.n_small = sv.size();
+    P.n_mid4 = mv4.size();
+    if (!mv4.empty()) {
+        GX_TRY(P.d_mv4.alloc(mv4.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_mv4.p, mv4.data(), mv4.size() * 4, hipMemcpyHostToDevice, s));
+    }
     if (!sv.empty()) {
         GX_TRY(P.d_sv.alloc(sv.size()));
         GX_HIP_TRY(hipMemcpyAsync(P.d_sv.p, sv.data(), sv.size() * 4, hipMemcpyHostToDevice, s));
@@ -452,6 +490,25 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
         GX_TRY(P.d_hoff.alloc(hoff.size()));
         GX_TRY(P.gk.alloc(total));
         GX_TRY(P.gc.alloc(total));
+        GX_TRY(P.vkey.alloc(hv.size()));
+        GX_HIP_TRY(hipMemsetAsync(P.vkey.p, 0, hv.size() * 8, s));
+        // the tables start clean; k_cdlp_huge_reduce resets every slot it consumes
+        hipLaunchKernelGGL(k_cdlp_fill_u32, dim3(grid_for(total, 256, 8192)), dim3(256), 0, s, P.gk.p, kEmpty, total);
+        GX_TRY(check_launch("k_cdlp_fill_u32"));
+        GX_HIP_TRY(hipMemsetAsync(P.gc.p, 0, (size_t)total * 4, s));
+        std::vector<int32_t> segv;
+        std::vector<int64_t> segb;
+        for (size_t i = 0; i < hv.size(); i++)
+            for (int64_t b = 0; b < (1ll << hl[i]); b += kHugeSeg) {
+                segv.push_back((int32_t)i);
+                segb.push_back(b);
+            }
+        P.n_seg = segv.size();
+        GX_TRY(P.d_segv.alloc(segv.size()));
+        GX_TRY(P.d_segb.alloc(segb.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_segv.p, segv.data(), segv.size() * 4, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_segb.p, segb.data(), segb.size() * 8, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
         GX_TRY(P.d_cvert.alloc(cvert.size()));
         GX_TRY(P.d_cbeg.alloc(cbeg.size()));
         GX_HIP_TRY(hipMemcpyAsync(P.d_hv.p, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, s));
@@ -508,6 +565,13 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
                            (int32_t)P.n_mid2);
         GX_TRY(check_launch("k_cdlp_mid2"));
     }
+    if (P.n_mid4) {
+        KTimer kt(ctx, "cdlp_mid4", s);
+        const unsigned grid4 = (unsigned)std::min<size_t>(P.n_mid4, (size_t)std::max(1, ctx->num_cus) * 2);
+        hipLaunchKernelGGL((k_cdlp_mid<kMid4Block, kMid4Slots>), dim3(grid4), dim3(kMid4Block), 0, s, a, P.d_mv4.p,
+                           (int32_t)P.n_mid4);
+        GX_TRY(check_launch("k_cdlp_mid4"));
+    }
     if (P.n_mid) {
         KTimer kt(ctx, "cdlp_mid", s);
         const unsigned mid_grid = (unsigned)std::min<size_t>(P.n_mid, (size_t)std::max(1, ctx->num_cus));
@@ -517,14 +581,15 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
     }
     if (P.n_huge) {
         KTimer kt(ctx, "cdlp_heavy", s);
-        GX_HIP_TRY(hipMemsetAsync(P.gk.p, 0xff, (size_t)P.total * 4, s));
-        GX_HIP_TRY(hipMemsetAsync(P.gc.p, 0, (size_t)P.total * 4, s));
         hipLaunchKernelGGL(k_cdlp_huge_insert, dim3((unsigned)P.n_chunks), dim3(kHugeBlock), 0, s, a, P.d_hv.p,
                            P.d_hoff.p, P.d_hl.p, P.d_cvert.p, P.d_cbeg.p, P.gk.p, P.gc.p);
         GX_TRY(check_launch("k_cdlp_huge_insert"));
-        hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)P.n_huge), dim3(kHugeBlock), 0, s, a, P.d_hv.p,
-                           P.d_hoff.p, P.d_hl.p, P.gk.p, P.gc.p);
+        hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)P.n_seg), dim3(kHugeBlock), 0, s, P.d_segv.p,
+                           P.d_segb.p, P.d_hoff.p, P.d_hl.p, P.gk.p, P.gc.p, P.vkey.p);
         GX_TRY(check_launch("k_cdlp_huge_reduce"));
+        hipLaunchKernelGGL(k_cdlp_huge_final, dim3(grid_for(P.n_huge, 64, 1024)), dim3(64), 0, s, a, P.d_hv.p,
+                           (int32_t)P.n_huge, P.vkey.p);
+        GX_TRY(check_launch("k_cdlp_huge_final"));
     }
     return GX_SUCCESS;
 }
@@ -547,21 +612,39 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     CdlpPlan P;
     GX_TRY(cdlp_plan(g, 0, n, P, s));
     DBuf<int32_t> la, lb;
-    DBuf<int> changed;
+    DBuf<int> changed;   // one flag per iteration
     GX_TRY(la.alloc(n));
     GX_TRY(lb.alloc(n));
-    GX_TRY(changed.alloc(1));
+    GX_TRY(changed.alloc(std::max(iters, 1)));
+    GX_HIP_TRY(hipMemsetAsync(changed.p, 0, sizeof(int) * std::max(iters, 1), s));
     hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, la.p, n);
     GX_TRY(check_launch("k_cdlp_iota"));
+    // Early exit at a fixed point (LAGraph_cdlp.c:328-332), checked one iteration late:
+    // iteration it is queued before the host waits for iteration it-1's flag, so the check
+    // never drains the stream.  An iteration run after a fixed point changes no label.
+    int *hflag = nullptr;
+    GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&hflag), sizeof(int) * std::max(iters, 1)));
+    std::unique_ptr<int, void (*)(int *)> hflag_guard(hflag, [](int *p) { (void)hipHostFree(p); });
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    GX_HIP_TRY(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+    GX_HIP_TRY(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+    struct EvGuard {
+        hipEvent_t *e;
+        ~EvGuard() {
+            (void)hipEventDestroy(e[0]);
+            (void)hipEventDestroy(e[1]);
+        }
+    } ev_guard{ev};
     int32_t *cur = la.p, *nxt = lb.p;
     for (int it = 0; it < iters; it++) {
-        GX_HIP_TRY(hipMemsetAsync(changed.p, 0, sizeof(int), s));
-        GX_TRY(cdlp_iteration(g, P, cur, nxt, changed.p, s));
-        int h_changed = 0;
-        GX_HIP_TRY(hipMemcpyAsync(&h_changed, changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
-        GX_HIP_TRY(hipStreamSynchronize(s));
+        GX_TRY(cdlp_iteration(g, P, cur, nxt, changed.p + it, s));
+        GX_HIP_TRY(hipMemcpyAsync(hflag + it, changed.p + it, sizeof(int), hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipEventRecord(ev[it & 1], s));
         std::swap(cur, nxt);
-        if (!h_changed) break;   // fixed point (LAGraph_cdlp.c:328-332)
+        if (it >= 1) {
+            GX_HIP_TRY(hipEventSynchronize(ev[(it - 1) & 1]));
+            if (!hflag[it - 1]) break;   // iteration it-1 was a fixed point, so is cur
+        }
     }
     GX_TRY(device_end(ctx));
     std::vector<int32_t> h(n);
