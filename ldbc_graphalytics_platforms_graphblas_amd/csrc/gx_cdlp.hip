@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
         a.nxt[v] = best;
         any |= best != old;
     }
-    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) *a.changed = 1;
+    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag(a.changed);
 }
 
 // Small vertices (kTiny < deg <= 64), from a list: one wave per vertex, labels in registers,
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
             any |= best != old;
         }
     }
-    if (any) *a.changed = 1;
+    if (any) raise_flag(a.changed);
 }
 
 // Light vertices (64 < deg <= kLdsHash/2), from a list: one wave per vertex.
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
             any |= best != old;
         }
     }
-    if (any) *a.changed = 1;
+    if (any) raise_flag(a.changed);
 }
 
 // Huge vertices (deg > kMidMax): the label multiset is cut into kHugeChunk-label chunks; a
@@ -327,7 +327,7 @@ __global__ void k_cdlp_huge_final(CdlpArgs a, const int32_t *__restrict__ hv, in
         const int32_t best = (int32_t)(kEmpty - (uint32_t)(vkey[hi] & 0xffffffffu));
         vkey[hi] = 0;   // clean for the next iteration
         a.nxt[v] = best;
-        if (best != a.lab[v]) *a.changed = 1;
+        if (best != a.lab[v]) raise_flag(a.changed);
     }
 }
 
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
         }
         __syncthreads();   // the table is cleared for the next vertex
     }
-    if (any) *a.changed = 1;
+    if (any) raise_flag(a.changed);
 }
 
 __global__ void k_cdlp_iota(int32_t *a, int64_t n) {

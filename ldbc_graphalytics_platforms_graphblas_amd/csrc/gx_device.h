@@ -101,9 +101,13 @@ struct gx_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string device_name;
     int num_cus = 0;
+    // auxiliary streams for independent kernels of one step (fork/join by events), lazy
+    hipStream_t aux[2] = {nullptr, nullptr};
+    hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
 };
 
 namespace gx {
+int ensure_aux_streams(gx_ctx *ctx);
 // SSSP edge layout: every row of A split into its light (w < delta) edges, then its heavy
 // ones; built once per graph and delta by gx_sssp.
 struct SsspLayout {
@@ -203,6 +207,14 @@ __device__ __forceinline__ int64_t row_of_edge(const int64_t *rp, int64_t nrows,
         else hi = mid;
     }
     return lo;
+}
+
+// Raise a shared "something changed" flag.  Thousands of waves writing one word serialise
+// on one L2 channel (~11 ns per access, MI355X_MICROARCH.md "dequeue"); only a wave that
+// still reads it clear writes it (idempotent, so the race is harmless).
+__device__ __forceinline__ void raise_flag(int *flag) {
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 typedef int gx_v4i __attribute__((ext_vector_type(4)));

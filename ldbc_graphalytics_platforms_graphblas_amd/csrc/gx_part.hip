@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kPartBlock) void k_wccp_hook(const int64_t *__restr
             }
         }
     }
-    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) *changed = 1;
+    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag(changed);
 }
 
 __global__ __launch_bounds__(kPartBlock) void k_wccp_compress(int32_t *parent, int64_t n) {

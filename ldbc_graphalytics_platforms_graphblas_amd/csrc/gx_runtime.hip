@@ -66,6 +66,11 @@ extern "C" int gx_free(gx_ctx *ctx) {
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    for (int i = 0; i < 2; i++) {
+        if (ctx->aux[i]) (void)hipStreamDestroy(ctx->aux[i]);
+        if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
+    }
+    if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return GX_SUCCESS;
@@ -100,6 +105,16 @@ int collect_timings(gx_ctx *ctx) {
         ctx->event_pool.push_back(p.b);
     }
     ctx->pending.clear();
+    return GX_SUCCESS;
+}
+
+int ensure_aux_streams(gx_ctx *ctx) {
+    if (ctx->aux[0]) return GX_SUCCESS;
+    for (int i = 0; i < 2; i++) {
+        GX_HIP_TRY(hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking));
+        GX_HIP_TRY(hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming));
+    }
+    GX_HIP_TRY(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
     return GX_SUCCESS;
 }
 

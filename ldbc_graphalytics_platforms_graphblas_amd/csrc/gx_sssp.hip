@@ -157,7 +157,10 @@ __device__ __forceinline__ void wave_min_to(unsigned long long m, unsigned long 
         const unsigned long long o = __shfl_xor(m, off, kWave);
         m = o < m ? o : m;
     }
-    if ((threadIdx.x & (kWave - 1)) == 0 && m != ~0ull) atomicMin(dst, m);
+    // one shared word for the whole grid: only a wave that would lower it issues the atomic
+    if ((threadIdx.x & (kWave - 1)) == 0 && m != ~0ull &&
+        m < __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin(dst, m);
 }
 
 // Per-wave LDS staging of queue pushes.  Improvements are sparse (well under 1% of the

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(kWccBlock) void k_wcc_hook(const int64_t *__restric
             }
         }
     }
-    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) *changed = 1;
+    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag(changed);
 }
 
 __global__ __launch_bounds__(kWccBlock) void k_wcc_compress(int32_t *parent, int64_t n) {
