@@ -70,7 +70,7 @@ DEFAULT_GRAPH = {"pr": "SYN-7_5", "cdlp": "SYN-7_5", "bfs": "SYN-g500-22", "wcc"
 DOMINANT = {"bfs": "bfs_topdown", "wcc": "wcc_hook", "sssp": "sssp_relax", "cdlp": "cdlp_light",
             "lcc": "lcc_triangles"}
 KERNELS = {"bfs": ["bfs_topdown", "bfs_bottomup"], "wcc": ["wcc_sample", "wcc_hook", "wcc_compress"],
-           "sssp": ["sssp_relax", "sssp_advance"], "cdlp": ["cdlp_tiny", "cdlp_small", "cdlp_light", "cdlp_mid2", "cdlp_mid", "cdlp_heavy"],
+           "sssp": ["sssp_relax", "sssp_advance"], "cdlp": ["cdlp_tiny", "cdlp_small", "cdlp_light", "cdlp_mid2", "cdlp_mid4", "cdlp_mid", "cdlp_heavy"],
            "lcc": ["lcc_orient", "lcc_triangles"]}
 
 
@@ -133,17 +133,23 @@ def run_algorithm(args):
     first_ms = (time.perf_counter() - t1) * 1e3
     for _ in range(max(0, args.warmup - 1)):
         call()
-    ctx.reset_kernel_stats()
-    ctx.set_kernel_timing(True)
+    # timed steps without per-kernel events (they add a gap around every launch)
     dev_ms = []
     t1 = time.perf_counter()
     for _ in range(args.steps):
         out = call()
         dev_ms.append(ctx.last_device_ms())
     wall = time.perf_counter() - t1
+    # per-kernel breakdown from a separate instrumented pass
+    stat_runs = max(1, min(args.steps, 3))
+    ctx.reset_kernel_stats()
+    ctx.set_kernel_timing(True)
+    for _ in range(stat_runs):
+        call()
     ctx.set_kernel_timing(False)
     kl, kms = ctx.kernel_stats(DOMINANT[alg])
-    per_kernel = {k: dict(zip(("launches", "ms_per_run"), (lambda t: (t[0], t[1] / max(1, args.steps)))(
+    kms = kms * args.steps / stat_runs   # scaled to the timed steps (dominant_kernel_ms_per_run divides)
+    per_kernel = {k: dict(zip(("launches", "ms_per_run"), (lambda t: (t[0], t[1] / stat_runs))(
         ctx.kernel_stats(k)))) for k in KERNELS[alg]}
     t_dev = float(np.median(dev_ms)) / 1e3
     # work units and algorithmic bytes (SURVEY.md 8d / BASELINE.md)
@@ -168,16 +174,17 @@ def run_algorithm(args):
         sdeg = np.diff(cl.rowptr.astype(np.int64))
         work = cl.nnz
         # bytes of the algorithm that runs (gx_lcc.hip): orientation reads every closure entry
-        # (5 B) and the degree of its column (16 B) and writes the kept ones (5 B); the
-        # triangle pass builds a table from O(v) (5 B/entry + 16 B row bounds per oriented edge)
-        # and probes every entry of O(u) for each oriented edge (v, u) (5 B each).
+        # (5 B) and the degree of its column (16 B) and writes the kept ones packed (4 B); the
+        # transpose writes, radix-sorts (3 passes of 8-B keys) and unpacks the m oriented
+        # entries (~68 B each); the triangle pass probes every entry of O(v) for each oriented
+        # edge (v, u) (4 B each, sum of |O(v)|^2) and builds a table from O(u) per work item.
         srows = np.repeat(np.arange(n, dtype=np.int64), sdeg)
         scols = cl.colidx.astype(np.int64)
         keep = (sdeg[scols] > sdeg[srows]) | ((sdeg[scols] == sdeg[srows]) & (scols > srows))
         odeg = np.bincount(srows[keep], minlength=n).astype(np.int64)
         m_or = int(keep.sum())
-        wedges = int(odeg[scols[keep]].sum())
-        nbytes = 26 * cl.nnz + 5 * m_or + 21 * m_or + 5 * wedges + 8 * (n + 1)
+        probes = int((odeg.astype(np.float64) ** 2).sum())
+        nbytes = 25 * cl.nnz + 68 * m_or + 4 * probes + 8 * (n + 1)
         ref_model_bytes = 4 * int((sdeg.astype(np.float64) ** 2).sum()) + 4 * cl.nnz + 8 * (n + 1)
         unit = "edges/s"
     if alg != "lcc":

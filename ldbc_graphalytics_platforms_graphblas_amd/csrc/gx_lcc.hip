@@ -10,14 +10,18 @@
 // Triangles are enumerated once each on the degree-ordered orientation O of S (edge v->u
 // when (deg u, u) > (deg v, v)), whose out-degrees are at most sqrt(2|E|).
 //   orientation : stream compaction of S by 64-entry slabs (ballot masks + one scan);
-//   triangles   : per vertex v, O(v) goes into an LDS hash table (flag byte kept with each
-//                 key); the lists O(u), u in O(v), are walked by load-balanced waves and every
-//                 x probed: a hit is the triangle {v, u, x}.  The three contributions are
-//                 summed on chip (v in a register, u in an LDS slot per u, x in its hash slot)
-//                 and leave as one 64-bit atomic per (vertex, contribution target).
-//   tiers       : wave per vertex for |O(v)| <= kWaveMax, workgroup per vertex up to
-//                 kBlockMax, a merge-intersection fallback beyond (not reached on
-//                 degree-oriented graphs below ~2^25 edges).
+//   transpose   : I = O^T by a radix sort of (x, v) keys on x only.
+//   triangles   : each triangle {v, u, x} (v -> u, v -> x, u -> x) is found at its middle
+//                 vertex u: O(u) goes into an LDS hash table (flag popcount kept with each
+//                 key) and the lists O(v), v in I(u), are walked by load-balanced waves and
+//                 probed -- sum |O(v)| probes over oriented edges, 0.45x of probing O(u) per
+//                 (v, u).  The three contributions are summed on chip (u in a register, v in
+//                 an LDS slot per v, x in its hash slot) and leave as one 64-bit atomic per
+//                 (work item, contribution target).
+//   tiers       : work item (u, 64 in-neighbours) per wave for |O(u)| <= kWaveMax, (u, 256)
+//                 per workgroup up to kBlockMax, a merge-intersection fallback beyond (not
+//                 reached on degree-oriented graphs below ~2^25 edges).
+// Oriented entries are packed as (vertex << 2) | popcount(flag), so n < 2^29.
 // Counts are exact integers, so the result is deterministic and equal to the oracle bit for
 // bit (one fp64 division per vertex).
 #include <cstring>
@@ -109,78 +113,140 @@ __global__ void k_orient_rows(const int64_t *__restrict__ rp, const uint64_t *__
         orp[v] = kept_before(mask, cpre, rp[v]);
 }
 
+// Oriented entries are packed as (x << 2) | popcount(flag): one 4-byte load per probe.
 __global__ __launch_bounds__(kLccBlock) void k_orient_scatter(const int32_t *__restrict__ ci,
                                                               const uint8_t *__restrict__ fl, int64_t nnz,
                                                               const uint64_t *__restrict__ mask,
-                                                              const int64_t *__restrict__ cpre, int32_t *oci,
-                                                              uint8_t *ofl) {
+                                                              const int64_t *__restrict__ cpre, uint32_t *ocode) {
     for (int64_t e = (int64_t)blockIdx.x * kLccBlock + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * kLccBlock) {
         const int64_t sl = e / kWave;
         const int b = (int)(e % kWave);
         const uint64_t m = mask[sl];
         if ((m >> b) & 1ull) {
             const int64_t pos = cpre[sl] + (b ? __popcll(m & ((1ull << b) - 1)) : 0);
-            oci[pos] = ci[e];
-            ofl[pos] = fl[e];
+            ocode[pos] = ((uint32_t)ci[e] << 2) | (uint32_t)__popc(fl[e]);
         }
     }
 }
 
-// ---- vertex tiers ----
-// Tier lists.  A workgroup stages one kClassTile-vertex tile in LDS (positions from LDS
-// atomics) and flushes each tier with one global atomic: per-wave appends to three shared
-// counters were ~65K same-address atomics, ~11 ns each serialised.
+// In-orientation I (transpose of O): keys (x << 32) | (v << 2 | p) for every v -> x.
+__global__ void k_orient_tkeys(const int64_t *__restrict__ orp, const uint32_t *__restrict__ ocode, int64_t n,
+                               uint64_t *keys) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        for (int64_t k = orp[v]; k < orp[v + 1]; k++) {
+            const uint32_t c = ocode[k];
+            keys[k] = ((uint64_t)(c >> 2) << 32) | (((uint32_t)v << 2) | (c & 3u));
+        }
+}
+
+__global__ void k_keys_to_in_csr(const uint64_t *__restrict__ keys, int64_t m, int64_t n, int64_t *irp,
+                                 uint32_t *icode) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t <= n) {
+        const uint64_t target = (uint64_t)t << 32;
+        int64_t lo = 0, hi = m;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < target) lo = mid + 1;
+            else hi = mid;
+        }
+        irp[t] = lo;
+    }
+    for (int64_t k = t; k < m; k += (int64_t)gridDim.x * blockDim.x) icode[k] = (uint32_t)(keys[k] & 0xffffffffu);
+}
+
+// ---- work items ----
+// A triangle {v, u, x} with v -> u, v -> x, u -> x (ranks v < u < x) is found once, at its
+// middle vertex u: O(u) goes into an LDS hash table and the lists O(v) of the in-neighbours
+// v in I(u) are probed against it.  This costs sum over oriented edges (v, u) of |O(v)|,
+// less than half of probing O(u) for every (v, u) (2.4 G -> 1.06 G probes on SYN-cit).
+// Work item = (u, chunk of I(u)): kWaveGroup in-neighbours for the wave tier, kBlockGroup for
+// the workgroup tier, so hubs with large in-lists spread over many waves.
+constexpr int kWaveGroup = kWave;
+constexpr int kBlockGroup = kLccBlock;
 constexpr int kClassTile = 4096;
 
-__global__ __launch_bounds__(kLccBlock) void k_lcc_classify(const int64_t *__restrict__ orp, int64_t v0, int64_t v1,
-                                                            int32_t *wave_list, uint32_t *wave_cnt,
-                                                            int32_t *block_list, uint32_t *block_cnt,
-                                                            int32_t *big_list, uint32_t *big_cnt) {
-    __shared__ int32_t buf[3][kClassTile];
-    __shared__ uint32_t cnt[3], base[3];
-    int32_t *lists[3] = {wave_list, block_list, big_list};
+__global__ __launch_bounds__(kLccBlock) void k_lcc_items(const int64_t *__restrict__ orp,
+                                                         const int64_t *__restrict__ irp, int64_t v0, int64_t v1,
+                                                         uint64_t *wave_items, uint32_t *wave_cnt,
+                                                         uint64_t *block_items, uint32_t *block_cnt,
+                                                         int32_t *big_list, uint32_t *big_cnt) {
+    __shared__ uint32_t tot[3], base[3], off[3];
     uint32_t *gcnt[3] = {wave_cnt, block_cnt, big_cnt};
     for (int64_t t0 = v0 + (int64_t)blockIdx.x * kClassTile; t0 < v1; t0 += (int64_t)gridDim.x * kClassTile) {
         const int64_t t1 = min(t0 + (int64_t)kClassTile, v1);
-        if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
-        __syncthreads();
-        for (int64_t v = t0 + threadIdx.x; v < t1; v += kLccBlock) {
-            const int64_t d = orp[v + 1] - orp[v];
-            const int tier = d <= 0 ? -1 : (d <= kWaveMax ? 0 : (d <= kBlockMax ? 1 : 2));
-            if (tier >= 0) buf[tier][atomicAdd(&cnt[tier], 1u)] = (int32_t)v;
+        if (threadIdx.x < 3) {
+            tot[threadIdx.x] = 0;
+            off[threadIdx.x] = 0;
         }
         __syncthreads();
-        if (threadIdx.x < 3) base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(gcnt[threadIdx.x], cnt[threadIdx.x]) : 0u;
-        __syncthreads();
-        for (int t = 0; t < 3; t++)
-            for (uint32_t i = threadIdx.x; i < cnt[t]; i += kLccBlock) lists[t][base[t] + i] = buf[t][i];
-        __syncthreads();
+        for (int pass = 0; pass < 2; pass++) {
+            for (int64_t u = t0 + threadIdx.x; u < t1; u += kLccBlock) {
+                const int64_t d = orp[u + 1] - orp[u], e = irp[u + 1] - irp[u];
+                if (d == 0 || e == 0) continue;
+                const int tier = d <= kWaveMax ? 0 : (d <= kBlockMax ? 1 : 2);
+                const uint32_t ni = tier == 0 ? (uint32_t)((e + kWaveGroup - 1) / kWaveGroup)
+                                              : (tier == 1 ? (uint32_t)((e + kBlockGroup - 1) / kBlockGroup) : 1u);
+                if (pass == 0) {
+                    atomicAdd(&tot[tier], ni);
+                } else {
+                    const uint32_t pos = base[tier] + atomicAdd(&off[tier], ni);
+                    if (tier == 2) {
+                        big_list[pos] = (int32_t)u;
+                    } else {
+                        uint64_t *items = tier == 0 ? wave_items : block_items;
+                        for (uint32_t j = 0; j < ni; j++) items[pos + j] = ((uint64_t)u << 32) | j;
+                    }
+                }
+            }
+            __syncthreads();
+            if (pass == 0 && threadIdx.x < 3)
+                base[threadIdx.x] = tot[threadIdx.x] ? atomicAdd(gcnt[threadIdx.x], tot[threadIdx.x]) : 0u;
+            __syncthreads();
+        }
     }
 }
 
-// Probe the lists O(u) of the u in [g, g + 64) of O(v) (one u per lane) against the table.
-// Lanes walk the concatenated lists 64 entries at a time (owner lane by shuffle search).
-// Returns v's contribution; u's contributions go to ucnt[lane], x's into the table values.
-__device__ __forceinline__ unsigned long long probe_group(const int64_t *__restrict__ orp,
-                                                          const int32_t *__restrict__ oci,
-                                                          const uint8_t *__restrict__ ofl, int64_t b, int64_t d,
-                                                          int64_t g, const int32_t *hkey, uint32_t *hval,
-                                                          uint32_t hmask, uint32_t *ucnt, int lane) {
-    const int64_t i = g + lane;
-    const bool has = i < d;
-    const int32_t u = has ? oci[b + i] : 0;
-    const uint32_t fvu = has ? (uint32_t)__popc(ofl[b + i]) : 0u;
-    const int64_t ub = has ? orp[u] : 0;
-    const int32_t ul = has ? (int32_t)(orp[u + 1] - ub) : 0;
-    int32_t incl = ul;
+// Build the hash table of O(u) (key x, value popcount(u,x) << 30) with `nthreads` threads.
+__device__ __forceinline__ void table_build(const int64_t *__restrict__ orp, const uint32_t *__restrict__ ocode,
+                                            int32_t u, int32_t *hkey, uint32_t *hval, uint32_t slots, int tid,
+                                            int nthreads) {
+    const int64_t b = orp[u], d = orp[u + 1] - b;
+    const uint32_t hmask = slots - 1;
+    for (int64_t i = tid; i < d; i += nthreads) {
+        const uint32_t c = ocode[b + i];
+        const int32_t x = (int32_t)(c >> 2);
+        uint32_t h = hash_slot(x, hmask);
+        while (atomicCAS(&hkey[h], -1, x) != -1) h = (h + 1) & hmask;   // keys of a row are distinct
+        hval[h] = (c & 3u) << 30;
+    }
+}
+
+// Probe the lists O(v) of the (up to 64) in-neighbours icode[ib .. ie) of u, one per lane,
+// against the table of O(u).  Lanes walk the concatenated lists 64 entries at a time (owner
+// lane by shuffle search).  Returns u's contribution; v's go to vcnt[lane], x's into the
+// table values.
+__device__ __forceinline__ unsigned long long probe_in_group(const int64_t *__restrict__ orp,
+                                                             const uint32_t *__restrict__ ocode,
+                                                             const uint32_t *__restrict__ icode, int64_t ib,
+                                                             int64_t ie, const int32_t *hkey, uint32_t *hval,
+                                                             uint32_t hmask, uint32_t *vcnt, int lane) {
+    const int64_t i = ib + lane;
+    const bool has = i < ie;
+    const uint32_t ic = has ? icode[i] : 0u;
+    const int32_t v = (int32_t)(ic >> 2);
+    const uint32_t p_vu = ic & 3u;
+    const int64_t vb = has ? orp[v] : 0;
+    const int32_t vl = has ? (int32_t)(orp[v + 1] - vb) : 0;
+    int32_t incl = vl;
 #pragma unroll
     for (int off = 1; off < kWave; off <<= 1) {
         const int32_t y = __shfl_up(incl, off, kWave);
         if (lane >= off) incl += y;
     }
     const int32_t total = __shfl(incl, kWave - 1, kWave);
-    const int32_t excl = incl - ul;
-    unsigned long long tv = 0;
+    const int32_t excl = incl - vl;
+    unsigned long long tu = 0;
     for (int32_t e0 = 0; e0 < total; e0 += kWave) {
         const int32_t e_raw = e0 + lane;
         const bool act = e_raw < total;
@@ -189,146 +255,144 @@ __device__ __forceinline__ unsigned long long probe_group(const int64_t *__restr
 #pragma unroll
         for (int step = kWave / 2; step > 0; step >>= 1)
             if (__shfl(incl, o + step - 1, kWave) <= e) o += step;
-        const int64_t k = __shfl(ub, o, kWave) + (e - __shfl(excl, o, kWave));
-        const uint32_t f_vu = __shfl(fvu, o, kWave);
-        const int32_t x = oci[k];
-        const uint32_t f_ux = (uint32_t)__popc(ofl[k]);
+        const int64_t k = __shfl(vb, o, kWave) + (e - __shfl(excl, o, kWave));
+        const uint32_t f_vu = __shfl(p_vu, o, kWave);
+        const uint32_t c = ocode[k];
         if (act) {
+            const int32_t x = (int32_t)(c >> 2);
             uint32_t h = hash_slot(x, hmask);
             int32_t key;
             while ((key = hkey[h]) != x && key != -1) h = (h + 1) & hmask;
             if (key == x) {
-                tv += f_ux;                                      // v: directions between u and x
-                atomicAdd(&ucnt[o], hval[h] >> 30);              // u: directions between v and x
-                atomicAdd(&hval[h], f_vu);                       // x: directions between v and u
+                tu += c & 3u;                              // u: directions between v and x
+                atomicAdd(&vcnt[o], hval[h] >> 30);        // v: directions between u and x
+                atomicAdd(&hval[h], f_vu);                 // x: directions between v and u
             }
         }
     }
-    return tv;
+    return tu;
+}
+
+__device__ __forceinline__ uint32_t table_slots(int64_t d) {
+    uint32_t slots = 64;
+    while (slots < 2 * (uint32_t)d) slots <<= 1;
+    return slots;
 }
 
 __global__ __launch_bounds__(kLccBlock) void k_lcc_wave(const int64_t *__restrict__ orp,
-                                                        const int32_t *__restrict__ oci,
-                                                        const uint8_t *__restrict__ ofl,
-                                                        const int32_t *__restrict__ list, uint32_t count,
+                                                        const uint32_t *__restrict__ ocode,
+                                                        const int64_t *__restrict__ irp,
+                                                        const uint32_t *__restrict__ icode,
+                                                        const uint64_t *__restrict__ items, uint32_t count,
                                                         unsigned long long *tc) {
     __shared__ int32_t s_key[kWavesPerBlock][kWaveSlots];
     __shared__ uint32_t s_val[kWavesPerBlock][kWaveSlots];
-    __shared__ uint32_t s_ucnt[kWavesPerBlock][kWave];
+    __shared__ uint32_t s_vcnt[kWavesPerBlock][kWave];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
     int32_t *hkey = s_key[wv];
     uint32_t *hval = s_val[wv];
-    uint32_t *ucnt = s_ucnt[wv];
+    uint32_t *vcnt = s_vcnt[wv];
     const uint32_t nw = gridDim.x * kWavesPerBlock;
     for (uint32_t li = blockIdx.x * kWavesPerBlock + wv; li < count; li += nw) {
-        const int32_t v = list[li];
-        const int64_t b = orp[v], d = orp[v + 1] - b;
-        uint32_t slots = 64;
-        while (slots < 2 * (uint32_t)d) slots <<= 1;
-        const uint32_t hmask = slots - 1;
+        const uint64_t item = items[li];
+        const int32_t u = (int32_t)(item >> 32);
+        const int64_t ib = irp[u] + (int64_t)(uint32_t)item * kWaveGroup, ie = min(irp[u + 1], ib + kWaveGroup);
+        const uint32_t slots = table_slots(orp[u + 1] - orp[u]);
         for (uint32_t s = lane; s < slots; s += kWave) {
             hkey[s] = -1;
             hval[s] = 0;
         }
+        vcnt[lane] = 0;
         wave_sync_lds();
-        for (int64_t i = lane; i < d; i += kWave) {
-            const int32_t x = oci[b + i];
-            uint32_t h = hash_slot(x, hmask);
-            while (atomicCAS(&hkey[h], -1, x) != -1) h = (h + 1) & hmask;   // keys of a row are distinct
-            hval[h] = (uint32_t)__popc(ofl[b + i]) << 30;
-        }
+        table_build(orp, ocode, u, hkey, hval, slots, lane, kWave);
         wave_sync_lds();
-        unsigned long long tv = 0;
-        for (int64_t g = 0; g < d; g += kWave) {
-            ucnt[lane] = 0;
-            wave_sync_lds();
-            tv += probe_group(orp, oci, ofl, b, d, g, hkey, hval, hmask, ucnt, lane);
-            wave_sync_lds();
-            const uint32_t c = ucnt[lane];
-            if (c && g + lane < d) atomicAdd(&tc[oci[b + g + lane]], (unsigned long long)c);
-        }
+        unsigned long long tu = probe_in_group(orp, ocode, icode, ib, ie, hkey, hval, slots - 1, vcnt, lane);
+        wave_sync_lds();
+        const uint32_t c = vcnt[lane];
+        if (c && ib + lane < ie) atomicAdd(&tc[icode[ib + lane] >> 2], (unsigned long long)c);
         for (uint32_t s = lane; s < slots; s += kWave) {
-            const uint32_t c = hval[s] & kCntMask;
-            if (c) atomicAdd(&tc[hkey[s]], (unsigned long long)c);
+            const uint32_t cx = hval[s] & kCntMask;
+            if (cx) atomicAdd(&tc[hkey[s]], (unsigned long long)cx);
         }
-        for (int off = 32; off > 0; off >>= 1) tv += __shfl_xor(tv, off, kWave);
-        if (lane == 0 && tv) atomicAdd(&tc[v], tv);
+        for (int off = 32; off > 0; off >>= 1) tu += __shfl_xor(tu, off, kWave);
+        if (lane == 0 && tu) atomicAdd(&tc[u], tu);
         wave_sync_lds();
     }
 }
 
 __global__ __launch_bounds__(kLccBlock) void k_lcc_block(const int64_t *__restrict__ orp,
-                                                         const int32_t *__restrict__ oci,
-                                                         const uint8_t *__restrict__ ofl,
-                                                         const int32_t *__restrict__ list, uint32_t count,
+                                                         const uint32_t *__restrict__ ocode,
+                                                         const int64_t *__restrict__ irp,
+                                                         const uint32_t *__restrict__ icode,
+                                                         const uint64_t *__restrict__ items, uint32_t count,
                                                          unsigned long long *tc) {
     __shared__ int32_t hkey[kBlockSlots];
     __shared__ uint32_t hval[kBlockSlots];
-    __shared__ uint32_t s_ucnt[kWavesPerBlock][kWave];
+    __shared__ uint32_t s_vcnt[kWavesPerBlock][kWave];
+    __shared__ unsigned long long s_tu[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-    uint32_t *ucnt = s_ucnt[wv];
+    uint32_t *vcnt = s_vcnt[wv];
     for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
-        const int32_t v = list[li];
-        const int64_t b = orp[v], d = orp[v + 1] - b;
-        uint32_t slots = 64;
-        while (slots < 2 * (uint32_t)d) slots <<= 1;
-        const uint32_t hmask = slots - 1;
+        const uint64_t item = items[li];
+        const int32_t u = (int32_t)(item >> 32);
+        const int64_t ib0 = irp[u] + (int64_t)(uint32_t)item * kBlockGroup, ie0 = min(irp[u + 1], ib0 + kBlockGroup);
+        const uint32_t slots = table_slots(orp[u + 1] - orp[u]);
         for (uint32_t s = threadIdx.x; s < slots; s += kLccBlock) {
             hkey[s] = -1;
             hval[s] = 0;
         }
+        vcnt[lane] = 0;
         __syncthreads();
-        for (int64_t i = threadIdx.x; i < d; i += kLccBlock) {
-            const int32_t x = oci[b + i];
-            uint32_t h = hash_slot(x, hmask);
-            while (atomicCAS(&hkey[h], -1, x) != -1) h = (h + 1) & hmask;
-            hval[h] = (uint32_t)__popc(ofl[b + i]) << 30;
-        }
+        table_build(orp, ocode, u, hkey, hval, slots, threadIdx.x, kLccBlock);
         __syncthreads();
-        unsigned long long tv = 0;
-        for (int64_t g = (int64_t)wv * kWave; g < d; g += kLccBlock) {
-            ucnt[lane] = 0;
-            wave_sync_lds();
-            tv += probe_group(orp, oci, ofl, b, d, g, hkey, hval, hmask, ucnt, lane);
-            wave_sync_lds();
-            const uint32_t c = ucnt[lane];
-            if (c && g + lane < d) atomicAdd(&tc[oci[b + g + lane]], (unsigned long long)c);
-        }
+        const int64_t ib = ib0 + (int64_t)wv * kWave, ie = min(ie0, ib + kWave);
+        unsigned long long tu = 0;
+        if (ib < ie) tu = probe_in_group(orp, ocode, icode, ib, ie, hkey, hval, slots - 1, vcnt, lane);
+        wave_sync_lds();
+        const uint32_t c = vcnt[lane];
+        if (c && ib + lane < ie) atomicAdd(&tc[icode[ib + lane] >> 2], (unsigned long long)c);
+        for (int off = 32; off > 0; off >>= 1) tu += __shfl_xor(tu, off, kWave);
+        if (lane == 0) s_tu[wv] = tu;
         __syncthreads();
         for (uint32_t s = threadIdx.x; s < slots; s += kLccBlock) {
-            const uint32_t c = hval[s] & kCntMask;
-            if (c) atomicAdd(&tc[hkey[s]], (unsigned long long)c);
+            const uint32_t cx = hval[s] & kCntMask;
+            if (cx) atomicAdd(&tc[hkey[s]], (unsigned long long)cx);
         }
-        for (int off = 32; off > 0; off >>= 1) tv += __shfl_xor(tv, off, kWave);
-        if (lane == 0 && tv) atomicAdd(&tc[v], tv);
+        if (threadIdx.x == 0) {
+            unsigned long long t = 0;
+            for (int w = 0; w < kWavesPerBlock; w++) t += s_tu[w];
+            if (t) atomicAdd(&tc[u], t);
+        }
         __syncthreads();
     }
 }
 
-// Fallback for |O(v)| > kBlockMax: thread per oriented edge (v, u) of one vertex, merge
-// intersection of the sorted lists O(v) and O(u).
-__global__ __launch_bounds__(kLccBlock) void k_lcc_merge_row(const int64_t *__restrict__ orp,
-                                                             const int32_t *__restrict__ oci,
-                                                             const uint8_t *__restrict__ ofl, int32_t v,
-                                                             unsigned long long *tc) {
-    const int64_t b = orp[v], ie_v = orp[v + 1];
-    for (int64_t e = b + (int64_t)blockIdx.x * kLccBlock + threadIdx.x; e < ie_v;
-         e += (int64_t)gridDim.x * kLccBlock) {
-        const int32_t u = oci[e];
-        const unsigned cvu = __popc(ofl[e]);
-        int64_t i = b, j = orp[u];
-        const int64_t je = orp[u + 1];
+// Fallback for |O(u)| > kBlockMax: thread per in-neighbour v of one u, merge intersection of
+// the sorted lists O(v) and O(u).
+__global__ __launch_bounds__(kLccBlock) void k_lcc_merge_in(const int64_t *__restrict__ orp,
+                                                            const uint32_t *__restrict__ ocode,
+                                                            const int64_t *__restrict__ irp,
+                                                            const uint32_t *__restrict__ icode, int32_t u,
+                                                            unsigned long long *tc) {
+    const int64_t ub = orp[u], ue = orp[u + 1];
+    for (int64_t t = irp[u] + (int64_t)blockIdx.x * kLccBlock + threadIdx.x; t < irp[u + 1];
+         t += (int64_t)gridDim.x * kLccBlock) {
+        const uint32_t ic = icode[t];
+        const int32_t v = (int32_t)(ic >> 2);
+        const uint32_t p_vu = ic & 3u;
+        int64_t i = orp[v], j = ub;
+        const int64_t ie = orp[v + 1];
         unsigned long long tv = 0, tu = 0;
-        while (i < ie_v && j < je) {
-            const int32_t x = oci[i], y = oci[j];
-            if (x < y) {
+        while (i < ie && j < ue) {
+            const uint32_t a = ocode[i], b = ocode[j];
+            if ((a >> 2) < (b >> 2)) {
                 i++;
-            } else if (x > y) {
+            } else if ((a >> 2) > (b >> 2)) {
                 j++;
             } else {
-                tv += __popc(ofl[j]);
-                tu += __popc(ofl[i]);
-                atomicAdd(&tc[x], (unsigned long long)cvu);
+                tv += b & 3u;   // v: directions between u and x
+                tu += a & 3u;   // u: directions between v and x
+                atomicAdd(&tc[a >> 2], (unsigned long long)p_vu);
                 i++;
                 j++;
             }
@@ -338,16 +402,22 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_merge_row(const int64_t *__re
     }
 }
 
-// Work estimate of vertex v for balancing ranks: |O(v)| + sum over u in O(v) of |O(u)|.
-__global__ void k_lcc_work(const int64_t *__restrict__ orp, const int32_t *__restrict__ oci, int64_t n,
-                           uint64_t *work) {
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
-        uint64_t w = 1;
-        for (int64_t k = orp[v]; k < orp[v + 1]; k++) {
-            const int32_t u = oci[k];
-            w += 1 + (uint64_t)(orp[u + 1] - orp[u]);
+// Work estimate of vertex u for balancing ranks: sum over v in I(u) of 1 + |O(v)|, plus
+// |O(u)|.  One wave per vertex (hubs have long in-lists).
+__global__ __launch_bounds__(kLccBlock) void k_lcc_work(const int64_t *__restrict__ orp,
+                                                        const int64_t *__restrict__ irp,
+                                                        const uint32_t *__restrict__ icode, int64_t n,
+                                                        uint64_t *work) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t u = ((int64_t)blockIdx.x * kLccBlock + threadIdx.x) / kWave; u < n; u += nw) {
+        uint64_t w = 0;
+        for (int64_t k = irp[u] + lane; k < irp[u + 1]; k += kWave) {
+            const int32_t v = (int32_t)(icode[k] >> 2);
+            w += 1 + (uint64_t)(orp[v + 1] - orp[v]);
         }
-        work[v] = w;
+        for (int off = 32; off > 0; off >>= 1) w += __shfl_xor(w, off, kWave);
+        if (lane == 0) work[u] = w + 1 + (uint64_t)(orp[u + 1] - orp[u]);
     }
 }
 
@@ -360,12 +430,12 @@ __global__ void k_lcc_final(const int64_t *__restrict__ srp, const unsigned long
     }
 }
 
-// Degree-ordered orientation O of the closure S (CSR: orp, oci, ofl).
+// Degree-ordered orientation O of the closure S (CSR orp / ocode) and its transpose I
+// (irp / icode, entries (v << 2) | popcount of the v -> u entry).
 struct LccOrient {
     int64_t m = 0;
-    DBuf<int64_t> orp;
-    DBuf<int32_t> oci;
-    DBuf<uint8_t> ofl;
+    DBuf<int64_t> orp, irp;
+    DBuf<uint32_t> ocode, icode;
 };
 
 int lcc_orient(gx_graph *g, LccOrient &O, hipStream_t s) {
@@ -381,6 +451,7 @@ int lcc_orient(gx_graph *g, LccOrient &O, hipStream_t s) {
     GX_TRY(cnt.alloc(nslabs + 1));
     GX_TRY(cpre.alloc(nslabs + 1));
     GX_TRY(O.orp.alloc(n + 1));
+    GX_TRY(O.irp.alloc(n + 1));
     GX_HIP_TRY(hipMemsetAsync(cnt.p + nslabs, 0, sizeof(int32_t), s));
     GX_HIP_TRY(hipMemsetAsync(mask.p + nslabs, 0, sizeof(uint64_t), s));
     KTimer kt(ctx, "lcc_orient", s);
@@ -400,32 +471,56 @@ int lcc_orient(gx_graph *g, LccOrient &O, hipStream_t s) {
     GX_TRY(check_launch("k_orient_rows"));
     GX_HIP_TRY(hipMemcpyAsync(&O.m, O.orp.p + n, 8, hipMemcpyDeviceToHost, s));
     GX_HIP_TRY(hipStreamSynchronize(s));
-    GX_TRY(O.oci.alloc(O.m));
-    GX_TRY(O.ofl.alloc(O.m));
+    GX_TRY(O.ocode.alloc(O.m, 16));
+    GX_TRY(O.icode.alloc(O.m, 16));
     if (nnz)
         hipLaunchKernelGGL(k_orient_scatter, dim3(grid_for(nnz, kLccBlock, 16384)), dim3(kLccBlock), 0, s, S.ci.p,
-                           S.flag.p, nnz, mask.p, cpre.p, O.oci.p, O.ofl.p);
+                           S.flag.p, nnz, mask.p, cpre.p, O.ocode.p);
     GX_TRY(check_launch("k_orient_scatter"));
+    // transpose: sort (x, v|p) keys by x only (bits 32 .. 32+log2 n), then row pointers
+    DBuf<uint64_t> k0, k1;
+    GX_TRY(k0.alloc(O.m + 1));
+    GX_TRY(k1.alloc(O.m + 1));
+    if (O.m) {
+        hipLaunchKernelGGL(k_orient_tkeys, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, O.orp.p, O.ocode.p, n,
+                           k0.p);
+        GX_TRY(check_launch("k_orient_tkeys"));
+        int hb = 1;
+        while ((1ll << hb) <= n) hb++;
+        size_t sbytes = 0;
+        GX_HIP_TRY(rocprim::radix_sort_keys(nullptr, sbytes, k0.p, k1.p, (size_t)O.m, 32, 32 + hb, s));
+        DBuf<char> stmp;
+        GX_TRY(stmp.alloc(sbytes));
+        GX_HIP_TRY(rocprim::radix_sort_keys(stmp.p, sbytes, k0.p, k1.p, (size_t)O.m, 32, 32 + hb, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));   // stmp is freed at scope end
+    }
+    hipLaunchKernelGGL(k_keys_to_in_csr, dim3(grid_for((uint64_t)n + 1, 256, 1u << 30)), dim3(256), 0, s, k1.p, O.m, n,
+                       O.irp.p, O.icode.p);
+    GX_TRY(check_launch("k_keys_to_in_csr"));
     GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries are freed on return
     return GX_SUCCESS;
 }
 
-// Adds the triangle contributions of every triangle whose lowest-ranked vertex (the
-// orientation source) lies in [v0, v1) into tc (n counters).
+// Adds the contributions of every triangle whose middle vertex (in orientation rank) lies in
+// [v0, v1) into tc (n counters).
 int lcc_count_range(gx_graph *g, const LccOrient &O, int64_t v0, int64_t v1, unsigned long long *tc,
                     hipStream_t s) {
     gx_ctx *ctx = g->ctx;
-    const int64_t n = (int64_t)g->n, nv = v1 - v0;
+    const int64_t nv = v1 - v0;
     if (nv <= 0 || O.m == 0) return GX_SUCCESS;
-    DBuf<int32_t> lists;
+    const uint64_t icap = (uint64_t)nv + (uint64_t)O.m / kWaveGroup + 64;
+    DBuf<uint64_t> witems, bitems;
+    DBuf<int32_t> big;
     DBuf<uint32_t> counts;
-    GX_TRY(lists.alloc(3 * (uint64_t)nv));
+    GX_TRY(witems.alloc(icap));
+    GX_TRY(bitems.alloc(icap));
+    GX_TRY(big.alloc(nv));
     GX_TRY(counts.alloc(3));
     GX_HIP_TRY(hipMemsetAsync(counts.p, 0, 12, s));
-    hipLaunchKernelGGL(k_lcc_classify, dim3((unsigned)std::min<int64_t>((nv + kClassTile - 1) / kClassTile, 2048)),
-                       dim3(kLccBlock), 0, s, O.orp.p, v0, v1, lists.p,
-                       counts.p, lists.p + nv, counts.p + 1, lists.p + 2 * nv, counts.p + 2);
-    GX_TRY(check_launch("k_lcc_classify"));
+    hipLaunchKernelGGL(k_lcc_items, dim3((unsigned)std::min<int64_t>((nv + kClassTile - 1) / kClassTile, 2048)),
+                       dim3(kLccBlock), 0, s, O.orp.p, O.irp.p, v0, v1, witems.p, counts.p, bitems.p, counts.p + 1,
+                       big.p, counts.p + 2);
+    GX_TRY(check_launch("k_lcc_items"));
     uint32_t hc[3] = {0, 0, 0};
     GX_HIP_TRY(hipMemcpyAsync(hc, counts.p, 12, hipMemcpyDeviceToHost, s));
     GX_HIP_TRY(hipStreamSynchronize(s));
@@ -433,25 +528,24 @@ int lcc_count_range(gx_graph *g, const LccOrient &O, int64_t v0, int64_t v1, uns
         KTimer kt(ctx, "lcc_triangles", s);
         if (hc[0])
             hipLaunchKernelGGL(k_lcc_wave, dim3(grid_for((uint64_t)hc[0] * kWave, kLccBlock, 8192)), dim3(kLccBlock),
-                               0, s, O.orp.p, O.oci.p, O.ofl.p, lists.p, hc[0], tc);
+                               0, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, witems.p, hc[0], tc);
         GX_TRY(check_launch("k_lcc_wave"));
         if (hc[1])
             hipLaunchKernelGGL(k_lcc_block, dim3(std::min<uint32_t>(hc[1], 4096)), dim3(kLccBlock), 0, s, O.orp.p,
-                               O.oci.p, O.ofl.p, lists.p + nv, hc[1], tc);
+                               O.ocode.p, O.irp.p, O.icode.p, bitems.p, hc[1], tc);
         GX_TRY(check_launch("k_lcc_block"));
         if (hc[2]) {
-            std::vector<int32_t> big(hc[2]);
-            GX_HIP_TRY(hipMemcpyAsync(big.data(), lists.p + 2 * nv, hc[2] * 4, hipMemcpyDeviceToHost, s));
+            std::vector<int32_t> hb(hc[2]);
+            GX_HIP_TRY(hipMemcpyAsync(hb.data(), big.p, hc[2] * 4, hipMemcpyDeviceToHost, s));
             GX_HIP_TRY(hipStreamSynchronize(s));
-            for (int32_t v : big) {
-                hipLaunchKernelGGL(k_lcc_merge_row, dim3(64), dim3(kLccBlock), 0, s, O.orp.p, O.oci.p, O.ofl.p, v,
-                                   tc);
-                GX_TRY(check_launch("k_lcc_merge_row"));
+            for (int32_t u : hb) {
+                hipLaunchKernelGGL(k_lcc_merge_in, dim3(64), dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p,
+                                   O.icode.p, u, tc);
+                GX_TRY(check_launch("k_lcc_merge_in"));
             }
         }
     }
-    GX_HIP_TRY(hipStreamSynchronize(s));   // lists are freed on return
-    (void)n;
+    GX_HIP_TRY(hipStreamSynchronize(s));   // item lists are freed on return
     return GX_SUCCESS;
 }
 
@@ -462,6 +556,8 @@ using namespace gx;
 
 extern "C" int gx_lcc(gx_graph *g, double *lcc) {
     if (!g || !lcc) return fail(GX_NULL_POINTER, "gx_lcc: null argument");
+    if (g->n >= (1ull << 29))
+        return fail(GX_NOT_IMPLEMENTED, "gx_lcc: more than 2^29 vertices (packed oriented entries)");
     gx_ctx *ctx = g->ctx;
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -493,6 +589,8 @@ struct gx_lcc_part {
 
 extern "C" int gx_lcc_part_create(gx_graph *g, gx_lcc_part **part) {
     if (!g || !part) return fail(GX_NULL_POINTER, "gx_lcc_part_create: null argument");
+    if (g->n >= (1ull << 29))
+        return fail(GX_NOT_IMPLEMENTED, "gx_lcc_part_create: more than 2^29 vertices (packed oriented entries)");
     GX_HIP_TRY(hipSetDevice(g->ctx->device));
     GX_TRY(ensure_closure(g));
     auto p = std::make_unique<gx_lcc_part>();
@@ -512,8 +610,8 @@ extern "C" int gx_lcc_part_ranges(gx_lcc_part *part, int nranks, uint64_t *range
     if (n) {
         DBuf<uint64_t> work;
         GX_TRY(work.alloc(n));
-        hipLaunchKernelGGL(k_lcc_work, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, part->orient.orp.p,
-                           part->orient.oci.p, n, work.p);
+        hipLaunchKernelGGL(k_lcc_work, dim3(grid_for((uint64_t)n * kWave, kLccBlock, 8192)), dim3(kLccBlock), 0, s,
+                           part->orient.orp.p, part->orient.irp.p, part->orient.icode.p, n, work.p);
         GX_TRY(check_launch("k_lcc_work"));
         GX_HIP_TRY(hipMemcpyAsync(w.data(), work.p, n * 8, hipMemcpyDeviceToHost, s));
         GX_HIP_TRY(hipStreamSynchronize(s));
