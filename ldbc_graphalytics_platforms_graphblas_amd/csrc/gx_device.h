@@ -217,6 +217,34 @@ __device__ __forceinline__ void raise_flag(int *flag) {
         __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- 64-entry slabs of a CSR (one wave per slab, lane = entry) ----
+// srow[sl] = the row holding entry sl*64, srow[nslabs] = n - 1 (gx_runtime.hip).
+int slab_rows(const int64_t *rp, int64_t n, int64_t nslabs, int64_t *srow, hipStream_t s);
+
+// Row of entry ee (inside slab sl): the slab's rows lie in [srow[sl], srow[sl+1]]; when that
+// range is at most 64 rows each lane finds its row by a 6-step shuffle search, else by its
+// own binary search.  Every lane of the wave must call it (shuffles).
+__device__ __forceinline__ int64_t slab_row_of(const int64_t *__restrict__ rp, const int64_t *__restrict__ srow,
+                                               int64_t n, int64_t sl, int64_t ee, int lane) {
+    const int64_t r0 = srow[sl], r1 = srow[sl + 1];
+    if (r1 - r0 < kWave) {
+        const int64_t rpk = rp[min(r0 + 1 + lane, n)];
+        int o = 0;
+#pragma unroll
+        for (int step = kWave / 2; step > 0; step >>= 1)
+            if (__shfl(rpk, o + step - 1, kWave) <= ee) o += step;
+        return r0 + o;
+    }
+    int64_t lo = r0, hi = r1 + 1;   // rp[lo] <= ee < rp[hi]
+    if (hi > n) hi = n;
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (rp[mid] <= ee) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 typedef int gx_v4i __attribute__((ext_vector_type(4)));
 
 // 16-byte non-temporal load (read-once streams: keep L2 for the gathered vectors).

@@ -18,9 +18,10 @@
 //                 (v, u).  The three contributions are summed on chip (u in a register, v in
 //                 an LDS slot per v, x in its hash slot) and leave as one 64-bit atomic per
 //                 (work item, contribution target).
-//   tiers       : work item (u, 64 in-neighbours) per wave for |O(u)| <= kWaveMax, (u, 256)
-//                 per workgroup up to kBlockMax, a merge-intersection fallback beyond (not
-//                 reached on degree-oriented graphs below ~2^25 edges).
+//   tiers       : work item (u, 64 in-neighbours) per wave for |O(u)| <= 512 (512- or
+//                 1024-slot tables), (u, 256) per workgroup up to kBlockMax (LDS sized to the
+//                 tier's largest |O(u)|), a merge-intersection fallback beyond (not reached
+//                 on degree-oriented graphs below ~2^25 edges).
 // Oriented entries are packed as (vertex << 2) | popcount(flag), so n < 2^29.
 // Counts are exact integers, so the result is deterministic and equal to the oracle bit for
 // bit (one fp64 division per vertex).
@@ -37,10 +38,10 @@ namespace {
 
 constexpr int kLccBlock = 256;
 constexpr int kWavesPerBlock = kLccBlock / kWave;
-constexpr int kWaveMax = 256;          // wave tier: |O(v)| <= 256, table <= 512 slots
-constexpr int kWaveSlots = 512;
-constexpr int kBlockMax = 8192;        // workgroup tier: table of 16384 slots (128 KiB)
-constexpr int kBlockSlots = 16384;
+constexpr int kWaveMax = 256;          // wave tiers: |O(u)| <= 256 (512-slot tables) ...
+constexpr int kWave2Max = 512;         // ... and <= 512 (1024-slot tables)
+constexpr int kBlockMax = 8192;        // workgroup tier: table sized to the tier's largest |O(u)|
+constexpr int kBlockSlots = 16384;     //   (dynamic LDS, at most 128 KiB)
 constexpr uint32_t kCntMask = (1u << 30) - 1;   // hash value: flag popcount << 30 | x count
 
 __device__ __forceinline__ bool ranks_above(int64_t du, int32_t u, int64_t dv, int32_t v) {
@@ -57,31 +58,10 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ---- orientation by slab compaction ----
-// One wave per 64-entry slab of S: lane = entry, its row found by a shuffle search over the
-// slab's (at most 64) rows or a binary search; kept = the column ranks above the row.
-__device__ __forceinline__ int64_t slab_row(const int64_t *__restrict__ rp, int64_t n, int64_t e0, int64_t e_last,
-                                            int64_t ee, int lane) {
-    const int64_t r0 = row_of_edge(rp, n, e0), r1 = row_of_edge(rp, n, e_last);
-    if (r1 - r0 < kWave) {
-        const int64_t rpk = rp[min(r0 + 1 + lane, n)];
-        int o = 0;
-#pragma unroll
-        for (int step = kWave / 2; step > 0; step >>= 1)
-            if (__shfl(rpk, o + step - 1, kWave) <= ee) o += step;
-        return r0 + o;
-    }
-    int64_t lo = r0, hi = r1 + 1;
-    while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (rp[mid] <= ee) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
+// ---- orientation by slab compaction (one wave per 64-entry slab of S, lane = entry) ----
 __global__ __launch_bounds__(kLccBlock) void k_orient_masks(const int64_t *__restrict__ rp,
-                                                            const int32_t *__restrict__ ci, int64_t n, int64_t nnz,
+                                                            const int32_t *__restrict__ ci,
+                                                            const int64_t *__restrict__ srow, int64_t n, int64_t nnz,
                                                             int64_t nslabs, uint64_t *mask, int32_t *cnt) {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
@@ -90,7 +70,7 @@ __global__ __launch_bounds__(kLccBlock) void k_orient_masks(const int64_t *__res
         const int64_t e = e0 + lane;
         const bool valid = e < nnz;
         const int64_t ee = valid ? e : e_last;
-        const int64_t v = slab_row(rp, n, e0, e_last, ee, lane);
+        const int64_t v = slab_row_of(rp, srow, n, sl, ee, lane);
         const int32_t u = ci[ee];
         const bool keep = valid && ranks_above(rp[u + 1] - rp[u], u, rp[v + 1] - rp[v], (int32_t)v);
         const uint64_t m = __ballot(keep);
@@ -168,14 +148,14 @@ constexpr int kClassTile = 4096;
 
 __global__ __launch_bounds__(kLccBlock) void k_lcc_items(const int64_t *__restrict__ orp,
                                                          const int64_t *__restrict__ irp, int64_t v0, int64_t v1,
-                                                         uint64_t *wave_items, uint32_t *wave_cnt,
-                                                         uint64_t *block_items, uint32_t *block_cnt,
-                                                         int32_t *big_list, uint32_t *big_cnt) {
-    __shared__ uint32_t tot[3], base[3], off[3];
-    uint32_t *gcnt[3] = {wave_cnt, block_cnt, big_cnt};
+                                                         uint64_t *items0, uint64_t *items1, uint64_t *items2,
+                                                         int32_t *big_list, uint32_t *counts /* 4 tiers + max d */) {
+    constexpr int kTiers = 4;
+    __shared__ uint32_t tot[kTiers], base[kTiers], off[kTiers];
+    uint64_t *items[3] = {items0, items1, items2};
     for (int64_t t0 = v0 + (int64_t)blockIdx.x * kClassTile; t0 < v1; t0 += (int64_t)gridDim.x * kClassTile) {
         const int64_t t1 = min(t0 + (int64_t)kClassTile, v1);
-        if (threadIdx.x < 3) {
+        if (threadIdx.x < kTiers) {
             tot[threadIdx.x] = 0;
             off[threadIdx.x] = 0;
         }
@@ -184,24 +164,24 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_items(const int64_t *__restri
             for (int64_t u = t0 + threadIdx.x; u < t1; u += kLccBlock) {
                 const int64_t d = orp[u + 1] - orp[u], e = irp[u + 1] - irp[u];
                 if (d == 0 || e == 0) continue;
-                const int tier = d <= kWaveMax ? 0 : (d <= kBlockMax ? 1 : 2);
-                const uint32_t ni = tier == 0 ? (uint32_t)((e + kWaveGroup - 1) / kWaveGroup)
-                                              : (tier == 1 ? (uint32_t)((e + kBlockGroup - 1) / kBlockGroup) : 1u);
+                const int tier = d <= kWaveMax ? 0 : (d <= kWave2Max ? 1 : (d <= kBlockMax ? 2 : 3));
+                const int64_t group = tier == 2 ? kBlockGroup : kWaveGroup;
+                const uint32_t ni = tier == 3 ? 1u : (uint32_t)((e + group - 1) / group);
                 if (pass == 0) {
                     atomicAdd(&tot[tier], ni);
+                    if (tier == 2) atomicMax(&counts[4], (uint32_t)d);
                 } else {
                     const uint32_t pos = base[tier] + atomicAdd(&off[tier], ni);
-                    if (tier == 2) {
+                    if (tier == 3) {
                         big_list[pos] = (int32_t)u;
                     } else {
-                        uint64_t *items = tier == 0 ? wave_items : block_items;
-                        for (uint32_t j = 0; j < ni; j++) items[pos + j] = ((uint64_t)u << 32) | j;
+                        for (uint32_t j = 0; j < ni; j++) items[tier][pos + j] = ((uint64_t)u << 32) | j;
                     }
                 }
             }
             __syncthreads();
-            if (pass == 0 && threadIdx.x < 3)
-                base[threadIdx.x] = tot[threadIdx.x] ? atomicAdd(gcnt[threadIdx.x], tot[threadIdx.x]) : 0u;
+            if (pass == 0 && threadIdx.x < kTiers)
+                base[threadIdx.x] = tot[threadIdx.x] ? atomicAdd(&counts[threadIdx.x], tot[threadIdx.x]) : 0u;
             __syncthreads();
         }
     }
@@ -279,6 +259,7 @@ __device__ __forceinline__ uint32_t table_slots(int64_t d) {
     return slots;
 }
 
+template <int kWaveSlots>
 __global__ __launch_bounds__(kLccBlock) void k_lcc_wave(const int64_t *__restrict__ orp,
                                                         const uint32_t *__restrict__ ocode,
                                                         const int64_t *__restrict__ irp,
@@ -325,9 +306,10 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_block(const int64_t *__restri
                                                          const int64_t *__restrict__ irp,
                                                          const uint32_t *__restrict__ icode,
                                                          const uint64_t *__restrict__ items, uint32_t count,
-                                                         unsigned long long *tc) {
-    __shared__ int32_t hkey[kBlockSlots];
-    __shared__ uint32_t hval[kBlockSlots];
+                                                         uint32_t max_slots, unsigned long long *tc) {
+    extern __shared__ uint32_t dyn[];   // max_slots keys, then max_slots values
+    int32_t *hkey = reinterpret_cast<int32_t *>(dyn);
+    uint32_t *hval = dyn + max_slots;
     __shared__ uint32_t s_vcnt[kWavesPerBlock][kWave];
     __shared__ unsigned long long s_tu[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
@@ -452,12 +434,15 @@ int lcc_orient(gx_graph *g, LccOrient &O, hipStream_t s) {
     GX_TRY(cpre.alloc(nslabs + 1));
     GX_TRY(O.orp.alloc(n + 1));
     GX_TRY(O.irp.alloc(n + 1));
+    DBuf<int64_t> srow;
+    GX_TRY(srow.alloc(nslabs + 1));
     GX_HIP_TRY(hipMemsetAsync(cnt.p + nslabs, 0, sizeof(int32_t), s));
     GX_HIP_TRY(hipMemsetAsync(mask.p + nslabs, 0, sizeof(uint64_t), s));
     KTimer kt(ctx, "lcc_orient", s);
+    GX_TRY(slab_rows(S.rp.p, n, nslabs, srow.p, s));
     if (nslabs)
         hipLaunchKernelGGL(k_orient_masks, dim3(grid_for((uint64_t)nslabs * kWave, kLccBlock, 16384)), dim3(kLccBlock),
-                           0, s, S.rp.p, S.ci.p, n, nnz, nslabs, mask.p, cnt.p);
+                           0, s, S.rp.p, S.ci.p, srow.p, n, nnz, nslabs, mask.p, cnt.p);
     GX_TRY(check_launch("k_orient_masks"));
     size_t tmp_bytes = 0;
     GX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt.p, cpre.p, (int64_t)0, (size_t)(nslabs + 1),
@@ -509,34 +494,48 @@ int lcc_count_range(gx_graph *g, const LccOrient &O, int64_t v0, int64_t v1, uns
     const int64_t nv = v1 - v0;
     if (nv <= 0 || O.m == 0) return GX_SUCCESS;
     const uint64_t icap = (uint64_t)nv + (uint64_t)O.m / kWaveGroup + 64;
-    DBuf<uint64_t> witems, bitems;
+    DBuf<uint64_t> items0, items1, items2;
     DBuf<int32_t> big;
     DBuf<uint32_t> counts;
-    GX_TRY(witems.alloc(icap));
-    GX_TRY(bitems.alloc(icap));
+    GX_TRY(items0.alloc(icap));
+    GX_TRY(items1.alloc(icap));
+    GX_TRY(items2.alloc(icap));
     GX_TRY(big.alloc(nv));
-    GX_TRY(counts.alloc(3));
-    GX_HIP_TRY(hipMemsetAsync(counts.p, 0, 12, s));
+    GX_TRY(counts.alloc(5));
+    GX_HIP_TRY(hipMemsetAsync(counts.p, 0, 20, s));
     hipLaunchKernelGGL(k_lcc_items, dim3((unsigned)std::min<int64_t>((nv + kClassTile - 1) / kClassTile, 2048)),
-                       dim3(kLccBlock), 0, s, O.orp.p, O.irp.p, v0, v1, witems.p, counts.p, bitems.p, counts.p + 1,
-                       big.p, counts.p + 2);
+                       dim3(kLccBlock), 0, s, O.orp.p, O.irp.p, v0, v1, items0.p, items1.p, items2.p, big.p, counts.p);
     GX_TRY(check_launch("k_lcc_items"));
-    uint32_t hc[3] = {0, 0, 0};
-    GX_HIP_TRY(hipMemcpyAsync(hc, counts.p, 12, hipMemcpyDeviceToHost, s));
+    uint32_t hc[5] = {0, 0, 0, 0, 0};
+    GX_HIP_TRY(hipMemcpyAsync(hc, counts.p, 20, hipMemcpyDeviceToHost, s));
     GX_HIP_TRY(hipStreamSynchronize(s));
     {
         KTimer kt(ctx, "lcc_triangles", s);
         if (hc[0])
-            hipLaunchKernelGGL(k_lcc_wave, dim3(grid_for((uint64_t)hc[0] * kWave, kLccBlock, 8192)), dim3(kLccBlock),
-                               0, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, witems.p, hc[0], tc);
-        GX_TRY(check_launch("k_lcc_wave"));
+            hipLaunchKernelGGL(k_lcc_wave<512>, dim3(grid_for((uint64_t)hc[0] * kWave, kLccBlock, 8192)),
+                               dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items0.p, hc[0], tc);
+        GX_TRY(check_launch("k_lcc_wave<512>"));
         if (hc[1])
-            hipLaunchKernelGGL(k_lcc_block, dim3(std::min<uint32_t>(hc[1], 4096)), dim3(kLccBlock), 0, s, O.orp.p,
-                               O.ocode.p, O.irp.p, O.icode.p, bitems.p, hc[1], tc);
-        GX_TRY(check_launch("k_lcc_block"));
+            hipLaunchKernelGGL(k_lcc_wave<1024>, dim3(grid_for((uint64_t)hc[1] * kWave, kLccBlock, 8192)),
+                               dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items1.p, hc[1], tc);
+        GX_TRY(check_launch("k_lcc_wave<1024>"));
         if (hc[2]) {
-            std::vector<int32_t> hb(hc[2]);
-            GX_HIP_TRY(hipMemcpyAsync(hb.data(), big.p, hc[2] * 4, hipMemcpyDeviceToHost, s));
+            const uint32_t slots = std::max<uint32_t>(64, std::min<uint32_t>(kBlockSlots, [&] {
+                uint32_t x = 64;
+                while (x < 2 * hc[4]) x <<= 1;
+                return x;
+            }()));
+            if (slots * 8 > 65536)
+                GX_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lcc_block),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(slots * 8)));
+            hipLaunchKernelGGL(k_lcc_block, dim3(std::min<uint32_t>(hc[2], 4096)), dim3(kLccBlock),
+                               (size_t)slots * 8, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items2.p, hc[2], slots,
+                               tc);
+        }
+        GX_TRY(check_launch("k_lcc_block"));
+        if (hc[3]) {
+            std::vector<int32_t> hb(hc[3]);
+            GX_HIP_TRY(hipMemcpyAsync(hb.data(), big.p, hc[3] * 4, hipMemcpyDeviceToHost, s));
             GX_HIP_TRY(hipStreamSynchronize(s));
             for (int32_t u : hb) {
                 hipLaunchKernelGGL(k_lcc_merge_in, dim3(64), dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p,

@@ -108,6 +108,21 @@ int collect_timings(gx_ctx *ctx) {
     return GX_SUCCESS;
 }
 
+// each row scatters its own slab starts: no per-slab binary search
+__global__ void k_slab_rows(const int64_t *__restrict__ rp, int64_t n, int64_t nslabs, int64_t *srow) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = rp[v], e = rp[v + 1];
+        for (int64_t sl = (b + kWave - 1) / kWave; sl * kWave < e; sl++) srow[sl] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) srow[nslabs] = n > 0 ? n - 1 : 0;
+}
+
+int slab_rows(const int64_t *rp, int64_t n, int64_t nslabs, int64_t *srow, hipStream_t s) {
+    hipLaunchKernelGGL(k_slab_rows, dim3(grid_for((uint64_t)std::max<int64_t>(n, 1), 256, 8192)), dim3(256), 0, s, rp,
+                       n, nslabs, srow);
+    return check_launch("k_slab_rows");
+}
+
 int ensure_aux_streams(gx_ctx *ctx) {
     if (ctx->aux[0]) return GX_SUCCESS;
     for (int i = 0; i < 2; i++) {

@@ -559,7 +559,8 @@ __global__ __launch_bounds__(256) void k_light_rows(const int64_t *__restrict__ 
 // One wave per slab; lane = entry.  The slab's rows lie in [r0, r1] (two uniform binary
 // searches); when that range is at most 64 rows each lane finds its row by a 6-step shuffle
 // search over rp[r0+1 .. r0+64], else by its own binary search.
-__global__ __launch_bounds__(256) void k_light_scatter(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+__global__ __launch_bounds__(256) void k_light_scatter(const int64_t *__restrict__ rp, const int64_t *__restrict__ srow,
+                                                       const int32_t *__restrict__ ci,
                                                        const double *__restrict__ w, const uint64_t *__restrict__ mask,
                                                        const int64_t *__restrict__ cpre, const int64_t *__restrict__ Ls,
                                                        const int64_t *__restrict__ lend, int64_t n, int64_t nnz,
@@ -568,28 +569,10 @@ __global__ __launch_bounds__(256) void k_light_scatter(const int64_t *__restrict
     const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
     for (int64_t sl = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; sl < nslabs; sl += nw) {
         const int64_t e0 = sl * kWave, e_last = min(e0 + kWave, nnz) - 1;
-        const int64_t r0 = row_of_edge(rp, n, e0), r1 = row_of_edge(rp, n, e_last);
         const int64_t e = e0 + lane;
         const bool valid = e < nnz;
         const int64_t ee = valid ? e : e_last;
-        int64_t r;
-        if (r1 - r0 < kWave) {
-            // lane k holds rp[r0 + 1 + k] (clamped); row = r0 + #{k : rp[r0+1+k] <= e}
-            const int64_t rpk = rp[min(r0 + 1 + lane, n)];
-            int o = 0;
-#pragma unroll
-            for (int step = kWave / 2; step > 0; step >>= 1)
-                if (__shfl(rpk, o + step - 1, kWave) <= ee) o += step;
-            r = r0 + o;
-        } else {
-            int64_t lo = r0, hi = r1 + 1;   // rp[lo] <= ee < rp[hi]
-            while (hi - lo > 1) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (rp[mid] <= ee) lo = mid;
-                else hi = mid;
-            }
-            r = lo;
-        }
+        const int64_t r = slab_row_of(rp, srow, n, sl, ee, lane);
         if (valid) {
             const uint64_t m = mask[sl];
             const bool light = (m >> lane) & 1ull;
@@ -637,7 +620,10 @@ int ensure_sssp_layout(gx_graph *g, double delta, hipStream_t s) {
         GX_TRY(check_launch("k_light_rows"));
     }
     if (nslabs) {
-        hipLaunchKernelGGL(k_light_scatter, dim3(wgrid), dim3(256), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, mask.p,
+        DBuf<int64_t> srow;
+        GX_TRY(srow.alloc(nslabs + 1));
+        GX_TRY(slab_rows(g->A.rp.p, n, nslabs, srow.p, s));
+        hipLaunchKernelGGL(k_light_scatter, dim3(wgrid), dim3(256), 0, s, g->A.rp.p, srow.p, g->A.ci.p, g->A.w.p, mask.p,
                            cpre.p, Ls.p, L->lend.p, n, nnz, nslabs, L->ci.p, L->w.p);
         GX_TRY(check_launch("k_light_scatter"));
     }

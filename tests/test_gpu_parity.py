@@ -158,3 +158,21 @@ def test_empty_and_isolated(ctx):
                                O.pagerank(e, False, 0.85, 4), rtol=PR_RTOL)
     np.testing.assert_array_equal(gpu_run(ctx, ge, "CDLP", iters=2), O.cdlp(e, False, 2))
     np.testing.assert_array_equal(gpu_run(ctx, ge, "WCC"), O.wcc(e))
+
+
+def test_dense_tiers(ctx):
+    """A 700-clique inside a sparse random graph (directed and undirected): oriented rows of
+    up to 699 entries exercise LCC's workgroup tier, and degrees past 512 the CDLP mid tiers."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    rng = np.random.default_rng(7)
+    n, k = 5000, 700
+    a, b = np.triu_indices(k, 1)
+    flip = rng.random(len(a)) < 0.5   # direct each clique edge one way or the other
+    src = np.concatenate([np.where(flip, a, b), rng.integers(0, n, 20000)])
+    dst = np.concatenate([np.where(flip, b, a), rng.integers(0, n, 20000)])
+    keep = src != dst
+    for directed in (False, True):
+        csr = csr_from_edges(n, src[keep], dst[keep], None, symmetric=not directed)
+        g = _G(csr, directed)
+        np.testing.assert_array_equal(gpu_run(ctx, g, "LCC"), O.lcc(csr, directed))
+        np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=4), O.cdlp(csr, directed, 4))
