@@ -282,6 +282,15 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     unsigned long long mymin = ~0ull, n_skip = 0;
     const uint32_t stride = gridDim.x * kSsspBlock;
     const uint32_t nround = (count + stride - 1) / stride;
+    // pushes are staged per wave in LDS and flushed in bulk, as in k_sssp_relax
+    __shared__ Stage stages[kSsspBlock / kWave];
+    Stage &sg = stages[threadIdx.x / kWave];
+    uint32_t staged = 0;
+    const int lane = threadIdx.x & (kWave - 1);
+    uint64_t *near_out = B.q[qin];
+    uint32_t *near_count = &B.st->qcnt[qin];
+    int32_t *ovf = B.ovf[epoch & 1];
+    uint32_t *ovf_count = &B.st->ovf_cnt[epoch & 1];
     for (uint32_t it = 0; it < nround; it++) {
         const uint32_t f = it * stride + blockIdx.x * kSsspBlock + threadIdx.x;
         bool to_near = false, to_ring = false, to_ovf = false, to_set = false;
@@ -316,14 +325,19 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
                 }
             }
         }
-        if (mode != 2) {
-            wave_append_items(to_near ? nch : 0u, v, B.q[qin], &B.st->qcnt[qin]);
-            if (mode == 1) wave_append_vertex(to_set, v, B.settled, &B.st->settled_cnt);
-        } else {
-            wave_append_ring(to_ring, slot, v, B);
-            wave_append_vertex(to_ovf, v, B.ovf[epoch & 1], &B.st->ovf_cnt[epoch & 1]);
+        const bool take = to_near | to_ring | to_ovf;
+        const uint64_t mask = __ballot(take);
+        if (mask == 0) continue;
+        if (take) {
+            const uint32_t pos = staged + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
+            sg.v[pos] = v;
+            sg.tag[pos] = to_near ? ((uint32_t)kTagNear | (to_set ? 0x80u : 0u) | (nch << 8))
+                                  : (to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot);
         }
+        staged += (uint32_t)__popcll(mask);
+        if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
     }
+    if (staged) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
     if (mode == 2) wave_min_to(mymin, &B.st->ovf_minb);
     wave_count(B.stats, 7, n_skip);
 }
