@@ -374,7 +374,7 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     dist = None
-    if world > 1:
+    if world > 1 or "MASTER_ADDR" in os.environ:   # under torch.distributed.run: RCCL, even at N=1
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
@@ -384,7 +384,7 @@ def main():
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
     from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import GpuStep, PartitionedPageRank, hub_relabel, \
-        local_rows
+        local_pieces, local_rows
 
     gname = args.graph or "SYN-7_5"
     workload = f"PageRank {gname} (R-MAT scale {args.scale}, ef {args.edgefactor}, seed {args.seed}, undirected)"
@@ -393,19 +393,23 @@ def main():
     t_gen = time.time() - t_gen
     n, nnz = csr.n, csr.nnz
     perm, hub = hub_relabel(csr)   # hub-first layout (what gx_pagerank does internally)
-    lr = local_rows(hub, directed=False, nranks=world, rank=rank)
+    # N > 1: each rank's rows are cut into `pieces` virtual ranks whose all-gathers overlap
+    # the next piece's SpMV (pr_partition.local_pieces)
+    pieces = max(1, int(os.environ.get("GX_PR_PIECES", "2" if world > 1 else "1"))) if dist else 1
+    lrs = local_pieces(hub, False, world, rank, pieces) if pieces > 1 else \
+        [local_rows(hub, directed=False, nranks=world, rank=rank)]
 
     ctx = Context(local_rank)
     dev_name, cus = ctx.info()
     t_setup = time.perf_counter()
-    stepper = GpuStep(ctx, n, world, lr, args.damping)   # H2D upload + pull-plan build
+    steppers = [GpuStep(ctx, n, world * pieces, lr, args.damping) for lr in lrs]   # H2D upload + plans
     torch.cuda.synchronize(device)
     t_setup = time.perf_counter() - t_setup
     # a real (non-null) stream: libgx launches on it and RCCL orders against it
     stream = torch.cuda.Stream(device)
     torch.cuda.set_stream(stream)
-    gather = (lambda out, inp: dist.all_gather_into_tensor(out, inp)) if dist else None
-    pr = PartitionedPageRank(stepper, world, lr.rows, device, all_gather=gather,
+    gather = (lambda out, inp: dist.all_gather_into_tensor(out, inp, async_op=True)) if dist else None
+    pr = PartitionedPageRank(steppers, world, [lr.rows for lr in lrs], device, all_gather=gather,
                              stream_handle=lambda: stream.cuda_stream)
 
     def barrier():
@@ -436,22 +440,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # result of the last step (for the parity check on rank 0)
-    local_rank_out = pr.rank_out[:lr.rows].detach().cpu().numpy()
+    # result of the last step (for the parity check on rank 0), assembled by virtual rank
+    mine = [(lr.rank, o[:lr.rows].detach().cpu().numpy()) for lr, o in zip(lrs, pr.rank_outs)]
     if dist:
         parts = [None] * world
-        dist.all_gather_object(parts, local_rank_out)
-        result = np.concatenate(parts)
-    else:
-        result = local_rank_out
+        dist.all_gather_object(parts, mine)
+        mine = [t for part in parts for t in part]
+    result = np.concatenate([a for _, a in sorted(mine, key=lambda t: t[0])])
     result = result[perm]   # back to the generator's vertex order
 
     edges_total = nnz * args.iters * args.steps
     value = edges_total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # roofline of k_pr_pull on this rank (per launch)
-    bytes_per_launch = 4 * lr.nnz + 8 * (lr.rows + 1) + 8 * lr.rows + 8 * lr.rows
+    # roofline of k_pr_pull on this rank (per launch, averaged over the pieces)
+    bytes_per_launch = sum(4 * lr.nnz + 8 * (lr.rows + 1) + 8 * lr.rows + 8 * lr.rows for lr in lrs) / len(lrs)
     mean_launch_s = (pull_ms / launches) / 1e3 if launches else float("nan")
     achieved = bytes_per_launch / mean_launch_s / 1e9
     traffic = pmc_traffic(workload) if world == 1 else None
@@ -497,7 +500,7 @@ def main():
                 "nnz": nnz,
                 "iterations": args.iters,
                 "damping": args.damping,
-                "parallelism": f"row{world}",
+                "parallelism": f"row{world}" + (f", {pieces} pipelined pieces" if pieces > 1 else ""),
                 "device": dev_name,
                 "cus": cus,
             },
@@ -522,7 +525,8 @@ def main():
             "graph_gen_s": t_gen,
         }
         print(json.dumps(line), flush=True)
-    stepper.close()
+    for st in steppers:
+        st.close()
     ctx.close()
     if dist:
         dist.destroy_process_group()

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import Callable, Optional
+from typing import Callable, List, Optional, Sequence, Union
 
 import numpy as np
 
@@ -84,17 +84,32 @@ class LocalRows:
         return int(self.rowptr[-1])
 
 
-def local_rows(csr: CSR, directed: bool, nranks: int, rank: int, pull: Optional[CSR] = None) -> LocalRows:
-    """Slice the pull matrix for `rank` (pull = A' for directed graphs)."""
-    if pull is None:
-        pull = csr.transpose() if directed else csr
-    bounds = partition_rows(pull.rowptr, nranks)
+def _slice_rows(csr: CSR, pull: CSR, bounds: np.ndarray, rank: int) -> LocalRows:
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
     z0, z1 = int(pull.rowptr[r0]), int(pull.rowptr[r1])
     rp = (pull.rowptr[r0:r1 + 1] - np.uint64(z0)).astype(np.uint64)
     ci = np.ascontiguousarray(pull.colidx[z0:z1], dtype=np.uint64)
     outdeg = np.diff(csr.rowptr.astype(np.int64))[r0:r1].astype(np.uint64)
     return LocalRows(bounds, rank, np.ascontiguousarray(rp), ci, np.ascontiguousarray(outdeg))
+
+
+def local_rows(csr: CSR, directed: bool, nranks: int, rank: int, pull: Optional[CSR] = None) -> LocalRows:
+    """Slice the pull matrix for `rank` (pull = A' for directed graphs)."""
+    if pull is None:
+        pull = csr.transpose() if directed else csr
+    return _slice_rows(csr, pull, partition_rows(pull.rowptr, nranks), rank)
+
+
+def local_pieces(csr: CSR, directed: bool, nranks: int, rank: int, pieces: int,
+                 pull: Optional[CSR] = None) -> List[LocalRows]:
+    """Pipelined layout: the pull matrix is cut into nranks * pieces ranges (balanced by
+    entries) and rank k owns the virtual ranks p * nranks + k, p < pieces.  Piece p of every
+    rank is then one contiguous slab of the exchanged vector (chunks p*nranks .. p*nranks +
+    nranks - 1), so each piece is all-gathered on its own while the next one computes."""
+    if pull is None:
+        pull = csr.transpose() if directed else csr
+    bounds = partition_rows(pull.rowptr, nranks * pieces)
+    return [_slice_rows(csr, pull, bounds, p * nranks + rank) for p in range(pieces)]
 
 
 class GpuStep:
@@ -132,37 +147,78 @@ class GpuStep:
 
 
 class PartitionedPageRank:
-    """Runs `iters` PageRank iterations with one exchange per iteration.
+    """Runs `iters` PageRank iterations with one exchange per iteration and piece.
 
-    `stepper` provides init(x_local, stream), step(x_full, x_local, rank_out, stream) and
-    `chunk`; `all_gather(out_full, in_local)` is torch.distributed.all_gather_into_tensor
-    for nranks > 1.  With one rank the two buffers simply swap roles.
+    `stepper` (or a list of them, one per piece: see local_pieces) provides
+    init(x_local, stream), step(x_full, x_local, rank_out, stream) and `chunk`;
+    `all_gather(out, inp)` is torch.distributed.all_gather_into_tensor for nranks > 1 and may
+    return an async work handle (async_op=True): piece p's gather then runs while piece p+1
+    computes, and all handles are waited for before the next iteration reads the vector.
+    The gathered vector is double-buffered so that a gather never overwrites values a later
+    piece of the same iteration still reads.  With one rank and one piece the two buffers
+    simply swap roles.
     """
 
-    def __init__(self, stepper, nranks: int, rows_local: int, device, all_gather: Optional[Callable] = None,
-                 stream_handle: Callable[[], int] = lambda: 0):
+    def __init__(self, stepper, nranks: int, rows_local: Union[int, Sequence[int]], device,
+                 all_gather: Optional[Callable] = None, stream_handle: Callable[[], int] = lambda: 0):
         import torch
-        self.s = stepper
+        self.steps = list(stepper) if isinstance(stepper, (list, tuple)) else [stepper]
+        rows = list(rows_local) if isinstance(rows_local, (list, tuple)) else [rows_local]
+        if len(rows) != len(self.steps):
+            raise ValueError("one rows_local per piece")
+        self.gathered = all_gather is not None   # else one rank, one piece: buffers swap
+        if not self.gathered and (nranks != 1 or len(self.steps) != 1):
+            raise ValueError("several ranks or pieces need an all_gather")
         self.nranks = nranks
-        self.rows = rows_local
+        self.rows = rows
         self.all_gather = all_gather
         self.stream = stream_handle
-        ch = stepper.chunk
-        self.x_local = torch.zeros(ch, dtype=torch.float64, device=device)
-        self.x_full = torch.zeros(ch * nranks, dtype=torch.float64, device=device)
-        self.rank_out = torch.zeros(max(rows_local, 1), dtype=torch.float64, device=device)
+        ch = self.steps[0].chunk
+        self.chunk = ch
+        npieces = len(self.steps)
+        self.x_local = [torch.zeros(ch, dtype=torch.float64, device=device) for _ in range(npieces)]
+        self.x_read = torch.zeros(ch * nranks * npieces, dtype=torch.float64, device=device)
+        self.x_write = torch.zeros_like(self.x_read) if self.gathered else None
+        self.rank_outs = [torch.zeros(max(r, 1), dtype=torch.float64, device=device) for r in rows]
 
-    def _exchange(self):
-        if self.nranks == 1:
-            self.x_local, self.x_full = self.x_full, self.x_local
-        else:
-            self.all_gather(self.x_full, self.x_local)
+    @property
+    def rank_out(self):
+        """Scores of the (single) piece; see rank_outs for several pieces."""
+        return self.rank_outs[0]
+
+    def _piece(self, x, p):
+        span = self.chunk * self.nranks
+        return x[p * span:(p + 1) * span]
+
+    def _gather_all(self, target):
+        handles = [self.all_gather(self._piece(target, p), self.x_local[p]) for p in range(len(self.steps))]
+        for h in handles:
+            if h is not None:
+                h.wait()
 
     def run(self, iters: int):
-        self.s.init(self.x_local, self.stream())
-        self._exchange()
+        npieces = len(self.steps)
+        for p in range(npieces):
+            self.steps[p].init(self.x_local[p], self.stream())
+        if not self.gathered:
+            self.x_local[0], self.x_read = self.x_read, self.x_local[0]
+        else:
+            self._gather_all(self.x_read)
         for it in range(iters):
-            self.s.step(self.x_full, self.x_local, self.rank_out if it == iters - 1 else None, self.stream())
-            if it < iters - 1:
-                self._exchange()
-        return self.rank_out[:self.rows]
+            last = it == iters - 1
+            handles = []
+            for p in range(npieces):
+                self.steps[p].step(self.x_read, self.x_local[p], self.rank_outs[p] if last else None, self.stream())
+                if not last and self.gathered:
+                    handles.append(self.all_gather(self._piece(self.x_write, p), self.x_local[p]))
+            if last:
+                break
+            if not self.gathered:
+                self.x_local[0], self.x_read = self.x_read, self.x_local[0]
+            else:
+                for h in handles:
+                    if h is not None:
+                        h.wait()
+                self.x_read, self.x_write = self.x_write, self.x_read
+        return self.rank_outs[0][:self.rows[0]] if npieces == 1 else \
+            [o[:r] for o, r in zip(self.rank_outs, self.rows)]

@@ -17,7 +17,8 @@ import torch.multiprocessing as mp
 
 from conftest import ROOT  # noqa: F401  (sys.path)
 from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
-from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import (PartitionedPageRank, hub_relabel, local_rows,
+from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import (PartitionedPageRank, hub_relabel, local_pieces,
+                                                                    local_rows,
                                                                     partition_rows)
 from oracle import oracle as O
 
@@ -63,19 +64,31 @@ def _gloo_gather(out, inp):
         out.copy_(torch.cat(parts))
 
 
-def _worker(rank, world, port, q):
+def _gloo_gather_async(out, inp):
+    """The bench's async form: the gather of piece p runs while piece p+1 computes."""
+    return dist.all_gather(list(out.chunk(dist.get_world_size())), inp, async_op=True)
+
+
+def _worker(rank, world, port, q, pieces=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         csr = rmat(11, 8, 5)
         perm, hub = hub_relabel(csr)
-        lr = local_rows(hub, directed=False, nranks=world, rank=rank)
-        pr = PartitionedPageRank(CpuStep(csr.n, world, lr, 0.85), world, lr.rows, "cpu", all_gather=_gloo_gather)
-        out = pr.run(7).numpy().copy()
+        if pieces == 1:
+            lr = local_rows(hub, directed=False, nranks=world, rank=rank)
+            pr = PartitionedPageRank(CpuStep(csr.n, world, lr, 0.85), world, lr.rows, "cpu", all_gather=_gloo_gather)
+            mine = [(rank, pr.run(7).numpy().copy())]
+        else:
+            lrs = local_pieces(hub, False, world, rank, pieces)
+            pr = PartitionedPageRank([CpuStep(csr.n, world * pieces, lr, 0.85) for lr in lrs], world,
+                                     [lr.rows for lr in lrs], "cpu", all_gather=_gloo_gather_async)
+            mine = [(lr.rank, o.numpy().copy()) for lr, o in zip(lrs, pr.run(7))]
         parts = [None] * world
-        dist.all_gather_object(parts, out)
+        dist.all_gather_object(parts, mine)
         if rank == 0:
-            q.put(np.concatenate(parts)[perm])
+            ordered = sorted((v for part in parts for v in part), key=lambda t: t[0])
+            q.put(np.concatenate([a for _, a in ordered])[perm])
     finally:
         dist.destroy_process_group()
 
@@ -113,11 +126,12 @@ def test_hub_relabel_is_isomorphic():
     np.testing.assert_allclose(a, b, rtol=1e-12)
 
 
-def test_gloo_world2_matches_oracle():
+@pytest.mark.parametrize("pieces", [1, 2])
+def test_gloo_world2_matches_oracle(pieces):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, pieces)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
