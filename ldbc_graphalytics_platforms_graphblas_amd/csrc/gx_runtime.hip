@@ -42,7 +42,9 @@ extern "C" int gx_init(int device, gx_ctx **out) {
                                          prop.gcnArchName);
     gx_ctx *ctx = new gx_ctx();
     ctx->device = device;
-    ctx->device_name = prop.name;
+    // the marketing name comes from libdrm's amdgpu.ids, absent on some images: keep the arch
+    ctx->device_name = prop.name[0] ? std::string(prop.name) + " (" + prop.gcnArchName + ")"
+                                    : std::string(prop.gcnArchName);
     ctx->num_cus = prop.multiProcessorCount;
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
