@@ -228,11 +228,12 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
 // Sum of the scores of this rank's dangling vertices into the chunk's last slot.
 // dlist == nullptr: the dangling rows are the contiguous range [d0, d0 + nd) (hub-first
 // order puts every out-degree-0 vertex last), read coalesced.  Workgroup partials are
-// combined in workgroup order by the last arriver (deterministic).
+// combined by the last arriver's whole workgroup in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void k_pr_dangling(const int32_t *__restrict__ dlist, int64_t d0,
                                                      int64_t nd, int64_t per, double *x, int64_t slot,
                                                      double *part, uint32_t *ticket) {
     __shared__ double wred[256 / kWave];
+    __shared__ int last;
     const int tid = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(b0 + per, nd);
     double s = 0.0;
@@ -244,24 +245,35 @@ __global__ __launch_bounds__(256) void k_pr_dangling(const int32_t *__restrict__
     s = wave_sum(s);
     if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = s;
     __syncthreads();
-    if (tid != 0) return;
-    const double tot = (wred[0] + wred[1]) + (wred[2] + wred[3]);
     const uint32_t G = gridDim.x;
-    if (G == 1) {
-        x[slot] = tot;
-        return;
+    if (tid == 0) {
+        const double tot = (wred[0] + wred[1]) + (wred[2] + wred[3]);
+        if (G == 1) {
+            x[slot] = tot;
+            last = 0;
+        } else {
+            __hip_atomic_store(&part[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+        }
     }
-    __hip_atomic_store(&part[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t != G - 1) return;
+    __syncthreads();
+    if (!last) return;
+    // the last arriver sums the partials with the whole workgroup (a serial loop of agent-
+    // scope loads by one thread took ~20 us); thread t always takes partials t, t+256, ...
+    // and the tree below is fixed, so the sum is the same in every run
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    double all = 0.0;
-    for (uint32_t j = 0; j < G; j++)
-        all += __hip_atomic_load(&part[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    x[slot] = all;
+    double a = 0.0;
+    for (uint32_t j = tid; j < G; j += 256) a += __hip_atomic_load(&part[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a = wave_sum(a);
+    __syncthreads();
+    if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = a;
+    __syncthreads();
+    if (tid == 0) {
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x[slot] = (wred[0] + wred[1]) + (wred[2] + wred[3]);
+    }
 }
 
 __global__ void k_pr_init(const int32_t *__restrict__ outdeg, int64_t rows, double inv_n,
