@@ -74,6 +74,20 @@ KERNELS = {"bfs": ["bfs_topdown", "bfs_bottomup"], "wcc": ["wcc_sample", "wcc_ho
            "lcc": ["lcc_orient", "lcc_triangles"]}
 
 
+def host_cpu() -> dict:
+    """nproc and the CPU model name, recorded with every CPU baseline."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
 def stream_copy_gbs(device, nbytes: int = 1 << 30, reps: int = 10) -> float:
     """Measured device-to-device copy bandwidth (read + write bytes / time), the STREAM-copy
     denominator SURVEY.md 8d asks for beside the 8 TB/s spec."""
@@ -212,7 +226,8 @@ def run_algorithm(args):
             ref, cores = O.lcc(csr, directed, nthreads=threads), threads
         t_cpu = time.perf_counter() - t1
         cpu = {"value": work / t_cpu, "unit": unit, "cores": cores, "kind": "port",
-               "sample": f"one full {alg} run on the same {gname} graph (oracle/gx_oracle.c), {t_cpu:.2f} s"}
+               "sample": f"one full {alg} run on the same {gname} graph (oracle/gx_oracle.c), {t_cpu:.2f} s",
+               **host_cpu()}
         parity = "bit-exact" if np.array_equal(out, ref) else f"MISMATCH ({int((out != ref).sum())} vertices)"
     line = {
         "metric": METRIC, "value": work / t_dev, "unit": unit, "n_gpus": 1, "steps": args.steps,
@@ -475,7 +490,7 @@ def main():
             runs += 1
         cpu = {"value": nnz * args.iters * runs / t_cpu, "unit": "edges/s", "cores": threads, "kind": "port",
                "sample": f"{runs} full PageRank run(s) ({args.iters} iterations) on the same {gname} graph, "
-                         f"OpenMP pull restatement (oracle/gx_oracle.c), {t_cpu:.2f} s"}
+                         f"OpenMP pull restatement (oracle/gx_oracle.c), {t_cpu:.2f} s", **host_cpu()}
         parity = float(np.max(np.abs(result - ref) / np.abs(ref)))
 
     if rank == 0:
