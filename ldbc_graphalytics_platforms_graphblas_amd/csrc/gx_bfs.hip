@@ -318,8 +318,6 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         depth++;
     }
     GX_TRY(device_end(ctx));
-    std::vector<int32_t> h(n);
-    GX_HIP_TRY(hipMemcpy(h.data(), level.p, n * 4, hipMemcpyDeviceToHost));
-    for (int64_t v = 0; v < n; v++) level_out[v] = h[v] < 0 ? INT64_MAX : (int64_t)h[v];
+    GX_TRY(download(ctx, level_out, level.p, (uint64_t)n, Xfer::Levels));
     return GX_SUCCESS;
 }

@@ -647,9 +647,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         }
     }
     GX_TRY(device_end(ctx));
-    std::vector<int32_t> h(n);
-    GX_HIP_TRY(hipMemcpy(h.data(), cur, n * 4, hipMemcpyDeviceToHost));
-    for (int64_t v = 0; v < n; v++) labels[v] = (uint64_t)h[v];
+    GX_TRY(download(ctx, labels, cur, (uint64_t)n, Xfer::Widen32));
     return GX_SUCCESS;
 }
 

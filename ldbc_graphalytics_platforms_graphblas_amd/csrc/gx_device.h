@@ -101,6 +101,11 @@ struct gx_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string device_name;
     int num_cus = 0;
+    // pinned staging for uploads and result hand-back (allocated by gx_init, outside the
+    // Graphalytics processing time); two buffers so host work overlaps the DMA
+    static constexpr size_t kStageBytes = 32u << 20;
+    void *staging[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
     // auxiliary streams for independent kernels of one step (fork/join by events), lazy
     hipStream_t aux[2] = {nullptr, nullptr};
     hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
@@ -108,6 +113,10 @@ struct gx_ctx {
 
 namespace gx {
 int ensure_aux_streams(gx_ctx *ctx);
+// Device -> host copy of `count` elements through the context's pinned staging buffers, the
+// conversion of each chunk (parallel, on the host) overlapping the next chunk's DMA.
+enum class Xfer { Raw64, Levels, Widen32 };   // f64/u64 as is; int32 level -> int64 (INF); int32 -> uint64
+int download(gx_ctx *ctx, void *dst, const void *src_dev, uint64_t count, Xfer kind);
 // SSSP edge layout: every row of A split into its light (w < delta) edges, then its heavy
 // ones; built once per graph and delta by gx_sssp.
 struct SsspLayout {

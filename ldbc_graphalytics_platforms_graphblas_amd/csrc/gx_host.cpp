@@ -515,3 +515,48 @@ extern "C" int gx_read_mtx(const char *path, gx_csr *out) {
     for (uint64_t i = 0; i < nr; i++) out->rowptr[i + 1] += out->rowptr[i];
     return GX_SUCCESS;
 }
+
+// ---------------------------------------------------------------- host helpers (OpenMP)
+
+namespace gx {
+
+bool host_narrow(const uint64_t *in, uint64_t count, uint64_t limit, int32_t *out) {
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+    for (int64_t k = 0; k < (int64_t)count; k++) {
+        const uint64_t c = in[k];
+        bad |= c >= limit;
+        out[k] = (int32_t)c;
+    }
+    return bad == 0;
+}
+
+void host_copy(void *dst, const void *src, size_t bytes) {
+    constexpr size_t kBlock = 1 << 20;
+    const int64_t nb = (int64_t)((bytes + kBlock - 1) / kBlock);
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nb; b++) {
+        const size_t off = (size_t)b * kBlock;
+        std::memcpy(static_cast<char *>(dst) + off, static_cast<const char *>(src) + off,
+                    std::min(kBlock, bytes - off));
+    }
+}
+
+bool host_monotone(const uint64_t *rp, uint64_t n) {
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+    for (int64_t i = 0; i < (int64_t)n; i++) bad |= rp[i + 1] < rp[i];
+    return bad == 0;
+}
+
+void host_levels(const int32_t *in, uint64_t n, int64_t *out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t v = 0; v < (int64_t)n; v++) out[v] = in[v] < 0 ? INT64_MAX : (int64_t)in[v];
+}
+
+void host_widen(const int32_t *in, uint64_t n, uint64_t *out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t v = 0; v < (int64_t)n; v++) out[v] = (uint64_t)(uint32_t)in[v];
+}
+
+}  // namespace gx

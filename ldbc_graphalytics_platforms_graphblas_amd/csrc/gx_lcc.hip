@@ -575,7 +575,7 @@ extern "C" int gx_lcc(gx_graph *g, double *lcc) {
     hipLaunchKernelGGL(k_lcc_final, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->S.rp.p, tc.p, n, out.p);
     GX_TRY(check_launch("k_lcc_final"));
     GX_TRY(device_end(ctx));
-    GX_HIP_TRY(hipMemcpy(lcc, out.p, n * 8, hipMemcpyDeviceToHost));
+    GX_TRY(download(ctx, lcc, out.p, (uint64_t)n, Xfer::Raw64));
     return GX_SUCCESS;
 }
 

@@ -593,8 +593,7 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
         for (uint64_t v = 0; v < n; v++) rank[v] = 1.0 / (double)n;
         return GX_SUCCESS;
     }
-    GX_HIP_TRY(hipMemcpyAsync(rank, p->result.p, n * 8, hipMemcpyDeviceToHost, s));
-    GX_HIP_TRY(hipStreamSynchronize(s));
+    GX_TRY(download(ctx, rank, p->result.p, n, Xfer::Raw64));
     return GX_SUCCESS;
 }
 

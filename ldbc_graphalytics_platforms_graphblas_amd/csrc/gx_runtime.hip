@@ -5,6 +5,7 @@
 // The transforms run on the device with rocPRIM radix sorts over packed 64-bit
 // (row << 32 | col) keys, so their rows come out sorted by column.
 #include <cstring>
+#include <memory>
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
@@ -49,8 +50,23 @@ extern "C" int gx_init(int device, gx_ctx **out) {
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+    for (int i = 0; i < 2 && e == hipSuccess; i++) {
+        e = hipHostMalloc(&ctx->staging[i], gx_ctx::kStageBytes);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming);
+    }
+    // warm the runtime's fill and copy paths (first use initialises them): outside the
+    // processing time, like the reference's LAGraph_Init
+    if (e == hipSuccess) {
+        void *d = nullptr;
+        e = hipMalloc(&d, 1 << 20);
+        if (e == hipSuccess) e = hipMemsetAsync(d, 0, 1 << 20, ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d, ctx->staging[0], 1 << 20, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(ctx->staging[1], d, 1 << 20, hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (d) (void)hipFree(d);
+    }
     if (e != hipSuccess) {
-        delete ctx;
+        gx_free(ctx);
         return fail(GX_DEVICE_ERROR, std::string("gx_init: ") + hipGetErrorString(e));
     }
     *out = ctx;
@@ -73,6 +89,10 @@ extern "C" int gx_free(gx_ctx *ctx) {
         if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
     }
     if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
+    for (int i = 0; i < 2; i++) {
+        if (ctx->stage_ev[i]) (void)hipEventDestroy(ctx->stage_ev[i]);
+        if (ctx->staging[i]) (void)hipHostFree(ctx->staging[i]);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return GX_SUCCESS;
@@ -123,6 +143,45 @@ int slab_rows(const int64_t *rp, int64_t n, int64_t nslabs, int64_t *srow, hipSt
     hipLaunchKernelGGL(k_slab_rows, dim3(grid_for((uint64_t)std::max<int64_t>(n, 1), 256, 8192)), dim3(256), 0, s, rp,
                        n, nslabs, srow);
     return check_launch("k_slab_rows");
+}
+
+int download(gx_ctx *ctx, void *dst, const void *src_dev, uint64_t count, Xfer kind) {
+    const size_t elem = kind == Xfer::Raw64 ? 8 : 4;
+    const uint64_t chunk = gx_ctx::kStageBytes / elem;
+    hipStream_t s = ctx->stream;
+    auto convert = [&](uint64_t off, uint64_t cnt, const void *buf) {
+        switch (kind) {
+            case Xfer::Raw64:
+                host_copy(static_cast<char *>(dst) + off * 8, buf, cnt * 8);
+                break;
+            case Xfer::Levels:
+                host_levels(static_cast<const int32_t *>(buf), cnt, static_cast<int64_t *>(dst) + off);
+                break;
+            case Xfer::Widen32:
+                host_widen(static_cast<const int32_t *>(buf), cnt, static_cast<uint64_t *>(dst) + off);
+                break;
+        }
+    };
+    uint64_t prev_off = 0, prev_cnt = 0;
+    int c = 0;
+    for (uint64_t off = 0; off < count; off += chunk, c++) {
+        const int b = c & 1;
+        const uint64_t cnt = std::min<uint64_t>(chunk, count - off);
+        GX_HIP_TRY(hipMemcpyAsync(ctx->staging[b], static_cast<const char *>(src_dev) + off * elem, cnt * elem,
+                                  hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipEventRecord(ctx->stage_ev[b], s));
+        if (c >= 1) {   // convert the previous chunk while this one copies
+            GX_HIP_TRY(hipEventSynchronize(ctx->stage_ev[b ^ 1]));
+            convert(prev_off, prev_cnt, ctx->staging[b ^ 1]);
+        }
+        prev_off = off;
+        prev_cnt = cnt;
+    }
+    if (c >= 1) {
+        GX_HIP_TRY(hipEventSynchronize(ctx->stage_ev[(c - 1) & 1]));
+        convert(prev_off, prev_cnt, ctx->staging[(c - 1) & 1]);
+    }
+    return GX_SUCCESS;
 }
 
 int ensure_aux_streams(gx_ctx *ctx) {
@@ -182,6 +241,38 @@ extern "C" int gx_last_device_ms(gx_ctx *ctx, double *ms) {
 
 // --------------------------------------------------------------------------- graph
 
+namespace gx {
+namespace {
+
+// Host -> device in chunks through the context's two pinned staging buffers: host threads
+// fill one (conversion / validation) while the DMA engine drains the other.  Replaces one
+// single-threaded conversion pass plus a pageable copy, which dominated the Graphalytics
+// processing time of the small-iteration algorithms.
+// fill(first, count, staging) writes `count` elements of `elem` bytes; false = bad input.
+template <class Fill>
+int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool *bad) {
+    const uint64_t chunk = gx_ctx::kStageBytes / elem;
+    hipStream_t s = ctx->stream;
+    *bad = false;
+    int c = 0;
+    for (uint64_t off = 0; off < count; off += chunk, c++) {
+        const int b = c & 1;
+        const uint64_t cnt = std::min<uint64_t>(chunk, count - off);
+        if (c >= 2) GX_HIP_TRY(hipEventSynchronize(ctx->stage_ev[b]));   // its previous copy is done
+        if (!fill(off, cnt, ctx->staging[b])) {
+            *bad = true;
+            break;
+        }
+        GX_HIP_TRY(hipMemcpyAsync(dst + off * elem, ctx->staging[b], cnt * elem, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipEventRecord(ctx->stage_ev[b], s));
+    }
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    return GX_SUCCESS;
+}
+
+}  // namespace
+}  // namespace gx
+
 extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **out) {
     if (!ctx || !A || !out) return fail(GX_NULL_POINTER, "gx_graph_create: null argument");
     *out = nullptr;
@@ -191,18 +282,10 @@ extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_gr
         return fail(GX_NOT_IMPLEMENTED, "gx_graph_create: n >= 2^31 needs 64-bit column indices");
     if (A->rowptr[0] != 0 || A->rowptr[A->n] != A->nnz)
         return fail(GX_INVALID_VALUE, "gx_graph_create: inconsistent row pointers");
+    if (!host_monotone(A->rowptr, A->n)) return fail(GX_INVALID_VALUE, "gx_graph_create: row pointers not monotone");
     GX_HIP_TRY(hipSetDevice(ctx->device));
     const uint64_t n = A->n, nnz = A->nnz;
-    std::vector<int32_t> ci(nnz);
-    for (uint64_t i = 0; i < n; i++) {
-        if (A->rowptr[i + 1] < A->rowptr[i])
-            return fail(GX_INVALID_VALUE, "gx_graph_create: row pointers not monotone");
-    }
-    for (uint64_t k = 0; k < nnz; k++) {
-        if (A->colidx[k] >= n) return fail(GX_INVALID_INDEX, "gx_graph_create: column out of range");
-        ci[k] = (int32_t)A->colidx[k];
-    }
-    gx_graph *g = new gx_graph();
+    std::unique_ptr<gx_graph> g(new gx_graph());
     g->ctx = ctx;
     g->n = n;
     g->nnz = nnz;
@@ -210,24 +293,30 @@ extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_gr
     g->weighted = A->vals != nullptr;
     g->A.n = n;
     g->A.nnz = nnz;
-    g->A.h_rp.assign(A->rowptr, A->rowptr + n + 1);
-    int rc = g->A.rp.alloc(n + 1);
-    if (rc == GX_SUCCESS) rc = g->A.ci.alloc(nnz, 16);
-    if (rc == GX_SUCCESS && g->weighted) rc = g->A.w.alloc(nnz);
-    if (rc != GX_SUCCESS) {
-        delete g;
-        return rc;
-    }
-    hipError_t e = hipMemcpy(g->A.rp.p, g->A.h_rp.data(), (n + 1) * 8, hipMemcpyHostToDevice);
-    if (e == hipSuccess && nnz) e = hipMemcpy(g->A.ci.p, ci.data(), nnz * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess && g->weighted && nnz)
-        e = hipMemcpy(g->A.w.p, A->vals, nnz * 8, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        delete g;
-        return fail(GX_DEVICE_ERROR, std::string("gx_graph_create: upload failed: ") + hipGetErrorString(e));
-    }
+    g->A.h_rp.resize(n + 1);
+    host_copy(g->A.h_rp.data(), A->rowptr, (n + 1) * 8);
+    GX_TRY(g->A.rp.alloc(n + 1));
+    GX_TRY(g->A.ci.alloc(nnz, 16));
+    if (g->weighted) GX_TRY(g->A.w.alloc(nnz));
+    bool bad = false;
+    GX_TRY(upload(ctx, reinterpret_cast<char *>(g->A.rp.p), n + 1, 8,
+                  [&](uint64_t off, uint64_t cnt, void *buf) {
+                      host_copy(buf, g->A.h_rp.data() + off, cnt * 8);
+                      return true;
+                  }, &bad));
+    GX_TRY(upload(ctx, reinterpret_cast<char *>(g->A.ci.p), nnz, 4,
+                  [&](uint64_t off, uint64_t cnt, void *buf) {
+                      return host_narrow(A->colidx + off, cnt, n, static_cast<int32_t *>(buf));
+                  }, &bad));
+    if (bad) return fail(GX_INVALID_INDEX, "gx_graph_create: column out of range");
+    if (g->weighted)
+        GX_TRY(upload(ctx, reinterpret_cast<char *>(g->A.w.p), nnz, 8,
+                      [&](uint64_t off, uint64_t cnt, void *buf) {
+                          host_copy(buf, static_cast<const double *>(A->vals) + off, cnt * 8);
+                          return true;
+                      }, &bad));
     g->A.built = true;
-    *out = g;
+    *out = g.release();
     return GX_SUCCESS;
 }
 

@@ -773,6 +773,6 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
                      delta, h.round, (long long)h.cur, h.epoch, (unsigned long long)steps, c[0], c[1], c[2], c[3],
                      c[4], c[5], c[6], c[7]);
     }
-    GX_HIP_TRY(hipMemcpy(dist_out, dist.p, n * 8, hipMemcpyDeviceToHost));
+    GX_TRY(download(ctx, dist_out, dist.p, (uint64_t)n, Xfer::Raw64));
     return GX_SUCCESS;
 }

@@ -224,8 +224,6 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         if (round > 100000) return fail(GX_PANIC, "gx_wcc: hooking did not converge");
     }
     GX_TRY(device_end(ctx));
-    std::vector<int32_t> h(n);
-    GX_HIP_TRY(hipMemcpy(h.data(), parent.p, n * 4, hipMemcpyDeviceToHost));
-    for (int64_t v = 0; v < n; v++) comp[v] = (uint64_t)h[v];
+    GX_TRY(download(ctx, comp, parent.p, (uint64_t)n, Xfer::Widen32));
     return GX_SUCCESS;
 }

@@ -129,8 +129,10 @@ int Main(int argc, char **argv, Algorithm alg) {
         std::vector<double> vals;
         std::vector<uint64_t> labels;
 
-        std::cout << "Processing starts at: " << GetCurrentMilliseconds() << std::endl;
+        const auto t_start = GetCurrentMilliseconds();
+        std::cout << "Processing starts at: " << t_start << std::endl;
         OK(gx_graph_create(H.ctx, &A.csr, p.directed ? 1 : 0, &H.g), "gx_graph_create");
+        const auto t_uploaded = GetCurrentMilliseconds();
         switch (alg) {
             case Algorithm::BFS:
                 level.resize(n);
@@ -157,9 +159,12 @@ int Main(int argc, char **argv, Algorithm alg) {
                 OK(gx_lcc(H.g, vals.data()), "gx_lcc");
                 break;
         }
-        std::cout << "Processing ends at: " << GetCurrentMilliseconds() << std::endl;
+        const auto t_end = GetCurrentMilliseconds();
+        std::cout << "Processing ends at: " << t_end << std::endl;
         double dev_ms = 0;
         gx_last_device_ms(H.ctx, &dev_ms);
+        std::cout << "Upload time: " << (t_uploaded - t_start) << " ms" << std::endl;
+        std::cout << "Algorithm time: " << (t_end - t_uploaded) << " ms" << std::endl;
         std::cout << "Device time: " << dev_ms << " ms" << std::endl;
 
         OutFile out(p.output_file);
