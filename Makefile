@@ -42,7 +42,7 @@ $(BUILD)/%.o: $(CSRC)/%.cpp $(wildcard $(CSRC)/*.h) include/gx.h | $(BUILD)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
 $(LIBGX): $(HIP_OBJS) $(HOST_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -Wl,-soname,libgx.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -ldl -Wl,-soname,libgx.so
 
 $(BUILD)/exe_common.o: $(EXESRC)/common.cpp $(EXESRC)/common.h include/gx.h | $(BUILD)
 	$(CXX) $(CXXFLAGS) -c $< -o $@

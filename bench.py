@@ -398,8 +398,8 @@ def main():
 
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
-    from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import GpuStep, PartitionedPageRank, hub_relabel, \
-        local_pieces, local_rows
+    from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import Comm, DevicePageRank, GpuStep, \
+        PartitionedPageRank, hub_relabel, local_pieces, local_rows
 
     gname = args.graph or "SYN-7_5"
     workload = f"PageRank {gname} (R-MAT scale {args.scale}, ef {args.edgefactor}, seed {args.seed}, undirected)"
@@ -423,9 +423,33 @@ def main():
     # a real (non-null) stream: libgx launches on it and RCCL orders against it
     stream = torch.cuda.Stream(device)
     torch.cuda.set_stream(stream)
-    gather = (lambda out, inp: dist.all_gather_into_tensor(out, inp, async_op=True)) if dist else None
-    pr = PartitionedPageRank(steppers, world, [lr.rows for lr in lrs], device, all_gather=gather,
-                             stream_handle=lambda: stream.cuda_stream)
+    # driver "device" (default): libgx enqueues the whole run -- SpMVs and ncclAllGathers on its
+    # own RCCL communicator -- and replays it as one hipGraph; "host": one ctypes call and one
+    # torch.distributed all-gather per piece and iteration (pr_partition.PartitionedPageRank)
+    driver = os.environ.get("GX_PR_DRIVER", "device")
+    use_graph = os.environ.get("GX_PR_GRAPH", "1") != "0"
+    comm = None
+    if driver == "device":
+        if dist:
+            def share_id(uid: bytes) -> bytes:
+                box = [uid]
+                dist.broadcast_object_list(box, src=0)
+                return box[0]
+            comm = Comm(ctx, world, rank, share_id)
+        dpr = DevicePageRank(steppers, comm, use_graph=use_graph)
+
+        class _Run:
+            def run(self, iters):
+                dpr.run(iters, stream.cuda_stream)
+        pr = _Run()
+    else:
+        gather = (lambda out, inp: dist.all_gather_into_tensor(out, inp, async_op=True)) if dist else None
+        pr = PartitionedPageRank(steppers, world, [lr.rows for lr in lrs], device, all_gather=gather,
+                                 stream_handle=lambda: stream.cuda_stream)
+    # hipEvents around every k_pr_pull launch during the timed steps (roofline.achieved).  At
+    # N > 1 the timed steps replay the captured graph (events would force direct launches), so
+    # the launch durations come from an instrumented pass right after them instead.
+    events_in_timed = world == 1 or driver != "device" or not use_graph
 
     def barrier():
         torch.cuda.synchronize(device)
@@ -441,13 +465,18 @@ def main():
         pr.run(args.iters)
     barrier()
     ctx.reset_kernel_stats()
-    ctx.set_kernel_timing(True)
+    ctx.set_kernel_timing(events_in_timed)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pr.run(args.iters)
     barrier()
     elapsed = time.perf_counter() - t0
+    if not events_in_timed:
+        ctx.set_kernel_timing(True)
+        for _ in range(max(1, min(args.steps, 5))):
+            pr.run(args.iters)
+        barrier()
     ctx.set_kernel_timing(False)
     launches, pull_ms = ctx.kernel_stats("pr_pull")
     if dist:
@@ -456,7 +485,10 @@ def main():
         elapsed = float(t.item())
 
     # result of the last step (for the parity check on rank 0), assembled by virtual rank
-    mine = [(lr.rank, o[:lr.rows].detach().cpu().numpy()) for lr, o in zip(lrs, pr.rank_outs)]
+    if driver == "device":
+        mine = list(zip([lr.rank for lr in lrs], dpr.scores([lr.rows for lr in lrs])))
+    else:
+        mine = [(lr.rank, o[:lr.rows].detach().cpu().numpy()) for lr, o in zip(lrs, pr.rank_outs)]
     if dist:
         parts = [None] * world
         dist.all_gather_object(parts, mine)
@@ -516,6 +548,8 @@ def main():
                 "iterations": args.iters,
                 "damping": args.damping,
                 "parallelism": f"row{world}" + (f", {pieces} pipelined pieces" if pieces > 1 else ""),
+                "driver": driver + (", hipGraph" if driver == "device" and use_graph else ""),
+                "roofline_events": "timed steps" if events_in_timed else "instrumented pass after the timed steps",
                 "device": dev_name,
                 "cus": cus,
             },
@@ -540,6 +574,10 @@ def main():
             "graph_gen_s": t_gen,
         }
         print(json.dumps(line), flush=True)
+    if driver == "device":
+        dpr.close()
+        if comm is not None:
+            comm.close()
     for st in steppers:
         st.close()
     ctx.close()

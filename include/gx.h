@@ -178,6 +178,37 @@ int gx_pr_part_step(gx_pr_part *part, const double *x_full, double *x_local,
                     double *rank_out, void *stream);
 int gx_pr_part_free(gx_pr_part *part);
 
+/* ---- device-driven multi-GPU PageRank (RCCL inside libgx) --------------------------
+ * The same partition, but the whole run -- init, every iteration's SpMV and every
+ * all-gather -- is enqueued by one call (optionally captured once into a hipGraph and
+ * replayed), instead of one host round trip per iteration and rank.
+ * Replaces the per-iteration GrB_mxv of LAGr_PageRankGX (pr.cpp:61) on N GPUs.
+ *
+ *   gx_comm_unique_id : rank 0 creates the RCCL id (128 opaque bytes); the caller
+ *                       shares it with every rank (e.g. torch.distributed broadcast).
+ *   gx_comm_create    : collective over the `nranks` processes (ncclCommInitRank); rank
+ *                       numbering must equal the partition's.
+ *   gx_pr_dist_create : `npieces` pieces of this rank, piece p = virtual rank
+ *                       p*nranks + rank of a gx_pr_part partition into nranks*npieces
+ *                       ranges (pr_partition.local_pieces).  comm == NULL means one rank
+ *                       (pieces exchanged by device copies).  Borrows the pieces.
+ *   gx_pr_dist_run    : `iters` iterations; use_graph != 0 captures the run into a
+ *                       hipGraph on first use (re-captured when iters/stream change) and
+ *                       replays it.  Asynchronous on `stream` (NULL = context stream).
+ *                       With kernel timing on (gx_set_kernel_timing) launches are direct.
+ *   gx_pr_dist_scores : waits for the last run, copies piece `piece`'s scores (its rows,
+ *                       in the partition's row order) to host memory.
+ * ------------------------------------------------------------------------------- */
+typedef struct gx_comm gx_comm;
+typedef struct gx_pr_dist gx_pr_dist;
+int gx_comm_unique_id(uint8_t *id /* 128 bytes */);
+int gx_comm_create(gx_ctx *ctx, int nranks, int rank, const uint8_t *id, gx_comm **comm);
+int gx_comm_free(gx_comm *comm);
+int gx_pr_dist_create(gx_comm *comm, gx_pr_part *const *pieces, int npieces, gx_pr_dist **dist);
+int gx_pr_dist_run(gx_pr_dist *dist, int iters, int use_graph, void *stream);
+int gx_pr_dist_scores(gx_pr_dist *dist, int piece, double *scores);
+int gx_pr_dist_free(gx_pr_dist *dist);
+
 /* ---------------------------------------------------------------------------------
  * Multi-GPU steps for the other algorithms.  The graph is replicated on
  * every rank (gx_graph_create on each device); rank k owns the vertex range

@@ -75,6 +75,13 @@ SIGNATURES = [
     ("gx_pr_part_init", C.c_int, [_P, _P, _P]),
     ("gx_pr_part_step", C.c_int, [_P, _P, _P, _P, _P]),
     ("gx_pr_part_free", C.c_int, [_P]),
+    ("gx_comm_unique_id", C.c_int, [C.c_char_p]),
+    ("gx_comm_create", C.c_int, [_P, C.c_int, C.c_int, C.c_char_p, C.POINTER(_P)]),
+    ("gx_comm_free", C.c_int, [_P]),
+    ("gx_pr_dist_create", C.c_int, [_P, C.POINTER(_P), C.c_int, C.POINTER(_P)]),
+    ("gx_pr_dist_run", C.c_int, [_P, C.c_int, C.c_int, _P]),
+    ("gx_pr_dist_scores", C.c_int, [_P, C.c_int, _DP]),
+    ("gx_pr_dist_free", C.c_int, [_P]),
     # multi-GPU steps (device pointers as c_void_p)
     ("gx_bfs_part_init", C.c_int, [_P, C.c_uint64, _P, _P]),
     ("gx_bfs_part_expand", C.c_int, [_P, C.c_uint64, C.c_uint64, _P, C.c_int64, _P, _P]),

@@ -1,0 +1,324 @@
+// gx_comm.hip -- RCCL communicator and the device-driven partitioned PageRank loop.
+//
+// the pull matrix is 1-D row partitioned over the GPUs (one process per GPU)
+// and the rank vector is all-gathered over xGMI every iteration.  The reference has no
+// distributed path; this replaces the per-iteration GrB_mxv of LAGr_PageRankGX
+// (pr.cpp:61) when it runs on several GPUs.
+//
+// gx_pr_part_step is one iteration of one rank (or piece); driving the iterations from
+// Python costs one ctypes call plus one torch.distributed collective per piece and
+// iteration (~60 us of host time each, measured), more than the per-rank SpMV at 8 GPUs.
+// gx_pr_dist runs a whole PageRank from here instead: every kernel and every
+// ncclAllGather is enqueued by one C call, and with `use_graph` the whole run (init, all
+// iterations, all gathers) is captured once into a hipGraph and replayed, so the host
+// cost per run is one graph launch.
+//
+// Pipelining (pr_partition.local_pieces): a rank owns `npieces` virtual ranks
+// p * nranks + rank.  Piece p's chunks of all ranks form one contiguous slab of the
+// exchanged vector, so each piece is gathered by its own ncclAllGather on the comm
+// stream while the compute stream runs the next piece's SpMV:
+//
+//   compute: step(0) step(1) ... step(P-1) |wait comm| step(0) ...
+//   comm   :        gather(0) gather(1) ... gather(P-1)|
+//
+// The vector is double-buffered (x_read / x_write) so a gather never overwrites values
+// that a later piece of the same iteration still reads.
+//
+// RCCL is opened lazily with dlopen: torch's copy when the process already has one
+// (same soname, librccl.so.1), else ROCm's.  libgx itself has no link dependency on it,
+// so the single-GPU executables never load RCCL.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "gx_pr.h"
+
+namespace gx {
+namespace {
+
+struct Rccl {
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+    std::string error;
+    bool ok = false;
+};
+
+const Rccl &rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);   // torch's, if loaded
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char *e = dlerror();
+            r.error = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+            return;
+        }
+        r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
+        r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+        r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.error_string;
+        if (!r.ok) r.error = "librccl.so.1 lacks an expected entry point";
+    });
+    return r;
+}
+
+int rccl_fail(const char *what, ncclResult_t e) {
+    return fail(GX_DEVICE_ERROR, std::string(what) + ": " + rccl().error_string(e));
+}
+
+#define GX_NCCL_TRY(what, expr)                         \
+    do {                                                \
+        ncclResult_t _r = (expr);                       \
+        if (_r != ncclSuccess) return rccl_fail(what, _r); \
+    } while (0)
+
+}  // namespace
+}  // namespace gx
+
+using namespace gx;
+
+struct gx_comm {
+    gx_ctx *ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+namespace {
+
+struct PrDist {
+    gx_ctx *ctx = nullptr;
+    gx_comm *comm = nullptr;           // null: one rank (pieces exchanged by D2D copies)
+    std::vector<PrPart *> pieces;
+    int world = 1, rank = 0;           // real ranks
+    uint64_t chunk = 0;
+    DBuf<double> xa, xb;               // gathered vector, double-buffered
+    std::vector<std::unique_ptr<DBuf<double>>> xl;   // per piece: its local chunk
+    std::vector<std::unique_ptr<DBuf<double>>> ro;   // per piece: scores of its rows
+    hipStream_t cs = nullptr;          // comm stream
+    std::vector<hipEvent_t> ev_piece;
+    hipEvent_t ev_comm = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    hipGraph_t graph = nullptr;
+    int g_iters = -1;
+    hipStream_t g_stream = nullptr;
+    hipStream_t last_stream = nullptr;
+
+    ~PrDist() {
+        (void)hipSetDevice(ctx->device);
+        if (gexec) (void)hipGraphExecDestroy(gexec);
+        if (graph) (void)hipGraphDestroy(graph);
+        for (hipEvent_t e : ev_piece) (void)hipEventDestroy(e);
+        if (ev_comm) (void)hipEventDestroy(ev_comm);
+        if (cs) (void)hipStreamDestroy(cs);
+    }
+
+    size_t span() const { return chunk * (size_t)world; }   // one piece's slab
+
+    // exchange piece p's local chunk into slab p of `x` (after what s has enqueued so far)
+    int gather(int p, double *x, hipStream_t s) {
+        double *dst = x + (size_t)p * span();
+        if (!comm) {
+            GX_HIP_TRY(hipMemcpyAsync(dst, xl[p]->p, chunk * sizeof(double), hipMemcpyDeviceToDevice, s));
+            return GX_SUCCESS;
+        }
+        GX_HIP_TRY(hipEventRecord(ev_piece[p], s));
+        GX_HIP_TRY(hipStreamWaitEvent(cs, ev_piece[p], 0));
+        GX_NCCL_TRY("ncclAllGather", rccl().all_gather(xl[p]->p, dst, chunk, ncclFloat64, comm->comm, cs));
+        return GX_SUCCESS;
+    }
+
+    int join(hipStream_t s) {   // compute stream waits for every gather issued so far
+        if (!comm) return GX_SUCCESS;
+        GX_HIP_TRY(hipEventRecord(ev_comm, cs));
+        GX_HIP_TRY(hipStreamWaitEvent(s, ev_comm, 0));
+        return GX_SUCCESS;
+    }
+
+    int enqueue(int iters, hipStream_t s) {
+        const int np = (int)pieces.size();
+        const bool swap_only = !comm && np == 1;   // one rank, one piece: no exchange at all
+        double *xr = xa.p, *xw = xb.p;
+        for (int p = 0; p < np; p++) GX_TRY(pr_init(pieces[p], swap_only ? xr : xl[p]->p, s));
+        if (!swap_only) {
+            for (int p = 0; p < np; p++) GX_TRY(gather(p, xr, s));
+            GX_TRY(join(s));
+        }
+        for (int it = 0; it < iters; it++) {
+            const bool last = it == iters - 1;
+            for (int p = 0; p < np; p++) {
+                double *out = swap_only ? xw : xl[p]->p;
+                GX_TRY(pr_step(pieces[p], xr, out, last ? ro[p]->p : nullptr, s));
+                if (!last && !swap_only) GX_TRY(gather(p, xw, s));
+            }
+            if (last) break;
+            if (!swap_only) GX_TRY(join(s));
+            std::swap(xr, xw);
+        }
+        return GX_SUCCESS;
+    }
+
+    int run(int iters, bool use_graph, hipStream_t s) {
+        last_stream = s;
+        // kernel timing brackets launches with events, which a replayed graph would not
+        // refresh: timed runs go through direct launches
+        if (!use_graph || ctx->timing) return enqueue(iters, s);
+        if (!gexec || g_iters != iters || g_stream != s) {
+            if (gexec) (void)hipGraphExecDestroy(gexec);
+            if (graph) (void)hipGraphDestroy(graph);
+            gexec = nullptr;
+            graph = nullptr;
+            GX_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            const int rc = enqueue(iters, s);
+            hipGraph_t g = nullptr;
+            const hipError_t e = hipStreamEndCapture(s, &g);
+            if (rc != GX_SUCCESS) {
+                if (g) (void)hipGraphDestroy(g);
+                return rc;
+            }
+            if (e != hipSuccess) return fail(GX_DEVICE_ERROR, std::string("PageRank capture: ") + hipGetErrorString(e));
+            graph = g;
+            GX_HIP_TRY(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+            g_iters = iters;
+            g_stream = s;
+        }
+        GX_HIP_TRY(hipGraphLaunch(gexec, s));
+        return GX_SUCCESS;
+    }
+};
+
+}  // namespace
+
+struct gx_pr_dist {
+    PrDist d;
+};
+
+extern "C" int gx_comm_unique_id(uint8_t *id) {
+    if (!id) return fail(GX_NULL_POINTER, "gx_comm_unique_id: null argument");
+    const Rccl &r = rccl();
+    if (!r.ok) return fail(GX_NOT_IMPLEMENTED, r.error);
+    ncclUniqueId u;
+    GX_NCCL_TRY("ncclGetUniqueId", r.get_unique_id(&u));
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_comm_create(gx_ctx *ctx, int nranks, int rank, const uint8_t *id, gx_comm **out) {
+    if (!ctx || !id || !out) return fail(GX_NULL_POINTER, "gx_comm_create: null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GX_INVALID_VALUE, "gx_comm_create: bad rank/nranks");
+    const Rccl &r = rccl();
+    if (!r.ok) return fail(GX_NOT_IMPLEMENTED, r.error);
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t c = nullptr;
+    GX_NCCL_TRY("ncclCommInitRank", r.comm_init_rank(&c, nranks, u, rank));
+    auto *cm = new gx_comm();
+    cm->ctx = ctx;
+    cm->comm = c;
+    cm->nranks = nranks;
+    cm->rank = rank;
+    *out = cm;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_comm_free(gx_comm *comm) {
+    if (!comm) return GX_SUCCESS;
+    (void)hipSetDevice(comm->ctx->device);
+    (void)hipDeviceSynchronize();
+    if (comm->comm) (void)rccl().comm_destroy(comm->comm);
+    delete comm;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_pr_dist_create(gx_comm *comm, gx_pr_part *const *parts, int npieces, gx_pr_dist **out) {
+    if (!parts || !out || npieces < 1) return fail(GX_NULL_POINTER, "gx_pr_dist_create: null argument");
+    const int world = comm ? comm->nranks : 1, rank = comm ? comm->rank : 0;
+    PrPart *p0 = reinterpret_cast<PrPart *>(parts[0]);
+    if (!p0) return fail(GX_NULL_POINTER, "gx_pr_dist_create: null piece");
+    if (comm && comm->ctx != p0->ctx) return fail(GX_INVALID_VALUE, "gx_pr_dist_create: comm and pieces on different contexts");
+    for (int p = 0; p < npieces; p++) {
+        PrPart *q = reinterpret_cast<PrPart *>(parts[p]);
+        if (!q) return fail(GX_NULL_POINTER, "gx_pr_dist_create: null piece");
+        if (q->ctx != p0->ctx || q->chunk != p0->chunk || q->n_global != p0->n_global)
+            return fail(GX_INVALID_VALUE, "gx_pr_dist_create: pieces of different partitions");
+        if (q->nranks != world * npieces || q->rank != p * world + rank)
+            return fail(GX_INVALID_VALUE, "gx_pr_dist_create: piece p must be virtual rank p * nranks + rank "
+                                          "of a partition into nranks * npieces ranges");
+    }
+    gx_ctx *ctx = p0->ctx;
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    auto *h = new gx_pr_dist();
+    PrDist &d = h->d;
+    d.ctx = ctx;
+    d.comm = comm;
+    d.world = world;
+    d.rank = rank;
+    d.chunk = p0->chunk;
+    for (int p = 0; p < npieces; p++) d.pieces.push_back(reinterpret_cast<PrPart *>(parts[p]));
+    const size_t full = d.chunk * (size_t)world * (size_t)npieces;
+    int rc = d.xa.alloc(full);
+    if (rc == GX_SUCCESS) rc = d.xb.alloc(full);
+    d.xl.resize(npieces);
+    d.ro.resize(npieces);
+    for (int p = 0; p < npieces && rc == GX_SUCCESS; p++) {
+        rc = d.xl[p]->alloc(d.chunk);
+        if (rc == GX_SUCCESS) rc = d.ro[p]->alloc(std::max<uint64_t>(d.pieces[p]->rows, 1));
+    }
+    hipError_t e = hipSuccess;
+    if (rc == GX_SUCCESS) e = hipMemset(d.xa.p, 0, full * sizeof(double));
+    if (rc == GX_SUCCESS && e == hipSuccess) e = hipMemset(d.xb.p, 0, full * sizeof(double));
+    if (rc == GX_SUCCESS && e == hipSuccess && comm) {
+        e = hipStreamCreateWithFlags(&d.cs, hipStreamNonBlocking);
+        d.ev_piece.assign(npieces, nullptr);
+        for (int p = 0; p < npieces && e == hipSuccess; p++)
+            e = hipEventCreateWithFlags(&d.ev_piece[p], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&d.ev_comm, hipEventDisableTiming);
+    }
+    if (rc == GX_SUCCESS && e != hipSuccess)
+        rc = fail(GX_DEVICE_ERROR, std::string("gx_pr_dist_create: ") + hipGetErrorString(e));
+    if (rc != GX_SUCCESS) {
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_pr_dist_run(gx_pr_dist *h, int iters, int use_graph, void *stream) {
+    if (!h) return fail(GX_NULL_POINTER, "gx_pr_dist_run: null argument");
+    if (iters < 1) return fail(GX_INVALID_VALUE, "gx_pr_dist_run: iters must be >= 1");
+    PrDist &d = h->d;
+    GX_HIP_TRY(hipSetDevice(d.ctx->device));
+    return d.run(iters, use_graph != 0, stream ? (hipStream_t)stream : d.ctx->stream);
+}
+
+extern "C" int gx_pr_dist_scores(gx_pr_dist *h, int piece, double *scores) {
+    if (!h || !scores) return fail(GX_NULL_POINTER, "gx_pr_dist_scores: null argument");
+    PrDist &d = h->d;
+    if (piece < 0 || piece >= (int)d.pieces.size()) return fail(GX_INVALID_INDEX, "gx_pr_dist_scores: bad piece");
+    GX_HIP_TRY(hipSetDevice(d.ctx->device));
+    if (d.last_stream) GX_HIP_TRY(hipStreamSynchronize(d.last_stream));
+    const uint64_t rows = d.pieces[piece]->rows;
+    if (rows) GX_HIP_TRY(hipMemcpy(scores, d.ro[piece]->p, rows * sizeof(double), hipMemcpyDeviceToHost));
+    return GX_SUCCESS;
+}
+
+extern "C" int gx_pr_dist_free(gx_pr_dist *h) {
+    if (!h) return GX_SUCCESS;
+    (void)hipSetDevice(h->d.ctx->device);
+    (void)hipDeviceSynchronize();
+    delete h;
+    return GX_SUCCESS;
+}

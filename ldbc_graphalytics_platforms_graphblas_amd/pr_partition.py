@@ -222,3 +222,71 @@ class PartitionedPageRank:
                 self.x_read, self.x_write = self.x_write, self.x_read
         return self.rank_outs[0][:self.rows[0]] if npieces == 1 else \
             [o[:r] for o, r in zip(self.rank_outs, self.rows)]
+
+
+class Comm:
+    """RCCL communicator inside libgx (gx_comm_*), bootstrapped over torch.distributed.
+
+    Rank 0 creates the RCCL id (gx_comm_unique_id) and `share_id(bytes) -> bytes` hands it
+    to every rank (bench.py: torch.distributed.broadcast_object_list); the rank numbering is
+    the partition's.  ncclCommInitRank is collective: every rank constructs its Comm
+    together."""
+
+    def __init__(self, ctx, nranks: int, rank: int, share_id: Callable[[bytes], bytes]):
+        from . import _native as N
+        self.N = N
+        lib = N.lib()
+        uid = C.create_string_buffer(128)
+        if rank == 0:
+            N.check(lib.gx_comm_unique_id(uid), "gx_comm_unique_id")
+        got = share_id(uid.raw if rank == 0 else b"")
+        if len(got) != 128:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        uid = C.create_string_buffer(got, 128)
+        self.handle = C.c_void_p()
+        N.check(lib.gx_comm_create(ctx.handle, nranks, rank, uid, C.byref(self.handle)), "gx_comm_create")
+        self.nranks, self.rank = nranks, rank
+
+    def close(self) -> None:
+        if self.handle:
+            self.N.lib().gx_comm_free(self.handle)
+            self.handle = C.c_void_p()
+
+
+class DevicePageRank:
+    """The whole partitioned PageRank enqueued by libgx (gx_pr_dist_*): every iteration's
+    SpMV per piece and every ncclAllGather in one C call, optionally captured once into a
+    hipGraph and replayed (`use_graph`).  Same partition, pieces and results as
+    PartitionedPageRank, without a host round trip per iteration.
+
+    `steppers` are the GpuStep pieces of this rank (piece p = virtual rank p*nranks+rank);
+    `comm` is a Comm, or None for one rank."""
+
+    def __init__(self, steppers: Sequence["GpuStep"], comm: Optional[Comm], use_graph: bool = True):
+        from . import _native as N
+        self.N = N
+        self.steps = list(steppers)
+        arr = (C.c_void_p * len(self.steps))(*[s.part.value for s in self.steps])
+        self.handle = C.c_void_p()
+        N.check(N.lib().gx_pr_dist_create(comm.handle if comm is not None else None, arr, len(self.steps),
+                                          C.byref(self.handle)), "gx_pr_dist_create")
+        self.use_graph = use_graph
+
+    def run(self, iters: int, stream: int = 0) -> None:
+        """Asynchronous on `stream` (a hipStream_t handle; 0 = the context stream)."""
+        self.N.check(self.N.lib().gx_pr_dist_run(self.handle, iters, int(self.use_graph),
+                                                 C.c_void_p(stream) if stream else None), "gx_pr_dist_run")
+
+    def scores(self, rows: Sequence[int]) -> List[np.ndarray]:
+        """Per piece, the scores of its rows (waits for the last run)."""
+        out = []
+        for p, r in enumerate(rows):
+            a = np.zeros(max(r, 1), dtype=np.float64)
+            self.N.check(self.N.lib().gx_pr_dist_scores(self.handle, p, self.N.as_dp(a)), "gx_pr_dist_scores")
+            out.append(a[:r])
+        return out
+
+    def close(self) -> None:
+        if self.handle:
+            self.N.lib().gx_pr_dist_free(self.handle)
+            self.handle = C.c_void_p()
