@@ -270,8 +270,10 @@ extern "C" int gx_pr_dist_create(gx_comm *comm, gx_pr_part *const *parts, int np
     const size_t full = d.chunk * (size_t)world * (size_t)npieces;
     int rc = d.xa.alloc(full);
     if (rc == GX_SUCCESS) rc = d.xb.alloc(full);
-    d.xl.resize(npieces);
-    d.ro.resize(npieces);
+    for (int p = 0; p < npieces; p++) {
+        d.xl.emplace_back(new DBuf<double>());
+        d.ro.emplace_back(new DBuf<double>());
+    }
     for (int p = 0; p < npieces && rc == GX_SUCCESS; p++) {
         rc = d.xl[p]->alloc(d.chunk);
         if (rc == GX_SUCCESS) rc = d.ro[p]->alloc(std::max<uint64_t>(d.pieces[p]->rows, 1));

@@ -181,6 +181,9 @@ int device_end(gx_ctx *ctx);
 // Sort packed (row << 32 | col) keys (rows < n) in place (k1 = scratch of the same size)
 // and build row pointers / column indices from them.  rp must hold n + 1 entries and ci
 // m entries; keys end up sorted in *keys.
+// Radix sort of (u64 key, u32 value) pairs on bits [0, end_bit) of the key, into k_out / v_out.
+int sort_pairs_u64_u32(uint64_t *k_in, uint64_t *k_out, uint32_t *v_in, uint32_t *v_out, size_t m, int end_bit,
+                       hipStream_t s);
 int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,
                      int32_t *ci, hipStream_t s);
 

@@ -79,8 +79,21 @@ struct PrPart {
     uint32_t dgrid = 0;
     DBuf<double> dpart;
     DBuf<uint32_t> dticket;
-    // hub-cached kernel (default): wave items, LDS hub prefix, fused dangling reduction
-    int kernel = 1;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive, default)
+    // column-sorted blocks (k_pr_pull_sorted, gx_pr_sorted.hip; the default)
+    DBuf<int32_t> sci;           // columns sorted within each block
+    DBuf<uint32_t> spk;          // packed (column - group base) << 12 | row
+    DBuf<uint32_t> gbase;        // base column per 64-entry group (bit 31: escape to sci)
+    int sorted_nnz = 65536;      // entries per block
+    int sorted_rows = 4096;      // rows per block (LDS accumulators)
+    int long_nnz = 65536;        // longer rows take the LONG segment path
+    int sorted_lds = 0;          // dynamic LDS bytes of the launch
+    int sorted_variant = 0;      // tuning: block size / gathers in flight (gx_pr_sorted.hip)
+    DBuf<int64_t> ssplit;        // per block: first sorted entry in the tail pass
+    DBuf<double> ypart;          // hub-pass row sums
+    int64_t hot_cols = 262144;   // columns of the hub pass (2 MiB of x)
+    bool two_pass = false;
+    // hub-cached kernel: wave items, LDS hub prefix, fused dangling reduction
+    int kernel = 2;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive), 2 = k_pr_pull_sorted
     bool int4_loads = false;     // k_pr_pull: 16-B index loads (lane stride 4) instead of lane-consecutive
     DBuf<WaveItem> items;
     uint32_t nitems = 0;
@@ -105,6 +118,12 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp,
 int pr_plan_hub(PrPart *p, const std::vector<int64_t> &h_rp);
 // One iteration with k_pr_pull_hub (pull + fused dangling sum).
 int pr_step_hub(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
+
+// Column-sorted block plan (k_pr_pull_sorted) and its iteration (gx_pr_sorted.hip).
+int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp);
+int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
+// Dangling-score sum of this rank into x_local's last chunk slot.
+int pr_dangling(PrPart *p, double *x_local, hipStream_t s);
 
 int pr_init(PrPart *p, double *x_local, hipStream_t s);
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);

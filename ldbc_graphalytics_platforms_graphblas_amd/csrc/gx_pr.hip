@@ -377,14 +377,16 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     GX_TRY(p->dpart.alloc(p->dgrid));
     GX_TRY(p->dticket.alloc(1));
     GX_HIP_TRY(hipMemset(p->dticket.p, 0, 4));
-    // kernel choice: GX_PR_KERNEL = hub (default) | adaptive
-    if (const char *e = std::getenv("GX_PR_KERNEL")) p->kernel = std::strcmp(e, "hub") == 0 ? 0 : 1;
+    // kernel choice: GX_PR_KERNEL = sorted (default) | adaptive | hub
+    if (const char *e = std::getenv("GX_PR_KERNEL"))
+        p->kernel = std::strcmp(e, "hub") == 0 ? 0 : std::strcmp(e, "adaptive") == 0 ? 1 : 2;
     if (const char *e = std::getenv("GX_PR_INT4")) p->int4_loads = std::atoi(e) != 0;
     if (p->kernel == 0) GX_TRY(pr_plan_hub(p, h_rp));
+    if (p->kernel == 2) GX_TRY(pr_plan_sorted(p, h_rp));
     return GX_SUCCESS;
 }
 
-static int pr_dangling(PrPart *p, double *x_local, hipStream_t s) {
+int pr_dangling(PrPart *p, double *x_local, hipStream_t s) {
     if (p->nd == 0) return GX_SUCCESS;
     const int64_t per = (int64_t)((p->nd + p->dgrid - 1) / p->dgrid);
     hipLaunchKernelGGL(k_pr_dangling, dim3(p->dgrid), dim3(256), 0, s, p->d_range ? nullptr : p->dlist.p,
@@ -404,6 +406,7 @@ int pr_init(PrPart *p, double *x_local, hipStream_t s) {
 
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s) {
     if (p->kernel == 0) return pr_step_hub(p, x_full, x_local, rank_out, s);
+    if (p->kernel == 2) return pr_step_sorted(p, x_full, x_local, rank_out, s);
     const double dn = (double)p->n_global;
     PullArgs a;
     a.blocks = p->blocks.p;

@@ -1,0 +1,461 @@
+// gx_pr_sorted.hip -- PageRank pull SpMV over column-sorted row blocks (k_pr_pull_sorted).
+//
+// Same iteration as k_pr_pull (gx_pr.hip; Graphalytics PR, LAGr_PageRankGX pr.cpp:61):
+//     r(v) = teleport + sum_{u in in(v)} x(u);   x'(v) = r(v) / (outdeg(v)/d)
+// but the x gathers are issued in column order.
+//
+// Why: the x gathers are random 8-byte reads, and what bounds them is the number of 128-B
+// line requests they generate (each distinct line a wave-instruction touches is one L1
+// miss), not the HBM bytes of the matrix.  Gathering row by row, a 64-lane
+// instruction covered 1.33 gathers per line on SYN-7_5 (44.7 M L2 requests per launch).
+// Sorting the entries of a block of rows by column id puts equal and neighbouring columns
+// into the same instruction, and each block sweeps x in increasing address order
+// (17.1 M requests with 64 Ki-entry blocks).
+//
+// Layout (built once per plan on the device by a radix sort of (block << 32 | column)):
+//   spk[e]   uint32 : (column - group base) << 12 | row of the entry within its block
+//   gbase[g] uint32 : base column of 64-entry group g (one wave-instruction); bit 31 set =
+//                     escape: the group spans >= 2^20 columns and reads them from sci
+//   sci[e]   int32  : the block-sorted columns (escape groups, pass split, plan)
+// A block keeps the CSR range [rp[row_begin], rp[row_end]) of its <= 4096 rows, so the
+// per-row epilogue is unchanged, and streams 4 B per entry like the CSR column index.
+// Gathered values are added into LDS row accumulators (ds_add_f64) in wave-arrival order:
+// scores agree with the row-order sum to ~1e-15 relative but are not bit-reproducible run
+// to run (the parity bar is 1e-12 relative, tests/test_gpu_parity.py).
+//
+// Two passes (one rank, columns reaching past `hot_cols`): the hub pass gathers only
+// columns below hot_cols (2 MiB of x by default, 96 % of SYN-7_5's entries; that slice
+// stays resident in every XCD's 4 MiB L2) and stores the row sums; the tail pass adds the
+// other columns and runs the epilogue.  A block's hub entries are a prefix of its sorted
+// order, so each pass streams one contiguous range per block (`split`).
+//
+// Rows longer than `long_nnz` keep the LONG path of k_pr_pull (a workgroup per 8192-entry
+// segment of the row, segments combined by the last arriver) in the hub pass; their blocks
+// come first.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "gx_pr.h"
+
+namespace gx {
+namespace {
+
+struct SortedArgs {
+    const RowBlock *blocks;
+    const int64_t *split;    // per block: first sorted entry whose column is >= hot_cols
+    const int32_t *ci;       // row-order columns (LONG rows)
+    const int32_t *sci;      // block-sorted columns (escape groups)
+    const uint32_t *spk;     // packed entries
+    const uint32_t *gbase;   // per 64-entry group: base column, bit 31 = escape
+    const int32_t *outdeg;
+    const double *x_in;
+    double *x_out;
+    double *rank_out;
+    double *ypart;           // hub-pass row sums (two passes)
+    int64_t chunk;
+    int nranks;
+    int zero_slot;
+    double teleport0, damping_over_n, damping;
+    const int32_t *long_first;
+    const int32_t *long_nseg;
+    double *long_part;
+    uint32_t *long_ticket;
+};
+
+__device__ __forceinline__ void sorted_epilogue(const SortedArgs &a, int32_t row, double s, double teleport) {
+    const double r = teleport + s;
+    if (a.rank_out) a.rank_out[row] = r;
+    const int32_t deg = a.outdeg[row];
+    a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+}
+
+// BS threads, U gathers in flight per lane.
+//   PASS 0 : every entry, then the epilogue (one pass).
+//   PASS 1 : hub pass -- entries with column < hot_cols, row sums stored to ypart; LONG rows
+//            are complete here.
+//   PASS 2 : tail pass over the sorted blocks only -- entries with column >= hot_cols added
+//            to ypart, then the epilogue.
+// PIPE: the next round's entries are loaded while this round's gathers are in flight.
+template <int BS, int U, int PASS, bool PIPE>
+__global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
+    extern __shared__ double acc[];   // one fp64 accumulator per row of the block
+    __shared__ double wred[BS / kWave];
+
+    const RowBlock b = a.blocks[blockIdx.x];
+    const int tid = threadIdx.x;
+    double dsum = 0.0;
+    for (int k = 0; k < a.nranks; k++) dsum += a.x_in[(int64_t)k * a.chunk + a.chunk - 1];
+    const double teleport = a.teleport0 + a.damping_over_n * dsum;
+    if (PASS != 2 && a.zero_slot && blockIdx.x == 0 && tid == 0) a.x_out[a.chunk - 1] = 0.0;
+
+    if (b.split < 0) {
+        // ---------------- block of rows, entries in column order ----------------
+        const int nrows = b.row_end - b.row_begin;
+        for (int i = tid; i < nrows; i += BS) acc[i] = PASS == 2 ? a.ypart[b.row_begin + i] : 0.0;
+        __syncthreads();
+        const int64_t z0 = b.nz_begin, z1 = b.nz_end;
+        const int64_t lo = PASS == 2 ? a.split[blockIdx.x] : z0;
+        const int64_t hi = PASS == 1 ? a.split[blockIdx.x] : z1;
+        if (lo < hi) {
+            const int64_t glast = (z1 - 1 - z0) >> 6;
+            const int64_t start = z0 + ((lo - z0) & ~(int64_t)(kWave - 1));   // 64-entry group aligned
+            const int lane = tid & (kWave - 1);
+            uint32_t pk[U], gb[U];
+            auto load_round = [&](int64_t k0) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int64_t e = k0 + (int64_t)u * BS;
+                    pk[u] = __builtin_nontemporal_load(a.spk + min(e, z1 - 1));
+                    // the group of the wave's first lane: the same for all 64 lanes
+                    const int g = (int)min((e - lane - z0) >> 6, glast);
+                    gb[u] = a.gbase[b.seg + __builtin_amdgcn_readfirstlane(g)];
+                }
+            };
+            int64_t k0 = start + tid;
+            if (PIPE) load_round(k0);
+            for (; k0 < hi; k0 += (int64_t)U * BS) {
+                if (!PIPE) load_round(k0);
+                int32_t c[U];
+                uint32_t r[U];
+                uint32_t esc = 0;
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    r[u] = pk[u] & 0xfffu;
+                    c[u] = (int32_t)(gb[u] + (pk[u] >> 12));
+                    esc |= gb[u];
+                }
+                if (esc & 0x80000000u) {   // wave-uniform: an escape group in this round
+#pragma unroll
+                    for (int u = 0; u < U; u++)
+                        if (gb[u] & 0x80000000u) c[u] = a.sci[min(k0 + (int64_t)u * BS, z1 - 1)];
+                }
+                double g[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
+                if (PIPE) load_round(k0 + (int64_t)U * BS);
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int64_t e = k0 + (int64_t)u * BS;
+                    if (e >= lo && e < hi) atomicAdd(&acc[r[u]], g[u]);
+                }
+            }
+        }
+        __syncthreads();
+        if (PASS == 1) {
+            for (int i = tid; i < nrows; i += BS) a.ypart[b.row_begin + i] = acc[i];
+        } else {
+            for (int i = tid; i < nrows; i += BS) sorted_epilogue(a, b.row_begin + i, acc[i], teleport);
+        }
+        return;
+    }
+    if (PASS == 2) return;   // LONG rows are complete after the hub pass
+
+    // ---------------- LONG: one segment of one long row (row order) ----------------
+    const int64_t zb = b.nz_begin, ze = b.nz_end;
+    double s0 = 0.0, s1 = 0.0;
+    for (int64_t k0 = zb + tid; k0 < ze; k0 += (int64_t)U * BS) {
+        int32_t c[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) c[u] = __builtin_nontemporal_load(a.ci + min(k0 + (int64_t)u * BS, ze - 1));
+        double g[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (k0 + (int64_t)u * BS < ze) ((u & 1) ? s1 : s0) += g[u];
+    }
+    const double s = wave_sum(s0 + s1);
+    if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = s;
+    __syncthreads();
+    if (tid != 0) return;
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < BS / kWave; w++) tot += wred[w];
+    const int32_t sp = b.split;
+    const int32_t nseg = a.long_nseg[sp];
+    if (nseg == 1) {
+        sorted_epilogue(a, b.row_begin, tot, teleport);
+        return;
+    }
+    const int32_t first = a.long_first[sp];
+    // publish the partial (agent scope), then take a ticket; the last arriver combines
+    __hip_atomic_store(&a.long_part[first + b.seg], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(&a.long_ticket[sp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t != (uint32_t)(nseg - 1)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double all = 0.0;
+    for (int j = 0; j < nseg; j++)
+        all += __hip_atomic_load(&a.long_part[first + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.long_ticket[sp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sorted_epilogue(a, b.row_begin, all, teleport);
+}
+
+// keys[coff + t] = (block << 32) | column, vals = block-relative row, for the t-th entry of
+// sorted block `blockIdx.x` (one workgroup per block, a wave per row).
+__global__ __launch_bounds__(256) void k_sorted_keys(const RowBlock *__restrict__ blocks, const int64_t *__restrict__ coff,
+                                                     const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                     uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    const RowBlock b = blocks[blockIdx.x];
+    const int64_t base = coff[blockIdx.x] - b.nz_begin;
+    const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    for (int32_t i = wave; i < b.row_end - b.row_begin; i += 256 / kWave) {
+        const int32_t row = b.row_begin + i;
+        for (int64_t e = rp[row] + lane; e < rp[row + 1]; e += kWave) {
+            keys[base + e] = ((uint64_t)blockIdx.x << 32) | (uint32_t)ci[e];
+            vals[base + e] = (uint32_t)i;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sorted_unpack(const RowBlock *__restrict__ blocks, const int64_t *__restrict__ coff,
+                                                       const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                       int32_t *__restrict__ sci, uint16_t *__restrict__ srl) {
+    const RowBlock b = blocks[blockIdx.x];
+    const int64_t c0 = coff[blockIdx.x];
+    for (int64_t t = threadIdx.x; t < b.nz_end - b.nz_begin; t += 256) {
+        sci[b.nz_begin + t] = (int32_t)(uint32_t)keys[c0 + t];
+        srl[b.nz_begin + t] = (uint16_t)vals[c0 + t];
+    }
+}
+
+// spk / gbase from the sorted sci / srl: one workgroup per sorted block, 64-entry groups
+// aligned to the block's first entry (the kernel's wave-instructions).
+__global__ __launch_bounds__(256) void k_sorted_pack(const RowBlock *__restrict__ blocks, const int32_t *__restrict__ sci,
+                                                     const uint16_t *__restrict__ srl, uint32_t *__restrict__ spk,
+                                                     uint32_t *__restrict__ gbase) {
+    const RowBlock b = blocks[blockIdx.x];
+    const int64_t z0 = b.nz_begin, z1 = b.nz_end;
+    for (int64_t e = z0 + threadIdx.x; e < z1; e += 256) {
+        const int64_t g = (e - z0) >> 6;
+        const int64_t first = z0 + (g << 6), last = min(first + 63, z1 - 1);
+        const uint32_t base = (uint32_t)sci[first];
+        const bool esc = (uint32_t)sci[last] - base >= (1u << 20);
+        spk[e] = esc ? (uint32_t)srl[e] : (((uint32_t)sci[e] - base) << 12) | (uint32_t)srl[e];
+        if (e == first) gbase[b.seg + g] = esc ? (base | 0x80000000u) : base;
+    }
+}
+
+// split[i] = first entry of sorted block i whose column is >= hot (LONG blocks: nz_begin).
+__global__ void k_sorted_split(const RowBlock *__restrict__ blocks, uint32_t nblocks, const int32_t *__restrict__ sci,
+                               int64_t hot, int64_t *__restrict__ split) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nblocks; i += gridDim.x * blockDim.x) {
+        const RowBlock b = blocks[i];
+        int64_t lo = b.nz_begin, hi = b.nz_end;
+        if (b.split < 0) {
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if ((int64_t)sci[mid] < hot) lo = mid + 1;
+                else hi = mid;
+            }
+        }
+        split[i] = lo;
+    }
+}
+
+int env_int(const char *name, int dflt, int lo, int hi) {
+    if (const char *e = std::getenv(name)) {
+        const int v = std::atoi(e);
+        if (v >= lo && v <= hi) return v;
+    }
+    return dflt;
+}
+
+template <int BS, int U, bool PIPE>
+void launch_sorted(const PrPart *p, const SortedArgs &a, hipStream_t s) {
+    const size_t lds = (size_t)p->sorted_lds;
+    if (!p->two_pass) {
+        hipLaunchKernelGGL((k_pr_pull_sorted<BS, U, 0, PIPE>), dim3(p->nblocks), dim3(BS), lds, s, a);
+        return;
+    }
+    hipLaunchKernelGGL((k_pr_pull_sorted<BS, U, 1, PIPE>), dim3(p->nblocks), dim3(BS), lds, s, a);
+    const uint32_t ns = p->nblocks - p->nlong_blocks;
+    if (ns) {
+        SortedArgs t = a;
+        t.blocks += p->nlong_blocks;
+        t.split += p->nlong_blocks;
+        hipLaunchKernelGGL((k_pr_pull_sorted<BS, U, 2, PIPE>), dim3(ns), dim3(BS), lds, s, t);
+    }
+}
+
+}  // namespace
+
+// Plan: rows longer than long_nnz -> LONG segment blocks (longest first); runs of the other
+// rows -> blocks of <= sorted_nnz entries and <= sorted_rows rows, entries sorted by column.
+int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp) {
+    const int64_t rows = (int64_t)h_rp.size() - 1;
+    const uint64_t nnz = (uint64_t)h_rp[rows];
+    // entries per block: GX_PR_SORTED_NNZ, else the largest power of two <= 65536 that still
+    // gives every CU a block (the partitions of many ranks or pieces are small)
+    int64_t B = p->sorted_nnz;
+    if (std::getenv("GX_PR_SORTED_NNZ")) {
+        B = env_int("GX_PR_SORTED_NNZ", p->sorted_nnz, 1024, 1 << 20);
+    } else {
+        const int64_t cus = std::max(1, p->ctx->num_cus);
+        while (B > 4096 && (int64_t)nnz < B * cus) B >>= 1;
+    }
+    p->sorted_nnz = (int)B;
+    p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)B, 1024, 1 << 24);
+    p->sorted_rows = env_int("GX_PR_SORTED_ROWS", p->sorted_rows, 64, 4096);   // 12-bit rows, LDS <= 32 KiB
+    // GX_PR_SORTED_VARIANT = 0 (1024 threads, 8 gathers in flight per lane, entry loads
+    // pipelined) | 1 (1024, 8, not pipelined) | 2 (512, 16, pipelined) | 3 (512, 8, pipelined)
+    p->sorted_variant = env_int("GX_PR_SORTED_VARIANT", 0, 0, 3);
+    // hub slice of x for the two-pass mode (GX_PR_HOT_COLS = 0: one pass).  One rank only:
+    // in a multi-rank exchange layout the hub columns are spread over every rank's chunk.
+    p->hot_cols = env_int("GX_PR_HOT_COLS", (int)p->hot_cols, 0, 1 << 30);
+    p->two_pass = p->hot_cols > 0 && p->nranks == 1 && (int64_t)p->chunk > p->hot_cols;
+    const int64_t R = p->sorted_rows, LT = std::max<int64_t>(p->long_nnz, 1);
+    std::vector<RowBlock> longb, sortb;
+    std::vector<int32_t> lfirst, lnseg;
+    std::vector<std::pair<int64_t, int32_t>> longrows;
+    int32_t nsegs = 0;
+    int64_t r = 0;
+    while (r < rows) {
+        const int64_t len = h_rp[r + 1] - h_rp[r];
+        if (len > LT) {
+            longrows.push_back({len, (int32_t)r});
+            r++;
+            continue;
+        }
+        const int64_t start = r;
+        int64_t nz = 0;
+        while (r < rows && r - start < R) {
+            const int64_t l = h_rp[r + 1] - h_rp[r];
+            if (l > LT || nz + l > B) break;
+            nz += l;
+            r++;
+        }
+        sortb.push_back({h_rp[start], h_rp[r], (int32_t)start, (int32_t)r, -1, 0});
+    }
+    // seg of a sorted block = index of its first 64-entry group in gbase
+    int64_t ngroups = 0;
+    for (RowBlock &b : sortb) {
+        b.seg = (int32_t)ngroups;
+        ngroups += (b.nz_end - b.nz_begin + 63) / 64;
+    }
+    std::stable_sort(longrows.begin(), longrows.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
+    for (const auto &lr : longrows) {
+        const int32_t row = lr.second;
+        const int32_t nseg = (int32_t)((lr.first + kSegNnz - 1) / kSegNnz);
+        const int32_t sp = (int32_t)lfirst.size();
+        lfirst.push_back(nsegs);
+        lnseg.push_back(nseg);
+        for (int32_t s = 0; s < nseg; s++) {
+            const int64_t zb = h_rp[row] + (int64_t)s * kSegNnz;
+            longb.push_back({zb, std::min(zb + kSegNnz, h_rp[row + 1]), row, row + 1, sp, s});
+        }
+        nsegs += nseg;
+    }
+    int64_t maxrows = 1;
+    for (const RowBlock &b : sortb) maxrows = std::max<int64_t>(maxrows, b.row_end - b.row_begin);
+    p->sorted_lds = (int)(maxrows * sizeof(double));
+    std::vector<RowBlock> all(longb);
+    all.insert(all.end(), sortb.begin(), sortb.end());
+    p->nblocks = (uint32_t)all.size();
+    p->nlong_blocks = (uint32_t)longb.size();
+    p->nlong = (uint32_t)lfirst.size();
+    p->nsegs = (uint32_t)nsegs;
+    GX_TRY(p->blocks.alloc(std::max<size_t>(all.size(), 1)));
+    GX_TRY(p->long_first.alloc(std::max<size_t>(lfirst.size(), 1)));
+    GX_TRY(p->long_nseg.alloc(std::max<size_t>(lnseg.size(), 1)));
+    GX_TRY(p->long_part.alloc(std::max<size_t>(nsegs, 1)));
+    GX_TRY(p->long_ticket.alloc(std::max<size_t>(lfirst.size(), 1)));
+    if (!all.empty())
+        GX_HIP_TRY(hipMemcpy(p->blocks.p, all.data(), all.size() * sizeof(RowBlock), hipMemcpyHostToDevice));
+    if (!lfirst.empty()) {
+        GX_HIP_TRY(hipMemcpy(p->long_first.p, lfirst.data(), lfirst.size() * 4, hipMemcpyHostToDevice));
+        GX_HIP_TRY(hipMemcpy(p->long_nseg.p, lnseg.data(), lnseg.size() * 4, hipMemcpyHostToDevice));
+    }
+    GX_HIP_TRY(hipMemset(p->long_ticket.p, 0, p->long_ticket.n * 4));
+    GX_TRY(p->ssplit.alloc(std::max<size_t>(all.size(), 1)));
+    if (p->two_pass) GX_TRY(p->ypart.alloc(std::max<int64_t>(rows, 1)));
+
+    // block-sorted columns and packed entries (entries of LONG rows stay unused there)
+    GX_TRY(p->sci.alloc(std::max<uint64_t>(nnz, 1), 16));
+    GX_TRY(p->spk.alloc(std::max<uint64_t>(nnz, 1), 16));
+    GX_TRY(p->gbase.alloc(std::max<int64_t>(ngroups, 1)));
+    hipStream_t s = p->ctx->stream;
+    std::vector<int64_t> coff(sortb.size());
+    int64_t m = 0;
+    for (size_t j = 0; j < sortb.size(); j++) {
+        coff[j] = m;
+        m += sortb[j].nz_end - sortb[j].nz_begin;
+    }
+    const RowBlock *d_sort = p->blocks.p + longb.size();
+    if (m > 0) {
+        DBuf<int64_t> d_coff;
+        DBuf<uint64_t> k0, k1;
+        DBuf<uint32_t> v0, v1;
+        DBuf<uint16_t> srl;
+        GX_TRY(d_coff.alloc(coff.size()));
+        GX_TRY(k0.alloc(m));
+        GX_TRY(k1.alloc(m));
+        GX_TRY(v0.alloc(m));
+        GX_TRY(v1.alloc(m));
+        GX_TRY(srl.alloc(std::max<uint64_t>(nnz, 1), 16));
+        GX_HIP_TRY(hipMemcpy(d_coff.p, coff.data(), coff.size() * 8, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_sorted_keys, dim3((unsigned)sortb.size()), dim3(256), 0, s, d_sort, d_coff.p, p->rp, p->ci,
+                           k0.p, v0.p);
+        GX_TRY(check_launch("k_sorted_keys"));
+        int bits = 1;
+        while ((1ull << bits) < sortb.size()) bits++;
+        GX_TRY(sort_pairs_u64_u32(k0.p, k1.p, v0.p, v1.p, (size_t)m, 32 + bits, s));
+        hipLaunchKernelGGL(k_sorted_unpack, dim3((unsigned)sortb.size()), dim3(256), 0, s, d_sort, d_coff.p, k1.p, v1.p,
+                           p->sci.p, srl.p);
+        GX_TRY(check_launch("k_sorted_unpack"));
+        hipLaunchKernelGGL(k_sorted_pack, dim3((unsigned)sortb.size()), dim3(256), 0, s, d_sort, p->sci.p, srl.p,
+                           p->spk.p, p->gbase.p);
+        GX_TRY(check_launch("k_sorted_pack"));
+        GX_HIP_TRY(hipStreamSynchronize(s));   // the key buffers are freed at return
+    }
+    if (!all.empty()) {
+        hipLaunchKernelGGL(k_sorted_split, dim3(grid_for(all.size(), 256, 1024)), dim3(256), 0, s, p->blocks.p,
+                           (uint32_t)all.size(), p->sci.p, (int64_t)p->hot_cols, p->ssplit.p);
+        GX_TRY(check_launch("k_sorted_split"));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+    }
+    return GX_SUCCESS;
+}
+
+int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s) {
+    const double dn = (double)p->n_global;
+    SortedArgs a;
+    a.blocks = p->blocks.p;
+    a.split = p->ssplit.p;
+    a.ci = p->ci;
+    a.sci = p->sci.p;
+    a.spk = p->spk.p;
+    a.gbase = p->gbase.p;
+    a.outdeg = p->outdeg;
+    a.x_in = x_full;
+    a.x_out = x_local;
+    a.rank_out = rank_out;
+    a.ypart = p->ypart.p;
+    a.chunk = (int64_t)p->chunk;
+    a.nranks = p->nranks;
+    a.zero_slot = p->nd == 0 ? 1 : 0;
+    a.teleport0 = (1.0 - p->damping) / dn;
+    a.damping_over_n = p->damping / dn;
+    a.damping = p->damping;
+    a.long_first = p->long_first.p;
+    a.long_nseg = p->long_nseg.p;
+    a.long_part = p->long_part.p;
+    a.long_ticket = p->long_ticket.p;
+    if (p->nblocks) {
+        KTimer kt(p->ctx, "pr_pull", s);   // both passes: one iteration's SpMV
+        switch (p->sorted_variant) {
+        case 1: launch_sorted<1024, 8, false>(p, a, s); break;
+        case 2: launch_sorted<512, 16, true>(p, a, s); break;
+        case 3: launch_sorted<512, 8, true>(p, a, s); break;
+        default: launch_sorted<1024, 8, true>(p, a, s); break;
+        }
+    } else if (a.zero_slot) {
+        GX_HIP_TRY(hipMemsetAsync(x_local + p->chunk - 1, 0, sizeof(double), s));
+    }
+    GX_TRY(check_launch("k_pr_pull_sorted"));
+    return pr_dangling(p, x_local, s);
+}
+
+}  // namespace gx

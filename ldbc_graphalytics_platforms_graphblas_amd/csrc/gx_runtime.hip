@@ -422,6 +422,18 @@ int key_bits(uint64_t n) {
 
 namespace gx {
 
+int sort_pairs_u64_u32(uint64_t *k_in, uint64_t *k_out, uint32_t *v_in, uint32_t *v_out, size_t m, int end_bit,
+                       hipStream_t s) {
+    if (!m) return GX_SUCCESS;
+    size_t tmp_bytes = 0;
+    GX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
+    DBuf<char> tmp;
+    GX_TRY(tmp.alloc(tmp_bytes));
+    GX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+    return GX_SUCCESS;
+}
+
 int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,
                      int32_t *ci, hipStream_t s) {
     if (m) {

@@ -176,3 +176,44 @@ def test_dense_tiers(ctx):
         g = _G(csr, directed)
         np.testing.assert_array_equal(gpu_run(ctx, g, "LCC"), O.lcc(csr, directed))
         np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=4), O.cdlp(csr, directed, 4))
+
+
+def test_pagerank_long_row_segments(ctx):
+    """A hub row of 150 000 entries, longer than a column-sorted block: LONG segments
+    combined by the last arriver, beside sorted blocks of random edges."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    n = 150001
+    rng = np.random.default_rng(3)
+    a, b = rng.integers(1, n, 200000), rng.integers(1, n, 200000)
+    keep = a != b
+    src = np.concatenate([np.zeros(n - 1, np.int64), a[keep]])
+    dst = np.concatenate([np.arange(1, n, dtype=np.int64), b[keep]])
+    csr = csr_from_edges(n, src, dst, None, symmetric=True)
+    np.testing.assert_allclose(gpu_run(ctx, _G(csr, False), "PR", damping=0.85, iters=6),
+                               O.pagerank(csr, False, 0.85, 6), rtol=PR_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("env", [{"GX_PR_HOT_COLS": "0"}, {"GX_PR_HOT_COLS": "1024"},
+                                 {"GX_PR_HOT_COLS": "1024", "GX_PR_SORTED_ROWS": "64"},
+                                 {"GX_PR_SORTED_VARIANT": "1"}, {"GX_PR_SORTED_VARIANT": "2"},
+                                 {"GX_PR_KERNEL": "adaptive"}])
+def test_pagerank_plan_variants(ctx, monkeypatch, env):
+    """One pass, two passes around a small hub slice, tiny blocks, the other block shapes and
+    the CSR-Adaptive kernel all give the oracle's scores (directed and undirected)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for g in (_rmat(14, 16, 4), _rmat(11, 8, 3, undirected=False)):
+        np.testing.assert_allclose(gpu_run(ctx, g, "PR", damping=0.85, iters=10),
+                                   O.pagerank(g.csr, g.directed, 0.85, 10), rtol=PR_RTOL, atol=0)
+
+
+def test_pagerank_escape_groups(ctx, monkeypatch):
+    """A perfect matching on 2^21 + 64 vertices in 64-row blocks: the 64 columns of a group
+    span more than 2^20 ids, so the groups escape to plain column ids; two passes."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    monkeypatch.setenv("GX_PR_SORTED_ROWS", "64")
+    n = (1 << 21) + 64
+    perm = np.random.default_rng(9).permutation(n)
+    csr = csr_from_edges(n, perm[0::2], perm[1::2], None, symmetric=True)
+    np.testing.assert_allclose(gpu_run(ctx, _G(csr, False), "PR", damping=0.85, iters=4),
+                               O.pagerank(csr, False, 0.85, 4), rtol=PR_RTOL, atol=0)
