@@ -399,7 +399,7 @@ def main():
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
     from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import Comm, DevicePageRank, GpuStep, \
-        PartitionedPageRank, hub_relabel, local_pieces, local_rows
+        PartitionedPageRank, hub_relabel, interleaved_relabel, partition_rows, slice_rows
 
     gname = args.graph or "SYN-7_5"
     workload = f"PageRank {gname} (R-MAT scale {args.scale}, ef {args.edgefactor}, seed {args.seed}, undirected)"
@@ -407,12 +407,21 @@ def main():
     csr = rmat(args.scale, args.edgefactor, args.seed, undirected=True)
     t_gen = time.time() - t_gen
     n, nnz = csr.n, csr.nnz
-    perm, hub = hub_relabel(csr)   # hub-first layout (what gx_pagerank does internally)
-    # N > 1: each rank's rows are cut into `pieces` virtual ranks whose all-gathers overlap
-    # the next piece's SpMV (pr_partition.local_pieces)
-    pieces = max(1, int(os.environ.get("GX_PR_PIECES", "2" if world > 1 else "1"))) if dist else 1
-    lrs = local_pieces(hub, False, world, rank, pieces) if pieces > 1 else \
-        [local_rows(hub, directed=False, nranks=world, rank=rank)]
+    # GX_PR_PIECES = P > 1: each rank owns P virtual ranks p * N + rank whose all-gathers overlap
+    # the next piece's SpMV (default 1: at N = 1 a 1/16 piece ran its SpMV at 0.48x the rate of
+    # a 1/8 one -- tools/pr_dist_n1.sh -- more than the overlap wins back).  Layout: the hub-first order (what gx_pagerank does internally) dealt
+    # round-robin over the N * pieces virtual ranks, so each owns n / (N * pieces) rows AND
+    # ~nnz / (N * pieces) entries and the exchanged vector is ~n long (interleaved_relabel);
+    # GX_PR_PARTITION=ranges keeps the round-1 contiguous hub-first ranges balanced by entries.
+    pieces = max(1, int(os.environ.get("GX_PR_PIECES", "1"))) if dist else 1
+    vranks = world * pieces
+    partition = os.environ.get("GX_PR_PARTITION", "interleave")
+    if partition == "ranges":
+        perm, hub = hub_relabel(csr)
+        bounds = partition_rows(hub.rowptr, vranks)
+    else:
+        perm, hub, bounds = interleaved_relabel(csr, vranks)
+    lrs = [slice_rows(hub, bounds, p * world + rank) for p in range(pieces)]
 
     ctx = Context(local_rank)
     dev_name, cus = ctx.info()
@@ -548,6 +557,8 @@ def main():
                 "iterations": args.iters,
                 "damping": args.damping,
                 "parallelism": f"row{world}" + (f", {pieces} pipelined pieces" if pieces > 1 else ""),
+                "partition": (partition + " over " + str(vranks) + " virtual ranks") if vranks > 1 else "one rank",
+                "exchanged_doubles_per_n": steppers[0].chunk * vranks / n,
                 "driver": driver + (", hipGraph" if driver == "device" and use_graph else ""),
                 "roofline_events": "timed steps" if events_in_timed else "instrumented pass after the timed steps",
                 "device": dev_name,

@@ -90,7 +90,7 @@ struct PrPart {
     int sorted_variant = 0;      // tuning: block size / gathers in flight (gx_pr_sorted.hip)
     DBuf<int64_t> ssplit;        // per block: first sorted entry in the tail pass
     DBuf<double> ypart;          // hub-pass row sums
-    int64_t hot_cols = 262144;   // columns of the hub pass (2 MiB of x)
+    int64_t hot_cols = 0;        // columns of the hub pass (0: one pass; GX_PR_HOT_COLS)
     bool two_pass = false;
     // hub-cached kernel: wave items, LDS hub prefix, fused dangling reduction
     int kernel = 2;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive), 2 = k_pr_pull_sorted

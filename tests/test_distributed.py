@@ -17,9 +17,9 @@ import torch.multiprocessing as mp
 
 from conftest import ROOT  # noqa: F401  (sys.path)
 from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
-from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import (PartitionedPageRank, hub_relabel, local_pieces,
-                                                                    local_rows,
-                                                                    partition_rows)
+from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import (PartitionedPageRank, hub_relabel,
+                                                                    interleaved_relabel, local_pieces, local_rows,
+                                                                    partition_rows, slice_rows)
 from oracle import oracle as O
 
 
@@ -69,13 +69,21 @@ def _gloo_gather_async(out, inp):
     return dist.all_gather(list(out.chunk(dist.get_world_size())), inp, async_op=True)
 
 
-def _worker(rank, world, port, q, pieces=1):
+def _worker(rank, world, port, q, pieces=1, layout="ranges"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         csr = rmat(11, 8, 5)
         perm, hub = hub_relabel(csr)
-        if pieces == 1:
+        if layout == "interleave":   # bench.py's default layout
+            perm, hub, bounds = interleaved_relabel(csr, world * pieces)
+            lrs = [slice_rows(hub, bounds, p * world + rank) for p in range(pieces)]
+            pr = PartitionedPageRank([CpuStep(csr.n, world * pieces, lr, 0.85) for lr in lrs], world,
+                                     [lr.rows for lr in lrs], "cpu", all_gather=_gloo_gather_async)
+            out = pr.run(7)
+            out = out if pieces > 1 else [out]
+            mine = [(lr.rank, o.numpy().copy()) for lr, o in zip(lrs, out)]
+        elif pieces == 1:
             lr = local_rows(hub, directed=False, nranks=world, rank=rank)
             pr = PartitionedPageRank(CpuStep(csr.n, world, lr, 0.85), world, lr.rows, "cpu", all_gather=_gloo_gather)
             mine = [(rank, pr.run(7).numpy().copy())]
@@ -110,6 +118,27 @@ def test_partition_rows_balanced():
         assert loads.max() <= csr.nnz / k + np.diff(rp).max() + 1
 
 
+def test_interleaved_relabel_balances_rows_and_entries():
+    """Dealing the hub-first order round-robin: equal row counts (+-1), entries within the
+    largest degree of each other, ~n exchanged doubles, and the same PageRank."""
+    csr = rmat(12, 16, 9)
+    maxdeg = int(np.diff(csr.rowptr.astype(np.int64)).max())
+    for k in (1, 2, 3, 8, 16):
+        perm, g, b = interleaved_relabel(csr, k)
+        b = b.astype(np.int64)
+        assert b[0] == 0 and b[-1] == csr.n
+        rows = np.diff(b)
+        assert rows.max() - rows.min() <= 1
+        rp = g.rowptr.astype(np.int64)
+        loads = rp[b[1:]] - rp[b[:-1]]
+        assert loads.sum() == csr.nnz and loads.max() - loads.min() <= maxdeg
+        np.testing.assert_allclose(O.pagerank(csr, False, 0.85, 5), O.pagerank(g, False, 0.85, 5)[perm], rtol=1e-12)
+    # the contiguous ranges of the hub-first order pad the exchange far beyond n
+    _, hub = hub_relabel(csr)
+    ranges = np.diff(partition_rows(hub.rowptr, 8).astype(np.int64))
+    assert 8 * (ranges.max() + 1) > 3 * csr.n
+
+
 def test_hub_relabel_is_isomorphic():
     csr = rmat(10, 8, 2)
     perm, hub = hub_relabel(csr)
@@ -126,12 +155,12 @@ def test_hub_relabel_is_isomorphic():
     np.testing.assert_allclose(a, b, rtol=1e-12)
 
 
-@pytest.mark.parametrize("pieces", [1, 2])
-def test_gloo_world2_matches_oracle(pieces):
+@pytest.mark.parametrize("pieces,layout", [(1, "ranges"), (2, "ranges"), (1, "interleave"), (2, "interleave")])
+def test_gloo_world2_matches_oracle(pieces, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, pieces)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, pieces, layout)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
@@ -189,9 +218,9 @@ def test_gpu_device_driven_pagerank(pieces, use_graph, with_comm):
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
     from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import Comm, DevicePageRank, GpuStep
     csr = rmat(13, 16, 11)
-    perm, hub = hub_relabel(csr)
+    perm, hub, bounds = interleaved_relabel(csr, pieces)
     ctx = Context(0)
-    lrs = local_pieces(hub, False, 1, 0, pieces)
+    lrs = [slice_rows(hub, bounds, p) for p in range(pieces)]
     steps = [GpuStep(ctx, csr.n, pieces, lr, 0.85) for lr in lrs]
     comm = Comm(ctx, 1, 0, lambda uid: uid) if with_comm else None
     dpr = DevicePageRank(steps, comm, use_graph=use_graph)
