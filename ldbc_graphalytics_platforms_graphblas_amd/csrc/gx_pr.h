@@ -92,6 +92,9 @@ struct PrPart {
     DBuf<double> ypart;          // hub-pass row sums
     int64_t hot_cols = 0;        // columns of the hub pass (0: one pass; GX_PR_HOT_COLS)
     bool two_pass = false;
+    int slices = 1;              // XCD column slices (k_pr_pull_sliced; GX_PR_SLICES)
+    DBuf<int64_t> sbound;        // per sorted block: slice boundaries
+    uint32_t nsorted = 0, nlong_pad = 0;
     // hub-cached kernel: wave items, LDS hub prefix, fused dangling reduction
     int kernel = 2;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive), 2 = k_pr_pull_sorted
     bool int4_loads = false;     // k_pr_pull: 16-B index loads (lane stride 4) instead of lane-consecutive

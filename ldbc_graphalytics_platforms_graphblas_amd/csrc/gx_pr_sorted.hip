@@ -61,6 +61,10 @@ struct SortedArgs {
     const int32_t *long_nseg;
     double *long_part;
     uint32_t *long_ticket;
+    // XCD slices (k_pr_pull_sliced)
+    const int64_t *sbound;   // per sorted block: slices + 1 entry boundaries
+    int64_t rows;            // local rows (ypart holds `slices` arrays of them)
+    uint32_t nlong, nlong_pad, nsorted;
 };
 
 __device__ __forceinline__ void sorted_epilogue(const SortedArgs &a, int32_t row, double s, double teleport) {
@@ -68,6 +72,118 @@ __device__ __forceinline__ void sorted_epilogue(const SortedArgs &a, int32_t row
     if (a.rank_out) a.rank_out[row] = r;
     const int32_t deg = a.outdeg[row];
     a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+}
+
+// A long row's sum: the epilogue, or (sliced mode) slot 0 of the row's slice partials, the
+// other slices zero.
+__device__ __forceinline__ void long_finish(const SortedArgs &a, int32_t row, double s, double teleport, double *yout,
+                                            int slices, int64_t rows) {
+    if (!yout) {
+        sorted_epilogue(a, row, s, teleport);
+        return;
+    }
+    yout[row] = s;
+    for (int j = 1; j < slices; j++) yout[(int64_t)j * rows + row] = 0.0;
+}
+
+// LONG: one segment of one long row (row order), a whole workgroup; segments of one row are
+// combined by the last arriver (agent-scope release/acquire ticket).
+template <int BS, int U>
+__device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock &b, double *wred, double teleport,
+                                             double *yout, int slices, int64_t rows) {
+    const int tid = threadIdx.x;
+    const int64_t zb = b.nz_begin, ze = b.nz_end;
+    double s0 = 0.0, s1 = 0.0;
+    for (int64_t k0 = zb + tid; k0 < ze; k0 += (int64_t)U * BS) {
+        int32_t c[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) c[u] = __builtin_nontemporal_load(a.ci + min(k0 + (int64_t)u * BS, ze - 1));
+        double g[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (k0 + (int64_t)u * BS < ze) ((u & 1) ? s1 : s0) += g[u];
+    }
+    const double s = wave_sum(s0 + s1);
+    if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = s;
+    __syncthreads();
+    if (tid != 0) return;
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < BS / kWave; w++) tot += wred[w];
+    const int32_t sp = b.split;
+    const int32_t nseg = a.long_nseg[sp];
+    if (nseg == 1) {
+        long_finish(a, b.row_begin, tot, teleport, yout, slices, rows);
+        return;
+    }
+    const int32_t first = a.long_first[sp];
+    // publish the partial (agent scope), then take a ticket; the last arriver combines
+    __hip_atomic_store(&a.long_part[first + b.seg], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(&a.long_ticket[sp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t != (uint32_t)(nseg - 1)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double all = 0.0;
+    for (int j = 0; j < nseg; j++)
+        all += __hip_atomic_load(&a.long_part[first + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.long_ticket[sp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long_finish(a, b.row_begin, all, teleport, yout, slices, rows);
+}
+
+// Adds x(column) of the sorted entries [lo, hi) of block b into the LDS row accumulators
+// (the loop starts at the 64-entry group holding lo, so wave-instructions stay group-aligned).
+template <int BS, int U, bool PIPE>
+__device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock &b, int64_t lo, int64_t hi,
+                                             double *acc) {
+    const int tid = threadIdx.x;
+    const int64_t z0 = b.nz_begin, z1 = b.nz_end;
+    if (lo < hi) {
+        const int64_t glast = (z1 - 1 - z0) >> 6;
+        const int64_t start = z0 + ((lo - z0) & ~(int64_t)(kWave - 1));   // 64-entry group aligned
+        const int lane = tid & (kWave - 1);
+        uint32_t pk[U], gb[U];
+        auto load_round = [&](int64_t k0) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t e = k0 + (int64_t)u * BS;
+                pk[u] = __builtin_nontemporal_load(a.spk + min(e, z1 - 1));
+                // the group of the wave's first lane: the same for all 64 lanes
+                const int g = (int)min((e - lane - z0) >> 6, glast);
+                gb[u] = a.gbase[b.seg + __builtin_amdgcn_readfirstlane(g)];
+            }
+        };
+        int64_t k0 = start + tid;
+        if (PIPE) load_round(k0);
+        for (; k0 < hi; k0 += (int64_t)U * BS) {
+            if (!PIPE) load_round(k0);
+            int32_t c[U];
+            uint32_t r[U];
+            uint32_t esc = 0;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                r[u] = pk[u] & 0xfffu;
+                c[u] = (int32_t)(gb[u] + (pk[u] >> 12));
+                esc |= gb[u];
+            }
+            if (esc & 0x80000000u) {   // wave-uniform: an escape group in this round
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (gb[u] & 0x80000000u) c[u] = a.sci[min(k0 + (int64_t)u * BS, z1 - 1)];
+            }
+            double g[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
+            if (PIPE) load_round(k0 + (int64_t)U * BS);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t e = k0 + (int64_t)u * BS;
+                if (e >= lo && e < hi) atomicAdd(&acc[r[u]], g[u]);
+            }
+        }
+    }
 }
 
 // BS threads, U gathers in flight per lane.
@@ -97,50 +213,7 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
         const int64_t z0 = b.nz_begin, z1 = b.nz_end;
         const int64_t lo = PASS == 2 ? a.split[blockIdx.x] : z0;
         const int64_t hi = PASS == 1 ? a.split[blockIdx.x] : z1;
-        if (lo < hi) {
-            const int64_t glast = (z1 - 1 - z0) >> 6;
-            const int64_t start = z0 + ((lo - z0) & ~(int64_t)(kWave - 1));   // 64-entry group aligned
-            const int lane = tid & (kWave - 1);
-            uint32_t pk[U], gb[U];
-            auto load_round = [&](int64_t k0) {
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int64_t e = k0 + (int64_t)u * BS;
-                    pk[u] = __builtin_nontemporal_load(a.spk + min(e, z1 - 1));
-                    // the group of the wave's first lane: the same for all 64 lanes
-                    const int g = (int)min((e - lane - z0) >> 6, glast);
-                    gb[u] = a.gbase[b.seg + __builtin_amdgcn_readfirstlane(g)];
-                }
-            };
-            int64_t k0 = start + tid;
-            if (PIPE) load_round(k0);
-            for (; k0 < hi; k0 += (int64_t)U * BS) {
-                if (!PIPE) load_round(k0);
-                int32_t c[U];
-                uint32_t r[U];
-                uint32_t esc = 0;
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    r[u] = pk[u] & 0xfffu;
-                    c[u] = (int32_t)(gb[u] + (pk[u] >> 12));
-                    esc |= gb[u];
-                }
-                if (esc & 0x80000000u) {   // wave-uniform: an escape group in this round
-#pragma unroll
-                    for (int u = 0; u < U; u++)
-                        if (gb[u] & 0x80000000u) c[u] = a.sci[min(k0 + (int64_t)u * BS, z1 - 1)];
-                }
-                double g[U];
-#pragma unroll
-                for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
-                if (PIPE) load_round(k0 + (int64_t)U * BS);
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int64_t e = k0 + (int64_t)u * BS;
-                    if (e >= lo && e < hi) atomicAdd(&acc[r[u]], g[u]);
-                }
-            }
-        }
+        gather_range<BS, U, PIPE>(a, b, lo, hi, acc);
         __syncthreads();
         if (PASS == 1) {
             for (int i = tid; i < nrows; i += BS) a.ypart[b.row_begin + i] = acc[i];
@@ -151,46 +224,76 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
     }
     if (PASS == 2) return;   // LONG rows are complete after the hub pass
 
-    // ---------------- LONG: one segment of one long row (row order) ----------------
-    const int64_t zb = b.nz_begin, ze = b.nz_end;
-    double s0 = 0.0, s1 = 0.0;
-    for (int64_t k0 = zb + tid; k0 < ze; k0 += (int64_t)U * BS) {
-        int32_t c[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) c[u] = __builtin_nontemporal_load(a.ci + min(k0 + (int64_t)u * BS, ze - 1));
-        double g[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (k0 + (int64_t)u * BS < ze) ((u & 1) ? s1 : s0) += g[u];
-    }
-    const double s = wave_sum(s0 + s1);
-    if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = s;
-    __syncthreads();
-    if (tid != 0) return;
-    double tot = 0.0;
-#pragma unroll
-    for (int w = 0; w < BS / kWave; w++) tot += wred[w];
-    const int32_t sp = b.split;
-    const int32_t nseg = a.long_nseg[sp];
-    if (nseg == 1) {
-        sorted_epilogue(a, b.row_begin, tot, teleport);
+    long_segment<BS, U>(a, b, wred, teleport, nullptr, 0, 0);
+}
+
+// XCD slices: the columns are cut into S ranges holding equal shares of the entries, and the
+// workgroups of slice j run on the XCDs with (workgroup index % 8) % S == j (blocks are dealt
+// round-robin over the 8 XCDs), so an XCD's L2 only ever holds its slices' part of x instead
+// of all of it.  Workgroup (block, slice) adds the block's entries of that column range into
+// LDS row sums and stores them to ypart[slice][row]; k_pr_sliced_epilogue adds the S partial
+// sums of every row in slice order and runs the epilogue.  LONG rows (the first nlong
+// workgroups, padded to a multiple of 8) write their sum to slice 0 and zeros elsewhere.
+template <int BS, int U, int S, bool PIPE>
+__global__ __launch_bounds__(BS) void k_pr_pull_sliced(SortedArgs a) {
+    extern __shared__ double acc[];
+    __shared__ double wred[BS / kWave];
+    const uint32_t w = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (a.zero_slot && w == 0 && tid == 0) a.x_out[a.chunk - 1] = 0.0;
+    if (w < a.nlong_pad) {
+        if (w >= a.nlong) return;
+        long_segment<BS, U>(a, a.blocks[w], wred, 0.0, a.ypart, S, a.rows);
         return;
     }
-    const int32_t first = a.long_first[sp];
-    // publish the partial (agent scope), then take a ticket; the last arriver combines
-    __hip_atomic_store(&a.long_part[first + b.seg], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t t = __hip_atomic_fetch_add(&a.long_ticket[sp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t != (uint32_t)(nseg - 1)) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    double all = 0.0;
-    for (int j = 0; j < nseg; j++)
-        all += __hip_atomic_load(&a.long_part[first + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.long_ticket[sp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sorted_epilogue(a, b.row_begin, all, teleport);
+    const uint32_t t = w - a.nlong_pad;
+    const int xcd = (int)(t & 7u), j = xcd % S;
+    const int64_t bi = (int64_t)(t >> 3) * (8 / S) + xcd / S;
+    if (bi >= a.nsorted) return;
+    const RowBlock b = a.blocks[a.nlong + bi];
+    const int nrows = b.row_end - b.row_begin;
+    for (int i = tid; i < nrows; i += BS) acc[i] = 0.0;
+    __syncthreads();
+    gather_range<BS, U, PIPE>(a, b, a.sbound[bi * (S + 1) + j], a.sbound[bi * (S + 1) + j + 1], acc);
+    __syncthreads();
+    double *y = a.ypart + (int64_t)j * a.rows + b.row_begin;
+    for (int i = tid; i < nrows; i += BS) y[i] = acc[i];
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void k_pr_sliced_epilogue(SortedArgs a) {
+    double dsum = 0.0;
+    for (int k = 0; k < a.nranks; k++) dsum += a.x_in[(int64_t)k * a.chunk + a.chunk - 1];
+    const double teleport = a.teleport0 + a.damping_over_n * dsum;
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < a.rows; r += (int64_t)gridDim.x * 256) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < S; j++) s += a.ypart[(int64_t)j * a.rows + r];
+        sorted_epilogue(a, (int32_t)r, s, teleport);
+    }
+}
+
+// sbound[i * (S + 1) + j] = first entry of sorted block i whose column is >= cuts[j]
+// (cuts[0] = 0, cuts[S] = every column): the block's entries of column slice j.
+__global__ void k_sorted_bounds(const RowBlock *__restrict__ blocks, uint32_t nsorted, const int32_t *__restrict__ sci,
+                                const int64_t *__restrict__ cuts, int S, int64_t *__restrict__ sbound) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsorted; i += gridDim.x * blockDim.x) {
+        const RowBlock b = blocks[i];
+        for (int j = 0; j <= S; j++) {
+            int64_t lo = b.nz_begin, hi = b.nz_end;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if ((int64_t)sci[mid] < cuts[j]) lo = mid + 1;
+                else hi = mid;
+            }
+            sbound[(int64_t)i * (S + 1) + j] = lo;
+        }
+    }
+}
+
+__global__ void k_col_hist(const int32_t *__restrict__ ci, int64_t nnz, uint32_t *__restrict__ cnt) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&cnt[ci[e]], 1u);
 }
 
 // keys[coff + t] = (block << 32) | column, vals = block-relative row, for the t-th entry of
@@ -280,6 +383,14 @@ void launch_sorted(const PrPart *p, const SortedArgs &a, hipStream_t s) {
     }
 }
 
+template <int BS, int U, int S>
+void launch_sliced(const PrPart *p, const SortedArgs &a, hipStream_t s) {
+    const uint32_t per = 8 / S;   // sorted blocks per group of 8 workgroups and slice
+    const uint32_t grid = p->nlong_pad + (p->nsorted + per - 1) / per * 8;
+    hipLaunchKernelGGL((k_pr_pull_sliced<BS, U, S, true>), dim3(grid), dim3(BS), (size_t)p->sorted_lds, s, a);
+    hipLaunchKernelGGL((k_pr_sliced_epilogue<S>), dim3(grid_for(p->rows, 256, 4096)), dim3(256), 0, s, a);
+}
+
 }  // namespace
 
 // Plan: rows longer than long_nnz -> LONG segment blocks (longest first); runs of the other
@@ -306,6 +417,10 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp) {
     // in a multi-rank exchange layout the hub columns are spread over every rank's chunk.
     p->hot_cols = env_int("GX_PR_HOT_COLS", (int)p->hot_cols, 0, 1 << 30);
     p->two_pass = p->hot_cols > 0 && p->nranks == 1 && (int64_t)p->chunk > p->hot_cols;
+    // XCD column slices (GX_PR_SLICES = 1, 2, 4 or 8; 1 = off); not combined with two passes
+    p->slices = env_int("GX_PR_SLICES", p->slices, 1, 8);
+    if (8 % p->slices) p->slices = 1;
+    if (p->two_pass) p->slices = 1;
     const int64_t R = p->sorted_rows, LT = std::max<int64_t>(p->long_nnz, 1);
     std::vector<RowBlock> longb, sortb;
     std::vector<int32_t> lfirst, lnseg;
@@ -410,6 +525,41 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp) {
         GX_TRY(check_launch("k_sorted_pack"));
         GX_HIP_TRY(hipStreamSynchronize(s));   // the key buffers are freed at return
     }
+    p->nsorted = (uint32_t)sortb.size();
+    p->nlong_pad = (p->nlong_blocks + 7u) & ~7u;
+    if (p->slices > 1 && !sortb.empty()) {
+        // column cuts with equal shares of the sorted blocks' entries
+        const int S = p->slices;
+        const uint64_t ncols = p->chunk * (uint64_t)p->nranks;
+        DBuf<uint32_t> cnt;
+        GX_TRY(cnt.alloc(ncols));
+        GX_HIP_TRY(hipMemsetAsync(cnt.p, 0, ncols * 4, s));
+        if (nnz) {
+            hipLaunchKernelGGL(k_col_hist, dim3(grid_for(nnz, 256, 16384)), dim3(256), 0, s, p->ci, (int64_t)nnz, cnt.p);
+            GX_TRY(check_launch("k_col_hist"));
+        }
+        std::vector<uint32_t> h(ncols);
+        GX_HIP_TRY(hipMemcpyAsync(h.data(), cnt.p, ncols * 4, hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int64_t> cuts(S + 1, 0);
+        cuts[S] = (int64_t)ncols;
+        uint64_t acc = 0;
+        int j = 1;
+        for (uint64_t c = 0; c < ncols && j < S; c++) {
+            acc += h[c];
+            while (j < S && acc * (uint64_t)S >= (uint64_t)j * nnz) cuts[j++] = (int64_t)c + 1;
+        }
+        for (; j < S; j++) cuts[j] = (int64_t)ncols;
+        DBuf<int64_t> d_cuts;
+        GX_TRY(d_cuts.alloc(S + 1));
+        GX_TRY(p->sbound.alloc((size_t)sortb.size() * (S + 1)));
+        GX_TRY(p->ypart.alloc((size_t)S * std::max<int64_t>(rows, 1)));
+        GX_HIP_TRY(hipMemcpy(d_cuts.p, cuts.data(), (S + 1) * 8, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_sorted_bounds, dim3(grid_for(sortb.size(), 256, 1024)), dim3(256), 0, s, d_sort,
+                           (uint32_t)sortb.size(), p->sci.p, d_cuts.p, S, p->sbound.p);
+        GX_TRY(check_launch("k_sorted_bounds"));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+    }
     if (!all.empty()) {
         hipLaunchKernelGGL(k_sorted_split, dim3(grid_for(all.size(), 256, 1024)), dim3(256), 0, s, p->blocks.p,
                            (uint32_t)all.size(), p->sci.p, (int64_t)p->hot_cols, p->ssplit.p);
@@ -443,7 +593,19 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.long_nseg = p->long_nseg.p;
     a.long_part = p->long_part.p;
     a.long_ticket = p->long_ticket.p;
-    if (p->nblocks) {
+    a.sbound = p->sbound.p;
+    a.rows = (int64_t)p->rows;
+    a.nlong = p->nlong_blocks;
+    a.nlong_pad = p->nlong_pad;
+    a.nsorted = p->nsorted;
+    if (p->nblocks && p->slices > 1) {
+        KTimer kt(p->ctx, "pr_pull", s);   // sliced SpMV + epilogue: one iteration
+        switch (p->slices) {
+        case 2: launch_sliced<1024, 8, 2>(p, a, s); break;
+        case 4: launch_sliced<1024, 8, 4>(p, a, s); break;
+        default: launch_sliced<1024, 8, 8>(p, a, s); break;
+        }
+    } else if (p->nblocks) {
         KTimer kt(p->ctx, "pr_pull", s);   // both passes: one iteration's SpMV
         switch (p->sorted_variant) {
         case 1: launch_sorted<1024, 8, false>(p, a, s); break;

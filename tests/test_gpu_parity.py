@@ -178,10 +178,13 @@ def test_dense_tiers(ctx):
         np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=4), O.cdlp(csr, directed, 4))
 
 
-def test_pagerank_long_row_segments(ctx):
+@pytest.mark.parametrize("slices", ["1", "4"])
+def test_pagerank_long_row_segments(ctx, monkeypatch, slices):
     """A hub row of 150 000 entries, longer than a column-sorted block: LONG segments
-    combined by the last arriver, beside sorted blocks of random edges."""
+    combined by the last arriver, beside sorted blocks of random edges (with and without XCD
+    column slices)."""
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    monkeypatch.setenv("GX_PR_SLICES", slices)
     n = 150001
     rng = np.random.default_rng(3)
     a, b = rng.integers(1, n, 200000), rng.integers(1, n, 200000)
@@ -196,6 +199,8 @@ def test_pagerank_long_row_segments(ctx):
 @pytest.mark.parametrize("env", [{"GX_PR_HOT_COLS": "0"}, {"GX_PR_HOT_COLS": "1024"},
                                  {"GX_PR_HOT_COLS": "1024", "GX_PR_SORTED_ROWS": "64"},
                                  {"GX_PR_SORTED_VARIANT": "1"}, {"GX_PR_SORTED_VARIANT": "2"},
+                                 {"GX_PR_SLICES": "2"}, {"GX_PR_SLICES": "4"}, {"GX_PR_SLICES": "8"},
+                                 {"GX_PR_SLICES": "8", "GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SLICES": "1"},
                                  {"GX_PR_KERNEL": "adaptive"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
     """One pass, two passes around a small hub slice, tiny blocks, the other block shapes and

@@ -11,13 +11,17 @@ run() {   # name, env...
     local name=$1; shift
     env "$@" timeout -k 10 200 python bench.py --no-cpu-baseline --steps 10 > "$OUT/$name.json" 2> "$OUT/$name.err" || exit 1
 }
-for rep in a b; do
-run v0$rep
-run v1$rep GX_PR_SORTED_VARIANT=1
-run v2$rep GX_PR_SORTED_VARIANT=2
-run v3$rep GX_PR_SORTED_VARIANT=3
-done
-run v1_hot256k GX_PR_SORTED_VARIANT=1 GX_PR_HOT_COLS=262144
-run v1_r2k GX_PR_SORTED_VARIANT=1 GX_PR_SORTED_ROWS=2048
-run v1_b128k GX_PR_SORTED_VARIANT=1 GX_PR_SORTED_NNZ=131072
+dist() {  # name, pieces, env...
+    local name=$1 P=$2; shift 2
+    env GX_PR_PIECES=$P "$@" timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/$name.json" 2> "$OUT/$name.err" || exit 1
+}
+run s1 GX_PR_SLICES=1
+run s2 GX_PR_SLICES=2
+run s4 GX_PR_SLICES=4
+run s8 GX_PR_SLICES=8
+run s4_b128k GX_PR_SLICES=4 GX_PR_SORTED_NNZ=131072
+run s8_b128k GX_PR_SLICES=8 GX_PR_SORTED_NNZ=131072
+dist p8_s1 8 GX_PR_SLICES=1
+dist p8_s4 8 GX_PR_SLICES=4
+dist p8_s8 8 GX_PR_SLICES=8
 echo sweep-ok
