@@ -95,6 +95,13 @@ struct PrPart {
     int slices = 1;              // XCD column slices (k_pr_pull_sliced; GX_PR_SLICES)
     DBuf<int64_t> sbound;        // per sorted block: slice boundaries
     uint32_t nsorted = 0, nlong_pad = 0;
+    // dangling-score sum fused into the one-pass sorted kernel: blocks holding out-degree-0
+    // rows publish a partial, the last of them adds them up in slot order
+    bool fused_dangling = false;
+    DBuf<int32_t> dslot;         // per block: its partial's slot, -1 = no dangling rows
+    DBuf<double> fdpart;
+    DBuf<uint32_t> fdticket;
+    uint32_t ndblocks = 0;
     // hub-cached kernel: wave items, LDS hub prefix, fused dangling reduction
     int kernel = 2;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive), 2 = k_pr_pull_sorted
     bool int4_loads = false;     // k_pr_pull: 16-B index loads (lane stride 4) instead of lane-consecutive
@@ -123,7 +130,7 @@ int pr_plan_hub(PrPart *p, const std::vector<int64_t> &h_rp);
 int pr_step_hub(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 
 // Column-sorted block plan (k_pr_pull_sorted) and its iteration (gx_pr_sorted.hip).
-int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp);
+int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vector<int32_t> &h_outdeg);
 int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 // Dangling-score sum of this rank into x_local's last chunk slot.
 int pr_dangling(PrPart *p, double *x_local, hipStream_t s);

@@ -382,7 +382,7 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
         p->kernel = std::strcmp(e, "hub") == 0 ? 0 : std::strcmp(e, "adaptive") == 0 ? 1 : 2;
     if (const char *e = std::getenv("GX_PR_INT4")) p->int4_loads = std::atoi(e) != 0;
     if (p->kernel == 0) GX_TRY(pr_plan_hub(p, h_rp));
-    if (p->kernel == 2) GX_TRY(pr_plan_sorted(p, h_rp));
+    if (p->kernel == 2) GX_TRY(pr_plan_sorted(p, h_rp, h_outdeg));
     return GX_SUCCESS;
 }
 

@@ -65,13 +65,46 @@ struct SortedArgs {
     const int64_t *sbound;   // per sorted block: slices + 1 entry boundaries
     int64_t rows;            // local rows (ypart holds `slices` arrays of them)
     uint32_t nlong, nlong_pad, nsorted;
+    // fused dangling sum (one pass): per block slot or -1, partials, ticket
+    const int32_t *dslot;
+    double *dpart;
+    uint32_t *dticket;
+    uint32_t ndblocks;
 };
 
-__device__ __forceinline__ void sorted_epilogue(const SortedArgs &a, int32_t row, double s, double teleport) {
+// Returns the row's score if the row is dangling (out-degree 0), else 0.
+__device__ __forceinline__ double sorted_epilogue(const SortedArgs &a, int32_t row, double s, double teleport) {
     const double r = teleport + s;
     if (a.rank_out) a.rank_out[row] = r;
     const int32_t deg = a.outdeg[row];
     a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+    return deg > 0 ? 0.0 : r;
+}
+
+// Fused dangling sum: the block's dangling scores d (one value per thread) are reduced, the
+// block publishes its partial in its slot (agent scope) and takes a ticket; the last of the
+// ndblocks participants adds the partials in slot order into the chunk's last x slot.
+template <int BS>
+__device__ __forceinline__ void dangling_publish(const SortedArgs &a, int32_t slot, double d, double *wred) {
+    d = wave_sum(d);
+    __syncthreads();   // wred may still be read by an earlier reduction
+    if ((threadIdx.x & (kWave - 1)) == 0) wred[threadIdx.x / kWave] = d;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < BS / kWave; w++) tot += wred[w];
+    __hip_atomic_store(&a.dpart[slot], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(a.dticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t != a.ndblocks - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double all = 0.0;
+    for (uint32_t j = 0; j < a.ndblocks; j++)
+        all += __hip_atomic_load(&a.dpart[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.dticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.x_out[a.chunk - 1] = all;
 }
 
 // A long row's sum: the epilogue, or (sliced mode) slot 0 of the row's slice partials, the
@@ -218,7 +251,12 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
         if (PASS == 1) {
             for (int i = tid; i < nrows; i += BS) a.ypart[b.row_begin + i] = acc[i];
         } else {
-            for (int i = tid; i < nrows; i += BS) sorted_epilogue(a, b.row_begin + i, acc[i], teleport);
+            double d = 0.0;
+            for (int i = tid; i < nrows; i += BS) d += sorted_epilogue(a, b.row_begin + i, acc[i], teleport);
+            if (PASS == 0 && a.dslot) {
+                const int32_t slot = a.dslot[blockIdx.x];
+                if (slot >= 0) dangling_publish<BS>(a, slot, d, wred);
+            }
         }
         return;
     }
@@ -395,7 +433,7 @@ void launch_sliced(const PrPart *p, const SortedArgs &a, hipStream_t s) {
 
 // Plan: rows longer than long_nnz -> LONG segment blocks (longest first); runs of the other
 // rows -> blocks of <= sorted_nnz entries and <= sorted_rows rows, entries sorted by column.
-int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp) {
+int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vector<int32_t> &h_outdeg) {
     const int64_t rows = (int64_t)h_rp.size() - 1;
     const uint64_t nnz = (uint64_t)h_rp[rows];
     // entries per block: GX_PR_SORTED_NNZ, else the largest power of two <= 65536 that still
@@ -560,6 +598,27 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp) {
         GX_TRY(check_launch("k_sorted_bounds"));
         GX_HIP_TRY(hipStreamSynchronize(s));
     }
+    // fused dangling sum: one pass, and every dangling row in a sorted block
+    {
+        std::vector<int32_t> slot(all.size(), -1);
+        bool long_dangling = false;
+        for (const RowBlock &b : longb) long_dangling |= h_outdeg[b.row_begin] == 0;
+        uint32_t nd = 0;
+        for (size_t i = longb.size(); i < all.size(); i++) {
+            bool any = false;
+            for (int32_t r2 = all[i].row_begin; r2 < all[i].row_end && !any; r2++) any = h_outdeg[r2] == 0;
+            if (any) slot[i] = (int32_t)nd++;
+        }
+        p->fused_dangling = p->nd > 0 && nd > 0 && !long_dangling && !p->two_pass && p->slices == 1;
+        p->ndblocks = nd;
+        if (p->fused_dangling) {
+            GX_TRY(p->dslot.alloc(all.size()));
+            GX_TRY(p->fdpart.alloc(nd));
+            GX_TRY(p->fdticket.alloc(1));
+            GX_HIP_TRY(hipMemcpy(p->dslot.p, slot.data(), all.size() * 4, hipMemcpyHostToDevice));
+            GX_HIP_TRY(hipMemset(p->fdticket.p, 0, 4));
+        }
+    }
     if (!all.empty()) {
         hipLaunchKernelGGL(k_sorted_split, dim3(grid_for(all.size(), 256, 1024)), dim3(256), 0, s, p->blocks.p,
                            (uint32_t)all.size(), p->sci.p, (int64_t)p->hot_cols, p->ssplit.p);
@@ -598,6 +657,10 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.nlong = p->nlong_blocks;
     a.nlong_pad = p->nlong_pad;
     a.nsorted = p->nsorted;
+    a.dslot = p->fused_dangling ? p->dslot.p : nullptr;
+    a.dpart = p->fdpart.p;
+    a.dticket = p->fdticket.p;
+    a.ndblocks = p->ndblocks;
     if (p->nblocks && p->slices > 1) {
         KTimer kt(p->ctx, "pr_pull", s);   // sliced SpMV + epilogue: one iteration
         switch (p->slices) {
@@ -617,7 +680,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
         GX_HIP_TRY(hipMemsetAsync(x_local + p->chunk - 1, 0, sizeof(double), s));
     }
     GX_TRY(check_launch("k_pr_pull_sorted"));
-    return pr_dangling(p, x_local, s);
+    return p->fused_dangling ? GX_SUCCESS : pr_dangling(p, x_local, s);
 }
 
 }  // namespace gx
