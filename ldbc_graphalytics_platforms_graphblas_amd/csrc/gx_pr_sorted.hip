@@ -83,28 +83,43 @@ __device__ __forceinline__ double sorted_epilogue(const SortedArgs &a, int32_t r
 
 // Fused dangling sum: the block's dangling scores d (one value per thread) are reduced, the
 // block publishes its partial in its slot (agent scope) and takes a ticket; the last of the
-// ndblocks participants adds the partials in slot order into the chunk's last x slot.
+// ndblocks participants adds the partials up with the whole workgroup (thread t takes slots
+// t, t + BS, ...; fixed tree, so the order is fixed) into the chunk's last x slot.  One thread
+// looping over agent-scope loads took ~8 us at the end of the launch.
 template <int BS>
-__device__ __forceinline__ void dangling_publish(const SortedArgs &a, int32_t slot, double d, double *wred) {
+__device__ __forceinline__ void dangling_publish(const SortedArgs &a, int32_t slot, double d, double *wred,
+                                                 int *last) {
+    const int tid = threadIdx.x;
     d = wave_sum(d);
     __syncthreads();   // wred may still be read by an earlier reduction
-    if ((threadIdx.x & (kWave - 1)) == 0) wred[threadIdx.x / kWave] = d;
+    if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = d;
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    double tot = 0.0;
+    if (tid == 0) {
+        double tot = 0.0;
 #pragma unroll
-    for (int w = 0; w < BS / kWave; w++) tot += wred[w];
-    __hip_atomic_store(&a.dpart[slot], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t t = __hip_atomic_fetch_add(a.dticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t != a.ndblocks - 1) return;
+        for (int w = 0; w < BS / kWave; w++) tot += wred[w];
+        __hip_atomic_store(&a.dpart[slot], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = __hip_atomic_fetch_add(a.dticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last = t == a.ndblocks - 1;
+    }
+    __syncthreads();
+    if (!*last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    double all = 0.0;
-    for (uint32_t j = 0; j < a.ndblocks; j++)
-        all += __hip_atomic_load(&a.dpart[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.dticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    a.x_out[a.chunk - 1] = all;
+    double v = 0.0;
+    for (uint32_t j = tid; j < a.ndblocks; j += BS) v += __hip_atomic_load(&a.dpart[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v = wave_sum(v);
+    __syncthreads();
+    if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = v;
+    __syncthreads();
+    if (tid == 0) {
+        double all = 0.0;
+#pragma unroll
+        for (int w = 0; w < BS / kWave; w++) all += wred[w];
+        __hip_atomic_store(a.dticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.x_out[a.chunk - 1] = all;
+    }
 }
 
 // A long row's sum: the epilogue, or (sliced mode) slot 0 of the row's slice partials, the
@@ -230,6 +245,7 @@ template <int BS, int U, int PASS, bool PIPE>
 __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
     extern __shared__ double acc[];   // one fp64 accumulator per row of the block
     __shared__ double wred[BS / kWave];
+    __shared__ int last;
 
     const RowBlock b = a.blocks[blockIdx.x];
     const int tid = threadIdx.x;
@@ -255,7 +271,7 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
             for (int i = tid; i < nrows; i += BS) d += sorted_epilogue(a, b.row_begin + i, acc[i], teleport);
             if (PASS == 0 && a.dslot) {
                 const int32_t slot = a.dslot[blockIdx.x];
-                if (slot >= 0) dangling_publish<BS>(a, slot, d, wred);
+                if (slot >= 0) dangling_publish<BS>(a, slot, d, wred, &last);
             }
         }
         return;
