@@ -437,16 +437,34 @@ def main():
     # torch.distributed all-gather per piece and iteration (pr_partition.PartitionedPageRank)
     driver = os.environ.get("GX_PR_DRIVER", "device")
     use_graph = os.environ.get("GX_PR_GRAPH", "1") != "0"
-    comm = None
+    comm = dpr = None
     if driver == "device":
-        if dist:
-            def share_id(uid: bytes) -> bytes:
-                box = [uid]
-                dist.broadcast_object_list(box, src=0)
-                return box[0]
-            comm = Comm(ctx, world, rank, share_id)
-        dpr = DevicePageRank(steppers, comm, use_graph=use_graph)
-
+        ok = 1
+        try:
+            if dist:
+                def share_id(uid: bytes) -> bytes:
+                    box = [uid]
+                    dist.broadcast_object_list(box, src=0)
+                    return box[0]
+                comm = Comm(ctx, world, rank, share_id)
+            dpr = DevicePageRank(steppers, comm, use_graph=use_graph)
+            dpr.run(args.iters, stream.cuda_stream)
+            torch.cuda.synchronize(device)
+        except Exception as e:   # noqa: BLE001 -- reported, then every rank takes the host driver
+            print(f"[bench] device-driven PageRank unavailable ({e}); using the host driver", file=sys.stderr)
+            ok = 0
+        if dist:   # all ranks agree, so nobody waits in a collective the others skip
+            t = torch.tensor([ok], dtype=torch.int32, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = int(t.item())
+        if not ok:
+            if dpr is not None:
+                dpr.close()
+            if comm is not None:
+                comm.close()
+            comm = dpr = None
+            driver = "host"
+    if driver == "device":
         class _Run:
             def run(self, iters):
                 dpr.run(iters, stream.cuda_stream)
@@ -585,10 +603,10 @@ def main():
             "graph_gen_s": t_gen,
         }
         print(json.dumps(line), flush=True)
-    if driver == "device":
+    if dpr is not None:
         dpr.close()
-        if comm is not None:
-            comm.close()
+    if comm is not None:
+        comm.close()
     for st in steppers:
         st.close()
     ctx.close()

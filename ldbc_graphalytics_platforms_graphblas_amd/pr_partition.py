@@ -268,11 +268,12 @@ class Comm:
         self.N = N
         lib = N.lib()
         uid = C.create_string_buffer(128)
-        if rank == 0:
-            N.check(lib.gx_comm_unique_id(uid), "gx_comm_unique_id")
-        got = share_id(uid.raw if rank == 0 else b"")
+        mine = b""
+        if rank == 0 and lib.gx_comm_unique_id(uid) == 0:
+            mine = uid.raw
+        got = share_id(mine)   # every rank takes part, also when rank 0 has no id
         if len(got) != 128:
-            raise ValueError("RCCL unique id must be 128 bytes")
+            raise RuntimeError("no RCCL unique id from rank 0: " + lib.gx_last_error().decode(errors="replace"))
         uid = C.create_string_buffer(got, 128)
         self.handle = C.c_void_p()
         N.check(lib.gx_comm_create(ctx.handle, nranks, rank, uid, C.byref(self.handle)), "gx_comm_create")
