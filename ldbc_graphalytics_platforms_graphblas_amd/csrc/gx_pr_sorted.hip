@@ -452,17 +452,17 @@ void launch_sliced(const PrPart *p, const SortedArgs &a, hipStream_t s) {
 int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vector<int32_t> &h_outdeg) {
     const int64_t rows = (int64_t)h_rp.size() - 1;
     const uint64_t nnz = (uint64_t)h_rp[rows];
-    // entries per block: GX_PR_SORTED_NNZ, else 65536 halved while the partition gives fewer
-    // than one block per CU (the partitions of many ranks or pieces are small), or doubled up
-    // to 1 Mi while it gives more than four per CU: large blocks merge more hub rows into one
-    // sorted sweep (SYN-7_5 best at 64 Ki, graph500-22 at 128 Ki, SYN-8_5 at 1 Mi: 252 -> 419
-    // G edges/s, tools/pr_sorted_sweep.sh)
+    // entries per block: GX_PR_SORTED_NNZ, else 65536 -- 32768 when the partition gives fewer
+    // than one block per CU (the 1/4 and 1/8 partitions of SYN-7_5 ran best at 32 Ki: 35 us vs
+    // 37 at 16 Ki and 67 at 64 Ki for 1/8), or doubled up to 1 Mi while it gives more than four
+    // per CU: large blocks merge more hub rows into one sorted sweep (SYN-7_5 best at 64 Ki,
+    // graph500-22 at 128 Ki, SYN-8_5 at 1 Mi: 252 -> 419 G edges/s, tools/pr_sorted_sweep.sh)
     int64_t B = p->sorted_nnz;
     if (std::getenv("GX_PR_SORTED_NNZ")) {
         B = env_int("GX_PR_SORTED_NNZ", p->sorted_nnz, 1024, 1 << 22);
     } else {
         const int64_t cus = std::max(1, p->ctx->num_cus);
-        while (B > 4096 && (int64_t)nnz < B * cus) B >>= 1;
+        while (B > 32768 && (int64_t)nnz < B * cus) B >>= 1;
         while (B < (1 << 20) && (int64_t)nnz > 4 * B * cus) B <<= 1;
     }
     p->sorted_nnz = (int)B;
