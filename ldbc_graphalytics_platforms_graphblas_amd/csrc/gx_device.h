@@ -124,6 +124,7 @@ struct SsspLayout {
     DBuf<int32_t> ci;
     DBuf<double> w;
     DBuf<int64_t> lend;   // end of the light part of row v (absolute entry index)
+    int64_t n_active = 0; // vertices with at least one edge
 };
 }  // namespace gx
 

@@ -70,6 +70,9 @@ struct SsspState {
     uint32_t qcnt[2];
     uint32_t ovf_cnt[2];
     uint32_t settled_cnt;         // vertices queued in the current bucket
+    int32_t pull;                 // heavy phase pulled by the unsettled vertices (k_sssp_pull)
+    uint32_t pull_min;            // settled-list size from which the heavy phase is pulled
+    unsigned long long smin;      // smallest distance on the settled list (pull bound)
     uint32_t ring_cnt[kRing];
 };
 
@@ -107,51 +110,6 @@ __device__ __forceinline__ void wave_count(unsigned long long *stats, int slot, 
     if ((threadIdx.x & (kWave - 1)) == 0 && x) atomicAdd(&stats[slot], x);
 }
 
-// wave-aggregated append of `k` consecutive items (vertex << 32 | j) per lane
-__device__ __forceinline__ void wave_append_items(uint32_t k, int32_t v, uint64_t *queue, uint32_t *qcount) {
-    const int lane = threadIdx.x & (kWave - 1);
-    uint32_t x = k;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, kWave);
-        if (lane >= off) x += y;
-    }
-    const uint32_t total = __shfl(x, kWave - 1, kWave);
-    if (total == 0) return;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(qcount, total);
-    base = __shfl(base, 0, kWave);
-    const uint32_t excl = x - k;
-    for (uint32_t j = 0; j < k; j++) queue[base + excl + j] = ((uint64_t)(uint32_t)v << 32) | j;
-}
-
-__device__ __forceinline__ void wave_append_vertex(bool take, int32_t v, int32_t *list, uint32_t *count) {
-    const uint64_t mask = __ballot(take);
-    if (mask == 0) return;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int leader = __ffsll((unsigned long long)mask) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
-    base = __shfl(base, leader, kWave);
-    if (take) list[base + __popcll(mask & ((1ull << lane) - 1))] = v;
-}
-
-// append v to ring slot `slot`; lanes are grouped by slot, one atomic per distinct slot
-__device__ __forceinline__ void wave_append_ring(bool take, int slot, int32_t v, const SsspBufs &B) {
-    const int lane = threadIdx.x & (kWave - 1);
-    uint64_t pending = __ballot(take);
-    while (pending) {
-        const int leader = __ffsll((unsigned long long)pending) - 1;
-        const int s = __shfl(slot, leader, kWave);
-        const uint64_t grp = __ballot(take && slot == s);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&B.st->ring_cnt[s], (uint32_t)__popcll(grp));
-        base = __shfl(base, leader, kWave);
-        if (take && slot == s) B.ring[(uint64_t)s * B.ring_cap + base + __popcll(grp & ((1ull << lane) - 1))] = v;
-        pending &= ~grp;
-    }
-}
-
 __device__ __forceinline__ void wave_min_to(unsigned long long m, unsigned long long *dst) {
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long o = __shfl_xor(m, off, kWave);
@@ -163,17 +121,23 @@ __device__ __forceinline__ void wave_min_to(unsigned long long m, unsigned long 
         atomicMin(dst, m);
 }
 
-// Per-wave LDS staging of queue pushes.  Improvements are sparse (well under 1% of the
-// relaxations), so pushing them one wave-slot at a time costs one same-address global atomic
-// per push on the few queue counters -- those serialise in one L2 channel and dominated the
-// kernel.  Pushes are staged as (vertex, tag) in LDS and flushed kStage at a time, with one
-// global atomic per queue per flush.
-constexpr int kStage = 512;
+// Per-wave LDS staging of queue pushes.  The queue counters are a handful of words shared by
+// the whole grid; device-scope atomics on one word serialise (about 20 ns apiece, measured:
+// a relax round's time tracked its push count, not its edge count).  Pushes are therefore
+// staged as (vertex, tag) in LDS and reserved in bulk: a flush counts the staged pushes per
+// queue (near items, settled list, overflow, each ring slot), takes every queue's range with
+// one atomic (the lanes of one instruction, one queue each) and then writes the entries.
+// Mid-kernel flushes (a full stage) are per wave; the final one is per workgroup, so a launch
+// costs at most one atomic per queue per workgroup plus one per full stage.
+constexpr int kStage = 1024;
 constexpr int kTagNear = kRing, kTagOvf = kRing + 1;   // tags 0..kRing-1 are ring slots
+constexpr int kCats = 3 + kRing;                       // near items, settled, overflow, ring slots
 
 struct Stage {
     int32_t v[kStage];
     uint32_t tag[kStage];   // bits 0-6 queue, bit 7 settled-list push, bits 8.. chunk count
+    uint32_t cnt[kCats];    // staged pushes per queue
+    uint32_t base[kCats];   // next free entry per queue (reserved range)
 };
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -182,10 +146,49 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void stage_flush(Stage &sg, uint32_t &n, const SsspBufs &B, uint64_t *near_out,
-                                            uint32_t *near_count, int32_t *ovf, uint32_t *ovf_count) {
-    wave_lds_sync();
+__device__ __forceinline__ uint32_t *queue_counter(int cat, const SsspBufs &B, uint32_t *near_count,
+                                                   uint32_t *ovf_count) {
+    return cat == 0 ? near_count : cat == 1 ? &B.st->settled_cnt : cat == 2 ? ovf_count : &B.st->ring_cnt[cat - 3];
+}
+
+// pass 1: per-queue totals of the n staged pushes into sg.cnt
+__device__ __forceinline__ void stage_count(Stage &sg, uint32_t n) {
     const int lane = threadIdx.x & (kWave - 1);
+    if (lane < kCats) sg.cnt[lane] = 0;
+    wave_lds_sync();
+    uint32_t items = 0, nset = 0, novf = 0;
+    for (uint32_t base = 0; base < n; base += kWave) {
+        const uint32_t i = base + lane;
+        if (i < n) {
+            const uint32_t tag = sg.tag[i], q = tag & 0x7Fu;
+            if (q == (uint32_t)kTagNear) {
+                items += tag >> 8;
+                nset += (tag >> 7) & 1u;
+            } else if (q == (uint32_t)kTagOvf) {
+                novf++;
+            } else {
+                atomicAdd(&sg.cnt[3 + q], 1u);
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        items += __shfl_xor(items, off, kWave);
+        nset += __shfl_xor(nset, off, kWave);
+        novf += __shfl_xor(novf, off, kWave);
+    }
+    if (lane == 0) {
+        sg.cnt[0] = items;
+        sg.cnt[1] = nset;
+        sg.cnt[2] = novf;
+    }
+    wave_lds_sync();
+}
+
+// pass 2: write the staged pushes into the ranges starting at sg.base
+__device__ __forceinline__ void stage_write(Stage &sg, uint32_t n, const SsspBufs &B, uint64_t *near_out,
+                                            int32_t *ovf) {
+    const int lane = threadIdx.x & (kWave - 1);
+    uint32_t r_items = sg.base[0], r_set = sg.base[1], r_ovf = sg.base[2];
     for (uint32_t base = 0; base < n; base += kWave) {
         const uint32_t i = base + lane;
         const bool valid = i < n;
@@ -193,12 +196,69 @@ __device__ __forceinline__ void stage_flush(Stage &sg, uint32_t &n, const SsspBu
         const uint32_t tag = valid ? sg.tag[i] : 0xFFu;
         const uint32_t q = tag & 0x7Fu;
         const bool near = valid && q == (uint32_t)kTagNear;
-        wave_append_items(near ? (tag >> 8) : 0u, v, near_out, near_count);
-        wave_append_vertex(near && (tag & 0x80u), v, B.settled, &B.st->settled_cnt);
-        wave_append_vertex(valid && q == (uint32_t)kTagOvf, v, ovf, ovf_count);
-        wave_append_ring(valid && q < (uint32_t)kRing, (int)q, v, B);
+        const uint32_t k = near ? (tag >> 8) : 0u;
+        uint32_t x = k;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, kWave);
+            if (lane >= off) x += y;
+        }
+        const uint32_t at = r_items + x - k;
+        for (uint32_t j = 0; j < k; j++) near_out[at + j] = ((uint64_t)(uint32_t)v << 32) | j;
+        r_items += __shfl(x, kWave - 1, kWave);
+        const uint64_t below = (1ull << lane) - 1;
+        const bool set = near && (tag & 0x80u);
+        const uint64_t ms = __ballot(set);
+        if (set) B.settled[r_set + __popcll(ms & below)] = v;
+        r_set += (uint32_t)__popcll(ms);
+        const bool to_ovf = valid && q == (uint32_t)kTagOvf;
+        const uint64_t mo = __ballot(to_ovf);
+        if (to_ovf) ovf[r_ovf + __popcll(mo & below)] = v;
+        r_ovf += (uint32_t)__popcll(mo);
+        if (valid && q < (uint32_t)kRing) B.ring[(uint64_t)q * B.ring_cap + atomicAdd(&sg.base[3 + q], 1u)] = v;
     }
     wave_lds_sync();
+}
+
+// full stage mid-kernel: reserve for this wave alone
+__device__ __forceinline__ void stage_flush(Stage &sg, uint32_t &n, const SsspBufs &B, uint64_t *near_out,
+                                            uint32_t *near_count, int32_t *ovf, uint32_t *ovf_count) {
+    wave_lds_sync();
+    stage_count(sg, n);
+    const int lane = threadIdx.x & (kWave - 1);
+    if (lane < kCats) {
+        const uint32_t c = sg.cnt[lane];
+        sg.base[lane] = c ? atomicAdd(queue_counter(lane, B, near_count, ovf_count), c) : 0u;
+    }
+    wave_lds_sync();
+    stage_write(sg, n, B, near_out, ovf);
+    n = 0;
+}
+
+// end of the kernel: one reservation per queue for the whole workgroup.  Every thread of
+// the workgroup must call it.
+__device__ __forceinline__ void stage_final(Stage *stages, uint32_t &n, const SsspBufs &B, uint64_t *near_out,
+                                            uint32_t *near_count, int32_t *ovf, uint32_t *ovf_count) {
+    constexpr int kWaves = kSsspBlock / kWave;
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    Stage &sg = stages[wid];
+    wave_lds_sync();
+    stage_count(sg, n);
+    __syncthreads();
+    if (wid == 0 && lane < kCats) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) {
+            const uint32_t c = stages[w].cnt[lane];
+            stages[w].base[lane] = tot;
+            tot += c;
+        }
+        const uint32_t b = tot ? atomicAdd(queue_counter(lane, B, near_count, ovf_count), tot) : 0u;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) stages[w].base[lane] += b;
+    }
+    __syncthreads();
+    if (n) stage_write(sg, n, B, near_out, ovf);
     n = 0;
 }
 
@@ -224,6 +284,8 @@ __global__ void k_sssp_plan(SsspState *st) {
     if (!st->heavy && st->settled_cnt > 0) {
         st->heavy = 1;
         st->mode = 3;
+        st->pull = st->settled_cnt >= st->pull_min;
+        st->smin = ~0ull;
         return;
     }
     st->heavy = 0;
@@ -279,6 +341,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     }
     const int64_t cur = st->cur, win_base = st->win_base, lim = win_base + kRing;
     const int32_t epoch = st->epoch;
+    const bool pull = mode == 3 && st->pull;
     unsigned long long mymin = ~0ull, n_skip = 0;
     const uint32_t stride = gridDim.x * kSsspBlock;
     const uint32_t nround = (count + stride - 1) / stride;
@@ -302,8 +365,12 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
             const unsigned long long db = B.dist[v];
             if (mode == 3) {
                 B.relaxed[v] = db;   // heavy edges now, light edges already relaxed at db
-                to_near = true;
-                nch = chunks_of(B.rp[v + 1] - B.lend[v]);
+                if (pull) {
+                    mymin = min(mymin, db);
+                } else {
+                    to_near = true;
+                    nch = chunks_of(B.rp[v + 1] - B.lend[v]);
+                }
             } else if (db == B.relaxed[v]) {
                 n_skip++;
             } else if (mode == 1) {
@@ -337,9 +404,144 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
         staged += (uint32_t)__popcll(mask);
         if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
     }
-    if (staged) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
+    stage_final(stages, staged, B, near_out, near_count, ovf, ovf_count);
     if (mode == 2) wave_min_to(mymin, &B.st->ovf_minb);
+    if (pull) wave_min_to(mymin, &B.st->smin);
     wave_count(B.stats, 7, n_skip);
+}
+
+// Heavy phase pulled by its targets (undirected graphs: the heavy edge (u, v, w) of a settled
+// u is also the heavy edge (v, u, w) of v).  When the settled list holds a large share of the
+// vertices -- the first buckets of a power-law graph hold most of the giant component --
+// pushing its heavy edges scans far more edges than can improve anything: nearly all of them
+// lead to vertices settled already.  Pulling skips every vertex whose distance is at most
+// fl(smin + delta), the smallest value a heavy relaxation from this bucket can produce, and
+// relaxes the heavy edges of the rest whose source is on the settled list (sstamp == cur),
+// with the push's operands (dist[u] + w) and the push's strict-min test, so the distances
+// are bit-identical.  Lanes take 64 consecutive vertices and walk their concatenated heavy
+// edges as k_sssp_relax walks items; a vertex's candidates meet in an LDS min (its whole row
+// is in the wave), so each improved vertex is written and queued once, by its own lane.
+__device__ __forceinline__ void sssp_pull(const SsspBufs &B, Stage *stages, unsigned long long *vmin) {
+    Stage &sg = stages[threadIdx.x / kWave];
+    constexpr int kSlots = 4;
+    const SsspState *st = B.st;
+    const int64_t cur = st->cur, lim = st->win_base + kRing;
+    const int32_t epoch = st->epoch, cur32 = (int32_t)cur;
+    const unsigned long long bound = dbits(bitsd(st->smin) + B.delta);
+    const uint64_t n = B.ring_cap;
+    uint64_t *near_out = B.q[0];   // a pull never pushes near items
+    uint32_t *near_count = &B.st->qcnt[0];
+    int32_t *ovf = B.ovf[epoch & 1];
+    uint32_t *ovf_count = &B.st->ovf_cnt[epoch & 1];
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t wave = (blockIdx.x * kSsspBlock + threadIdx.x) / kWave;
+    const uint64_t nwaves = gridDim.x * (kSsspBlock / kWave);
+    uint32_t staged = 0;
+    unsigned long long mymin = ~0ull, c_items = 0, c_edges = 0, c_try = 0, c_impr = 0, c_ring = 0, c_ovf = 0;
+    for (uint64_t base = wave * kWave; base < n; base += nwaves * kWave) {
+        const uint64_t v0 = base + lane;
+        int64_t rs = 0, sz = 0;
+        unsigned long long dv = 0;
+        if (v0 < n) {
+            dv = B.dist[v0];
+            if (dv > bound) {
+                rs = B.lend[v0];
+                sz = B.rp[v0 + 1] - rs;
+                c_items += sz > 0;
+            }
+        }
+        int64_t incl = sz;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int64_t y = __shfl_up(incl, off, kWave);
+            if (lane >= off) incl += y;
+        }
+        const int64_t total = __shfl(incl, kWave - 1, kWave);
+        if (total == 0) continue;
+        const int64_t excl = incl - sz;
+        vmin[lane] = dv;
+        wave_lds_sync();
+        for (int64_t e0 = 0; e0 < total; e0 += kWave * kSlots) {
+            int64_t k[kSlots];
+            int32_t u[kSlots], ss[kSlots], to[kSlots];
+            unsigned long long tdv[kSlots], du[kSlots];
+            double wk[kSlots];
+            bool act[kSlots];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) {
+                const int64_t e_raw = e0 + q * kWave + lane;
+                act[q] = e_raw < total;
+                const int64_t e = act[q] ? e_raw : total - 1;   // keep the loads in range
+                int o = 0;
+#pragma unroll
+                for (int step = kWave / 2; step > 0; step >>= 1)
+                    if (__shfl(incl, o + step - 1, kWave) <= e) o += step;
+                k[q] = __shfl(rs, o, kWave) + (e - __shfl(excl, o, kWave));
+                tdv[q] = __shfl(dv, o, kWave);
+                to[q] = o;
+            }
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) u[q] = B.ci[k[q]];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) wk[q] = B.w[k[q]];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) ss[q] = B.sstamp[u[q]];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++)
+                du[q] = __hip_atomic_load(&B.dist[u[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) {
+                c_edges += act[q];
+                if (act[q] && ss[q] == cur32) {
+                    c_try++;
+                    const unsigned long long ndb = dbits(bitsd(du[q]) + wk[q]);
+                    if (ndb < tdv[q]) atomicMin(&vmin[to[q]], ndb);
+                }
+            }
+        }
+        wave_lds_sync();
+        const unsigned long long m = vmin[lane];
+        wave_lds_sync();
+        bool to_ring = false, to_ovf = false;
+        int slot = 0;
+        if (m < dv) {
+            __hip_atomic_store(&B.dist[v0], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c_impr++;
+            int64_t b = bucket_of(bitsd(m), B.inv_delta);
+            if (b <= cur) b = cur + 1;
+            if (b < lim) {
+                if (claim(&B.bstamp[v0], (int32_t)b)) {
+                    to_ring = true;
+                    slot = (int)(b % kRing);
+                }
+            } else {
+                if (claim(&B.ostamp[v0], epoch)) to_ovf = true;
+                mymin = min(mymin, (unsigned long long)b);
+            }
+        }
+        c_ring += to_ring;
+        c_ovf += to_ovf;
+        const bool take = to_ring | to_ovf;
+        const uint64_t mask = __ballot(take);
+        if (mask == 0) continue;
+        if (take) {
+            const uint32_t pos = staged + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
+            sg.v[pos] = (int32_t)v0;
+            sg.tag[pos] = to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot;
+        }
+        staged += (uint32_t)__popcll(mask);
+        if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
+    }
+    stage_final(stages, staged, B, near_out, near_count, ovf, ovf_count);
+    wave_min_to(mymin, &B.st->ovf_minb);
+    if (B.stats) {
+        wave_count(B.stats, 0, c_items);
+        wave_count(B.stats, 1, c_edges);
+        wave_count(B.stats, 2, c_try);
+        wave_count(B.stats, 3, c_impr);
+        wave_count(B.stats, 5, c_ring);
+        wave_count(B.stats, 6, c_ovf);
+    }
 }
 
 // Relax the light (w < delta) or, in the heavy phase, the heavy out-edges of every near item;
@@ -356,8 +558,15 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
     const int32_t r = st->round;
     const int qin = r & 1;
     const uint32_t count = st->qcnt[qin];
-    if (count == 0) return;
     const bool heavy = st->heavy != 0;
+    __shared__ Stage stages[kSsspBlock / kWave];
+    Stage &sg = stages[threadIdx.x / kWave];
+    if (heavy && st->pull) {
+        __shared__ unsigned long long vmin[kSsspBlock];
+        sssp_pull(B, stages, vmin + (threadIdx.x & ~(kWave - 1)));
+        return;
+    }
+    if (count == 0) return;
     const int64_t cur = st->cur, lim = st->win_base + kRing;
     const int32_t epoch = st->epoch, rn = r + 1, cur32 = (int32_t)cur;
     const uint64_t *near_in = B.q[qin];
@@ -370,17 +579,18 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = (blockIdx.x * kSsspBlock + threadIdx.x) / kWave;
     const uint32_t nwaves = gridDim.x * (kSsspBlock / kWave);
-    __shared__ Stage stages[kSsspBlock / kWave];
-    Stage &sg = stages[threadIdx.x / kWave];
     uint32_t staged = 0;
     unsigned long long mymin = ~0ull, c_items = 0, c_edges = 0, c_try = 0, c_impr = 0, c_near = 0, c_ring = 0,
                        c_ovf = 0;
-    for (uint64_t base = (uint64_t)wave * kWave; base < count; base += (uint64_t)nwaves * kWave) {
+    // a wave takes up to 64 items, fewer when the queue is short, so that small rounds (a
+    // hub's chunks) spread over all waves instead of serialising in a few
+    const uint32_t ipw = min((uint32_t)kWave, max(1u, (count + nwaves - 1) / nwaves));
+    for (uint64_t base = (uint64_t)wave * ipw; base < count; base += (uint64_t)nwaves * ipw) {
         const uint64_t idx = base + lane;
         int64_t rs = 0;
         int32_t sz = 0;
         double du = 0.0;
-        if (idx < count) {
+        if (lane < (int)ipw && idx < count) {
             const uint64_t item = near_in[idx];
             const int32_t u = (int32_t)(item >> 32);
             const int64_t lo = heavy ? B.lend[u] : B.rp[u], hi = heavy ? B.rp[u + 1] : B.lend[u];
@@ -481,7 +691,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
             }
         }
     }
-    if (staged) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
+    stage_final(stages, staged, B, near_out, near_count, ovf, ovf_count);
     wave_min_to(mymin, &B.st->ovf_minb);
     if (B.stats) {
         wave_count(B.stats, 0, c_items);
@@ -507,7 +717,7 @@ __global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxe
     }
 }
 
-__global__ void k_sssp_seed(SsspBufs B, int32_t src) {
+__global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min) {
     SsspState *st = B.st;
     const uint32_t nch = chunks_of(B.lend[src] - B.rp[src]);
     for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x) B.q[0][j] = ((uint64_t)(uint32_t)src << 32) | j;
@@ -526,6 +736,9 @@ __global__ void k_sssp_seed(SsspBufs B, int32_t src) {
         st->epoch = 1;
         st->mode = 0;
         st->heavy = 0;
+        st->pull = 0;
+        st->pull_min = pull_min;
+        st->smin = ~0ull;
         st->slot = 0;
         st->consume = -1;
         st->split_src = 0;
@@ -603,6 +816,11 @@ int ensure_sssp_layout(gx_graph *g, double delta, hipStream_t s) {
     const int64_t n = (int64_t)g->n, nnz = (int64_t)g->nnz;
     auto L = std::make_unique<SsspLayout>();
     L->delta = delta;
+    L->n_active = n;
+    if ((int64_t)g->A.h_rp.size() == n + 1) {
+        L->n_active = 0;
+        for (int64_t v = 0; v < n; v++) L->n_active += g->A.h_rp[v + 1] != g->A.h_rp[v];
+    }
     GX_TRY(L->ci.alloc(nnz, 16));
     GX_TRY(L->w.alloc(nnz, 16));
     GX_TRY(L->lend.alloc(n));
@@ -734,7 +952,19 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nstamp.p,
                        bstamp.p, ostamp.p, sstamp.p, n);
     GX_TRY(check_launch("k_sssp_init"));
-    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src);
+    // heavy phases whose settled list holds at least 1/GX_SSSP_PULL_FRAC (default 4) of the
+    // non-isolated vertices are pulled (undirected graphs; GX_SSSP_PULL=0 never, 2 always)
+    uint32_t pull_min = 0xFFFFFFFFu;
+    {
+        const char *e = std::getenv("GX_SSSP_PULL");
+        const int mode = e ? std::atoi(e) : 1;
+        const char *f = std::getenv("GX_SSSP_PULL_FRAC");
+        const double frac = f ? std::atof(f) : 4.0;
+        if (!g->directed && mode == 2) pull_min = 1;
+        else if (!g->directed && mode == 1 && frac > 0.0)
+            pull_min = (uint32_t)std::max<double>(1.0, std::ceil((double)lay.n_active / frac));
+    }
+    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min);
     GX_TRY(check_launch("k_sssp_seed"));
     const unsigned grid = (unsigned)std::max(1, ctx->num_cus) * 8;
     // a bound every correct run stays far below: each step settles a vertex or a bucket
@@ -742,7 +972,39 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     uint64_t steps = 0;
     int batch = 4;
     int32_t done = 0;
+    // GX_SSSP_VERBOSE=2: one step per batch, a line per step (bucket, phase, items, work, time)
+    const bool per_step = verbose && std::atoi(std::getenv("GX_SSSP_VERBOSE")) >= 2;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    unsigned long long prev[8] = {};
+    if (per_step) {
+        batch = 1;
+        GX_HIP_TRY(hipEventCreate(&ev0));
+        GX_HIP_TRY(hipEventCreate(&ev1));
+    }
     while (!done) {
+        if (per_step) {
+            hipLaunchKernelGGL(k_sssp_plan, dim3(1), dim3(1), 0, s, st.p);
+            SsspState h;
+            GX_HIP_TRY(hipMemcpyAsync(&h, st.p, sizeof(h), hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipEventRecord(ev0, s));
+            hipLaunchKernelGGL(k_sssp_advance, dim3(grid), dim3(kSsspBlock), 0, s, B);
+            hipLaunchKernelGGL(k_sssp_relax, dim3(grid), dim3(kSsspBlock), 0, s, B);
+            GX_HIP_TRY(hipEventRecord(ev1, s));
+            unsigned long long c[8];
+            GX_HIP_TRY(hipMemcpyAsync(c, stats.p, 64, hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipMemcpyAsync(&done, &st.p->done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            float ms = 0.f;
+            GX_HIP_TRY(hipEventElapsedTime(&ms, ev0, ev1));
+            std::fprintf(stderr, "step %llu round %d bucket %lld mode %d heavy %d pull %d near %u settled %u | %.1f us "
+                         "items %llu edges %llu improved %llu near %llu ring %llu\n",
+                         (unsigned long long)steps, h.round, (long long)h.cur, h.mode, h.heavy, h.pull,
+                         h.qcnt[h.round & 1], h.settled_cnt, ms * 1e3, c[0] - prev[0], c[1] - prev[1],
+                         c[3] - prev[3], c[4] - prev[4], c[5] - prev[5]);
+            std::memcpy(prev, c, sizeof(c));
+            if (++steps > max_steps) return fail(GX_PANIC, "gx_sssp: delta-stepping did not converge");
+            continue;
+        }
         for (int i = 0; i < batch; i++) {
             hipLaunchKernelGGL(k_sssp_plan, dim3(1), dim3(1), 0, s, st.p);
             {
@@ -761,6 +1023,8 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         if (steps > max_steps) return fail(GX_PANIC, "gx_sssp: delta-stepping did not converge");
         batch = std::min(batch * 2, 32);
     }
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
     GX_TRY(device_end(ctx));
     if (verbose) {
         SsspState h;

@@ -222,3 +222,30 @@ def test_pagerank_escape_groups(ctx, monkeypatch):
     csr = csr_from_edges(n, perm[0::2], perm[1::2], None, symmetric=True)
     np.testing.assert_allclose(gpu_run(ctx, _G(csr, False), "PR", damping=0.85, iters=4),
                                O.pagerank(csr, False, 0.85, 4), rtol=PR_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("env", [{"GX_SSSP_PULL": "0"}, {"GX_SSSP_PULL": "2"},
+                                 {"GX_SSSP_PULL": "2", "GX_SSSP_DSCALE": "2"},
+                                 {"GX_SSSP_PULL": "2", "GX_SSSP_DSCALE": "200"},
+                                 {"GX_SSSP_PULL_FRAC": "50", "GX_SSSP_DSCALE": "5"}])
+def test_sssp_pull_heavy_phase(ctx, monkeypatch, env):
+    """Heavy phases pushed, always pulled, and pulled only for big settled lists, over narrow
+    and wide buckets, give the oracle's distances bit for bit -- also with integer weights
+    (ties at bucket boundaries) and on a directed graph (where the pull is never used)."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = _rmat(13, 16, 5, weighted=True)
+    s = _src(g)
+    np.testing.assert_array_equal(gpu_run(ctx, g, "SSSP", source=s), O.sssp(g.csr, s))
+    rng = np.random.default_rng(11)
+    n = 5000
+    a = rng.integers(0, n, 60000)
+    b = rng.integers(0, n, 60000)
+    a, b = np.unique(np.stack([np.minimum(a, b), np.maximum(a, b)]), axis=1)   # one weight per edge
+    w = rng.integers(1, 8, len(a)).astype(np.float64)
+    csr = csr_from_edges(n, a, b, w, symmetric=True)
+    np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "SSSP", source=0), O.sssp(csr, 0))
+    gd = _rmat(12, 8, 6, undirected=False, weighted=True)
+    s = _src(gd)
+    np.testing.assert_array_equal(gpu_run(ctx, gd, "SSSP", source=s), O.sssp(gd.csr, s))
