@@ -102,12 +102,14 @@ __device__ __forceinline__ bool claim(int32_t *stamp, int32_t tag) {
     return __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag && atomicExch(stamp, tag) != tag;
 }
 
+constexpr int kStatLanes = 256;
 // stats slots: 0 items, 1 edges scanned, 2 relaxations tried, 3 improvements, 4 near pushes,
 // 5 ring pushes, 6 overflow pushes, 7 bucket entries skipped as already relaxed
 __device__ __forceinline__ void wave_count(unsigned long long *stats, int slot, unsigned long long x) {
     if (!stats) return;
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
-    if ((threadIdx.x & (kWave - 1)) == 0 && x) atomicAdd(&stats[slot], x);
+    // spread over kStatLanes words per counter: one shared word would serialise the grid
+    if ((threadIdx.x & (kWave - 1)) == 0 && x) atomicAdd(&stats[slot * kStatLanes + (blockIdx.x % kStatLanes)], x);
 }
 
 __device__ __forceinline__ void wave_min_to(unsigned long long m, unsigned long long *dst) {
@@ -129,7 +131,7 @@ __device__ __forceinline__ void wave_min_to(unsigned long long m, unsigned long 
 // one atomic (the lanes of one instruction, one queue each) and then writes the entries.
 // Mid-kernel flushes (a full stage) are per wave; the final one is per workgroup, so a launch
 // costs at most one atomic per queue per workgroup plus one per full stage.
-constexpr int kStage = 1024;
+constexpr int kStage = 512;
 constexpr int kTagNear = kRing, kTagOvf = kRing + 1;   // tags 0..kRing-1 are ring slots
 constexpr int kCats = 3 + kRing;                       // near items, settled, overflow, ring slots
 
@@ -339,6 +341,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
         list = B.settled;
         count = st->settled_cnt;
     }
+    if ((uint64_t)blockIdx.x * kSsspBlock >= count) return;   // no entry for this workgroup
     const int64_t cur = st->cur, win_base = st->win_base, lim = win_base + kRing;
     const int32_t epoch = st->epoch;
     const bool pull = mode == 3 && st->pull;
@@ -585,6 +588,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
     // a wave takes up to 64 items, fewer when the queue is short, so that small rounds (a
     // hub's chunks) spread over all waves instead of serialising in a few
     const uint32_t ipw = min((uint32_t)kWave, max(1u, (count + nwaves - 1) / nwaves));
+    if ((uint64_t)blockIdx.x * (kSsspBlock / kWave) * ipw >= count) return;   // no item for this workgroup
     for (uint64_t base = (uint64_t)wave * ipw; base < count; base += (uint64_t)nwaves * ipw) {
         const uint64_t idx = base + lane;
         int64_t rs = 0;
@@ -924,7 +928,9 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         }
         g->mean_w = mean;
     }
-    double delta = 0.0, scale = 20.0;
+    // measured on the SYN stand-ins: 5 for undirected graphs, whose big early
+    // buckets are pulled, 2 for directed ones
+    double delta = 0.0, scale = g->directed ? 2.0 : 5.0;
     if (const char *e = std::getenv("GX_SSSP_DELTA")) delta = std::atof(e);
     if (const char *e = std::getenv("GX_SSSP_DSCALE")) scale = std::atof(e);
     if (!(delta > 0.0)) {
@@ -936,8 +942,8 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     const bool verbose = std::getenv("GX_SSSP_VERBOSE") != nullptr;
     DBuf<unsigned long long> stats;
     if (verbose) {
-        GX_TRY(stats.alloc(8));
-        GX_HIP_TRY(hipMemsetAsync(stats.p, 0, 64, s));
+        GX_TRY(stats.alloc(8 * kStatLanes));
+        GX_HIP_TRY(hipMemsetAsync(stats.p, 0, 8 * kStatLanes * sizeof(unsigned long long), s));
     }
     GX_TRY(device_begin(ctx));
     {
@@ -990,12 +996,14 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
             hipLaunchKernelGGL(k_sssp_advance, dim3(grid), dim3(kSsspBlock), 0, s, B);
             hipLaunchKernelGGL(k_sssp_relax, dim3(grid), dim3(kSsspBlock), 0, s, B);
             GX_HIP_TRY(hipEventRecord(ev1, s));
-            unsigned long long c[8];
-            GX_HIP_TRY(hipMemcpyAsync(c, stats.p, 64, hipMemcpyDeviceToHost, s));
+            std::vector<unsigned long long> raw(8 * kStatLanes);
+            GX_HIP_TRY(hipMemcpyAsync(raw.data(), stats.p, raw.size() * sizeof(raw[0]), hipMemcpyDeviceToHost, s));
             GX_HIP_TRY(hipMemcpyAsync(&done, &st.p->done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
             GX_HIP_TRY(hipStreamSynchronize(s));
             float ms = 0.f;
             GX_HIP_TRY(hipEventElapsedTime(&ms, ev0, ev1));
+            unsigned long long c[8] = {};
+            for (int i = 0; i < 8 * kStatLanes; i++) c[i / kStatLanes] += raw[i];
             std::fprintf(stderr, "step %llu round %d bucket %lld mode %d heavy %d pull %d near %u settled %u | %.1f us "
                          "items %llu edges %llu improved %llu near %llu ring %llu\n",
                          (unsigned long long)steps, h.round, (long long)h.cur, h.mode, h.heavy, h.pull,
@@ -1029,8 +1037,10 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     if (verbose) {
         SsspState h;
         GX_HIP_TRY(hipMemcpy(&h, st.p, sizeof(h), hipMemcpyDeviceToHost));
-        unsigned long long c[8];
-        GX_HIP_TRY(hipMemcpy(c, stats.p, 64, hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> raw(8 * kStatLanes);
+        GX_HIP_TRY(hipMemcpy(raw.data(), stats.p, raw.size() * sizeof(raw[0]), hipMemcpyDeviceToHost));
+        unsigned long long c[8] = {};
+        for (int i = 0; i < 8 * kStatLanes; i++) c[i / kStatLanes] += raw[i];
         std::fprintf(stderr,
                      "gx_sssp: delta %g rounds %d last bucket %lld epochs %d launched steps %llu | items %llu edges "
                      "%llu tried %llu improved %llu near %llu ring %llu ovf %llu skipped %llu\n",
