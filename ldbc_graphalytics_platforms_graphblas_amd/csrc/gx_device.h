@@ -15,6 +15,7 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -125,6 +126,7 @@ struct SsspLayout {
     DBuf<double> w;
     DBuf<int64_t> lend;   // end of the light part of row v (absolute entry index)
     int64_t n_active = 0; // vertices with at least one edge
+    std::shared_ptr<void> work;   // gx_sssp's work buffers and captured step graph (gx_sssp.hip)
 };
 }  // namespace gx
 

@@ -249,3 +249,19 @@ def test_sssp_pull_heavy_phase(ctx, monkeypatch, env):
     gd = _rmat(12, 8, 6, undirected=False, weighted=True)
     s = _src(gd)
     np.testing.assert_array_equal(gpu_run(ctx, gd, "SSSP", source=s), O.sssp(gd.csr, s))
+
+
+@pytest.mark.parametrize("graph_replay", ["1", "0"])
+def test_sssp_repeated_runs_reuse_work_buffers(ctx, monkeypatch, graph_replay):
+    """Runs from several sources on one resident graph reuse the cached work buffers (and the
+    captured step graph): every run starts from a clean state."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    monkeypatch.setenv("GX_SSSP_GRAPH", graph_replay)
+    g = _rmat(12, 16, 7, weighted=True)
+    G = A.Graph(ctx, g.csr, g.directed)
+    try:
+        deg = np.diff(g.csr.rowptr.astype(np.int64))
+        for s in (int(np.argmax(deg)), 0, int(np.argmax(deg)), g.csr.n - 1):
+            np.testing.assert_array_equal(A.LA_SSSP(G, s), O.sssp(g.csr, s))
+    finally:
+        G.close()
