@@ -643,11 +643,19 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
                                            __builtin_amdgcn_raw_buffer_load_b64(
                                                dist_r, in_class ? (uint32_t)v[q] * 8u : kOob, 0, 0));
             }
+            // Improvements, then their dedup claims, each step issued for all slots before any
+            // result is used: the claims are memory-side round trips, and chaining them slot by
+            // slot serialised up to 4 x 2 of them per lane.
+            int cls[kSlots];       // 0 nothing, 1 near, 2 ring slot, 3 overflow
+            int32_t tag[kSlots];
+            int32_t *stp[kSlots];
+            int slot[kSlots];
 #pragma unroll
             for (int q = 0; q < kSlots; q++) {
-                bool to_near = false, to_ring = false, to_ovf = false, to_set = false;
-                int slot = 0;
-                uint32_t nch = 0;
+                cls[q] = 0;
+                tag[q] = 0;
+                stp[q] = B.near_stamp;
+                slot[q] = 0;
                 c_edges += act[q];
                 if (act[q]) {
                     c_try++;
@@ -662,33 +670,71 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
                         int64_t b = bucket_of(nd, B.inv_delta);
                         if (heavy && b <= cur) b = cur + 1;
                         if (b <= cur) {
-                            if (claim(&B.near_stamp[v[q]], rn)) {
-                                to_near = true;
-                                nch = chunks_of(B.lend[v[q]] - B.rp[v[q]]);
-                                to_set = claim(&B.sstamp[v[q]], cur32);
-                            }
+                            cls[q] = 1;
+                            stp[q] = B.near_stamp + v[q];
+                            tag[q] = rn;
                         } else if (b < lim) {
-                            if (claim(&B.bstamp[v[q]], (int32_t)b)) {
-                                to_ring = true;
-                                slot = (int)(b % kRing);
-                            }
+                            cls[q] = 2;
+                            stp[q] = B.bstamp + v[q];
+                            tag[q] = (int32_t)b;
+                            slot[q] = (int)(b % kRing);
                         } else {
-                            if (claim(&B.ostamp[v[q]], epoch)) to_ovf = true;
+                            cls[q] = 3;
+                            stp[q] = B.ostamp + v[q];
+                            tag[q] = epoch;
                             mymin = min(mymin, (unsigned long long)b);
                         }
                     }
                 }
+            }
+            // claim = a plain load that filters repeats, then the exchange that settles races
+            int32_t seen[kSlots];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++)
+                seen[q] = cls[q] ? __hip_atomic_load(stp[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag[q];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++)
+                if (seen[q] != tag[q]) seen[q] = atomicExch(stp[q], tag[q]);
+            bool won[kSlots];
+            int64_t rlo[kSlots], rhi[kSlots];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) {
+                won[q] = cls[q] != 0 && seen[q] != tag[q];
+                rlo[q] = rhi[q] = 0;
+                if (won[q] && cls[q] == 1) {
+                    rlo[q] = B.rp[v[q]];
+                    rhi[q] = B.lend[v[q]];
+                }
+            }
+            // near pushes also join the settled list, once per bucket
+            int32_t sset[kSlots];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++)
+                sset[q] = (won[q] && cls[q] == 1)
+                              ? __hip_atomic_load(&B.sstamp[v[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : cur32;
+            bool to_set[kSlots];
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) {
+                to_set[q] = false;
+                if (sset[q] != cur32) to_set[q] = atomicExch(&B.sstamp[v[q]], cur32) != cur32;
+            }
+#pragma unroll
+            for (int q = 0; q < kSlots; q++) {
+                const bool to_near = won[q] && cls[q] == 1, to_ring = won[q] && cls[q] == 2,
+                           to_ovf = won[q] && cls[q] == 3;
+                const uint32_t nch = to_near ? chunks_of(rhi[q] - rlo[q]) : 0u;
                 c_near += to_near;
                 c_ring += to_ring;
                 c_ovf += to_ovf;
-                const bool take = to_near | to_ring | to_ovf;
+                const bool take = won[q];
                 const uint64_t mask = __ballot(take);
                 if (mask == 0) continue;
                 if (take) {
                     const uint32_t pos = staged + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
                     sg.v[pos] = v[q];
-                    sg.tag[pos] = to_near ? ((uint32_t)kTagNear | (to_set ? 0x80u : 0u) | (nch << 8))
-                                          : (to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot);
+                    sg.tag[pos] = to_near ? ((uint32_t)kTagNear | (to_set[q] ? 0x80u : 0u) | (nch << 8))
+                                          : (to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot[q]);
                 }
                 staged += (uint32_t)__popcll(mask);
                 if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
