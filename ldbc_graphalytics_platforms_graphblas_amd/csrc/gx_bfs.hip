@@ -11,6 +11,8 @@
 //               neighbours at a time, until it meets a frontier vertex.
 // Direction switching follows Beamer's heuristic (alpha = 14, beta = 24).  Levels are
 // unique, so the result is bit-exact whatever the traversal order.
+#include <cstdlib>
+
 #include "gx_device.h"
 
 namespace gx {
@@ -241,7 +243,13 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     GX_TRY(qcount.alloc(1));
     GX_TRY(nedges.alloc(1));
     GX_TRY(device_begin(ctx));
-    // in-edges: the graph itself when undirected, the transpose when already resident
+    // in-edges: the graph itself when undirected; for a directed graph the transpose, built on
+    // the device by the first call and cached (GX_BFS_TRANSPOSE=0: top-down only unless another
+    // algorithm already built it)
+    if (g->directed && !g->AT.built) {
+        const char *e = std::getenv("GX_BFS_TRANSPOSE");
+        if (!(e && std::atoi(e) == 0)) GX_TRY(ensure_transpose(g));
+    }
     const DevCSR *in = g->directed ? (g->AT.built ? &g->AT : nullptr) : &g->A;
     GX_HIP_TRY(hipMemsetAsync(level.p, 0xff, n * 4, s));
     hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, qcount.p, (int32_t)src);
