@@ -244,11 +244,14 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     GX_TRY(nedges.alloc(1));
     GX_TRY(device_begin(ctx));
     // in-edges: the graph itself when undirected; for a directed graph the transpose, built on
-    // the device by the first call and cached (GX_BFS_TRANSPOSE=0: top-down only unless another
-    // algorithm already built it)
+    // the device and cached once the graph serves a second BFS (a one-off run, like the
+    // Graphalytics executable's, would not win back the build).  GX_BFS_TRANSPOSE = 0 never,
+    // 1 from the second run (default), 2 from the first.
+    g->bfs_calls++;
     if (g->directed && !g->AT.built) {
         const char *e = std::getenv("GX_BFS_TRANSPOSE");
-        if (!(e && std::atoi(e) == 0)) GX_TRY(ensure_transpose(g));
+        const int mode = e ? std::atoi(e) : 1;
+        if (mode == 2 || (mode == 1 && g->bfs_calls >= 2)) GX_TRY(ensure_transpose(g));
     }
     const DevCSR *in = g->directed ? (g->AT.built ? &g->AT : nullptr) : &g->A;
     GX_HIP_TRY(hipMemsetAsync(level.p, 0xff, n * 4, s));

@@ -138,6 +138,7 @@ struct gx_graph {
     gx::DBuf<int32_t> outdeg;   // out-degree of every vertex (PR)
     gx::PrPart *pr = nullptr;   // cached single-rank PageRank plan
     double mean_w = -1.0;       // cached mean edge weight (SSSP bucket width), < 0 = not yet computed
+    int bfs_calls = 0;          // BFS runs on this graph (a directed graph builds A^T from the second)
     gx::SsspLayout *sssp = nullptr;   // cached light/heavy edge layout
 };
 

@@ -265,3 +265,20 @@ def test_sssp_repeated_runs_reuse_work_buffers(ctx, monkeypatch, graph_replay):
             np.testing.assert_array_equal(A.LA_SSSP(G, s), O.sssp(g.csr, s))
     finally:
         G.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_bfs_directed_transpose_policy(ctx, monkeypatch, mode):
+    """Directed BFS: top-down only (0), bottom-up over the cached transpose from the second run
+    (1, default) or from the first (2) -- every run gives the oracle's levels."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    monkeypatch.setenv("GX_BFS_TRANSPOSE", mode)
+    for spec in ((13, 8, 21), (12, 4, 22)):
+        g = _rmat(*spec, undirected=False)
+        G = A.Graph(ctx, g.csr, g.directed)
+        try:
+            deg = np.diff(g.csr.rowptr.astype(np.int64))
+            for s in (int(np.argmax(deg)), 1, int(np.argmax(deg))):
+                np.testing.assert_array_equal(A.LA_BFS(G, s), O.bfs(g.csr, s))
+        finally:
+            G.close()
