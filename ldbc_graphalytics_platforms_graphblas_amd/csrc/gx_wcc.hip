@@ -9,11 +9,11 @@
 //              followed by pointer jumping;
 //   giant    : the most frequent root among 1024 hashed vertices;
 //   finish   : one wave per vertex outside the giant component links its remaining neighbours.
-// Directed graphs (an edge is seen from one endpoint only):
-//   hook     : edge-balanced (one chunk of kEdgesPerThread entries per thread); the roots
-//              ru, rv of both endpoints are found by following parent pointers and the larger
-//              root is hooked below the smaller one with atomicMin; repeated until no change.
-//   compress : pointer jumping until every vertex points at its root.
+// Directed graphs (an edge is seen from one endpoint only): the same two sampling rounds over
+//   out-neighbours, then one edge-balanced pass (kWccEdgesPerThread entries per thread) links
+//   every remaining entry with the CAS link -- no vertex can be skipped -- and pointer
+//   jumping until every vertex points at its root.  (Min-label hooking repeated until no
+//   change took 2.48 ms on SYN-cit.)
 // parent[v] <= v always holds, so the root of each final tree is the smallest vertex index
 // of the component: comp[v] is canonical and equals the oracle's union-find labels exactly.
 #include <algorithm>
@@ -33,29 +33,6 @@ __device__ __forceinline__ int32_t find_root(const int32_t *parent, int32_t v) {
         p = parent[v];
     }
     return v;
-}
-
-__global__ __launch_bounds__(kWccBlock) void k_wcc_hook(const int64_t *__restrict__ rp,
-                                                        const int32_t *__restrict__ ci, int64_t n,
-                                                        int64_t nnz, int32_t *parent, int *changed) {
-    const int64_t t = (int64_t)blockIdx.x * kWccBlock + threadIdx.x;
-    const int64_t e0 = t * kWccEdgesPerThread;
-    bool any = false;
-    if (e0 < nnz) {
-        const int64_t e1 = min(e0 + kWccEdgesPerThread, nnz);
-        int64_t r = row_of_edge(rp, n, e0);
-        for (int64_t e = e0; e < e1; e++) {
-            while (rp[r + 1] <= e) r++;
-            int32_t ru = find_root(parent, (int32_t)r);
-            int32_t rv = find_root(parent, ci[e]);
-            if (ru != rv) {
-                const int32_t hi = max(ru, rv), lo = min(ru, rv);
-                atomicMin(&parent[hi], lo);
-                any = true;
-            }
-        }
-    }
-    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag(changed);
 }
 
 __global__ __launch_bounds__(kWccBlock) void k_wcc_compress(int32_t *parent, int64_t n) {
@@ -114,6 +91,24 @@ __global__ __launch_bounds__(kWccBlock) void k_afforest_finish(const int64_t *__
     }
 }
 
+// Directed graphs: an edge is stored at its source only, so no vertex may skip its row (the
+// giant-component shortcut above relies on seeing every edge from both ends).  After the two
+// sampling rounds, one edge-balanced pass links every remaining entry (row position >= 2):
+// Afforest's CAS link is a complete concurrent union, so one pass suffices.
+__global__ __launch_bounds__(kWccBlock) void k_wcc_link_edges(const int64_t *__restrict__ rp,
+                                                              const int32_t *__restrict__ ci, int64_t n,
+                                                              int64_t nnz, int skip, int32_t *parent) {
+    const int64_t t = (int64_t)blockIdx.x * kWccBlock + threadIdx.x;
+    const int64_t e0 = t * kWccEdgesPerThread;
+    if (e0 >= nnz) return;
+    const int64_t e1 = min(e0 + kWccEdgesPerThread, nnz);
+    int64_t r = row_of_edge(rp, n, e0);
+    for (int64_t e = e0; e < e1; e++) {
+        while (rp[r + 1] <= e) r++;
+        if (e - rp[r] >= skip) link(parent, (int32_t)r, ci[e]);
+    }
+}
+
 __global__ void k_sample_roots(const int32_t *parent, const int32_t *__restrict__ ids, int m, int32_t *roots) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x)
         roots[i] = find_root(parent, ids[i]);
@@ -138,9 +133,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
     const int64_t n = (int64_t)g->n, nnz = (int64_t)g->nnz;
     if (n == 0) return GX_SUCCESS;
     DBuf<int32_t> parent;
-    DBuf<int> changed;
     GX_TRY(parent.alloc(n));
-    GX_TRY(changed.alloc(1));
     GX_TRY(device_begin(ctx));
     hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, parent.p, n);
     GX_TRY(check_launch("k_iota"));
@@ -201,27 +194,33 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         }
         GX_TRY(check_launch("k_wcc_compress"));
     }
-    const unsigned hook_grid =
-        grid_for((uint64_t)((nnz + kWccEdgesPerThread - 1) / kWccEdgesPerThread), kWccBlock, 1u << 30);
-    for (int round = 0; g->directed; round++) {
-        int h_changed = 0;
-        GX_HIP_TRY(hipMemsetAsync(changed.p, 0, sizeof(int), s));
-        if (nnz) {
-            KTimer kt(ctx, "wcc_hook", s);
-            hipLaunchKernelGGL(k_wcc_hook, dim3(hook_grid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
-                               nnz, parent.p, changed.p);
+    if (g->directed && nnz) {
+        for (int r = 0; r < 2; r++) {
+            {
+                KTimer kt(ctx, "wcc_sample", s);
+                hipLaunchKernelGGL(k_afforest_sample, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, r,
+                                   parent.p);
+            }
+            GX_TRY(check_launch("k_afforest_sample"));
+            {
+                KTimer kt(ctx, "wcc_compress", s);
+                hipLaunchKernelGGL(k_wcc_compress, dim3(vgrid), dim3(kWccBlock), 0, s, parent.p, n);
+            }
+            GX_TRY(check_launch("k_wcc_compress"));
         }
-        GX_TRY(check_launch("k_wcc_hook"));
+        {
+            KTimer kt(ctx, "wcc_hook", s);
+            hipLaunchKernelGGL(k_wcc_link_edges,
+                               dim3(grid_for((uint64_t)((nnz + kWccEdgesPerThread - 1) / kWccEdgesPerThread),
+                                             kWccBlock, 1u << 30)),
+                               dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, nnz, 2, parent.p);
+        }
+        GX_TRY(check_launch("k_wcc_link_edges"));
         {
             KTimer kt(ctx, "wcc_compress", s);
-            hipLaunchKernelGGL(k_wcc_compress, dim3(grid_for(n, kWccBlock, 8192)), dim3(kWccBlock), 0, s,
-                               parent.p, n);
+            hipLaunchKernelGGL(k_wcc_compress, dim3(vgrid), dim3(kWccBlock), 0, s, parent.p, n);
         }
         GX_TRY(check_launch("k_wcc_compress"));
-        GX_HIP_TRY(hipMemcpyAsync(&h_changed, changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
-        GX_HIP_TRY(hipStreamSynchronize(s));
-        if (!h_changed) break;
-        if (round > 100000) return fail(GX_PANIC, "gx_wcc: hooking did not converge");
     }
     GX_TRY(device_end(ctx));
     GX_TRY(download(ctx, comp, parent.p, (uint64_t)n, Xfer::Widen32));

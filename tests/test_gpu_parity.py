@@ -282,3 +282,18 @@ def test_bfs_directed_transpose_policy(ctx, monkeypatch, mode):
                 np.testing.assert_array_equal(A.LA_BFS(G, s), O.bfs(g.csr, s))
         finally:
             G.close()
+
+
+def test_wcc_directed_sparse_many_components(ctx):
+    """Directed WCC (sampling + one link pass): sparse R-MAT graphs with many components, and
+    chains whose edges all point away from the component minimum (seen from one end only)."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    for spec in ((14, 2, 31), (13, 1, 32), (15, 4, 33)):
+        g = _rmat(*spec, undirected=False)
+        np.testing.assert_array_equal(gpu_run(ctx, g, "WCC"), O.wcc(g.csr))
+    n = 20000
+    perm = np.random.default_rng(5).permutation(n)
+    src, dst = perm[1:], perm[:-1]          # one long chain in random id order
+    keep = np.arange(n - 1) % 97 != 0        # cut into ~200 components
+    csr = csr_from_edges(n, src[keep], dst[keep], None, symmetric=False)
+    np.testing.assert_array_equal(gpu_run(ctx, _G(csr, True), "WCC"), O.wcc(csr))
