@@ -332,3 +332,5 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     GX_TRY(download(ctx, level_out, level.p, (uint64_t)n, Xfer::Levels));
     return GX_SUCCESS;
 }
+
+GX_MODULE_WARMER(bfs)

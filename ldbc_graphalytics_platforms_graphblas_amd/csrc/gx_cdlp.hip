@@ -694,3 +694,5 @@ extern "C" int gx_cdlp_part_free(gx_cdlp_part *part) {
     delete part;
     return GX_SUCCESS;
 }
+
+GX_MODULE_WARMER(cdlp)

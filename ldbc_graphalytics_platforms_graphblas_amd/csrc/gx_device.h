@@ -276,3 +276,28 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 }  // namespace gx
+
+// Module warm-up.  HIP loads a translation unit's code object on the first launch of one of
+// its kernels (about 20 ms for gx_runtime.hip with its rocprim sorts): gx_init launches one
+// empty kernel per .hip file, so that cost stays out of an algorithm's processing time, like
+// the fill/copy warm-up there.
+#define GX_MODULE_WARMER(name)                                                           \
+    namespace gx {                                                                       \
+    __global__ void warm_kernel_##name() {}                                              \
+    hipError_t warm_##name(hipStream_t s) {                                              \
+        hipLaunchKernelGGL(warm_kernel_##name, dim3(1), dim3(1), 0, s);                 \
+        return hipGetLastError();                                                        \
+    }                                                                                    \
+    }
+namespace gx {
+hipError_t warm_bfs(hipStream_t s);
+hipError_t warm_cdlp(hipStream_t s);
+hipError_t warm_lcc(hipStream_t s);
+hipError_t warm_part(hipStream_t s);
+hipError_t warm_pr(hipStream_t s);
+hipError_t warm_pr_hub(hipStream_t s);
+hipError_t warm_pr_sorted(hipStream_t s);
+hipError_t warm_runtime(hipStream_t s);
+hipError_t warm_sssp(hipStream_t s);
+hipError_t warm_wcc(hipStream_t s);
+}  // namespace gx

@@ -655,3 +655,5 @@ extern "C" int gx_lcc_part_free(gx_lcc_part *part) {
     delete part;
     return GX_SUCCESS;
 }
+
+GX_MODULE_WARMER(lcc)

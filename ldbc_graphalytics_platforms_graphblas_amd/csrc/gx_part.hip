@@ -258,3 +258,5 @@ extern "C" int gx_sssp_part_round(gx_graph *g, uint64_t v0, uint64_t v1, uint64_
                            g->A.rp.p, g->A.ci.p, g->A.w.p, (int64_t)v0, (int64_t)v1, flag, p, d);
     return check_launch("k_ssspp_relax");
 }
+
+GX_MODULE_WARMER(part)

@@ -689,3 +689,5 @@ extern "C" int gx_pr_part_free(gx_pr_part *part) {
     delete p;
     return GX_SUCCESS;
 }
+
+GX_MODULE_WARMER(pr)

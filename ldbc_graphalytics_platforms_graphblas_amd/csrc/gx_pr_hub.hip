@@ -387,3 +387,5 @@ int pr_step_hub(PrPart *p, const double *x_full, double *x_local, double *rank_o
 }
 
 }  // namespace gx
+
+GX_MODULE_WARMER(pr_hub)

@@ -704,3 +704,5 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
 }
 
 }  // namespace gx
+
+GX_MODULE_WARMER(pr_sorted)

@@ -1174,3 +1174,5 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     GX_TRY(download(ctx, dist_out, dist.p, (uint64_t)n, Xfer::Raw64));
     return GX_SUCCESS;
 }
+
+GX_MODULE_WARMER(sssp)

@@ -226,3 +226,5 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
     GX_TRY(download(ctx, comp, parent.p, (uint64_t)n, Xfer::Widen32));
     return GX_SUCCESS;
 }
+
+GX_MODULE_WARMER(wcc)
