@@ -55,6 +55,42 @@ __device__ __forceinline__ uint32_t hash_slot(uint32_t l, int log2ts) {
     return (l * 2654435761u) >> (32 - log2ts);
 }
 
+// Adds `c` occurrences of label l to an open-addressing LDS table of 2^log2ts slots.
+__device__ __forceinline__ void lds_table_add(uint32_t *K, uint32_t *C, uint32_t l, uint32_t c, int log2ts) {
+    const uint32_t mask = (1u << log2ts) - 1u;
+    uint32_t h = hash_slot(l, log2ts);
+    for (;;) {
+        const uint32_t prev = atomicCAS(&K[h], kEmpty, l);
+        if (prev == kEmpty || prev == l) {
+            atomicAdd(&C[h], c);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+// Wave-uniform call (every lane of the wave reaches it; `valid` marks lanes holding a label).
+// In each of kPeel rounds, the lanes whose label equals the first remaining lane's go in as
+// one add of their count. The wave's most repeated labels - the common case once CDLP's labels
+// start to agree - then do not serialise up to 64 same-address LDS atomics. The other lanes
+// insert one at a time.
+template <int kPeel = 1>
+__device__ __forceinline__ void lds_table_add_wave(uint32_t *K, uint32_t *C, uint32_t l, bool valid, int log2ts) {
+    const int lane = (int)(threadIdx.x & (kWave - 1));
+#pragma unroll
+    for (int r = 0; r < kPeel; r++) {
+        const unsigned long long act = __ballot(valid);
+        if (!act) return;
+        const int first = __ffsll((long long)act) - 1;
+        const uint32_t lead = __shfl(l, first, kWave);
+        const bool same = valid && l == lead;
+        const unsigned long long grp = __ballot(same);
+        if (lane == first) lds_table_add(K, C, lead, (uint32_t)__popcll(grp), log2ts);
+        valid = valid && !same;
+    }
+    if (valid) lds_table_add(K, C, l, 1u, log2ts);
+}
+
 __device__ __forceinline__ unsigned long long pack(uint32_t count, uint32_t label) {
     return ((unsigned long long)count << 32) | (unsigned long long)(kEmpty - label);
 }
@@ -183,17 +219,11 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int64_t k = lane; k < d; k += kWave) {
-                const uint32_t l = (uint32_t)label_at(a, ob, od, ib, k);
-                uint32_t h = hash_slot(l, log2ts);
-                for (;;) {
-                    const uint32_t prev = atomicCAS(&K[h], kEmpty, l);
-                    if (prev == kEmpty || prev == l) {
-                        atomicAdd(&C[h], 1u);
-                        break;
-                    }
-                    h = (h + 1) & (ts - 1);
-                }
+            for (int64_t k0 = 0; k0 < d; k0 += kWave) {
+                const int64_t k = k0 + lane;
+                const bool valid = k < d;
+                const uint32_t l = valid ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
+                lds_table_add_wave(K, C, l, valid, log2ts);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -251,17 +281,11 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
         C[s] = 0;
     }
     __syncthreads();
-    for (int64_t k = k0 + tid; k < k1; k += kHugeBlock) {
-        const uint32_t l = (uint32_t)label_at(a, ob, od, ib, k);
-        uint32_t h = hash_slot(l, kLog2);
-        for (;;) {
-            const uint32_t prev = atomicCAS(&K[h], kEmpty, l);
-            if (prev == kEmpty || prev == l) {
-                atomicAdd(&C[h], 1u);
-                break;
-            }
-            h = (h + 1) & (kHugeSlots - 1);
-        }
+    for (int64_t kb = k0; kb < k1; kb += kHugeBlock) {
+        const int64_t k = kb + tid;
+        const bool valid = k < k1;
+        const uint32_t l = valid ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
+        lds_table_add_wave(K, C, l, valid, kLog2);
     }
     __syncthreads();
     const int log2ts = hlog2[hi];
@@ -376,17 +400,11 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
             C[s] = 0;
         }
         __syncthreads();
-        for (int64_t k = tid; k < d; k += kMidBlock) {
-            const uint32_t l = (uint32_t)label_at(a, ob, od, ib, k);
-            uint32_t h = hash_slot(l, log2ts);
-            for (;;) {
-                const uint32_t prev = atomicCAS(&K[h], kEmpty, l);
-                if (prev == kEmpty || prev == l) {
-                    atomicAdd(&C[h], 1u);
-                    break;
-                }
-                h = (h + 1) & (ts - 1);
-            }
+        for (int64_t k0 = 0; k0 < d; k0 += kMidBlock) {
+            const int64_t k = k0 + tid;
+            const bool valid = k < d;
+            const uint32_t l = valid ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
+            lds_table_add_wave(K, C, l, valid, log2ts);
         }
         __syncthreads();
         unsigned long long key = 0;
