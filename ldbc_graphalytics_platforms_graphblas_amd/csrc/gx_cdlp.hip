@@ -11,7 +11,8 @@
 // are written (cdlp_kernel.cu:108-112, 1060-1063).
 //   deg <= 16        : one thread per vertex, labels and counts in registers.
 //   deg <= 64        : one wave per vertex, labels in registers, counts by 64 shuffles.
-//   deg <= kLdsHash/2: one wave per vertex, open-addressing hash table in that wave's LDS.
+//   deg <= kLdsHash/2: one wave per vertex, open-addressing hash table in that wave's LDS
+//   (kLightSlots slots for deg <= kLightSlots/2, kLdsHash slots above).
 //   deg <= 2048      : one 256-thread workgroup per vertex, 4K-slot LDS table (4 per CU).
 //   deg <= 4096      : one 512-thread workgroup per vertex, 8K-slot LDS table (2 per CU).
 //   deg <= 8192      : one 1024-thread workgroup per vertex, 16K-slot hash table in LDS
@@ -32,6 +33,7 @@ namespace {
 
 constexpr int kCdlpBlock = 256;
 constexpr int kLdsHash = 1024;   // slots per wave (8 KiB per wave of int32 key + int32 count)
+constexpr int kLightSlots = 256; // slots per wave for light vertices of degree <= 128
 constexpr uint32_t kEmpty = 0xffffffffu;
 
 struct CdlpArgs {
@@ -177,11 +179,14 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
     if (any) raise_flag(a.changed);
 }
 
-// Light vertices (64 < deg <= kLdsHash/2), from a list: one wave per vertex.
+// Light vertices (64 < deg <= kSlots/2), from a list: one wave per vertex. Two instances:
+// kLightSlots for deg <= kLightSlots/2 (2 KiB per wave, so LDS does not cap occupancy) and
+// kLdsHash for the rest.
+template <int kSlots>
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int32_t *__restrict__ lv,
                                                            int32_t nlight) {
-    __shared__ uint32_t keys[kCdlpBlock / kWave][kLdsHash];
-    __shared__ uint32_t cnts[kCdlpBlock / kWave][kLdsHash];
+    __shared__ uint32_t keys[kCdlpBlock / kWave][kSlots];
+    __shared__ uint32_t cnts[kCdlpBlock / kWave][kSlots];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     uint32_t *K = keys[wv];
@@ -443,7 +448,8 @@ struct CdlpPlan {
     size_t n_light = 0, n_mid2 = 0, n_mid = 0, n_huge = 0, n_chunks = 0;
     int64_t total = 0;
     DBuf<int32_t> d_hv, d_hl, d_mv, d_cvert, d_lv, d_mv2, d_sv, d_mv4;
-    size_t n_small = 0, n_mid4 = 0;
+    size_t n_small = 0, n_mid4 = 0, n_light_s = 0;
+    DBuf<int32_t> d_lvs;                // light vertices with degree <= kLightSlots / 2
     DBuf<int64_t> d_hoff, d_cbeg;
     DBuf<uint32_t> gk, gc;
     DBuf<unsigned long long> vkey;      // per huge vertex best key (zero between iterations)
@@ -453,7 +459,7 @@ struct CdlpPlan {
 };
 
 int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
-    std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv, mv4;
+    std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv, mv4, lvs;
     std::vector<int64_t> hoff, cbeg;
     int64_t total = 0;
     for (int64_t v = v0; v < v1; v++) {
@@ -463,6 +469,8 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
             // k_cdlp_tiny scans the range itself
         } else if (d <= kWave) {
             sv.push_back((int32_t)v);
+        } else if (d <= kLightSlots / 2) {
+            lvs.push_back((int32_t)v);
         } else if (d <= kLdsHash / 2) {
             lv.push_back((int32_t)v);
         } else if (d <= kMid2Max) {
@@ -487,6 +495,7 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
     P.v0 = v0;
     P.v1 = v1;
     P.n_light = lv.size();
+    P.n_light_s = lvs.size();
     P.n_small = sv.size();
     P.n_mid4 = mv4.size();
     if (!mv4.empty()) {
@@ -543,6 +552,10 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
         GX_TRY(P.d_mv2.alloc(mv2.size()));
         GX_HIP_TRY(hipMemcpyAsync(P.d_mv2.p, mv2.data(), mv2.size() * 4, hipMemcpyHostToDevice, s));
     }
+    if (!lvs.empty()) {
+        GX_TRY(P.d_lvs.alloc(lvs.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_lvs.p, lvs.data(), lvs.size() * 4, hipMemcpyHostToDevice, s));
+    }
     if (!lv.empty()) {
         GX_TRY(P.d_lv.alloc(lv.size()));
         GX_HIP_TRY(hipMemcpyAsync(P.d_lv.p, lv.data(), lv.size() * 4, hipMemcpyHostToDevice, s));
@@ -570,9 +583,15 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
                            dim3(kCdlpBlock), 0, s, a, P.d_sv.p, (int32_t)P.n_small);
         GX_TRY(check_launch("k_cdlp_small"));
     }
+    if (P.n_light_s) {
+        KTimer kt(ctx, "cdlp_light_s", s);
+        hipLaunchKernelGGL(k_cdlp_light<kLightSlots>, dim3(grid_for((uint64_t)P.n_light_s * kWave, kCdlpBlock, 8192)),
+                           dim3(kCdlpBlock), 0, s, a, P.d_lvs.p, (int32_t)P.n_light_s);
+        GX_TRY(check_launch("k_cdlp_light_s"));
+    }
     if (P.n_light) {
         KTimer kt(ctx, "cdlp_light", s);
-        hipLaunchKernelGGL(k_cdlp_light, dim3(grid_for((uint64_t)P.n_light * kWave, kCdlpBlock, 8192)),
+        hipLaunchKernelGGL(k_cdlp_light<kLdsHash>, dim3(grid_for((uint64_t)P.n_light * kWave, kCdlpBlock, 8192)),
                            dim3(kCdlpBlock), 0, s, a, P.d_lv.p, (int32_t)P.n_light);
         GX_TRY(check_launch("k_cdlp_light"));
     }
