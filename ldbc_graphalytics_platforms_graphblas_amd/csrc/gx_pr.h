@@ -36,6 +36,23 @@ struct WaveItem {
     int32_t pad;
 };
 
+// One workgroup's share of a column-sorted block (k_pr_pull_units, gx_pr_sorted.hip): the
+// sorted entries [lo, hi) of block `blk` in rounds of the kernel's U * BS entries, taking
+// every (step / (U * BS))-th round (interleaved units: every unit sweeps the block's whole
+// column range, so the units of a block move through x together).  A block cut into
+// nunits > 1 units sums its rows through per-unit partial slabs (slab + unit * rows doubles);
+// the last unit to arrive (ticket[part]) adds them in unit order and runs the epilogue.
+struct SortedUnit {
+    int64_t lo;
+    int64_t hi;
+    int64_t step;
+    int64_t slab;       // first double of the block's slabs in PrPart::uslab
+    int32_t blk;        // index into PrPart::blocks
+    int32_t part;       // ticket index of a multi-unit block, -1 when nunits == 1
+    int32_t unit;       // this unit's number within the block
+    int32_t nunits;
+};
+
 constexpr int kHubBlock = 1024;       // one 16-wave workgroup per CU
 constexpr int kItemNnz = 2048;        // entries per wave item
 constexpr int kItemRows = 512;        // rows per wave item
@@ -85,6 +102,14 @@ struct PrPart {
     DBuf<uint32_t> gbase;        // base column per 64-entry group (bit 31: escape to sci)
     int sorted_nnz = 65536;      // entries per block
     int sorted_rows = 4096;      // rows per block (LDS accumulators)
+    bool units_mode = false;     // split blocks (k_pr_pull_units)
+    int64_t unit_nnz = 0;        // target entries per unit
+    DBuf<SortedUnit> units;      // one-pass mode: one workgroup per unit, after the LONG blocks
+    uint32_t nunits = 0;
+    DBuf<double> uslab;          // partial row sums of the multi-unit blocks
+    DBuf<uint32_t> uticket;      // per multi-unit block: arrivals of the current iteration
+    DBuf<uint64_t> utimes;       // debug (GX_PR_UNIT_TIMES): per-workgroup timestamps
+    int utimes_launch = 0;
     int long_nnz = 65536;        // longer rows take the LONG segment path
     int sorted_lds = 0;          // dynamic LDS bytes of the launch
     int sorted_variant = 0;      // tuning: block size / gathers in flight (gx_pr_sorted.hip)

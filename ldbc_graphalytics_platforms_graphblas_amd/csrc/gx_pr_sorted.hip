@@ -33,6 +33,7 @@
 // segment of the row, segments combined by the last arriver) in the hub pass; their blocks
 // come first.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -70,6 +71,11 @@ struct SortedArgs {
     double *dpart;
     uint32_t *dticket;
     uint32_t ndblocks;
+    // split blocks (k_pr_pull_units)
+    const SortedUnit *units;
+    double *uslab;
+    uint32_t *uticket;
+    uint64_t *utimes;        // debug (GX_PR_UNIT_TIMES): per workgroup start, gather end, end, XCC
 };
 
 // Returns the row's score if the row is dangling (out-degree 0), else 0.
@@ -183,9 +189,11 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 
 // Adds x(column) of the sorted entries [lo, hi) of block b into the LDS row accumulators
 // (the loop starts at the 64-entry group holding lo, so wave-instructions stay group-aligned).
+// `step` (a multiple of U * BS) > U * BS: only every (step / (U * BS))-th round of U * BS
+// entries, from the one at lo (interleaved units of a split block).
 template <int BS, int U, bool PIPE>
 __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock &b, int64_t lo, int64_t hi,
-                                             double *acc) {
+                                             double *acc, int64_t step = (int64_t)U * BS) {
     const int tid = threadIdx.x;
     const int64_t z0 = b.nz_begin, z1 = b.nz_end;
     if (lo < hi) {
@@ -205,7 +213,7 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
         };
         int64_t k0 = start + tid;
         if (PIPE) load_round(k0);
-        for (; k0 < hi; k0 += (int64_t)U * BS) {
+        for (; k0 < hi; k0 += step) {
             if (!PIPE) load_round(k0);
             int32_t c[U];
             uint32_t r[U];
@@ -224,7 +232,7 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
             double g[U];
 #pragma unroll
             for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
-            if (PIPE) load_round(k0 + (int64_t)U * BS);
+            if (PIPE) load_round(k0 + step);
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const int64_t e = k0 + (int64_t)u * BS;
@@ -279,6 +287,93 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
     if (PASS == 2) return;   // LONG rows are complete after the hub pass
 
     long_segment<BS, U>(a, b, wred, teleport, nullptr, 0, 0);
+}
+
+// One-pass SpMV over split blocks.  Why split: a wave-instruction's gather costs one L2
+// request per distinct x line among its 64 sorted columns, so the more entries a block sorts
+// together, the more of them share a line (tools/pr_line_model.py on SYN-7_5: 12.8 M requests
+// per launch with 64 Ki-entry blocks, 5.0 M with 512 Ki).  A block that large would leave too
+// few workgroups for 256 CUs, so its sorted entries are cut into units of <= sorted_nnz
+// entries (whole 64-entry groups), one workgroup each, all with LDS accumulators for every
+// row of the block.  A multi-unit block's units store their row sums write-through (sc1) to
+// their own slab, drain them (vmcnt(0)) and take a ticket; the last arriver adds the slabs in
+// unit order with sc1 loads and runs the epilogue (MI355X_MICROARCH.md "Valid forms": sc1
+// stores drained before the counter add, sc1 loads by the workgroup whose add came last).
+// Workgroups [0, nlong) are the LONG row segments, as in k_pr_pull_sorted, padded to nlong_pad
+// (a multiple of 8, so that grid slot nlong_pad + 8 i + x lands on XCD list x).
+// TIMES: debug build with per-workgroup timestamps (GX_PR_UNIT_TIMES).
+template <int BS, int U, bool TIMES>
+__global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? 8 : 1)) void k_pr_pull_units(SortedArgs a) {   // 1024: two per CU
+    extern __shared__ double acc[];
+    __shared__ double wred[BS / kWave];
+    __shared__ int last;
+
+    const uint32_t w = blockIdx.x;
+    const int tid = threadIdx.x;
+    __shared__ uint64_t ts[2];   // TIMES: start, gather end (LDS, so no registers are held)
+    if (TIMES && tid == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
+    auto stamp = [&]() {
+        if (TIMES && tid == 0) {
+            a.utimes[4 * w + 0] = ts[0];
+            a.utimes[4 * w + 1] = ts[1];
+            a.utimes[4 * w + 2] = __builtin_amdgcn_s_memrealtime();
+            a.utimes[4 * w + 3] = (uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);   // HW_REG_XCC_ID[3:0]
+        }
+    };
+    double dsum = 0.0;
+    for (int k = 0; k < a.nranks; k++) dsum += a.x_in[(int64_t)k * a.chunk + a.chunk - 1];
+    const double teleport = a.teleport0 + a.damping_over_n * dsum;
+    if (a.zero_slot && w == 0 && tid == 0) a.x_out[a.chunk - 1] = 0.0;
+    if (w < a.nlong_pad) {
+        if (w < a.nlong) long_segment<BS, U>(a, a.blocks[w], wred, teleport, nullptr, 0, 0);
+        stamp();
+        return;
+    }
+    const SortedUnit u = a.units[w - a.nlong_pad];
+    if (u.blk < 0) return;   // padding of an XCD list
+    const RowBlock b = a.blocks[u.blk];
+    const int nrows = b.row_end - b.row_begin;
+    for (int i = tid; i < nrows; i += BS) acc[i] = 0.0;
+    __syncthreads();
+    gather_range<BS, U, true>(a, b, u.lo, u.hi, acc, u.step);
+    __syncthreads();
+    if (TIMES && tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
+    if (u.nunits > 1) {
+        double *mine = a.uslab + u.slab + (int64_t)u.unit * nrows;
+        for (int i = tid; i < nrows; i += BS)
+            __hip_atomic_store(&mine[i], acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t t = __hip_atomic_fetch_add(&a.uticket[u.part], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = t == (uint32_t)(u.nunits - 1);
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&a.uticket[u.part], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        if (!last) {
+            stamp();
+            return;
+        }
+        const double *slabs = a.uslab + u.slab;
+        for (int i = tid; i < nrows; i += BS) {
+            double s = 0.0;
+            for (int j = 0; j < u.nunits; j++)
+                s += __hip_atomic_load(&slabs[(int64_t)j * nrows + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            acc[i] = s;
+        }
+        // each thread reads back only the acc entries it wrote: no barrier needed
+    }
+    double d = 0.0;
+    for (int i = tid; i < nrows; i += BS) d += sorted_epilogue(a, b.row_begin + i, acc[i], teleport);
+    if (a.dslot) {
+        const int32_t slot = a.dslot[u.blk];
+        if (slot >= 0) dangling_publish<BS>(a, slot, d, wred, &last);
+    }
+    stamp();
 }
 
 // XCD slices: the columns are cut into S ranges holding equal shares of the entries, and the
@@ -452,21 +547,6 @@ void launch_sliced(const PrPart *p, const SortedArgs &a, hipStream_t s) {
 int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vector<int32_t> &h_outdeg) {
     const int64_t rows = (int64_t)h_rp.size() - 1;
     const uint64_t nnz = (uint64_t)h_rp[rows];
-    // entries per block: GX_PR_SORTED_NNZ, else 65536 -- 32768 when the partition gives fewer
-    // than one block per CU (the 1/4 and 1/8 partitions of SYN-7_5 ran best at 32 Ki: 35 us vs
-    // 37 at 16 Ki and 67 at 64 Ki for 1/8), or doubled up to 1 Mi while it gives more than four
-    // per CU: large blocks merge more hub rows into one sorted sweep (SYN-7_5 best at 64 Ki,
-    // graph500-22 at 128 Ki, SYN-8_5 at 1 Mi: 252 -> 419 G edges/s, tools/pr_sorted_sweep.sh)
-    int64_t B = p->sorted_nnz;
-    if (std::getenv("GX_PR_SORTED_NNZ")) {
-        B = env_int("GX_PR_SORTED_NNZ", p->sorted_nnz, 1024, 1 << 22);
-    } else {
-        const int64_t cus = std::max(1, p->ctx->num_cus);
-        while (B > 32768 && (int64_t)nnz < B * cus) B >>= 1;
-        while (B < (1 << 20) && (int64_t)nnz > 4 * B * cus) B <<= 1;
-    }
-    p->sorted_nnz = (int)B;
-    p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)B, 1024, 1 << 24);
     p->sorted_rows = env_int("GX_PR_SORTED_ROWS", p->sorted_rows, 64, 4096);   // 12-bit rows, LDS <= 32 KiB
     // GX_PR_SORTED_VARIANT = 0 (1024 threads, 8 gathers in flight per lane, entry loads
     // pipelined) | 1 (1024, 8, not pipelined) | 2 (512, 16, pipelined) | 3 (512, 8, pipelined)
@@ -479,6 +559,42 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     p->slices = env_int("GX_PR_SLICES", p->slices, 1, 8);
     if (8 % p->slices) p->slices = 1;
     if (p->two_pass) p->slices = 1;
+    const int64_t cus = std::max(1, p->ctx->num_cus);
+    // Split blocks (k_pr_pull_units; one pass, pipelined variants): sorted blocks of up to
+    // block_nnz = 4 T entries, each cut into units of at most T entries (interleaved rounds),
+    // one workgroup each; rows longer than T take the LONG path.  T = the power of two
+    // nearest nnz / CUs, clamped to [16 Ki, 1 Mi] (GX_PR_UNIT_NNZ, GX_PR_BLOCK_NNZ,
+    // GX_PR_LONG_NNZ override).  Measured (tools/pr_units_sweep.sh, us per launch): SYN-7_5
+    // T = 256 Ki 100 (the round-1 64 Ki single-workgroup blocks: 140), 128 Ki 107, 192 Ki 129,
+    // 240 Ki 118; graph500-22 256 Ki / 512 Ki 269 / 272 (round 1: 384); SYN-8_5 1 Mi 1187 with
+    // 4 Mi blocks, 1155 with 8 Mi, 2 Mi 1229 (round 1: 1489).
+    p->units_mode = !p->two_pass && p->slices == 1 && p->sorted_variant != 1 && !std::getenv("GX_PR_SORTED_NNZ");
+    const int64_t round = p->sorted_variant == 3 ? 512 * 8 : 1024 * 8;   // U * BS of the launch
+    int64_t B, T = 0;
+    if (p->units_mode) {
+        const double per_cu = std::max(1.0, (double)nnz / (double)cus);
+        int64_t t = 1 << 14;
+        while (t < (1 << 20) && (double)(2 * t) <= per_cu * 1.41421356) t *= 2;   // nearest power of two
+        T = env_int("GX_PR_UNIT_NNZ", (int)t, 1024, 1 << 30);
+        B = env_int("GX_PR_BLOCK_NNZ", (int)std::min<int64_t>(4 * T, 1 << 30), 1024, 1 << 30);
+        p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)T, 1024, 1 << 30);
+    } else {
+        // entries per block: GX_PR_SORTED_NNZ, else 65536 -- 32768 when the partition gives
+        // fewer than one block per CU (the 1/4 and 1/8 partitions of SYN-7_5 ran best at 32 Ki:
+        // 35 us vs 37 at 16 Ki and 67 at 64 Ki for 1/8), or doubled up to 1 Mi while it gives
+        // more than four per CU (round 1, one workgroup per block: tools/pr_sorted_sweep.sh)
+        B = p->sorted_nnz;
+        if (std::getenv("GX_PR_SORTED_NNZ")) {
+            B = env_int("GX_PR_SORTED_NNZ", p->sorted_nnz, 1024, 1 << 22);
+        } else {
+            while (B > 32768 && (int64_t)nnz < B * cus) B >>= 1;
+            while (B < (1 << 20) && (int64_t)nnz > 4 * B * cus) B <<= 1;
+        }
+        p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)B, 1024, 1 << 24);
+    }
+    p->sorted_nnz = (int)B;
+    p->unit_nnz = T;
+    const int64_t BB = B;
     const int64_t R = p->sorted_rows, LT = std::max<int64_t>(p->long_nnz, 1);
     std::vector<RowBlock> longb, sortb;
     std::vector<int32_t> lfirst, lnseg;
@@ -496,7 +612,7 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         int64_t nz = 0;
         while (r < rows && r - start < R) {
             const int64_t l = h_rp[r + 1] - h_rp[r];
-            if (l > LT || nz + l > B) break;
+            if (l > LT || nz + l > BB) break;
             nz += l;
             r++;
         }
@@ -618,6 +734,102 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         GX_TRY(check_launch("k_sorted_bounds"));
         GX_HIP_TRY(hipStreamSynchronize(s));
     }
+    // units of the split blocks (one pass): ceil(entries / T) per sorted block (at most one
+    // per round of entries)
+    p->nunits = 0;
+    if (p->units_mode && !sortb.empty()) {
+        p->unit_nnz = T;
+        // GX_PR_UNIT_LAYOUT = 1 (default): interleaved rounds of kUnitRound entries; 0:
+        // contiguous ranges (each unit its own column range: the units of a block then need
+        // different parts of x at the same time)
+        const bool interleave = env_int("GX_PR_UNIT_LAYOUT", 1, 0, 1) == 1;
+        const int64_t kUnitRound = round;
+        std::vector<SortedUnit> units;
+        int64_t slab = 0;
+        int32_t parts = 0;
+        for (size_t i = 0; i < sortb.size(); i++) {
+            const RowBlock &b = sortb[i];
+            const int64_t E = b.nz_end - b.nz_begin, G = (E + 63) / 64;
+            const int64_t rounds = (E + kUnitRound - 1) / kUnitRound;
+            const int32_t k = (int32_t)std::max<int64_t>(
+                1, std::min<int64_t>(interleave ? rounds : G, (E + T - 1) / T));
+            const int64_t rows_b = b.row_end - b.row_begin;
+            for (int32_t j = 0; j < k; j++) {
+                SortedUnit u;
+                if (interleave) {
+                    u.lo = b.nz_begin + kUnitRound * j;
+                    u.hi = b.nz_end;
+                    u.step = kUnitRound * k;
+                } else {
+                    u.lo = b.nz_begin + 64 * (G * j / k);
+                    u.hi = std::min(b.nz_begin + 64 * (G * (j + 1) / k), b.nz_end);
+                    u.step = kUnitRound;
+                }
+                u.slab = k > 1 ? slab : 0;
+                u.blk = (int32_t)(longb.size() + i);
+                u.part = k > 1 ? parts : -1;
+                u.unit = j;
+                u.nunits = k;
+                units.push_back(u);
+            }
+            if (k > 1) {
+                slab += (int64_t)k * rows_b;
+                parts++;
+            }
+        }
+        // Largest units first (GX_PR_UNIT_ORDER=1, the default): the launch lasts as long as
+        // the unit that finishes last, so the big units start in the first wave and the small
+        // ones fill the gaps at the end.  Cost ~ entries + 4 per row (zeroing, epilogue).
+        // Ties keep block order, so a block's units stay adjacent.
+        if (env_int("GX_PR_UNIT_ORDER", 1, 0, 1)) {
+            auto cost = [&](const SortedUnit &u) {
+                const RowBlock &b = sortb[u.blk - longb.size()];
+                const int64_t E = b.nz_end - b.nz_begin;
+                return (E + u.nunits - 1) / u.nunits + 4 * (int64_t)(b.row_end - b.row_begin);
+            };
+            std::stable_sort(units.begin(), units.end(),
+                             [&](const SortedUnit &x, const SortedUnit &y) { return cost(x) > cost(y); });
+        }
+        // XCD grouping (GX_PR_UNIT_XCD=1; off by default: SYN-7_5 took 117.7 us per launch with
+        // it against 102.9 without, tools/pr_units_sweep.sh): the units of one block sweep the same
+        // column range at the same time, so they share x lines -- if they run on one XCD, its
+        // L2 fetches each line once for all of them.  Workgroups are dealt round-robin over
+        // the 8 XCDs (MI355X_MICROARCH.md, dispatch: w and w + 8 share one; speed only, never
+        // correctness), so each block goes whole to the least-loaded of 8 lists and grid slot
+        // 8 i + x runs list x's i-th unit; short lists are padded with empty units (blk -1).
+        if (env_int("GX_PR_UNIT_XCD", 0, 0, 1) && units.size() > 8) {
+            std::vector<std::vector<SortedUnit>> lists(8);
+            std::vector<int64_t> load(8, 0);
+            for (size_t i = 0; i < units.size();) {
+                size_t j = i;
+                while (j < units.size() && units[j].blk == units[i].blk) j++;
+                const RowBlock &b = sortb[units[i].blk - longb.size()];
+                const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                for (size_t k = i; k < j; k++) lists[x].push_back(units[k]);
+                load[x] += b.nz_end - b.nz_begin;
+                i = j;
+            }
+            size_t L = 0;
+            for (const auto &l : lists) L = std::max(L, l.size());
+            SortedUnit empty{};
+            empty.blk = -1;
+            std::vector<SortedUnit> grid(8 * L, empty);
+            for (int x = 0; x < 8; x++)
+                for (size_t i = 0; i < lists[x].size(); i++) grid[8 * i + x] = lists[x][i];
+            units.swap(grid);
+        }
+        p->nunits = (uint32_t)units.size();
+        if (env_int("GX_PR_VERBOSE", 0, 0, 1))
+            std::fprintf(stderr, "[gx_pr] plan: rows %lld nnz %llu unit_nnz %lld block_nnz %d long_nnz %d: "
+                         "%zu sorted blocks, %u LONG blocks (%u rows), %u units, %d multi-unit blocks, slab %lld doubles\n",
+                         (long long)rows, (unsigned long long)nnz, (long long)T, p->sorted_nnz, p->long_nnz,
+                         sortb.size(), p->nlong_blocks, p->nlong, p->nunits, parts, (long long)slab);
+        GX_TRY(p->units.alloc(units.size()));
+        GX_HIP_TRY(hipMemcpy(p->units.p, units.data(), units.size() * sizeof(SortedUnit), hipMemcpyHostToDevice));
+        GX_TRY(p->uslab.alloc(std::max<int64_t>(slab, 1)));
+        GX_TRY(p->uticket.alloc(std::max<int32_t>(parts, 1)));
+        GX_HIP_TRY(hipMemset(p->uticket.p, 0, p->uticket.n * 4));
+    }
     // fused dangling sum: one pass, and every dangling row in a sorted block
     {
         std::vector<int32_t> slot(all.size(), -1);
@@ -681,7 +893,64 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.dpart = p->fdpart.p;
     a.dticket = p->fdticket.p;
     a.ndblocks = p->ndblocks;
-    if (p->nblocks && p->slices > 1) {
+    a.units = p->units.p;
+    a.uslab = p->uslab.p;
+    a.uticket = p->uticket.p;
+    a.utimes = nullptr;
+    const char *times_path = std::getenv("GX_PR_UNIT_TIMES");   // debug: not under graph capture
+    if (times_path && p->nunits) {
+        if (!p->utimes.p) GX_TRY(p->utimes.alloc(4 * (size_t)(p->nlong_blocks + p->nunits)));
+        a.utimes = p->utimes.p;
+    }
+    if (p->nunits) {
+        KTimer kt(p->ctx, "pr_pull", s);   // one iteration's SpMV (+ fused dangling sum)
+        const dim3 grid(p->nlong_pad + p->nunits);
+        // One 1024-thread workgroup per CU (GX_PR_UNIT_LDS, bytes: the LDS reserved per
+        // workgroup; 0 = only the accumulators, two per CU).  Fewer concurrent sweeps keep
+        // the XCD's L2 window of x smaller: SYN-7_5 one per CU 100-104 us per launch against
+        // 109-125 with two (tools/pr_units_sweep.sh).
+        const int pad = p->sorted_variant == 0 ? 96 * 1024 : 0;
+        const size_t lds = std::max<size_t>((size_t)p->sorted_lds, (size_t)env_int("GX_PR_UNIT_LDS", pad, 0, 160 * 1024 - 4096));
+        if (a.utimes) {
+            hipLaunchKernelGGL((k_pr_pull_units<1024, 8, true>), grid, dim3(1024), lds, s, a);
+        } else {
+            switch (p->sorted_variant) {
+            case 2: hipLaunchKernelGGL((k_pr_pull_units<512, 16, false>), grid, dim3(512), lds, s, a); break;
+            case 3: hipLaunchKernelGGL((k_pr_pull_units<512, 8, false>), grid, dim3(512), lds, s, a); break;
+            default: hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false>), grid, dim3(1024), lds, s, a); break;
+            }
+        }
+        if (a.utimes && ++p->utimes_launch == env_int("GX_PR_UNIT_TIMES_LAUNCH", 5, 1, 1 << 30)) {
+            const size_t nw = p->nlong_pad + p->nunits;
+            std::vector<uint64_t> t(4 * nw);
+            std::vector<SortedUnit> us(p->nunits);
+            std::vector<RowBlock> bs(p->nblocks);
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            GX_HIP_TRY(hipMemcpy(t.data(), p->utimes.p, t.size() * 8, hipMemcpyDeviceToHost));
+            GX_HIP_TRY(hipMemcpy(us.data(), p->units.p, us.size() * sizeof(SortedUnit), hipMemcpyDeviceToHost));
+            GX_HIP_TRY(hipMemcpy(bs.data(), p->blocks.p, bs.size() * sizeof(RowBlock), hipMemcpyDeviceToHost));
+            if (FILE *f = std::fopen(times_path, "w")) {
+                std::fprintf(f, "wg kind blk unit nunits entries rows t0 tgather t1 xcc\n");
+                for (size_t w = 0; w < nw; w++) {
+                    if (w >= p->nlong_blocks && w < p->nlong_pad) continue;
+                    if (w >= p->nlong_pad && us[w - p->nlong_pad].blk < 0) continue;
+                    const bool lng = w < p->nlong_blocks;
+                    const RowBlock &b = lng ? bs[w] : bs[us[w - p->nlong_pad].blk];
+                    long long ents = lng ? b.nz_end - b.nz_begin : 0;
+                    if (!lng) {
+                        const SortedUnit &u = us[w - p->nlong_pad];
+                        for (int64_t k0 = u.lo; k0 < u.hi; k0 += u.step) ents += std::min<int64_t>(u.step / u.nunits, u.hi - k0);
+                    }
+                    std::fprintf(f, "%zu %s %d %d %d %lld %d %llu %llu %llu %llu\n", w, lng ? "long" : "unit",
+                                 lng ? (int)w : us[w - p->nlong_pad].blk, lng ? 0 : us[w - p->nlong_pad].unit,
+                                 lng ? 1 : us[w - p->nlong_pad].nunits, ents, b.row_end - b.row_begin,
+                                 (unsigned long long)t[4 * w], (unsigned long long)t[4 * w + 1],
+                                 (unsigned long long)t[4 * w + 2], (unsigned long long)t[4 * w + 3]);
+                }
+                std::fclose(f);
+            }
+        }
+    } else if (p->nblocks && p->slices > 1) {
         KTimer kt(p->ctx, "pr_pull", s);   // sliced SpMV + epilogue: one iteration
         switch (p->slices) {
         case 2: launch_sliced<1024, 8, 2>(p, a, s); break;

@@ -201,10 +201,20 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, slices):
                                  {"GX_PR_SORTED_VARIANT": "1"}, {"GX_PR_SORTED_VARIANT": "2"},
                                  {"GX_PR_SLICES": "2"}, {"GX_PR_SLICES": "4"}, {"GX_PR_SLICES": "8"},
                                  {"GX_PR_SLICES": "8", "GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SLICES": "1"},
-                                 {"GX_PR_KERNEL": "adaptive"}])
+                                 {"GX_PR_KERNEL": "adaptive"},
+                                 {"GX_PR_SORTED_NNZ": "1024"},
+                                 {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536"},
+                                 {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "524288"},
+                                 {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536", "GX_PR_LONG_NNZ": "1024"},
+                                 {"GX_PR_UNIT_NNZ": "4096", "GX_PR_BLOCK_NNZ": "65536", "GX_PR_SORTED_VARIANT": "3"},
+                                 {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192", "GX_PR_UNIT_LAYOUT": "0"},
+                                 {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192", "GX_PR_SORTED_ROWS": "64",
+                                  "GX_PR_UNIT_LAYOUT": "0"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
-    """One pass, two passes around a small hub slice, tiny blocks, the other block shapes and
-    the CSR-Adaptive kernel all give the oracle's scores (directed and undirected)."""
+    """One pass, two passes around a small hub slice, tiny blocks, the other block shapes,
+    split blocks (several workgroups per sorted block, combined through slabs by the last
+    arriver) and the CSR-Adaptive kernel all give the oracle's scores (directed and
+    undirected)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     for g in (_rmat(14, 16, 4), _rmat(11, 8, 3, undirected=False)):
