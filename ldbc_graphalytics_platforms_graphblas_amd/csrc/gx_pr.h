@@ -98,7 +98,7 @@ struct PrPart {
     DBuf<uint32_t> dticket;
     // column-sorted blocks (k_pr_pull_sorted, gx_pr_sorted.hip; the default)
     DBuf<int32_t> sci;           // columns sorted within each block
-    DBuf<uint32_t> spk;          // packed (column - group base) << 12 | row
+    DBuf<uint32_t> spk;          // packed (column - group base) << 14 | row
     DBuf<uint32_t> gbase;        // base column per 64-entry group (bit 31: escape to sci)
     int sorted_nnz = 65536;      // entries per block
     int sorted_rows = 4096;      // rows per block (LDS accumulators)

@@ -13,9 +13,9 @@
 // (17.1 M requests with 64 Ki-entry blocks).
 //
 // Layout (built once per plan on the device by a radix sort of (block << 32 | column)):
-//   spk[e]   uint32 : (column - group base) << 12 | row of the entry within its block
+//   spk[e]   uint32 : (column - group base) << 14 | row of the entry within its block
 //   gbase[g] uint32 : base column of 64-entry group g (one wave-instruction); bit 31 set =
-//                     escape: the group spans >= 2^20 columns and reads them from sci
+//                     escape: the group spans >= 2^18 columns and reads them from sci
 //   sci[e]   int32  : the block-sorted columns (escape groups, pass split, plan)
 // A block keeps the CSR range [rp[row_begin], rp[row_end]) of its <= 4096 rows, so the
 // per-row epilogue is unchanged, and streams 4 B per entry like the CSR column index.
@@ -41,6 +41,8 @@
 
 namespace gx {
 namespace {
+
+constexpr int kRowBits = 14;   // packed entry: (column - group base) << kRowBits | row in block
 
 struct SortedArgs {
     const RowBlock *blocks;
@@ -220,8 +222,8 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
             uint32_t esc = 0;
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                r[u] = pk[u] & 0xfffu;
-                c[u] = (int32_t)(gb[u] + (pk[u] >> 12));
+                r[u] = pk[u] & ((1u << kRowBits) - 1);
+                c[u] = (int32_t)(gb[u] + (pk[u] >> kRowBits));
                 esc |= gb[u];
             }
             if (esc & 0x80000000u) {   // wave-uniform: an escape group in this round
@@ -358,12 +360,22 @@ __global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? 8 : 1)) void k_pr_pul
             stamp();
             return;
         }
+        // after tid 0's acquire (this CU's L1 invalidated) and the barrier, plain loads see the
+        // other units' slabs; four rows per thread at a time keep 4 x nunits loads in flight
+        // (a dependent chain of nunits loads per row left the last arriver reading for tens of
+        // microseconds on 16 Ki-row blocks)
         const double *slabs = a.uslab + u.slab;
-        for (int i = tid; i < nrows; i += BS) {
-            double s = 0.0;
-            for (int j = 0; j < u.nunits; j++)
-                s += __hip_atomic_load(&slabs[(int64_t)j * nrows + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            acc[i] = s;
+        for (int i0 = tid; i0 < nrows; i0 += 4 * BS) {
+            double s[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int j = 0; j < u.nunits; j++) {
+                const double *sl = slabs + (int64_t)j * nrows;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (i0 + q * BS < nrows) s[q] += sl[i0 + q * BS];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (i0 + q * BS < nrows) acc[i0 + q * BS] = s[q];
         }
         // each thread reads back only the acc entries it wrote: no barrier needed
     }
@@ -484,8 +496,8 @@ __global__ __launch_bounds__(256) void k_sorted_pack(const RowBlock *__restrict_
         const int64_t g = (e - z0) >> 6;
         const int64_t first = z0 + (g << 6), last = min(first + 63, z1 - 1);
         const uint32_t base = (uint32_t)sci[first];
-        const bool esc = (uint32_t)sci[last] - base >= (1u << 20);
-        spk[e] = esc ? (uint32_t)srl[e] : (((uint32_t)sci[e] - base) << 12) | (uint32_t)srl[e];
+        const bool esc = (uint32_t)sci[last] - base >= (1u << (32 - kRowBits));
+        spk[e] = esc ? (uint32_t)srl[e] : (((uint32_t)sci[e] - base) << kRowBits) | (uint32_t)srl[e];
         if (e == first) gbase[b.seg + g] = esc ? (base | 0x80000000u) : base;
     }
 }
@@ -547,7 +559,6 @@ void launch_sliced(const PrPart *p, const SortedArgs &a, hipStream_t s) {
 int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vector<int32_t> &h_outdeg) {
     const int64_t rows = (int64_t)h_rp.size() - 1;
     const uint64_t nnz = (uint64_t)h_rp[rows];
-    p->sorted_rows = env_int("GX_PR_SORTED_ROWS", p->sorted_rows, 64, 4096);   // 12-bit rows, LDS <= 32 KiB
     // GX_PR_SORTED_VARIANT = 0 (1024 threads, 8 gathers in flight per lane, entry loads
     // pipelined) | 1 (1024, 8, not pipelined) | 2 (512, 16, pipelined) | 3 (512, 8, pipelined)
     p->sorted_variant = env_int("GX_PR_SORTED_VARIANT", 0, 0, 3);
@@ -561,22 +572,32 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     if (p->two_pass) p->slices = 1;
     const int64_t cus = std::max(1, p->ctx->num_cus);
     // Split blocks (k_pr_pull_units; one pass, pipelined variants): sorted blocks of up to
-    // block_nnz = 4 T entries, each cut into units of at most T entries (interleaved rounds),
-    // one workgroup each; rows longer than T take the LONG path.  T = the power of two
-    // nearest nnz / CUs, clamped to [16 Ki, 1 Mi] (GX_PR_UNIT_NNZ, GX_PR_BLOCK_NNZ,
-    // GX_PR_LONG_NNZ override).  Measured (tools/pr_units_sweep.sh, us per launch): SYN-7_5
-    // T = 256 Ki 100 (the round-1 64 Ki single-workgroup blocks: 140), 128 Ki 107, 192 Ki 129,
-    // 240 Ki 118; graph500-22 256 Ki / 512 Ki 269 / 272 (round 1: 384); SYN-8_5 1 Mi 1187 with
-    // 4 Mi blocks, 1155 with 8 Mi, 2 Mi 1229 (round 1: 1489).
+    // block_nnz entries and sorted_rows rows, each cut into units of at most T entries
+    // (interleaved rounds), one workgroup each; rows longer than T take the LONG path.
+    // T = the power of two nearest nnz / CUs, clamped to [16 Ki, 1 Mi]; block_nnz = 4 T and
+    // 4 Ki rows, or 8 T and 16 Ki rows once nnz / CUs passes 2 Mi (GX_PR_UNIT_NNZ,
+    // GX_PR_BLOCK_NNZ, GX_PR_SORTED_ROWS, GX_PR_LONG_NNZ override).  Measured
+    // (tools/pr_units_sweep.sh, us per launch; round 1's 64 Ki single-workgroup blocks in
+    // brackets): SYN-7_5 T 256 Ki 100 [140] (128 Ki 107, 192 Ki 129, 240 Ki 118; 8 Ki rows
+    // 105, 16 Ki 111; 2 Mi blocks 124); graph500-22 T 512 Ki with 4 Mi blocks 267 [384];
+    // SYN-8_5 T 1 Mi, 16 Ki rows, 8 Mi blocks 1064-1070 [1489] (4 Ki rows, 4 Mi: 1187).  Per
+    // unit (tools/unit_times.py) the gathers run at ~2,900 entries/us, so the launch lasts
+    // about T / 2,900 us plus the epilogue of the last blocks; larger blocks cut the x line
+    // requests (tools/pr_line_model.py) but their last arriver adds more slabs per row.
     p->units_mode = !p->two_pass && p->slices == 1 && p->sorted_variant != 1 && !std::getenv("GX_PR_SORTED_NNZ");
     const int64_t round = p->sorted_variant == 3 ? 512 * 8 : 1024 * 8;   // U * BS of the launch
+    const double per_cu = std::max(1.0, (double)nnz / (double)cus);
+    const bool huge = per_cu > (double)(2 << 20);
+    // rows per block (LDS accumulators, kRowBits-bit row field; 16 Ki rows = 128 KiB of LDS,
+    // which the split-block mode's one workgroup per CU can take)
+    const int rmax = p->units_mode && p->sorted_variant == 0 ? 1 << kRowBits : 4096;
+    p->sorted_rows = env_int("GX_PR_SORTED_ROWS", p->units_mode && huge ? rmax : 4096, 64, rmax);
     int64_t B, T = 0;
     if (p->units_mode) {
-        const double per_cu = std::max(1.0, (double)nnz / (double)cus);
         int64_t t = 1 << 14;
         while (t < (1 << 20) && (double)(2 * t) <= per_cu * 1.41421356) t *= 2;   // nearest power of two
         T = env_int("GX_PR_UNIT_NNZ", (int)t, 1024, 1 << 30);
-        B = env_int("GX_PR_BLOCK_NNZ", (int)std::min<int64_t>(4 * T, 1 << 30), 1024, 1 << 30);
+        B = env_int("GX_PR_BLOCK_NNZ", (int)std::min<int64_t>((huge ? 8 : 4) * T, 1 << 30), 1024, 1 << 30);
         p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)T, 1024, 1 << 30);
     } else {
         // entries per block: GX_PR_SORTED_NNZ, else 65536 -- 32768 when the partition gives
