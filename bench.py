@@ -583,7 +583,7 @@ def main():
                 "cus": cus,
             },
             "roofline": {
-                "kernel": "k_pr_pull",
+                "kernel": "k_pr_pull_units",
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,

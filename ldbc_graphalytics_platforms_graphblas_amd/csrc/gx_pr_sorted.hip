@@ -33,6 +33,8 @@
 // segment of the row, segments combined by the last arriver) in the hub pass; their blocks
 // come first.
 #include <algorithm>
+#include <functional>
+#include <queue>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -552,6 +554,40 @@ void launch_sliced(const PrPart *p, const SortedArgs &a, hipStream_t s) {
     hipLaunchKernelGGL((k_pr_sliced_epilogue<S>), dim3(grid_for(p->rows, 256, 4096)), dim3(256), 0, s, a);
 }
 
+// Simulated duration (us) of one k_pr_pull_units launch: the units of every sorted block
+// (entries ents[i], rows rws[i]) cut at unit size t, and the LONG segments (lsegs), dealt
+// largest first to one workgroup slot per CU, each slot taking the next unit when it frees
+// (list scheduling; the grid is issued in that order).  Per-unit cost from the per-workgroup
+// timestamps (tools/unit_times.py on SYN-7_5): ~2,900 entries/us of gathers, ~2 ns per row
+// (zeroing, epilogue, slab store), ~1.5 us fixed, and the last arriver's slab reads.  It
+// picks the unit size, so that the units of the large blocks land in as few waves as the
+// CUs allow: e.g. SYN-7_5 at 232 Ki-entry units (5 per 1 Mi block, 325 large units for 256
+// CUs) took 130 us per launch against 100 at 256 Ki (4 per block, 260).
+double pr_unit_makespan(const std::vector<int64_t> &ents, const std::vector<int64_t> &rws,
+                        const std::vector<int64_t> &lsegs, int64_t t, int64_t round, int cus) {
+    constexpr double kRate = 2900.0, kRow = 0.002, kFixed = 1.5, kSlab = 0.0005;
+    std::vector<double> cost;
+    for (size_t i = 0; i < ents.size(); i++) {
+        const int64_t E = ents[i];
+        const int64_t k = std::max<int64_t>(1, std::min((E + round - 1) / round, (E + t - 1) / t));
+        const double c = (double)E / (double)k / kRate + kRow * (double)rws[i] + kFixed +
+                         (k > 1 ? kSlab * (double)rws[i] * (double)k : 0.0);
+        for (int64_t j = 0; j < k; j++) cost.push_back(c);
+    }
+    for (int64_t e : lsegs) cost.push_back((double)e / kRate + kFixed);
+    std::sort(cost.begin(), cost.end(), std::greater<double>());
+    std::priority_queue<double, std::vector<double>, std::greater<double>> slots;
+    for (int i = 0; i < std::max(1, cus); i++) slots.push(0.0);
+    double span = 0.0;
+    for (double c : cost) {
+        const double f = slots.top() + c;
+        slots.pop();
+        slots.push(f);
+        span = std::max(span, f);
+    }
+    return span;
+}
+
 }  // namespace
 
 // Plan: rows longer than long_nnz -> LONG segment blocks (longest first); runs of the other
@@ -573,17 +609,15 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     const int64_t cus = std::max(1, p->ctx->num_cus);
     // Split blocks (k_pr_pull_units; one pass, pipelined variants): sorted blocks of up to
     // block_nnz entries and sorted_rows rows, each cut into units of at most T entries
-    // (interleaved rounds), one workgroup each; rows longer than T take the LONG path.
-    // T = the power of two nearest nnz / CUs, clamped to [16 Ki, 1 Mi]; block_nnz = 4 T and
-    // 4 Ki rows, or 8 T and 16 Ki rows once nnz / CUs passes 2 Mi (GX_PR_UNIT_NNZ,
-    // GX_PR_BLOCK_NNZ, GX_PR_SORTED_ROWS, GX_PR_LONG_NNZ override).  Measured
-    // (tools/pr_units_sweep.sh, us per launch; round 1's 64 Ki single-workgroup blocks in
-    // brackets): SYN-7_5 T 256 Ki 100 [140] (128 Ki 107, 192 Ki 129, 240 Ki 118; 8 Ki rows
-    // 105, 16 Ki 111; 2 Mi blocks 124); graph500-22 T 512 Ki with 4 Mi blocks 267 [384];
-    // SYN-8_5 T 1 Mi, 16 Ki rows, 8 Mi blocks 1064-1070 [1489] (4 Ki rows, 4 Mi: 1187).  Per
-    // unit (tools/unit_times.py) the gathers run at ~2,900 entries/us, so the launch lasts
-    // about T / 2,900 us plus the epilogue of the last blocks; larger blocks cut the x line
-    // requests (tools/pr_line_model.py) but their last arriver adds more slabs per row.
+    // (interleaved rounds), one workgroup each, one workgroup per CU; rows longer than
+    // block_nnz / 4 take the LONG path.  block_nnz = 1 Mi with 4 Ki rows, 4 Mi once nnz / CUs
+    // passes 384 Ki, 8 Mi with 16 Ki rows once it passes 2 Mi; T is chosen below by simulating
+    // the launch
+    // (pr_unit_makespan).  GX_PR_BLOCK_NNZ, GX_PR_SORTED_ROWS, GX_PR_LONG_NNZ, GX_PR_UNIT_NNZ
+    // override.  Measured (tools/pr_units_sweep.sh, us per launch; round 1's 64 Ki
+    // single-workgroup blocks in brackets): SYN-7_5 100 [140]; graph500-22 267 [384]; SYN-8_5
+    // 1064-1070 [1489].  Larger blocks cut the x line requests (tools/pr_line_model.py) but
+    // give the last arriver more slabs per row.
     p->units_mode = !p->two_pass && p->slices == 1 && p->sorted_variant != 1 && !std::getenv("GX_PR_SORTED_NNZ");
     const int64_t round = p->sorted_variant == 3 ? 512 * 8 : 1024 * 8;   // U * BS of the launch
     const double per_cu = std::max(1.0, (double)nnz / (double)cus);
@@ -594,11 +628,8 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     p->sorted_rows = env_int("GX_PR_SORTED_ROWS", p->units_mode && huge ? rmax : 4096, 64, rmax);
     int64_t B, T = 0;
     if (p->units_mode) {
-        int64_t t = 1 << 14;
-        while (t < (1 << 20) && (double)(2 * t) <= per_cu * 1.41421356) t *= 2;   // nearest power of two
-        T = env_int("GX_PR_UNIT_NNZ", (int)t, 1024, 1 << 30);
-        B = env_int("GX_PR_BLOCK_NNZ", (int)std::min<int64_t>((huge ? 8 : 4) * T, 1 << 30), 1024, 1 << 30);
-        p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)T, 1024, 1 << 30);
+        B = env_int("GX_PR_BLOCK_NNZ", huge ? 8 << 20 : per_cu > 384.0 * 1024 ? 4 << 20 : 1 << 20, 1024, 1 << 30);
+        p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)std::max<int64_t>(B / 4, round), 1024, 1 << 30);
     } else {
         // entries per block: GX_PR_SORTED_NNZ, else 65536 -- 32768 when the partition gives
         // fewer than one block per CU (the 1/4 and 1/8 partitions of SYN-7_5 ran best at 32 Ki:
@@ -759,6 +790,28 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     // per round of entries)
     p->nunits = 0;
     if (p->units_mode && !sortb.empty()) {
+        if (std::getenv("GX_PR_UNIT_NNZ")) {
+            T = env_int("GX_PR_UNIT_NNZ", 65536, 1024, 1 << 30);
+        } else {
+            // the unit size whose simulated launch is shortest, over multiples of a round
+            std::vector<int64_t> ents, rws, lsegs;
+            for (const RowBlock &b : sortb) {
+                ents.push_back(b.nz_end - b.nz_begin);
+                rws.push_back(b.row_end - b.row_begin);
+            }
+            for (const RowBlock &b : longb) lsegs.push_back(b.nz_end - b.nz_begin);
+            double best = 0.0;
+            const int64_t emax = *std::max_element(ents.begin(), ents.end());
+            for (int64_t t = round; t <= std::max<int64_t>(round, emax); t += round) {
+                const double m = pr_unit_makespan(ents, rws, lsegs, t, round, (int)cus);
+                if (T == 0 || m < best * 0.999) {
+                    best = m;
+                    T = t;
+                }
+            }
+            if (env_int("GX_PR_VERBOSE", 0, 0, 1))
+                std::fprintf(stderr, "[gx_pr] unit size %lld: simulated launch %.1f us\n", (long long)T, best);
+        }
         p->unit_nnz = T;
         // GX_PR_UNIT_LAYOUT = 1 (default): interleaved rounds of kUnitRound entries; 0:
         // contiguous ranges (each unit its own column range: the units of a block then need
