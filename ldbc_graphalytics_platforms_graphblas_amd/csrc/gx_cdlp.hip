@@ -23,6 +23,7 @@
 // The winner is the maximum of the 64-bit key (count << 32) | ~label, i.e. the highest
 // count and among equal counts the smallest label.
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <vector>
 
@@ -224,12 +225,18 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int64_t k0 = 0; k0 < d; k0 += kWave) {
-                const int64_t k = k0 + lane;
-                const bool valid = k < d;
-                const uint32_t l = valid ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
-                lds_table_add_wave(K, C, l, valid, log2ts);
+            // all of the vertex's label gathers in flight before the first insert (the
+            // atomics would otherwise order one round's gathers behind the last one's inserts)
+            constexpr int R = kSlots / (2 * kWave);
+            uint32_t L[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int64_t k = (int64_t)r * kWave + lane;
+                L[r] = k < d ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
             }
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if ((int64_t)r * kWave < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kWave + lane < d, log2ts);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -286,12 +293,16 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
         C[s] = 0;
     }
     __syncthreads();
-    for (int64_t kb = k0; kb < k1; kb += kHugeBlock) {
-        const int64_t k = kb + tid;
-        const bool valid = k < k1;
-        const uint32_t l = valid ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
-        lds_table_add_wave(K, C, l, valid, kLog2);
+    constexpr int R = kHugeChunk / kHugeBlock;   // the chunk's gathers all in flight first
+    uint32_t L[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int64_t k = k0 + (int64_t)r * kHugeBlock + tid;
+        L[r] = k < k1 ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
     }
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        if (k0 + (int64_t)r * kHugeBlock < k1) lds_table_add_wave(K, C, L[r], k0 + (int64_t)r * kHugeBlock + tid < k1, kLog2);
     __syncthreads();
     const int log2ts = hlog2[hi];
     const int64_t ts = 1ll << log2ts;
@@ -405,12 +416,17 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
             C[s] = 0;
         }
         __syncthreads();
-        for (int64_t k0 = 0; k0 < d; k0 += kMidBlock) {
-            const int64_t k = k0 + tid;
-            const bool valid = k < d;
-            const uint32_t l = valid ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
-            lds_table_add_wave(K, C, l, valid, log2ts);
+        // all of the vertex's label gathers in flight before the first insert
+        constexpr int R = kMidSlots / (2 * kMidBlock);
+        uint32_t L[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int64_t k = (int64_t)r * kMidBlock + tid;
+            L[r] = k < d ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
         }
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            if ((int64_t)r * kMidBlock < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kMidBlock + tid < d, log2ts);
         __syncthreads();
         unsigned long long key = 0;
         for (int s = tid; s < ts; s += kMidBlock) {
@@ -433,6 +449,12 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
         __syncthreads();   // the table is cleared for the next vertex
     }
     if (any) raise_flag(a.changed);
+}
+
+// The iteration's changed flag to pinned host memory: one lane's store over PCIe, instead of a
+// 4-byte hipMemcpyAsync, which ran as a ~40 us blit kernel (profiles/r01_cdlp_kernel_stats.csv).
+__global__ void k_cdlp_flag_out(const int *__restrict__ changed, int *hflag) {
+    if (threadIdx.x == 0) *hflag = *changed;
 }
 
 __global__ void k_cdlp_iota(int32_t *a, int64_t n) {
@@ -566,35 +588,30 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
 
 // One synchronous iteration for the plan's vertices: nxt[v] for v in [v0, v1) from cur
 // (the full label array); *changed is set when a label moved (caller zeroes it).
+// The tier kernels write disjoint vertices and only read `cur`, so they run on three streams
+// (GX_CDLP_STREAMS=0: all on s).  Alone, each tier kept a CU at a fraction of its wave
+// slots: the workgroup-per-vertex tiers by their LDS tables, the others by their tails; side
+// by side, a CU holds a mid-tier workgroup and light/tiny waves at once.
 int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s) {
     gx_ctx *ctx = g->ctx;
     const int64_t n = (int64_t)g->n;
     CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr,
                cur,       nxt,       n,      changed, P.v0, P.v1};
-    if (P.v1 > P.v0) {
-        KTimer kt(ctx, "cdlp_tiny", s);
-        hipLaunchKernelGGL(k_cdlp_tiny, dim3(grid_for((uint64_t)(P.v1 - P.v0), kCdlpBlock, 8192)), dim3(kCdlpBlock),
-                           0, s, a);
+    static const bool multi = [] {
+        const char *e = std::getenv("GX_CDLP_STREAMS");
+        return !e || std::atoi(e) != 0;
+    }();
+    hipStream_t s1 = s, s2 = s;
+    if (multi) {
+        GX_TRY(ensure_aux_streams(ctx));
+        s1 = ctx->aux[0];
+        s2 = ctx->aux[1];
+        GX_HIP_TRY(hipEventRecord(ctx->fork_ev, s));
+        GX_HIP_TRY(hipStreamWaitEvent(s1, ctx->fork_ev, 0));
+        GX_HIP_TRY(hipStreamWaitEvent(s2, ctx->fork_ev, 0));
     }
-    GX_TRY(check_launch("k_cdlp_tiny"));
-    if (P.n_small) {
-        KTimer kt(ctx, "cdlp_small", s);
-        hipLaunchKernelGGL(k_cdlp_small, dim3(grid_for((uint64_t)P.n_small * kWave, kCdlpBlock, 8192)),
-                           dim3(kCdlpBlock), 0, s, a, P.d_sv.p, (int32_t)P.n_small);
-        GX_TRY(check_launch("k_cdlp_small"));
-    }
-    if (P.n_light_s) {
-        KTimer kt(ctx, "cdlp_light_s", s);
-        hipLaunchKernelGGL(k_cdlp_light<kLightSlots>, dim3(grid_for((uint64_t)P.n_light_s * kWave, kCdlpBlock, 8192)),
-                           dim3(kCdlpBlock), 0, s, a, P.d_lvs.p, (int32_t)P.n_light_s);
-        GX_TRY(check_launch("k_cdlp_light_s"));
-    }
-    if (P.n_light) {
-        KTimer kt(ctx, "cdlp_light", s);
-        hipLaunchKernelGGL(k_cdlp_light<kLdsHash>, dim3(grid_for((uint64_t)P.n_light * kWave, kCdlpBlock, 8192)),
-                           dim3(kCdlpBlock), 0, s, a, P.d_lv.p, (int32_t)P.n_light);
-        GX_TRY(check_launch("k_cdlp_light"));
-    }
+    // s: mid2, mid, tiny; s1: huge, mid4; s2: light, small, light_s (about a third of an
+    // iteration's kernel time each on SYN-7_5)
     if (P.n_mid2) {
         KTimer kt(ctx, "cdlp_mid2", s);
         const unsigned grid2 = (unsigned)std::min<size_t>(P.n_mid2, (size_t)std::max(1, ctx->num_cus) * 4);
@@ -602,12 +619,23 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
                            (int32_t)P.n_mid2);
         GX_TRY(check_launch("k_cdlp_mid2"));
     }
-    if (P.n_mid4) {
-        KTimer kt(ctx, "cdlp_mid4", s);
-        const unsigned grid4 = (unsigned)std::min<size_t>(P.n_mid4, (size_t)std::max(1, ctx->num_cus) * 2);
-        hipLaunchKernelGGL((k_cdlp_mid<kMid4Block, kMid4Slots>), dim3(grid4), dim3(kMid4Block), 0, s, a, P.d_mv4.p,
-                           (int32_t)P.n_mid4);
-        GX_TRY(check_launch("k_cdlp_mid4"));
+    if (P.n_huge) {
+        KTimer kt(ctx, "cdlp_heavy", s1);
+        hipLaunchKernelGGL(k_cdlp_huge_insert, dim3((unsigned)P.n_chunks), dim3(kHugeBlock), 0, s1, a, P.d_hv.p,
+                           P.d_hoff.p, P.d_hl.p, P.d_cvert.p, P.d_cbeg.p, P.gk.p, P.gc.p);
+        GX_TRY(check_launch("k_cdlp_huge_insert"));
+        hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)P.n_seg), dim3(kHugeBlock), 0, s1, P.d_segv.p,
+                           P.d_segb.p, P.d_hoff.p, P.d_hl.p, P.gk.p, P.gc.p, P.vkey.p);
+        GX_TRY(check_launch("k_cdlp_huge_reduce"));
+        hipLaunchKernelGGL(k_cdlp_huge_final, dim3(grid_for(P.n_huge, 64, 1024)), dim3(64), 0, s1, a, P.d_hv.p,
+                           (int32_t)P.n_huge, P.vkey.p);
+        GX_TRY(check_launch("k_cdlp_huge_final"));
+    }
+    if (P.n_light) {
+        KTimer kt(ctx, "cdlp_light", s2);
+        hipLaunchKernelGGL(k_cdlp_light<kLdsHash>, dim3(grid_for((uint64_t)P.n_light * kWave, kCdlpBlock, 8192)),
+                           dim3(kCdlpBlock), 0, s2, a, P.d_lv.p, (int32_t)P.n_light);
+        GX_TRY(check_launch("k_cdlp_light"));
     }
     if (P.n_mid) {
         KTimer kt(ctx, "cdlp_mid", s);
@@ -616,17 +644,36 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
                            (int32_t)P.n_mid);
         GX_TRY(check_launch("k_cdlp_mid"));
     }
-    if (P.n_huge) {
-        KTimer kt(ctx, "cdlp_heavy", s);
-        hipLaunchKernelGGL(k_cdlp_huge_insert, dim3((unsigned)P.n_chunks), dim3(kHugeBlock), 0, s, a, P.d_hv.p,
-                           P.d_hoff.p, P.d_hl.p, P.d_cvert.p, P.d_cbeg.p, P.gk.p, P.gc.p);
-        GX_TRY(check_launch("k_cdlp_huge_insert"));
-        hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)P.n_seg), dim3(kHugeBlock), 0, s, P.d_segv.p,
-                           P.d_segb.p, P.d_hoff.p, P.d_hl.p, P.gk.p, P.gc.p, P.vkey.p);
-        GX_TRY(check_launch("k_cdlp_huge_reduce"));
-        hipLaunchKernelGGL(k_cdlp_huge_final, dim3(grid_for(P.n_huge, 64, 1024)), dim3(64), 0, s, a, P.d_hv.p,
-                           (int32_t)P.n_huge, P.vkey.p);
-        GX_TRY(check_launch("k_cdlp_huge_final"));
+    if (P.n_mid4) {
+        KTimer kt(ctx, "cdlp_mid4", s1);
+        const unsigned grid4 = (unsigned)std::min<size_t>(P.n_mid4, (size_t)std::max(1, ctx->num_cus) * 2);
+        hipLaunchKernelGGL((k_cdlp_mid<kMid4Block, kMid4Slots>), dim3(grid4), dim3(kMid4Block), 0, s1, a, P.d_mv4.p,
+                           (int32_t)P.n_mid4);
+        GX_TRY(check_launch("k_cdlp_mid4"));
+    }
+    if (P.n_small) {
+        KTimer kt(ctx, "cdlp_small", s2);
+        hipLaunchKernelGGL(k_cdlp_small, dim3(grid_for((uint64_t)P.n_small * kWave, kCdlpBlock, 8192)),
+                           dim3(kCdlpBlock), 0, s2, a, P.d_sv.p, (int32_t)P.n_small);
+        GX_TRY(check_launch("k_cdlp_small"));
+    }
+    if (P.n_light_s) {
+        KTimer kt(ctx, "cdlp_light_s", s2);
+        hipLaunchKernelGGL(k_cdlp_light<kLightSlots>, dim3(grid_for((uint64_t)P.n_light_s * kWave, kCdlpBlock, 8192)),
+                           dim3(kCdlpBlock), 0, s2, a, P.d_lvs.p, (int32_t)P.n_light_s);
+        GX_TRY(check_launch("k_cdlp_light_s"));
+    }
+    if (P.v1 > P.v0) {
+        KTimer kt(ctx, "cdlp_tiny", s);
+        hipLaunchKernelGGL(k_cdlp_tiny, dim3(grid_for((uint64_t)(P.v1 - P.v0), kCdlpBlock, 8192)), dim3(kCdlpBlock),
+                           0, s, a);
+        GX_TRY(check_launch("k_cdlp_tiny"));
+    }
+    if (multi) {
+        GX_HIP_TRY(hipEventRecord(ctx->join_ev[0], s1));
+        GX_HIP_TRY(hipEventRecord(ctx->join_ev[1], s2));
+        GX_HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[0], 0));
+        GX_HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[1], 0));
     }
     return GX_SUCCESS;
 }
@@ -659,9 +706,10 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     // Early exit at a fixed point (LAGraph_cdlp.c:328-332), checked one iteration late:
     // iteration it is queued before the host waits for iteration it-1's flag, so the check
     // never drains the stream.  An iteration run after a fixed point changes no label.
-    int *hflag = nullptr;
-    GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&hflag), sizeof(int) * std::max(iters, 1)));
+    int *hflag = nullptr, *dflag = nullptr;
+    GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&hflag), sizeof(int) * std::max(iters, 1), hipHostMallocMapped));
     std::unique_ptr<int, void (*)(int *)> hflag_guard(hflag, [](int *p) { (void)hipHostFree(p); });
+    GX_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&dflag), hflag, 0));
     hipEvent_t ev[2] = {nullptr, nullptr};
     GX_HIP_TRY(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
     GX_HIP_TRY(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
@@ -675,7 +723,8 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     int32_t *cur = la.p, *nxt = lb.p;
     for (int it = 0; it < iters; it++) {
         GX_TRY(cdlp_iteration(g, P, cur, nxt, changed.p + it, s));
-        GX_HIP_TRY(hipMemcpyAsync(hflag + it, changed.p + it, sizeof(int), hipMemcpyDeviceToHost, s));
+        hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(64), 0, s, changed.p + it, dflag + it);
+        GX_TRY(check_launch("k_cdlp_flag_out"));
         GX_HIP_TRY(hipEventRecord(ev[it & 1], s));
         std::swap(cur, nxt);
         if (it >= 1) {

@@ -307,3 +307,42 @@ def test_wcc_directed_sparse_many_components(ctx):
     keep = np.arange(n - 1) % 97 != 0        # cut into ~200 components
     csr = csr_from_edges(n, src[keep], dst[keep], None, symmetric=False)
     np.testing.assert_array_equal(gpu_run(ctx, _G(csr, True), "WCC"), O.wcc(csr))
+
+
+def _tier_graph(directed: bool):
+    """CDLP tier boundaries in one graph: a star of 10 000 leaves (the huge tier), hubs of
+    degree ~3 000 and ~6 000 (the 4 096- and 8 192-degree workgroup tiers), and rows of
+    degree exactly 128 and 129 (the two light-tier table instances), over a sparse random
+    background.  Several leaves share a few labels, so labels agree after a few iterations
+    and the wave-aggregated insert sees groups of more than one lane."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    rng = np.random.default_rng(11)
+    n = 30000
+    src, dst = [], []
+    def star(center, leaves):
+        src.append(np.full(len(leaves), center, np.int64))
+        dst.append(np.asarray(leaves, np.int64))
+    # centers 0-4 take no other edge; leaves and background live in [5, n)
+    star(0, np.arange(5, 10005))                                  # huge tier (> 8 192)
+    star(1, rng.choice(np.arange(5, n), 3000, replace=False))     # 2 049-4 096
+    star(2, rng.choice(np.arange(5, n), 6000, replace=False))     # 4 097-8 192
+    star(3, rng.choice(np.arange(5, n), 128, replace=False))      # exactly 128
+    star(4, rng.choice(np.arange(5, n), 129, replace=False))      # exactly 129
+    # background: vertices also link to a few shared labels
+    src.append(rng.integers(5, n, 40000))
+    dst.append(rng.integers(5, 55, 40000))
+    s, d = np.concatenate(src), np.concatenate(dst)
+    keep = s != d
+    return csr_from_edges(n, s[keep], d[keep], None, symmetric=not directed)
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_cdlp_tier_boundaries(ctx, directed):
+    """CDLP over every degree tier and the 128/129 light-tier split, against the oracle."""
+    csr = _tier_graph(directed)
+    deg = np.diff(csr.rowptr.astype(np.int64))
+    if not directed:
+        assert {128, 129} <= set(deg.tolist()) and deg.max() > 8192
+    g = _G(csr, directed)
+    for iters in (1, 3, 6):
+        np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=iters), O.cdlp(csr, directed, iters))
