@@ -71,6 +71,8 @@ SIGNATURES = [
     ("gx_last_device_ms", C.c_int, [_P, _DP]),
     ("gx_pr_part_create", C.c_int, [_P, C.c_uint64, C.c_int, C.c_int, _U64P, _U64P, _U64P, _U64P,
                                     C.c_double, C.POINTER(_P)]),
+    ("gx_pr_part_create_live", C.c_int, [_P, C.c_uint64, C.c_int, C.c_int, _U64P, _U64P, _U64P, _U64P, _U64P,
+                                         C.c_double, C.POINTER(_P)]),
     ("gx_pr_part_chunk", C.c_int, [_P, _U64P]),
     ("gx_pr_part_init", C.c_int, [_P, _P, _P]),
     ("gx_pr_part_step", C.c_int, [_P, _P, _P, _P, _P]),

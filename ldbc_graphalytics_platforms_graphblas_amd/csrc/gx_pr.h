@@ -53,6 +53,14 @@ struct SortedUnit {
     int32_t nunits;
 };
 
+// x of local row `row`: rows [0, live) sit in the exchanged chunk, the rest (out-degree 0, so
+// no rank ever gathers them) in the rank-private xd, so that only the gathered prefix of each
+// rank's rows travels in the all-gather (gx_pr_part_create_live).
+__device__ __forceinline__ void store_x(double *x_out, double *xd, int64_t live, int64_t row, double v) {
+    if (row < live) x_out[row] = v;
+    else xd[row - live] = v;
+}
+
 constexpr int kHubBlock = 1024;       // one 16-wave workgroup per CU
 constexpr int kItemNnz = 2048;        // entries per wave item
 constexpr int kItemRows = 512;        // rows per wave item
@@ -69,6 +77,8 @@ struct PrPart {
     int nranks = 1, rank = 0;
     uint64_t rows = 0;       // local rows
     uint64_t chunk = 0;      // doubles per rank chunk (last one = dangling slot)
+    uint64_t live = ~0ull;   // local rows kept in the chunk; rows [live, rows) have x in xd (~0: all)
+    DBuf<double> xd;         // x of the rows past `live` (out-degree 0, never gathered)
     double damping = 0.85;
     // pull matrix of the local rows (column ids already in the padded chunk layout)
     DBuf<int64_t> rp_own;    // when the plan owns its matrix

@@ -49,6 +49,8 @@ struct PullArgs {
     const int32_t *long_nseg;
     double *long_part;
     uint32_t *long_ticket;
+    double *xd;
+    int64_t live;
 };
 
 __device__ __forceinline__ void pr_epilogue(const PullArgs &a, int32_t row, double s,
@@ -56,7 +58,7 @@ __device__ __forceinline__ void pr_epilogue(const PullArgs &a, int32_t row, doub
     const double r = teleport + s;
     if (a.rank_out) a.rank_out[row] = r;
     const int32_t deg = a.outdeg[row];
-    a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+    store_x(a.x_out, a.xd, a.live, row, deg > 0 ? r / ((double)deg / a.damping) : r);
 }
 
 template <int NB, bool STRIDE1>
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
         if (writer) {
             const double r = teleport + s;
             if (a.rank_out) a.rank_out[r0 + row] = r;
-            a.x_out[r0 + row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+            store_x(a.x_out, a.xd, a.live, r0 + row, deg > 0 ? r / ((double)deg / a.damping) : r);
         }
         return;
     }
@@ -231,16 +233,23 @@ __global__ __launch_bounds__(kPullBlock) void k_pr_pull(PullArgs a) {
 // combined by the last arriver's whole workgroup in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void k_pr_dangling(const int32_t *__restrict__ dlist, int64_t d0,
                                                      int64_t nd, int64_t per, double *x, int64_t slot,
-                                                     double *part, uint32_t *ticket) {
+                                                     double *part, uint32_t *ticket, const double *xd,
+                                                     int64_t live) {
     __shared__ double wred[256 / kWave];
     __shared__ int last;
     const int tid = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(b0 + per, nd);
     double s = 0.0;
     if (dlist) {
-        for (int64_t i = b0 + tid; i < b1; i += 256) s += x[dlist[i]];
+        for (int64_t i = b0 + tid; i < b1; i += 256) {
+            const int64_t r = dlist[i];
+            s += r < live ? x[r] : xd[r - live];
+        }
     } else {
-        for (int64_t i = b0 + tid; i < b1; i += 256) s += x[d0 + i];
+        for (int64_t i = b0 + tid; i < b1; i += 256) {
+            const int64_t r = d0 + i;
+            s += r < live ? x[r] : xd[r - live];
+        }
     }
     s = wave_sum(s);
     if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = s;
@@ -277,11 +286,11 @@ __global__ __launch_bounds__(256) void k_pr_dangling(const int32_t *__restrict__
 }
 
 __global__ void k_pr_init(const int32_t *__restrict__ outdeg, int64_t rows, double inv_n,
-                          double damping, double *x, int64_t slot, int zero_slot) {
+                          double damping, double *x, int64_t slot, int zero_slot, double *xd, int64_t live) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t deg = outdeg[i];
-        x[i] = deg > 0 ? inv_n / ((double)deg / damping) : inv_n;
+        store_x(x, xd, live, i, deg > 0 ? inv_n / ((double)deg / damping) : inv_n);
     }
     if (zero_slot && blockIdx.x == 0 && threadIdx.x == 0) x[slot] = 0.0;
 }
@@ -292,6 +301,8 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
             const int32_t *d_outdeg, const std::vector<int32_t> &h_outdeg) {
     const int64_t rows = (int64_t)h_rp.size() - 1;
     p->rows = (uint64_t)rows;
+    if (p->live > p->rows) p->live = p->rows;   // no live prefix given: all rows
+    if (p->live < p->rows) GX_TRY(p->xd.alloc(p->rows - p->live));
     // tuning knobs (plan time): GX_PR_STREAM_NNZ = 1024 | 2048 | 4096, GX_PR_ONLY = long | stream
     if (const char *e = std::getenv("GX_PR_STREAM_NNZ")) {
         const int v = std::atoi(e);
@@ -391,7 +402,7 @@ int pr_dangling(PrPart *p, double *x_local, hipStream_t s) {
     const int64_t per = (int64_t)((p->nd + p->dgrid - 1) / p->dgrid);
     hipLaunchKernelGGL(k_pr_dangling, dim3(p->dgrid), dim3(256), 0, s, p->d_range ? nullptr : p->dlist.p,
                        (int64_t)p->d0, (int64_t)p->nd, per,
-                       x_local, (int64_t)p->chunk - 1, p->dpart.p, p->dticket.p);
+                       x_local, (int64_t)p->chunk - 1, p->dpart.p, p->dticket.p, p->xd.p, (int64_t)p->live);
     return check_launch("k_pr_dangling");
 }
 
@@ -399,7 +410,7 @@ int pr_init(PrPart *p, double *x_local, hipStream_t s) {
     const double inv_n = 1.0 / (double)p->n_global;
     hipLaunchKernelGGL(k_pr_init, dim3(grid_for(p->rows, 256, 8192)), dim3(256), 0, s, p->outdeg,
                        (int64_t)p->rows, inv_n, p->damping, x_local, (int64_t)p->chunk - 1,
-                       p->nd == 0 ? 1 : 0);
+                       p->nd == 0 ? 1 : 0, p->xd.p, (int64_t)p->live);
     GX_TRY(check_launch("k_pr_init"));
     return pr_dangling(p, x_local, s);
 }
@@ -426,6 +437,8 @@ int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, 
     a.long_nseg = p->long_nseg.p;
     a.long_part = p->long_part.p;
     a.long_ticket = p->long_ticket.p;
+    a.xd = p->xd.p;
+    a.live = (int64_t)p->live;
     uint32_t nb = p->nblocks;
     a.block_offset = 0;
     if (p->only == 1) nb = p->nlong_blocks;
@@ -606,22 +619,39 @@ extern "C" int gx_pr_part_create(gx_ctx *ctx, uint64_t n_global, int nranks, int
                                  const uint64_t *row_ranges, const uint64_t *rowptr_local,
                                  const uint64_t *colidx_local, const uint64_t *outdeg_local,
                                  double damping, gx_pr_part **out) {
+    return gx_pr_part_create_live(ctx, n_global, nranks, rank, row_ranges, nullptr, rowptr_local, colidx_local,
+                                  outdeg_local, damping, out);
+}
+
+extern "C" int gx_pr_part_create_live(gx_ctx *ctx, uint64_t n_global, int nranks, int rank,
+                                      const uint64_t *row_ranges, const uint64_t *live_rows,
+                                      const uint64_t *rowptr_local, const uint64_t *colidx_local,
+                                      const uint64_t *outdeg_local, double damping, gx_pr_part **out) {
     if (!ctx || !row_ranges || !rowptr_local || !outdeg_local || !out)
         return fail(GX_NULL_POINTER, "gx_pr_part_create: null argument");
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GX_INVALID_VALUE, "bad rank/nranks");
     if (row_ranges[0] != 0 || row_ranges[nranks] != n_global)
         return fail(GX_INVALID_VALUE, "row_ranges must cover [0, n)");
     GX_HIP_TRY(hipSetDevice(ctx->device));
-    uint64_t maxrows = 0;
+    // the exchanged prefix of every rank: its live rows (all of them without live_rows)
+    std::vector<uint64_t> live(nranks);
+    uint64_t maxlive = 0;
     for (int k = 0; k < nranks; k++) {
         if (row_ranges[k + 1] < row_ranges[k]) return fail(GX_INVALID_VALUE, "row_ranges not monotone");
-        maxrows = std::max(maxrows, row_ranges[k + 1] - row_ranges[k]);
+        live[k] = row_ranges[k + 1] - row_ranges[k];
+        if (live_rows) {
+            if (live_rows[k] > live[k]) return fail(GX_INVALID_VALUE, "live_rows beyond the rank's rows");
+            live[k] = live_rows[k];
+        }
+        maxlive = std::max(maxlive, live[k]);
     }
-    const uint64_t chunk = round_up(maxrows + 1, 32);
+    const uint64_t chunk = round_up(maxlive + 1, 32);
     if (chunk * (uint64_t)nranks >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "partition too large");
     const uint64_t rows = row_ranges[rank + 1] - row_ranges[rank];
     const uint64_t nnz = rowptr_local[rows];
     if (nnz && !colidx_local) return fail(GX_NULL_POINTER, "null colidx");
+    for (uint64_t i = live[rank]; i < rows; i++)
+        if (outdeg_local[i] != 0) return fail(GX_INVALID_VALUE, "a row past live_rows has out-edges");
     std::vector<int64_t> h_rp(rows + 1);
     for (uint64_t i = 0; i <= rows; i++) h_rp[i] = (int64_t)rowptr_local[i];
     std::vector<int32_t> ci(nnz);
@@ -629,6 +659,8 @@ extern "C" int gx_pr_part_create(gx_ctx *ctx, uint64_t n_global, int nranks, int
         const uint64_t c = colidx_local[k];
         if (c >= n_global) return fail(GX_INVALID_INDEX, "column out of range");
         const int owner = (int)(std::upper_bound(row_ranges, row_ranges + nranks + 1, c) - row_ranges) - 1;
+        if (c - row_ranges[owner] >= live[owner])
+            return fail(GX_INVALID_VALUE, "a column is past its owner's live rows (a vertex without out-edges)");
         ci[k] = (int32_t)((uint64_t)owner * chunk + (c - row_ranges[owner]));
     }
     std::vector<int32_t> h_outdeg(rows);
@@ -639,6 +671,7 @@ extern "C" int gx_pr_part_create(gx_ctx *ctx, uint64_t n_global, int nranks, int
     p->nranks = nranks;
     p->rank = rank;
     p->chunk = chunk;
+    p->live = live[rank];
     p->damping = damping;
     int rc = p->rp_own.alloc(rows + 1);
     if (rc == GX_SUCCESS) rc = p->ci_own.alloc(nnz, 16);

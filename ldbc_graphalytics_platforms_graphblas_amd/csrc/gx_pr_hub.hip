@@ -52,6 +52,8 @@ struct HubArgs {
     uint32_t *long_ticket;
     double *gpart;
     uint32_t *gticket;
+    double *xd;
+    int64_t live;
 };
 
 // Buffer resource of a global array (stride 0, raw byte offsets, range-checked).
@@ -115,7 +117,7 @@ __device__ __forceinline__ double finish_row(const HubArgs &a, int32_t row, doub
                                              int32_t deg) {
     const double r = teleport + s;
     if (a.rank_out) a.rank_out[row] = r;
-    a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+    store_x(a.x_out, a.xd, a.live, row, deg > 0 ? r / ((double)deg / a.damping) : r);
     return deg == 0 ? r : 0.0;   // contribution to the dangling sum
 }
 
@@ -377,6 +379,8 @@ int pr_step_hub(PrPart *p, const double *x_full, double *x_local, double *rank_o
     a.long_nseg = p->hlong_nseg.p;
     a.long_part = p->hlong_part.p;
     a.long_ticket = p->hlong_ticket.p;
+    a.xd = p->xd.p;
+    a.live = (int64_t)p->live;
     a.gpart = p->gpart.p;
     a.gticket = p->gticket.p;
     {

@@ -80,6 +80,8 @@ struct SortedArgs {
     double *uslab;
     uint32_t *uticket;
     uint64_t *utimes;        // debug (GX_PR_UNIT_TIMES): per workgroup start, gather end, end, XCC
+    double *xd;              // x of the rows past `live` (store_x, gx_pr.h)
+    int64_t live;
 };
 
 // Returns the row's score if the row is dangling (out-degree 0), else 0.
@@ -87,7 +89,7 @@ __device__ __forceinline__ double sorted_epilogue(const SortedArgs &a, int32_t r
     const double r = teleport + s;
     if (a.rank_out) a.rank_out[row] = r;
     const int32_t deg = a.outdeg[row];
-    a.x_out[row] = deg > 0 ? r / ((double)deg / a.damping) : r;
+    store_x(a.x_out, a.xd, a.live, row, deg > 0 ? r / ((double)deg / a.damping) : r);
     return deg > 0 ? 0.0 : r;
 }
 
@@ -611,8 +613,8 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     // block_nnz entries and sorted_rows rows, each cut into units of at most T entries
     // (interleaved rounds), one workgroup each, one workgroup per CU; rows longer than
     // block_nnz / 4 take the LONG path.  block_nnz = 1 Mi with 4 Ki rows, 4 Mi once nnz / CUs
-    // passes 384 Ki, 8 Mi with 16 Ki rows once it passes 2 Mi; T is chosen below by simulating
-    // the launch
+    // passes 384 Ki, 8 Mi with 16 Ki rows once it passes 2 Mi, at most 4x the power of two
+    // nearest nnz / CUs; T is chosen below by simulating the launch
     // (pr_unit_makespan).  GX_PR_BLOCK_NNZ, GX_PR_SORTED_ROWS, GX_PR_LONG_NNZ, GX_PR_UNIT_NNZ
     // override.  Measured (tools/pr_units_sweep.sh, us per launch; round 1's 64 Ki
     // single-workgroup blocks in brackets): SYN-7_5 100 [140]; graph500-22 267 [384]; SYN-8_5
@@ -628,7 +630,13 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     p->sorted_rows = env_int("GX_PR_SORTED_ROWS", p->units_mode && huge ? rmax : 4096, 64, rmax);
     int64_t B, T = 0;
     if (p->units_mode) {
-        B = env_int("GX_PR_BLOCK_NNZ", huge ? 8 << 20 : per_cu > 384.0 * 1024 ? 4 << 20 : 1 << 20, 1024, 1 << 30);
+        // ... and at most 4x the power of two nearest nnz / CUs, so that a small partition
+        // (one rank of eight) keeps about 4 units per block: a 1/8 piece of SYN-7_5 with 1 Mi
+        // blocks cut into 32 units each ran 50 us per launch against 34 with 128 Ki blocks
+        int64_t pow2 = 1 << 14;
+        while (pow2 < (1 << 24) && (double)(2 * pow2) <= per_cu * 1.41421356) pow2 *= 2;
+        const int64_t bdef = std::min<int64_t>(huge ? 8 << 20 : per_cu > 384.0 * 1024 ? 4 << 20 : 1 << 20, 4 * pow2);
+        B = env_int("GX_PR_BLOCK_NNZ", (int)bdef, 1024, 1 << 30);
         p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)std::max<int64_t>(B / 4, round), 1024, 1 << 30);
     } else {
         // entries per block: GX_PR_SORTED_NNZ, else 65536 -- 32768 when the partition gives
@@ -970,6 +978,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.units = p->units.p;
     a.uslab = p->uslab.p;
     a.uticket = p->uticket.p;
+    a.xd = p->xd.p;
+    a.live = (int64_t)p->live;
     a.utimes = nullptr;
     const char *times_path = std::getenv("GX_PR_UNIT_TIMES");   // debug: not under graph capture
     if (times_path && p->nunits) {

@@ -11,6 +11,9 @@ full replica of the rank vector.  One iteration is:
 The exchange layout is `nranks` chunks of `chunk` doubles; rank k's rows sit at the start of
 chunk k and its dangling-score sum in the chunk's last slot, so a single
 all_gather_into_tensor carries both the vector and the dangling mass (no extra all-reduce).
+Rows without out-edges are never gathered by anyone: when every rank's such rows come last
+(hub-first order), only each rank's leading `live` rows go in its chunk
+(gx_pr_part_create_live), and the exchanged vector shrinks by their share (29.5 % of SYN-7_5).
 The reference has no distributed path ("Collective call sites: none"); this is
 the exchange step the north star adds.
 """
@@ -92,6 +95,22 @@ def partition_rows(rowptr: np.ndarray, nranks: int) -> np.ndarray:
     return bounds
 
 
+def live_rows(csr: CSR, bounds: np.ndarray) -> Optional[np.ndarray]:
+    """Per part k, the number of leading rows of [bounds[k], bounds[k+1]) with out-edges, if
+    every part's rows without out-edges come after all its rows with them (hub-first orders:
+    interleaved_relabel, hub_relabel + partition_rows); else None (every row exchanged)."""
+    deg = np.diff(csr.rowptr.astype(np.int64))
+    b = np.asarray(bounds, dtype=np.int64)
+    out = np.zeros(len(b) - 1, dtype=np.uint64)
+    for k in range(len(b) - 1):
+        seg = deg[b[k]:b[k + 1]]
+        live = int(np.count_nonzero(seg))
+        if live and not (seg[:live] > 0).all():
+            return None
+        out[k] = live
+    return out
+
+
 @dataclass
 class LocalRows:
     row_ranges: np.ndarray   # uint64[nranks+1]
@@ -99,6 +118,7 @@ class LocalRows:
     rowptr: np.ndarray       # uint64[rows+1], starting at 0
     colidx: np.ndarray       # uint64[nnz_local], global column ids
     outdeg: np.ndarray       # uint64[rows], out-degree of each local row's vertex
+    live: Optional[np.ndarray] = None   # uint64[nranks]: live_rows() of the partition, or None
 
     @property
     def rows(self) -> int:
@@ -115,7 +135,8 @@ def _slice_rows(csr: CSR, pull: CSR, bounds: np.ndarray, rank: int) -> LocalRows
     rp = (pull.rowptr[r0:r1 + 1] - np.uint64(z0)).astype(np.uint64)
     ci = np.ascontiguousarray(pull.colidx[z0:z1], dtype=np.uint64)
     outdeg = np.diff(csr.rowptr.astype(np.int64))[r0:r1].astype(np.uint64)
-    return LocalRows(bounds, rank, np.ascontiguousarray(rp), ci, np.ascontiguousarray(outdeg))
+    return LocalRows(bounds, rank, np.ascontiguousarray(rp), ci, np.ascontiguousarray(outdeg),
+                     live_rows(csr, bounds))
 
 
 def slice_rows(csr: CSR, bounds: np.ndarray, part: int, pull: Optional[CSR] = None) -> LocalRows:
@@ -151,12 +172,14 @@ class GpuStep:
         self.N = N
         self.lib = N.lib()
         self.part = C.c_void_p()
-        N.check(self.lib.gx_pr_part_create(ctx.handle, n_global, nranks, lr.rank, N.as_u64p(lr.row_ranges),
-                                           N.as_u64p(lr.rowptr),
-                                           N.as_u64p(lr.colidx) if lr.nnz else None,
-                                           N.as_u64p(lr.outdeg) if lr.rows else
-                                           N.as_u64p(np.zeros(1, np.uint64)),
-                                           damping, C.byref(self.part)), "gx_pr_part_create")
+        self._live = None if lr.live is None else np.ascontiguousarray(lr.live, dtype=np.uint64)
+        N.check(self.lib.gx_pr_part_create_live(ctx.handle, n_global, nranks, lr.rank, N.as_u64p(lr.row_ranges),
+                                                N.as_u64p(self._live) if self._live is not None else None,
+                                                N.as_u64p(lr.rowptr),
+                                                N.as_u64p(lr.colidx) if lr.nnz else None,
+                                                N.as_u64p(lr.outdeg) if lr.rows else
+                                                N.as_u64p(np.zeros(1, np.uint64)),
+                                                damping, C.byref(self.part)), "gx_pr_part_create_live")
         ch = C.c_uint64(0)
         N.check(self.lib.gx_pr_part_chunk(self.part, C.byref(ch)), "gx_pr_part_chunk")
         self.chunk = ch.value

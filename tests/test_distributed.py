@@ -18,8 +18,8 @@ import torch.multiprocessing as mp
 from conftest import ROOT  # noqa: F401  (sys.path)
 from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
 from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import (PartitionedPageRank, hub_relabel,
-                                                                    interleaved_relabel, local_pieces, local_rows,
-                                                                    partition_rows, slice_rows)
+                                                                    interleaved_relabel, live_rows, local_pieces,
+                                                                    local_rows, partition_rows, slice_rows)
 from oracle import oracle as O
 
 
@@ -28,9 +28,13 @@ class CpuStep:
 
     def __init__(self, n_global, nranks, lr, damping):
         rr = lr.row_ranges.astype(np.int64)
-        self.chunk = int(((rr[1:] - rr[:-1]).max() + 1 + 31) // 32 * 32)
+        live = (rr[1:] - rr[:-1]) if lr.live is None else lr.live.astype(np.int64)   # gx_pr_part_create_live
+        self.chunk = int((live.max() + 1 + 31) // 32 * 32)
+        self.live = int(live[lr.rank])
         owner = np.searchsorted(rr, lr.colidx.astype(np.int64), side="right") - 1
-        self.cols = owner * self.chunk + (lr.colidx.astype(np.int64) - rr[owner])
+        li = lr.colidx.astype(np.int64) - rr[owner]
+        assert (li < live[owner]).all(), "a column past its owner's live rows"
+        self.cols = owner * self.chunk + li
         self.rp = lr.rowptr.astype(np.int64)
         self.deg = lr.outdeg.astype(np.int64)
         self.rows = lr.rows
@@ -41,7 +45,7 @@ class CpuStep:
     def init(self, x_local, stream):
         inv_n = 1.0 / self.n
         x = np.where(self.deg > 0, inv_n / (self.deg / self.d), inv_n)
-        x_local[:self.rows] = torch.from_numpy(x)
+        x_local[:self.live] = torch.from_numpy(x[:self.live])
         x_local[self.chunk - 1] = float(np.sum(np.where(self.deg == 0, inv_n, 0.0)))
 
     def step(self, x_full, x_local, rank_out, stream):
@@ -51,7 +55,7 @@ class CpuStep:
         s = np.add.reduceat(np.append(xf[self.cols], 0.0), self.rp[:-1]) if len(self.cols) else np.zeros(self.rows)
         s = np.where(np.diff(self.rp) > 0, s, 0.0)
         r = tele + s
-        x_local[:self.rows] = torch.from_numpy(np.where(self.deg > 0, r / (self.deg / self.d), r))
+        x_local[:self.live] = torch.from_numpy(np.where(self.deg > 0, r / (self.deg / self.d), r)[:self.live])
         x_local[self.chunk - 1] = float(np.sum(np.where(self.deg == 0, r, 0.0)))
         if rank_out is not None:
             rank_out[:self.rows] = torch.from_numpy(r)
@@ -139,6 +143,34 @@ def test_interleaved_relabel_balances_rows_and_entries():
     assert 8 * (ranges.max() + 1) > 3 * csr.n
 
 
+def test_live_rows_prefix_and_exchange_size():
+    """Hub-first layouts keep every part's rows without out-edges last, so only the leading
+    live rows are exchanged: the padded exchange is ~(vertices with out-edges) doubles."""
+    csr = rmat(12, 16, 9)
+    deg = np.diff(csr.rowptr.astype(np.int64))
+    has_out = int(np.count_nonzero(deg))
+    assert has_out < csr.n                        # R-MAT leaves isolated vertices
+    for k in (1, 2, 8):
+        perm, g, b = interleaved_relabel(csr, k)
+        live = live_rows(g, b)
+        assert live is not None and int(live.sum()) == has_out
+        gdeg = np.diff(g.rowptr.astype(np.int64))
+        b = b.astype(np.int64)
+        for j in range(k):
+            seg = gdeg[b[j]:b[j + 1]]
+            assert (seg[:int(live[j])] > 0).all() and (seg[int(live[j]):] == 0).all()
+        chunk = (int(live.max()) + 1 + 31) // 32 * 32
+        assert k * chunk <= has_out + 33 * k          # vs ~n with every row exchanged
+        _, hub = hub_relabel(csr)
+        assert live_rows(hub, partition_rows(hub.rowptr, k)) is not None
+    # an order that interleaves dangling rows with live ones has no live prefix
+    order = np.argsort(deg, kind="stable")[::-1].copy()
+    order[[0, -1]] = order[[-1, 0]]
+    from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import relabel
+    _, bad = relabel(csr, order)
+    assert live_rows(bad, np.array([0, csr.n], dtype=np.uint64)) is None
+
+
 def test_hub_relabel_is_isomorphic():
     csr = rmat(10, 8, 2)
     perm, hub = hub_relabel(csr)
@@ -173,8 +205,10 @@ def test_gloo_world2_matches_oracle(pieces, layout):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nranks", [1, 2, 3])
-def test_gpu_partition_api_simulated_ranks(nranks):
-    """gx_pr_part_* with `nranks` parts on one device; the exchange is a device concat."""
+@pytest.mark.parametrize("live", [True, False])
+def test_gpu_partition_api_simulated_ranks(nranks, live):
+    """gx_pr_part_* with `nranks` parts on one device; the exchange is a device concat.
+    live: only the rows with out-edges are exchanged (gx_pr_part_create_live); else all."""
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
     from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import GpuStep
     csr = rmat(13, 16, 11)
@@ -184,6 +218,8 @@ def test_gpu_partition_api_simulated_ranks(nranks):
     steps, lrs = [], []
     for r in range(nranks):
         lr = local_rows(hub, directed=False, nranks=nranks, rank=r)
+        if not live:
+            lr.live = None
         lrs.append(lr)
         steps.append(GpuStep(ctx, csr.n, nranks, lr, 0.85))
     chunk = steps[0].chunk
