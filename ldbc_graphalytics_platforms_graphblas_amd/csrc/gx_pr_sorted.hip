@@ -614,7 +614,8 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     // (interleaved rounds), one workgroup each, one workgroup per CU; rows longer than
     // block_nnz / 4 take the LONG path.  block_nnz = 1 Mi with 4 Ki rows, 4 Mi once nnz / CUs
     // passes 384 Ki, 8 Mi with 16 Ki rows once it passes 2 Mi, at most 4x the power of two
-    // nearest nnz / CUs; T is chosen below by simulating the launch
+    // nearest nnz / CUs; T is a quarter block, or past 2 Mi entries per CU chosen below by
+    // simulating the launch
     // (pr_unit_makespan).  GX_PR_BLOCK_NNZ, GX_PR_SORTED_ROWS, GX_PR_LONG_NNZ, GX_PR_UNIT_NNZ
     // override.  Measured (tools/pr_units_sweep.sh, us per launch; round 1's 64 Ki
     // single-workgroup blocks in brackets): SYN-7_5 100 [140]; graph500-22 267 [384]; SYN-8_5
@@ -800,6 +801,11 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     if (p->units_mode && !sortb.empty()) {
         if (std::getenv("GX_PR_UNIT_NNZ")) {
             T = env_int("GX_PR_UNIT_NNZ", 65536, 1024, 1 << 30);
+        } else if (!huge) {
+            // a quarter block: measured best on SYN-7_5 (256 Ki of 1 Mi: 100 us per launch;
+            // 232 Ki: 130) and on its 1/8 partition (32 Ki of 128 Ki: 33.5 us; the simulation's
+            // choice, 24 Ki: 38.8; 64 Ki: 47.7; tools/pr_piece_sweep.sh)
+            T = std::max<int64_t>(round, (B / 4 + round - 1) / round * round);
         } else {
             // the unit size whose simulated launch is shortest, over multiples of a round
             std::vector<int64_t> ents, rws, lsegs;
