@@ -105,7 +105,9 @@ int gx_rmat_csr(int scale, int edgefactor, double a, double b, double c, uint64_
 /* ---- device graph ------------------------------------------------------------ */
 
 /* Uploads A to HBM (int64 row pointers, int32 column indices when n < 2^31).
- * Replaces LAGraph_New(&G, &A, kind) (bfs.cpp:78). */
+ * Replaces LAGraph_New(&G, &A, kind) (bfs.cpp:78).  A row must not hold the same column
+ * twice (a GrB_Matrix cannot; gx_read_grb/_mtx and gx_rmat_csr never produce it): CDLP's first
+ * iteration on an undirected graph relies on it. */
 int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **g);
 int gx_graph_free(gx_graph *g);
 int gx_graph_info(gx_graph *g, uint64_t *n, uint64_t *nnz, int *directed, int *weighted);

@@ -47,11 +47,59 @@ struct CdlpArgs {
     int64_t n;
     int *changed;
     int64_t v0, v1;       // vertices updated by this call (the whole graph, or one rank's range)
+    // active set (gx_cdlp, from the third iteration): a vertex none of whose neighbours changed
+    // label in the previous iteration keeps its label, so only vertices with act[v] == stamp
+    // are recomputed, unless *dense (too many changes) or act is null (every vertex)
+    const int32_t *act;
+    int32_t stamp;
+    const int *dense;
+    // first iteration of an undirected graph: labels are still the vertex ids, so every label
+    // occurs once and the result is the smallest neighbour label (the fork's
+    // cdlp_first_iteration_findmin, cdlp_kernel.cu:76-116, without its directed-graph error)
+    int first;
 };
+
+// Uniform per launch: whether every vertex is recomputed.
+__device__ __forceinline__ bool all_active(const CdlpArgs &a) { return !a.act || *a.dense; }
+
+__device__ __forceinline__ bool active(const CdlpArgs &a, bool all, int64_t v) { return all || a.act[v] == a.stamp; }
 
 __device__ __forceinline__ int32_t label_at(const CdlpArgs &a, int64_t ob, int64_t od, int64_t ib,
                                             int64_t k) {
     return k < od ? a.lab[a.ciA[ob + k]] : a.lab[a.ciT[ib + (k - od)]];
+}
+
+// Where a vertex's labels come from: out-edges [ob, ob + od) of A, then in-edges [ib, ib + id)
+// of A' (directed graphs).
+struct VMeta {
+    int64_t ob, ib;
+    int32_t od, id;
+};
+
+__device__ __forceinline__ VMeta vmeta(const CdlpArgs &a, int64_t v) {
+    VMeta m;
+    m.ob = a.rpA[v];
+    m.od = (int32_t)(a.rpA[v + 1] - m.ob);
+    m.ib = 0;
+    m.id = 0;
+    if (a.rpT) {
+        m.ib = a.rpT[v];
+        m.id = (int32_t)(a.rpT[v + 1] - m.ib);
+    }
+    return m;
+}
+
+// An inactive vertex reads as degree 0 (no label loads; it keeps its label).
+__device__ __forceinline__ VMeta vmeta_act(const CdlpArgs &a, bool all, int64_t v) {
+    if (active(a, all, v)) return vmeta(a, v);
+    VMeta m;
+    m.ob = m.ib = 0;
+    m.od = m.id = 0;
+    return m;
+}
+
+__device__ __forceinline__ int32_t col_at(const CdlpArgs &a, const VMeta &m, int64_t k) {
+    return k < m.od ? a.ciA[m.ob + k] : a.ciT[m.ib + (k - m.od)];
 }
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t l, int log2ts) {
@@ -107,6 +155,54 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     return v;
 }
 
+// ---- strict-majority fast path -------------------------------------------------------
+// A label held by more than half of a vertex's d neighbours is its unique most frequent
+// label, so it is the CDLP result whatever the tie rule.  Boyer-Moore voting finds the only
+// possible candidate in one pass; pairwise merges of (candidate, count) in any order keep it
+// (each merge cancels pairs of different labels); counting the candidate exactly then
+// decides.  Once CDLP labels settle, almost every vertex has such a label (SYN-7_5 from the
+// third iteration on: every vertex of degree > 16, 61 % of those <= 16), and the hash table,
+// the shuffle counts or the register compares are skipped.
+struct Vote {
+    uint32_t c;   // candidate label (kEmpty: none)
+    uint32_t n;   // surplus
+};
+
+__device__ __forceinline__ Vote vote_add(Vote v, uint32_t l, bool valid) {
+    if (!valid) return v;
+    if (v.n == 0) return {l, 1u};
+    return v.c == l ? Vote{v.c, v.n + 1u} : Vote{v.c, v.n - 1u};
+}
+
+__device__ __forceinline__ Vote vote_merge(Vote a, Vote b) {
+    if (a.c == b.c) return {a.c, a.n + b.n};
+    return a.n >= b.n ? Vote{a.c, a.n - b.n} : Vote{b.c, b.n - a.n};
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor(v, off, kWave));
+    return v;
+}
+
+// Merge down to lane 0 (xor butterflies would leave different candidates in different lanes).
+__device__ __forceinline__ Vote wave_vote(Vote v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        Vote o;
+        o.c = __shfl_down(v.c, off, kWave);
+        o.n = __shfl_down(v.n, off, kWave);
+        v = vote_merge(v, o);
+    }
+    return v;
+}
+
 // Tiny vertices (deg <= kTiny, including isolated ones): one THREAD per vertex, labels in
 // registers (clamped loads, all in flight), mode by register compares -- 64 vertices per wave
 // instead of one (two thirds of the vertices of a power-law graph have degree <= 8).
@@ -114,6 +210,7 @@ constexpr int kTiny = 16;
 
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
     bool any = false;
+    const bool all = all_active(a);
     for (int64_t v = a.v0 + (int64_t)blockIdx.x * kCdlpBlock + threadIdx.x; v < a.v1;
          v += (int64_t)gridDim.x * kCdlpBlock) {
         const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
@@ -126,22 +223,37 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
         if (d > kTiny) continue;
         const int32_t old = a.lab[v];
         int32_t best = old;
-        if (d > 0) {
+        if (d > 0 && active(a, all, v)) {
             uint32_t L[kTiny];
 #pragma unroll
             for (int k = 0; k < kTiny; k++) L[k] = (uint32_t)label_at(a, ob, od, ib, min((int64_t)k, d - 1));
-            uint32_t bc = 0, bl = kEmpty;
+            Vote vt{kEmpty, 0u};
 #pragma unroll
-            for (int i = 0; i < kTiny; i++) {
-                uint32_t c = 0;
+            for (int k = 0; k < kTiny; k++) vt = vote_add(vt, L[k], k < d);
+            uint32_t nc = 0;
 #pragma unroll
-                for (int j = 0; j < kTiny; j++) c += (j < d && L[j] == L[i]) ? 1u : 0u;
-                if (i < d && (c > bc || (c == bc && L[i] < bl))) {
-                    bc = c;
-                    bl = L[i];
+            for (int k = 0; k < kTiny; k++) nc += (k < d && L[k] == vt.c) ? 1u : 0u;
+            if (a.first) {
+                uint32_t mn = kEmpty;
+#pragma unroll
+                for (int k = 0; k < kTiny; k++) mn = k < d ? min(mn, L[k]) : mn;
+                best = (int32_t)mn;
+            } else if (2 * (int64_t)nc > d) {
+                best = (int32_t)vt.c;   // strict majority
+            } else {
+                uint32_t bc = 0, bl = kEmpty;
+#pragma unroll
+                for (int i = 0; i < kTiny; i++) {
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int j = 0; j < kTiny; j++) c += (j < d && L[j] == L[i]) ? 1u : 0u;
+                    if (i < d && (c > bc || (c == bc && L[i] < bl))) {
+                        bc = c;
+                        bl = L[i];
+                    }
                 }
+                best = (int32_t)bl;
             }
-            best = (int32_t)bl;
         }
         a.nxt[v] = best;
         any |= best != old;
@@ -157,21 +269,28 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
     const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
     bool any = false;
+    const bool all = all_active(a);
     for (int64_t i = gw; i < nsmall; i += nw) {
         const int64_t v = sv[i];
-        const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
-        int64_t ib = 0, id = 0;
-        if (a.rpT) {
-            ib = a.rpT[v];
-            id = a.rpT[v + 1] - ib;
-        }
+        const VMeta m = vmeta_act(a, all, v);
+        const int64_t ob = m.ob, od = m.od, ib = m.ib, id = m.id;
         const int64_t d = od + id;
         const int32_t old = a.lab[v];
         const uint32_t my = lane < d ? (uint32_t)label_at(a, ob, od, ib, lane) : kEmpty;
-        uint32_t c = 0;
-        for (int j = 0; j < d; j++) c += (__shfl(my, j, kWave) == my) ? 1u : 0u;
-        const unsigned long long key = lane < d ? pack(c, my) : 0ull;
-        const int32_t best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+        const uint32_t cand = __shfl(wave_vote(Vote{my, lane < d ? 1u : 0u}).c, 0, kWave);
+        int32_t best;
+        if (d == 0) {
+            best = old;   // inactive (or isolated)
+        } else if (a.first) {
+            best = (int32_t)wave_min_u32(my);
+        } else if (2 * (int64_t)__popcll(__ballot(lane < d && my == cand)) > d) {
+            best = (int32_t)cand;   // strict majority
+        } else {
+            uint32_t c = 0;
+            for (int j = 0; j < d; j++) c += (__shfl(my, j, kWave) == my) ? 1u : 0u;
+            const unsigned long long key = lane < d ? pack(c, my) : 0ull;
+            best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+        }
         if (lane == 0) {
             a.nxt[v] = best;
             any |= best != old;
@@ -180,44 +299,60 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
     if (any) raise_flag(a.changed);
 }
 
-// Light vertices (64 < deg <= kSlots/2), from a list: one wave per vertex. Two instances:
-// kLightSlots for deg <= kLightSlots/2 (2 KiB per wave, so LDS does not cap occupancy) and
-// kLdsHash for the rest.
+// Light vertices (64 < deg <= kSlots/2), from a list: one wave per vertex, an LDS hash table of
+// 2 deg slots per wave.  Two instances: kLightSlots for deg <= kLightSlots/2 (2 KiB per wave,
+// so LDS does not cap occupancy) and kLdsHash for the rest.
 template <int kSlots>
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int32_t *__restrict__ lv,
                                                            int32_t nlight) {
     __shared__ uint32_t keys[kCdlpBlock / kWave][kSlots];
     __shared__ uint32_t cnts[kCdlpBlock / kWave][kSlots];
+    constexpr int R = kSlots / (2 * kWave);   // label rounds of the largest vertex of the tier
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     uint32_t *K = keys[wv];
     uint32_t *C = cnts[wv];
-    const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
+    int64_t i = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
+    if (i >= nlight) return;
     bool any = false;
-    for (int64_t i = gw; i < nlight; i += nw) {
-        const int64_t v = lv[i];
-        const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
-        int64_t ib = 0, id = 0;
-        if (a.rpT) {
-            ib = a.rpT[v];
-            id = a.rpT[v + 1] - ib;
-        }
-        const int64_t d = od + id;
+    const bool all = all_active(a);
+    // software-pipelined over the wave's vertices like k_cdlp_mid: the next vertex's
+    // dependent loads are issued one link at a time between this vertex's LDS phases
+    int64_t v = lv[i];
+    VMeta m = vmeta_act(a, all, v);
+    uint32_t L[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int64_t k = (int64_t)r * kWave + lane;
+        L[r] = k < (int64_t)m.od + m.id ? (uint32_t)a.lab[col_at(a, m, k)] : kEmpty;
+    }
+    for (;;) {
+        const int64_t d = (int64_t)m.od + m.id;
+        const int64_t inext = i + nw;
+        const bool more = inext < nlight;
+        const int64_t vn = more ? (int64_t)lv[inext] : v;      // next vertex, link 1
         const int32_t old = a.lab[v];
-        int32_t best;
-        if (d == 0) {
-            best = old;
-        } else if (d <= kWave) {
-            const uint32_t my = lane < d ? (uint32_t)label_at(a, ob, od, ib, lane) : kEmpty;
-            uint32_t c = 0;
-            for (int j = 0; j < d; j++) c += (__shfl(my, j, kWave) == my) ? 1u : 0u;
-            const unsigned long long key = lane < d ? pack(c, my) : 0ull;
-            best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
-        } else {
-            int log2ts = 1;
-            while ((1ll << log2ts) < 2 * d) log2ts++;
-            const int ts = 1 << log2ts;
+        // strict-majority fast path (a wave-uniform branch)
+        Vote vt{kEmpty, 0u};
+#pragma unroll
+        for (int r = 0; r < R; r++) vt = vote_add(vt, L[r], (int64_t)r * kWave + lane < d);
+        uint32_t cand = __shfl(wave_vote(vt).c, 0, kWave);
+        int64_t nc = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            if ((int64_t)r * kWave < d) nc += __popcll(__ballot((int64_t)r * kWave + lane < d && L[r] == cand));
+        if (a.first) {
+            uint32_t mn = kEmpty;
+#pragma unroll
+            for (int r = 0; r < R; r++) mn = (int64_t)r * kWave + lane < d ? min(mn, L[r]) : mn;
+            cand = wave_min_u32(mn);
+        }
+        const bool maj = 2 * nc > d || a.first || d == 0;   // d == 0: inactive, keeps its label
+        int log2ts = 1;
+        while ((1ll << log2ts) < 2 * d) log2ts++;
+        const int ts = 1 << log2ts;
+        if (!maj) {
             for (int s = lane; s < ts; s += kWave) {
                 K[s] = kEmpty;
                 C[s] = 0;
@@ -225,22 +360,25 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // all of the vertex's label gathers in flight before the first insert (the
-            // atomics would otherwise order one round's gathers behind the last one's inserts)
-            constexpr int R = kSlots / (2 * kWave);
-            uint32_t L[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int64_t k = (int64_t)r * kWave + lane;
-                L[r] = k < d ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
-            }
+        }
+        const VMeta mn = vmeta_act(a, all, vn);                 // link 2
+        const int64_t dn = more ? (int64_t)mn.od + mn.id : 0;
+        if (!maj) {
 #pragma unroll
             for (int r = 0; r < R; r++)
                 if ((int64_t)r * kWave < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kWave + lane < d, log2ts);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            unsigned long long key = 0;
+        }
+        int32_t cn[R];                                          // link 3
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int64_t k = (int64_t)r * kWave + lane;
+            cn[r] = k < dn ? col_at(a, mn, k) : -1;
+        }
+        unsigned long long key = 0;
+        if (!maj) {
             for (int s = lane; s < ts; s += kWave) {
                 const uint32_t c = C[s];
                 if (c) {
@@ -248,7 +386,13 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
                     key = kk > key ? kk : key;
                 }
             }
-            best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) L[r] = cn[r] >= 0 ? (uint32_t)a.lab[cn[r]] : kEmpty;   // link 4
+        const int32_t best = d == 0 ? old
+                             : maj ? (int32_t)cand
+                                   : (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+        if (!maj) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -257,6 +401,10 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
             a.nxt[v] = best;
             any |= best != old;
         }
+        if (!more) break;
+        i = inext;
+        v = vn;
+        m = mn;
     }
     if (any) raise_flag(a.changed);
 }
@@ -274,13 +422,15 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
                                                                  const int32_t *__restrict__ hlog2,
                                                                  const int32_t *__restrict__ cvert,
                                                                  const int64_t *__restrict__ cbeg,
-                                                                 uint32_t *gkeys, uint32_t *gcnts) {
+                                                                 uint32_t *gkeys, uint32_t *gcnts,
+                                                                 unsigned long long *vkey) {
     __shared__ uint32_t K[kHugeSlots];
     __shared__ uint32_t C[kHugeSlots];
     constexpr int kLog2 = 13;   // log2(kHugeSlots)
     const int tid = threadIdx.x;
     const int32_t hi = cvert[blockIdx.x];
     const int64_t v = hv[hi];
+    if (!active(a, all_active(a), v)) return;   // its tables stay clean; k_cdlp_huge_final keeps the label
     const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
     int64_t ib = 0, id = 0;
     if (a.rpT) {
@@ -299,6 +449,14 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
     for (int r = 0; r < R; r++) {
         const int64_t k = k0 + (int64_t)r * kHugeBlock + tid;
         L[r] = k < k1 ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
+    }
+    if (a.first) {   // the chunk's smallest label, as a count-1 key (no tables)
+        uint32_t mn = kEmpty;
+#pragma unroll
+        for (int r = 0; r < R; r++) mn = k0 + (int64_t)r * kHugeBlock + tid < k1 ? min(mn, L[r]) : mn;
+        mn = wave_min_u32(mn);
+        if ((tid & (kWave - 1)) == 0 && mn != kEmpty) atomicMax(&vkey[hi], pack(1u, mn));
+        return;
     }
 #pragma unroll
     for (int r = 0; r < R; r++)
@@ -329,13 +487,16 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
 // every slot read is reset, so the tables are clean for the next iteration without a memset.
 constexpr int64_t kHugeSeg = 16384;
 
-__global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_reduce(const int32_t *__restrict__ sv,
+__global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_reduce(CdlpArgs a, const int32_t *__restrict__ hv,
+                                                                 const int32_t *__restrict__ sv,
                                                                  const int64_t *__restrict__ sbeg,
                                                                  const int64_t *__restrict__ hoff,
                                                                  const int32_t *__restrict__ hlog2, uint32_t *gkeys,
                                                                  uint32_t *gcnts, unsigned long long *vkey) {
     __shared__ unsigned long long red[kHugeBlock / kWave];
     const int32_t hi = sv[blockIdx.x];
+    // first iteration: the key is final already; inactive vertex: its tables were not touched
+    if (a.first || !active(a, all_active(a), hv[hi])) return;
     const int64_t ts = 1ll << hlog2[hi];
     const int64_t s0 = sbeg[blockIdx.x], s1 = min(s0 + kHugeSeg, ts);
     uint32_t *GK = gkeys + hoff[hi];
@@ -364,7 +525,8 @@ __global__ void k_cdlp_huge_final(CdlpArgs a, const int32_t *__restrict__ hv, in
                                   unsigned long long *vkey) {
     for (int32_t hi = blockIdx.x * blockDim.x + threadIdx.x; hi < nhuge; hi += gridDim.x * blockDim.x) {
         const int64_t v = hv[hi];
-        const int32_t best = (int32_t)(kEmpty - (uint32_t)(vkey[hi] & 0xffffffffu));
+        const int32_t best = active(a, all_active(a), v) ? (int32_t)(kEmpty - (uint32_t)(vkey[hi] & 0xffffffffu))
+                                                         : a.lab[v];
         vkey[hi] = 0;   // clean for the next iteration
         a.nxt[v] = best;
         if (best != a.lab[v]) raise_flag(a.changed);
@@ -376,12 +538,10 @@ __global__ void k_cdlp_fill_u32(uint32_t *p, uint32_t v, int64_t n) {
         p[i] = v;
 }
 
-// Medium vertices (kLdsHash/2 < deg <= kMidMax): one 1024-thread workgroup per vertex with a
-// 16K-slot hash table in LDS (128 KiB, one workgroup per CU); workgroups loop over the
-// medium-vertex list so the table is reused without a relaunch.
-// Two sizes: 1024 threads / 16K slots (128 KiB, one workgroup per CU) for deg <= 8192, and
-// 256 threads / 4K slots (32 KiB, four workgroups per CU) for deg <= 2048, which keeps four
-// vertices in flight per CU for the many mid vertices near the bottom of the range.
+// Medium-tier shapes (k_cdlp_mid below): 1024 threads / 16K slots (128 KiB, one workgroup
+// per CU) for deg <= 8192, 512 / 8K for deg <= 4096 and 256 / 4K (32 KiB, four workgroups per
+// CU) for deg <= 2048, which keeps four vertices in flight per CU for the many mid vertices
+// near the bottom of the range.
 constexpr int kMidBlock = 1024;
 constexpr int kMidSlots = 16384;
 constexpr int64_t kMidMax = kMidSlots / 2;
@@ -392,61 +552,142 @@ constexpr int kMid4Block = 512;   // deg <= 4096: 8K slots (64 KiB), two workgro
 constexpr int kMid4Slots = 8192;
 constexpr int64_t kMid4Max = kMid4Slots / 2;
 
+// Medium vertices (kLdsHash/2 < deg <= kMidSlots/2): one workgroup per vertex with a
+// kMidSlots-slot hash table in LDS; workgroups loop over the medium-vertex list so the table
+// is reused without a relaunch.  Three sizes (kMid2 / kMid4 / kMid): 256 threads, 4K slots,
+// 4 per CU; 512, 8K, 2 per CU; 1024, 16K, 1 per CU.
+// Software-pipelined over the list: a vertex's labels sit at the end of a chain of dependent
+// loads (list -> row pointers -> column ids -> labels, ~1 us each), so the next vertex's chain
+// is issued one link at a time between the current vertex's LDS phases (clear, insert, scan):
+// each load's wait lands after the LDS work that follows its issue.
 template <int kMidBlock, int kMidSlots>
 __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_t *__restrict__ mv, int32_t nmid) {
     __shared__ uint32_t K[kMidSlots];
     __shared__ uint32_t C[kMidSlots];
     __shared__ unsigned long long red[kMidBlock / kWave];
+    __shared__ uint32_t cnt[kMidBlock / kWave];
+    __shared__ uint32_t bcast[1];
+    constexpr int R = kMidSlots / (2 * kMidBlock);
     const int tid = threadIdx.x;
     bool any = false;
-    for (int32_t i = blockIdx.x; i < nmid; i += gridDim.x) {
-        const int64_t v = mv[i];
-        const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
-        int64_t ib = 0, id = 0;
-        if (a.rpT) {
-            ib = a.rpT[v];
-            id = a.rpT[v + 1] - ib;
+    int32_t i = blockIdx.x;
+    if (i >= nmid) return;
+    const bool all = all_active(a);
+    int64_t v = mv[i];
+    VMeta m = vmeta_act(a, all, v);
+    uint32_t L[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int64_t k = (int64_t)r * kMidBlock + tid;
+        L[r] = k < (int64_t)m.od + m.id ? (uint32_t)a.lab[col_at(a, m, k)] : kEmpty;
+    }
+    for (;;) {
+        const int64_t d = (int64_t)m.od + m.id;
+        const int32_t inext = i + (int32_t)gridDim.x;
+        const bool more = inext < nmid;
+        // link 1 of the next vertex: its id
+        const int64_t vn = more ? (int64_t)mv[inext] : v;
+        // strict-majority fast path: the workgroup's candidate, then its exact count (the
+        // first iteration of an undirected graph: the smallest label).  d, a.first and so the
+        // branches are the same in every thread; an inactive vertex (d == 0) skips it all.
+        uint32_t cand = kEmpty;
+        bool maj = true;
+        if (d > 0 && a.first) {
+            uint32_t mn = kEmpty;
+#pragma unroll
+            for (int r = 0; r < R; r++) mn = (int64_t)r * kMidBlock + tid < d ? min(mn, L[r]) : mn;
+            mn = wave_min_u32(mn);
+            if ((tid & (kWave - 1)) == 0) cnt[tid / kWave] = mn;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kMidBlock / kWave; j++) cand = min(cand, cnt[j]);
+        } else if (d > 0) {
+            Vote vt{kEmpty, 0u};
+#pragma unroll
+            for (int r = 0; r < R; r++) vt = vote_add(vt, L[r], (int64_t)r * kMidBlock + tid < d);
+            vt = wave_vote(vt);
+            if ((tid & (kWave - 1)) == 0) red[tid / kWave] = ((unsigned long long)vt.c << 32) | vt.n;
+            __syncthreads();
+            if (tid == 0) {
+                Vote w{(uint32_t)(red[0] >> 32), (uint32_t)red[0]};
+                for (int j = 1; j < kMidBlock / kWave; j++) w = vote_merge(w, Vote{(uint32_t)(red[j] >> 32), (uint32_t)red[j]});
+                bcast[0] = w.c;
+            }
+            __syncthreads();
+            cand = bcast[0];
+            uint32_t mc = 0;
+#pragma unroll
+            for (int r = 0; r < R; r++) mc += ((int64_t)r * kMidBlock + tid < d && L[r] == cand) ? 1u : 0u;
+            mc = wave_sum_u32(mc);
+            if ((tid & (kWave - 1)) == 0) cnt[tid / kWave] = mc;
+            __syncthreads();
+            uint32_t nc = 0;
+#pragma unroll
+            for (int j = 0; j < kMidBlock / kWave; j++) nc += cnt[j];
+            maj = 2 * (int64_t)nc > d;
         }
-        const int64_t d = od + id;
         int log2ts = 1;
         while ((1ll << log2ts) < 2 * d) log2ts++;
         const int ts = 1 << log2ts;
-        for (int s = tid; s < ts; s += kMidBlock) {
-            K[s] = kEmpty;
-            C[s] = 0;
+        if (!maj) {
+            for (int s = tid; s < ts; s += kMidBlock) {
+                K[s] = kEmpty;
+                C[s] = 0;
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        // all of the vertex's label gathers in flight before the first insert
-        constexpr int R = kMidSlots / (2 * kMidBlock);
-        uint32_t L[R];
+        // link 2: its row pointers
+        const VMeta mn = vmeta_act(a, all, vn);
+        const int64_t dn = more ? (int64_t)mn.od + mn.id : 0;
+        if (!maj) {
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if ((int64_t)r * kMidBlock < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kMidBlock + tid < d, log2ts);
+            __syncthreads();
+        }
+        // link 3: its column ids
+        int32_t cn[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const int64_t k = (int64_t)r * kMidBlock + tid;
-            L[r] = k < d ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
+            cn[r] = k < dn ? col_at(a, mn, k) : -1;
         }
-#pragma unroll
-        for (int r = 0; r < R; r++)
-            if ((int64_t)r * kMidBlock < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kMidBlock + tid < d, log2ts);
-        __syncthreads();
         unsigned long long key = 0;
-        for (int s = tid; s < ts; s += kMidBlock) {
-            const uint32_t c = C[s];
-            if (c) {
-                const unsigned long long kk = pack(c, K[s]);
-                key = kk > key ? kk : key;
+        if (!maj) {
+            for (int s = tid; s < ts; s += kMidBlock) {
+                const uint32_t c = C[s];
+                if (c) {
+                    const unsigned long long kk = pack(c, K[s]);
+                    key = kk > key ? kk : key;
+                }
             }
         }
-        key = wave_max_u64(key);
-        if ((tid & (kWave - 1)) == 0) red[tid / kWave] = key;
-        __syncthreads();
-        if (tid == 0) {
-            unsigned long long m = red[0];
-            for (int w = 1; w < kMidBlock / kWave; w++) m = red[w] > m ? red[w] : m;
-            const int32_t best = (int32_t)(kEmpty - (uint32_t)(m & 0xffffffffu));
-            a.nxt[v] = best;
-            any |= best != a.lab[v];
+        // link 4: its labels
+#pragma unroll
+        for (int r = 0; r < R; r++) L[r] = cn[r] >= 0 ? (uint32_t)a.lab[cn[r]] : kEmpty;
+        if (maj) {
+            if (tid == 0) {
+                const int32_t best = d == 0 ? a.lab[v] : (int32_t)cand;
+                a.nxt[v] = best;
+                any |= best != a.lab[v];
+            }
+        } else {
+            key = wave_max_u64(key);
+            if ((tid & (kWave - 1)) == 0) red[tid / kWave] = key;
+            __syncthreads();
+            if (tid == 0) {
+                unsigned long long mx = red[0];
+                for (int w = 1; w < kMidBlock / kWave; w++) mx = red[w] > mx ? red[w] : mx;
+                const int32_t best = (int32_t)(kEmpty - (uint32_t)(mx & 0xffffffffu));
+                a.nxt[v] = best;
+                any |= best != a.lab[v];
+            }
         }
-        __syncthreads();   // the table is cleared for the next vertex
+        if (d > 0) __syncthreads();   // red / cnt / bcast and the table are free for the next vertex
+        if (!more) break;
+        i = inext;
+        v = vn;
+        m = mn;
     }
     if (any) raise_flag(a.changed);
 }
@@ -455,6 +696,62 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
 // 4-byte hipMemcpyAsync, which ran as a ~40 us blit kernel (profiles/r01_cdlp_kernel_stats.csv).
 __global__ void k_cdlp_flag_out(const int *__restrict__ changed, int *hflag) {
     if (threadIdx.x == 0) *hflag = *changed;
+}
+
+// Active set of the next iteration (gx_cdlp): the vertices whose label changed in the last
+// one (prev != cur) are listed, then every in- and out-neighbour of a listed vertex gets
+// act = stamp.  The list is kCdlpSubs sub-lists of `sub` entries, one per wave index mod
+// kCdlpSubs, each with its own counter (one counter for all serialised ~23 K wave atomics at
+// ~700 us on SYN-cit); more than `sub` changes in any sub-list -> *dense, every vertex is
+// recomputed.  SYN-7_5 from the fifth iteration on: ~500 changes and ~780 active vertices
+// (3 % of the entries) against 1 M vertices.
+constexpr int kCdlpSubs = 256;
+
+__global__ __launch_bounds__(256) void k_cdlp_changed(const int32_t *__restrict__ prev, const int32_t *__restrict__ cur,
+                                                      int64_t n, int32_t *list, int64_t sub, unsigned int *count) {
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t v0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~(kWave - 1)); v0 < n; v0 += (int64_t)gridDim.x * 256) {
+        const int64_t v = v0 + lane;
+        const bool ch = v < n && prev[v] != cur[v];
+        const unsigned long long m = __ballot(ch);
+        if (!m) continue;
+        const int j = (int)((v0 / kWave) & (kCdlpSubs - 1));
+        unsigned int base = 0;
+        if (lane == 0) {
+            // past capacity only the overflow matters: stop adding
+            base = __hip_atomic_load(&count[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (base <= (unsigned int)sub) base = atomicAdd(&count[j], (unsigned int)__popcll(m));
+        }
+        base = __shfl(base, 0, kWave);
+        const unsigned int idx = base + (unsigned int)__popcll(m & ((1ull << lane) - 1ull));
+        if (ch && idx < (unsigned int)sub) list[(int64_t)j * sub + idx] = (int32_t)v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cdlp_mark(const int64_t *__restrict__ rpA, const int32_t *__restrict__ ciA,
+                                                   const int64_t *__restrict__ rpT, const int32_t *__restrict__ ciT,
+                                                   const int32_t *__restrict__ list, int64_t sub,
+                                                   const unsigned int *count, int32_t *act, int32_t stamp,
+                                                   int *dense) {
+    __shared__ int over;
+    if (threadIdx.x == 0) over = 0;
+    __syncthreads();
+    if (count[threadIdx.x] > (unsigned int)sub) over = 1;   // kCdlpSubs == blockDim.x
+    __syncthreads();
+    if (over) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *dense = 1;
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *dense = 0;
+    for (int j = 0; j < kCdlpSubs; j++) {
+        const int64_t c = count[j];
+        for (int64_t i = blockIdx.x; i < c; i += gridDim.x) {
+            const int64_t u = list[(int64_t)j * sub + i];
+            for (int64_t e = rpA[u] + threadIdx.x; e < rpA[u + 1]; e += 256) act[ciA[e]] = stamp;
+            if (rpT)
+                for (int64_t e = rpT[u] + threadIdx.x; e < rpT[u + 1]; e += 256) act[ciT[e]] = stamp;
+        }
+    }
 }
 
 __global__ void k_cdlp_iota(int32_t *a, int64_t n) {
@@ -592,11 +889,12 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
 // (GX_CDLP_STREAMS=0: all on s).  Alone, each tier kept a CU at a fraction of its wave
 // slots: the workgroup-per-vertex tiers by their LDS tables, the others by their tails; side
 // by side, a CU holds a mid-tier workgroup and light/tiny waves at once.
-int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s) {
+int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
+                   const int32_t *act = nullptr, int32_t stamp = 0, const int *dense = nullptr, bool first = false) {
     gx_ctx *ctx = g->ctx;
     const int64_t n = (int64_t)g->n;
     CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr,
-               cur,       nxt,       n,      changed, P.v0, P.v1};
+               cur,       nxt,       n,      changed, P.v0, P.v1, act, stamp, dense, first && !g->directed ? 1 : 0};
     static const bool multi = [] {
         const char *e = std::getenv("GX_CDLP_STREAMS");
         return !e || std::atoi(e) != 0;
@@ -622,10 +920,10 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
     if (P.n_huge) {
         KTimer kt(ctx, "cdlp_heavy", s1);
         hipLaunchKernelGGL(k_cdlp_huge_insert, dim3((unsigned)P.n_chunks), dim3(kHugeBlock), 0, s1, a, P.d_hv.p,
-                           P.d_hoff.p, P.d_hl.p, P.d_cvert.p, P.d_cbeg.p, P.gk.p, P.gc.p);
+                           P.d_hoff.p, P.d_hl.p, P.d_cvert.p, P.d_cbeg.p, P.gk.p, P.gc.p, P.vkey.p);
         GX_TRY(check_launch("k_cdlp_huge_insert"));
-        hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)P.n_seg), dim3(kHugeBlock), 0, s1, P.d_segv.p,
-                           P.d_segb.p, P.d_hoff.p, P.d_hl.p, P.gk.p, P.gc.p, P.vkey.p);
+        hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)P.n_seg), dim3(kHugeBlock), 0, s1, a, P.d_hv.p,
+                           P.d_segv.p, P.d_segb.p, P.d_hoff.p, P.d_hl.p, P.gk.p, P.gc.p, P.vkey.p);
         GX_TRY(check_launch("k_cdlp_huge_reduce"));
         hipLaunchKernelGGL(k_cdlp_huge_final, dim3(grid_for(P.n_huge, 64, 1024)), dim3(64), 0, s1, a, P.d_hv.p,
                            (int32_t)P.n_huge, P.vkey.p);
@@ -683,6 +981,60 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
 
 using namespace gx;
 
+namespace gx {
+namespace {
+// What gx_cdlp keeps on the graph between calls (gx_graph::cdlp): the tier lists (built on
+// the host from the row pointers: ~3 ms of idle device per call on SYN-7_5 when rebuilt) and
+// the label, flag and active-set buffers.  Iteration-count-sized buffers grow on demand.
+struct CdlpCache {
+    CdlpPlan P;
+    DBuf<int32_t> la, lb, act, clist;
+    DBuf<int> changed, dense;
+    DBuf<unsigned int> ccount;
+    int *hflag = nullptr, *dflag = nullptr;
+    int cap_iters = 0;
+    int64_t sub = 0;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    ~CdlpCache() {
+        if (hflag) (void)hipHostFree(hflag);
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+int cdlp_cache(gx_graph *g, int iters, CdlpCache **out, hipStream_t s) {
+    const int64_t n = (int64_t)g->n;
+    auto *C = static_cast<CdlpCache *>(g->cdlp.get());
+    if (!C) {
+        auto fresh = std::make_shared<CdlpCache>();
+        GX_TRY(cdlp_plan(g, 0, n, fresh->P, s));
+        GX_TRY(fresh->la.alloc(n));
+        GX_TRY(fresh->lb.alloc(n));
+        GX_TRY(fresh->act.alloc(n));
+        fresh->sub = std::max<int64_t>(16, n / 32 / kCdlpSubs);   // entries per sub-list
+        GX_TRY(fresh->clist.alloc((size_t)fresh->sub * kCdlpSubs));
+        GX_TRY(fresh->dense.alloc(1));
+        GX_HIP_TRY(hipEventCreateWithFlags(&fresh->ev[0], hipEventDisableTiming));
+        GX_HIP_TRY(hipEventCreateWithFlags(&fresh->ev[1], hipEventDisableTiming));
+        g->cdlp = fresh;
+        C = fresh.get();
+    }
+    if (iters > C->cap_iters) {
+        const int cap = std::max(iters, 16);
+        GX_TRY(C->changed.alloc(cap));
+        GX_TRY(C->ccount.alloc((size_t)cap * kCdlpSubs));
+        if (C->hflag) (void)hipHostFree(C->hflag);
+        C->hflag = nullptr;
+        GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&C->hflag), sizeof(int) * cap, hipHostMallocMapped));
+        GX_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&C->dflag), C->hflag, 0));
+        C->cap_iters = cap;
+    }
+    *out = C;
+    return GX_SUCCESS;
+}
+}  // namespace
+}  // namespace gx
+
 extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     if (!g || !labels) return fail(GX_NULL_POINTER, "gx_cdlp: null argument");
     if (iters < 0) return fail(GX_INVALID_VALUE, "gx_cdlp: negative iteration count");
@@ -693,37 +1045,52 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     if (n == 0) return GX_SUCCESS;
     GX_TRY(device_begin(ctx));
     if (g->directed) GX_TRY(ensure_transpose(g));
-    CdlpPlan P;
-    GX_TRY(cdlp_plan(g, 0, n, P, s));
-    DBuf<int32_t> la, lb;
-    DBuf<int> changed;   // one flag per iteration
-    GX_TRY(la.alloc(n));
-    GX_TRY(lb.alloc(n));
-    GX_TRY(changed.alloc(std::max(iters, 1)));
-    GX_HIP_TRY(hipMemsetAsync(changed.p, 0, sizeof(int) * std::max(iters, 1), s));
-    hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, la.p, n);
+    CdlpCache *C = nullptr;
+    GX_TRY(cdlp_cache(g, std::max(iters, 1), &C, s));
+    CdlpPlan &P = C->P;
+    GX_HIP_TRY(hipMemsetAsync(C->changed.p, 0, sizeof(int) * std::max(iters, 1), s));
+    hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, C->la.p, n);
     GX_TRY(check_launch("k_cdlp_iota"));
     // Early exit at a fixed point (LAGraph_cdlp.c:328-332), checked one iteration late:
     // iteration it is queued before the host waits for iteration it-1's flag, so the check
     // never drains the stream.  An iteration run after a fixed point changes no label.
-    int *hflag = nullptr, *dflag = nullptr;
-    GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&hflag), sizeof(int) * std::max(iters, 1), hipHostMallocMapped));
-    std::unique_ptr<int, void (*)(int *)> hflag_guard(hflag, [](int *p) { (void)hipHostFree(p); });
-    GX_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&dflag), hflag, 0));
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    GX_HIP_TRY(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
-    GX_HIP_TRY(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
-    struct EvGuard {
-        hipEvent_t *e;
-        ~EvGuard() {
-            (void)hipEventDestroy(e[0]);
-            (void)hipEventDestroy(e[1]);
-        }
-    } ev_guard{ev};
-    int32_t *cur = la.p, *nxt = lb.p;
+    int *hflag = C->hflag, *dflag = C->dflag;
+    hipEvent_t *ev = C->ev;
+    // active set (GX_CDLP_ACTIVE=0: every vertex every iteration): from iteration 2 on, the
+    // changes of the last iteration are listed (up to n / 32 of them) and their neighbours
+    // marked with the iteration's stamp before the tier kernels run
+    static const bool use_active = [] {
+        const char *e = std::getenv("GX_CDLP_ACTIVE");
+        return !e || std::atoi(e) != 0;
+    }();
+    const bool active = use_active && iters > 2;
+    const int64_t sub = C->sub;
+    if (active) {
+        hipLaunchKernelGGL(k_cdlp_fill_u32, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s,
+                           reinterpret_cast<uint32_t *>(C->act.p), 0xffffffffu, n);   // stamp -1: never active
+        GX_TRY(check_launch("k_cdlp_fill_u32"));
+        GX_HIP_TRY(hipMemsetAsync(C->ccount.p, 0, sizeof(unsigned int) * kCdlpSubs * iters, s));
+    }
+    int32_t *cur = C->la.p, *nxt = C->lb.p;
     for (int it = 0; it < iters; it++) {
-        GX_TRY(cdlp_iteration(g, P, cur, nxt, changed.p + it, s));
-        hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(64), 0, s, changed.p + it, dflag + it);
+        int *changed = C->changed.p + it;
+        if (active && it >= 2) {
+            // nxt still holds the input of iteration it-1, cur its output
+            KTimer kt(ctx, "cdlp_mark", s);
+            unsigned int *cnt = C->ccount.p + (size_t)it * kCdlpSubs;
+            hipLaunchKernelGGL(k_cdlp_changed, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, nxt, cur, n, C->clist.p,
+                               sub, cnt);
+            GX_TRY(check_launch("k_cdlp_changed"));
+            hipLaunchKernelGGL(k_cdlp_mark, dim3(1024), dim3(kCdlpSubs), 0, s, g->A.rp.p, g->A.ci.p,
+                               g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr, C->clist.p, sub,
+                               cnt, C->act.p, (int32_t)it, C->dense.p);
+            GX_TRY(check_launch("k_cdlp_mark"));
+            GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p));
+        } else {
+            // iteration 0: labels are the vertex ids (k_cdlp_iota)
+            GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0));
+        }
+        hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(64), 0, s, changed, dflag + it);
         GX_TRY(check_launch("k_cdlp_flag_out"));
         GX_HIP_TRY(hipEventRecord(ev[it & 1], s));
         std::swap(cur, nxt);

@@ -346,3 +346,15 @@ def test_cdlp_tier_boundaries(ctx, directed):
     g = _G(csr, directed)
     for iters in (1, 3, 6):
         np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=iters), O.cdlp(csr, directed, iters))
+
+
+@pytest.mark.parametrize("active", ["1", "0"])
+def test_cdlp_active_set(ctx, monkeypatch, active):
+    """From the third iteration gx_cdlp recomputes only the neighbours of the last iteration's
+    changes (GX_CDLP_ACTIVE=0: every vertex): labels equal the oracle's at every count, on
+    graphs whose labels settle and on ones that keep oscillating (directed and undirected)."""
+    monkeypatch.setenv("GX_CDLP_ACTIVE", active)
+    for g in (_rmat(14, 16, 4), _rmat(12, 4, 8), _rmat(11, 8, 3, undirected=False), _G(_tier_graph(False), False),
+              _G(_tier_graph(True), True)):
+        for iters in (2, 3, 5, 12):
+            np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=iters), O.cdlp(g.csr, g.directed, iters))
