@@ -57,7 +57,14 @@ struct CdlpArgs {
     // occurs once and the result is the smallest neighbour label (the fork's
     // cdlp_first_iteration_findmin, cdlp_kernel.cu:76-116, without its directed-graph error)
     int first;
+    // sparse iteration: k_cdlp_sparse_wave / _group recompute the active vertices of degree
+    // <= kMidMax from the lists k_cdlp_mark built, and the tier kernels (the huge ones aside)
+    // have nothing to do unless *dense
+    int sparse;
+    int cshards;   // *changed is cshards words kFlagStride apart (raise_flag_sharded)
 };
+
+__device__ __forceinline__ bool tier_idle(const CdlpArgs &a) { return a.sparse && *a.dense == 0; }
 
 // Uniform per launch: whether every vertex is recomputed.
 __device__ __forceinline__ bool all_active(const CdlpArgs &a) { return !a.act || *a.dense; }
@@ -209,6 +216,7 @@ __device__ __forceinline__ Vote wave_vote(Vote v) {
 constexpr int kTiny = 16;
 
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
+    if (tier_idle(a)) return;
     bool any = false;
     const bool all = all_active(a);
     for (int64_t v = a.v0 + (int64_t)blockIdx.x * kCdlpBlock + threadIdx.x; v < a.v1;
@@ -258,13 +266,14 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
         a.nxt[v] = best;
         any |= best != old;
     }
-    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag(a.changed);
+    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag_sharded(a.changed, a.cshards);
 }
 
 // Small vertices (kTiny < deg <= 64), from a list: one wave per vertex, labels in registers,
 // counts by shuffles; no LDS, so the kernel runs at full occupancy.
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int32_t *__restrict__ sv,
                                                            int32_t nsmall) {
+    if (tier_idle(a)) return;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
@@ -296,7 +305,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
             any |= best != old;
         }
     }
-    if (any) raise_flag(a.changed);
+    if (any) raise_flag_sharded(a.changed, a.cshards);
 }
 
 // Light vertices (64 < deg <= kSlots/2), from a list: one wave per vertex, an LDS hash table of
@@ -305,6 +314,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
 template <int kSlots>
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int32_t *__restrict__ lv,
                                                            int32_t nlight) {
+    if (tier_idle(a)) return;
     __shared__ uint32_t keys[kCdlpBlock / kWave][kSlots];
     __shared__ uint32_t cnts[kCdlpBlock / kWave][kSlots];
     constexpr int R = kSlots / (2 * kWave);   // label rounds of the largest vertex of the tier
@@ -406,7 +416,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
         v = vn;
         m = mn;
     }
-    if (any) raise_flag(a.changed);
+    if (any) raise_flag_sharded(a.changed, a.cshards);
 }
 
 // Huge vertices (deg > kMidMax): the label multiset is cut into kHugeChunk-label chunks; a
@@ -529,7 +539,7 @@ __global__ void k_cdlp_huge_final(CdlpArgs a, const int32_t *__restrict__ hv, in
                                                          : a.lab[v];
         vkey[hi] = 0;   // clean for the next iteration
         a.nxt[v] = best;
-        if (best != a.lab[v]) raise_flag(a.changed);
+        if (best != a.lab[v]) raise_flag_sharded(a.changed, a.cshards);
     }
 }
 
@@ -562,6 +572,7 @@ constexpr int64_t kMid4Max = kMid4Slots / 2;
 // each load's wait lands after the LDS work that follows its issue.
 template <int kMidBlock, int kMidSlots>
 __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_t *__restrict__ mv, int32_t nmid) {
+    if (tier_idle(a)) return;
     __shared__ uint32_t K[kMidSlots];
     __shared__ uint32_t C[kMidSlots];
     __shared__ unsigned long long red[kMidBlock / kWave];
@@ -689,69 +700,355 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
         v = vn;
         m = mn;
     }
-    if (any) raise_flag(a.changed);
+    if (any) raise_flag_sharded(a.changed, a.cshards);
 }
 
 // The iteration's changed flag to pinned host memory: one lane's store over PCIe, instead of a
 // 4-byte hipMemcpyAsync, which ran as a ~40 us blit kernel (profiles/r01_cdlp_kernel_stats.csv).
-__global__ void k_cdlp_flag_out(const int *__restrict__ changed, int *hflag) {
-    if (threadIdx.x == 0) *hflag = *changed;
+__global__ void k_cdlp_flag_out(const int *__restrict__ changed, int shards, int *hflag) {
+    const int t = threadIdx.x;   // one lane per shard (shards <= kWave)
+    const bool set = t < shards && changed[t * kFlagStride] != 0;
+    const bool any = __ballot(set) != 0;
+    if (t == 0) *hflag = any ? 1 : 0;
 }
 
-// Active set of the next iteration (gx_cdlp): the vertices whose label changed in the last
-// one (prev != cur) are listed, then every in- and out-neighbour of a listed vertex gets
-// act = stamp.  The list is kCdlpSubs sub-lists of `sub` entries, one per wave index mod
-// kCdlpSubs, each with its own counter (one counter for all serialised ~23 K wave atomics at
-// ~700 us on SYN-cit); more than `sub` changes in any sub-list -> *dense, every vertex is
-// recomputed.  SYN-7_5 from the fifth iteration on: ~500 changes and ~780 active vertices
-// (3 % of the entries) against 1 M vertices.
+// Active set of the next iteration (gx_cdlp).  k_cdlp_changed lists the vertices whose label
+// changed in the last iteration (prev != cur), as chunks of kMarkChunk neighbours, and sets
+// prev = cur for them: prev (the buffer the iteration writes) then equals cur everywhere, so
+// a sparse iteration writes only its active vertices.  k_cdlp_mark gives every in- and
+// out-neighbour in a listed chunk act = stamp and appends each newly marked vertex of degree
+// <= kMidMax to one of three lists by degree (<= 512, <= 2048, <= 8192), which
+// k_cdlp_sparse_wave / k_cdlp_sparse_group recompute; huge vertices keep their tier kernels,
+// which skip inactive ones.  SYN-7_5 from the fifth iteration on: ~500 changes and ~780 active
+// vertices (3 % of the entries).
+// Every list is kCdlpSubs shards with a counter each, the counters kCntStride words apart:
+// device-scope atomics on one address serialise (one counter for all: ~23 K wave atomics,
+// ~700 us on SYN-cit), and so do counters that share a 128-byte line.  An overflowing shard
+// sets *dense, and the tier kernels recompute every vertex.
+// Shard j of a list is read by the waves (workgroups) w with w % kCdlpSubs == j: every
+// shard gets the same share of the grid (a whole-grid sweep of each shard in turn left all
+// but a few waves idle and cost a dependent-load chain per shard: ~120 us on SYN-7_5).
 constexpr int kCdlpSubs = 256;
+constexpr int kCntStride = 32;             // 128 bytes between two counters
+constexpr int kCdlpLists = 4;              // change chunks, then the three activation lists
+constexpr int64_t kMarkChunk = 2048;
+constexpr int64_t kSparseWaveMax = 512;    // wave per vertex, 1024-slot tables
+constexpr int64_t kSparseG2Max = kMid2Max; // 256-thread workgroup, 4K slots
+// the rest up to kMidMax: 1024-thread workgroup, 16K slots
 
-__global__ __launch_bounds__(256) void k_cdlp_changed(const int32_t *__restrict__ prev, const int32_t *__restrict__ cur,
-                                                      int64_t n, int32_t *list, int64_t sub, unsigned int *count) {
+__device__ __forceinline__ int64_t cdlp_degree(const int64_t *rpA, const int64_t *rpT, int64_t v) {
+    int64_t d = rpA[v + 1] - rpA[v];
+    if (rpT) d += rpT[v + 1] - rpT[v];
+    return d;
+}
+
+__device__ __forceinline__ unsigned int shard_count(const unsigned int *count, int j, int64_t cap) {
+    return (unsigned int)min((int64_t)count[j * kCntStride], cap);
+}
+
+// One reservation per workgroup and 256 vertices.
+__global__ __launch_bounds__(256) void k_cdlp_changed(int32_t *__restrict__ prev, const int32_t *__restrict__ cur,
+                                                      const int64_t *__restrict__ rpA, const int64_t *__restrict__ rpT,
+                                                      int64_t n, uint64_t *list, int64_t sub, unsigned int *count,
+                                                      int *dense) {
+    __shared__ uint32_t wtot[256 / kWave];
+    __shared__ uint32_t bbase;
     const int lane = threadIdx.x & (kWave - 1);
-    for (int64_t v0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~(kWave - 1)); v0 < n; v0 += (int64_t)gridDim.x * 256) {
-        const int64_t v = v0 + lane;
-        const bool ch = v < n && prev[v] != cur[v];
-        const unsigned long long m = __ballot(ch);
-        if (!m) continue;
-        const int j = (int)((v0 / kWave) & (kCdlpSubs - 1));
-        unsigned int base = 0;
-        if (lane == 0) {
-            // past capacity only the overflow matters: stop adding
-            base = __hip_atomic_load(&count[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (base <= (unsigned int)sub) base = atomicAdd(&count[j], (unsigned int)__popcll(m));
+    const int wv = threadIdx.x / kWave;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *dense = 0;   // k_cdlp_mark only ever raises it
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < n; b0 += (int64_t)gridDim.x * 256) {
+        const int64_t v = b0 + threadIdx.x;
+        const int32_t cv = v < n ? cur[v] : 0;
+        const bool ch = v < n && prev[v] != cv;
+        if (ch) prev[v] = cv;
+        const uint32_t chunks = ch ? (uint32_t)((cdlp_degree(rpA, rpT, v) + kMarkChunk - 1) / kMarkChunk) : 0u;
+        uint32_t pre = chunks;   // inclusive prefix within the wave
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const uint32_t t = __shfl_up(pre, off, kWave);
+            if (lane >= off) pre += t;
         }
-        base = __shfl(base, 0, kWave);
-        const unsigned int idx = base + (unsigned int)__popcll(m & ((1ull << lane) - 1ull));
-        if (ch && idx < (unsigned int)sub) list[(int64_t)j * sub + idx] = (int32_t)v;
+        if (lane == kWave - 1) wtot[wv] = pre;
+        pre -= chunks;
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < 256 / kWave; w++) {
+            const uint32_t t = wtot[w];
+            before += w < wv ? t : 0u;
+            total += t;
+        }
+        if (total) {
+            if (threadIdx.x == 0) {
+                const int j = (int)((b0 / 256) % kCdlpSubs);
+                unsigned int *cnt = count + j * kCntStride;
+                // past capacity only the overflow matters: stop adding
+                unsigned int base = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (base <= (unsigned int)sub) base = atomicAdd(cnt, total);
+                bbase = base;
+            }
+            __syncthreads();
+            const unsigned int base = bbase + before + pre;
+            const int j = (int)((b0 / 256) % kCdlpSubs);
+            for (uint32_t c = 0; c < chunks; c++)
+                if (base + c < (unsigned int)sub) list[(int64_t)j * sub + base + c] = ((uint64_t)v << 32) | c;
+        }
+        __syncthreads();   // wtot and bbase are free again
     }
 }
 
+// One wave per listed chunk; appends go to shard (wave index mod kCdlpSubs) of their list, one
+// reservation per wave, list and 64 neighbours.
 __global__ __launch_bounds__(256) void k_cdlp_mark(const int64_t *__restrict__ rpA, const int32_t *__restrict__ ciA,
                                                    const int64_t *__restrict__ rpT, const int32_t *__restrict__ ciT,
-                                                   const int32_t *__restrict__ list, int64_t sub,
-                                                   const unsigned int *count, int32_t *act, int32_t stamp,
-                                                   int *dense) {
+                                                   const uint64_t *__restrict__ list, int64_t sub,
+                                                   unsigned int *counts, int32_t *act, int32_t stamp, int *dense,
+                                                   int32_t *al, int64_t asub) {
     __shared__ int over;
     if (threadIdx.x == 0) over = 0;
     __syncthreads();
-    if (count[threadIdx.x] > (unsigned int)sub) over = 1;   // kCdlpSubs == blockDim.x
+    if (counts[threadIdx.x * kCntStride] > (unsigned int)sub) over = 1;   // kCdlpSubs == blockDim.x
     __syncthreads();
     if (over) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *dense = 1;
         return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *dense = 0;
-    for (int j = 0; j < kCdlpSubs; j++) {
-        const int64_t c = count[j];
-        for (int64_t i = blockIdx.x; i < c; i += gridDim.x) {
-            const int64_t u = list[(int64_t)j * sub + i];
-            for (int64_t e = rpA[u] + threadIdx.x; e < rpA[u + 1]; e += 256) act[ciA[e]] = stamp;
-            if (rpT)
-                for (int64_t e = rpT[u] + threadIdx.x; e < rpT[u + 1]; e += 256) act[ciT[e]] = stamp;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t gw = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave;
+    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);   // a multiple of kCdlpSubs
+    const int j = (int)(gw % kCdlpSubs);
+    const int64_t c = counts[j * kCntStride];
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int64_t i = gw / kCdlpSubs; i < c; i += nw / kCdlpSubs) {
+        const uint64_t e = list[(int64_t)j * sub + i];
+        const int64_t u = (int64_t)(e >> 32);
+        const int64_t ob = rpA[u], od = rpA[u + 1] - ob;
+        const int64_t ib = rpT ? rpT[u] : 0, id = rpT ? rpT[u + 1] - ib : 0;
+        const int64_t k0 = (int64_t)(uint32_t)e * kMarkChunk, k1 = min(k0 + kMarkChunk, od + id);
+        for (int64_t kb = k0; kb < k1; kb += kWave) {
+            const int64_t k = kb + lane;
+            int64_t w = -1;
+            if (k < k1) w = k < od ? ciA[ob + k] : ciT[ib + (k - od)];
+            const bool fresh = w >= 0 && atomicExch(&act[w], stamp) != stamp;
+            const int64_t dw = fresh ? cdlp_degree(rpA, rpT, w) : 0;
+            // activation list 1 + L: L = 0 (wave), 1 (256-thread group), 2 (1024-thread group)
+            const int L = !fresh || dw > kMidMax ? -1 : dw <= kSparseWaveMax ? 0 : dw <= kSparseG2Max ? 1 : 2;
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const unsigned long long m = __ballot(L == q);
+                if (!m) continue;
+                unsigned int b = 0;
+                if (lane == 0) b = atomicAdd(&counts[((1 + q) * kCdlpSubs + j) * kCntStride], (unsigned int)__popcll(m));
+                b = __shfl(b, 0, kWave);
+                if (L == q) {
+                    const unsigned int idx = b + (unsigned int)__popcll(m & below);
+                    if (idx < (unsigned int)asub) al[((int64_t)q * kCdlpSubs + j) * asub + idx] = (int32_t)w;
+                    else *dense = 1;
+                }
+            }
         }
     }
+}
+
+// Sparse iterations, active vertices of degree <= kSparseWaveMax: one wave each (the light
+// tier's method: strict-majority vote, else a 2d-slot LDS hash table).
+__global__ __launch_bounds__(256) void k_cdlp_sparse_wave(CdlpArgs a, const int32_t *__restrict__ wl, int64_t asub,
+                                                          const unsigned int *wcount) {
+    if (*a.dense) return;
+    constexpr int kSlots = 2 * kSparseWaveMax;
+    constexpr int R = kSparseWaveMax / kWave;
+    __shared__ uint32_t keys[256 / kWave][kSlots];
+    __shared__ uint32_t cnts[256 / kWave][kSlots];
+    const int lane = threadIdx.x & (kWave - 1);
+    uint32_t *K = keys[threadIdx.x / kWave];
+    uint32_t *C = cnts[threadIdx.x / kWave];
+    const int64_t gw = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave;
+    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);   // a multiple of kCdlpSubs
+    const int j = (int)(gw % kCdlpSubs);
+    const int64_t c = shard_count(wcount, j, asub);
+    bool any = false;
+    for (int64_t i = gw / kCdlpSubs; i < c; i += nw / kCdlpSubs) {
+        const int64_t v = wl[(int64_t)j * asub + i];
+        const VMeta m = vmeta(a, v);
+        const int64_t d = (int64_t)m.od + m.id;
+        uint32_t L[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int64_t k = (int64_t)r * kWave + lane;
+            L[r] = k < d ? (uint32_t)a.lab[col_at(a, m, k)] : kEmpty;
+        }
+        const int32_t old = a.lab[v];
+        Vote vt{kEmpty, 0u};
+#pragma unroll
+        for (int r = 0; r < R; r++) vt = vote_add(vt, L[r], (int64_t)r * kWave + lane < d);
+        const uint32_t cand = __shfl(wave_vote(vt).c, 0, kWave);
+        int64_t nc = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            if ((int64_t)r * kWave < d) nc += __popcll(__ballot((int64_t)r * kWave + lane < d && L[r] == cand));
+        int32_t best = old;
+        if (d > 0 && 2 * nc > d) {
+            best = (int32_t)cand;
+        } else if (d > 0) {
+            int log2ts = 1;
+            while ((1ll << log2ts) < 2 * d) log2ts++;
+            const int ts = 1 << log2ts;
+            for (int t = lane; t < ts; t += kWave) {
+                K[t] = kEmpty;
+                C[t] = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if ((int64_t)r * kWave < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kWave + lane < d, log2ts);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            unsigned long long key = 0;
+            for (int t = lane; t < ts; t += kWave) {
+                const uint32_t cc = C[t];
+                if (cc) {
+                    const unsigned long long kk = pack(cc, K[t]);
+                    key = kk > key ? kk : key;
+                }
+            }
+            best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane == 0) {
+            a.nxt[v] = best;
+            any |= best != old;
+        }
+    }
+    if (any) raise_flag_sharded(a.changed, a.cshards);
+}
+
+// Sparse iterations, active vertices of kSparseWaveMax < degree <= kMidMax: one workgroup each
+// with a kSlots-slot LDS table (the mid tier's method, without its pipelining).  Two shapes:
+// 256 threads / 4K slots (four workgroups per CU) up to kSparseG2Max, 1024 / 16K above.
+template <int kBlock, int kSlots>
+__global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const int32_t *__restrict__ gl,
+                                                              int64_t asub, const unsigned int *gcount) {
+    if (*a.dense) return;
+    __shared__ uint32_t K[kSlots];
+    __shared__ uint32_t C[kSlots];
+    __shared__ unsigned long long red[kBlock / kWave];
+    __shared__ uint32_t cnt[kBlock / kWave];
+    __shared__ uint32_t bcast[1];
+    constexpr int R = kSlots / (2 * kBlock);
+    constexpr int NW = kBlock / kWave;
+    const int tid = threadIdx.x;
+    const int j = (int)(blockIdx.x % kCdlpSubs);   // the grid is a multiple of kCdlpSubs
+    const int64_t c = shard_count(gcount, j, asub);
+    bool any = false;
+    for (int64_t i = blockIdx.x / kCdlpSubs; i < c; i += gridDim.x / kCdlpSubs) {
+        const int64_t v = gl[(int64_t)j * asub + i];
+        const VMeta m = vmeta(a, v);
+        const int64_t d = (int64_t)m.od + m.id;
+        uint32_t L[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int64_t k = (int64_t)r * kBlock + tid;
+            L[r] = k < d ? (uint32_t)a.lab[col_at(a, m, k)] : kEmpty;
+        }
+        Vote vt{kEmpty, 0u};
+#pragma unroll
+        for (int r = 0; r < R; r++) vt = vote_add(vt, L[r], (int64_t)r * kBlock + tid < d);
+        vt = wave_vote(vt);
+        if ((tid & (kWave - 1)) == 0) red[tid / kWave] = ((unsigned long long)vt.c << 32) | vt.n;
+        __syncthreads();
+        if (tid == 0) {
+            Vote w{(uint32_t)(red[0] >> 32), (uint32_t)red[0]};
+            for (int q = 1; q < NW; q++) w = vote_merge(w, Vote{(uint32_t)(red[q] >> 32), (uint32_t)red[q]});
+            bcast[0] = w.c;
+        }
+        __syncthreads();
+        const uint32_t cand = bcast[0];
+        uint32_t mc = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) mc += ((int64_t)r * kBlock + tid < d && L[r] == cand) ? 1u : 0u;
+        mc = wave_sum_u32(mc);
+        if ((tid & (kWave - 1)) == 0) cnt[tid / kWave] = mc;
+        __syncthreads();
+        uint32_t nc = 0;
+#pragma unroll
+        for (int q = 0; q < NW; q++) nc += cnt[q];
+        int32_t best = (int32_t)cand;
+        if (2 * (int64_t)nc <= d) {
+            int log2ts = 1;
+            while ((1ll << log2ts) < 2 * d) log2ts++;
+            const int ts = 1 << log2ts;
+            for (int t = tid; t < ts; t += kBlock) {
+                K[t] = kEmpty;
+                C[t] = 0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if ((int64_t)r * kBlock < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kBlock + tid < d, log2ts);
+            __syncthreads();
+            unsigned long long key = 0;
+            for (int t = tid; t < ts; t += kBlock) {
+                const uint32_t cc = C[t];
+                if (cc) {
+                    const unsigned long long kk = pack(cc, K[t]);
+                    key = kk > key ? kk : key;
+                }
+            }
+            key = wave_max_u64(key);
+            if ((tid & (kWave - 1)) == 0) red[tid / kWave] = key;   // red was last read before bcast
+            __syncthreads();
+            unsigned long long mx = red[0];
+            for (int q = 1; q < NW; q++) mx = red[q] > mx ? red[q] : mx;
+            best = (int32_t)(kEmpty - (uint32_t)(mx & 0xffffffffu));
+        }
+        if (tid == 0) {
+            const int32_t old = a.lab[v];
+            a.nxt[v] = best;
+            any |= best != old;
+        }
+        __syncthreads();   // red / cnt / bcast / the table are free for the next vertex
+    }
+    if (any) raise_flag_sharded(a.changed, a.cshards);
+}
+
+// First iteration of an undirected graph whose rows are sorted by column: every label is still
+// its vertex id, so the result is the row's first column (the smallest neighbour), one load per
+// vertex instead of a pass over every label (~470 us of tier kernels on SYN-7_5).
+__global__ __launch_bounds__(256) void k_cdlp_first_sorted(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                           int64_t v0, int64_t v1, int32_t *nxt, int *changed,
+                                                           int cshards) {
+    bool any = false;
+    for (int64_t v = v0 + (int64_t)blockIdx.x * 256 + threadIdx.x; v < v1; v += (int64_t)gridDim.x * 256) {
+        const int64_t b = rp[v];
+        const int32_t l = rp[v + 1] > b ? ci[b] : (int32_t)v;
+        nxt[v] = l;
+        any |= l != (int32_t)v;
+    }
+    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag_sharded(changed, cshards);
+}
+
+// Whether every row of a CSR is sorted by column (strictly: rows hold no duplicates): the row
+// starts as a bitmap over the entries, then one compare per entry.
+__global__ __launch_bounds__(256) void k_row_start_bits(const int64_t *__restrict__ rp, int64_t n, uint32_t *bits) {
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += (int64_t)gridDim.x * 256) {
+        const int64_t b = rp[v];
+        if (rp[v + 1] > b) atomicOr(&bits[b >> 5], 1u << (b & 31));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rows_sorted(const int32_t *__restrict__ ci, int64_t nnz,
+                                                     const uint32_t *__restrict__ bits, int *sorted) {
+    bool bad = false;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k + 1 < nnz; k += (int64_t)gridDim.x * 256) {
+        const int64_t k1 = k + 1;
+        bad |= ci[k1] <= ci[k] && !((bits[k1 >> 5] >> (k1 & 31)) & 1u);
+    }
+    if (__ballot(bad) && (threadIdx.x & (kWave - 1)) == 0) *sorted = 0;
 }
 
 __global__ void k_cdlp_iota(int32_t *a, int64_t n) {
@@ -776,6 +1073,12 @@ struct CdlpPlan {
     DBuf<int64_t> d_segb;
     size_t n_seg = 0;
 };
+
+// Switches read at every call (tests flip them within one process); unset means on.
+bool env_on(const char *name) {
+    const char *e = std::getenv(name);
+    return !e || std::atoi(e) != 0;
+}
 
 int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
     std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv, mv4, lvs;
@@ -889,16 +1192,36 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
 // (GX_CDLP_STREAMS=0: all on s).  Alone, each tier kept a CU at a fraction of its wave
 // slots: the workgroup-per-vertex tiers by their LDS tables, the others by their tails; side
 // by side, a CU holds a mid-tier workgroup and light/tiny waves at once.
+// The active vertices of a sparse iteration (k_cdlp_mark): kCdlpSubs shards of asub entries.
+struct SparseLists {
+    const int32_t *al;            // kCdlpLists - 1 lists of kCdlpSubs shards of asub entries
+    int64_t asub;
+    const unsigned int *counts;   // the change list's counters, then the three lists'
+};
+
 int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
-                   const int32_t *act = nullptr, int32_t stamp = 0, const int *dense = nullptr, bool first = false) {
+                   const int32_t *act = nullptr, int32_t stamp = 0, const int *dense = nullptr, bool first = false,
+                   const SparseLists *sl = nullptr, int cshards = 1) {
     gx_ctx *ctx = g->ctx;
     const int64_t n = (int64_t)g->n;
     CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr,
-               cur,       nxt,       n,      changed, P.v0, P.v1, act, stamp, dense, first && !g->directed ? 1 : 0};
-    static const bool multi = [] {
-        const char *e = std::getenv("GX_CDLP_STREAMS");
-        return !e || std::atoi(e) != 0;
-    }();
+               cur,       nxt,       n,      changed, P.v0, P.v1, act, stamp, dense, first && !g->directed ? 1 : 0,
+               sl ? 1 : 0, cshards};
+    if (sl) {
+        // exit at once when *dense (the tier kernels below then recompute every vertex)
+        KTimer kt(ctx, "cdlp_sparse", s);
+        const int64_t shards = (int64_t)kCdlpSubs * sl->asub;
+        const unsigned int *cnt = sl->counts + kCdlpSubs * kCntStride;
+        hipLaunchKernelGGL(k_cdlp_sparse_wave, dim3(8 * kCdlpSubs), dim3(256), 0, s, a, sl->al, sl->asub, cnt);
+        GX_TRY(check_launch("k_cdlp_sparse_wave"));
+        hipLaunchKernelGGL((k_cdlp_sparse_group<kMid2Block, kMid2Slots>), dim3(4 * kCdlpSubs), dim3(kMid2Block), 0, s,
+                           a, sl->al + shards, sl->asub, cnt + kCdlpSubs * kCntStride);
+        GX_TRY(check_launch("k_cdlp_sparse_group2"));
+        hipLaunchKernelGGL((k_cdlp_sparse_group<kMidBlock, kMidSlots>), dim3(kCdlpSubs), dim3(kMidBlock), 0, s, a,
+                           sl->al + 2 * shards, sl->asub, cnt + 2 * kCdlpSubs * kCntStride);
+        GX_TRY(check_launch("k_cdlp_sparse_group"));
+    }
+    const bool multi = env_on("GX_CDLP_STREAMS");
     hipStream_t s1 = s, s2 = s;
     if (multi) {
         GX_TRY(ensure_aux_streams(ctx));
@@ -988,12 +1311,14 @@ namespace {
 // the label, flag and active-set buffers.  Iteration-count-sized buffers grow on demand.
 struct CdlpCache {
     CdlpPlan P;
-    DBuf<int32_t> la, lb, act, clist;
+    DBuf<int32_t> la, lb, act, al;
+    DBuf<uint64_t> clist;
     DBuf<int> changed, dense;
     DBuf<unsigned int> ccount;
     int *hflag = nullptr, *dflag = nullptr;
     int cap_iters = 0;
-    int64_t sub = 0;
+    int64_t sub = 0, asub = 0;
+    bool rows_sorted = false;   // A's rows sorted by column (k_rows_sorted)
     hipEvent_t ev[2] = {nullptr, nullptr};
     ~CdlpCache() {
         if (hflag) (void)hipHostFree(hflag);
@@ -1013,7 +1338,28 @@ int cdlp_cache(gx_graph *g, int iters, CdlpCache **out, hipStream_t s) {
         GX_TRY(fresh->act.alloc(n));
         fresh->sub = std::max<int64_t>(16, n / 32 / kCdlpSubs);   // entries per sub-list
         GX_TRY(fresh->clist.alloc((size_t)fresh->sub * kCdlpSubs));
+        fresh->asub = std::max<int64_t>(16, n / 16 / kCdlpSubs);   // active vertices per shard and list
+        GX_TRY(fresh->al.alloc((size_t)fresh->asub * kCdlpSubs * (kCdlpLists - 1)));
         GX_TRY(fresh->dense.alloc(1));
+        if (!g->directed && g->nnz > 0) {
+            DBuf<uint32_t> bits;
+            DBuf<int> flag;
+            const int64_t nnz = (int64_t)g->nnz;
+            GX_TRY(bits.alloc((size_t)(nnz + 31) / 32));
+            GX_TRY(flag.alloc(1));
+            GX_HIP_TRY(hipMemsetAsync(bits.p, 0, (size_t)(nnz + 31) / 32 * 4, s));
+            const int one = 1;
+            GX_HIP_TRY(hipMemcpyAsync(flag.p, &one, sizeof(int), hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(k_row_start_bits, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p, n, bits.p);
+            GX_TRY(check_launch("k_row_start_bits"));
+            hipLaunchKernelGGL(k_rows_sorted, dim3(grid_for(nnz, 256, 8192)), dim3(256), 0, s, g->A.ci.p, nnz, bits.p,
+                               flag.p);
+            GX_TRY(check_launch("k_rows_sorted"));
+            int sorted = 0;
+            GX_HIP_TRY(hipMemcpyAsync(&sorted, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            fresh->rows_sorted = sorted != 0;
+        }
         GX_HIP_TRY(hipEventCreateWithFlags(&fresh->ev[0], hipEventDisableTiming));
         GX_HIP_TRY(hipEventCreateWithFlags(&fresh->ev[1], hipEventDisableTiming));
         g->cdlp = fresh;
@@ -1021,8 +1367,8 @@ int cdlp_cache(gx_graph *g, int iters, CdlpCache **out, hipStream_t s) {
     }
     if (iters > C->cap_iters) {
         const int cap = std::max(iters, 16);
-        GX_TRY(C->changed.alloc(cap));
-        GX_TRY(C->ccount.alloc((size_t)cap * kCdlpSubs));
+        GX_TRY(C->changed.alloc((size_t)cap * kFlagShards * kFlagStride));
+        GX_TRY(C->ccount.alloc((size_t)cap * kCdlpLists * kCdlpSubs * kCntStride));
         if (C->hflag) (void)hipHostFree(C->hflag);
         C->hflag = nullptr;
         GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&C->hflag), sizeof(int) * cap, hipHostMallocMapped));
@@ -1048,7 +1394,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     CdlpCache *C = nullptr;
     GX_TRY(cdlp_cache(g, std::max(iters, 1), &C, s));
     CdlpPlan &P = C->P;
-    GX_HIP_TRY(hipMemsetAsync(C->changed.p, 0, sizeof(int) * std::max(iters, 1), s));
+    GX_HIP_TRY(hipMemsetAsync(C->changed.p, 0, sizeof(int) * kFlagShards * kFlagStride * std::max(iters, 1), s));
     hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, C->la.p, n);
     GX_TRY(check_launch("k_cdlp_iota"));
     // Early exit at a fixed point (LAGraph_cdlp.c:328-332), checked one iteration late:
@@ -1059,38 +1405,48 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     // active set (GX_CDLP_ACTIVE=0: every vertex every iteration): from iteration 2 on, the
     // changes of the last iteration are listed (up to n / 32 of them) and their neighbours
     // marked with the iteration's stamp before the tier kernels run
-    static const bool use_active = [] {
-        const char *e = std::getenv("GX_CDLP_ACTIVE");
-        return !e || std::atoi(e) != 0;
-    }();
+    const bool use_active = env_on("GX_CDLP_ACTIVE");
     const bool active = use_active && iters > 2;
+    // GX_CDLP_FIRST_SORTED=0: the first iteration by the tier kernels even when rows are sorted
+    const bool first_sorted = env_on("GX_CDLP_FIRST_SORTED");
+    // GX_CDLP_SPARSE=0: active vertices found by the tier kernels' act checks instead of lists
+    const bool use_sparse = env_on("GX_CDLP_SPARSE");
     const int64_t sub = C->sub;
     if (active) {
         hipLaunchKernelGGL(k_cdlp_fill_u32, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s,
                            reinterpret_cast<uint32_t *>(C->act.p), 0xffffffffu, n);   // stamp -1: never active
         GX_TRY(check_launch("k_cdlp_fill_u32"));
-        GX_HIP_TRY(hipMemsetAsync(C->ccount.p, 0, sizeof(unsigned int) * kCdlpSubs * iters, s));
+        GX_HIP_TRY(hipMemsetAsync(C->ccount.p, 0, sizeof(unsigned int) * kCdlpLists * kCdlpSubs * kCntStride * iters, s));
     }
     int32_t *cur = C->la.p, *nxt = C->lb.p;
     for (int it = 0; it < iters; it++) {
-        int *changed = C->changed.p + it;
+        int *changed = C->changed.p + (size_t)it * kFlagShards * kFlagStride;
         if (active && it >= 2) {
             // nxt still holds the input of iteration it-1, cur its output
             KTimer kt(ctx, "cdlp_mark", s);
-            unsigned int *cnt = C->ccount.p + (size_t)it * kCdlpSubs;
-            hipLaunchKernelGGL(k_cdlp_changed, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, nxt, cur, n, C->clist.p,
-                               sub, cnt);
+            unsigned int *cnt = C->ccount.p + (size_t)it * kCdlpLists * kCdlpSubs * kCntStride;
+            const int64_t *rpT = g->directed ? g->AT.rp.p : nullptr;
+            hipLaunchKernelGGL(k_cdlp_changed, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, nxt, cur, g->A.rp.p,
+                               rpT, n, C->clist.p, sub, cnt, C->dense.p);
             GX_TRY(check_launch("k_cdlp_changed"));
-            hipLaunchKernelGGL(k_cdlp_mark, dim3(1024), dim3(kCdlpSubs), 0, s, g->A.rp.p, g->A.ci.p,
-                               g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr, C->clist.p, sub,
-                               cnt, C->act.p, (int32_t)it, C->dense.p);
+            // 32 waves per shard of the change list (the grid must be a multiple of kCdlpSubs waves)
+            hipLaunchKernelGGL(k_cdlp_mark, dim3(8 * kCdlpSubs), dim3(kCdlpSubs), 0, s, g->A.rp.p, g->A.ci.p, rpT,
+                               g->directed ? g->AT.ci.p : nullptr, C->clist.p, sub, cnt, C->act.p, (int32_t)it,
+                               C->dense.p, C->al.p, C->asub);
             GX_TRY(check_launch("k_cdlp_mark"));
-            GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p));
+            const SparseLists sl{C->al.p, C->asub, cnt};
+            GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
+                                  use_sparse ? &sl : nullptr, kFlagShards));
+        } else if (it == 0 && C->rows_sorted && first_sorted) {
+            KTimer kt(ctx, "cdlp_first", s);
+            hipLaunchKernelGGL(k_cdlp_first_sorted, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p,
+                               g->A.ci.p, (int64_t)0, n, nxt, changed, kFlagShards);
+            GX_TRY(check_launch("k_cdlp_first_sorted"));
         } else {
             // iteration 0: labels are the vertex ids (k_cdlp_iota)
-            GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0));
+            GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0, nullptr, kFlagShards));
         }
-        hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(64), 0, s, changed, dflag + it);
+        hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(kWave), 0, s, changed, kFlagShards, dflag + it);
         GX_TRY(check_launch("k_cdlp_flag_out"));
         GX_HIP_TRY(hipEventRecord(ev[it & 1], s));
         std::swap(cur, nxt);

@@ -234,6 +234,17 @@ __device__ __forceinline__ void raise_flag(int *flag) {
         __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The same flag spread over `shards` words kFlagStride apart (one per 128-byte line): the
+// raise of workgroup b goes to word b % shards, so ~16 K raising waves of a thread-per-vertex
+// kernel hit kFlagShards lines instead of one (one word: ~150 us of serialised checks for
+// CDLP's first iteration on SYN-7_5).  Readers OR the words.
+constexpr int kFlagShards = 64;
+constexpr int kFlagStride = 32;
+
+__device__ __forceinline__ void raise_flag_sharded(int *flags, int shards) {
+    raise_flag(flags + (int)(blockIdx.x % (unsigned)shards) * kFlagStride);
+}
+
 // ---- 64-entry slabs of a CSR (one wave per slab, lane = entry) ----
 // srow[sl] = the row holding entry sl*64, srow[nslabs] = n - 1 (gx_runtime.hip).
 int slab_rows(const int64_t *rp, int64_t n, int64_t nslabs, int64_t *srow, hipStream_t s);

@@ -358,3 +358,34 @@ def test_cdlp_active_set(ctx, monkeypatch, active):
               _G(_tier_graph(True), True)):
         for iters in (2, 3, 5, 12):
             np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=iters), O.cdlp(g.csr, g.directed, iters))
+
+
+def _shuffle_rows(csr, seed=0):
+    """The same graph with every row's columns in a random order."""
+    import copy
+    rng = np.random.default_rng(seed)
+    out = copy.copy(csr)
+    rp = csr.rowptr.astype(np.int64)
+    keys = np.repeat(np.arange(len(rp) - 1), np.diff(rp)) * 2.0 + rng.random(int(rp[-1]))
+    out.colidx = csr.colidx[np.argsort(keys, kind="stable")]
+    return out
+
+
+@pytest.mark.parametrize("first_sorted", ["1", "0"])
+@pytest.mark.parametrize("sparse", ["1", "0"])
+def test_cdlp_row_order_and_sparse(ctx, monkeypatch, first_sorted, sparse):
+    """The first iteration of an undirected graph with sorted rows takes each row's first
+    column (GX_CDLP_FIRST_SORTED=0: the tier kernels' minimum); rows in random order take the
+    tier kernels.  Sparse iterations recompute listed active vertices (GX_CDLP_SPARSE=0: the
+    tier kernels' act checks).  Same labels as the oracle either way."""
+    monkeypatch.setenv("GX_CDLP_FIRST_SORTED", first_sorted)
+    monkeypatch.setenv("GX_CDLP_SPARSE", sparse)
+    g = _rmat(13, 8, 21)
+    shuffled = _shuffle_rows(g.csr)
+    assert not np.array_equal(shuffled.colidx, g.csr.colidx)
+    for csr in (g.csr, shuffled):
+        for iters in (1, 2, 4, 9):
+            np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "CDLP", iters=iters), O.cdlp(csr, False, iters))
+    t = _tier_graph(True)
+    for iters in (4, 9):
+        np.testing.assert_array_equal(gpu_run(ctx, _G(t, True), "CDLP", iters=iters), O.cdlp(t, True, iters))
