@@ -705,11 +705,12 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
 
 // The iteration's changed flag to pinned host memory: one lane's store over PCIe, instead of a
 // 4-byte hipMemcpyAsync, which ran as a ~40 us blit kernel (profiles/r01_cdlp_kernel_stats.csv).
-__global__ void k_cdlp_flag_out(const int *__restrict__ changed, int shards, int *hflag) {
+// Bit 0: a label changed; bit 1: the iteration's active set overflowed (*dense).
+__global__ void k_cdlp_flag_out(const int *__restrict__ changed, int shards, const int *dense, int *hflag) {
     const int t = threadIdx.x;   // one lane per shard (shards <= kWave)
     const bool set = t < shards && changed[t * kFlagStride] != 0;
     const bool any = __ballot(set) != 0;
-    if (t == 0) *hflag = any ? 1 : 0;
+    if (t == 0) *hflag = (any ? 1 : 0) | (dense && *dense ? 2 : 0);
 }
 
 // Active set of the next iteration (gx_cdlp).  k_cdlp_changed lists the vertices whose label
@@ -851,10 +852,14 @@ __global__ __launch_bounds__(256) void k_cdlp_mark(const int64_t *__restrict__ r
 }
 
 // Sparse iterations, active vertices of degree <= kSparseWaveMax: one wave each (the light
-// tier's method: strict-majority vote, else a 2d-slot LDS hash table).
+// tier's method: strict-majority vote, else a 2d-slot LDS hash table).  When *dense and the
+// iteration has no tier kernels (a sparse-only iteration, fl != null), every vertex of the
+// fallback list fl is recomputed instead.
 __global__ __launch_bounds__(256) void k_cdlp_sparse_wave(CdlpArgs a, const int32_t *__restrict__ wl, int64_t asub,
-                                                          const unsigned int *wcount) {
-    if (*a.dense) return;
+                                                          const unsigned int *wcount, const int32_t *__restrict__ fl,
+                                                          int64_t fn) {
+    const bool full = *a.dense != 0;
+    if (full && !fl) return;
     constexpr int kSlots = 2 * kSparseWaveMax;
     constexpr int R = kSparseWaveMax / kWave;
     __shared__ uint32_t keys[256 / kWave][kSlots];
@@ -865,10 +870,12 @@ __global__ __launch_bounds__(256) void k_cdlp_sparse_wave(CdlpArgs a, const int3
     const int64_t gw = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (256 / kWave);   // a multiple of kCdlpSubs
     const int j = (int)(gw % kCdlpSubs);
-    const int64_t c = shard_count(wcount, j, asub);
+    const int32_t *src = full ? fl : wl + (int64_t)j * asub;
+    const int64_t c = full ? fn : (int64_t)shard_count(wcount, j, asub);
+    const int64_t step = full ? nw : nw / kCdlpSubs;
     bool any = false;
-    for (int64_t i = gw / kCdlpSubs; i < c; i += nw / kCdlpSubs) {
-        const int64_t v = wl[(int64_t)j * asub + i];
+    for (int64_t i = full ? gw : gw / kCdlpSubs; i < c; i += step) {
+        const int64_t v = src[i];
         const VMeta m = vmeta(a, v);
         const int64_t d = (int64_t)m.od + m.id;
         uint32_t L[R];
@@ -930,10 +937,14 @@ __global__ __launch_bounds__(256) void k_cdlp_sparse_wave(CdlpArgs a, const int3
 // Sparse iterations, active vertices of kSparseWaveMax < degree <= kMidMax: one workgroup each
 // with a kSlots-slot LDS table (the mid tier's method, without its pipelining).  Two shapes:
 // 256 threads / 4K slots (four workgroups per CU) up to kSparseG2Max, 1024 / 16K above.
+// Fallback when *dense in a sparse-only iteration: every vertex of fl then fl2.
 template <int kBlock, int kSlots>
 __global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const int32_t *__restrict__ gl,
-                                                              int64_t asub, const unsigned int *gcount) {
-    if (*a.dense) return;
+                                                              int64_t asub, const unsigned int *gcount,
+                                                              const int32_t *__restrict__ fl, int64_t fn,
+                                                              const int32_t *__restrict__ fl2, int64_t fn2) {
+    const bool full = *a.dense != 0;
+    if (full && !fl && !fl2) return;
     __shared__ uint32_t K[kSlots];
     __shared__ uint32_t C[kSlots];
     __shared__ unsigned long long red[kBlock / kWave];
@@ -943,10 +954,12 @@ __global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const 
     constexpr int NW = kBlock / kWave;
     const int tid = threadIdx.x;
     const int j = (int)(blockIdx.x % kCdlpSubs);   // the grid is a multiple of kCdlpSubs
-    const int64_t c = shard_count(gcount, j, asub);
+    const int32_t *src = full ? fl : gl + (int64_t)j * asub;
+    const int64_t c = full ? fn + fn2 : (int64_t)shard_count(gcount, j, asub);
+    const int64_t step = full ? gridDim.x : gridDim.x / kCdlpSubs;
     bool any = false;
-    for (int64_t i = blockIdx.x / kCdlpSubs; i < c; i += gridDim.x / kCdlpSubs) {
-        const int64_t v = gl[(int64_t)j * asub + i];
+    for (int64_t i = full ? blockIdx.x : blockIdx.x / kCdlpSubs; i < c; i += step) {
+        const int64_t v = full && i >= fn ? fl2[i - fn] : src[i];   // full: fn == 0 when fl is null
         const VMeta m = vmeta(a, v);
         const int64_t d = (int64_t)m.od + m.id;
         uint32_t L[R];
@@ -1066,6 +1079,8 @@ struct CdlpPlan {
     DBuf<int32_t> d_hv, d_hl, d_mv, d_cvert, d_lv, d_mv2, d_sv, d_mv4;
     size_t n_small = 0, n_mid4 = 0, n_light_s = 0;
     DBuf<int32_t> d_lvs;                // light vertices with degree <= kLightSlots / 2
+    DBuf<int32_t> d_wall;               // every vertex of degree <= kSparseWaveMax (sparse fallback)
+    size_t n_wall = 0;
     DBuf<int64_t> d_hoff, d_cbeg;
     DBuf<uint32_t> gk, gc;
     DBuf<unsigned long long> vkey;      // per huge vertex best key (zero between iterations)
@@ -1081,12 +1096,13 @@ bool env_on(const char *name) {
 }
 
 int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
-    std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv, mv4, lvs;
+    std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv, mv4, lvs, wall;
     std::vector<int64_t> hoff, cbeg;
     int64_t total = 0;
     for (int64_t v = v0; v < v1; v++) {
         int64_t d = g->A.h_rp[v + 1] - g->A.h_rp[v];
         if (g->directed) d += g->AT.h_rp[v + 1] - g->AT.h_rp[v];
+        if (d <= kSparseWaveMax) wall.push_back((int32_t)v);
         if (d <= kTiny) {
             // k_cdlp_tiny scans the range itself
         } else if (d <= kWave) {
@@ -1178,6 +1194,11 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
         GX_TRY(P.d_lvs.alloc(lvs.size()));
         GX_HIP_TRY(hipMemcpyAsync(P.d_lvs.p, lvs.data(), lvs.size() * 4, hipMemcpyHostToDevice, s));
     }
+    P.n_wall = wall.size();
+    if (!wall.empty()) {
+        GX_TRY(P.d_wall.alloc(wall.size()));
+        GX_HIP_TRY(hipMemcpyAsync(P.d_wall.p, wall.data(), wall.size() * 4, hipMemcpyHostToDevice, s));
+    }
     if (!lv.empty()) {
         GX_TRY(P.d_lv.alloc(lv.size()));
         GX_HIP_TRY(hipMemcpyAsync(P.d_lv.p, lv.data(), lv.size() * 4, hipMemcpyHostToDevice, s));
@@ -1197,6 +1218,7 @@ struct SparseLists {
     const int32_t *al;            // kCdlpLists - 1 lists of kCdlpSubs shards of asub entries
     int64_t asub;
     const unsigned int *counts;   // the change list's counters, then the three lists'
+    bool only;                    // sparse-only: no tier kernels but the huge ones
 };
 
 int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
@@ -1207,18 +1229,24 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
     CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr,
                cur,       nxt,       n,      changed, P.v0, P.v1, act, stamp, dense, first && !g->directed ? 1 : 0,
                sl ? 1 : 0, cshards};
+    const bool tiers = !(sl && sl->only);   // sparse-only: the huge tier alone beside the sparse kernels
     if (sl) {
         // exit at once when *dense (the tier kernels below then recompute every vertex)
         KTimer kt(ctx, "cdlp_sparse", s);
         const int64_t shards = (int64_t)kCdlpSubs * sl->asub;
         const unsigned int *cnt = sl->counts + kCdlpSubs * kCntStride;
-        hipLaunchKernelGGL(k_cdlp_sparse_wave, dim3(8 * kCdlpSubs), dim3(256), 0, s, a, sl->al, sl->asub, cnt);
+        // a sparse-only iteration's fallback lists (nothing else recomputes these vertices)
+        const bool o = sl->only;
+        hipLaunchKernelGGL(k_cdlp_sparse_wave, dim3(8 * kCdlpSubs), dim3(256), 0, s, a, sl->al, sl->asub, cnt,
+                           o ? P.d_wall.p : nullptr, (int64_t)P.n_wall);
         GX_TRY(check_launch("k_cdlp_sparse_wave"));
         hipLaunchKernelGGL((k_cdlp_sparse_group<kMid2Block, kMid2Slots>), dim3(4 * kCdlpSubs), dim3(kMid2Block), 0, s,
-                           a, sl->al + shards, sl->asub, cnt + kCdlpSubs * kCntStride);
+                           a, sl->al + shards, sl->asub, cnt + kCdlpSubs * kCntStride, o ? P.d_mv2.p : nullptr,
+                           (int64_t)P.n_mid2, nullptr, (int64_t)0);
         GX_TRY(check_launch("k_cdlp_sparse_group2"));
         hipLaunchKernelGGL((k_cdlp_sparse_group<kMidBlock, kMidSlots>), dim3(kCdlpSubs), dim3(kMidBlock), 0, s, a,
-                           sl->al + 2 * shards, sl->asub, cnt + 2 * kCdlpSubs * kCntStride);
+                           sl->al + 2 * shards, sl->asub, cnt + 2 * kCdlpSubs * kCntStride, o ? P.d_mv4.p : nullptr,
+                           (int64_t)P.n_mid4, o ? P.d_mv.p : nullptr, (int64_t)P.n_mid);
         GX_TRY(check_launch("k_cdlp_sparse_group"));
     }
     const bool multi = env_on("GX_CDLP_STREAMS");
@@ -1233,7 +1261,7 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
     }
     // s: mid2, mid, tiny; s1: huge, mid4; s2: light, small, light_s (about a third of an
     // iteration's kernel time each on SYN-7_5)
-    if (P.n_mid2) {
+    if (tiers && P.n_mid2) {
         KTimer kt(ctx, "cdlp_mid2", s);
         const unsigned grid2 = (unsigned)std::min<size_t>(P.n_mid2, (size_t)std::max(1, ctx->num_cus) * 4);
         hipLaunchKernelGGL((k_cdlp_mid<kMid2Block, kMid2Slots>), dim3(grid2), dim3(kMid2Block), 0, s, a, P.d_mv2.p,
@@ -1252,39 +1280,39 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
                            (int32_t)P.n_huge, P.vkey.p);
         GX_TRY(check_launch("k_cdlp_huge_final"));
     }
-    if (P.n_light) {
+    if (tiers && P.n_light) {
         KTimer kt(ctx, "cdlp_light", s2);
         hipLaunchKernelGGL(k_cdlp_light<kLdsHash>, dim3(grid_for((uint64_t)P.n_light * kWave, kCdlpBlock, 8192)),
                            dim3(kCdlpBlock), 0, s2, a, P.d_lv.p, (int32_t)P.n_light);
         GX_TRY(check_launch("k_cdlp_light"));
     }
-    if (P.n_mid) {
+    if (tiers && P.n_mid) {
         KTimer kt(ctx, "cdlp_mid", s);
         const unsigned mid_grid = (unsigned)std::min<size_t>(P.n_mid, (size_t)std::max(1, ctx->num_cus));
         hipLaunchKernelGGL((k_cdlp_mid<kMidBlock, kMidSlots>), dim3(mid_grid), dim3(kMidBlock), 0, s, a, P.d_mv.p,
                            (int32_t)P.n_mid);
         GX_TRY(check_launch("k_cdlp_mid"));
     }
-    if (P.n_mid4) {
+    if (tiers && P.n_mid4) {
         KTimer kt(ctx, "cdlp_mid4", s1);
         const unsigned grid4 = (unsigned)std::min<size_t>(P.n_mid4, (size_t)std::max(1, ctx->num_cus) * 2);
         hipLaunchKernelGGL((k_cdlp_mid<kMid4Block, kMid4Slots>), dim3(grid4), dim3(kMid4Block), 0, s1, a, P.d_mv4.p,
                            (int32_t)P.n_mid4);
         GX_TRY(check_launch("k_cdlp_mid4"));
     }
-    if (P.n_small) {
+    if (tiers && P.n_small) {
         KTimer kt(ctx, "cdlp_small", s2);
         hipLaunchKernelGGL(k_cdlp_small, dim3(grid_for((uint64_t)P.n_small * kWave, kCdlpBlock, 8192)),
                            dim3(kCdlpBlock), 0, s2, a, P.d_sv.p, (int32_t)P.n_small);
         GX_TRY(check_launch("k_cdlp_small"));
     }
-    if (P.n_light_s) {
+    if (tiers && P.n_light_s) {
         KTimer kt(ctx, "cdlp_light_s", s2);
         hipLaunchKernelGGL(k_cdlp_light<kLightSlots>, dim3(grid_for((uint64_t)P.n_light_s * kWave, kCdlpBlock, 8192)),
                            dim3(kCdlpBlock), 0, s2, a, P.d_lvs.p, (int32_t)P.n_light_s);
         GX_TRY(check_launch("k_cdlp_light_s"));
     }
-    if (P.v1 > P.v0) {
+    if (tiers && P.v1 > P.v0) {
         KTimer kt(ctx, "cdlp_tiny", s);
         hipLaunchKernelGGL(k_cdlp_tiny, dim3(grid_for((uint64_t)(P.v1 - P.v0), kCdlpBlock, 8192)), dim3(kCdlpBlock),
                            0, s, a);
@@ -1319,7 +1347,7 @@ struct CdlpCache {
     int cap_iters = 0;
     int64_t sub = 0, asub = 0;
     bool rows_sorted = false;   // A's rows sorted by column (k_rows_sorted)
-    hipEvent_t ev[2] = {nullptr, nullptr};
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     ~CdlpCache() {
         if (hflag) (void)hipHostFree(hflag);
         for (hipEvent_t e : ev)
@@ -1360,8 +1388,7 @@ int cdlp_cache(gx_graph *g, int iters, CdlpCache **out, hipStream_t s) {
             GX_HIP_TRY(hipStreamSynchronize(s));
             fresh->rows_sorted = sorted != 0;
         }
-        GX_HIP_TRY(hipEventCreateWithFlags(&fresh->ev[0], hipEventDisableTiming));
-        GX_HIP_TRY(hipEventCreateWithFlags(&fresh->ev[1], hipEventDisableTiming));
+        for (hipEvent_t &e : fresh->ev) GX_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         g->cdlp = fresh;
         C = fresh.get();
     }
@@ -1397,9 +1424,11 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     GX_HIP_TRY(hipMemsetAsync(C->changed.p, 0, sizeof(int) * kFlagShards * kFlagStride * std::max(iters, 1), s));
     hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, C->la.p, n);
     GX_TRY(check_launch("k_cdlp_iota"));
-    // Early exit at a fixed point (LAGraph_cdlp.c:328-332), checked one iteration late:
-    // iteration it is queued before the host waits for iteration it-1's flag, so the check
-    // never drains the stream.  An iteration run after a fixed point changes no label.
+    // Early exit at a fixed point (LAGraph_cdlp.c:328-332), checked `lag` iterations late:
+    // iteration it is queued before the host waits for iteration it-lag's flag, so the check
+    // never drains the stream.  An iteration run after a fixed point changes no label.  Lag 2
+    // (GX_CDLP_LAG=1: one) keeps two iterations queued: sparse iterations of ~60 us are shorter
+    // than the host's launches for one.
     int *hflag = C->hflag, *dflag = C->dflag;
     hipEvent_t *ev = C->ev;
     // active set (GX_CDLP_ACTIVE=0: every vertex every iteration): from iteration 2 on, the
@@ -1411,6 +1440,12 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     const bool first_sorted = env_on("GX_CDLP_FIRST_SORTED");
     // GX_CDLP_SPARSE=0: active vertices found by the tier kernels' act checks instead of lists
     const bool use_sparse = env_on("GX_CDLP_SPARSE");
+    // GX_CDLP_SPARSE_ONLY=0: tier kernels launched (and idle) in sparse iterations too; =2:
+    // every active iteration sparse-only (a test of the fallback lists)
+    const char *so = std::getenv("GX_CDLP_SPARSE_ONLY");
+    const int sparse_only = !use_sparse ? 0 : so ? std::atoi(so) : 1;
+    const char *lg = std::getenv("GX_CDLP_LAG");
+    const int lag = lg && std::atoi(lg) == 1 ? 1 : 2;
     const int64_t sub = C->sub;
     if (active) {
         hipLaunchKernelGGL(k_cdlp_fill_u32, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s,
@@ -1434,7 +1469,11 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                                g->directed ? g->AT.ci.p : nullptr, C->clist.p, sub, cnt, C->act.p, (int32_t)it,
                                C->dense.p, C->al.p, C->asub);
             GX_TRY(check_launch("k_cdlp_mark"));
-            const SparseLists sl{C->al.p, C->asub, cnt};
+            // sparse-only (no idle tier launches, ~60 us per iteration on SYN-7_5) when iteration
+            // it-1-lag, the last whose flags the host has seen, did not overflow its lists: changes
+            // shrink as labels settle.  A wrong guess costs the fallback lists' full pass.
+            const bool only = sparse_only == 2 || (sparse_only == 1 && it >= 3 + lag && (hflag[it - 1 - lag] & 2) == 0);
+            const SparseLists sl{C->al.p, C->asub, cnt, only};
             GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
                                   use_sparse ? &sl : nullptr, kFlagShards));
         } else if (it == 0 && C->rows_sorted && first_sorted) {
@@ -1446,13 +1485,14 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             // iteration 0: labels are the vertex ids (k_cdlp_iota)
             GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0, nullptr, kFlagShards));
         }
-        hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(kWave), 0, s, changed, kFlagShards, dflag + it);
+        hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(kWave), 0, s, changed, kFlagShards,
+                           active && it >= 2 ? C->dense.p : nullptr, dflag + it);
         GX_TRY(check_launch("k_cdlp_flag_out"));
-        GX_HIP_TRY(hipEventRecord(ev[it & 1], s));
+        GX_HIP_TRY(hipEventRecord(ev[it % 3], s));
         std::swap(cur, nxt);
-        if (it >= 1) {
-            GX_HIP_TRY(hipEventSynchronize(ev[(it - 1) & 1]));
-            if (!hflag[it - 1]) break;   // iteration it-1 was a fixed point, so is cur
+        if (it >= lag) {
+            GX_HIP_TRY(hipEventSynchronize(ev[(it - lag) % 3]));
+            if (!(hflag[it - lag] & 1)) break;   // iteration it-lag was a fixed point, so is cur
         }
     }
     GX_TRY(device_end(ctx));

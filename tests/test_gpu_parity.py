@@ -372,14 +372,17 @@ def _shuffle_rows(csr, seed=0):
 
 
 @pytest.mark.parametrize("first_sorted", ["1", "0"])
-@pytest.mark.parametrize("sparse", ["1", "0"])
-def test_cdlp_row_order_and_sparse(ctx, monkeypatch, first_sorted, sparse):
+@pytest.mark.parametrize("sparse,only", [("1", "1"), ("1", "2"), ("1", "0"), ("0", "1")])
+def test_cdlp_row_order_and_sparse(ctx, monkeypatch, first_sorted, sparse, only):
     """The first iteration of an undirected graph with sorted rows takes each row's first
     column (GX_CDLP_FIRST_SORTED=0: the tier kernels' minimum); rows in random order take the
     tier kernels.  Sparse iterations recompute listed active vertices (GX_CDLP_SPARSE=0: the
-    tier kernels' act checks).  Same labels as the oracle either way."""
+    tier kernels' act checks); sparse-only iterations launch no tier kernel but the huge ones
+    (GX_CDLP_SPARSE_ONLY=2: every active iteration, so overflowing ones take the fallback
+    lists).  Same labels as the oracle either way."""
     monkeypatch.setenv("GX_CDLP_FIRST_SORTED", first_sorted)
     monkeypatch.setenv("GX_CDLP_SPARSE", sparse)
+    monkeypatch.setenv("GX_CDLP_SPARSE_ONLY", only)
     g = _rmat(13, 8, 21)
     shuffled = _shuffle_rows(g.csr)
     assert not np.array_equal(shuffled.colidx, g.csr.colidx)
