@@ -62,7 +62,17 @@ struct CdlpArgs {
     // have nothing to do unless *dense
     int sparse;
     int cshards;   // *changed is cshards words kFlagStride apart (raise_flag_sharded)
+    // staged labels (k_cdlp_stage): nl[e] = lab[column of entry e] for every entry of A, then
+    // (directed) of A' at nnzA + e, so a vertex's labels are contiguous loads instead of
+    // column-indexed gathers.  Valid in a dense iteration only: with an active set and
+    // !*dense the kernels gather through the columns (unstage()).
+    const int32_t *nl;
+    int64_t nnzA;
 };
+
+__device__ __forceinline__ void unstage(CdlpArgs &a) {
+    if (a.nl && a.act && *a.dense == 0) a.nl = nullptr;
+}
 
 __device__ __forceinline__ bool tier_idle(const CdlpArgs &a) { return a.sparse && *a.dense == 0; }
 
@@ -73,6 +83,7 @@ __device__ __forceinline__ bool active(const CdlpArgs &a, bool all, int64_t v) {
 
 __device__ __forceinline__ int32_t label_at(const CdlpArgs &a, int64_t ob, int64_t od, int64_t ib,
                                             int64_t k) {
+    if (a.nl) return k < od ? a.nl[ob + k] : a.nl[a.nnzA + ib + (k - od)];
     return k < od ? a.lab[a.ciA[ob + k]] : a.lab[a.ciT[ib + (k - od)]];
 }
 
@@ -108,6 +119,15 @@ __device__ __forceinline__ VMeta vmeta_act(const CdlpArgs &a, bool all, int64_t 
 __device__ __forceinline__ int32_t col_at(const CdlpArgs &a, const VMeta &m, int64_t k) {
     return k < m.od ? a.ciA[m.ob + k] : a.ciT[m.ib + (k - m.od)];
 }
+
+// Where label k of a vertex is read: an index into lsrc(a), the staged labels (no load to
+// find it) or the label array (through the column).
+__device__ __forceinline__ int64_t src_at(const CdlpArgs &a, const VMeta &m, int64_t k) {
+    if (a.nl) return k < m.od ? m.ob + k : a.nnzA + m.ib + (k - m.od);
+    return col_at(a, m, k);
+}
+
+__device__ __forceinline__ const int32_t *lsrc(const CdlpArgs &a) { return a.nl ? a.nl : a.lab; }
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t l, int log2ts) {
     return (l * 2654435761u) >> (32 - log2ts);
@@ -217,6 +237,7 @@ constexpr int kTiny = 16;
 
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
     if (tier_idle(a)) return;
+    unstage(a);
     bool any = false;
     const bool all = all_active(a);
     for (int64_t v = a.v0 + (int64_t)blockIdx.x * kCdlpBlock + threadIdx.x; v < a.v1;
@@ -274,6 +295,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int32_t *__restrict__ sv,
                                                            int32_t nsmall) {
     if (tier_idle(a)) return;
+    unstage(a);
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
@@ -315,6 +337,7 @@ template <int kSlots>
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int32_t *__restrict__ lv,
                                                            int32_t nlight) {
     if (tier_idle(a)) return;
+    unstage(a);
     __shared__ uint32_t keys[kCdlpBlock / kWave][kSlots];
     __shared__ uint32_t cnts[kCdlpBlock / kWave][kSlots];
     constexpr int R = kSlots / (2 * kWave);   // label rounds of the largest vertex of the tier
@@ -335,7 +358,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const int64_t k = (int64_t)r * kWave + lane;
-        L[r] = k < (int64_t)m.od + m.id ? (uint32_t)a.lab[col_at(a, m, k)] : kEmpty;
+        L[r] = k < (int64_t)m.od + m.id ? (uint32_t)lsrc(a)[src_at(a, m, k)] : kEmpty;
     }
     for (;;) {
         const int64_t d = (int64_t)m.od + m.id;
@@ -381,11 +404,11 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        int32_t cn[R];                                          // link 3
+        int64_t cn[R];                                          // link 3 (staged: no load)
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const int64_t k = (int64_t)r * kWave + lane;
-            cn[r] = k < dn ? col_at(a, mn, k) : -1;
+            cn[r] = k < dn ? src_at(a, mn, k) : -1;
         }
         unsigned long long key = 0;
         if (!maj) {
@@ -398,7 +421,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
             }
         }
 #pragma unroll
-        for (int r = 0; r < R; r++) L[r] = cn[r] >= 0 ? (uint32_t)a.lab[cn[r]] : kEmpty;   // link 4
+        for (int r = 0; r < R; r++) L[r] = cn[r] >= 0 ? (uint32_t)lsrc(a)[cn[r]] : kEmpty;   // link 4
         const int32_t best = d == 0 ? old
                              : maj ? (int32_t)cand
                                    : (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
@@ -440,7 +463,8 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
     const int tid = threadIdx.x;
     const int32_t hi = cvert[blockIdx.x];
     const int64_t v = hv[hi];
-    if (!active(a, all_active(a), v)) return;   // its tables stay clean; k_cdlp_huge_final keeps the label
+    if (!active(a, all_active(a), v)) return;
+    unstage(a);   // its tables stay clean; k_cdlp_huge_final keeps the label
     const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
     int64_t ib = 0, id = 0;
     if (a.rpT) {
@@ -573,6 +597,7 @@ constexpr int64_t kMid4Max = kMid4Slots / 2;
 template <int kMidBlock, int kMidSlots>
 __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_t *__restrict__ mv, int32_t nmid) {
     if (tier_idle(a)) return;
+    unstage(a);
     __shared__ uint32_t K[kMidSlots];
     __shared__ uint32_t C[kMidSlots];
     __shared__ unsigned long long red[kMidBlock / kWave];
@@ -590,7 +615,7 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const int64_t k = (int64_t)r * kMidBlock + tid;
-        L[r] = k < (int64_t)m.od + m.id ? (uint32_t)a.lab[col_at(a, m, k)] : kEmpty;
+        L[r] = k < (int64_t)m.od + m.id ? (uint32_t)lsrc(a)[src_at(a, m, k)] : kEmpty;
     }
     for (;;) {
         const int64_t d = (int64_t)m.od + m.id;
@@ -656,12 +681,12 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
                 if ((int64_t)r * kMidBlock < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kMidBlock + tid < d, log2ts);
             __syncthreads();
         }
-        // link 3: its column ids
-        int32_t cn[R];
+        // link 3: its column ids (staged labels: no load)
+        int64_t cn[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const int64_t k = (int64_t)r * kMidBlock + tid;
-            cn[r] = k < dn ? col_at(a, mn, k) : -1;
+            cn[r] = k < dn ? src_at(a, mn, k) : -1;
         }
         unsigned long long key = 0;
         if (!maj) {
@@ -675,7 +700,7 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
         }
         // link 4: its labels
 #pragma unroll
-        for (int r = 0; r < R; r++) L[r] = cn[r] >= 0 ? (uint32_t)a.lab[cn[r]] : kEmpty;
+        for (int r = 0; r < R; r++) L[r] = cn[r] >= 0 ? (uint32_t)lsrc(a)[cn[r]] : kEmpty;
         if (maj) {
             if (tid == 0) {
                 const int32_t best = d == 0 ? a.lab[v] : (int32_t)cand;
@@ -1064,6 +1089,130 @@ __global__ __launch_bounds__(256) void k_rows_sorted(const int32_t *__restrict__
     if (__ballot(bad) && (threadIdx.x & (kWave - 1)) == 0) *sorted = 0;
 }
 
+// ---- staged labels --------------------------------------------------------------------
+// A dense iteration's labels are gathered once, in column order, instead of one column-indexed
+// load per entry inside the tier kernels: the entries (of A, then of A' for directed graphs)
+// are cut into kStageBlock-entry blocks whose entries the plan sorts by column, so a wave's 64
+// gathers fall on few lines of the label array (with the hub-first relabelling the most
+// gathered labels share the first lines); each block is put back in entry order in LDS and
+// written out contiguous.  SYN-7_5: ~58 M label line requests per iteration gathered row by
+// row against ~16 M sorted (tools/pr_line_model.py's count with 4-byte labels).
+constexpr int kStageBlock = 16384;
+constexpr int kStageThreads = 1024;
+
+__global__ __launch_bounds__(kStageThreads) void k_cdlp_stage(const int32_t *__restrict__ lab,
+                                                              const int32_t *__restrict__ scol,
+                                                              const uint16_t *__restrict__ spos, int64_t ns,
+                                                              int32_t *__restrict__ nl, const int *dense) {
+    if (dense && *dense == 0) return;   // an active-set iteration that stayed sparse
+    __shared__ int32_t buf[kStageBlock];
+    constexpr int R = kStageBlock / kStageThreads;
+    const int tid = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * kStageBlock;
+    const int m = (int)min((int64_t)kStageBlock, ns - b0);
+    int32_t c[R];
+    uint32_t q[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int k = r * kStageThreads + tid;
+        c[r] = k < m ? scol[b0 + k] : 0;
+        q[r] = k < m ? (uint32_t)spos[b0 + k] : 0u;
+    }
+    int32_t l[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) l[r] = lab[c[r]];   // column 0 for the padding: a valid address
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        if (r * kStageThreads + tid < m) buf[q[r]] = l[r];
+    __syncthreads();
+    if (m == kStageBlock) {
+        int4 *o = reinterpret_cast<int4 *>(nl + b0);
+        const int4 *bi = reinterpret_cast<const int4 *>(buf);
+        for (int i = tid; i < kStageBlock / 4; i += kStageThreads) o[i] = bi[i];
+    } else {
+        for (int i = tid; i < m; i += kStageThreads) nl[b0 + i] = buf[i];
+    }
+}
+
+// Plan of the staging: key = block << 32 | column, value = position in the block.
+__global__ void k_stage_keys(const int32_t *__restrict__ ciA, int64_t nnzA, const int32_t *__restrict__ ciT,
+                             int64_t ns, uint64_t *keys, uint32_t *vals) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = (uint32_t)(k < nnzA ? ciA[k] : ciT[k - nnzA]);
+        keys[k] = ((uint64_t)(k / kStageBlock) << 32) | c;
+        vals[k] = (uint32_t)(k % kStageBlock);
+    }
+}
+
+__global__ void k_stage_split(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals, int64_t ns,
+                              int32_t *scol, uint16_t *spos) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += (int64_t)gridDim.x * blockDim.x) {
+        scol[k] = (int32_t)(uint32_t)keys[k];
+        spos[k] = (uint16_t)vals[k];
+    }
+}
+
+// Hub-first relabelling of a CSR: keys[e] = perm[row] << 32 | perm[col], sorted into the
+// relabelled CSR (the PageRank plan's transform, gx_pr.hip).
+__global__ void k_cdlp_permute_keys(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci, int64_t n,
+                                    int64_t nnz, const int32_t *__restrict__ perm, uint64_t *__restrict__ keys) {
+    constexpr int kPer = 16;
+    const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPer;
+    if (e0 >= nnz) return;
+    const int64_t e1 = min(e0 + kPer, nnz);
+    int64_t r = row_of_edge(rp, n, e0);
+    for (int64_t e = e0; e < e1; e++) {
+        while (rp[r + 1] <= e) r++;
+        keys[e] = ((uint64_t)(uint32_t)perm[r] << 32) | (uint32_t)perm[ci[e]];
+    }
+}
+
+// out[v] = in[idx[v]]
+__global__ void k_cdlp_gather_i32(const int32_t *__restrict__ in, const int32_t *__restrict__ idx, int64_t n,
+                                  int32_t *__restrict__ out) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        out[v] = in[idx[v]];
+}
+
+// The graph CDLP runs on: the caller's (partitioned API, GX_CDLP_RELABEL=0) or its hub-first
+// relabelling (gx_cdlp).  Label VALUES stay the caller's vertex ids either way, so the
+// smallest-label tie rule is unchanged.
+struct CdlpGraph {
+    gx_ctx *ctx = nullptr;
+    int64_t n = 0;
+    bool directed = false;
+    const int64_t *rpA = nullptr, *rpT = nullptr;
+    const int32_t *ciA = nullptr, *ciT = nullptr;
+    const int64_t *h_rpA = nullptr, *h_rpT = nullptr;
+    int64_t nnzA = 0, nnzT = 0;
+};
+
+CdlpGraph cdlp_view(gx_graph *g) {
+    CdlpGraph v;
+    v.ctx = g->ctx;
+    v.n = (int64_t)g->n;
+    v.directed = g->directed;
+    v.rpA = g->A.rp.p;
+    v.ciA = g->A.ci.p;
+    v.h_rpA = g->A.h_rp.data();
+    v.nnzA = (int64_t)g->A.nnz;
+    if (g->directed) {
+        v.rpT = g->AT.rp.p;
+        v.ciT = g->AT.ci.p;
+        v.h_rpT = g->AT.h_rp.data();
+        v.nnzT = (int64_t)g->AT.nnz;
+    }
+    return v;
+}
+
+// Staged labels of one iteration: the plan's sorted blocks and the output array.
+struct StageArgs {
+    const int32_t *scol;
+    const uint16_t *spos;
+    int64_t ns;
+    int32_t *nl;
+};
+
 __global__ void k_cdlp_iota(int32_t *a, int64_t n) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
          v += (int64_t)gridDim.x * blockDim.x)
@@ -1089,19 +1238,19 @@ struct CdlpPlan {
     size_t n_seg = 0;
 };
 
-// Switches read at every call (tests flip them within one process); unset means on.
-bool env_on(const char *name) {
+// Switches read at every call (tests flip them within one process); unset means `dflt`.
+bool env_on(const char *name, bool dflt = true) {
     const char *e = std::getenv(name);
-    return !e || std::atoi(e) != 0;
+    return e ? std::atoi(e) != 0 : dflt;
 }
 
-int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
+int cdlp_plan(const CdlpGraph &g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
     std::vector<int32_t> hv, hl, mv, cvert, lv, mv2, sv, mv4, lvs, wall;
     std::vector<int64_t> hoff, cbeg;
     int64_t total = 0;
     for (int64_t v = v0; v < v1; v++) {
-        int64_t d = g->A.h_rp[v + 1] - g->A.h_rp[v];
-        if (g->directed) d += g->AT.h_rp[v + 1] - g->AT.h_rp[v];
+        int64_t d = g.h_rpA[v + 1] - g.h_rpA[v];
+        if (g.directed) d += g.h_rpT[v + 1] - g.h_rpT[v];
         if (d <= kSparseWaveMax) wall.push_back((int32_t)v);
         if (d <= kTiny) {
             // k_cdlp_tiny scans the range itself
@@ -1209,10 +1358,10 @@ int cdlp_plan(gx_graph *g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream_t s) {
 
 // One synchronous iteration for the plan's vertices: nxt[v] for v in [v0, v1) from cur
 // (the full label array); *changed is set when a label moved (caller zeroes it).
-// The tier kernels write disjoint vertices and only read `cur`, so they run on three streams
-// (GX_CDLP_STREAMS=0: all on s).  Alone, each tier kept a CU at a fraction of its wave
-// slots: the workgroup-per-vertex tiers by their LDS tables, the others by their tails; side
-// by side, a CU holds a mid-tier workgroup and light/tiny waves at once.
+// The tier kernels write disjoint vertices and only read `cur`, so they can run on three
+// streams (GX_CDLP_STREAMS=1).  That paid while the tiers were slow (SYN-7_5 10.5 -> 9.8 ms);
+// with the current tiers the overlapped kernels slow each other down and one stream is
+// faster (SYN-7_5 3.39 -> 2.89 ms, SYN-cit 3.61 -> 3.37).
 // The active vertices of a sparse iteration (k_cdlp_mark): kCdlpSubs shards of asub entries.
 struct SparseLists {
     const int32_t *al;            // kCdlpLists - 1 lists of kCdlpSubs shards of asub entries
@@ -1221,14 +1370,22 @@ struct SparseLists {
     bool only;                    // sparse-only: no tier kernels but the huge ones
 };
 
-int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
+int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
                    const int32_t *act = nullptr, int32_t stamp = 0, const int *dense = nullptr, bool first = false,
-                   const SparseLists *sl = nullptr, int cshards = 1) {
-    gx_ctx *ctx = g->ctx;
-    const int64_t n = (int64_t)g->n;
-    CdlpArgs a{g->A.rp.p, g->A.ci.p, g->directed ? g->AT.rp.p : nullptr, g->directed ? g->AT.ci.p : nullptr,
-               cur,       nxt,       n,      changed, P.v0, P.v1, act, stamp, dense, first && !g->directed ? 1 : 0,
-               sl ? 1 : 0, cshards};
+                   const SparseLists *sl = nullptr, int cshards = 1, const StageArgs *st = nullptr) {
+    gx_ctx *ctx = g.ctx;
+    const int64_t n = g.n;
+    CdlpArgs a{g.rpA,  g.ciA,  g.rpT, g.ciT,  cur,        nxt,     n,        changed,
+               P.v0,   P.v1,   act,   stamp,  dense,      first && !g.directed ? 1 : 0,
+               sl ? 1 : 0,     cshards,       nullptr,    g.nnzA};
+    if (st && st->ns > 0 && !(sl && sl->only)) {
+        // runs only when the iteration is dense (every vertex recomputed)
+        KTimer kt(ctx, "cdlp_stage", s);
+        hipLaunchKernelGGL(k_cdlp_stage, dim3((unsigned)((st->ns + kStageBlock - 1) / kStageBlock)),
+                           dim3(kStageThreads), 0, s, cur, st->scol, st->spos, st->ns, st->nl, act ? dense : nullptr);
+        GX_TRY(check_launch("k_cdlp_stage"));
+        a.nl = st->nl;
+    }
     const bool tiers = !(sl && sl->only);   // sparse-only: the huge tier alone beside the sparse kernels
     if (sl) {
         // exit at once when *dense (the tier kernels below then recompute every vertex)
@@ -1249,7 +1406,7 @@ int cdlp_iteration(gx_graph *g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, i
                            (int64_t)P.n_mid4, o ? P.d_mv.p : nullptr, (int64_t)P.n_mid);
         GX_TRY(check_launch("k_cdlp_sparse_group"));
     }
-    const bool multi = env_on("GX_CDLP_STREAMS");
+    const bool multi = env_on("GX_CDLP_STREAMS", false);
     hipStream_t s1 = s, s2 = s;
     if (multi) {
         GX_TRY(ensure_aux_streams(ctx));
@@ -1334,10 +1491,21 @@ using namespace gx;
 
 namespace gx {
 namespace {
-// What gx_cdlp keeps on the graph between calls (gx_graph::cdlp): the tier lists (built on
-// the host from the row pointers: ~3 ms of idle device per call on SYN-7_5 when rebuilt) and
-// the label, flag and active-set buffers.  Iteration-count-sized buffers grow on demand.
+// What gx_cdlp keeps on the graph between calls (gx_graph::cdlp): the hub-first relabelled
+// graph, the staging plan, the tier lists (built on the host from the row pointers: ~3 ms of
+// idle device per call on SYN-7_5 when rebuilt) and the label, flag and active-set buffers.
+// Iteration-count-sized buffers grow on demand.
 struct CdlpCache {
+    bool relabel = false;
+    CdlpGraph G;                          // the graph the iterations run on
+    DBuf<int64_t> rpA, rpT;               // relabelled copies (relabel)
+    DBuf<int32_t> ciA, ciT;
+    std::vector<int64_t> h_rpA, h_rpT;
+    DBuf<int32_t> order, perm;            // order[p]: the caller's vertex at p; perm = its inverse
+    DBuf<int32_t> scol, nl;               // staging plan (k_cdlp_stage) and staged labels
+    DBuf<uint16_t> spos;
+    int64_t ns = 0;
+    bool staged_plan = false;
     CdlpPlan P;
     DBuf<int32_t> la, lb, act, al;
     DBuf<uint64_t> clist;
@@ -1355,12 +1523,111 @@ struct CdlpCache {
     }
 };
 
-int cdlp_cache(gx_graph *g, int iters, CdlpCache **out, hipStream_t s) {
+// Relabel one CSR of the graph by perm into (rp, ci).
+int cdlp_relabel_csr(const DevCSR &M, int64_t n, const int32_t *perm, DBuf<int64_t> &rp, DBuf<int32_t> &ci,
+                     hipStream_t s) {
+    GX_TRY(rp.alloc(n + 1));
+    GX_TRY(ci.alloc(M.nnz, 16));
+    DBuf<uint64_t> keys, scratch;
+    GX_TRY(keys.alloc(M.nnz));
+    GX_TRY(scratch.alloc(M.nnz));
+    if (M.nnz) {
+        hipLaunchKernelGGL(k_cdlp_permute_keys, dim3(grid_for((M.nnz + 15) / 16, 256, 1u << 30)), dim3(256), 0, s,
+                           M.rp.p, M.ci.p, n, (int64_t)M.nnz, perm, keys.p);
+        GX_TRY(check_launch("k_cdlp_permute_keys"));
+    }
+    GX_TRY(sort_keys_to_csr(keys, scratch, M.nnz, n, rp.p, ci.p, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // keys die at return
+    return GX_SUCCESS;
+}
+
+// Hub-first order by total degree (out + in), ties by id: the most gathered labels share the
+// first lines of the label array (the PageRank plan's order, gx_pr.hip hub_order).
+int cdlp_relabel(gx_graph *g, CdlpCache &C, hipStream_t s) {
+    const int64_t n = (int64_t)g->n;
+    std::vector<int64_t> deg(n);
+    int64_t maxd = 0;
+    for (int64_t v = 0; v < n; v++) {
+        deg[v] = g->A.h_rp[v + 1] - g->A.h_rp[v];
+        if (g->directed) deg[v] += g->AT.h_rp[v + 1] - g->AT.h_rp[v];
+        maxd = std::max(maxd, deg[v]);
+    }
+    std::vector<int64_t> start((size_t)maxd + 2, 0);
+    for (int64_t v = 0; v < n; v++) start[(size_t)(maxd - deg[v]) + 1]++;
+    for (size_t k = 1; k < start.size(); k++) start[k] += start[k - 1];
+    std::vector<int32_t> order(n), perm(n);
+    for (int64_t v = 0; v < n; v++) {
+        const int64_t pos = start[(size_t)(maxd - deg[v])]++;
+        order[pos] = (int32_t)v;
+        perm[v] = (int32_t)pos;
+    }
+    auto new_rp = [&](const std::vector<int64_t> &h, std::vector<int64_t> &out) {
+        out.assign(n + 1, 0);
+        for (int64_t i = 0; i < n; i++) out[i + 1] = out[i] + (h[order[i] + 1] - h[order[i]]);
+    };
+    new_rp(g->A.h_rp, C.h_rpA);
+    if (g->directed) new_rp(g->AT.h_rp, C.h_rpT);
+    GX_TRY(C.order.alloc(n));
+    GX_TRY(C.perm.alloc(n));
+    GX_HIP_TRY(hipMemcpyAsync(C.order.p, order.data(), n * 4, hipMemcpyHostToDevice, s));
+    GX_HIP_TRY(hipMemcpyAsync(C.perm.p, perm.data(), n * 4, hipMemcpyHostToDevice, s));
+    GX_TRY(cdlp_relabel_csr(g->A, n, C.perm.p, C.rpA, C.ciA, s));
+    if (g->directed) GX_TRY(cdlp_relabel_csr(g->AT, n, C.perm.p, C.rpT, C.ciT, s));
+    C.G.rpA = C.rpA.p;
+    C.G.ciA = C.ciA.p;
+    C.G.h_rpA = C.h_rpA.data();
+    if (g->directed) {
+        C.G.rpT = C.rpT.p;
+        C.G.ciT = C.ciT.p;
+        C.G.h_rpT = C.h_rpT.data();
+    }
+    return GX_SUCCESS;
+}
+
+// The staging plan: every entry's column, sorted within kStageBlock-entry blocks, and its
+// position in the block.
+int cdlp_stage_plan(CdlpCache &C, hipStream_t s) {
+    C.staged_plan = true;
+    const CdlpGraph &G = C.G;
+    const int64_t ns = G.nnzA + G.nnzT;
+    C.ns = ns;
+    if (!ns) return GX_SUCCESS;
+    GX_TRY(C.scol.alloc(ns));
+    GX_TRY(C.spos.alloc(ns));
+    GX_TRY(C.nl.alloc(ns, 16));
+    DBuf<uint64_t> k0, k1;
+    DBuf<uint32_t> v0, v1;
+    GX_TRY(k0.alloc(ns));
+    GX_TRY(k1.alloc(ns));
+    GX_TRY(v0.alloc(ns));
+    GX_TRY(v1.alloc(ns));
+    hipLaunchKernelGGL(k_stage_keys, dim3(grid_for(ns, 256, 1u << 20)), dim3(256), 0, s, G.ciA, G.nnzA, G.ciT, ns,
+                       k0.p, v0.p);
+    GX_TRY(check_launch("k_stage_keys"));
+    const int64_t nblocks = (ns + kStageBlock - 1) / kStageBlock;
+    int b = 1;
+    while ((1ll << b) < nblocks) b++;
+    GX_TRY(sort_pairs_u64_u32(k0.p, k1.p, v0.p, v1.p, (size_t)ns, 32 + b, s));
+    hipLaunchKernelGGL(k_stage_split, dim3(grid_for(ns, 256, 1u << 20)), dim3(256), 0, s, k1.p, v1.p, ns, C.scol.p,
+                       C.spos.p);
+    GX_TRY(check_launch("k_stage_split"));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // the sort buffers die at return
+    return GX_SUCCESS;
+}
+
+int cdlp_cache(gx_graph *g, int iters, bool relabel, bool stage, CdlpCache **out, hipStream_t s) {
     const int64_t n = (int64_t)g->n;
     auto *C = static_cast<CdlpCache *>(g->cdlp.get());
+    if (C && C->relabel != relabel) {
+        g->cdlp.reset();   // GX_CDLP_RELABEL changed between calls
+        C = nullptr;
+    }
     if (!C) {
         auto fresh = std::make_shared<CdlpCache>();
-        GX_TRY(cdlp_plan(g, 0, n, fresh->P, s));
+        fresh->relabel = relabel;
+        fresh->G = cdlp_view(g);
+        if (relabel) GX_TRY(cdlp_relabel(g, *fresh, s));
+        GX_TRY(cdlp_plan(fresh->G, 0, n, fresh->P, s));
         GX_TRY(fresh->la.alloc(n));
         GX_TRY(fresh->lb.alloc(n));
         GX_TRY(fresh->act.alloc(n));
@@ -1369,7 +1636,7 @@ int cdlp_cache(gx_graph *g, int iters, CdlpCache **out, hipStream_t s) {
         fresh->asub = std::max<int64_t>(16, n / 16 / kCdlpSubs);   // active vertices per shard and list
         GX_TRY(fresh->al.alloc((size_t)fresh->asub * kCdlpSubs * (kCdlpLists - 1)));
         GX_TRY(fresh->dense.alloc(1));
-        if (!g->directed && g->nnz > 0) {
+        if (!relabel && !g->directed && g->nnz > 0) {
             DBuf<uint32_t> bits;
             DBuf<int> flag;
             const int64_t nnz = (int64_t)g->nnz;
@@ -1392,6 +1659,7 @@ int cdlp_cache(gx_graph *g, int iters, CdlpCache **out, hipStream_t s) {
         g->cdlp = fresh;
         C = fresh.get();
     }
+    if (stage && !C->staged_plan) GX_TRY(cdlp_stage_plan(*C, s));
     if (iters > C->cap_iters) {
         const int cap = std::max(iters, 16);
         GX_TRY(C->changed.alloc((size_t)cap * kFlagShards * kFlagStride));
@@ -1418,12 +1686,24 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     if (n == 0) return GX_SUCCESS;
     GX_TRY(device_begin(ctx));
     if (g->directed) GX_TRY(ensure_transpose(g));
+    // GX_CDLP_RELABEL=0: iterate on the caller's vertex order; GX_CDLP_STAGE=1: dense
+    // iterations read staged labels (k_cdlp_stage; measured slower)
+    const bool relabel = env_on("GX_CDLP_RELABEL");
+    const bool stage = env_on("GX_CDLP_STAGE", false);
     CdlpCache *C = nullptr;
-    GX_TRY(cdlp_cache(g, std::max(iters, 1), &C, s));
+    GX_TRY(cdlp_cache(g, std::max(iters, 1), relabel, stage, &C, s));
     CdlpPlan &P = C->P;
+    const CdlpGraph &G = C->G;
+    const StageArgs sa{C->scol.p, C->spos.p, C->ns, C->nl.p};
+    const StageArgs *st = stage && C->ns > 0 ? &sa : nullptr;
     GX_HIP_TRY(hipMemsetAsync(C->changed.p, 0, sizeof(int) * kFlagShards * kFlagStride * std::max(iters, 1), s));
-    hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, C->la.p, n);
-    GX_TRY(check_launch("k_cdlp_iota"));
+    if (relabel) {
+        // labels are the caller's vertex ids, at the relabelled positions
+        GX_HIP_TRY(hipMemcpyAsync(C->la.p, C->order.p, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    } else {
+        hipLaunchKernelGGL(k_cdlp_iota, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, C->la.p, n);
+        GX_TRY(check_launch("k_cdlp_iota"));
+    }
     // Early exit at a fixed point (LAGraph_cdlp.c:328-332), checked `lag` iterations late:
     // iteration it is queued before the host waits for iteration it-lag's flag, so the check
     // never drains the stream.  An iteration run after a fixed point changes no label.  Lag 2
@@ -1460,30 +1740,28 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             // nxt still holds the input of iteration it-1, cur its output
             KTimer kt(ctx, "cdlp_mark", s);
             unsigned int *cnt = C->ccount.p + (size_t)it * kCdlpLists * kCdlpSubs * kCntStride;
-            const int64_t *rpT = g->directed ? g->AT.rp.p : nullptr;
-            hipLaunchKernelGGL(k_cdlp_changed, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, nxt, cur, g->A.rp.p,
-                               rpT, n, C->clist.p, sub, cnt, C->dense.p);
+            hipLaunchKernelGGL(k_cdlp_changed, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, nxt, cur, G.rpA, G.rpT,
+                               n, C->clist.p, sub, cnt, C->dense.p);
             GX_TRY(check_launch("k_cdlp_changed"));
             // 32 waves per shard of the change list (the grid must be a multiple of kCdlpSubs waves)
-            hipLaunchKernelGGL(k_cdlp_mark, dim3(8 * kCdlpSubs), dim3(kCdlpSubs), 0, s, g->A.rp.p, g->A.ci.p, rpT,
-                               g->directed ? g->AT.ci.p : nullptr, C->clist.p, sub, cnt, C->act.p, (int32_t)it,
-                               C->dense.p, C->al.p, C->asub);
+            hipLaunchKernelGGL(k_cdlp_mark, dim3(8 * kCdlpSubs), dim3(kCdlpSubs), 0, s, G.rpA, G.ciA, G.rpT, G.ciT,
+                               C->clist.p, sub, cnt, C->act.p, (int32_t)it, C->dense.p, C->al.p, C->asub);
             GX_TRY(check_launch("k_cdlp_mark"));
             // sparse-only (no idle tier launches, ~60 us per iteration on SYN-7_5) when iteration
             // it-1-lag, the last whose flags the host has seen, did not overflow its lists: changes
             // shrink as labels settle.  A wrong guess costs the fallback lists' full pass.
             const bool only = sparse_only == 2 || (sparse_only == 1 && it >= 3 + lag && (hflag[it - 1 - lag] & 2) == 0);
             const SparseLists sl{C->al.p, C->asub, cnt, only};
-            GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
-                                  use_sparse ? &sl : nullptr, kFlagShards));
-        } else if (it == 0 && C->rows_sorted && first_sorted) {
+            GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
+                                  use_sparse ? &sl : nullptr, kFlagShards, st));
+        } else if (it == 0 && !relabel && C->rows_sorted && first_sorted) {
             KTimer kt(ctx, "cdlp_first", s);
-            hipLaunchKernelGGL(k_cdlp_first_sorted, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p,
-                               g->A.ci.p, (int64_t)0, n, nxt, changed, kFlagShards);
+            hipLaunchKernelGGL(k_cdlp_first_sorted, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, G.rpA, G.ciA,
+                               (int64_t)0, n, nxt, changed, kFlagShards);
             GX_TRY(check_launch("k_cdlp_first_sorted"));
         } else {
-            // iteration 0: labels are the vertex ids (k_cdlp_iota)
-            GX_TRY(cdlp_iteration(g, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0, nullptr, kFlagShards));
+            // iteration 0: labels are the caller's vertex ids
+            GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0, nullptr, kFlagShards, st));
         }
         hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(kWave), 0, s, changed, kFlagShards,
                            active && it >= 2 ? C->dense.p : nullptr, dflag + it);
@@ -1494,6 +1772,11 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             GX_HIP_TRY(hipEventSynchronize(ev[(it - lag) % 3]));
             if (!(hflag[it - lag] & 1)) break;   // iteration it-lag was a fixed point, so is cur
         }
+    }
+    if (relabel) {   // back to the caller's vertex order
+        hipLaunchKernelGGL(k_cdlp_gather_i32, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, cur, C->perm.p, n, nxt);
+        GX_TRY(check_launch("k_cdlp_gather_i32"));
+        cur = nxt;
     }
     GX_TRY(device_end(ctx));
     GX_TRY(download(ctx, labels, cur, (uint64_t)n, Xfer::Widen32));
@@ -1513,7 +1796,7 @@ extern "C" int gx_cdlp_part_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_cdl
     if (g->directed) GX_TRY(ensure_transpose(g));
     auto p = std::make_unique<gx_cdlp_part>();
     p->g = g;
-    GX_TRY(cdlp_plan(g, (int64_t)v0, (int64_t)v1, p->plan, g->ctx->stream));
+    GX_TRY(cdlp_plan(cdlp_view(g), (int64_t)v0, (int64_t)v1, p->plan, g->ctx->stream));
     *part = p.release();
     return GX_SUCCESS;
 }
@@ -1536,7 +1819,7 @@ extern "C" int gx_cdlp_part_step(gx_cdlp_part *part, const int32_t *labels, int3
     gx_graph *g = part->g;
     GX_HIP_TRY(hipSetDevice(g->ctx->device));
     hipStream_t s = (hipStream_t)stream;   // NULL = the null stream (torch's default)
-    return cdlp_iteration(g, part->plan, labels, next, changed, s);
+    return cdlp_iteration(cdlp_view(g), part->plan, labels, next, changed, s);
 }
 
 extern "C" int gx_cdlp_part_free(gx_cdlp_part *part) {

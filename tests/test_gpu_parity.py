@@ -392,3 +392,19 @@ def test_cdlp_row_order_and_sparse(ctx, monkeypatch, first_sorted, sparse, only)
     t = _tier_graph(True)
     for iters in (4, 9):
         np.testing.assert_array_equal(gpu_run(ctx, _G(t, True), "CDLP", iters=iters), O.cdlp(t, True, iters))
+
+
+@pytest.mark.parametrize("relabel,stage,streams", [("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("0", "1", "1"),
+                                                   ("1", "0", "1")])
+def test_cdlp_layouts(ctx, monkeypatch, relabel, stage, streams):
+    """gx_cdlp on the hub-first relabelled graph (GX_CDLP_RELABEL, the default) or the caller's
+    order, with labels gathered by the tier kernels or staged in column-sorted blocks
+    (GX_CDLP_STAGE=1), tiers on one stream or three (GX_CDLP_STREAMS=1): label values stay the
+    caller's vertex ids, so every layout matches the oracle exactly."""
+    monkeypatch.setenv("GX_CDLP_RELABEL", relabel)
+    monkeypatch.setenv("GX_CDLP_STAGE", stage)
+    monkeypatch.setenv("GX_CDLP_STREAMS", streams)
+    for g in (_rmat(12, 16, 2), _rmat(11, 8, 3, undirected=False), _G(_tier_graph(False), False),
+              _G(_tier_graph(True), True)):
+        for iters in (1, 3, 10):
+            np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=iters), O.cdlp(g.csr, g.directed, iters))
