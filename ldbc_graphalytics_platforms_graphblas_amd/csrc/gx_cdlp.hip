@@ -317,10 +317,21 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
         } else if (2 * (int64_t)__popcll(__ballot(lane < d && my == cand)) > d) {
             best = (int32_t)cand;   // strict majority
         } else {
-            uint32_t c = 0;
-            for (int j = 0; j < d; j++) c += (__shfl(my, j, kWave) == my) ? 1u : 0u;
-            const unsigned long long key = lane < d ? pack(c, my) : 0ull;
-            best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+            // one round per distinct label: the first remaining lane's label, its lanes by one
+            // ballot (lane reads, no LDS; the d shuffles this replaces were ds_bpermute each)
+            unsigned long long rem = __ballot(lane < d);
+            uint32_t bc = 0, bl = kEmpty;
+            while (rem) {
+                const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)my, __ffsll((long long)rem) - 1);
+                const unsigned long long eq = __ballot(my == l) & rem;
+                const uint32_t c = (uint32_t)__popcll(eq);
+                if (c > bc || (c == bc && l < bl)) {
+                    bc = c;
+                    bl = l;
+                }
+                rem &= ~eq;
+            }
+            best = (int32_t)bl;
         }
         if (lane == 0) {
             a.nxt[v] = best;
@@ -1507,7 +1518,7 @@ struct CdlpCache {
     int64_t ns = 0;
     bool staged_plan = false;
     CdlpPlan P;
-    DBuf<int32_t> la, lb, act, al;
+    DBuf<int32_t> la, lb, act, al, tmp;
     DBuf<uint64_t> clist;
     DBuf<int> changed, dense;
     DBuf<unsigned int> ccount;
@@ -1636,7 +1647,10 @@ int cdlp_cache(gx_graph *g, int iters, bool relabel, bool stage, CdlpCache **out
         fresh->asub = std::max<int64_t>(16, n / 16 / kCdlpSubs);   // active vertices per shard and list
         GX_TRY(fresh->al.alloc((size_t)fresh->asub * kCdlpSubs * (kCdlpLists - 1)));
         GX_TRY(fresh->dense.alloc(1));
-        if (!relabel && !g->directed && g->nnz > 0) {
+        if (!g->directed && g->nnz > 0) {
+            // the caller's rows sorted: the first iteration is each row's first column
+            // (k_cdlp_first_sorted on the caller's graph, then moved to the relabelled order)
+            GX_TRY(fresh->tmp.alloc(n));
             DBuf<uint32_t> bits;
             DBuf<int> flag;
             const int64_t nnz = (int64_t)g->nnz;
@@ -1754,11 +1768,18 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             const SparseLists sl{C->al.p, C->asub, cnt, only};
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
                                   use_sparse ? &sl : nullptr, kFlagShards, st));
-        } else if (it == 0 && !relabel && C->rows_sorted && first_sorted) {
+        } else if (it == 0 && C->rows_sorted && first_sorted) {
+            // on the caller's graph and vertex order (whose rows the check found sorted)
             KTimer kt(ctx, "cdlp_first", s);
-            hipLaunchKernelGGL(k_cdlp_first_sorted, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, G.rpA, G.ciA,
-                               (int64_t)0, n, nxt, changed, kFlagShards);
+            int32_t *out = relabel ? C->tmp.p : nxt;
+            hipLaunchKernelGGL(k_cdlp_first_sorted, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p,
+                               g->A.ci.p, (int64_t)0, n, out, changed, kFlagShards);
             GX_TRY(check_launch("k_cdlp_first_sorted"));
+            if (relabel) {   // nxt[p] = result of the caller's vertex order[p]
+                hipLaunchKernelGGL(k_cdlp_gather_i32, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, C->tmp.p,
+                                   C->order.p, n, nxt);
+                GX_TRY(check_launch("k_cdlp_gather_i32"));
+            }
         } else {
             // iteration 0: labels are the caller's vertex ids
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0, nullptr, kFlagShards, st));
