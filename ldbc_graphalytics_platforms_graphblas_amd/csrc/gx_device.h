@@ -141,6 +141,7 @@ struct gx_graph {
     int bfs_calls = 0;          // BFS runs on this graph (a directed graph builds A^T from the second)
     gx::SsspLayout *sssp = nullptr;   // cached light/heavy edge layout
     std::shared_ptr<void> cdlp;       // gx_cdlp's tier lists and buffers (gx_cdlp.hip CdlpCache)
+    std::shared_ptr<void> lcc;        // gx_lcc's orientation and work items (gx_lcc.hip LccCache)
 };
 
 namespace gx {

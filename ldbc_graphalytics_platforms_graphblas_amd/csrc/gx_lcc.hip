@@ -486,38 +486,55 @@ int lcc_orient(gx_graph *g, LccOrient &O, hipStream_t s) {
     return GX_SUCCESS;
 }
 
-// Adds the contributions of every triangle whose middle vertex (in orientation rank) lies in
-// [v0, v1) into tc (n counters).
-int lcc_count_range(gx_graph *g, const LccOrient &O, int64_t v0, int64_t v1, unsigned long long *tc,
-                    hipStream_t s) {
-    gx_ctx *ctx = g->ctx;
+// The work items of the middle vertices in [v0, v1), by tier (k_lcc_items).
+struct LccItems {
+    DBuf<uint64_t> items0, items1, items2;
+    DBuf<int32_t> big;
+    std::vector<int32_t> h_big;
+    uint32_t hc[5] = {0, 0, 0, 0, 0};   // items per tier, then the largest workgroup-tier |O(u)|
+};
+
+int lcc_items(const LccOrient &O, int64_t v0, int64_t v1, LccItems &L, hipStream_t s) {
     const int64_t nv = v1 - v0;
     if (nv <= 0 || O.m == 0) return GX_SUCCESS;
     const uint64_t icap = (uint64_t)nv + (uint64_t)O.m / kWaveGroup + 64;
-    DBuf<uint64_t> items0, items1, items2;
-    DBuf<int32_t> big;
     DBuf<uint32_t> counts;
-    GX_TRY(items0.alloc(icap));
-    GX_TRY(items1.alloc(icap));
-    GX_TRY(items2.alloc(icap));
-    GX_TRY(big.alloc(nv));
+    GX_TRY(L.items0.alloc(icap));
+    GX_TRY(L.items1.alloc(icap));
+    GX_TRY(L.items2.alloc(icap));
+    GX_TRY(L.big.alloc(nv));
     GX_TRY(counts.alloc(5));
     GX_HIP_TRY(hipMemsetAsync(counts.p, 0, 20, s));
     hipLaunchKernelGGL(k_lcc_items, dim3((unsigned)std::min<int64_t>((nv + kClassTile - 1) / kClassTile, 2048)),
-                       dim3(kLccBlock), 0, s, O.orp.p, O.irp.p, v0, v1, items0.p, items1.p, items2.p, big.p, counts.p);
+                       dim3(kLccBlock), 0, s, O.orp.p, O.irp.p, v0, v1, L.items0.p, L.items1.p, L.items2.p, L.big.p,
+                       counts.p);
     GX_TRY(check_launch("k_lcc_items"));
-    uint32_t hc[5] = {0, 0, 0, 0, 0};
-    GX_HIP_TRY(hipMemcpyAsync(hc, counts.p, 20, hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipMemcpyAsync(L.hc, counts.p, 20, hipMemcpyDeviceToHost, s));
     GX_HIP_TRY(hipStreamSynchronize(s));
+    if (L.hc[3]) {
+        L.h_big.resize(L.hc[3]);
+        GX_HIP_TRY(hipMemcpyAsync(L.h_big.data(), L.big.p, L.hc[3] * 4, hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+    }
+    return GX_SUCCESS;
+}
+
+// Adds the contributions of every triangle whose middle vertex is one of the items' into tc
+// (n counters).
+int lcc_count_items(gx_graph *g, const LccOrient &O, const LccItems &L, unsigned long long *tc, hipStream_t s) {
+    gx_ctx *ctx = g->ctx;
+    if (O.m == 0) return GX_SUCCESS;
+    const uint32_t *hc = L.hc;
+    const uint64_t *items0 = L.items0.p, *items1 = L.items1.p, *items2 = L.items2.p;
     {
         KTimer kt(ctx, "lcc_triangles", s);
         if (hc[0])
             hipLaunchKernelGGL(k_lcc_wave<512>, dim3(grid_for((uint64_t)hc[0] * kWave, kLccBlock, 8192)),
-                               dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items0.p, hc[0], tc);
+                               dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items0, hc[0], tc);
         GX_TRY(check_launch("k_lcc_wave<512>"));
         if (hc[1])
             hipLaunchKernelGGL(k_lcc_wave<1024>, dim3(grid_for((uint64_t)hc[1] * kWave, kLccBlock, 8192)),
-                               dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items1.p, hc[1], tc);
+                               dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items1, hc[1], tc);
         GX_TRY(check_launch("k_lcc_wave<1024>"));
         if (hc[2]) {
             const uint32_t slots = std::max<uint32_t>(64, std::min<uint32_t>(kBlockSlots, [&] {
@@ -529,24 +546,39 @@ int lcc_count_range(gx_graph *g, const LccOrient &O, int64_t v0, int64_t v1, uns
                 GX_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lcc_block),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(slots * 8)));
             hipLaunchKernelGGL(k_lcc_block, dim3(std::min<uint32_t>(hc[2], 4096)), dim3(kLccBlock),
-                               (size_t)slots * 8, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items2.p, hc[2], slots,
+                               (size_t)slots * 8, s, O.orp.p, O.ocode.p, O.irp.p, O.icode.p, items2, hc[2], slots,
                                tc);
         }
         GX_TRY(check_launch("k_lcc_block"));
         if (hc[3]) {
-            std::vector<int32_t> hb(hc[3]);
-            GX_HIP_TRY(hipMemcpyAsync(hb.data(), big.p, hc[3] * 4, hipMemcpyDeviceToHost, s));
-            GX_HIP_TRY(hipStreamSynchronize(s));
-            for (int32_t u : hb) {
+            for (int32_t u : L.h_big) {
                 hipLaunchKernelGGL(k_lcc_merge_in, dim3(64), dim3(kLccBlock), 0, s, O.orp.p, O.ocode.p, O.irp.p,
                                    O.icode.p, u, tc);
                 GX_TRY(check_launch("k_lcc_merge_in"));
             }
         }
     }
+    return GX_SUCCESS;
+}
+
+int lcc_count_range(gx_graph *g, const LccOrient &O, int64_t v0, int64_t v1, unsigned long long *tc,
+                    hipStream_t s) {
+    LccItems L;
+    GX_TRY(lcc_items(O, v0, v1, L, s));
+    GX_TRY(lcc_count_items(g, O, L, tc, s));
     GX_HIP_TRY(hipStreamSynchronize(s));   // item lists are freed on return
     return GX_SUCCESS;
 }
+
+// What gx_lcc keeps on the graph between calls (gx_graph::lcc), next to the cached closure
+// it is derived from: the orientation O, its transpose I and the work items (~2.2 ms of
+// sorts, scans and host round trips per call on SYN-cit when rebuilt).
+struct LccCache {
+    LccOrient O;
+    LccItems L;
+    DBuf<unsigned long long> tc;
+    DBuf<double> out;
+};
 
 }  // namespace
 }  // namespace gx
@@ -564,18 +596,22 @@ extern "C" int gx_lcc(gx_graph *g, double *lcc) {
     if (n == 0) return GX_SUCCESS;
     GX_TRY(device_begin(ctx));
     GX_TRY(ensure_closure(g));
-    LccOrient O;
-    GX_TRY(lcc_orient(g, O, s));
-    DBuf<unsigned long long> tc;
-    DBuf<double> out;
-    GX_TRY(tc.alloc(n));
-    GX_TRY(out.alloc(n));
-    GX_HIP_TRY(hipMemsetAsync(tc.p, 0, n * 8, s));
-    GX_TRY(lcc_count_range(g, O, 0, n, tc.p, s));
-    hipLaunchKernelGGL(k_lcc_final, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->S.rp.p, tc.p, n, out.p);
+    auto *C = static_cast<LccCache *>(g->lcc.get());
+    if (!C) {
+        auto fresh = std::make_shared<LccCache>();
+        GX_TRY(lcc_orient(g, fresh->O, s));
+        GX_TRY(lcc_items(fresh->O, 0, n, fresh->L, s));
+        GX_TRY(fresh->tc.alloc(n));
+        GX_TRY(fresh->out.alloc(n));
+        g->lcc = fresh;
+        C = fresh.get();
+    }
+    GX_HIP_TRY(hipMemsetAsync(C->tc.p, 0, n * 8, s));
+    GX_TRY(lcc_count_items(g, C->O, C->L, C->tc.p, s));
+    hipLaunchKernelGGL(k_lcc_final, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->S.rp.p, C->tc.p, n, C->out.p);
     GX_TRY(check_launch("k_lcc_final"));
     GX_TRY(device_end(ctx));
-    GX_TRY(download(ctx, lcc, out.p, (uint64_t)n, Xfer::Raw64));
+    GX_TRY(download(ctx, lcc, C->out.p, (uint64_t)n, Xfer::Raw64));
     return GX_SUCCESS;
 }
 
