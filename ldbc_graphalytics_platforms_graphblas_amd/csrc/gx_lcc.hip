@@ -202,15 +202,43 @@ __device__ __forceinline__ void table_build(const int64_t *__restrict__ orp, con
     }
 }
 
+// Per-wave LDS scratch of probe_in_group: the nonempty lists by rank, and the list starts
+// falling in the current 64-entry window.
+struct WaveScratch {
+    uint64_t rank[kWave];   // (O(v) start - list offset) as 48-bit signed | popcount(v,u) << 48 | lane << 56
+    uint8_t mark[kWave];
+};
+
+// Which list holds position E0 + lane of the concatenated lists, and where that entry is in
+// ocode: lists starting inside the window mark their offset, one ballot turns the marks into a
+// mask, and the list's rank is cb (lists started before the window) plus the marks at or below
+// the lane.  Replaces a 6-step shuffle binary search (six dependent ds_bpermute per window).
+__device__ __forceinline__ int64_t probe_locate(WaveScratch *ws, int32_t excl, int32_t vl, int lane, int32_t E0,
+                                                int32_t total, int &cb, uint64_t &pk, bool &act) {
+    if (vl > 0 && excl >= E0 && excl < E0 + kWave) ws->mark[excl - E0] = 1;
+    wave_sync_lds();
+    const unsigned long long M = __ballot(ws->mark[lane] != 0);
+    ws->mark[lane] = 0;
+    const int32_t e = E0 + lane;
+    act = e < total;
+    const unsigned long long upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1ull);
+    const int r = cb + __popcll(M & upto) - 1;
+    cb += __popcll(M);
+    pk = act ? ws->rank[r] : 0ull;
+    wave_sync_lds();
+    return ((int64_t)(pk << 16) >> 16) + e;
+}
+
 // Probe the lists O(v) of the (up to 64) in-neighbours icode[ib .. ie) of u, one per lane,
-// against the table of O(u).  Lanes walk the concatenated lists 64 entries at a time (owner
-// lane by shuffle search).  Returns u's contribution; v's go to vcnt[lane], x's into the
-// table values.
+// against the table of O(u).  Lanes walk the concatenated lists 64 entries at a time; the next
+// window's entries are located and loaded before the current one is probed.  Returns u's
+// contribution; v's go to vcnt[lane], x's into the table values.
 __device__ __forceinline__ unsigned long long probe_in_group(const int64_t *__restrict__ orp,
                                                              const uint32_t *__restrict__ ocode,
                                                              const uint32_t *__restrict__ icode, int64_t ib,
                                                              int64_t ie, const int32_t *hkey, uint32_t *hval,
-                                                             uint32_t hmask, uint32_t *vcnt, int lane) {
+                                                             uint32_t hmask, uint32_t *vcnt, int lane,
+                                                             WaveScratch *ws) {
     const int64_t i = ib + lane;
     const bool has = i < ie;
     const uint32_t ic = has ? icode[i] : 0u;
@@ -226,27 +254,35 @@ __device__ __forceinline__ unsigned long long probe_in_group(const int64_t *__re
     }
     const int32_t total = __shfl(incl, kWave - 1, kWave);
     const int32_t excl = incl - vl;
+    const unsigned long long ne = __ballot(vl > 0);
+    if (vl > 0)
+        ws->rank[__popcll(ne & ((1ull << lane) - 1ull))] =
+            ((uint64_t)(vb - excl) & 0xffffffffffffull) | ((uint64_t)p_vu << 48) | ((uint64_t)lane << 56);
+    ws->mark[lane] = 0;
     unsigned long long tu = 0;
+    if (total == 0) return tu;
+    int cb = 0;
+    uint64_t pk;
+    bool act;
+    int64_t k = probe_locate(ws, excl, vl, lane, 0, total, cb, pk, act);
+    uint32_t c = act ? ocode[k] : 0u;
     for (int32_t e0 = 0; e0 < total; e0 += kWave) {
-        const int32_t e_raw = e0 + lane;
-        const bool act = e_raw < total;
-        const int32_t e = act ? e_raw : total - 1;
-        int o = 0;
-#pragma unroll
-        for (int step = kWave / 2; step > 0; step >>= 1)
-            if (__shfl(incl, o + step - 1, kWave) <= e) o += step;
-        const int64_t k = __shfl(vb, o, kWave) + (e - __shfl(excl, o, kWave));
-        const uint32_t f_vu = __shfl(p_vu, o, kWave);
-        const uint32_t c = ocode[k];
-        if (act) {
-            const int32_t x = (int32_t)(c >> 2);
+        const uint32_t cc = c;
+        const uint64_t pc = pk;
+        const bool ac = act;
+        if (e0 + kWave < total) {
+            k = probe_locate(ws, excl, vl, lane, e0 + kWave, total, cb, pk, act);
+            c = act ? ocode[k] : 0u;
+        }
+        if (ac) {
+            const int32_t x = (int32_t)(cc >> 2);
             uint32_t h = hash_slot(x, hmask);
             int32_t key;
             while ((key = hkey[h]) != x && key != -1) h = (h + 1) & hmask;
             if (key == x) {
-                tu += c & 3u;                              // u: directions between v and x
-                atomicAdd(&vcnt[o], hval[h] >> 30);        // v: directions between u and x
-                atomicAdd(&hval[h], f_vu);                 // x: directions between v and u
+                tu += cc & 3u;                                         // u: directions between v and x
+                atomicAdd(&vcnt[pc >> 56], hval[h] >> 30);             // v: directions between u and x
+                atomicAdd(&hval[h], (uint32_t)(pc >> 48) & 3u);        // x: directions between v and u
             }
         }
     }
@@ -269,6 +305,7 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_wave(const int64_t *__restric
     __shared__ int32_t s_key[kWavesPerBlock][kWaveSlots];
     __shared__ uint32_t s_val[kWavesPerBlock][kWaveSlots];
     __shared__ uint32_t s_vcnt[kWavesPerBlock][kWave];
+    __shared__ WaveScratch s_ws[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
     int32_t *hkey = s_key[wv];
     uint32_t *hval = s_val[wv];
@@ -287,7 +324,8 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_wave(const int64_t *__restric
         wave_sync_lds();
         table_build(orp, ocode, u, hkey, hval, slots, lane, kWave);
         wave_sync_lds();
-        unsigned long long tu = probe_in_group(orp, ocode, icode, ib, ie, hkey, hval, slots - 1, vcnt, lane);
+        unsigned long long tu =
+            probe_in_group(orp, ocode, icode, ib, ie, hkey, hval, slots - 1, vcnt, lane, &s_ws[wv]);
         wave_sync_lds();
         const uint32_t c = vcnt[lane];
         if (c && ib + lane < ie) atomicAdd(&tc[icode[ib + lane] >> 2], (unsigned long long)c);
@@ -311,6 +349,7 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_block(const int64_t *__restri
     int32_t *hkey = reinterpret_cast<int32_t *>(dyn);
     uint32_t *hval = dyn + max_slots;
     __shared__ uint32_t s_vcnt[kWavesPerBlock][kWave];
+    __shared__ WaveScratch s_ws[kWavesPerBlock];
     __shared__ unsigned long long s_tu[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
     uint32_t *vcnt = s_vcnt[wv];
@@ -329,7 +368,7 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_block(const int64_t *__restri
         __syncthreads();
         const int64_t ib = ib0 + (int64_t)wv * kWave, ie = min(ie0, ib + kWave);
         unsigned long long tu = 0;
-        if (ib < ie) tu = probe_in_group(orp, ocode, icode, ib, ie, hkey, hval, slots - 1, vcnt, lane);
+        if (ib < ie) tu = probe_in_group(orp, ocode, icode, ib, ie, hkey, hval, slots - 1, vcnt, lane, &s_ws[wv]);
         wave_sync_lds();
         const uint32_t c = vcnt[lane];
         if (c && ib + lane < ie) atomicAdd(&tc[icode[ib + lane] >> 2], (unsigned long long)c);
