@@ -64,8 +64,12 @@ struct SsspState {
     int32_t epoch;                // relaxations append to overflow[epoch & 1]
     int32_t mode;                 // advance: 0 none, 1 open ring slot, 2 split overflow, 3 heavy items
     int32_t heavy;                // relax phase: 0 light edges, 1 heavy edges
-    int32_t slot;                 // ring slot opened (mode 1)
-    int32_t consume;              // ring slot to clear at the next plan, -1 none
+    int32_t slot;                 // first ring slot opened (mode 1)
+    int32_t nslots;               // ring slots opened together (bucket fusion, mode 1)
+    int32_t consume;              // first ring slot to clear at the next plan, -1 none
+    int32_t consume_n;            // ... and how many
+    uint32_t fuse;                // bucket fusion: open further buckets while the entries stay <= fuse
+    int32_t fuse_max;             // ... and at most fuse_max buckets (<= kRing)
     int32_t split_src;            // overflow list being split (mode 2)
     uint32_t qcnt[2];
     uint32_t ovf_cnt[2];
@@ -276,7 +280,7 @@ __global__ void k_sssp_plan(SsspState *st) {
     }
     const int32_t r = ++st->round;
     if (st->consume >= 0) {
-        st->ring_cnt[st->consume] = 0;
+        for (int j = 0; j < st->consume_n; j++) st->ring_cnt[(st->consume + j) % kRing] = 0;
         st->consume = -1;
     }
     const int qin = r & 1;
@@ -296,10 +300,25 @@ __global__ void k_sssp_plan(SsspState *st) {
     for (int64_t b = st->cur + 1; b < lim; b++) {
         const int s = (int)(b % kRing);
         if (st->ring_cnt[s] > 0) {
-            st->cur = b;
+            // bucket fusion: the later buckets of a sparse tail (SYN-8_5 from bucket ~20: ~40 K
+            // entries, almost no light edges) cost a plan/advance/relax triple each, mostly
+            // fixed cost; while the entries stay within `fuse`, the next buckets are opened
+            // with it and settled as one.  Distances are the relaxation fixed point whatever
+            // the grouping (a heavy edge landing inside the group goes past it, as always).
+            uint32_t tot = st->ring_cnt[s];
+            int64_t last = b;
+            for (int64_t b2 = b + 1; b2 < lim && b2 < b + st->fuse_max; b2++) {
+                const uint32_t c = st->ring_cnt[b2 % kRing];
+                if (tot + c > st->fuse) break;
+                tot += c;
+                last = b2;
+            }
+            st->cur = last;
             st->mode = 1;
             st->slot = s;
+            st->nslots = (int32_t)(last - b + 1);
             st->consume = s;
+            st->consume_n = st->nslots;
             return;
         }
     }
@@ -331,9 +350,13 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     const int qin = r & 1;
     const int32_t *list;
     uint32_t count;
+    int32_t fslot = 0, fn = 1;
     if (mode == 1) {
-        list = B.ring + (uint64_t)st->slot * B.ring_cap;
-        count = st->ring_cnt[st->slot];
+        fslot = st->slot;
+        fn = st->nslots;
+        list = B.ring + (uint64_t)fslot * B.ring_cap;
+        count = 0;
+        for (int j = 0; j < fn; j++) count += st->ring_cnt[(fslot + j) % kRing];
     } else if (mode == 2) {
         list = B.ovf[st->split_src];
         count = st->ovf_cnt[st->split_src];
@@ -342,6 +365,9 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
         count = st->settled_cnt;
     }
     if ((uint64_t)blockIdx.x * kSsspBlock >= count) return;   // no entry for this workgroup
+    __shared__ uint32_t fcnt[kRing];                            // fused slots' entry counts (mode 1)
+    if (fn > 1 && (int)threadIdx.x < fn) fcnt[threadIdx.x] = st->ring_cnt[(fslot + threadIdx.x) % kRing];
+    __syncthreads();
     const int64_t cur = st->cur, win_base = st->win_base, lim = win_base + kRing;
     const int32_t epoch = st->epoch;
     const bool pull = mode == 3 && st->pull;
@@ -364,7 +390,14 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
         int slot = 0;
         uint32_t nch = 0;
         if (f < count) {
-            v = list[f];
+            if (fn > 1) {   // entry f of the fused slots' concatenation
+                uint32_t g = f;
+                int j = 0;
+                while (g >= fcnt[j]) g -= fcnt[j++];
+                v = B.ring[(uint64_t)((fslot + j) % kRing) * B.ring_cap + g];
+            } else {
+                v = list[f];
+            }
             const unsigned long long db = B.dist[v];
             if (mode == 3) {
                 B.relaxed[v] = db;   // heavy edges now, light edges already relaxed at db
@@ -377,11 +410,14 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
             } else if (db == B.relaxed[v]) {
                 n_skip++;
             } else if (mode == 1) {
-                // entries are unique within a slot: plain stores
-                B.near_stamp[v] = r;
-                B.sstamp[v] = (int32_t)cur;
-                to_near = to_set = true;
-                nch = chunks_of(B.lend[v] - B.rp[v]);
+                // entries are unique within a slot (plain stores); a vertex can sit in two
+                // fused slots, so there the near stamp is claimed
+                if (fn == 1 || claim(&B.near_stamp[v], r)) {
+                    if (fn == 1) B.near_stamp[v] = r;
+                    B.sstamp[v] = (int32_t)cur;
+                    to_near = to_set = true;
+                    nch = chunks_of(B.lend[v] - B.rp[v]);
+                }
             } else {
                 const int64_t b = max(bucket_of(bitsd(db), B.inv_delta), win_base);
                 if (b < lim) {
@@ -767,7 +803,7 @@ __global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxe
     }
 }
 
-__global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min) {
+__global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t fuse, int32_t fuse_max) {
     SsspState *st = B.st;
     const uint32_t nch = chunks_of(B.lend[src] - B.rp[src]);
     for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x) B.q[0][j] = ((uint64_t)(uint32_t)src << 32) | j;
@@ -790,7 +826,11 @@ __global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min) {
         st->pull_min = pull_min;
         st->smin = ~0ull;
         st->slot = 0;
+        st->nslots = 1;
         st->consume = -1;
+        st->consume_n = 0;
+        st->fuse = fuse;
+        st->fuse_max = fuse_max;
         st->split_src = 0;
         st->qcnt[0] = nch;
         st->qcnt[1] = 0;
@@ -1027,9 +1067,10 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         }
         g->mean_w = mean;
     }
-    // measured on the SYN stand-ins: 5 for undirected graphs, whose big early
-    // buckets are pulled, 2 for directed ones
-    double delta = 0.0, scale = g->directed ? 2.0 : 5.0;
+    // measured on the SYN stand-ins with bucket fusion: 4 for undirected graphs,
+    // whose big early buckets are pulled (below ~2.5 the first bucket no longer reaches the
+    // pull threshold on SYN-8_5: 14.8 ms), 0.5 for directed ones
+    double delta = 0.0, scale = g->directed ? 0.5 : 4.0;
     if (const char *e = std::getenv("GX_SSSP_DELTA")) delta = std::atof(e);
     if (const char *e = std::getenv("GX_SSSP_DSCALE")) scale = std::atof(e);
     if (!(delta > 0.0)) {
@@ -1078,7 +1119,13 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         else if (!g->directed && mode == 1 && frac > 0.0)
             pull_min = (uint32_t)std::max<double>(1.0, std::ceil((double)lay.n_active / frac));
     }
-    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min);
+    // bucket fusion bounds (GX_SSSP_FUSE entries, 0 = one bucket at a time; GX_SSSP_FUSE_MAX
+    // buckets)
+    uint32_t fuse = 0xFFFFFFFFu;
+    int32_t fuse_max = kRing;
+    if (const char *e = std::getenv("GX_SSSP_FUSE")) fuse = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char *e = std::getenv("GX_SSSP_FUSE_MAX")) fuse_max = std::max(1, std::min(kRing, std::atoi(e)));
+    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min, fuse, fuse_max);
     GX_TRY(check_launch("k_sssp_seed"));
     const unsigned grid = (unsigned)std::max(1, ctx->num_cus) * 8;
     // a bound every correct run stays far below: each step settles a vertex or a bucket
