@@ -237,11 +237,14 @@ def test_pagerank_escape_groups(ctx, monkeypatch):
 @pytest.mark.parametrize("env", [{"GX_SSSP_PULL": "0"}, {"GX_SSSP_PULL": "2"},
                                  {"GX_SSSP_PULL": "2", "GX_SSSP_DSCALE": "2"},
                                  {"GX_SSSP_PULL": "2", "GX_SSSP_DSCALE": "200"},
-                                 {"GX_SSSP_PULL_FRAC": "50", "GX_SSSP_DSCALE": "5"}])
+                                 {"GX_SSSP_PULL_FRAC": "50", "GX_SSSP_DSCALE": "5"},
+                                 {"GX_SSSP_FUSE": "0"}, {"GX_SSSP_FUSE": "300", "GX_SSSP_DSCALE": "0.5"},
+                                 {"GX_SSSP_FUSE_MAX": "3", "GX_SSSP_DSCALE": "1"}])
 def test_sssp_pull_heavy_phase(ctx, monkeypatch, env):
     """Heavy phases pushed, always pulled, and pulled only for big settled lists, over narrow
-    and wide buckets, give the oracle's distances bit for bit -- also with integer weights
-    (ties at bucket boundaries) and on a directed graph (where the pull is never used)."""
+    and wide buckets, with buckets opened one at a time or fused (GX_SSSP_FUSE entries,
+    GX_SSSP_FUSE_MAX buckets), give the oracle's distances bit for bit -- also with integer
+    weights (ties at bucket boundaries) and on a directed graph (where the pull is never used)."""
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
     for k, v in env.items():
         monkeypatch.setenv(k, v)
