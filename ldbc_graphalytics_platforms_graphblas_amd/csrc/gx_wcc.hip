@@ -17,6 +17,7 @@
 // parent[v] <= v always holds, so the root of each final tree is the smallest vertex index
 // of the component: comp[v] is canonical and equals the oracle's union-find labels exactly.
 #include <algorithm>
+#include <cstdlib>
 
 #include "gx_device.h"
 
@@ -60,6 +61,35 @@ __device__ __forceinline__ void link(int32_t *parent, int32_t u, int32_t v) {
         if (ph == high && atomicCAS(&parent[high], high, low) == high) break;
         p1 = __hip_atomic_load(&parent[ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         p2 = __hip_atomic_load(&parent[low], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Afforest sampling round 0 from the identity forest without atomics: a vertex whose first
+// neighbour is smaller points at it (plain store of its own entry; pointers only go down, so
+// no cycle), and only the vertices whose first neighbour is larger link in a second pass.
+__global__ __launch_bounds__(kWccBlock) void k_afforest_hook0(const int64_t *__restrict__ rp,
+                                                              const int32_t *__restrict__ ci, int64_t n,
+                                                              int32_t *parent) {
+    for (int64_t v = (int64_t)blockIdx.x * kWccBlock + threadIdx.x; v < n;
+         v += (int64_t)gridDim.x * kWccBlock) {
+        const int64_t k = rp[v];
+        if (k < rp[v + 1]) {
+            const int32_t u = ci[k];
+            if (u < (int32_t)v) parent[v] = u;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kWccBlock) void k_afforest_link0(const int64_t *__restrict__ rp,
+                                                              const int32_t *__restrict__ ci, int64_t n,
+                                                              int32_t *parent) {
+    for (int64_t v = (int64_t)blockIdx.x * kWccBlock + threadIdx.x; v < n;
+         v += (int64_t)gridDim.x * kWccBlock) {
+        const int64_t k = rp[v];
+        if (k < rp[v + 1]) {
+            const int32_t u = ci[k];
+            if (u > (int32_t)v) link(parent, (int32_t)v, u);
+        }
     }
 }
 
@@ -141,11 +171,19 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
     if (!g->directed && nnz) {
         // ---- Afforest: sample two neighbours per vertex, find the giant component from
         // 1024 sampled roots, then link only the remaining edges of the other vertices.
+        const bool hook0 = !std::getenv("GX_WCC_HOOK0") || std::atoi(std::getenv("GX_WCC_HOOK0")) != 0;
         for (int r = 0; r < 2; r++) {
             {
                 KTimer kt(ctx, "wcc_sample", s);
-                hipLaunchKernelGGL(k_afforest_sample, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, r,
-                                   parent.p);
+                if (r == 0 && hook0) {
+                    hipLaunchKernelGGL(k_afforest_hook0, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
+                                       parent.p);
+                    hipLaunchKernelGGL(k_afforest_link0, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
+                                       parent.p);
+                } else {
+                    hipLaunchKernelGGL(k_afforest_sample, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
+                                       r, parent.p);
+                }
             }
             GX_TRY(check_launch("k_afforest_sample"));
             {
