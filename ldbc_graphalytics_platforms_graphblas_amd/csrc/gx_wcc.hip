@@ -113,11 +113,25 @@ __global__ __launch_bounds__(kWccBlock) void k_afforest_finish(const int64_t *__
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t w0 = ((int64_t)blockIdx.x * kWccBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kWccBlock / kWave);
-    for (int64_t v = w0; v < n; v += nw) {
-        const int64_t b = rp[v] + skip, e = rp[v + 1];
-        if (b >= e) continue;
-        if (find_root(parent, (int32_t)v) == giant) continue;
-        for (int64_t k = b + lane; k < e; k += kWave) link(parent, (int32_t)v, ci[k]);
+    // the giant-component test for 64 vertices at once (one per lane, coalesced), then the
+    // wave links the rows of the few outside it (a wave walking its vertices one by one spent
+    // a dependent root lookup per vertex)
+    for (int64_t base = w0 * kWave; base < n; base += nw * kWave) {
+        const int64_t v = base + lane;
+        int64_t b = 0, e = 0;
+        bool need = false;
+        if (v < n) {
+            b = rp[v] + skip;
+            e = rp[v + 1];
+            need = b < e && find_root(parent, (int32_t)v) != giant;
+        }
+        unsigned long long m = __ballot(need);
+        while (m) {
+            const int l = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int64_t vb = __shfl(b, l, kWave), ve = __shfl(e, l, kWave);
+            for (int64_t k = vb + lane; k < ve; k += kWave) link(parent, (int32_t)(base + l), ci[k]);
+        }
     }
 }
 
@@ -222,7 +236,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         }
         {
             KTimer kt(ctx, "wcc_hook", s);
-            hipLaunchKernelGGL(k_afforest_finish, dim3(grid_for((uint64_t)n * kWave, kWccBlock, 8192)),
+            hipLaunchKernelGGL(k_afforest_finish, dim3(grid_for((uint64_t)n, kWccBlock, 8192)),
                                dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, 2, giant, parent.p);
         }
         GX_TRY(check_launch("k_afforest_finish"));
