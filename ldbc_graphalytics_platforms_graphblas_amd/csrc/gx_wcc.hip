@@ -93,6 +93,49 @@ __global__ __launch_bounds__(kWccBlock) void k_afforest_link0(const int64_t *__r
     }
 }
 
+// Afforest sampling round r >= 1, first pass, on a compressed forest: the roots of v and of its
+// r-th neighbour are joined by an atomicMin of the higher root's parent (issued only if it
+// lowers it).  Many pairs target the same root, and there CAS links retried in series (534 us
+// of a 1.1 ms WCC on SYN-g500-22); here the lowest wins at once and the pairs whose union was
+// lost are few and retried by k_afforest_sample with distinct targets.  Pointers only go
+// down, so no cycle; only pointers of roots change, so earlier unions stand.
+__global__ __launch_bounds__(kWccBlock) void k_afforest_minhook(const int64_t *__restrict__ rp,
+                                                                const int32_t *__restrict__ ci, int64_t n, int r,
+                                                                int32_t *parent) {
+    // wave-uniform trip count: the ballots and shuffles below see every lane
+    for (int64_t base = (int64_t)blockIdx.x * kWccBlock + (threadIdx.x & ~(kWave - 1)); base < n;
+         base += (int64_t)gridDim.x * kWccBlock) {
+        const int64_t v = base + (threadIdx.x & (kWave - 1));
+        const int64_t k = v < n ? rp[v] + r : 0;
+        int32_t high = 0, low = 0;
+        bool want = false;
+        if (v < n && k < rp[v + 1]) {
+            const int32_t r1 = __hip_atomic_load(&parent[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int32_t r2 = __hip_atomic_load(&parent[ci[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            high = max(r1, r2);
+            low = min(r1, r2);
+            want = r1 != r2 && low < __hip_atomic_load(&parent[high], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // lanes aiming at the same root as the first remaining lane send one atomic with their
+        // smallest low (two rounds): a few hot roots drew most of the atomics, in series
+        const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+        for (int round = 0; round < 2; round++) {
+            const unsigned long long act = __ballot(want);
+            if (!act) break;
+            const int first = __ffsll((long long)act) - 1;
+            const int32_t lead = __shfl(high, first, kWave);
+            const bool same = want && high == lead;
+            int32_t m = same ? low : 0x7fffffff;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) m = min(m, __shfl_xor(m, off, kWave));
+            if (lane == first) __hip_atomic_fetch_min(&parent[lead], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            want = want && !same;
+        }
+        if (want) __hip_atomic_fetch_min(&parent[high], low, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Afforest sampling round r: link every vertex with its r-th neighbour.
 __global__ __launch_bounds__(kWccBlock) void k_afforest_sample(const int64_t *__restrict__ rp,
                                                                const int32_t *__restrict__ ci, int64_t n,
@@ -164,6 +207,46 @@ __global__ void k_iota(int32_t *a, int64_t n) {
         a[v] = (int32_t)v;
 }
 
+// Afforest's two sampling rounds (each vertex with its first, then its second neighbour),
+// each followed by pointer jumping: round 0 by k_afforest_hook0/link0, round 1 by min-hook
+// passes before the CAS links (GX_WCC_HOOK0=0 / GX_WCC_MINHOOK=0: CAS links only).
+int afforest_sample(gx_graph *g, int32_t *parent, unsigned vgrid, hipStream_t s) {
+    gx_ctx *ctx = g->ctx;
+    const int64_t n = (int64_t)g->n;
+    // default on for undirected graphs only: on SYN-cit (directed, out-neighbours) the
+    // passes cost more than the CAS links they spare (1.21 vs 1.09 ms)
+    const bool und = !g->directed;
+    const bool hook0 = std::getenv("GX_WCC_HOOK0") ? std::atoi(std::getenv("GX_WCC_HOOK0")) != 0 : und;
+    const int minhook = std::getenv("GX_WCC_MINHOOK") ? std::atoi(std::getenv("GX_WCC_MINHOOK")) : (und ? 1 : 0);
+    for (int r = 0; r < 2; r++) {
+        for (int pass = 0; r > 0 && pass < minhook; pass++) {
+            KTimer kt(ctx, "wcc_sample", s);
+            hipLaunchKernelGGL(k_afforest_minhook, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, r,
+                               parent);
+            hipLaunchKernelGGL(k_wcc_compress, dim3(vgrid), dim3(kWccBlock), 0, s, parent, n);
+        }
+        {
+            KTimer kt(ctx, "wcc_sample", s);
+            if (r == 0 && hook0) {
+                hipLaunchKernelGGL(k_afforest_hook0, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
+                                   parent);
+                hipLaunchKernelGGL(k_afforest_link0, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
+                                   parent);
+            } else {
+                hipLaunchKernelGGL(k_afforest_sample, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
+                                   r, parent);
+            }
+        }
+        GX_TRY(check_launch("k_afforest_sample"));
+        {
+            KTimer kt(ctx, "wcc_compress", s);
+            hipLaunchKernelGGL(k_wcc_compress, dim3(vgrid), dim3(kWccBlock), 0, s, parent, n);
+        }
+        GX_TRY(check_launch("k_wcc_compress"));
+    }
+    return GX_SUCCESS;
+}
+
 }  // namespace
 }  // namespace gx
 
@@ -185,27 +268,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
     if (!g->directed && nnz) {
         // ---- Afforest: sample two neighbours per vertex, find the giant component from
         // 1024 sampled roots, then link only the remaining edges of the other vertices.
-        const bool hook0 = !std::getenv("GX_WCC_HOOK0") || std::atoi(std::getenv("GX_WCC_HOOK0")) != 0;
-        for (int r = 0; r < 2; r++) {
-            {
-                KTimer kt(ctx, "wcc_sample", s);
-                if (r == 0 && hook0) {
-                    hipLaunchKernelGGL(k_afforest_hook0, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
-                                       parent.p);
-                    hipLaunchKernelGGL(k_afforest_link0, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
-                                       parent.p);
-                } else {
-                    hipLaunchKernelGGL(k_afforest_sample, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n,
-                                       r, parent.p);
-                }
-            }
-            GX_TRY(check_launch("k_afforest_sample"));
-            {
-                KTimer kt(ctx, "wcc_compress", s);
-                hipLaunchKernelGGL(k_wcc_compress, dim3(vgrid), dim3(kWccBlock), 0, s, parent.p, n);
-            }
-            GX_TRY(check_launch("k_wcc_compress"));
-        }
+        GX_TRY(afforest_sample(g, parent.p, vgrid, s));
         constexpr int kSamples = 1024;
         std::vector<int32_t> ids(kSamples), roots(kSamples);
         uint64_t h = 0x9E3779B97F4A7C15ull;
@@ -247,19 +310,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         GX_TRY(check_launch("k_wcc_compress"));
     }
     if (g->directed && nnz) {
-        for (int r = 0; r < 2; r++) {
-            {
-                KTimer kt(ctx, "wcc_sample", s);
-                hipLaunchKernelGGL(k_afforest_sample, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, r,
-                                   parent.p);
-            }
-            GX_TRY(check_launch("k_afforest_sample"));
-            {
-                KTimer kt(ctx, "wcc_compress", s);
-                hipLaunchKernelGGL(k_wcc_compress, dim3(vgrid), dim3(kWccBlock), 0, s, parent.p, n);
-            }
-            GX_TRY(check_launch("k_wcc_compress"));
-        }
+        GX_TRY(afforest_sample(g, parent.p, vgrid, s));
         {
             KTimer kt(ctx, "wcc_hook", s);
             hipLaunchKernelGGL(k_wcc_link_edges,

@@ -411,3 +411,24 @@ def test_cdlp_layouts(ctx, monkeypatch, relabel, stage, streams):
               _G(_tier_graph(True), True)):
         for iters in (1, 3, 10):
             np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=iters), O.cdlp(g.csr, g.directed, iters))
+
+
+@pytest.mark.parametrize("env", [{"GX_WCC_HOOK0": "0", "GX_WCC_MINHOOK": "0"}, {"GX_WCC_MINHOOK": "0"},
+                                 {"GX_WCC_MINHOOK": "3"}, {}])
+def test_wcc_sampling_modes(ctx, monkeypatch, env):
+    """Afforest's sampling rounds with CAS links only, with the plain-store first round, and
+    with min-hook passes before the second round's links: the same canonical labels, on
+    undirected and directed graphs, sparse ones with many components and shuffled rows."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for g in (_rmat(14, 16, 4), _rmat(14, 2, 31), _rmat(13, 1, 32, undirected=False), _rmat(12, 8, 3, undirected=False)):
+        np.testing.assert_array_equal(gpu_run(ctx, g, "WCC"), O.wcc(g.csr))
+    g = _rmat(13, 4, 9)
+    shuffled = _shuffle_rows(g.csr, seed=3)
+    np.testing.assert_array_equal(gpu_run(ctx, _G(shuffled, False), "WCC"), O.wcc(shuffled))
+    n = 20000
+    perm = np.random.default_rng(5).permutation(n)
+    keep = np.arange(n - 1) % 97 != 0
+    csr = csr_from_edges(n, perm[1:][keep], perm[:-1][keep], None, symmetric=True)
+    np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "WCC"), O.wcc(csr))
