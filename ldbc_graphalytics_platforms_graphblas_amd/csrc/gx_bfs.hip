@@ -12,6 +12,7 @@
 // Direction switching follows Beamer's heuristic (alpha = 14, beta = 24).  Levels are
 // unique, so the result is bit-exact whatever the traversal order.
 #include <cstdlib>
+#include <memory>
 
 #include "gx_device.h"
 
@@ -48,7 +49,7 @@ __device__ __forceinline__ uint32_t chunks_of(int64_t deg) {
 }
 
 // top-down: one wave per work item (<= kChunk edges of one frontier vertex)
-__global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown(const int64_t *__restrict__ rp,
+__device__ __forceinline__ void bfs_topdown(const int64_t *__restrict__ rp,
                                                            const int32_t *__restrict__ ci,
                                                            const uint64_t *__restrict__ qin,
                                                            uint32_t qsize, int32_t *level,
@@ -87,12 +88,20 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown(const int64_t *__rest
     if (lane == 0 && edges) atomicAdd(next_edges, edges);
 }
 
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown(const int64_t *__restrict__ rp,
+                                                           const int32_t *__restrict__ ci,
+                                                           const uint64_t *__restrict__ qin, uint32_t qsize,
+                                                           int32_t *level, int32_t depth, uint64_t *qout,
+                                                           uint32_t *qcount, unsigned long long *next_edges) {
+    bfs_topdown(rp, ci, qin, qsize, level, depth, qout, qcount, next_edges);
+}
+
 // bottom-up: one thread per vertex; in-edges in (rpi, cii)
 // Frontier bitmap for bottom-up steps: bit u set iff level[u] == depth.  One 64-bit word per
 // wave (ballot over 64 consecutive vertices); n/8 bytes, so it stays resident in every XCD's
 // L2 while the bottom-up probes hit it at random (the int32 level array does not).
-__global__ __launch_bounds__(kBfsBlock) void k_bfs_bitmap(const int32_t *__restrict__ level, int64_t n,
-                                                          int32_t depth, uint64_t *fb) {
+__device__ __forceinline__ void bfs_bitmap(const int32_t *__restrict__ level, int64_t n, int32_t depth,
+                                           uint64_t *fb) {
     const int64_t stride = (int64_t)gridDim.x * kBfsBlock;
     const int64_t nround = (n + stride - 1) / stride;
     for (int64_t r = 0; r < nround; r++) {
@@ -100,6 +109,11 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bitmap(const int32_t *__restr
         const uint64_t m = __ballot(v < n && level[v] == depth);
         if ((threadIdx.x & (kWave - 1)) == 0 && v < n) fb[v >> 6] = m;
     }
+}
+
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_bitmap(const int32_t *__restrict__ level, int64_t n,
+                                                          int32_t depth, uint64_t *fb) {
+    bfs_bitmap(level, n, depth, fb);
 }
 
 __device__ __forceinline__ uint32_t in_frontier(const uint64_t *__restrict__ fb, int32_t u) {
@@ -111,7 +125,7 @@ __device__ __forceinline__ uint32_t in_frontier(const uint64_t *__restrict__ fb,
 // is left in `level` (no queue: a queue append per wave is one same-address atomic per wave,
 // ~11 ns each serialised, which dominated); found vertices and their out-edges are summed
 // per workgroup and leave as one atomic each.
-__global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__restrict__ rpi,
+__device__ __forceinline__ void bfs_bottomup(const int64_t *__restrict__ rpi,
                                                             const int32_t *__restrict__ cii,
                                                             const int64_t *__restrict__ rpo,
                                                             const uint64_t *__restrict__ fb, int64_t n,
@@ -158,13 +172,21 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__res
     }
 }
 
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__restrict__ rpi,
+                                                            const int32_t *__restrict__ cii,
+                                                            const int64_t *__restrict__ rpo,
+                                                            const uint64_t *__restrict__ fb, int64_t n,
+                                                            int32_t *level, int32_t depth,
+                                                            unsigned long long *counters) {
+    bfs_bottomup(rpi, cii, rpo, fb, n, level, depth, counters);
+}
+
 // Top-down queue of the vertices at `depth` (after bottom-up steps), built per tile of
 // kQTile consecutive vertices: count the tile's items, one atomicAdd for its base, write.
 constexpr int64_t kQTile = 4096;
 
-__global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue(const int64_t *__restrict__ rp,
-                                                               const int32_t *__restrict__ level, int64_t n,
-                                                               int32_t depth, uint64_t *queue, uint32_t *qcount) {
+__device__ __forceinline__ void bfs_level_queue(const int64_t *__restrict__ rp, const int32_t *__restrict__ level,
+                                                int64_t n, int32_t depth, uint64_t *queue, uint32_t *qcount) {
     __shared__ uint32_t wsum[kBfsBlock / kWave];
     __shared__ uint32_t tile_base;
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -206,6 +228,113 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue(const int64_t *__
             __syncthreads();
         }
     }
+}
+
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue(const int64_t *__restrict__ rp,
+                                                               const int32_t *__restrict__ level, int64_t n,
+                                                               int32_t depth, uint64_t *queue, uint32_t *qcount) {
+    bfs_level_queue(rp, level, n, depth, queue, qcount);
+}
+
+// ---- device-driven levels ----------------------------------------------------------------
+// The host-driven loop read the frontier counts back after every level to choose the
+// direction: ~30-50 us of idle device per level (SYN-g500-22: ~7 levels, 0.48 ms per BFS of
+// which ~0.25 ms kernels).  Here a one-thread plan kernel consumes the last level's counts,
+// applies Beamer's rule and selects the level's kernels; the others exit at once.  The host
+// queues levels in batches and reads the done flag one batch late.
+struct BfsState {
+    int32_t depth;
+    int32_t mode;          // 0 done / idle, 1 top-down, 2 bottom-up
+    int32_t done;
+    int32_t started;
+    int32_t qi;            // top-down input queue q[qi], its count qcnt[qi]
+    int32_t have_queue;    // the frontier is in q[qi] (else only in `level`)
+    int32_t need_queue;    // this top-down level first rebuilds q[qi] from `level`
+    int32_t bottom_up;
+    int32_t has_in;
+    int32_t pad;
+    unsigned long long mf, mu, fsize, n;
+    uint32_t qcnt[2];
+    unsigned long long nedges;
+    unsigned long long bucnt[2];   // bottom-up: found, their out-edges
+};
+
+__global__ void k_bfs_plan(BfsState *st) {
+    if (st->done) {
+        st->mode = 0;
+        return;
+    }
+    if (st->started) {   // the last level's results
+        unsigned long long next_edges, next_size;
+        if (st->mode == 2) {
+            next_size = st->bucnt[0];
+            next_edges = st->bucnt[1];
+            st->have_queue = 0;
+        } else {
+            st->qi ^= 1;
+            next_size = st->qcnt[st->qi];
+            next_edges = st->nedges;
+            st->have_queue = 1;
+        }
+        st->mu = st->mu > st->mf ? st->mu - st->mf : 0ull;
+        st->mf = next_edges;
+        st->fsize = next_size;
+        st->depth++;
+    }
+    st->started = 1;
+    if (st->fsize == 0) {
+        st->done = 1;
+        st->mode = 0;
+        return;
+    }
+    // Beamer: TD -> BU when the frontier's edges exceed the unexplored ones / 14; BU -> TD when
+    // the frontier shrinks below n / 24
+    if (st->has_in) {
+        if (!st->bottom_up && st->mf > st->mu / 14) st->bottom_up = 1;
+        else if (st->bottom_up && (long long)st->fsize < (long long)(st->n / 24)) st->bottom_up = 0;
+    }
+    if (st->bottom_up) {
+        st->mode = 2;
+        st->bucnt[0] = st->bucnt[1] = 0;
+    } else {
+        st->mode = 1;
+        st->need_queue = !st->have_queue;
+        if (st->need_queue) st->qcnt[st->qi] = 0;
+        st->qcnt[st->qi ^ 1] = 0;
+        st->nedges = 0;
+    }
+}
+
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_bitmap_dev(const int32_t *__restrict__ level, int64_t n,
+                                                              const BfsState *st, uint64_t *fb) {
+    if (st->mode != 2) return;
+    bfs_bitmap(level, n, st->depth, fb);
+}
+
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup_dev(const int64_t *__restrict__ rpi,
+                                                                const int32_t *__restrict__ cii,
+                                                                const int64_t *__restrict__ rpo,
+                                                                const uint64_t *__restrict__ fb, int64_t n,
+                                                                int32_t *level, BfsState *st) {
+    if (st->mode != 2) return;
+    bfs_bottomup(rpi, cii, rpo, fb, n, level, st->depth, st->bucnt);
+}
+
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue_dev(const int64_t *__restrict__ rp,
+                                                                   const int32_t *__restrict__ level, int64_t n,
+                                                                   BfsState *st, uint64_t *q0, uint64_t *q1) {
+    if (st->mode != 1 || !st->need_queue) return;
+    const int qi = st->qi;
+    bfs_level_queue(rp, level, n, st->depth, qi ? q1 : q0, &st->qcnt[qi]);
+}
+
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown_dev(const int64_t *__restrict__ rp,
+                                                               const int32_t *__restrict__ ci, int32_t *level,
+                                                               BfsState *st, uint64_t *q0, uint64_t *q1) {
+    if (st->mode != 1) return;
+    const int qi = st->qi;
+    bfs_topdown(rp, ci, qi ? q1 : q0, st->qcnt[qi], level, st->depth, qi ? q0 : q1, &st->qcnt[qi ^ 1],
+                &st->nedges);
 }
 
 __global__ void k_bfs_seed(const int64_t *__restrict__ rp, int32_t *level, uint64_t *queue, uint32_t *qcount,
@@ -255,6 +384,68 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     }
     const DevCSR *in = g->directed ? (g->AT.built ? &g->AT : nullptr) : &g->A;
     GX_HIP_TRY(hipMemsetAsync(level.p, 0xff, n * 4, s));
+    const unsigned bu_grid = (unsigned)std::min<int64_t>(grid_for(n, kBfsBlock, 8192), 1024);
+    const char *de = std::getenv("GX_BFS_DEVICE");
+    if (!de || std::atoi(de) != 0) {
+        // device-driven levels (k_bfs_plan), queued in batches; the done flag is read one
+        // batch late
+        DBuf<BfsState> st;
+        GX_TRY(st.alloc(1));
+        BfsState h{};
+        const int64_t dsrc = g->A.h_rp[src + 1] - g->A.h_rp[src];
+        h.have_queue = 1;
+        h.has_in = in != nullptr;
+        h.n = (unsigned long long)n;
+        h.mf = (unsigned long long)dsrc;
+        h.mu = g->nnz;
+        h.fsize = (unsigned long long)((dsrc + kChunk - 1) / kChunk);
+        GX_HIP_TRY(hipMemcpyAsync(st.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, &st.p->qcnt[0],
+                           (int32_t)src);
+        GX_TRY(check_launch("k_bfs_seed"));
+        int32_t *h_done = nullptr;
+        hipEvent_t ev = nullptr;
+        GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_done), sizeof(int32_t), hipHostMallocDefault));
+        std::unique_ptr<int32_t, void (*)(int32_t *)> done_guard(h_done, [](int32_t *p) { (void)hipHostFree(p); });
+        GX_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        std::unique_ptr<ihipEvent_t, void (*)(hipEvent_t)> ev_guard(ev, [](hipEvent_t e) { (void)hipEventDestroy(e); });
+        const unsigned vgrid = grid_for(n, kBfsBlock, 8192);
+        const unsigned qgrid = (unsigned)std::min<int64_t>((n + kQTile - 1) / kQTile, 2048);
+        auto enqueue = [&](int k) -> int {
+            for (int i = 0; i < k; i++) {
+                hipLaunchKernelGGL(k_bfs_plan, dim3(1), dim3(1), 0, s, st.p);
+                if (in) {
+                    KTimer kt(ctx, "bfs_bottomup", s);
+                    hipLaunchKernelGGL(k_bfs_bitmap_dev, dim3(vgrid), dim3(kBfsBlock), 0, s, level.p, n, st.p,
+                                       fbits.p);
+                    hipLaunchKernelGGL(k_bfs_bottomup_dev, dim3(bu_grid), dim3(kBfsBlock), 0, s, in->rp.p, in->ci.p,
+                                       g->A.rp.p, fbits.p, n, level.p, st.p);
+                }
+                KTimer kt(ctx, "bfs_topdown", s);
+                if (in)
+                    hipLaunchKernelGGL(k_bfs_level_queue_dev, dim3(qgrid), dim3(kBfsBlock), 0, s, g->A.rp.p, level.p,
+                                       n, st.p, q0.p, q1.p);
+                hipLaunchKernelGGL(k_bfs_topdown_dev, dim3(8192), dim3(kBfsBlock), 0, s, g->A.rp.p, g->A.ci.p,
+                                   level.p, st.p, q0.p, q1.p);
+            }
+            return check_launch("k_bfs_topdown_dev");
+        };
+        // a first batch of kFirst levels covers a power-law graph's whole traversal (SYN-g500-22:
+        // 6 levels), then batches of kBatch; levels queued past the end cost ~20 us each
+        constexpr int kFirst = 6, kBatch = 2;
+        GX_TRY(enqueue(kFirst));
+        for (int64_t levels = kFirst;; levels += kBatch) {
+            GX_HIP_TRY(hipMemcpyAsync(h_done, &st.p->done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipEventRecord(ev, s));
+            GX_TRY(enqueue(kBatch));
+            GX_HIP_TRY(hipEventSynchronize(ev));
+            if (*h_done) break;
+            if (levels > n + 2 * kFirst) return fail(GX_PANIC, "gx_bfs: level loop did not end");
+        }
+        GX_TRY(device_end(ctx));
+        GX_TRY(download(ctx, level_out, level.p, (uint64_t)n, Xfer::Levels));
+        return GX_SUCCESS;
+    }
     hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, qcount.p, (int32_t)src);
     GX_TRY(check_launch("k_bfs_seed"));
     uint32_t qsize = 0;
@@ -273,7 +464,6 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     // bottom-up step they are only in `level` until a top-down step needs the queue)
     bool have_queue = true;
     uint64_t fsize = qsize;
-    const unsigned bu_grid = (unsigned)std::min<int64_t>(grid_for(n, kBfsBlock, 8192), 1024);
     while (fsize > 0) {
         // Beamer switch: TD -> BU when the frontier's edges exceed the unexplored ones / 14;
         // BU -> TD when the frontier shrinks below n / 24.
