@@ -432,3 +432,20 @@ def test_wcc_sampling_modes(ctx, monkeypatch, env):
     keep = np.arange(n - 1) % 97 != 0
     csr = csr_from_edges(n, perm[1:][keep], perm[:-1][keep], None, symmetric=True)
     np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "WCC"), O.wcc(csr))
+
+
+@pytest.mark.parametrize("device", ["1", "0"])
+def test_bfs_level_driver(ctx, monkeypatch, device):
+    """BFS levels planned on the device (GX_BFS_DEVICE=1, batches of levels, done flag read a
+    batch late) or by the host: the oracle's levels on power-law graphs (top-down and
+    bottom-up levels), a 3 000-level chain (many batches) and an isolated source."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    monkeypatch.setenv("GX_BFS_DEVICE", device)
+    for g in (_rmat(14, 16, 4), _rmat(12, 8, 3, undirected=False)):
+        s = _src(g)
+        np.testing.assert_array_equal(gpu_run(ctx, g, "BFS", source=s), O.bfs(g.csr, s))
+    n = 3000
+    perm = np.random.default_rng(2).permutation(n)
+    csr = csr_from_edges(n + 1, perm[:-1], perm[1:], None, symmetric=True)   # vertex n isolated
+    for s in (int(perm[0]), int(perm[n // 2]), n):
+        np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "BFS", source=s), O.bfs(csr, s))
