@@ -1700,9 +1700,14 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     if (n == 0) return GX_SUCCESS;
     GX_TRY(device_begin(ctx));
     if (g->directed) GX_TRY(ensure_transpose(g));
-    // GX_CDLP_RELABEL=0: iterate on the caller's vertex order; GX_CDLP_STAGE=1: dense
-    // iterations read staged labels (k_cdlp_stage; measured slower)
-    const bool relabel = env_on("GX_CDLP_RELABEL");
+    // The relabelled copy costs ~90 ms to build on SYN-cit (4.2 M vertices) and saves ~1.3 ms
+    // per call, so, like BFS's transpose, it is built once the graph serves a second CDLP run:
+    // a one-off run (the Graphalytics executable's) stays in the caller's order.
+    // GX_CDLP_RELABEL=0 never, 1 from the first run.  GX_CDLP_STAGE=1: dense iterations read
+    // staged labels (k_cdlp_stage; measured slower)
+    g->cdlp_calls++;
+    const char *re = std::getenv("GX_CDLP_RELABEL");
+    const bool relabel = re ? std::atoi(re) != 0 : g->cdlp_calls >= 2;
     const bool stage = env_on("GX_CDLP_STAGE", false);
     CdlpCache *C = nullptr;
     GX_TRY(cdlp_cache(g, std::max(iters, 1), relabel, stage, &C, s));
