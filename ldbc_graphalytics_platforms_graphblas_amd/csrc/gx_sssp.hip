@@ -1068,8 +1068,7 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         g->mean_w = mean;
     }
     // measured on the SYN stand-ins with bucket fusion: 4 for undirected graphs,
-    // whose big early buckets are pulled (below ~2.5 the first bucket no longer reaches the
-    // pull threshold on SYN-8_5: 14.8 ms), 0.5 for directed ones
+    // whose big early buckets are pulled, 0.5 for directed ones
     double delta = 0.0, scale = g->directed ? 0.5 : 4.0;
     if (const char *e = std::getenv("GX_SSSP_DELTA")) delta = std::atof(e);
     if (const char *e = std::getenv("GX_SSSP_DSCALE")) scale = std::atof(e);
@@ -1107,14 +1106,16 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nstamp.p,
                        bstamp.p, ostamp.p, sstamp.p, n);
     GX_TRY(check_launch("k_sssp_init"));
-    // heavy phases whose settled list holds at least 1/GX_SSSP_PULL_FRAC (default 4) of the
-    // non-isolated vertices are pulled (undirected graphs; GX_SSSP_PULL=0 never, 2 always)
+    // heavy phases whose settled list holds at least 1/GX_SSSP_PULL_FRAC (default 8) of the
+    // non-isolated vertices are pulled (undirected graphs; GX_SSSP_PULL=0 never, 2 always).
+    // 8 rather than 4: the same times at the default bucket width, and no cliff below it (a
+    // scale of 2-2.5 left SYN-8_5's first bucket short of 1/4 and pushed it: 14.8 ms; 8.2 at 1/8)
     uint32_t pull_min = 0xFFFFFFFFu;
     {
         const char *e = std::getenv("GX_SSSP_PULL");
         const int mode = e ? std::atoi(e) : 1;
         const char *f = std::getenv("GX_SSSP_PULL_FRAC");
-        const double frac = f ? std::atof(f) : 4.0;
+        const double frac = f ? std::atof(f) : 8.0;
         if (!g->directed && mode == 2) pull_min = 1;
         else if (!g->directed && mode == 1 && frac > 0.0)
             pull_min = (uint32_t)std::max<double>(1.0, std::ceil((double)lay.n_active / frac));
