@@ -239,10 +239,13 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
 #pragma unroll
             for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
             if (PIPE) load_round(k0 + step);
+            // entries outside [lo, hi) add 0.0 instead of branching round the add: behind a
+            // branch the compiler sank the first gather below the next round's entry loads and
+            // waited for all of them (vmcnt(0)) before the first add
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const int64_t e = k0 + (int64_t)u * BS;
-                if (e >= lo && e < hi) atomicAdd(&acc[r[u]], g[u]);
+                atomicAdd(&acc[r[u]], e >= lo && e < hi ? g[u] : 0.0);
             }
         }
     }
