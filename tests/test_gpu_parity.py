@@ -201,7 +201,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, slices):
                                  {"GX_PR_SORTED_VARIANT": "1"}, {"GX_PR_SORTED_VARIANT": "2"},
                                  {"GX_PR_SLICES": "2"}, {"GX_PR_SLICES": "4"}, {"GX_PR_SLICES": "8"},
                                  {"GX_PR_SLICES": "8", "GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SLICES": "1"},
-                                 {"GX_PR_KERNEL": "adaptive"}, {"GX_PR_NARROW": "0"},
+                                 {"GX_PR_KERNEL": "adaptive"},
                                  {"GX_PR_SORTED_ROWS": "16384", "GX_PR_UNIT_NNZ": "16384"},
                                  {"GX_PR_SORTED_ROWS": "2048", "GX_PR_SLICES": "2"},
                                  {"GX_PR_SORTED_NNZ": "1024"},
@@ -214,7 +214,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, slices):
                                   "GX_PR_UNIT_LAYOUT": "0"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
     """One pass, two passes around a small hub slice, tiny blocks, the other block shapes,
-    narrow (16-bit) groups off and with 12-, 11- and 14-bit rows, split blocks (several workgroups per sorted block, combined through slabs by the last
+    16 Ki- and 2 Ki-row blocks, split blocks (several workgroups per sorted block, combined through slabs by the last
     arriver) and the CSR-Adaptive kernel all give the oracle's scores (directed and
     undirected)."""
     for k, v in env.items():
