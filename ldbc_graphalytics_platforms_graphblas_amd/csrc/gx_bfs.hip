@@ -353,6 +353,11 @@ using namespace gx;
 extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     if (!g || !level_out) return fail(GX_NULL_POINTER, "gx_bfs: null argument");
     if (src >= g->n) return fail(GX_INVALID_INDEX, "gx_bfs: source out of range");
+    {
+        gx_graph *h = nullptr;   // hub-first copy from the second call (gx_runtime.hip hub_for)
+        GX_TRY(hub_for(g, ++g->hub_bfs_calls, &h, &src));
+        if (h) return gx_bfs(h, src, level_out);
+    }
     gx_ctx *ctx = g->ctx;
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -442,8 +447,10 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
             if (*h_done) break;
             if (levels > n + 2 * kFirst) return fail(GX_PANIC, "gx_bfs: level loop did not end");
         }
+        const void *res = nullptr;
+        GX_TRY(remap_out(g, level.p, 4, s, &res));
         GX_TRY(device_end(ctx));
-        GX_TRY(download(ctx, level_out, level.p, (uint64_t)n, Xfer::Levels));
+        GX_TRY(download(ctx, level_out, res, (uint64_t)n, Xfer::Levels));
         return GX_SUCCESS;
     }
     hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, qcount.p, (int32_t)src);
@@ -518,8 +525,10 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         fsize = next_size;
         depth++;
     }
+    const void *res = nullptr;
+    GX_TRY(remap_out(g, level.p, 4, s, &res));
     GX_TRY(device_end(ctx));
-    GX_TRY(download(ctx, level_out, level.p, (uint64_t)n, Xfer::Levels));
+    GX_TRY(download(ctx, level_out, res, (uint64_t)n, Xfer::Levels));
     return GX_SUCCESS;
 }
 

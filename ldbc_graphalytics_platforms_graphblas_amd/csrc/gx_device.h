@@ -143,6 +143,17 @@ struct gx_graph {
     gx::SsspLayout *sssp = nullptr;   // cached light/heavy edge layout
     std::shared_ptr<void> cdlp;       // gx_cdlp's tier lists and buffers (gx_cdlp.hip CdlpCache)
     std::shared_ptr<void> lcc;        // gx_lcc's orientation and work items (gx_lcc.hip LccCache)
+    // Hub-first relabelled copy of an undirected graph (gx_runtime.hip hub_for): BFS, WCC and
+    // SSSP run on it from their second call on the graph.  perm[v] = v's id in the copy, order
+    // its inverse; on the copy, out_perm / out_order point at the parent's perm / order.
+    std::shared_ptr<gx_graph> hub;
+    gx::DBuf<int32_t> hub_perm, hub_order;
+    std::vector<int32_t> h_hub_perm;
+    const int32_t *out_perm = nullptr;
+    const int32_t *out_order = nullptr;
+    gx::DBuf<uint64_t> remap_tmp;         // on a copy: n words of scratch for the remap
+    int64_t live = 0;                     // on a copy: vertices of degree > 0 (a prefix of its ids)
+    int sssp_calls = 0, wcc_calls = 0, hub_bfs_calls = 0;
 };
 
 namespace gx {
@@ -177,6 +188,14 @@ struct KTimer {
         }
     }
 };
+
+// The graph a call runs on: g itself, or its hub-first copy (built on demand and cached) when
+// g is undirected and this is the algorithm's `calls`-th call with calls >= 2 (GX_HUB = 0 never,
+// 1 from the second call (default), 2 from the first).  *src is renamed into the copy's ids.
+int hub_for(gx_graph *g, int calls, gx_graph **out, uint64_t *src);
+// The results to download: on a copy (g->out_perm set) buf scattered through out_order into
+// the parent's vertex order (g->remap_tmp; elem = 4 or 8 bytes, n entries), else buf itself.
+int remap_out(gx_graph *g, const void *buf, int elem, hipStream_t s, const void **res);
 
 // Collect elapsed times of finished timed launches into ctx->stats.
 int collect_timings(gx_ctx *ctx);

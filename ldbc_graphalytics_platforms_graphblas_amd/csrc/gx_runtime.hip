@@ -6,6 +6,7 @@
 // (row << 32 | col) keys, so their rows come out sorted by column.
 #include <cstring>
 #include <memory>
+#include <cstdlib>
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
@@ -333,6 +334,122 @@ extern "C" int gx_graph_free(gx_graph *g) {
     delete g;
     return GX_SUCCESS;
 }
+
+namespace gx {
+namespace {
+
+// Row i of the copy = row order[i] of the parent, columns renamed through perm (one wave per
+// row; row contents keep the parent's order).
+__global__ __launch_bounds__(256) void k_hub_copy(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                  const double *__restrict__ w, const int32_t *__restrict__ order,
+                                                  const int32_t *__restrict__ perm, const int64_t *__restrict__ nrp,
+                                                  int64_t n, int32_t *__restrict__ nci, double *__restrict__ nw) {
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; i < n; i += (int64_t)gridDim.x * 256 / kWave) {
+        const int64_t src = rp[order[i]], len = nrp[i + 1] - nrp[i], dst = nrp[i];
+        for (int64_t k = lane; k < len; k += kWave) {
+            nci[dst + k] = perm[ci[src + k]];
+            if (w) nw[dst + k] = w[src + k];
+        }
+    }
+}
+
+// out[order[x]] = in[x]: the copy's results in the caller's order.  A scatter, not a gather
+// through perm: the reads stream and the random accesses are stores, which nothing waits for.
+template <typename T>
+__global__ void k_scatter_by(const T *__restrict__ in, const int32_t *__restrict__ order, int64_t n, T *__restrict__ out) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x)
+        out[order[x]] = in[x];
+}
+
+void free_copy(gx_graph *h) { (void)gx_graph_free(h); }
+
+// Hub-first order by degree (descending, ties by id; a counting sort on the host row
+// pointers), the copy's row pointers, then the rows renamed on the device.
+int build_hub(gx_graph *g) {
+    const int64_t n = (int64_t)g->n;
+    hipStream_t s = g->ctx->stream;
+    const std::vector<int64_t> &h = g->A.h_rp;
+    int64_t maxd = 0;
+    for (int64_t v = 0; v < n; v++) maxd = std::max(maxd, h[v + 1] - h[v]);
+    std::vector<int64_t> start((size_t)maxd + 2, 0);
+    for (int64_t v = 0; v < n; v++) start[(size_t)(maxd - (h[v + 1] - h[v])) + 1]++;
+    for (size_t k = 1; k < start.size(); k++) start[k] += start[k - 1];
+    std::vector<int32_t> order(n);
+    g->h_hub_perm.assign(n, 0);
+    for (int64_t v = 0; v < n; v++) {
+        const int64_t pos = start[(size_t)(maxd - (h[v + 1] - h[v]))]++;
+        order[pos] = (int32_t)v;
+        g->h_hub_perm[v] = (int32_t)pos;
+    }
+    std::shared_ptr<gx_graph> c(new gx_graph(), free_copy);
+    c->ctx = g->ctx;
+    c->n = g->n;
+    c->nnz = g->nnz;
+    c->directed = false;
+    c->weighted = g->weighted;
+    c->mean_w = g->mean_w;
+    c->A.n = g->n;
+    c->A.nnz = g->nnz;
+    c->A.h_rp.assign(n + 1, 0);
+    for (int64_t i = 0; i < n; i++) c->A.h_rp[i + 1] = c->A.h_rp[i] + (h[order[i] + 1] - h[order[i]]);
+    GX_TRY(g->hub_perm.alloc(std::max<int64_t>(n, 1)));
+    GX_TRY(g->hub_order.alloc(std::max<int64_t>(n, 1)));
+    GX_TRY(c->A.rp.alloc(n + 1));
+    GX_TRY(c->A.ci.alloc(g->nnz, 16));
+    if (g->weighted) GX_TRY(c->A.w.alloc(g->nnz));
+    GX_HIP_TRY(hipMemcpyAsync(g->hub_perm.p, g->h_hub_perm.data(), n * 4, hipMemcpyHostToDevice, s));
+    GX_HIP_TRY(hipMemcpyAsync(g->hub_order.p, order.data(), n * 4, hipMemcpyHostToDevice, s));
+    GX_HIP_TRY(hipMemcpyAsync(c->A.rp.p, c->A.h_rp.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (n) {
+        hipLaunchKernelGGL(k_hub_copy, dim3(grid_for((uint64_t)n * kWave, 256, 1u << 20)), dim3(256), 0, s, g->A.rp.p,
+                           g->A.ci.p, g->weighted ? g->A.w.p : nullptr, g->hub_order.p, g->hub_perm.p, c->A.rp.p, n,
+                           c->A.ci.p, g->weighted ? c->A.w.p : nullptr);
+        GX_TRY(check_launch("k_hub_copy"));
+    }
+    GX_HIP_TRY(hipStreamSynchronize(s));   // the host vectors die at return
+    GX_TRY(c->remap_tmp.alloc(std::max<int64_t>(n, 1)));
+    c->live = 0;
+    while (c->live < n && c->A.h_rp[c->live + 1] > c->A.h_rp[c->live]) c->live++;
+    c->A.built = true;
+    c->out_perm = g->hub_perm.p;
+    c->out_order = g->hub_order.p;
+    g->hub = c;
+    return GX_SUCCESS;
+}
+
+}  // namespace
+
+int hub_for(gx_graph *g, int calls, gx_graph **out, uint64_t *src) {
+    *out = nullptr;
+    if (g->directed || g->out_perm || g->n < 2) return GX_SUCCESS;
+    const char *e = std::getenv("GX_HUB");
+    const int mode = e ? std::atoi(e) : 1;
+    if (!(mode == 2 || (mode == 1 && calls >= 2))) return GX_SUCCESS;
+    if (!g->hub) GX_TRY(build_hub(g));
+    if (src) *src = (uint64_t)g->h_hub_perm[*src];
+    *out = g->hub.get();
+    return GX_SUCCESS;
+}
+
+int remap_out(gx_graph *g, const void *buf, int elem, hipStream_t s, const void **res) {
+    *res = buf;
+    if (!g->out_perm || !g->n) return GX_SUCCESS;
+    const int64_t n = (int64_t)g->n;
+    void *tmp = g->remap_tmp.p;   // n words, allocated with the copy
+    const unsigned grid = grid_for((uint64_t)n, 256, 8192);
+    if (elem == 8)
+        hipLaunchKernelGGL(k_scatter_by<uint64_t>, dim3(grid), dim3(256), 0, s, static_cast<const uint64_t *>(buf),
+                           g->out_order, n, static_cast<uint64_t *>(tmp));
+    else
+        hipLaunchKernelGGL(k_scatter_by<uint32_t>, dim3(grid), dim3(256), 0, s, static_cast<const uint32_t *>(buf),
+                           g->out_order, n, static_cast<uint32_t *>(tmp));
+    GX_TRY(check_launch("k_scatter_by"));
+    *res = tmp;
+    return GX_SUCCESS;
+}
+
+}  // namespace gx
 
 extern "C" int gx_graph_info(gx_graph *g, uint64_t *n, uint64_t *nnz, int *directed, int *weighted) {
     if (!g) return fail(GX_NULL_POINTER, "gx_graph_info: null graph");

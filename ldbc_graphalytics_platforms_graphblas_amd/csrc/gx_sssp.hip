@@ -1044,6 +1044,11 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     if (src >= g->n) return fail(GX_INVALID_INDEX, "gx_sssp: source out of range");
     if ((int64_t)g->n >= kMaxBufVertices)
         return fail(GX_NOT_IMPLEMENTED, "gx_sssp: more than 2^28 vertices (buffer-load offsets are 31-bit)");
+    {
+        gx_graph *h = nullptr;   // hub-first copy from the second call (gx_runtime.hip hub_for)
+        GX_TRY(hub_for(g, ++g->sssp_calls, &h, &src));
+        if (h) return gx_sssp(h, src, dist_out);
+    }
     gx_ctx *ctx = g->ctx;
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -1205,6 +1210,8 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     }
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    const void *res = nullptr;
+    GX_TRY(remap_out(g, dist.p, 8, s, &res));
     GX_TRY(device_end(ctx));
     if (verbose) {
         SsspState h;
@@ -1219,7 +1226,7 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
                      delta, h.round, (long long)h.cur, h.epoch, (unsigned long long)steps, c[0], c[1], c[2], c[3],
                      c[4], c[5], c[6], c[7]);
     }
-    GX_TRY(download(ctx, dist_out, dist.p, (uint64_t)n, Xfer::Raw64));
+    GX_TRY(download(ctx, dist_out, res, (uint64_t)n, Xfer::Raw64));
     return GX_SUCCESS;
 }
 

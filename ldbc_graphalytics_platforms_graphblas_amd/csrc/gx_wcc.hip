@@ -247,6 +247,40 @@ int afforest_sample(gx_graph *g, int32_t *parent, unsigned vgrid, hipStream_t s)
     return GX_SUCCESS;
 }
 
+// Labels of a run on the hub-first copy (gx_graph::out_perm): a component's label is its
+// smallest vertex id in the caller's numbering, the min of order[] over its members.  The
+// giant component's members (root `giant`) meet in a workgroup min first, since one word
+// taking an atomic per member would serialise millions of them; the rest take one each.
+__global__ __launch_bounds__(kWccBlock) void k_wcc_min_orig(const int32_t *__restrict__ parent,
+                                                            const int32_t *__restrict__ order, int64_t n,
+                                                            int32_t giant, int32_t *__restrict__ minorig) {
+    __shared__ int32_t wmin[kWccBlock / kWave];
+    int32_t lm = 0x7fffffff;
+    for (int64_t x = (int64_t)blockIdx.x * kWccBlock + threadIdx.x; x < n; x += (int64_t)gridDim.x * kWccBlock) {
+        const int32_t r = parent[x], o = order[x];
+        if (r == giant) lm = min(lm, o);
+        else atomicMin(&minorig[r], o);
+    }
+    for (int off = kWave / 2; off > 0; off >>= 1) lm = min(lm, __shfl_xor(lm, off, kWave));
+    if ((threadIdx.x & (kWave - 1)) == 0) wmin[threadIdx.x / kWave] = lm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kWccBlock / kWave; w++) lm = min(lm, wmin[w]);
+        if (giant >= 0 && lm != 0x7fffffff) atomicMin(&minorig[giant], lm);
+    }
+}
+
+// out[order[x]] = the label of x's component; vertices past `live` have no edges and are
+// their own component.  Scattered through order (streaming reads, random stores).
+__global__ void k_wcc_label_orig(const int32_t *__restrict__ parent, const int32_t *__restrict__ order,
+                                 const int32_t *__restrict__ minorig, int64_t n, int64_t live,
+                                 int32_t *__restrict__ out) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t o = order[x];
+        out[o] = x < live ? minorig[parent[x]] : o;
+    }
+}
+
 }  // namespace
 }  // namespace gx
 
@@ -259,6 +293,12 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
     hipStream_t s = ctx->stream;
     const int64_t n = (int64_t)g->n, nnz = (int64_t)g->nnz;
     if (n == 0) return GX_SUCCESS;
+    {
+        gx_graph *h = nullptr;   // hub-first copy from the second call (gx_runtime.hip hub_for)
+        GX_TRY(hub_for(g, ++g->wcc_calls, &h, nullptr));
+        if (h) return gx_wcc(h, comp);
+    }
+    int32_t giant = -1;
     DBuf<int32_t> parent;
     GX_TRY(parent.alloc(n));
     GX_TRY(device_begin(ctx));
@@ -287,7 +327,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         GX_HIP_TRY(hipMemcpyAsync(roots.data(), d_roots.p, kSamples * 4, hipMemcpyDeviceToHost, s));
         GX_HIP_TRY(hipStreamSynchronize(s));
         std::sort(roots.begin(), roots.end());
-        int32_t giant = roots[0];
+        giant = roots[0];
         int best = 0;
         for (int i = 0, j; i < kSamples; i = j) {
             for (j = i; j < kSamples && roots[j] == roots[i]; j++) {
@@ -325,8 +365,22 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         }
         GX_TRY(check_launch("k_wcc_compress"));
     }
+    const int32_t *res = parent.p;
+    if (g->out_perm) {
+        int32_t *minorig = reinterpret_cast<int32_t *>(g->remap_tmp.p), *lab = minorig + n;   // 2n int32
+        const int64_t live = g->live;   // roots of components with edges are below it
+        if (live) {
+            GX_HIP_TRY(hipMemsetAsync(minorig, 0x7f, (size_t)live * 4, s));
+            hipLaunchKernelGGL(k_wcc_min_orig, dim3(grid_for((uint64_t)live, kWccBlock, 2048)), dim3(kWccBlock), 0,
+                               s, parent.p, g->out_order, live, giant, minorig);
+        }
+        hipLaunchKernelGGL(k_wcc_label_orig, dim3(vgrid), dim3(256), 0, s, parent.p, g->out_order, minorig, n, live,
+                           lab);
+        GX_TRY(check_launch("k_wcc_label_orig"));
+        res = lab;
+    }
     GX_TRY(device_end(ctx));
-    GX_TRY(download(ctx, comp, parent.p, (uint64_t)n, Xfer::Widen32));
+    GX_TRY(download(ctx, comp, res, (uint64_t)n, Xfer::Widen32));
     return GX_SUCCESS;
 }
 

@@ -451,3 +451,39 @@ def test_bfs_level_driver(ctx, monkeypatch, device):
     csr = csr_from_edges(n + 1, perm[:-1], perm[1:], None, symmetric=True)   # vertex n isolated
     for s in (int(perm[0]), int(perm[n // 2]), n):
         np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "BFS", source=s), O.bfs(csr, s))
+
+
+@pytest.mark.parametrize("hub", ["1", "2"])
+def test_hub_first_copy(ctx, monkeypatch, hub):
+    """BFS, WCC and SSSP on the hub-first relabelled copy of an undirected graph (built from
+    the second call on a graph, GX_HUB=1, or from the first, GX_HUB=2): results come back in
+    the caller's vertex order -- levels and distances gathered through the permutation, WCC
+    labels renamed to each component's smallest caller id -- on graphs with many components,
+    isolated vertices and unreachable ones, over three calls on one graph."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    monkeypatch.setenv("GX_HUB", hub)
+    n = 30000
+    perm = np.random.default_rng(11).permutation(n)
+    keep = np.arange(n - 1) % 53 != 0
+    chains = csr_from_edges(n, perm[1:][keep], perm[:-1][keep], None, symmetric=True)
+    for csr in (_rmat(13, 8, 21).csr, _rmat(12, 2, 22).csr, chains):
+        G = A.Graph(ctx, csr, False)
+        try:
+            src = int(np.argmax(np.diff(csr.rowptr.astype(np.int64))))
+            ref_bfs, ref_wcc = O.bfs(csr, src), O.wcc(csr)
+            for _ in range(3):
+                np.testing.assert_array_equal(A.LA_BFS(G, src), ref_bfs)
+                np.testing.assert_array_equal(A.LA_BFS(G, 1), O.bfs(csr, 1))
+                np.testing.assert_array_equal(A.WeaklyConnectedComponents(G), ref_wcc)
+        finally:
+            G.close()
+    for csr in (_rmat(13, 8, 23, weighted=True).csr, _rmat(12, 2, 24, weighted=True).csr):
+        G = A.Graph(ctx, csr, False)
+        try:
+            src = int(np.argmax(np.diff(csr.rowptr.astype(np.int64))))
+            ref = O.sssp(csr, src)
+            for _ in range(3):
+                np.testing.assert_array_equal(A.LA_SSSP(G, src), ref)
+        finally:
+            G.close()
