@@ -410,7 +410,7 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         GX_TRY(check_launch("k_bfs_seed"));
         int32_t *h_done = nullptr;
         hipEvent_t ev = nullptr;
-        GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_done), sizeof(int32_t), hipHostMallocDefault));
+        GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_done), 4 * sizeof(int32_t), hipHostMallocDefault));
         std::unique_ptr<int32_t, void (*)(int32_t *)> done_guard(h_done, [](int32_t *p) { (void)hipHostFree(p); });
         GX_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         std::unique_ptr<ihipEvent_t, void (*)(hipEvent_t)> ev_guard(ev, [](hipEvent_t e) { (void)hipEventDestroy(e); });
@@ -435,20 +435,44 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
             }
             return check_launch("k_bfs_topdown_dev");
         };
-        // a first batch of kFirst levels covers a power-law graph's whole traversal (SYN-g500-22:
-        // 6 levels), then batches of kBatch; levels queued past the end cost ~20 us each
+        // A first batch of levels, then batches of kBatch with the done flag read one batch
+        // late; a level queued past the end costs ~20 us (five launches that exit at once).
+        // The first batch is the number of steps the last BFS on this graph took (a repeated
+        // or nearby source needs the same: SYN-g500-22 8), else kFirst; when it was enough,
+        // the host waits for it and queues nothing more.
         constexpr int kFirst = 6, kBatch = 2;
-        GX_TRY(enqueue(kFirst));
-        for (int64_t levels = kFirst;; levels += kBatch) {
-            GX_HIP_TRY(hipMemcpyAsync(h_done, &st.p->done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        const int first = g->bfs_steps_hint > 0 ? g->bfs_steps_hint : kFirst;
+        // h_done[0..2] = depth, mode, done of the state (one copy)
+        auto read_state = [&]() -> int {
+            GX_HIP_TRY(hipMemcpyAsync(h_done, &st.p->depth, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
             GX_HIP_TRY(hipEventRecord(ev, s));
-            GX_TRY(enqueue(kBatch));
-            GX_HIP_TRY(hipEventSynchronize(ev));
-            if (*h_done) break;
-            if (levels > n + 2 * kFirst) return fail(GX_PANIC, "gx_bfs: level loop did not end");
-        }
+            return GX_SUCCESS;
+        };
         const void *res = nullptr;
-        GX_TRY(remap_out(g, level.p, 4, s, &res));
+        GX_TRY(enqueue(first));
+        int64_t levels = first;
+        GX_TRY(read_state());
+        if (g->bfs_steps_hint > 0) {
+            // the results' remap is queued behind the levels it expects to be the last, so it
+            // runs while the host reads the flag (queued again below if they were not)
+            GX_TRY(remap_out(g, level.p, 4, s, &res));
+            GX_HIP_TRY(hipEventSynchronize(ev));
+        } else {
+            GX_TRY(enqueue(kBatch));
+            levels += kBatch;
+            GX_HIP_TRY(hipEventSynchronize(ev));
+        }
+        const bool more = !h_done[2];
+        while (!h_done[2]) {
+            GX_TRY(read_state());
+            GX_TRY(enqueue(kBatch));
+            levels += kBatch;
+            GX_HIP_TRY(hipEventSynchronize(ev));
+            if (levels > n + 2 * kFirst + 8) return fail(GX_PANIC, "gx_bfs: level loop did not end");
+        }
+        // steps this BFS needed: its levels plus the plan step that found the frontier empty
+        g->bfs_steps_hint = h_done[0] + 1;
+        if (!res || more) GX_TRY(remap_out(g, level.p, 4, s, &res));
         GX_TRY(device_end(ctx));
         GX_TRY(download(ctx, level_out, res, (uint64_t)n, Xfer::Levels));
         return GX_SUCCESS;
