@@ -140,6 +140,8 @@ struct gx_graph {
     double mean_w = -1.0;       // cached mean edge weight (SSSP bucket width), < 0 = not yet computed
     int bfs_calls = 0;          // BFS runs on this graph (a directed graph builds A^T from the second)
     int bfs_steps_hint = 0;     // device-driven level steps the last BFS took (gx_bfs first batch)
+    gx::DBuf<int32_t> wcc_ids;  // Afforest's sampled vertices (+ one word: the giant root)
+    int64_t wcc_ids_n = 0;
     int cdlp_calls = 0;         // CDLP runs (the relabelled copy is built from the second)
     gx::SsspLayout *sssp = nullptr;   // cached light/heavy edge layout
     std::shared_ptr<void> cdlp;       // gx_cdlp's tier lists and buffers (gx_cdlp.hip CdlpCache)

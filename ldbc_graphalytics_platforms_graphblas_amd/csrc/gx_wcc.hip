@@ -152,8 +152,9 @@ __global__ __launch_bounds__(kWccBlock) void k_afforest_sample(const int64_t *__
 // giant component and another vertex is seen from the other vertex).  One wave per vertex.
 __global__ __launch_bounds__(kWccBlock) void k_afforest_finish(const int64_t *__restrict__ rp,
                                                                const int32_t *__restrict__ ci, int64_t n,
-                                                               int skip, int32_t giant, int32_t *parent) {
+                                                               int skip, const int32_t *giant_p, int32_t *parent) {
     const int lane = threadIdx.x & (kWave - 1);
+    const int32_t giant = *giant_p;
     const int64_t w0 = ((int64_t)blockIdx.x * kWccBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kWccBlock / kWave);
     // the giant-component test for 64 vertices at once (one per lane, coalesced), then the
@@ -196,9 +197,32 @@ __global__ __launch_bounds__(kWccBlock) void k_wcc_link_edges(const int64_t *__r
     }
 }
 
-__global__ void k_sample_roots(const int32_t *parent, const int32_t *__restrict__ ids, int m, int32_t *roots) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x)
-        roots[i] = find_root(parent, ids[i]);
+// Afforest's giant component: the most frequent root among kSamples sampled vertices (ties:
+// the smallest root), chosen by one workgroup (each thread counts its sample's root among
+// all of them in LDS), so the host does not wait for the samples between the passes.
+constexpr int kSamples = 1024;
+
+__global__ __launch_bounds__(kSamples) void k_pick_giant(const int32_t *parent, const int32_t *__restrict__ ids,
+                                                         int32_t *giant) {
+    __shared__ int32_t roots[kSamples];
+    __shared__ unsigned long long best[kSamples / kWave];
+    const int t = threadIdx.x;
+    const int32_t r = find_root(parent, ids[t]);
+    roots[t] = r;
+    __syncthreads();
+    uint32_t c = 0;
+    for (int j = 0; j < kSamples; j++) c += roots[j] == r;
+    unsigned long long key = ((unsigned long long)c << 32) | (uint32_t)(0x7fffffff - r);
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(key, off, kWave);
+        key = o > key ? o : key;
+    }
+    if ((t & (kWave - 1)) == 0) best[t / kWave] = key;
+    __syncthreads();
+    if (t == 0) {
+        for (int w = 1; w < kSamples / kWave; w++) key = best[w] > key ? best[w] : key;
+        *giant = 0x7fffffff - (int32_t)(uint32_t)key;
+    }
 }
 
 __global__ void k_iota(int32_t *a, int64_t n) {
@@ -253,8 +277,9 @@ int afforest_sample(gx_graph *g, int32_t *parent, unsigned vgrid, hipStream_t s)
 // taking an atomic per member would serialise millions of them; the rest take one each.
 __global__ __launch_bounds__(kWccBlock) void k_wcc_min_orig(const int32_t *__restrict__ parent,
                                                             const int32_t *__restrict__ order, int64_t n,
-                                                            int32_t giant, int32_t *__restrict__ minorig) {
+                                                            const int32_t *giant_p, int32_t *__restrict__ minorig) {
     __shared__ int32_t wmin[kWccBlock / kWave];
+    const int32_t giant = giant_p ? *giant_p : -1;
     int32_t lm = 0x7fffffff;
     for (int64_t x = (int64_t)blockIdx.x * kWccBlock + threadIdx.x; x < n; x += (int64_t)gridDim.x * kWccBlock) {
         const int32_t r = parent[x], o = order[x];
@@ -298,7 +323,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         GX_TRY(hub_for(g, ++g->wcc_calls, &h, nullptr));
         if (h) return gx_wcc(h, comp);
     }
-    int32_t giant = -1;
+    int32_t *giant_d = nullptr;   // device word holding the giant component's root
     DBuf<int32_t> parent;
     GX_TRY(parent.alloc(n));
     GX_TRY(device_begin(ctx));
@@ -309,38 +334,27 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         // ---- Afforest: sample two neighbours per vertex, find the giant component from
         // 1024 sampled roots, then link only the remaining edges of the other vertices.
         GX_TRY(afforest_sample(g, parent.p, vgrid, s));
-        constexpr int kSamples = 1024;
-        std::vector<int32_t> ids(kSamples), roots(kSamples);
-        uint64_t h = 0x9E3779B97F4A7C15ull;
-        for (int i = 0; i < kSamples; i++) {
-            h ^= h >> 31;
-            h *= 0xBF58476D1CE4E5B9ull;
-            h ^= h >> 29;
-            ids[i] = (int32_t)(h % (uint64_t)n);
-        }
-        DBuf<int32_t> d_ids, d_roots;
-        GX_TRY(d_ids.alloc(kSamples));
-        GX_TRY(d_roots.alloc(kSamples));
-        GX_HIP_TRY(hipMemcpyAsync(d_ids.p, ids.data(), kSamples * 4, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_sample_roots, dim3(4), dim3(256), 0, s, parent.p, d_ids.p, kSamples, d_roots.p);
-        GX_TRY(check_launch("k_sample_roots"));
-        GX_HIP_TRY(hipMemcpyAsync(roots.data(), d_roots.p, kSamples * 4, hipMemcpyDeviceToHost, s));
-        GX_HIP_TRY(hipStreamSynchronize(s));
-        std::sort(roots.begin(), roots.end());
-        giant = roots[0];
-        int best = 0;
-        for (int i = 0, j; i < kSamples; i = j) {
-            for (j = i; j < kSamples && roots[j] == roots[i]; j++) {
+        // sample ids: a fixed hash sequence, uploaded once per graph size
+        if (!g->wcc_ids.p || g->wcc_ids_n != n) {
+            std::vector<int32_t> ids(kSamples);
+            uint64_t h = 0x9E3779B97F4A7C15ull;
+            for (int i = 0; i < kSamples; i++) {
+                h ^= h >> 31;
+                h *= 0xBF58476D1CE4E5B9ull;
+                h ^= h >> 29;
+                ids[i] = (int32_t)(h % (uint64_t)n);
             }
-            if (j - i > best) {
-                best = j - i;
-                giant = roots[i];
-            }
+            GX_TRY(g->wcc_ids.alloc(kSamples + 1));   // + the chosen root
+            GX_HIP_TRY(hipMemcpy(g->wcc_ids.p, ids.data(), kSamples * 4, hipMemcpyHostToDevice));
+            g->wcc_ids_n = n;
         }
+        giant_d = g->wcc_ids.p + kSamples;
+        hipLaunchKernelGGL(k_pick_giant, dim3(1), dim3(kSamples), 0, s, parent.p, g->wcc_ids.p, giant_d);
+        GX_TRY(check_launch("k_pick_giant"));
         {
             KTimer kt(ctx, "wcc_hook", s);
             hipLaunchKernelGGL(k_afforest_finish, dim3(grid_for((uint64_t)n, kWccBlock, 8192)),
-                               dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, 2, giant, parent.p);
+                               dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, 2, giant_d, parent.p);
         }
         GX_TRY(check_launch("k_afforest_finish"));
         {
@@ -372,7 +386,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         if (live) {
             GX_HIP_TRY(hipMemsetAsync(minorig, 0x7f, (size_t)live * 4, s));
             hipLaunchKernelGGL(k_wcc_min_orig, dim3(grid_for((uint64_t)live, kWccBlock, 2048)), dim3(kWccBlock), 0,
-                               s, parent.p, g->out_order, live, giant, minorig);
+                               s, parent.p, g->out_order, live, giant_d, minorig);
         }
         hipLaunchKernelGGL(k_wcc_label_orig, dim3(vgrid), dim3(256), 0, s, parent.p, g->out_order, minorig, n, live,
                            lab);
