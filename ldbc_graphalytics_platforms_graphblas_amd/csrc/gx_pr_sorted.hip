@@ -197,56 +197,129 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // (the loop starts at the 64-entry group holding lo, so wave-instructions stay group-aligned).
 // `step` (a multiple of U * BS) > U * BS: only every (step / (U * BS))-th round of U * BS
 // entries, from the one at lo (interleaved units of a split block).
-template <int BS, int U, bool PIPE>
+//
+// X4 (the units kernel's default): four consecutive entries per lane from one 16-B load, so a
+// round costs U / 4 index-load instructions per lane instead of U.  What bounds the launch is
+// the CU's rate of vector memory instructions, not bytes or cache lines (tools/pr_acc_probe.sh,
+// DESIGN.md 4): with every gather folded into 32 KiB of x, or into 1/16 of its lines, a launch
+// still took 93-94 us against 101-103; without the LDS adds 98.5; with 3 of 8 gathers 79.5;
+// with no gathers 70.  Wave w takes the U / 4 256-entry supergroups [R + 256 (w U/4 + v), +256)
+// of round R; lane l holds entries 4l .. 4l+3 of each, all in 64-entry group l / 16 of the
+// supergroup.  The four group bases are scalar loads issued with the index loads and selected
+// per lane when the round is computed (a select right after the loads waited for them).
+template <int BS, int U, bool PIPE, bool X4 = false>
 __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock &b, int64_t lo, int64_t hi,
                                              double *acc, int64_t step = (int64_t)U * BS) {
     const int tid = threadIdx.x;
     const int64_t z0 = b.nz_begin, z1 = b.nz_end;
-    if (lo < hi) {
-        const int64_t glast = (z1 - 1 - z0) >> 6;
-        const int64_t start = z0 + ((lo - z0) & ~(int64_t)(kWave - 1));   // 64-entry group aligned
-        const int lane = tid & (kWave - 1);
-        uint32_t pk[U], gb[U];
-        auto load_round = [&](int64_t k0) {
+    if (lo >= hi) return;
+    const int64_t glast = (z1 - 1 - z0) >> 6;
+    const int64_t start = z0 + ((lo - z0) & ~(int64_t)(kWave - 1));   // 64-entry group aligned
+    const int lane = tid & (kWave - 1);
+    if constexpr (X4) {
+        static_assert(U % 4 == 0, "X4 takes four entries per load");
+        constexpr int V = U / 4;
+        const int wave = tid >> 6;
+        const int sub = lane >> 4;
+        uint4 q[V];
+        uint32_t gbs[V][4];   // the 4 group bases of each supergroup (uniform)
+        auto load_round = [&](int64_t R) {
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int64_t e = k0 + (int64_t)u * BS;
-                pk[u] = __builtin_nontemporal_load(a.spk + min(e, z1 - 1));
-                // the group of the wave's first lane: the same for all 64 lanes
-                const int g = (int)min((e - lane - z0) >> 6, glast);
-                gb[u] = a.gbase[b.seg + __builtin_amdgcn_readfirstlane(g)];
+            for (int v = 0; v < V; v++) {
+                const int64_t sg = R + (int64_t)(wave * V + v) * 256;
+                // clamped into the block; spk's allocation slack covers the 3 entries past z1 - 1
+                // (dword-aligned 16-B loads)
+                q[v] = *reinterpret_cast<const uint4 *>(a.spk + min(sg + 4 * lane, z1 - 1));
+                // readfirstlane is convergent, so the loads cannot sink into the select's
+                // branches.  Groups past the block's last read the next block's bases or the
+                // allocation's slack, for entries that ok[] masks.
+                const int g = __builtin_amdgcn_readfirstlane((int)(b.seg + ((sg - z0) >> 6)));
+#pragma unroll
+                for (int k = 0; k < 4; k++) gbs[v][k] = __builtin_amdgcn_readfirstlane(a.gbase[g + k]);
             }
         };
-        int64_t k0 = start + tid;
-        if (PIPE) load_round(k0);
-        for (; k0 < hi; k0 += step) {
-            if (!PIPE) load_round(k0);
+        int64_t R = start;
+        load_round(R);
+        for (; R < hi; R += step) {
             int32_t c[U];
             uint32_t r[U];
-            uint32_t esc = 0;
+            bool ok[U];
+            uint32_t esc = 0, gb[V];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                r[u] = pk[u] & ((1u << kRowBits) - 1);
-                c[u] = (int32_t)(gb[u] + (pk[u] >> kRowBits));
-                esc |= gb[u];
+            for (int v = 0; v < V; v++) {
+                gb[v] = sub == 0 ? gbs[v][0] : sub == 1 ? gbs[v][1] : sub == 2 ? gbs[v][2] : gbs[v][3];
+                const uint32_t w4[4] = {q[v].x, q[v].y, q[v].z, q[v].w};
+                const int64_t e4 = R + (int64_t)(wave * V + v) * 256 + 4 * lane;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    // entries outside [lo, hi) (and whatever the clamped load brought) gather
+                    // x(0) and add 0.0 to row 0
+                    const int i = 4 * v + j;
+                    ok[i] = e4 + j >= lo && e4 + j < hi;
+                    r[i] = ok[i] ? (w4[j] & ((1u << kRowBits) - 1)) : 0u;
+                    c[i] = ok[i] ? (int32_t)(gb[v] + (w4[j] >> kRowBits)) : 0;
+                }
+                esc |= gb[v];
             }
-            if (esc & 0x80000000u) {   // wave-uniform: an escape group in this round
+            if (__builtin_amdgcn_readfirstlane(__ballot(esc & 0x80000000u) != 0)) {   // an escape group
 #pragma unroll
-                for (int u = 0; u < U; u++)
-                    if (gb[u] & 0x80000000u) c[u] = a.sci[min(k0 + (int64_t)u * BS, z1 - 1)];
+                for (int v = 0; v < V; v++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int i = 4 * v + j;
+                        const int64_t e = R + (int64_t)(wave * V + v) * 256 + 4 * lane + j;
+                        if ((gb[v] & 0x80000000u) && ok[i]) c[i] = a.sci[e];
+                    }
             }
             double g[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
-            if (PIPE) load_round(k0 + step);
-            // entries outside [lo, hi) add 0.0 instead of branching round the add: behind a
-            // branch the compiler sank the first gather below the next round's entry loads and
-            // waited for all of them (vmcnt(0)) before the first add
+            for (int i = 0; i < U; i++) g[i] = a.x_in[c[i]];
+            load_round(R + step);
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int64_t e = k0 + (int64_t)u * BS;
-                atomicAdd(&acc[r[u]], e >= lo && e < hi ? g[u] : 0.0);
-            }
+            for (int i = 0; i < U; i++) atomicAdd(&acc[r[i]], ok[i] ? g[i] : 0.0);
+        }
+        return;
+    }
+    uint32_t pk[U], gb[U];
+    auto load_round = [&](int64_t k0) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t e = k0 + (int64_t)u * BS;
+            pk[u] = __builtin_nontemporal_load(a.spk + min(e, z1 - 1));
+            // the group of the wave's first lane: the same for all 64 lanes
+            const int g = (int)min((e - lane - z0) >> 6, glast);
+            gb[u] = a.gbase[b.seg + __builtin_amdgcn_readfirstlane(g)];
+        }
+    };
+    int64_t k0 = start + tid;
+    if (PIPE) load_round(k0);
+    for (; k0 < hi; k0 += step) {
+        if (!PIPE) load_round(k0);
+        int32_t c[U];
+        uint32_t r[U];
+        uint32_t esc = 0;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            r[u] = pk[u] & ((1u << kRowBits) - 1);
+            c[u] = (int32_t)(gb[u] + (pk[u] >> kRowBits));
+            esc |= gb[u];
+        }
+        if (esc & 0x80000000u) {   // wave-uniform: an escape group in this round
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (gb[u] & 0x80000000u) c[u] = a.sci[min(k0 + (int64_t)u * BS, z1 - 1)];
+        }
+        double g[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) g[u] = a.x_in[c[u]];
+        if (PIPE) load_round(k0 + step);
+        // entries outside [lo, hi) add 0.0 instead of branching round the add: behind a
+        // branch the compiler sank the first gather below the next round's entry loads and
+        // waited for all of them (vmcnt(0)) before the first add
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t e = k0 + (int64_t)u * BS;
+            atomicAdd(&acc[r[u]], e >= lo && e < hi ? g[u] : 0.0);
         }
     }
 }
@@ -311,7 +384,7 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
 // Workgroups [0, nlong) are the LONG row segments, as in k_pr_pull_sorted, padded to nlong_pad
 // (a multiple of 8, so that grid slot nlong_pad + 8 i + x lands on XCD list x).
 // TIMES: debug build with per-workgroup timestamps (GX_PR_UNIT_TIMES).
-template <int BS, int U, bool TIMES>
+template <int BS, int U, bool TIMES, bool X4 = false>
 __global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? 8 : 1)) void k_pr_pull_units(SortedArgs a) {   // 1024: two per CU
     extern __shared__ double acc[];
     __shared__ double wred[BS / kWave];
@@ -344,7 +417,7 @@ __global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? 8 : 1)) void k_pr_pul
     const int nrows = b.row_end - b.row_begin;
     for (int i = tid; i < nrows; i += BS) acc[i] = 0.0;
     __syncthreads();
-    gather_range<BS, U, true>(a, b, u.lo, u.hi, acc, u.step);
+    gather_range<BS, U, true, X4>(a, b, u.lo, u.hi, acc, u.step);
     __syncthreads();
     if (TIMES && tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
     if (u.nunits > 1) {
@@ -603,6 +676,7 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     // GX_PR_SORTED_VARIANT = 0 (1024 threads, 8 gathers in flight per lane, entry loads
     // pipelined) | 1 (1024, 8, not pipelined) | 2 (512, 16, pipelined) | 3 (512, 8, pipelined)
     p->sorted_variant = env_int("GX_PR_SORTED_VARIANT", 0, 0, 3);
+    p->index_x4 = env_int("GX_PR_INDEX_X4", 1, 0, 1);
     // hub slice of x for the two-pass mode (GX_PR_HOT_COLS = 0: one pass).  One rank only:
     // in a multi-rank exchange layout the hub columns are spread over every rank's chunk.
     p->hot_cols = env_int("GX_PR_HOT_COLS", (int)p->hot_cols, 0, 1 << 30);
@@ -728,7 +802,7 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     // block-sorted columns and packed entries (entries of LONG rows stay unused there)
     GX_TRY(p->sci.alloc(std::max<uint64_t>(nnz, 1), 16));
     GX_TRY(p->spk.alloc(std::max<uint64_t>(nnz, 1), 16));
-    GX_TRY(p->gbase.alloc(std::max<int64_t>(ngroups, 1)));
+    GX_TRY(p->gbase.alloc(std::max<int64_t>(ngroups, 1), 16));
     hipStream_t s = p->ctx->stream;
     std::vector<int64_t> coff(sortb.size());
     int64_t m = 0;
@@ -1005,12 +1079,17 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
         const int pad = p->sorted_variant == 0 ? 96 * 1024 : 0;
         const size_t lds = std::max<size_t>((size_t)p->sorted_lds, (size_t)env_int("GX_PR_UNIT_LDS", pad, 0, 160 * 1024 - 4096));
         if (a.utimes) {
-            hipLaunchKernelGGL((k_pr_pull_units<1024, 8, true>), grid, dim3(1024), lds, s, a);
+            if (p->index_x4) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, true, true>), grid, dim3(1024), lds, s, a);
+            else hipLaunchKernelGGL((k_pr_pull_units<1024, 8, true, false>), grid, dim3(1024), lds, s, a);
         } else {
             switch (p->sorted_variant) {
             case 2: hipLaunchKernelGGL((k_pr_pull_units<512, 16, false>), grid, dim3(512), lds, s, a); break;
             case 3: hipLaunchKernelGGL((k_pr_pull_units<512, 8, false>), grid, dim3(512), lds, s, a); break;
-            default: hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false>), grid, dim3(1024), lds, s, a); break;
+            default:
+                // GX_PR_INDEX_X4=0: one 4-B index load per entry (round 2's kernel)
+                if (p->index_x4) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true>), grid, dim3(1024), lds, s, a);
+                else hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, false>), grid, dim3(1024), lds, s, a);
+                break;
             }
         }
         if (a.utimes && ++p->utimes_launch == env_int("GX_PR_UNIT_TIMES_LAUNCH", 5, 1, 1 << 30)) {
