@@ -231,9 +231,11 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
                 // (dword-aligned 16-B loads)
                 q[v] = *reinterpret_cast<const uint4 *>(a.spk + min(sg + 4 * lane, z1 - 1));
                 // readfirstlane is convergent, so the loads cannot sink into the select's
-                // branches.  Groups past the block's last read the next block's bases or the
-                // allocation's slack, for entries that ok[] masks.
-                const int g = __builtin_amdgcn_readfirstlane((int)(b.seg + ((sg - z0) >> 6)));
+                // branches.  A supergroup past the block's end (the tail of the last round, or
+                // the prefetch past it) reads the last group's bases; the up to 3 groups past
+                // the last read the next block's bases or gbase's allocation slack, for entries
+                // that ok[] masks.
+                const int g = __builtin_amdgcn_readfirstlane((int)(b.seg + min((sg - z0) >> 6, glast)));
 #pragma unroll
                 for (int k = 0; k < 4; k++) gbs[v][k] = __builtin_amdgcn_readfirstlane(a.gbase[g + k]);
             }
