@@ -387,7 +387,7 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
 // (a multiple of 8, so that grid slot nlong_pad + 8 i + x lands on XCD list x).
 // TIMES: debug build with per-workgroup timestamps (GX_PR_UNIT_TIMES).
 template <int BS, int U, bool TIMES, bool X4 = false>
-__global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? 8 : 1)) void k_pr_pull_units(SortedArgs a) {   // 1024: two per CU
+__global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? (U >= 16 ? 4 : 8) : 1)) void k_pr_pull_units(SortedArgs a) {   // 1024: two per CU
     extern __shared__ double acc[];
     __shared__ double wred[BS / kWave];
     __shared__ int last;
@@ -677,7 +677,7 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     const uint64_t nnz = (uint64_t)h_rp[rows];
     // GX_PR_SORTED_VARIANT = 0 (1024 threads, 8 gathers in flight per lane, entry loads
     // pipelined) | 1 (1024, 8, not pipelined) | 2 (512, 16, pipelined) | 3 (512, 8, pipelined)
-    p->sorted_variant = env_int("GX_PR_SORTED_VARIANT", 0, 0, 3);
+    p->sorted_variant = env_int("GX_PR_SORTED_VARIANT", 0, 0, 4);
     p->index_x4 = env_int("GX_PR_INDEX_X4", 1, 0, 1);
     // hub slice of x for the two-pass mode (GX_PR_HOT_COLS = 0: one pass).  One rank only:
     // in a multi-rank exchange layout the hub columns are spread over every rank's chunk.
@@ -701,12 +701,12 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     // 1064-1070 [1489].  Larger blocks cut the x line requests (tools/pr_line_model.py) but
     // give the last arriver more slabs per row.
     p->units_mode = !p->two_pass && p->slices == 1 && p->sorted_variant != 1 && !std::getenv("GX_PR_SORTED_NNZ");
-    const int64_t round = p->sorted_variant == 3 ? 512 * 8 : 1024 * 8;   // U * BS of the launch
+    const int64_t round = p->sorted_variant == 3 ? 512 * 8 : p->sorted_variant == 4 ? 1024 * 16 : 1024 * 8;   // U * BS of the launch
     const double per_cu = std::max(1.0, (double)nnz / (double)cus);
     const bool huge = per_cu > (double)(2 << 20);
     // rows per block (LDS accumulators, kRowBits-bit row field; 16 Ki rows = 128 KiB of LDS,
     // which the split-block mode's one workgroup per CU can take)
-    const int rmax = p->units_mode && p->sorted_variant == 0 ? 1 << kRowBits : 4096;
+    const int rmax = p->units_mode && (p->sorted_variant == 0 || p->sorted_variant == 4) ? 1 << kRowBits : 4096;
     p->sorted_rows = env_int("GX_PR_SORTED_ROWS", p->units_mode && huge ? rmax : 4096, 64, rmax);
     int64_t B, T = 0;
     if (p->units_mode) {
@@ -1078,7 +1078,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
         // workgroup; 0 = only the accumulators, two per CU).  Fewer concurrent sweeps keep
         // the XCD's L2 window of x smaller: SYN-7_5 one per CU 100-104 us per launch against
         // 109-125 with two (tools/pr_units_sweep.sh).
-        const int pad = p->sorted_variant == 0 ? 96 * 1024 : 0;
+        const int pad = p->sorted_variant == 0 || p->sorted_variant == 4 ? 96 * 1024 : 0;
         const size_t lds = std::max<size_t>((size_t)p->sorted_lds, (size_t)env_int("GX_PR_UNIT_LDS", pad, 0, 160 * 1024 - 4096));
         if (a.utimes) {
             if (p->index_x4) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, true, true>), grid, dim3(1024), lds, s, a);
@@ -1087,6 +1087,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
             switch (p->sorted_variant) {
             case 2: hipLaunchKernelGGL((k_pr_pull_units<512, 16, false>), grid, dim3(512), lds, s, a); break;
             case 3: hipLaunchKernelGGL((k_pr_pull_units<512, 8, false>), grid, dim3(512), lds, s, a); break;
+            case 4: hipLaunchKernelGGL((k_pr_pull_units<1024, 16, false, true>), grid, dim3(1024), lds, s, a); break;
             default:
                 // GX_PR_INDEX_X4=0: one 4-B index load per entry (round 2's kernel)
                 if (p->index_x4) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true>), grid, dim3(1024), lds, s, a);
