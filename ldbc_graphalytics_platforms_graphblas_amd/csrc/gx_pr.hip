@@ -285,14 +285,16 @@ __global__ __launch_bounds__(256) void k_pr_dangling(const int32_t *__restrict__
     }
 }
 
+// x = PR_0 / (outdeg / d) (dangling rows: PR_0 itself), and the chunk's dangling slot = the
+// sum of its dangling rows' PR_0 = nd / n, known at plan time (no k_pr_dangling launch per run).
 __global__ void k_pr_init(const int32_t *__restrict__ outdeg, int64_t rows, double inv_n,
-                          double damping, double *x, int64_t slot, int zero_slot, double *xd, int64_t live) {
+                          double damping, double *x, int64_t slot, double dangling0, double *xd, int64_t live) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t deg = outdeg[i];
         store_x(x, xd, live, i, deg > 0 ? inv_n / ((double)deg / damping) : inv_n);
     }
-    if (zero_slot && blockIdx.x == 0 && threadIdx.x == 0) x[slot] = 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) x[slot] = dangling0;
 }
 
 }  // namespace
@@ -410,9 +412,8 @@ int pr_init(PrPart *p, double *x_local, hipStream_t s) {
     const double inv_n = 1.0 / (double)p->n_global;
     hipLaunchKernelGGL(k_pr_init, dim3(grid_for(p->rows, 256, 8192)), dim3(256), 0, s, p->outdeg,
                        (int64_t)p->rows, inv_n, p->damping, x_local, (int64_t)p->chunk - 1,
-                       p->nd == 0 ? 1 : 0, p->xd.p, (int64_t)p->live);
-    GX_TRY(check_launch("k_pr_init"));
-    return pr_dangling(p, x_local, s);
+                       (double)p->nd / (double)p->n_global, p->xd.p, (int64_t)p->live);
+    return check_launch("k_pr_init");
 }
 
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s) {
