@@ -200,7 +200,7 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 //
 // X4 (the units kernel's default): four consecutive entries per lane from one 16-B load, so a
 // round costs U / 4 index-load instructions per lane instead of U.  What bounds the launch is
-// the CU's rate of vector memory instructions, not bytes or cache lines (tools/pr_acc_probe.sh,
+// the CU's rate of vector memory instructions, not bytes or cache lines (timing probes,
 // DESIGN.md 4): with every gather folded into 32 KiB of x, or into 1/16 of its lines, a launch
 // still took 93-94 us against 101-103; without the LDS adds 98.5; with 3 of 8 gathers 79.5;
 // with no gathers 70.  Wave w takes the U / 4 256-entry supergroups [R + 256 (w U/4 + v), +256)
