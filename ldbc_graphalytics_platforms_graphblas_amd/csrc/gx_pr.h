@@ -126,6 +126,7 @@ struct PrPart {
     int sorted_lds = 0;          // dynamic LDS bytes of the launch
     int sorted_variant = 0;      // tuning: block size / gathers in flight (gx_pr_sorted.hip)
     int index_x4 = 1;            // units kernel: four entries per 16-B index load (GX_PR_INDEX_X4)
+    int pipe2 = 1;               // X4 units kernel pipelined across rounds (GX_PR_PIPE2, default on)
     DBuf<int64_t> ssplit;        // per block: first sorted entry in the tail pass
     DBuf<double> ypart;          // hub-pass row sums
     int64_t hot_cols = 0;        // columns of the hub pass (0: one pass; GX_PR_HOT_COLS)

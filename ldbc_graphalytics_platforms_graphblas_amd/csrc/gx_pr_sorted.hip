@@ -207,7 +207,7 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // of round R; lane l holds entries 4l .. 4l+3 of each, all in 64-entry group l / 16 of the
 // supergroup.  The four group bases are scalar loads issued with the index loads and selected
 // per lane when the round is computed (a select right after the loads waited for them).
-template <int BS, int U, bool PIPE, bool X4 = false>
+template <int BS, int U, bool PIPE, bool X4 = false, bool P2 = false>
 __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock &b, int64_t lo, int64_t hi,
                                              double *acc, int64_t step = (int64_t)U * BS) {
     const int tid = threadIdx.x;
@@ -216,6 +216,93 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
     const int64_t glast = (z1 - 1 - z0) >> 6;
     const int64_t start = z0 + ((lo - z0) & ~(int64_t)(kWave - 1));   // 64-entry group aligned
     const int lane = tid & (kWave - 1);
+    if constexpr (X4 && P2) {
+        // X4 pipelined across rounds (GX_PR_PIPE2): round k+1's gathers are issued before
+        // round k's LDS adds, with the index loads two rounds ahead; buffers A/B alternate
+        // (no copies of pending loads, which would wait for them)
+        constexpr int V = U / 4;
+        const int wave = tid >> 6;
+        const int sub = lane >> 4;
+        struct Rd {
+            uint4 q[V];
+            uint32_t gbs[V][4];
+        };
+        struct Gt {
+            double g[U];
+            uint32_t r[U];
+            bool ok[U];
+        };
+        auto load = [&](Rd &d, int64_t R) {
+#pragma unroll
+            for (int v = 0; v < V; v++) {
+                const int64_t sg = R + (int64_t)(wave * V + v) * 256;
+                d.q[v] = *reinterpret_cast<const uint4 *>(a.spk + min(sg + 4 * lane, z1 - 1));
+                const int g = __builtin_amdgcn_readfirstlane((int)(b.seg + min((sg - z0) >> 6, glast)));
+#pragma unroll
+                for (int k = 0; k < 4; k++) d.gbs[v][k] = __builtin_amdgcn_readfirstlane(a.gbase[g + k]);
+            }
+        };
+        auto issue = [&](const Rd &d, int64_t R, Gt &t) {
+            int32_t c[U];
+            uint32_t esc = 0, gb[V];
+#pragma unroll
+            for (int v = 0; v < V; v++) {
+                gb[v] = sub == 0 ? d.gbs[v][0] : sub == 1 ? d.gbs[v][1] : sub == 2 ? d.gbs[v][2] : d.gbs[v][3];
+                const uint32_t w4[4] = {d.q[v].x, d.q[v].y, d.q[v].z, d.q[v].w};
+                const int64_t e4 = R + (int64_t)(wave * V + v) * 256 + 4 * lane;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int i = 4 * v + j;
+                    t.ok[i] = e4 + j >= lo && e4 + j < hi;
+                    t.r[i] = t.ok[i] ? (w4[j] & ((1u << kRowBits) - 1)) : 0u;
+                    c[i] = t.ok[i] ? (int32_t)(gb[v] + (w4[j] >> kRowBits)) : 0;
+                }
+                esc |= gb[v];
+            }
+            if (__builtin_amdgcn_readfirstlane(__ballot(esc & 0x80000000u) != 0)) {
+#pragma unroll
+                for (int v = 0; v < V; v++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int i = 4 * v + j;
+                        const int64_t e = R + (int64_t)(wave * V + v) * 256 + 4 * lane + j;
+                        if ((gb[v] & 0x80000000u) && t.ok[i]) c[i] = a.sci[e];
+                    }
+            }
+#pragma unroll
+            for (int i = 0; i < U; i++) t.g[i] = a.x_in[c[i]];
+        };
+        auto add = [&](const Gt &t) {
+#pragma unroll
+            for (int i = 0; i < U; i++) atomicAdd(&acc[t.r[i]], t.ok[i] ? t.g[i] : 0.0);
+        };
+        Rd dA, dB;
+        Gt tA, tB;
+        int64_t R = start;
+        load(dA, R);
+        load(dB, R + step);
+        issue(dA, R, tA);
+        load(dA, R + 2 * step);
+        for (;;) {
+            if (R + step >= hi) {
+                add(tA);
+                break;
+            }
+            issue(dB, R + step, tB);
+            load(dB, R + 3 * step);
+            add(tA);
+            R += step;
+            if (R + step >= hi) {
+                add(tB);
+                break;
+            }
+            issue(dA, R + step, tA);
+            load(dA, R + 3 * step);
+            add(tB);
+            R += step;
+        }
+        return;
+    }
     if constexpr (X4) {
         static_assert(U % 4 == 0, "X4 takes four entries per load");
         constexpr int V = U / 4;
@@ -386,8 +473,8 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
 // Workgroups [0, nlong) are the LONG row segments, as in k_pr_pull_sorted, padded to nlong_pad
 // (a multiple of 8, so that grid slot nlong_pad + 8 i + x lands on XCD list x).
 // TIMES: debug build with per-workgroup timestamps (GX_PR_UNIT_TIMES).
-template <int BS, int U, bool TIMES, bool X4 = false>
-__global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? (U >= 16 ? 4 : 8) : 1)) void k_pr_pull_units(SortedArgs a) {   // 1024: two per CU
+template <int BS, int U, bool TIMES, bool X4 = false, bool P2 = false>
+__global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? (U >= 16 || P2 ? 4 : 8) : 1)) void k_pr_pull_units(SortedArgs a) {   // 1024: two per CU
     extern __shared__ double acc[];
     __shared__ double wred[BS / kWave];
     __shared__ int last;
@@ -419,7 +506,7 @@ __global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? (U >= 16 ? 4 : 8) : 1
     const int nrows = b.row_end - b.row_begin;
     for (int i = tid; i < nrows; i += BS) acc[i] = 0.0;
     __syncthreads();
-    gather_range<BS, U, true, X4>(a, b, u.lo, u.hi, acc, u.step);
+    gather_range<BS, U, true, X4, P2>(a, b, u.lo, u.hi, acc, u.step);
     __syncthreads();
     if (TIMES && tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
     if (u.nunits > 1) {
@@ -679,6 +766,7 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     // pipelined) | 1 (1024, 8, not pipelined) | 2 (512, 16, pipelined) | 3 (512, 8, pipelined)
     p->sorted_variant = env_int("GX_PR_SORTED_VARIANT", 0, 0, 4);
     p->index_x4 = env_int("GX_PR_INDEX_X4", 1, 0, 1);
+    p->pipe2 = env_int("GX_PR_PIPE2", 1, 0, 1);
     // hub slice of x for the two-pass mode (GX_PR_HOT_COLS = 0: one pass).  One rank only:
     // in a multi-rank exchange layout the hub columns are spread over every rank's chunk.
     p->hot_cols = env_int("GX_PR_HOT_COLS", (int)p->hot_cols, 0, 1 << 30);
@@ -1090,7 +1178,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
             case 4: hipLaunchKernelGGL((k_pr_pull_units<1024, 16, false, true>), grid, dim3(1024), lds, s, a); break;
             default:
                 // GX_PR_INDEX_X4=0: one 4-B index load per entry (round 2's kernel)
-                if (p->index_x4) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true>), grid, dim3(1024), lds, s, a);
+                if (p->index_x4 && p->pipe2) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true, true>), grid, dim3(1024), lds, s, a);
+                else if (p->index_x4) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true>), grid, dim3(1024), lds, s, a);
                 else hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, false>), grid, dim3(1024), lds, s, a);
                 break;
             }

@@ -200,6 +200,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, slices):
                                  {"GX_PR_HOT_COLS": "1024", "GX_PR_SORTED_ROWS": "64"},
                                  {"GX_PR_SORTED_VARIANT": "1"}, {"GX_PR_SORTED_VARIANT": "2"},
                                  {"GX_PR_SORTED_VARIANT": "4"}, {"GX_PR_INDEX_X4": "0"}, {"GX_PR_UNIT_LDS": "0"},
+                                 {"GX_PR_PIPE2": "0"}, {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536", "GX_PR_PIPE2": "0"},
                                  {"GX_PR_SLICES": "2"}, {"GX_PR_SLICES": "4"}, {"GX_PR_SLICES": "8"},
                                  {"GX_PR_SLICES": "8", "GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SLICES": "1"},
                                  {"GX_PR_KERNEL": "adaptive"},
