@@ -26,7 +26,7 @@ HOST_OBJS := $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))
 EXES := bfs pr sssp wcc cdlp lcc converter
 EXE_BINS := $(addprefix bin/exe/,$(EXES))
 
-.PHONY: all lib exe oracle clean
+.PHONY: all lib exe oracle clean probe
 all: lib exe oracle
 lib: $(LIBGX)
 exe: $(EXE_BINS)
@@ -57,3 +57,14 @@ oracle/liboracle.so: oracle/gx_oracle.c
 
 clean:
 	rm -rf $(BUILD) $(LIBGX) $(EXE_BINS) oracle/liboracle.so
+
+# Diagnostic build (not the product): libgx with the PageRank timing probes of
+# gx_pr_sorted.hip (GX_PR_PROBE=1..7, wrong results by design), for tools/pr_probe.sh
+# (tools/ travels to the GPU box; build/ does not).
+PROBE_DIR := $(BUILD)/probe
+probe: tools/probe/libgx.so
+$(PROBE_DIR)/gx_pr_sorted.hip.o: $(CSRC)/gx_pr_sorted.hip $(wildcard $(CSRC)/*.h) include/gx.h | $(BUILD)
+	mkdir -p $(PROBE_DIR)
+	$(HIPCC) $(HIPFLAGS) -DGX_PR_PROBES -c $< -o $@
+tools/probe/libgx.so: $(filter-out $(BUILD)/gx_pr_sorted.hip.o,$(HIP_OBJS)) $(PROBE_DIR)/gx_pr_sorted.hip.o $(HOST_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -ldl -Wl,-soname,libgx.so

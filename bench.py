@@ -1,24 +1,30 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Graphalytics PageRank edges/s on MI355X (BASELINE.json configs[1]).
+"""Headline benchmark: Graphalytics PageRank edges/s on MI355X.
 
-Workload: PageRank, d = 0.85, 10 iterations, fp64, on SYN-7_5 -- the
-seeded stand-in for datagen-7_5-fb (no network for the real dataset): undirected R-MAT
-(a,b,c,d) = (0.57,0.19,0.19,0.05), scale 20, edgefactor 32, seed 75, duplicates and
-self-loops removed, vertex ids randomly permuted.  One "step" = one complete PageRank run
-(init + 10 pull iterations) with the graph resident in HBM.
+Workload (the north-star target "datagen-8_5-fb PageRank at 1 GPU"):
+PageRank, d = 0.85, 10 iterations, fp64, on SYN-8_5 -- the seeded stand-in for datagen-8_5-fb
+(no network for the real dataset): undirected R-MAT (a,b,c,d) = (0.57,0.19,0.19,0.05), scale 23,
+edgefactor 40, seed 85, duplicates and self-loops removed, vertex ids randomly permuted
+(8.4 M vertices, 628 M stored entries).  One "step" = one complete PageRank run (init + 10 pull
+iterations) with the graph resident in HBM.  At N = 1 the line also carries `secondary`: the
+same measurement on SYN-7_5 (configs[1]'s datagen-7_5-fb stand-in, scale 20, ef 32, seed 75).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--graph SYN-7_5]
 
 N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL): the pull matrix is
-row-partitioned by nnz and the rank vector is all-gathered every iteration (strong scaling
-on the same graph).  Rank 0 prints ONE JSON line.
+row-partitioned and the rank vector is all-gathered every iteration (strong scaling on the
+same graph).  Rank 0 prints ONE JSON line.
 
 value    = (stored entries * iterations * K) / max-over-ranks wall time of the K steps
-roofline = k_pr_pull: algorithmic bytes per launch (4 nnz + 8 (n+1) + 8 n + 8 n, SURVEY.md
+roofline = k_pr_pull_units: algorithmic bytes per launch (4 nnz + 8 (n+1) + 8 n + 8 n, SURVEY.md
            8d) / mean launch duration from hipEvents on the launch stream during the timed
            steps; peak 8.0 TB/s (MI355X HBM3E); traffic from the committed rocprofv3 PMC pass.
+processing_ms = the Graphalytics processing time of the executable path (bin/exe/pr brackets
+           gx_graph_create's upload + one gx_pagerank call, whose first call builds the plan:
+           pr.cpp:77-79 brackets LAGraph_New .. LAGr_PageRankGX the same way).
 cpu_baseline = the oracle's OpenMP PageRank (oracle/gx_oracle.c, "port" -- SuiteSparse is not
-           installed) timed on this host on the same graph, rank 0 at N = 1 only.
+           installed) on every host core this process may use (the cgroup CPU quota, e.g. 16 on
+           the GPU box), on the same graph, rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -43,15 +49,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--scale", type=int, default=20)
-    ap.add_argument("--edgefactor", type=int, default=32)
-    ap.add_argument("--seed", type=int, default=75)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--damping", type=float, default=0.85)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="PR: skip the SYN-7_5 secondary measurement")
     ap.add_argument("--algorithm", default="pr", choices=["pr", "bfs", "wcc", "sssp", "cdlp", "lcc"],
-                    help="pr = the headline (BASELINE configs[1]); the others measure configs 3-5 on 1 GPU")
+                    help="pr = the headline (SYN-8_5, BASELINE configs[3]'s graph); the others measure configs 3-5 "
+                         "on 1 GPU")
     ap.add_argument("--graph", default=None, choices=sorted(PRESETS), help="synthetic stand-in (SURVEY.md 8d)")
     ap.add_argument("--partitioned", action="store_true",
                     help="run --algorithm through the multi-GPU (vertex-range) path even at N=1")
@@ -65,7 +70,7 @@ PRESETS = {
     "SYN-8_5": dict(scale=23, ef=40, seed=85, undirected=True, weighted=True, stands_for="datagen-8_5-fb"),
     "SYN-cit": dict(scale=22, ef=4, seed=3, undirected=False, weighted=False, stands_for="cit-Patents"),
 }
-DEFAULT_GRAPH = {"pr": "SYN-7_5", "cdlp": "SYN-7_5", "bfs": "SYN-g500-22", "wcc": "SYN-g500-22",
+DEFAULT_GRAPH = {"pr": "SYN-8_5", "cdlp": "SYN-7_5", "bfs": "SYN-g500-22", "wcc": "SYN-g500-22",
                  "sssp": "SYN-8_5", "lcc": "SYN-cit"}
 # the dominant kernel of each algorithm: the KTimer names summed (CDLP's light tier runs as
 # two launches, the 256-slot instance "cdlp_light_s" and the 1024-slot "cdlp_light")
@@ -78,8 +83,22 @@ KERNELS = {"bfs": ["bfs_topdown", "bfs_bottomup"], "wcc": ["wcc_sample", "wcc_ho
            "lcc": ["lcc_orient", "lcc_triangles"]}
 
 
+def usable_cores() -> int:
+    """Host cores this process may use: the CPU affinity mask, capped by the cgroup CPU quota
+    (cgroup v2 cpu.max; the GPU box grants 16 of its 256 CPUs this way, and `nproc` reports
+    the same 16 there through OMP_NUM_THREADS)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def host_cpu() -> dict:
-    """nproc and the CPU model name, recorded with every CPU baseline."""
+    """Core counts and the CPU model name, recorded with every CPU baseline."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -89,7 +108,15 @@ def host_cpu() -> dict:
                     break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "cpu_model": model}
+    import shutil
+    import subprocess
+    nproc = None
+    if shutil.which("nproc"):
+        try:
+            nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+        except ValueError:
+            pass
+    return {"nproc": nproc, "cpu_count": os.cpu_count(), "usable_cores": usable_cores(), "cpu_model": model}
 
 
 def stream_copy_gbs(device, nbytes: int = 1 << 30, reps: int = 10) -> float:
@@ -219,22 +246,27 @@ def run_algorithm(args):
     parity = None
     if not args.no_cpu_baseline:
         from oracle import oracle as O
-        threads = min(16, os.cpu_count() or 1)
+        threads = usable_cores()
+        # the multithreaded baselines (direction-optimising BFS, lock-free union-find WCC,
+        # delta-stepping SSSP; CDLP and LCC are OpenMP over vertices) on every usable core
         t1 = time.perf_counter()
         if alg == "bfs":
-            ref, cores = O.bfs(csr, src), 1
+            base = O.bfs_par(csr, src, not directed, nthreads=threads)
         elif alg == "wcc":
-            ref, cores = O.wcc(csr), 1
+            base = O.wcc_par(csr, nthreads=threads)
         elif alg == "sssp":
-            ref, cores = O.sssp(csr, src), 1
+            base = O.sssp_par(csr, src, 0.0, nthreads=threads)
         elif alg == "cdlp":
-            ref, cores = O.cdlp(csr, directed, iters, nthreads=threads), threads
+            base = O.cdlp(csr, directed, iters, nthreads=threads)
         else:
-            ref, cores = O.lcc(csr, directed, nthreads=threads), threads
+            base = O.lcc(csr, directed, nthreads=threads)
         t_cpu = time.perf_counter() - t1
-        cpu = {"value": work / t_cpu, "unit": unit, "cores": cores, "kind": "port",
-               "sample": f"one full {alg} run on the same {gname} graph (oracle/gx_oracle.c), {t_cpu:.2f} s",
-               **host_cpu()}
+        cpu = {"value": work / t_cpu, "unit": unit, "cores": threads, "kind": "port",
+               "sample": f"one full {alg} run on the same {gname} graph (oracle/gx_oracle.c, {threads} threads), "
+                         f"{t_cpu:.2f} s", **host_cpu()}
+        # parity against the serial checker (the *_par baselines equal it bitwise, tests)
+        ref = {"bfs": lambda: O.bfs(csr, src), "wcc": lambda: O.wcc(csr), "sssp": lambda: O.sssp(csr, src)}.get(
+            alg, lambda: base)()
         parity = "bit-exact" if np.array_equal(out, ref) else f"MISMATCH ({int((out != ref).sum())} vertices)"
     line = {
         "metric": METRIC, "value": work / t_dev, "unit": unit, "n_gpus": 1, "steps": args.steps,
@@ -268,8 +300,9 @@ def pmc_traffic(workload: str):
         return None
     try:
         d = json.loads(p.read_text())
-        if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
+        for e in d.get("entries", [d]):
+            if e.get("workload") == workload:
+                return e.get("hbm_bytes_per_launch")
     except Exception:
         return None
     return None
@@ -351,7 +384,7 @@ def run_algorithm_distributed(args):
     parity = None
     if rank == 0 and not args.no_cpu_baseline:
         from oracle import oracle as O
-        threads = min(16, os.cpu_count() or 1)
+        threads = usable_cores()
         ref = {"bfs": lambda: O.bfs(csr, src), "wcc": lambda: O.wcc(csr), "sssp": lambda: O.sssp(csr, src),
                "cdlp": lambda: O.cdlp(csr, directed, args.iters, nthreads=threads),
                "lcc": lambda: O.lcc(csr, directed, nthreads=threads)}[alg]()
@@ -377,49 +410,26 @@ def run_algorithm_distributed(args):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
+def pr_workload(gname: str) -> str:
+    P = PRESETS[gname]
+    return f"PageRank {gname} (R-MAT scale {P['scale']}, ef {P['ef']}, seed {P['seed']}, undirected)"
+
+
+def measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True):
+    """K timed PageRank runs of the partitioned path (gx_pr_part_* + gx_pr_dist_*, which is
+    gx_pagerank's kernel at N = 1) on this rank's share of `csr`; returns the timings, the
+    k_pr_pull_units launch statistics and (rank 0, collect) the scores in csr's vertex order."""
     import torch
-
-    if args.algorithm != "pr":
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1 or args.partitioned:
-            return run_algorithm_distributed(args)
-        return run_algorithm(args)
-    if args.graph and args.graph != "SYN-7_5":
-        P = PRESETS[args.graph]
-        args.scale, args.edgefactor, args.seed = P["scale"], P["ef"], P["seed"]
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    dist = None
-    if world > 1 or "MASTER_ADDR" in os.environ:   # under torch.distributed.run: RCCL, even at N=1
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    device = torch.device("cuda", local_rank)
-    torch.cuda.set_device(device)
-
-    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
-    from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
     from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import Comm, DevicePageRank, GpuStep, \
         PartitionedPageRank, hub_relabel, interleaved_relabel, partition_rows, slice_rows
-
-    gname = args.graph or "SYN-7_5"
-    workload = f"PageRank {gname} (R-MAT scale {args.scale}, ef {args.edgefactor}, seed {args.seed}, undirected)"
-    t_gen = time.time()
-    csr = rmat(args.scale, args.edgefactor, args.seed, undirected=True)
-    t_gen = time.time() - t_gen
     n, nnz = csr.n, csr.nnz
     # GX_PR_PIECES = P > 1: each rank owns P virtual ranks p * N + rank whose all-gathers overlap
     # the next piece's SpMV (default 1: at N = 1 a 1/16 piece ran its SpMV at 0.48x the rate of
-    # a 1/8 one -- tools/pr_dist_n1.sh -- more than the overlap wins back).  Layout: the hub-first order (what gx_pagerank does internally) dealt
-    # round-robin over the N * pieces virtual ranks, so each owns n / (N * pieces) rows AND
-    # ~nnz / (N * pieces) entries and the exchanged vector is ~n long (interleaved_relabel);
-    # GX_PR_PARTITION=ranges keeps the round-1 contiguous hub-first ranges balanced by entries.
+    # a 1/8 one -- tools/pr_dist_n1.sh -- more than the overlap wins back).  Layout: the hub-first
+    # order (what gx_pagerank does internally) dealt round-robin over the N * pieces virtual
+    # ranks, so each owns n / (N * pieces) rows AND ~nnz / (N * pieces) entries and the
+    # exchanged vector is ~n long (interleaved_relabel); GX_PR_PARTITION=ranges keeps the
+    # round-1 contiguous hub-first ranges balanced by entries.
     pieces = max(1, int(os.environ.get("GX_PR_PIECES", "1"))) if dist else 1
     vranks = world * pieces
     partition = os.environ.get("GX_PR_PARTITION", "interleave")
@@ -429,16 +439,11 @@ def main():
     else:
         perm, hub, bounds = interleaved_relabel(csr, vranks)
     lrs = [slice_rows(hub, bounds, p * world + rank) for p in range(pieces)]
-
-    ctx = Context(local_rank)
-    dev_name, cus = ctx.info()
+    del hub
     t_setup = time.perf_counter()
     steppers = [GpuStep(ctx, n, world * pieces, lr, args.damping) for lr in lrs]   # H2D upload + plans
     torch.cuda.synchronize(device)
     t_setup = time.perf_counter() - t_setup
-    # a real (non-null) stream: libgx launches on it and RCCL orders against it
-    stream = torch.cuda.Stream(device)
-    torch.cuda.set_stream(stream)
     # driver "device" (default): libgx enqueues the whole run -- SpMVs and ncclAllGathers on its
     # own RCCL communicator -- and replays it as one hipGraph; "host": one ctypes call and one
     # torch.distributed all-gather per piece and iteration (pr_partition.PartitionedPageRank)
@@ -517,49 +522,139 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    result = None
+    if collect:
+        # result of the last step (parity check on rank 0), assembled by virtual rank
+        if driver == "device":
+            mine = list(zip([lr.rank for lr in lrs], dpr.scores([lr.rows for lr in lrs])))
+        else:
+            mine = [(lr.rank, o[:lr.rows].detach().cpu().numpy()) for lr, o in zip(lrs, pr.rank_outs)]
+        if dist:
+            parts = [None] * world
+            dist.all_gather_object(parts, mine)
+            mine = [t for part in parts for t in part]
+        result = np.concatenate([a for _, a in sorted(mine, key=lambda t: t[0])])[perm]   # generator's order
+    # roofline of k_pr_pull_units on this rank (per launch, averaged over the pieces)
+    bytes_per_launch = sum(4 * lr.nnz + 8 * (lr.rows + 1) + 8 * lr.rows + 8 * lr.rows for lr in lrs) / len(lrs)
+    mean_launch_s = (pull_ms / launches) / 1e3 if launches else float("nan")
+    out = dict(elapsed=elapsed, t_setup=t_setup, t_first=t_first, launches=launches, mean_launch_s=mean_launch_s,
+               bytes_per_launch=bytes_per_launch, achieved=bytes_per_launch / mean_launch_s / 1e9,
+               driver=driver, use_graph=use_graph, pieces=pieces, vranks=vranks, partition=partition,
+               events_in_timed=events_in_timed, exchanged=steppers[0].chunk * vranks / n, result=result)
+    if dpr is not None:
+        dpr.close()
+    if comm is not None:
+        comm.close()
+    for st in steppers:
+        st.close()
+    torch.cuda.synchronize(device)
+    torch.cuda.empty_cache()
+    return out
 
-    # result of the last step (for the parity check on rank 0), assembled by virtual rank
-    if driver == "device":
-        mine = list(zip([lr.rank for lr in lrs], dpr.scores([lr.rows for lr in lrs])))
-    else:
-        mine = [(lr.rank, o[:lr.rows].detach().cpu().numpy()) for lr, o in zip(lrs, pr.rank_outs)]
-    if dist:
-        parts = [None] * world
-        dist.all_gather_object(parts, mine)
-        mine = [t for part in parts for t in part]
-    result = np.concatenate([a for _, a in sorted(mine, key=lambda t: t[0])])
-    result = result[perm]   # back to the generator's vertex order
 
+def exe_path_pr(csr, args, ctx):
+    """The Graphalytics processing time of bin/exe/pr (exe/common.cpp): the markers bracket
+    gx_graph_create (H2D upload) and one gx_pagerank call, whose first call on a graph also
+    builds the hub-first pull plan (pr.cpp:77-79 brackets LAGraph_New .. LAGr_PageRankGX, with
+    LAGraph_Cached_OutDegree / _AT inside).  A second call shows the warm cost of the API."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    t0 = time.perf_counter()
+    G = A.Graph(ctx, csr, False)
+    t_up = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    r = A.LA_PR(G, args.damping, args.iters)
+    t_call = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    A.LA_PR(G, args.damping, args.iters)
+    t_warm = time.perf_counter() - t0
+    G.close()
+    return dict(upload_ms=t_up * 1e3, first_call_ms=t_call * 1e3, warm_call_ms=t_warm * 1e3,
+                processing_ms=(t_up + t_call) * 1e3), r
+
+
+def main():
+    args = parse()
+    import torch
+
+    if args.algorithm != "pr":
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1 or args.partitioned:
+            return run_algorithm_distributed(args)
+        return run_algorithm(args)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    dist = None
+    if world > 1 or "MASTER_ADDR" in os.environ:   # under torch.distributed.run: RCCL, even at N=1
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
+
+    gname = args.graph or DEFAULT_GRAPH["pr"]
+    P = PRESETS[gname]
+    workload = pr_workload(gname)
+    t_gen = time.time()
+    csr = rmat(P["scale"], P["ef"], P["seed"], undirected=True)
+    t_gen = time.time() - t_gen
+    n, nnz = csr.n, csr.nnz
+
+    ctx = Context(local_rank)
+    dev_name, cus = ctx.info()
+    # a real (non-null) stream: libgx launches on it and RCCL orders against it
+    stream = torch.cuda.Stream(device)
+    torch.cuda.set_stream(stream)
+    m = measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True)
+    elapsed = m["elapsed"]
     edges_total = nnz * args.iters * args.steps
     value = edges_total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
-
-    # roofline of k_pr_pull on this rank (per launch, averaged over the pieces)
-    bytes_per_launch = sum(4 * lr.nnz + 8 * (lr.rows + 1) + 8 * lr.rows + 8 * lr.rows for lr in lrs) / len(lrs)
-    mean_launch_s = (pull_ms / launches) / 1e3 if launches else float("nan")
-    achieved = bytes_per_launch / mean_launch_s / 1e9
     traffic = pmc_traffic(workload) if world == 1 else None
     copy_gbs = stream_copy_gbs(device) if rank == 0 else None
-    proc_ms = (t_setup + t_first) * 1e3
 
+    exe = None
+    secondary = None
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import oracle as O
-        threads = min(16, os.cpu_count() or 1)
-        # bounded sample: whole PageRank runs on the same graph until the budget is spent
-        runs, t_cpu, ref = 0, 0.0, None
-        while runs == 0 or (t_cpu < args.cpu_seconds and runs < 200):
-            t1 = time.perf_counter()
-            ref = O.pagerank(csr, False, args.damping, args.iters, nthreads=threads)
-            t_cpu += time.perf_counter() - t1
-            runs += 1
-        cpu = {"value": nnz * args.iters * runs / t_cpu, "unit": "edges/s", "cores": threads, "kind": "port",
-               "sample": f"{runs} full PageRank run(s) ({args.iters} iterations) on the same {gname} graph, "
-                         f"OpenMP pull restatement (oracle/gx_oracle.c), {t_cpu:.2f} s", **host_cpu()}
-        parity = float(np.max(np.abs(result - ref) / np.abs(ref)))
+    if rank == 0 and world == 1:
+        exe, exe_r = exe_path_pr(csr, args, ctx)
+        if not args.no_cpu_baseline:
+            from oracle import oracle as O
+            threads = usable_cores()
+            # bounded sample: whole PageRank runs on the same graph until the budget is spent
+            runs, t_cpu, ref = 0, 0.0, None
+            while runs == 0 or (t_cpu < args.cpu_seconds and runs < 200):
+                t1 = time.perf_counter()
+                ref = O.pagerank(csr, False, args.damping, args.iters, nthreads=threads)
+                t_cpu += time.perf_counter() - t1
+                runs += 1
+            cpu = {"value": nnz * args.iters * runs / t_cpu, "unit": "edges/s", "cores": threads, "kind": "port",
+                   "sample": f"{runs} full PageRank run(s) ({args.iters} iterations) on the same {gname} graph, "
+                             f"OpenMP pull restatement (oracle/gx_oracle.c) on {threads} threads, {t_cpu:.2f} s",
+                   **host_cpu()}
+            parity = float(np.max(np.abs(m["result"] - ref) / np.abs(ref)))
+            exe["parity_max_rel_err_vs_oracle"] = float(np.max(np.abs(exe_r - ref) / np.abs(ref)))
+        if not args.no_secondary and gname != "SYN-7_5":
+            # configs[1]'s graph (datagen-7_5-fb stand-in), same measurement, no CPU leg
+            S = PRESETS["SYN-7_5"]
+            csr2 = rmat(S["scale"], S["ef"], S["seed"], undirected=True)
+            m2 = measure_pr(csr2, args, ctx, device, stream, 1, 0, None, collect=False)
+            secondary = {"workload": pr_workload("SYN-7_5"), "n": csr2.n, "nnz": csr2.nnz,
+                         "value": csr2.nnz * args.iters * args.steps / m2["elapsed"],
+                         "ms_per_step": m2["elapsed"] * 1e3 / args.steps,
+                         "mean_launch_us": m2["mean_launch_s"] * 1e6, "bytes_per_launch": m2["bytes_per_launch"],
+                         "roofline_frac": m2["achieved"] / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic(pr_workload("SYN-7_5"))}
 
     if rank == 0:
+        achieved = m["achieved"]
         line = {
             "metric": METRIC,
             "value": value,
@@ -572,7 +667,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic (seeded R-MAT stand-in for {PRESETS[gname]['stands_for']}; no network for the real dataset)",
+            "data": f"synthetic (seeded R-MAT stand-in for {P['stands_for']}; no network for the real dataset)",
             "config": {
                 "workload": workload,
                 "algorithm": "pagerank",
@@ -581,11 +676,12 @@ def main():
                 "nnz": nnz,
                 "iterations": args.iters,
                 "damping": args.damping,
-                "parallelism": f"row{world}" + (f", {pieces} pipelined pieces" if pieces > 1 else ""),
-                "partition": (partition + " over " + str(vranks) + " virtual ranks") if vranks > 1 else "one rank",
-                "exchanged_doubles_per_n": steppers[0].chunk * vranks / n,
-                "driver": driver + (", hipGraph" if driver == "device" and use_graph else ""),
-                "roofline_events": "timed steps" if events_in_timed else "instrumented pass after the timed steps",
+                "parallelism": f"row{world}" + (f", {m['pieces']} pipelined pieces" if m["pieces"] > 1 else ""),
+                "partition": (m["partition"] + " over " + str(m["vranks"]) + " virtual ranks") if m["vranks"] > 1
+                else "one rank",
+                "exchanged_doubles_per_n": m["exchanged"],
+                "driver": m["driver"] + (", hipGraph" if m["driver"] == "device" and m["use_graph"] else ""),
+                "roofline_events": "timed steps" if m["events_in_timed"] else "instrumented pass after the timed steps",
                 "device": dev_name,
                 "cus": cus,
             },
@@ -597,25 +693,23 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "bytes_per_launch": bytes_per_launch,
-                "mean_launch_us": mean_launch_s * 1e6,
-                "launches": launches,
+                "bytes_per_launch": m["bytes_per_launch"],
+                "mean_launch_us": m["mean_launch_s"] * 1e6,
+                "launches": m["launches"],
                 "stream_copy_gbs": copy_gbs,
                 "frac_of_stream": achieved / copy_gbs if copy_gbs else None,
             },
-            "processing_ms": proc_ms,
-            "evps": (n + nnz // 2) / (proc_ms / 1e3),
+            "processing_ms": exe["processing_ms"] if exe else None,
+            "processing": exe,
+            "evps": (n + nnz // 2) / (exe["processing_ms"] / 1e3) if exe else None,
+            "bench_setup_ms": (m["t_setup"] + m["t_first"]) * 1e3,
             "cpu_baseline": cpu,
+            "speedup_vs_cpu": value / cpu["value"] if cpu else None,
             "parity_max_rel_err_vs_oracle": parity,
+            "secondary": secondary,
             "graph_gen_s": t_gen,
         }
         print(json.dumps(line), flush=True)
-    if dpr is not None:
-        dpr.close()
-    if comm is not None:
-        comm.close()
-    for st in steppers:
-        st.close()
     ctx.close()
     if dist:
         dist.destroy_process_group()

@@ -74,9 +74,11 @@ int gx_device_info(gx_ctx *ctx, char *name, size_t name_len, int *num_cus);
 /* ---- graph I/O (host, no SuiteSparse) --------------------------------------- */
 
 /* Replaces ReadMatrixMarket -> binread (graphio.cpp:10-15, graphio.h:49-285).
- * Reads sparse / hypersparse, CSR or CSC, any GrB type; bool/integer values are
- * treated as structure (iso), FP32/FP64 values become fp64 weights.  Output arrays
- * are allocated by libgx; release with gx_csr_release. */
+ * Reads every kind binread reads (graphio.h:114-117): sparse, hypersparse, bitmap and
+ * full, CSR or CSC, any GrB type; bool/integer values are treated as structure,
+ * FP32/FP64 values become fp64 weights (an iso FP64 matrix -- all weights equal -- gives
+ * every entry that weight).  Output arrays are allocated by libgx; release with
+ * gx_csr_release. */
 int gx_read_grb(const char *path, gx_csr *out);
 /* Replaces binwrite (graphio.h:310-615): writes a SuiteSparse-compatible sparse CSR
  * `.grb` (BOOL iso when vals == NULL, else FP64). */
@@ -139,6 +141,48 @@ int gx_cdlp(gx_graph *g, int iters, uint64_t *labels);
 
 /* LAGraph_lcc(&d, A, symmetric = !directed) (lcc.cpp:61-71). */
 int gx_lcc(gx_graph *g, double *lcc);
+
+/* ---- op-level GraphBLAS entry points (unit parity) ------------------
+ * The operations the reference's LAGraph calls are built from, on the device graph g
+ * (A = its adjacency; the matrix value of an entry is its fp64 weight, 1 when unweighted).
+ * Vectors are dense host arrays of length n with an optional presence byte per entry
+ * (NULL = every entry present); absent entries hold the monoid identity.
+ *   semiring              u / w types          reference use
+ *   GX_PLUS_SECOND_FP64   double / double      GrB_mxv(t, .., plus_second_fp64, AT, w), pr.cpp:61
+ *                                              (LAGr_PageRankGX): mxv with GX_DESC_T0 runs the
+ *                                              PageRank kernel itself
+ *   GX_MIN_SECOND_UINT64  uint64 / uint64      GrB_mxm(S, .., GrB_MIN_SECOND_SEMIRING_UINT64, ..),
+ *                                              LAGraph_cdlp.c:272-281; FastSV (wcc.cpp:61)
+ *   GX_ANY_PAIR_BOOL      (presence) / uint8   BFS frontier vxm (bfs.cpp:80)
+ *   GX_MIN_PLUS_FP64      double / double      SSSP relaxation vxm (sssp.cpp:78)
+ *   GX_PLUS_PAIR_INT64    (presence) / int64   triangle counts (lcc.cpp:68)
+ * gx_mxv: t(i) = (+)_j mult(M(i,j), u(j)) over stored M(i,j) and present u(j), M = A (A' with
+ *         GX_DESC_T0);  gx_vxm: t(j) = (+)_i mult(u(i), A(i,j)) (A' with GX_DESC_T0);
+ *         SECOND(x,y) = y, PLUS(x,y) = x+y, PAIR = 1; t(i) present iff a term exists.  Then
+ *         w<mask> = t, or w (+)= t with GX_DESC_ACCUM (old w present per w_present, or all
+ *         when it is NULL); mask = n structural bytes or NULL, complemented by
+ *         GX_DESC_MASK_COMP; masked-out entries are kept, or cleared by GX_DESC_REPLACE.
+ *         w is read (for the kept / accumulated entries) and written; w_present, if given,
+ *         likewise.  u may be NULL for the PAIR semirings and vxm's SECOND ones.
+ * gx_mxm_masked: C<A> = A (+).(x) A' with GX_PLUS_PAIR_INT64 and desc 0: c[e] for the stored
+ *         entry e = (i, j) of A (in A's entry order, nnz values) is |{k : A(i,k), A(j,k)}|,
+ *         the dot product of rows i and j (rows must not repeat a column).  Other semirings
+ *         and descriptors: GX_NOT_IMPLEMENTED.
+ * ------------------------------------------------------------------------------- */
+#define GX_PLUS_SECOND_FP64 0
+#define GX_MIN_SECOND_UINT64 1
+#define GX_ANY_PAIR_BOOL 2
+#define GX_MIN_PLUS_FP64 3
+#define GX_PLUS_PAIR_INT64 4
+#define GX_DESC_T0 1          /* GrB_INP0 = GrB_TRAN */
+#define GX_DESC_MASK_COMP 2   /* GrB_MASK = GrB_COMP (structural mask) */
+#define GX_DESC_REPLACE 4     /* GrB_OUTP = GrB_REPLACE */
+#define GX_DESC_ACCUM 8       /* accum = the semiring's monoid */
+int gx_mxv(gx_graph *g, int semiring, int desc, const uint8_t *mask, const void *u, const uint8_t *u_present,
+           void *w, uint8_t *w_present);
+int gx_vxm(gx_graph *g, int semiring, int desc, const uint8_t *mask, const void *u, const uint8_t *u_present,
+           void *w, uint8_t *w_present);
+int gx_mxm_masked(gx_graph *g, int semiring, int desc, int64_t *c);
 
 /* ---- timing ---------------------------------------------------------------------
  * Kernel-level timing with hipEvents on the stream the kernels run on.  When enabled,

@@ -65,6 +65,9 @@ SIGNATURES = [
     ("gx_wcc", C.c_int, [_P, _U64P]),
     ("gx_cdlp", C.c_int, [_P, C.c_int, _U64P]),
     ("gx_lcc", C.c_int, [_P, _DP]),
+    ("gx_mxv", C.c_int, [_P, C.c_int, C.c_int, _P, _P, _P, _P, _P]),
+    ("gx_vxm", C.c_int, [_P, C.c_int, C.c_int, _P, _P, _P, _P, _P]),
+    ("gx_mxm_masked", C.c_int, [_P, C.c_int, C.c_int, _I64P]),
     ("gx_set_kernel_timing", C.c_int, [_P, C.c_int]),
     ("gx_kernel_stats", C.c_int, [_P, C.c_char_p, _U64P, _DP]),
     ("gx_reset_kernel_stats", C.c_int, [_P]),

@@ -141,6 +141,45 @@ def LA_LCC(G: Graph) -> np.ndarray:
 
 # ----------------------------------------------------------------- serialisers
 
+# ---- op-level GraphBLAS calls (include/gx.h gx_mxv / gx_vxm / gx_mxm_masked) ----
+PLUS_SECOND_FP64, MIN_SECOND_UINT64, ANY_PAIR_BOOL, MIN_PLUS_FP64, PLUS_PAIR_INT64 = range(5)
+DESC_T0, DESC_MASK_COMP, DESC_REPLACE, DESC_ACCUM = 1, 2, 4, 8
+_OUT_DTYPE = {PLUS_SECOND_FP64: np.float64, MIN_SECOND_UINT64: np.uint64, ANY_PAIR_BOOL: np.uint8,
+              MIN_PLUS_FP64: np.float64, PLUS_PAIR_INT64: np.int64}
+
+
+def _vp(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _op_vector(fn: str, G: Graph, semiring: int, u, u_present, mask, desc, w, w_present):
+    out = np.array(w, dtype=_OUT_DTYPE[semiring], copy=True) if w is not None else \
+        np.zeros(G.n, dtype=_OUT_DTYPE[semiring])
+    outp = None if w_present is None else np.array(w_present, dtype=np.uint8, copy=True)
+    uu = None if u is None else np.ascontiguousarray(u)
+    up = None if u_present is None else np.ascontiguousarray(u_present, dtype=np.uint8)
+    mk = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+    N.check(getattr(N.lib(), fn)(G.handle, semiring, desc, _vp(mk), _vp(uu), _vp(up), _vp(out), _vp(outp)), fn)
+    return out, outp
+
+
+def mxv(G: Graph, semiring: int, u=None, u_present=None, mask=None, desc: int = 0, w=None, w_present=None):
+    """gx_mxv: w<mask> (+)= A (+).(x) u  (GrB_mxv; A' with DESC_T0).  Returns (w, w_present)."""
+    return _op_vector("gx_mxv", G, semiring, u, u_present, mask, desc, w, w_present)
+
+
+def vxm(G: Graph, semiring: int, u=None, u_present=None, mask=None, desc: int = 0, w=None, w_present=None):
+    """gx_vxm: w<mask> (+)= u (+).(x) A  (GrB_vxm; A' with DESC_T0).  Returns (w, w_present)."""
+    return _op_vector("gx_vxm", G, semiring, u, u_present, mask, desc, w, w_present)
+
+
+def mxm_masked(G: Graph, semiring: int = PLUS_PAIR_INT64, desc: int = 0) -> np.ndarray:
+    """gx_mxm_masked: C<A> = A (+).(x) A' with PLUS_PAIR, one int64 per stored entry of A."""
+    c = np.zeros(max(G.nnz, 1), dtype=np.int64)
+    N.check(N.lib().gx_mxm_masked(G.handle, semiring, desc, N.as_i64p(c)), "gx_mxm_masked")
+    return c[:G.nnz]
+
+
 def _fmt_double(x: float) -> str:
     return "%.16e" % x   # ostream precision(16) + scientific (pr.cpp:26-27)
 

@@ -440,8 +440,10 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         // The first batch is the number of steps the last BFS on this graph took (a repeated
         // or nearby source needs the same: SYN-g500-22 8), else kFirst; when it was enough,
         // the host waits for it and queues nothing more.
-        constexpr int kFirst = 6, kBatch = 2;
-        const int first = g->bfs_steps_hint > 0 ? g->bfs_steps_hint : kFirst;
+        // The hint is capped (kMaxFirst): after a deep BFS (a long chain) a shallow one would
+        // otherwise queue thousands of idle levels at ~20 us each.
+        constexpr int kFirst = 6, kBatch = 2, kMaxFirst = 24;
+        const int first = g->bfs_steps_hint > 0 ? std::min(g->bfs_steps_hint, kMaxFirst) : kFirst;
         // h_done[0..2] = depth, mode, done of the state (one copy)
         auto read_state = [&]() -> int {
             GX_HIP_TRY(hipMemcpyAsync(h_done, &st.p->depth, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));

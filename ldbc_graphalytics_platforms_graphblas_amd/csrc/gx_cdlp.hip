@@ -1786,8 +1786,11 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                 GX_TRY(check_launch("k_cdlp_gather_i32"));
             }
         } else {
-            // iteration 0: labels are the caller's vertex ids
-            GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0, nullptr, kFlagShards, st));
+            // iteration 0: labels are the caller's vertex ids.  The smallest-neighbour shortcut
+            // (`first`) assumes no row repeats a column; k_rows_sorted found the caller's rows
+            // strictly ascending, i.e. duplicate-free (else the counting path runs).
+            GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0 && C->rows_sorted, nullptr,
+                                  kFlagShards, st));
         }
         hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(kWave), 0, s, changed, kFlagShards,
                            active && it >= 2 ? C->dense.p : nullptr, dflag + it);

@@ -298,6 +298,9 @@ __device__ __forceinline__ int64_t slab_row_of(const int64_t *__restrict__ rp, c
 }
 
 typedef int gx_v4i __attribute__((ext_vector_type(4)));
+// four dwords loaded by one 16-B load from an address that is only 4-B aligned (a CSR offset):
+// the type says so, and gfx950 still emits one global_load_dwordx4
+typedef uint32_t gx_u32x4 __attribute__((ext_vector_type(4), aligned(4)));
 
 // 16-byte non-temporal load (read-once streams: keep L2 for the gathered vectors).
 __device__ __forceinline__ int4 load_nt(const int4 *p) {
@@ -329,6 +332,7 @@ namespace gx {
 hipError_t warm_bfs(hipStream_t s);
 hipError_t warm_cdlp(hipStream_t s);
 hipError_t warm_lcc(hipStream_t s);
+hipError_t warm_ops(hipStream_t s);
 hipError_t warm_part(hipStream_t s);
 hipError_t warm_pr(hipStream_t s);
 hipError_t warm_pr_hub(hipStream_t s);

@@ -13,6 +13,8 @@
 //   int32  typecode   0 BOOL ... 8 UINT64, 9 FP32, 10 FP64
 //   size_t typesize
 //   then Ap[nvec+1], [Ah[nvec]], Ai[nvals] (uint64), Ax[iso ? 1 : nvals] (typesize each)
+//   (bitmap: Ab[nrows*ncols] int8 presence bytes, then Ax[iso ? 1 : nrows*ncols];
+//    full: Ax[iso ? 1 : nrows*ncols] only -- graphio.h:175-186, 211-216)
 #include <algorithm>
 #include <cctype>
 #include <cinttypes>
@@ -133,47 +135,74 @@ extern "C" int gx_read_grb(const char *path, gx_csr *out) {
         iso = true;
         kind -= 100;
     }
+    // kinds as binread decodes them (graphio.h:114-117): 1 hyper, 0/2 sparse, 4 bitmap, 8 full
     const bool is_hyper = kind == 1;
     const bool is_sparse = kind == 0 || kind == 2;
-    if (!is_hyper && !is_sparse)
-        return fail(GX_NOT_IMPLEMENTED, "bitmap/full .grb matrices are not supported");
+    const bool is_bitmap = kind == 4;
+    const bool is_full = kind == 8;
+    if (!is_hyper && !is_sparse && !is_bitmap && !is_full)
+        return fail(GX_NOT_IMPLEMENTED, "unknown .grb matrix kind");
     if (typecode < 0 || typecode > 10 || typesize == 0 || typesize > 16)
         return fail(GX_NOT_IMPLEMENTED, "unsupported .grb value type");
     if (fmt != 0 && fmt != 1) return fail(GX_INVALID_VALUE, "bad .grb format field");
     if (nrows != ncols) return fail(GX_INVALID_VALUE, "adjacency matrix must be square");
     const uint64_t nmajor = fmt == 0 ? nrows : ncols;
-    if (is_sparse && nvec != nmajor) nvec = nmajor;   // sparse: nvec = vdim
+    const uint64_t nminor = fmt == 0 ? ncols : nrows;
+    // Weighted iff the values are floating point (relabel.py:11-16 writes FP64 for weighted
+    // graphs and BOOL iso for unweighted ones).  An iso FP32/FP64 matrix -- SuiteSparse stores
+    // one when every weight is equal -- is weighted too, each entry carrying the one value.
+    const bool weighted = typecode == 9 || typecode == 10;
 
-    std::vector<uint64_t> Ap(nvec + 1), Ah(is_hyper ? nvec : 0), Ai(nvals);
-    if (!read_n(fp, Ap.data(), nvec + 1)) return fail(GX_IO_ERROR, "truncated Ap");
-    if (is_hyper && !read_n(fp, Ah.data(), nvec)) return fail(GX_IO_ERROR, "truncated Ah");
-    if (!read_n(fp, Ai.data(), nvals)) return fail(GX_IO_ERROR, "truncated Ai");
-    const uint64_t nx = iso ? 1 : nvals;
-    std::vector<unsigned char> Ax(nx * typesize);
-    if (!read_n(fp, Ax.data(), Ax.size())) return fail(GX_IO_ERROR, "truncated Ax");
-    if (Ap[0] != 0 || Ap[nvec] != nvals) return fail(GX_INVALID_VALUE, "corrupt Ap");
-    for (uint64_t k = 0; k < nvals; k++)
-        if (Ai[k] >= nrows) return fail(GX_INVALID_INDEX, "column index out of range");
-
-    // Weighted iff the values are floating point and not iso (relabel.py:11-16 writes
-    // FP64 for weighted graphs and BOOL iso for unweighted ones).
-    const bool weighted = (typecode == 9 || typecode == 10) && !iso;
-
-    // Expand the (hyper)sparse major dimension to a full pointer array.
-    std::vector<uint64_t> P(nmajor + 1, 0);
-    if (is_hyper) {
-        for (uint64_t k = 0; k < nvec; k++) {
-            if (Ah[k] >= nmajor) return fail(GX_INVALID_INDEX, "hyper index out of range");
-            P[Ah[k] + 1] = Ap[k + 1] - Ap[k];
-        }
-        for (uint64_t i = 0; i < nmajor; i++) P[i + 1] += P[i];
-    } else {
-        P.assign(Ap.begin(), Ap.end());
-    }
+    // The major dimension as a full pointer array P, the minor index of every entry in Ai and,
+    // for weighted graphs, its value in X.
+    std::vector<uint64_t> P(nmajor + 1, 0), Ai;
     std::vector<double> X;
-    if (weighted) {
-        X.resize(nvals);
-        for (uint64_t k = 0; k < nvals; k++) X[k] = value_as_double(&Ax[k * typesize], typecode);
+    if (is_hyper || is_sparse) {
+        if (is_sparse && nvec != nmajor) nvec = nmajor;   // sparse: nvec = vdim
+        std::vector<uint64_t> Ap(nvec + 1), Ah(is_hyper ? nvec : 0);
+        Ai.resize(nvals);
+        if (!read_n(fp, Ap.data(), nvec + 1)) return fail(GX_IO_ERROR, "truncated Ap");
+        if (is_hyper && !read_n(fp, Ah.data(), nvec)) return fail(GX_IO_ERROR, "truncated Ah");
+        if (!read_n(fp, Ai.data(), nvals)) return fail(GX_IO_ERROR, "truncated Ai");
+        const uint64_t nx = iso ? 1 : nvals;
+        std::vector<unsigned char> Ax(nx * typesize);
+        if (!read_n(fp, Ax.data(), Ax.size())) return fail(GX_IO_ERROR, "truncated Ax");
+        if (Ap[0] != 0 || Ap[nvec] != nvals) return fail(GX_INVALID_VALUE, "corrupt Ap");
+        for (uint64_t k = 0; k < nvals; k++)
+            if (Ai[k] >= nminor) return fail(GX_INVALID_INDEX, "column index out of range");
+        if (is_hyper) {
+            for (uint64_t k = 0; k < nvec; k++) {
+                if (Ah[k] >= nmajor) return fail(GX_INVALID_INDEX, "hyper index out of range");
+                P[Ah[k] + 1] = Ap[k + 1] - Ap[k];
+            }
+            for (uint64_t i = 0; i < nmajor; i++) P[i + 1] += P[i];
+        } else {
+            P.assign(Ap.begin(), Ap.end());
+        }
+        if (weighted) {
+            X.resize(nvals);
+            for (uint64_t k = 0; k < nvals; k++) X[k] = value_as_double(&Ax[(iso ? 0 : k) * typesize], typecode);
+        }
+    } else {
+        // bitmap / full (graphio.h:175-186, 211-216): nrows*ncols cells in major order, a
+        // presence byte per cell for bitmap (full: every cell present), then the values.
+        if (nrows > (1ull << 20)) return fail(GX_NOT_IMPLEMENTED, "dense .grb kind too large for a graph");
+        const uint64_t cells = nrows * ncols;
+        std::vector<int8_t> Ab(is_bitmap ? cells : 0);
+        if (is_bitmap && !read_n(fp, Ab.data(), cells)) return fail(GX_IO_ERROR, "truncated Ab");
+        const uint64_t nx = iso ? 1 : cells;
+        std::vector<unsigned char> Ax(nx * typesize);
+        if (!read_n(fp, Ax.data(), Ax.size())) return fail(GX_IO_ERROR, "truncated Ax");
+        for (uint64_t m = 0; m < nmajor; m++) {
+            for (uint64_t j = 0; j < nminor; j++) {
+                const uint64_t cell = m * nminor + j;
+                if (is_bitmap && !Ab[cell]) continue;
+                Ai.push_back(j);
+                if (weighted) X.push_back(value_as_double(&Ax[(iso ? 0 : cell) * typesize], typecode));
+            }
+            P[m + 1] = Ai.size();
+        }
+        nvals = Ai.size();
     }
 
     out->n = nrows;
@@ -187,8 +216,8 @@ extern "C" int gx_read_grb(const char *path, gx_csr *out) {
     }
     if (fmt == 0) {
         std::memcpy(out->rowptr, P.data(), (nrows + 1) * sizeof(uint64_t));
-        std::memcpy(out->colidx, Ai.data(), nvals * sizeof(uint64_t));
-        if (weighted) std::memcpy(out->vals, X.data(), nvals * sizeof(double));
+        if (nvals) std::memcpy(out->colidx, Ai.data(), nvals * sizeof(uint64_t));
+        if (weighted && nvals) std::memcpy(out->vals, X.data(), nvals * sizeof(double));
         // SuiteSparse may leave rows jumbled; sort every row (values follow).
         #pragma omp parallel for schedule(dynamic, 1024)
         for (int64_t i = 0; i < (int64_t)nrows; i++) {

@@ -175,6 +175,9 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
 int pr_dangling(PrPart *p, double *x_local, hipStream_t s);
 
 int pr_init(PrPart *p, double *x_local, hipStream_t s);
+// gx_pagerank's single-rank plan of a graph: its pull matrix (A' when directed, which must be
+// built) relabelled hub-first, column-sorted blocks, x buffers and the hub-first perm.
+int pr_single_plan(gx_graph *g, PrPart **out);
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 
 }  // namespace gx

@@ -515,7 +515,9 @@ void hub_order(const std::vector<int32_t> &outdeg, std::vector<int32_t> &order, 
     }
 }
 
-int pr_single_plan(gx_graph *g, PrPart **out) {
+}  // namespace
+
+int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     const uint64_t n = g->n;
     gx_ctx *ctx = g->ctx;
     hipStream_t s = ctx->stream;
@@ -578,8 +580,6 @@ int pr_single_plan(gx_graph *g, PrPart **out) {
     *out = p;
     return GX_SUCCESS;
 }
-
-}  // namespace
 
 extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank) {
     if (!g || !rank) return fail(GX_NULL_POINTER, "gx_pagerank: null argument");

@@ -207,7 +207,11 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // of round R; lane l holds entries 4l .. 4l+3 of each, all in 64-entry group l / 16 of the
 // supergroup.  The four group bases are scalar loads issued with the index loads and selected
 // per lane when the round is computed (a select right after the loads waited for them).
-template <int BS, int U, bool PIPE, bool X4 = false, bool P2 = false>
+// PROBE (diagnostic builds only, -DGX_PR_PROBES; wrong results by design): 1 no LDS adds
+// (register sum), 2 no gathers, 3 neither, 4 gathers folded into x[c & 4095] (L1 hits),
+// 5 no gathers + conflict-free LDS adds (acc[tid]), 6 gathers + conflict-free LDS adds,
+// 7 no index loads (entries synthesised from the position).
+template <int BS, int U, bool PIPE, bool X4 = false, bool P2 = false, int PROBE = 0>
 __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock &b, int64_t lo, int64_t hi,
                                              double *acc, int64_t step = (int64_t)U * BS) {
     const int tid = threadIdx.x;
@@ -236,7 +240,14 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
 #pragma unroll
             for (int v = 0; v < V; v++) {
                 const int64_t sg = R + (int64_t)(wave * V + v) * 256;
-                d.q[v] = *reinterpret_cast<const uint4 *>(a.spk + min(sg + 4 * lane, z1 - 1));
+                if constexpr (PROBE == 7) {
+                    const uint32_t e0 = (uint32_t)(sg + 4 * lane - z0);
+                    d.q[v] = make_uint4(((e0 >> 4) << kRowBits) | (e0 & 4095u), (((e0 + 1) >> 4) << kRowBits) | ((e0 + 1) & 4095u),
+                                        (((e0 + 2) >> 4) << kRowBits) | ((e0 + 2) & 4095u), (((e0 + 3) >> 4) << kRowBits) | ((e0 + 3) & 4095u));
+                } else {
+                    const gx_u32x4 q4 = *reinterpret_cast<const gx_u32x4 *>(a.spk + min(sg + 4 * lane, z1 - 1));
+                    d.q[v] = make_uint4(q4.x, q4.y, q4.z, q4.w);
+                }
                 const int g = __builtin_amdgcn_readfirstlane((int)(b.seg + min((sg - z0) >> 6, glast)));
 #pragma unroll
                 for (int k = 0; k < 4; k++) d.gbs[v][k] = __builtin_amdgcn_readfirstlane(a.gbase[g + k]);
@@ -259,7 +270,7 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
                 }
                 esc |= gb[v];
             }
-            if (__builtin_amdgcn_readfirstlane(__ballot(esc & 0x80000000u) != 0)) {
+            if (PROBE != 7 && __builtin_amdgcn_readfirstlane(__ballot(esc & 0x80000000u) != 0)) {
 #pragma unroll
                 for (int v = 0; v < V; v++)
 #pragma unroll
@@ -270,11 +281,20 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
                     }
             }
 #pragma unroll
-            for (int i = 0; i < U; i++) t.g[i] = a.x_in[c[i]];
+            for (int i = 0; i < U; i++) {
+                if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5) t.g[i] = (double)c[i];
+                else if constexpr (PROBE == 4) t.g[i] = a.x_in[c[i] & 4095];
+                else t.g[i] = a.x_in[c[i]];
+            }
         };
+        double rsum = 0.0;   // PROBE 1 / 3
         auto add = [&](const Gt &t) {
 #pragma unroll
-            for (int i = 0; i < U; i++) atomicAdd(&acc[t.r[i]], t.ok[i] ? t.g[i] : 0.0);
+            for (int i = 0; i < U; i++) {
+                if constexpr (PROBE == 1 || PROBE == 3) rsum += t.ok[i] ? t.g[i] : 0.0;
+                else if constexpr (PROBE == 5 || PROBE == 6) atomicAdd(&acc[tid], t.ok[i] ? t.g[i] : 0.0);
+                else atomicAdd(&acc[t.r[i]], t.ok[i] ? t.g[i] : 0.0);
+            }
         };
         Rd dA, dB;
         Gt tA, tB;
@@ -301,6 +321,7 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
             add(tB);
             R += step;
         }
+        if constexpr (PROBE == 1 || PROBE == 3) atomicAdd(&acc[tid], rsum);
         return;
     }
     if constexpr (X4) {
@@ -316,7 +337,8 @@ __device__ __forceinline__ void gather_range(const SortedArgs &a, const RowBlock
                 const int64_t sg = R + (int64_t)(wave * V + v) * 256;
                 // clamped into the block; spk's allocation slack covers the 3 entries past z1 - 1
                 // (dword-aligned 16-B loads)
-                q[v] = *reinterpret_cast<const uint4 *>(a.spk + min(sg + 4 * lane, z1 - 1));
+                const gx_u32x4 q4 = *reinterpret_cast<const gx_u32x4 *>(a.spk + min(sg + 4 * lane, z1 - 1));
+                q[v] = make_uint4(q4.x, q4.y, q4.z, q4.w);
                 // readfirstlane is convergent, so the loads cannot sink into the select's
                 // branches.  A supergroup past the block's end (the tail of the last round, or
                 // the prefetch past it) reads the last group's bases; the up to 3 groups past
@@ -473,7 +495,7 @@ __global__ __launch_bounds__(BS) void k_pr_pull_sorted(SortedArgs a) {
 // Workgroups [0, nlong) are the LONG row segments, as in k_pr_pull_sorted, padded to nlong_pad
 // (a multiple of 8, so that grid slot nlong_pad + 8 i + x lands on XCD list x).
 // TIMES: debug build with per-workgroup timestamps (GX_PR_UNIT_TIMES).
-template <int BS, int U, bool TIMES, bool X4 = false, bool P2 = false>
+template <int BS, int U, bool TIMES, bool X4 = false, bool P2 = false, int PROBE = 0>
 __global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? (U >= 16 || P2 ? 4 : 8) : 1)) void k_pr_pull_units(SortedArgs a) {   // 1024: two per CU
     extern __shared__ double acc[];
     __shared__ double wred[BS / kWave];
@@ -506,7 +528,7 @@ __global__ __launch_bounds__(BS, TIMES ? 1 : (BS >= 1024 ? (U >= 16 || P2 ? 4 : 
     const int nrows = b.row_end - b.row_begin;
     for (int i = tid; i < nrows; i += BS) acc[i] = 0.0;
     __syncthreads();
-    gather_range<BS, U, true, X4, P2>(a, b, u.lo, u.hi, acc, u.step);
+    gather_range<BS, U, true, X4, P2, PROBE>(a, b, u.lo, u.hi, acc, u.step);
     __syncthreads();
     if (TIMES && tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
     if (u.nunits > 1) {
@@ -1178,6 +1200,17 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
             case 4: hipLaunchKernelGGL((k_pr_pull_units<1024, 16, false, true>), grid, dim3(1024), lds, s, a); break;
             default:
                 // GX_PR_INDEX_X4=0: one 4-B index load per entry (round 2's kernel)
+#ifdef GX_PR_PROBES
+                if (const char *pe = std::getenv("GX_PR_PROBE")) {
+                    switch (std::atoi(pe)) {
+#define GX_PROBE_CASE(k) case k: hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true, true, k>), grid, dim3(1024), lds, s, a); break;
+                    GX_PROBE_CASE(1) GX_PROBE_CASE(2) GX_PROBE_CASE(3) GX_PROBE_CASE(4) GX_PROBE_CASE(5) GX_PROBE_CASE(6) GX_PROBE_CASE(7)
+#undef GX_PROBE_CASE
+                    default: hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true, true>), grid, dim3(1024), lds, s, a);
+                    }
+                    break;
+                }
+#endif
                 if (p->index_x4 && p->pipe2) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true, true>), grid, dim3(1024), lds, s, a);
                 else if (p->index_x4) hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, true>), grid, dim3(1024), lds, s, a);
                 else hipLaunchKernelGGL((k_pr_pull_units<1024, 8, false, false>), grid, dim3(1024), lds, s, a);

@@ -1157,7 +1157,8 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         // was enough, the remap to the caller's order (hub-first copy) is queued behind it
         // instead of an idle replay, and runs while the host reads the flag.
         GX_TRY(W.capture(B, grid, s));
-        const int hint = W.replays_hint;
+        // capped, so that one long run (a deep chain) cannot queue many idle replays for the next
+        const int hint = std::min(W.replays_hint, 12);
         auto read_state = [&]() -> int {
             GX_HIP_TRY(hipMemcpyAsync(W.h_done, &st.p->round, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
             GX_HIP_TRY(hipEventRecord(W.ev, s));

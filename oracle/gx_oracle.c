@@ -415,3 +415,374 @@ int orc_lcc(int64_t n, const int64_t *rp, const int64_t *ci, int directed, doubl
     free(srp); free(sci); free(oci); free(trp); free(tci);
     return ORC_OK;
 }
+
+/* ====================================================================================
+ * Parallel CPU baselines (bench.py's cpu_baseline leg).  The functions above are the
+ * checkers; these compute the same results with every host core, so that the GPU/CPU ratio
+ * is against a multithreaded CPU implementation like SuiteSparse's (GxB_GLOBAL_NTHREADS =
+ * --threadnum, bfs.cpp:88-89).  Each returns bitwise the result of its serial counterpart
+ * (tests/test_oracle_parallel.py): BFS levels and min-id WCC labels are unique, and SSSP's
+ * relaxation fixed point does not depend on the order (see orc_sssp).
+ * ==================================================================================== */
+
+/* BFS, direction-optimising (Beamer et al.; LAGr_BreadthFirstSearch is push/pull too):
+ * top-down levels claim vertices with a CAS on level[]; when the frontier's out-edges pass
+ * 1/14 of the unexplored edges a level is run bottom-up (only for symmetric graphs, whose
+ * in-edges are the out-edges: the reference never builds A' for BFS, bfs.cpp:76-80). */
+int orc_bfs_par(int64_t n, const int64_t *rp, const int64_t *ci, int64_t src, int symmetric,
+                int64_t *level, int nthreads) {
+    if (src < 0 || src >= n) return ORC_INVALID;
+    orc_set_threads(nthreads);
+    int64_t *front = (int64_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+    int64_t *next = (int64_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+    if (!front || !next) { free(front); free(next); return ORC_OOM; }
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) level[i] = INT64_MAX;
+    level[src] = 0;
+    front[0] = src;
+    int64_t nf = 1, depth = 0;
+    int64_t edges_unexplored = rp[n];
+    int bottom_up = 0;
+    while (nf > 0) {
+        int64_t mf = 0;
+        #pragma omp parallel for reduction(+:mf) schedule(static)
+        for (int64_t i = 0; i < nf; i++) mf += rp[front[i] + 1] - rp[front[i]];
+        edges_unexplored -= mf;
+        if (symmetric && !bottom_up && mf > edges_unexplored / 14) bottom_up = 1;
+        else if (bottom_up && nf < n / 24) bottom_up = 0;
+        int64_t nn = 0;
+        if (bottom_up) {
+            #pragma omp parallel for reduction(+:nn) schedule(dynamic, 1024)
+            for (int64_t v = 0; v < n; v++) {
+                if (level[v] != INT64_MAX) continue;
+                for (int64_t k = rp[v]; k < rp[v + 1]; k++)
+                    if (level[ci[k]] == depth) { level[v] = depth + 1; nn++; break; }
+            }
+            /* the next frontier: vertices just reached (one pass, in vertex order) */
+            int64_t m = 0;
+            for (int64_t v = 0; v < n; v++) if (level[v] == depth + 1) next[m++] = v;
+            nn = m;
+        } else {
+            #pragma omp parallel
+            {
+                int64_t buf[256];
+                int nb = 0;
+                #pragma omp for schedule(dynamic, 64)
+                for (int64_t i = 0; i < nf; i++) {
+                    const int64_t u = front[i];
+                    for (int64_t k = rp[u]; k < rp[u + 1]; k++) {
+                        const int64_t v = ci[k];
+                        if (level[v] == INT64_MAX &&
+                            __sync_bool_compare_and_swap(&level[v], INT64_MAX, depth + 1)) {
+                            buf[nb++] = v;
+                            if (nb == 256) {
+                                const int64_t at = __sync_fetch_and_add(&nn, 256);
+                                memcpy(next + at, buf, sizeof(buf));
+                                nb = 0;
+                            }
+                        }
+                    }
+                }
+                if (nb) {
+                    const int64_t at = __sync_fetch_and_add(&nn, nb);
+                    memcpy(next + at, buf, (size_t)nb * sizeof(int64_t));
+                }
+            }
+        }
+        int64_t *t = front; front = next; next = t;
+        nf = nn;
+        depth++;
+    }
+    free(front); free(next);
+    return ORC_OK;
+}
+
+/* WCC: lock-free union-find (min-root linking by CAS, path halving), every stored edge
+ * joins its endpoints, so directed graphs need no explicit A LOR A' (wcc.cpp:54-55).  Roots
+ * are component minima, so the labels equal orc_wcc's. */
+static int64_t par_find(int64_t *p, int64_t x) {
+    for (;;) {
+        int64_t y = __atomic_load_n(&p[x], __ATOMIC_RELAXED);
+        if (y == x) return x;
+        int64_t z = __atomic_load_n(&p[y], __ATOMIC_RELAXED);
+        if (z != y) __sync_bool_compare_and_swap(&p[x], y, z);   /* halving */
+        x = y;
+    }
+}
+
+int orc_wcc_par(int64_t n, const int64_t *rp, const int64_t *ci, uint64_t *comp, int nthreads) {
+    orc_set_threads(nthreads);
+    int64_t *p = (int64_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+    if (!p) return ORC_OOM;
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) p[i] = i;
+    #pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t u = 0; u < n; u++) {
+        for (int64_t k = rp[u]; k < rp[u + 1]; k++) {
+            int64_t a = u, b = ci[k];
+            for (;;) {
+                a = par_find(p, a);
+                b = par_find(p, b);
+                if (a == b) break;
+                if (a < b) { int64_t t = a; a = b; b = t; }      /* link the larger root */
+                if (__sync_bool_compare_and_swap(&p[a], a, b)) break;
+            }
+        }
+    }
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) comp[i] = (uint64_t)par_find(p, i);
+    free(p);
+    return ORC_OK;
+}
+
+/* SSSP: parallel delta-stepping (Meyer & Sanders; the GAP benchmark's shared-frontier form),
+ * distances as fp64 bit patterns lowered by CAS (non-negative doubles order like their
+ * bits).  Per-thread bins; the smallest non-empty bin of any thread is the next frontier;
+ * a thread keeps processing its own current bin while it stays small (bin fusion).  The
+ * result is the relaxation fixed point, bitwise equal to orc_sssp's Dijkstra. */
+typedef struct { int64_t *v; int64_t len, cap; } orc_vec;
+
+static int vec_push(orc_vec *b, int64_t x) {
+    if (b->len == b->cap) {
+        int64_t nc = b->cap ? 2 * b->cap : 64;
+        int64_t *nv = (int64_t *)realloc(b->v, (size_t)nc * sizeof(int64_t));
+        if (!nv) return 0;
+        b->v = nv;
+        b->cap = nc;
+    }
+    b->v[b->len++] = x;
+    return 1;
+}
+
+static int relax_min(double *dist, int64_t v, double nd) {
+    uint64_t *slot = (uint64_t *)&dist[v];
+    uint64_t old = __atomic_load_n(slot, __ATOMIC_RELAXED);
+    uint64_t nb;
+    memcpy(&nb, &nd, 8);
+    while (nb < old) {
+        if (__atomic_compare_exchange_n(slot, &old, nb, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return 1;
+    }
+    return 0;
+}
+
+int orc_sssp_par(int64_t n, const int64_t *rp, const int64_t *ci, const double *w, int64_t src,
+                 double delta, double *dist, int nthreads) {
+    if (src < 0 || src >= n) return ORC_INVALID;
+    if (!(delta > 0)) return ORC_INVALID;
+    orc_set_threads(nthreads);
+    const int64_t nnz = rp[n];
+    const int64_t kMaxBin = INT64_MAX / 2;
+    int64_t *frontier = (int64_t *)malloc((size_t)(nnz + n + 1) * sizeof(int64_t));
+    if (!frontier) return ORC_OOM;
+    #pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) dist[i] = INFINITY;
+    dist[src] = 0.0;
+    frontier[0] = src;
+    int64_t shared_bin[2] = {0, kMaxBin}, tails[2] = {1, 0};
+    int oom = 0;
+    #pragma omp parallel reduction(|:oom)
+    {
+        orc_vec *bins = NULL;
+        int64_t nbins = 0;
+        int64_t iter = 0;
+        while (__atomic_load_n(&shared_bin[iter & 1], __ATOMIC_ACQUIRE) != kMaxBin) {
+            int64_t *cur_bin = &shared_bin[iter & 1], *next_bin = &shared_bin[(iter + 1) & 1];
+            int64_t *cur_tail = &tails[iter & 1], *next_tail = &tails[(iter + 1) & 1];
+            const int64_t b = *cur_bin;
+            const int64_t ct = *cur_tail;
+            #define ORC_RELAX(u_)                                                              \
+                do {                                                                           \
+                    const int64_t uu = (u_);                                                   \
+                    const double du = dist[uu];                                                \
+                    for (int64_t k = rp[uu]; k < rp[uu + 1]; k++) {                             \
+                        const double nd = du + w[k];                                           \
+                        if (relax_min(dist, ci[k], nd)) {                                      \
+                            const int64_t db = (int64_t)(nd / delta);                          \
+                            if (db >= nbins) {                                                 \
+                                orc_vec *nbs = (orc_vec *)realloc(bins, (size_t)(db + 1) * sizeof(orc_vec)); \
+                                if (!nbs) { oom = 1; break; }                                  \
+                                memset(nbs + nbins, 0, (size_t)(db + 1 - nbins) * sizeof(orc_vec)); \
+                                bins = nbs;                                                    \
+                                nbins = db + 1;                                                \
+                            }                                                                  \
+                            if (!vec_push(&bins[db], ci[k])) { oom = 1; break; }               \
+                        }                                                                      \
+                    }                                                                          \
+                } while (0)
+            #pragma omp for schedule(dynamic, 64) nowait
+            for (int64_t i = 0; i < ct; i++) {
+                const int64_t u = frontier[i];
+                if (dist[u] >= delta * (double)b) ORC_RELAX(u);
+            }
+            /* bin fusion: keep going on this thread's own small current bin */
+            while (b < nbins && bins[b].len > 0 && bins[b].len < 1000) {
+                int64_t len = bins[b].len;
+                int64_t *copy = (int64_t *)malloc((size_t)len * sizeof(int64_t));
+                if (!copy) { oom = 1; break; }
+                memcpy(copy, bins[b].v, (size_t)len * sizeof(int64_t));
+                bins[b].len = 0;
+                for (int64_t i = 0; i < len; i++) ORC_RELAX(copy[i]);
+                free(copy);
+            }
+            #undef ORC_RELAX
+            for (int64_t j = b; j < nbins; j++) {
+                if (bins[j].len > 0) {
+                    int64_t cur = __atomic_load_n(next_bin, __ATOMIC_RELAXED);
+                    while (j < cur && !__atomic_compare_exchange_n(next_bin, &cur, j, 0, __ATOMIC_RELAXED,
+                                                                   __ATOMIC_RELAXED)) {}
+                    break;
+                }
+            }
+            #pragma omp barrier
+            #pragma omp single
+            {
+                *cur_bin = kMaxBin;
+                *cur_tail = 0;
+            }
+            const int64_t nb = __atomic_load_n(next_bin, __ATOMIC_RELAXED);
+            if (nb < nbins && bins[nb].len > 0) {
+                const int64_t at = __atomic_fetch_add(next_tail, bins[nb].len, __ATOMIC_RELAXED);
+                if (at + bins[nb].len <= nnz + n + 1)   /* a bin's pushes never exceed its edges in practice */
+                    memcpy(frontier + at, bins[nb].v, (size_t)bins[nb].len * sizeof(int64_t));
+                else
+                    oom = 1;
+                bins[nb].len = 0;
+            }
+            iter++;
+            #pragma omp barrier
+        }
+        for (int64_t j = 0; j < nbins; j++) free(bins[j].v);
+        free(bins);
+    }
+    free(frontier);
+    return oom ? ORC_OOM : ORC_OK;
+}
+
+/* ====================================================================================
+ * Op-level GraphBLAS restatements, the checkers of gx_mxv / gx_vxm / gx_mxm_masked
+ * (include/gx.h).  The built-in semirings the reference's LAGraph calls use:
+ *   PLUS_SECOND_FP64   GrB_mxv(t, .., LAGraph_plus_second_fp64, AT, w) in LAGr_PageRankGX
+ *                      (pr.cpp:61)
+ *   MIN_SECOND_UINT64  GrB_mxm(S, .., GrB_MIN_SECOND_SEMIRING_UINT64, S, L)
+ *                      (LAGraph_cdlp.c:272-281); FastSV's mxv (LAGr_ConnectedComponents, wcc.cpp:61)
+ *   ANY_PAIR_BOOL      the BFS frontier vxm (LAGr_BreadthFirstSearch, bfs.cpp:80)
+ *   MIN_PLUS_FP64      the SSSP relaxation vxm (LAGr_SingleSourceShortestPath, sssp.cpp:78)
+ *   PLUS_PAIR_INT64    triangle counts, masked mxm (LAGraph_lcc, lcc.cpp:68)
+ * Semantics (GraphBLAS C API 2.0, dense vectors with a presence byte per entry):
+ *   mxv: t(i) = (+)_{j : M(i,j) stored, u(j) present} mult(M(i,j), u(j)),  M = A, or A' with T0
+ *   vxm: t(j) = (+)_{i : A(i,j) stored, u(i) present} mult(u(i), A(i,j)),  A' with T0
+ *   (SECOND(x, y) = y, PLUS(x, y) = x + y, PAIR = 1; the matrix value is the fp64 weight, 1 for
+ *   an unweighted graph); t(i) is present iff some term exists.  Then w<mask> (+)= t:
+ *   where the (structural, optionally complemented) mask is false, w is kept (cleared with
+ *   REPLACE); elsewhere w = t, or w (+) t with ACCUM.  Absent entries hold the monoid identity
+ *   (0, UINT64_MAX, false, +inf, 0).
+ *   mxm_masked: C<A> = A (+).(x) A' with PLUS_PAIR: c(e) for the stored entry e = (i, j) of A
+ *   is |{k : A(i,k) and A(j,k) stored}| (the dot product of rows i and j; rows must not repeat a
+ *   column), in A's entry order.
+ * ==================================================================================== */
+enum { ORC_PLUS_SECOND_FP64 = 0, ORC_MIN_SECOND_UINT64 = 1, ORC_ANY_PAIR_BOOL = 2, ORC_MIN_PLUS_FP64 = 3,
+       ORC_PLUS_PAIR_INT64 = 4 };
+#define ORC_DESC_T0 1
+#define ORC_DESC_MASK_COMP 2
+#define ORC_DESC_REPLACE 4
+#define ORC_DESC_ACCUM 8
+
+int orc_mxv(int64_t n, const int64_t *rp, const int64_t *ci, const double *wt, int sr, int vxm, int desc,
+            const uint8_t *mask, const void *u, const uint8_t *u_present, void *out, uint8_t *out_present) {
+    if (sr < 0 || sr > 4) return ORC_INVALID;
+    const int use_t = (vxm != 0) ^ ((desc & ORC_DESC_T0) != 0);
+    const int64_t *mrp = rp, *mci = ci;
+    const double *mw = wt;
+    int64_t *trp = NULL, *tci = NULL;
+    double *tw = NULL;
+    if (use_t) {
+        int rc = orc_transpose(n, rp, ci, wt, &trp, &tci, wt ? &tw : NULL);
+        if (rc) return rc;
+        mrp = trp; mci = tci; mw = tw;
+    }
+    const double *ud = (const double *)u;
+    const uint64_t *uu = (const uint64_t *)u;
+    for (int64_t i = 0; i < n; i++) {
+        double accd = (sr == ORC_MIN_PLUS_FP64) ? INFINITY : 0.0;
+        uint64_t accu = UINT64_MAX;
+        int64_t acci = 0;
+        int hit = 0;
+        for (int64_t k = mrp[i]; k < mrp[i + 1]; k++) {
+            const int64_t j = mci[k];
+            if (u_present && !u_present[j]) continue;
+            const double a = mw ? mw[k] : 1.0;
+            hit = 1;
+            switch (sr) {
+                case ORC_PLUS_SECOND_FP64: accd += vxm ? a : ud[j]; break;
+                case ORC_MIN_SECOND_UINT64: {
+                    const uint64_t v = vxm ? (uint64_t)a : uu[j];
+                    if (v < accu) accu = v;
+                    break;
+                }
+                case ORC_MIN_PLUS_FP64: {
+                    const double v = vxm ? ud[j] + a : a + ud[j];
+                    if (v < accd) accd = v;
+                    break;
+                }
+                case ORC_PLUS_PAIR_INT64: acci++; break;
+                default: break;   /* ANY_PAIR: the hit itself */
+            }
+        }
+        const int allowed = !mask || ((mask[i] != 0) != ((desc & ORC_DESC_MASK_COMP) != 0));
+        const int old = out_present ? out_present[i] != 0 : 1;
+        int present = hit;
+        if (!allowed) {
+            if (!(desc & ORC_DESC_REPLACE)) continue;
+            present = 0;
+            hit = 0;
+        } else if ((desc & ORC_DESC_ACCUM) && old) {
+            present = 1;
+            if (hit) {
+                switch (sr) {
+                    case ORC_PLUS_SECOND_FP64: accd = ((double *)out)[i] + accd; break;
+                    case ORC_MIN_SECOND_UINT64: if (((uint64_t *)out)[i] < accu) accu = ((uint64_t *)out)[i]; break;
+                    case ORC_MIN_PLUS_FP64: if (((double *)out)[i] < accd) accd = ((double *)out)[i]; break;
+                    case ORC_PLUS_PAIR_INT64: acci += ((int64_t *)out)[i]; break;
+                    default: break;
+                }
+            } else {
+                if (out_present) out_present[i] = 1;
+                continue;   /* w(i) kept */
+            }
+        }
+        if (out_present) out_present[i] = (uint8_t)present;
+        switch (sr) {
+            case ORC_PLUS_SECOND_FP64: ((double *)out)[i] = present ? accd : 0.0; break;
+            case ORC_MIN_SECOND_UINT64: ((uint64_t *)out)[i] = present ? accu : UINT64_MAX; break;
+            case ORC_ANY_PAIR_BOOL: ((uint8_t *)out)[i] = (uint8_t)(present ? 1 : 0); break;
+            case ORC_MIN_PLUS_FP64: ((double *)out)[i] = present ? accd : INFINITY; break;
+            default: ((int64_t *)out)[i] = present ? acci : 0; break;
+        }
+    }
+    free(trp); free(tci); free(tw);
+    return ORC_OK;
+}
+
+int orc_mxm_masked(int64_t n, const int64_t *rp, const int64_t *ci, int sr, int desc, int64_t *c) {
+    if (sr != ORC_PLUS_PAIR_INT64 || desc != 0) return ORC_INVALID;
+    const int64_t nnz = rp[n];
+    int64_t *s = (int64_t *)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(int64_t));
+    if (!s) return ORC_OOM;
+    memcpy(s, ci, (size_t)nnz * sizeof(int64_t));
+    for (int64_t i = 0; i < n; i++) qsort(s + rp[i], (size_t)(rp[i + 1] - rp[i]), sizeof(int64_t), cmp_u64);
+    #pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t i = 0; i < n; i++) {
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            const int64_t j = ci[e];
+            int64_t a = rp[i], b = rp[j], cnt = 0;
+            while (a < rp[i + 1] && b < rp[j + 1]) {
+                if (s[a] < s[b]) a++;
+                else if (s[a] > s[b]) b++;
+                else { cnt++; a++; b++; }
+            }
+            c[e] = cnt;
+        }
+    }
+    free(s);
+    return ORC_OK;
+}

@@ -129,3 +129,54 @@ def test_rmat_deterministic():
         assert (np.diff(row.astype(np.int64)) > 0).all()
     w = rmat(9, 4, 3, weighted=True)
     assert w.vals is not None and (w.vals > 0).all() and (w.vals <= 1).all()
+
+
+def _grb_fields(fmt, kind, n, nvec, nvals, typecode, typesize):
+    return (b"x" * 512 + np.array([fmt, kind], np.int32).tobytes() + np.array([0.0625]).tobytes() +
+            np.array([n, n], np.uint64).tobytes() + np.array([-1], np.int64).tobytes() +
+            np.array([nvec, nvals], np.uint64).tobytes() + np.array([typecode], np.int32).tobytes() +
+            np.array([typesize], np.uint64).tobytes())
+
+
+def test_iso_fp64_grb_is_weighted(tmp_path):
+    """An iso FP64 matrix (SuiteSparse stores one when every weight is equal) keeps its
+    weight on every entry, so SSSP runs on it as the reference's does (graphio.h:191-216)."""
+    from ldbc_graphalytics_platforms_graphblas_amd import graphio
+    # 3x3 CSR sparse iso FP64 (kind 102), entries (0,1) (1,2) (2,0), all weight 2.5
+    raw = (_grb_fields(0, 102, 3, 3, 3, 10, 8) + np.array([0, 1, 2, 3], np.uint64).tobytes() +
+           np.array([1, 2, 0], np.uint64).tobytes() + np.array([2.5]).tobytes())
+    (tmp_path / "iso.grb").write_bytes(raw)
+    csr = graphio.read_grb(tmp_path / "iso.grb")
+    np.testing.assert_array_equal(csr.rowptr, [0, 1, 2, 3])
+    np.testing.assert_array_equal(csr.colidx, [1, 2, 0])
+    np.testing.assert_array_equal(csr.vals, [2.5, 2.5, 2.5])
+    # iso BOOL stays unweighted
+    raw = (_grb_fields(0, 102, 3, 3, 3, 0, 1) + np.array([0, 1, 2, 3], np.uint64).tobytes() +
+           np.array([1, 2, 0], np.uint64).tobytes() + b"\x01")
+    (tmp_path / "b.grb").write_bytes(raw)
+    assert graphio.read_grb(tmp_path / "b.grb").vals is None
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_bitmap_and_full_grb(tmp_path, fmt):
+    """Bitmap (kind 4) and full (kind 8) matrices, by row and by column (graphio.h:175-186,
+    211-216, 250-277): Ab presence bytes then Ax, or Ax alone."""
+    from ldbc_graphalytics_platforms_graphblas_amd import graphio
+    dense = np.array([[0, 1.5, 0], [2.0, 0, 3.0], [0, 0, 4.0]])
+    present = dense != 0
+    cells = dense if fmt == 0 else dense.T   # major order: rows for BY_ROW, columns for BY_COL
+    pres = present if fmt == 0 else present.T
+    raw = (_grb_fields(fmt, 4, 3, 3, int(present.sum()), 10, 8) + pres.astype(np.int8).tobytes() +
+           cells.astype(np.float64).tobytes())
+    (tmp_path / "bm.grb").write_bytes(raw)
+    csr = graphio.read_grb(tmp_path / "bm.grb")
+    np.testing.assert_array_equal(csr.rowptr, [0, 1, 3, 4])
+    np.testing.assert_array_equal(csr.colidx, [1, 0, 2, 2])
+    np.testing.assert_array_equal(csr.vals, [1.5, 2.0, 3.0, 4.0])
+    # full iso BOOL: every cell an edge (self-loops included), unweighted
+    raw = _grb_fields(fmt, 108, 3, 3, 9, 0, 1) + b"\x01"
+    (tmp_path / "full.grb").write_bytes(raw)
+    csr = graphio.read_grb(tmp_path / "full.grb")
+    np.testing.assert_array_equal(csr.rowptr, [0, 3, 6, 9])
+    np.testing.assert_array_equal(csr.colidx, [0, 1, 2] * 3)
+    assert csr.vals is None
