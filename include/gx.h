@@ -264,6 +264,24 @@ int gx_pr_dist_run(gx_pr_dist *dist, int iters, int use_graph, void *stream);
 int gx_pr_dist_scores(gx_pr_dist *dist, int piece, double *scores);
 int gx_pr_dist_free(gx_pr_dist *dist);
 
+/* ---- one process, N GPUs (the executables' GX_NGPUS switch) ------------------------
+ * gx_pagerank_multi: Graphalytics PageRank of the host CSR A on the ndev devices of `ctxs`
+ * (one gx_ctx per distinct device).  The pull matrix (A' built on the host for a directed
+ * graph) is 1-D row partitioned: the hub-first order is dealt round-robin over the devices
+ * (gx_pr_partition), each device gets its rows with columns already in the exchange layout,
+ * and every iteration is one SpMV per device (k_pr_pull_units) plus one grouped in-process
+ * RCCL all-gather (ncclCommInitAll over the devices, xGMI) of the live rows and dangling
+ * slots.  rank[v] in A's vertex order.  Replaces LA_PR (pr.cpp:47-66) when bin/exe/pr runs with
+ * GX_NGPUS=N: execute-job.sh cannot pass new flags (execute-job.sh:68-151), and the CLI stays
+ * one process.
+ * gx_pr_partition (host only, no GPU): order[i] = the vertex at hub-first position i
+ * (out-degree descending, ties by id); part k owns positions k, k + nparts, ... as its local
+ * rows 0, 1, ...: rows[k] of them, the first live[k] with out-edges (nparts entries each).
+ * ------------------------------------------------------------------------------- */
+int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, double damping, int iters,
+                      double *rank);
+int gx_pr_partition(uint64_t n, const uint64_t *rowptr, int nparts, uint32_t *order, uint64_t *rows, uint64_t *live);
+
 /* ---------------------------------------------------------------------------------
  * Multi-GPU steps for the other algorithms.  The graph is replicated on
  * every rank (gx_graph_create on each device); rank k owns the vertex range

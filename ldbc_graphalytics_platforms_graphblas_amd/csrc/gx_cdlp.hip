@@ -62,17 +62,7 @@ struct CdlpArgs {
     // have nothing to do unless *dense
     int sparse;
     int cshards;   // *changed is cshards words kFlagStride apart (raise_flag_sharded)
-    // staged labels (k_cdlp_stage): nl[e] = lab[column of entry e] for every entry of A, then
-    // (directed) of A' at nnzA + e, so a vertex's labels are contiguous loads instead of
-    // column-indexed gathers.  Valid in a dense iteration only: with an active set and
-    // !*dense the kernels gather through the columns (unstage()).
-    const int32_t *nl;
-    int64_t nnzA;
 };
-
-__device__ __forceinline__ void unstage(CdlpArgs &a) {
-    if (a.nl && a.act && *a.dense == 0) a.nl = nullptr;
-}
 
 __device__ __forceinline__ bool tier_idle(const CdlpArgs &a) { return a.sparse && *a.dense == 0; }
 
@@ -83,7 +73,6 @@ __device__ __forceinline__ bool active(const CdlpArgs &a, bool all, int64_t v) {
 
 __device__ __forceinline__ int32_t label_at(const CdlpArgs &a, int64_t ob, int64_t od, int64_t ib,
                                             int64_t k) {
-    if (a.nl) return k < od ? a.nl[ob + k] : a.nl[a.nnzA + ib + (k - od)];
     return k < od ? a.lab[a.ciA[ob + k]] : a.lab[a.ciT[ib + (k - od)]];
 }
 
@@ -120,14 +109,10 @@ __device__ __forceinline__ int32_t col_at(const CdlpArgs &a, const VMeta &m, int
     return k < m.od ? a.ciA[m.ob + k] : a.ciT[m.ib + (k - m.od)];
 }
 
-// Where label k of a vertex is read: an index into lsrc(a), the staged labels (no load to
-// find it) or the label array (through the column).
-__device__ __forceinline__ int64_t src_at(const CdlpArgs &a, const VMeta &m, int64_t k) {
-    if (a.nl) return k < m.od ? m.ob + k : a.nnzA + m.ib + (k - m.od);
-    return col_at(a, m, k);
-}
+// Where label k of a vertex is read: an index into lsrc(a), the label array (through the column).
+__device__ __forceinline__ int64_t src_at(const CdlpArgs &a, const VMeta &m, int64_t k) { return col_at(a, m, k); }
 
-__device__ __forceinline__ const int32_t *lsrc(const CdlpArgs &a) { return a.nl ? a.nl : a.lab; }
+__device__ __forceinline__ const int32_t *lsrc(const CdlpArgs &a) { return a.lab; }
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t l, int log2ts) {
     return (l * 2654435761u) >> (32 - log2ts);
@@ -237,7 +222,6 @@ constexpr int kTiny = 16;
 
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
     if (tier_idle(a)) return;
-    unstage(a);
     bool any = false;
     const bool all = all_active(a);
     for (int64_t v = a.v0 + (int64_t)blockIdx.x * kCdlpBlock + threadIdx.x; v < a.v1;
@@ -295,7 +279,6 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int32_t *__restrict__ sv,
                                                            int32_t nsmall) {
     if (tier_idle(a)) return;
-    unstage(a);
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t gw = ((int64_t)blockIdx.x * kCdlpBlock + threadIdx.x) / kWave;
     const int64_t nw = (int64_t)gridDim.x * (kCdlpBlock / kWave);
@@ -348,7 +331,6 @@ template <int kSlots>
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int32_t *__restrict__ lv,
                                                            int32_t nlight) {
     if (tier_idle(a)) return;
-    unstage(a);
     __shared__ uint32_t keys[kCdlpBlock / kWave][kSlots];
     __shared__ uint32_t cnts[kCdlpBlock / kWave][kSlots];
     constexpr int R = kSlots / (2 * kWave);   // label rounds of the largest vertex of the tier
@@ -415,7 +397,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        int64_t cn[R];                                          // link 3 (staged: no load)
+        int64_t cn[R];                                          // link 3
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const int64_t k = (int64_t)r * kWave + lane;
@@ -475,7 +457,6 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
     const int32_t hi = cvert[blockIdx.x];
     const int64_t v = hv[hi];
     if (!active(a, all_active(a), v)) return;
-    unstage(a);   // its tables stay clean; k_cdlp_huge_final keeps the label
     const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
     int64_t ib = 0, id = 0;
     if (a.rpT) {
@@ -608,7 +589,6 @@ constexpr int64_t kMid4Max = kMid4Slots / 2;
 template <int kMidBlock, int kMidSlots>
 __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_t *__restrict__ mv, int32_t nmid) {
     if (tier_idle(a)) return;
-    unstage(a);
     __shared__ uint32_t K[kMidSlots];
     __shared__ uint32_t C[kMidSlots];
     __shared__ unsigned long long red[kMidBlock / kWave];
@@ -692,7 +672,7 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
                 if ((int64_t)r * kMidBlock < d) lds_table_add_wave(K, C, L[r], (int64_t)r * kMidBlock + tid < d, log2ts);
             __syncthreads();
         }
-        // link 3: its column ids (staged labels: no load)
+        // link 3: its column ids
         int64_t cn[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -1100,69 +1080,6 @@ __global__ __launch_bounds__(256) void k_rows_sorted(const int32_t *__restrict__
     if (__ballot(bad) && (threadIdx.x & (kWave - 1)) == 0) *sorted = 0;
 }
 
-// ---- staged labels --------------------------------------------------------------------
-// A dense iteration's labels are gathered once, in column order, instead of one column-indexed
-// load per entry inside the tier kernels: the entries (of A, then of A' for directed graphs)
-// are cut into kStageBlock-entry blocks whose entries the plan sorts by column, so a wave's 64
-// gathers fall on few lines of the label array (with the hub-first relabelling the most
-// gathered labels share the first lines); each block is put back in entry order in LDS and
-// written out contiguous.  SYN-7_5: ~58 M label line requests per iteration gathered row by
-// row against ~16 M sorted (tools/pr_line_model.py's count with 4-byte labels).
-constexpr int kStageBlock = 16384;
-constexpr int kStageThreads = 1024;
-
-__global__ __launch_bounds__(kStageThreads) void k_cdlp_stage(const int32_t *__restrict__ lab,
-                                                              const int32_t *__restrict__ scol,
-                                                              const uint16_t *__restrict__ spos, int64_t ns,
-                                                              int32_t *__restrict__ nl, const int *dense) {
-    if (dense && *dense == 0) return;   // an active-set iteration that stayed sparse
-    __shared__ int32_t buf[kStageBlock];
-    constexpr int R = kStageBlock / kStageThreads;
-    const int tid = threadIdx.x;
-    const int64_t b0 = (int64_t)blockIdx.x * kStageBlock;
-    const int m = (int)min((int64_t)kStageBlock, ns - b0);
-    int32_t c[R];
-    uint32_t q[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int k = r * kStageThreads + tid;
-        c[r] = k < m ? scol[b0 + k] : 0;
-        q[r] = k < m ? (uint32_t)spos[b0 + k] : 0u;
-    }
-    int32_t l[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) l[r] = lab[c[r]];   // column 0 for the padding: a valid address
-#pragma unroll
-    for (int r = 0; r < R; r++)
-        if (r * kStageThreads + tid < m) buf[q[r]] = l[r];
-    __syncthreads();
-    if (m == kStageBlock) {
-        int4 *o = reinterpret_cast<int4 *>(nl + b0);
-        const int4 *bi = reinterpret_cast<const int4 *>(buf);
-        for (int i = tid; i < kStageBlock / 4; i += kStageThreads) o[i] = bi[i];
-    } else {
-        for (int i = tid; i < m; i += kStageThreads) nl[b0 + i] = buf[i];
-    }
-}
-
-// Plan of the staging: key = block << 32 | column, value = position in the block.
-__global__ void k_stage_keys(const int32_t *__restrict__ ciA, int64_t nnzA, const int32_t *__restrict__ ciT,
-                             int64_t ns, uint64_t *keys, uint32_t *vals) {
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t c = (uint32_t)(k < nnzA ? ciA[k] : ciT[k - nnzA]);
-        keys[k] = ((uint64_t)(k / kStageBlock) << 32) | c;
-        vals[k] = (uint32_t)(k % kStageBlock);
-    }
-}
-
-__global__ void k_stage_split(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals, int64_t ns,
-                              int32_t *scol, uint16_t *spos) {
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += (int64_t)gridDim.x * blockDim.x) {
-        scol[k] = (int32_t)(uint32_t)keys[k];
-        spos[k] = (uint16_t)vals[k];
-    }
-}
-
 // Hub-first relabelling of a CSR: keys[e] = perm[row] << 32 | perm[col], sorted into the
 // relabelled CSR (the PageRank plan's transform, gx_pr.hip).
 __global__ void k_cdlp_permute_keys(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci, int64_t n,
@@ -1217,13 +1134,6 @@ CdlpGraph cdlp_view(gx_graph *g) {
 }
 
 // Staged labels of one iteration: the plan's sorted blocks and the output array.
-struct StageArgs {
-    const int32_t *scol;
-    const uint16_t *spos;
-    int64_t ns;
-    int32_t *nl;
-};
-
 __global__ void k_cdlp_iota(int32_t *a, int64_t n) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
          v += (int64_t)gridDim.x * blockDim.x)
@@ -1369,10 +1279,9 @@ int cdlp_plan(const CdlpGraph &g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream
 
 // One synchronous iteration for the plan's vertices: nxt[v] for v in [v0, v1) from cur
 // (the full label array); *changed is set when a label moved (caller zeroes it).
-// The tier kernels write disjoint vertices and only read `cur`, so they can run on three
-// streams (GX_CDLP_STREAMS=1).  That paid while the tiers were slow (SYN-7_5 10.5 -> 9.8 ms);
-// with the current tiers the overlapped kernels slow each other down and one stream is
-// faster (SYN-7_5 3.39 -> 2.89 ms, SYN-cit 3.61 -> 3.37).
+// The tier kernels write disjoint vertices and only read `cur`; on three streams they paid
+// while they were slow (SYN-7_5 10.5 -> 9.8 ms), with the current tiers one stream is faster
+// (3.39 -> 2.89 ms, SYN-cit 3.61 -> 3.37), so they run on one.
 // The active vertices of a sparse iteration (k_cdlp_mark): kCdlpSubs shards of asub entries.
 struct SparseLists {
     const int32_t *al;            // kCdlpLists - 1 lists of kCdlpSubs shards of asub entries
@@ -1383,20 +1292,12 @@ struct SparseLists {
 
 int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
                    const int32_t *act = nullptr, int32_t stamp = 0, const int *dense = nullptr, bool first = false,
-                   const SparseLists *sl = nullptr, int cshards = 1, const StageArgs *st = nullptr) {
+                   const SparseLists *sl = nullptr, int cshards = 1) {
     gx_ctx *ctx = g.ctx;
     const int64_t n = g.n;
     CdlpArgs a{g.rpA,  g.ciA,  g.rpT, g.ciT,  cur,        nxt,     n,        changed,
                P.v0,   P.v1,   act,   stamp,  dense,      first && !g.directed ? 1 : 0,
-               sl ? 1 : 0,     cshards,       nullptr,    g.nnzA};
-    if (st && st->ns > 0 && !(sl && sl->only)) {
-        // runs only when the iteration is dense (every vertex recomputed)
-        KTimer kt(ctx, "cdlp_stage", s);
-        hipLaunchKernelGGL(k_cdlp_stage, dim3((unsigned)((st->ns + kStageBlock - 1) / kStageBlock)),
-                           dim3(kStageThreads), 0, s, cur, st->scol, st->spos, st->ns, st->nl, act ? dense : nullptr);
-        GX_TRY(check_launch("k_cdlp_stage"));
-        a.nl = st->nl;
-    }
+               sl ? 1 : 0,     cshards};
     const bool tiers = !(sl && sl->only);   // sparse-only: the huge tier alone beside the sparse kernels
     if (sl) {
         // exit at once when *dense (the tier kernels below then recompute every vertex)
@@ -1417,18 +1318,7 @@ int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t 
                            (int64_t)P.n_mid4, o ? P.d_mv.p : nullptr, (int64_t)P.n_mid);
         GX_TRY(check_launch("k_cdlp_sparse_group"));
     }
-    const bool multi = env_on("GX_CDLP_STREAMS", false);
-    hipStream_t s1 = s, s2 = s;
-    if (multi) {
-        GX_TRY(ensure_aux_streams(ctx));
-        s1 = ctx->aux[0];
-        s2 = ctx->aux[1];
-        GX_HIP_TRY(hipEventRecord(ctx->fork_ev, s));
-        GX_HIP_TRY(hipStreamWaitEvent(s1, ctx->fork_ev, 0));
-        GX_HIP_TRY(hipStreamWaitEvent(s2, ctx->fork_ev, 0));
-    }
-    // s: mid2, mid, tiny; s1: huge, mid4; s2: light, small, light_s (about a third of an
-    // iteration's kernel time each on SYN-7_5)
+    hipStream_t s1 = s, s2 = s;   // one stream: overlapped tier kernels slowed each other down
     if (tiers && P.n_mid2) {
         KTimer kt(ctx, "cdlp_mid2", s);
         const unsigned grid2 = (unsigned)std::min<size_t>(P.n_mid2, (size_t)std::max(1, ctx->num_cus) * 4);
@@ -1486,12 +1376,6 @@ int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t 
                            0, s, a);
         GX_TRY(check_launch("k_cdlp_tiny"));
     }
-    if (multi) {
-        GX_HIP_TRY(hipEventRecord(ctx->join_ev[0], s1));
-        GX_HIP_TRY(hipEventRecord(ctx->join_ev[1], s2));
-        GX_HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[0], 0));
-        GX_HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[1], 0));
-    }
     return GX_SUCCESS;
 }
 
@@ -1513,10 +1397,6 @@ struct CdlpCache {
     DBuf<int32_t> ciA, ciT;
     std::vector<int64_t> h_rpA, h_rpT;
     DBuf<int32_t> order, perm;            // order[p]: the caller's vertex at p; perm = its inverse
-    DBuf<int32_t> scol, nl;               // staging plan (k_cdlp_stage) and staged labels
-    DBuf<uint16_t> spos;
-    int64_t ns = 0;
-    bool staged_plan = false;
     CdlpPlan P;
     DBuf<int32_t> la, lb, act, al, tmp;
     DBuf<uint64_t> clist;
@@ -1597,36 +1477,7 @@ int cdlp_relabel(gx_graph *g, CdlpCache &C, hipStream_t s) {
 
 // The staging plan: every entry's column, sorted within kStageBlock-entry blocks, and its
 // position in the block.
-int cdlp_stage_plan(CdlpCache &C, hipStream_t s) {
-    C.staged_plan = true;
-    const CdlpGraph &G = C.G;
-    const int64_t ns = G.nnzA + G.nnzT;
-    C.ns = ns;
-    if (!ns) return GX_SUCCESS;
-    GX_TRY(C.scol.alloc(ns));
-    GX_TRY(C.spos.alloc(ns));
-    GX_TRY(C.nl.alloc(ns, 16));
-    DBuf<uint64_t> k0, k1;
-    DBuf<uint32_t> v0, v1;
-    GX_TRY(k0.alloc(ns));
-    GX_TRY(k1.alloc(ns));
-    GX_TRY(v0.alloc(ns));
-    GX_TRY(v1.alloc(ns));
-    hipLaunchKernelGGL(k_stage_keys, dim3(grid_for(ns, 256, 1u << 20)), dim3(256), 0, s, G.ciA, G.nnzA, G.ciT, ns,
-                       k0.p, v0.p);
-    GX_TRY(check_launch("k_stage_keys"));
-    const int64_t nblocks = (ns + kStageBlock - 1) / kStageBlock;
-    int b = 1;
-    while ((1ll << b) < nblocks) b++;
-    GX_TRY(sort_pairs_u64_u32(k0.p, k1.p, v0.p, v1.p, (size_t)ns, 32 + b, s));
-    hipLaunchKernelGGL(k_stage_split, dim3(grid_for(ns, 256, 1u << 20)), dim3(256), 0, s, k1.p, v1.p, ns, C.scol.p,
-                       C.spos.p);
-    GX_TRY(check_launch("k_stage_split"));
-    GX_HIP_TRY(hipStreamSynchronize(s));   // the sort buffers die at return
-    return GX_SUCCESS;
-}
-
-int cdlp_cache(gx_graph *g, int iters, bool relabel, bool stage, CdlpCache **out, hipStream_t s) {
+int cdlp_cache(gx_graph *g, int iters, bool relabel, CdlpCache **out, hipStream_t s) {
     const int64_t n = (int64_t)g->n;
     auto *C = static_cast<CdlpCache *>(g->cdlp.get());
     if (C && C->relabel != relabel) {
@@ -1673,7 +1524,6 @@ int cdlp_cache(gx_graph *g, int iters, bool relabel, bool stage, CdlpCache **out
         g->cdlp = fresh;
         C = fresh.get();
     }
-    if (stage && !C->staged_plan) GX_TRY(cdlp_stage_plan(*C, s));
     if (iters > C->cap_iters) {
         const int cap = std::max(iters, 16);
         GX_TRY(C->changed.alloc((size_t)cap * kFlagShards * kFlagStride));
@@ -1703,18 +1553,14 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     // The relabelled copy costs ~90 ms to build on SYN-cit (4.2 M vertices) and saves ~1.3 ms
     // per call, so, like BFS's transpose, it is built once the graph serves a second CDLP run:
     // a one-off run (the Graphalytics executable's) stays in the caller's order.
-    // GX_CDLP_RELABEL=0 never, 1 from the first run.  GX_CDLP_STAGE=1: dense iterations read
-    // staged labels (k_cdlp_stage; measured slower)
+    // GX_CDLP_RELABEL=0 never, 1 from the first run.
     g->cdlp_calls++;
     const char *re = std::getenv("GX_CDLP_RELABEL");
     const bool relabel = re ? std::atoi(re) != 0 : g->cdlp_calls >= 2;
-    const bool stage = env_on("GX_CDLP_STAGE", false);
     CdlpCache *C = nullptr;
-    GX_TRY(cdlp_cache(g, std::max(iters, 1), relabel, stage, &C, s));
+    GX_TRY(cdlp_cache(g, std::max(iters, 1), relabel, &C, s));
     CdlpPlan &P = C->P;
     const CdlpGraph &G = C->G;
-    const StageArgs sa{C->scol.p, C->spos.p, C->ns, C->nl.p};
-    const StageArgs *st = stage && C->ns > 0 ? &sa : nullptr;
     GX_HIP_TRY(hipMemsetAsync(C->changed.p, 0, sizeof(int) * kFlagShards * kFlagStride * std::max(iters, 1), s));
     if (relabel) {
         // labels are the caller's vertex ids, at the relabelled positions
@@ -1772,7 +1618,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             const bool only = sparse_only == 2 || (sparse_only == 1 && it >= 3 + lag && (hflag[it - 1 - lag] & 2) == 0);
             const SparseLists sl{C->al.p, C->asub, cnt, only};
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
-                                  use_sparse ? &sl : nullptr, kFlagShards, st));
+                                  use_sparse ? &sl : nullptr, kFlagShards));
         } else if (it == 0 && C->rows_sorted && first_sorted) {
             // on the caller's graph and vertex order (whose rows the check found sorted)
             KTimer kt(ctx, "cdlp_first", s);
@@ -1790,7 +1636,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             // (`first`) assumes no row repeats a column; k_rows_sorted found the caller's rows
             // strictly ascending, i.e. duplicate-free (else the counting path runs).
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0 && C->rows_sorted, nullptr,
-                                  kFlagShards, st));
+                                  kFlagShards));
         }
         hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(kWave), 0, s, changed, kFlagShards,
                            active && it >= 2 ? C->dense.p : nullptr, dflag + it);

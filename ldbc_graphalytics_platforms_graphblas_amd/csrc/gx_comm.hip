@@ -46,6 +46,9 @@ struct Rccl {
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
                                hipStream_t) = nullptr;
+    ncclResult_t (*comm_init_all)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
     std::string error;
     bool ok = false;
@@ -68,7 +71,11 @@ const Rccl &rccl() {
         r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
         r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
         r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
-        r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.error_string;
+        r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+        r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+        r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
+        r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.error_string &&
+               r.comm_init_all && r.group_start && r.group_end;
         if (!r.ok) r.error = "librccl.so.1 lacks an expected entry point";
     });
     return r;
@@ -314,6 +321,161 @@ extern "C" int gx_pr_dist_scores(gx_pr_dist *h, int piece, double *scores) {
     if (d.last_stream) GX_HIP_TRY(hipStreamSynchronize(d.last_stream));
     const uint64_t rows = d.pieces[piece]->rows;
     if (rows) GX_HIP_TRY(hipMemcpy(scores, d.ro[piece]->p, rows * sizeof(double), hipMemcpyDeviceToHost));
+    return GX_SUCCESS;
+}
+
+// ---------------------------------------------------------------- one process, N GPUs
+
+namespace {
+
+// The in-process run of gx_pagerank_multi: one PrPart, stream and RCCL communicator per device
+// (ncclCommInitAll), every collective issued for all devices inside one group.
+struct MultiRun {
+    int ndev = 0;
+    std::vector<gx_ctx *> ctx;
+    std::vector<ncclComm_t> comm;
+    std::vector<PrPart *> part;
+    std::vector<std::unique_ptr<DBuf<double>>> xr, xw, xl, ro;
+    uint64_t chunk = 0;
+
+    ~MultiRun() {
+        for (int d = 0; d < ndev; d++) {
+            (void)hipSetDevice(ctx[d]->device);
+            (void)hipStreamSynchronize(ctx[d]->stream);
+        }
+        for (ncclComm_t c : comm)
+            if (c) (void)rccl().comm_destroy(c);
+        for (int d = 0; d < ndev; d++) {
+            (void)hipSetDevice(ctx[d]->device);
+            delete part[d];
+            xr[d].reset();
+            xw[d].reset();
+            xl[d].reset();
+            ro[d].reset();
+        }
+    }
+
+    // every device's local chunk into every device's `dst` (the exchanged vector)
+    int gather(std::vector<std::unique_ptr<DBuf<double>>> &dst) {
+        const Rccl &r = rccl();
+        GX_NCCL_TRY("ncclGroupStart", r.group_start());
+        for (int d = 0; d < ndev; d++) {
+            const ncclResult_t e = r.all_gather(xl[d]->p, dst[d]->p, chunk, ncclFloat64, comm[d], ctx[d]->stream);
+            if (e != ncclSuccess) {
+                (void)r.group_end();
+                return rccl_fail("ncclAllGather", e);
+            }
+        }
+        GX_NCCL_TRY("ncclGroupEnd", r.group_end());
+        return GX_SUCCESS;
+    }
+};
+
+}  // namespace
+
+extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, double damping,
+                                 int iters, double *rank) {
+    if (!ctxs || !A || !rank || (A->nnz && !A->colidx) || !A->rowptr)
+        return fail(GX_NULL_POINTER, "gx_pagerank_multi: null argument");
+    if (ndev < 1) return fail(GX_INVALID_VALUE, "gx_pagerank_multi: ndev < 1");
+    if (iters < 0) return fail(GX_INVALID_VALUE, "gx_pagerank_multi: negative iteration count");
+    const uint64_t n = A->n;
+    if (n == 0) return GX_SUCCESS;
+    if (iters == 0) {
+        for (uint64_t v = 0; v < n; v++) rank[v] = 1.0 / (double)n;
+        return GX_SUCCESS;
+    }
+    if (n >= (1ull << 31) - 64) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: n >= 2^31");
+    for (int d = 0; d < ndev; d++)
+        for (int e = 0; e < d; e++)
+            if (!ctxs[d] || ctxs[d]->device == ctxs[e]->device)
+                return fail(GX_INVALID_VALUE, "gx_pagerank_multi: one context per distinct device");
+    if (!ctxs[0]) return fail(GX_NULL_POINTER, "gx_pagerank_multi: null context");
+    const Rccl &r = rccl();
+    if (!r.ok) return fail(GX_NOT_IMPLEMENTED, r.error);
+    // the pull matrix: A' for a directed graph (LAGraph_Cached_AT, pr.cpp:60), A itself else
+    const uint64_t *prp = A->rowptr, *pci = A->colidx;
+    std::vector<uint64_t> trp, tci;
+    if (directed) {
+        trp.resize(n + 1);
+        tci.resize(std::max<uint64_t>(A->nnz, 1));
+        host_transpose(n, A->rowptr, A->colidx, trp.data(), tci.data());
+        prp = trp.data();
+        pci = tci.data();
+    }
+    // interleaved hub-first partition (gx_pr_partition; pr_partition.interleaved_relabel):
+    // position i of the hub-first order goes to device i % ndev as its local row i / ndev
+    std::vector<uint32_t> order(n);
+    std::vector<uint64_t> rows(ndev), live(ndev);
+    GX_TRY(gx_pr_partition(n, A->rowptr, ndev, order.data(), rows.data(), live.data()));
+    uint64_t maxlive = 0;
+    for (int d = 0; d < ndev; d++) maxlive = std::max(maxlive, live[d]);
+    MultiRun M;
+    M.ndev = ndev;
+    M.chunk = (maxlive + 1 + 31) / 32 * 32;   // + the dangling slot
+    if (M.chunk * (uint64_t)ndev >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
+    // column map: vertex -> its place in the exchanged vector (owner * chunk + local row)
+    std::vector<int32_t> colmap(n);
+    for (uint64_t i = 0; i < n; i++) colmap[order[i]] = (int32_t)((i % ndev) * M.chunk + i / ndev);
+    M.ctx.assign(ctxs, ctxs + ndev);
+    M.comm.assign(ndev, nullptr);
+    M.part.assign(ndev, nullptr);
+    for (int d = 0; d < ndev; d++) {
+        M.xr.emplace_back(new DBuf<double>());
+        M.xw.emplace_back(new DBuf<double>());
+        M.xl.emplace_back(new DBuf<double>());
+        M.ro.emplace_back(new DBuf<double>());
+    }
+    std::vector<int> devs(ndev);
+    for (int d = 0; d < ndev; d++) devs[d] = ctxs[d]->device;
+    GX_NCCL_TRY("ncclCommInitAll", r.comm_init_all(M.comm.data(), ndev, devs.data()));
+    std::vector<std::vector<uint32_t>> mine(ndev);
+    for (int d = 0; d < ndev; d++) {
+        std::vector<uint32_t> &vr = mine[d];
+        vr.resize(rows[d]);
+        for (uint64_t j = 0; j < rows[d]; j++) vr[j] = order[(uint64_t)d + j * ndev];
+        std::vector<int64_t> h_rp(rows[d] + 1);
+        uint64_t nz = 0;
+        for (uint64_t j = 0; j < rows[d]; j++) nz += prp[vr[j] + 1] - prp[vr[j]];
+        std::vector<int32_t> ci(nz), outdeg(rows[d]);
+        host_pick_rows(prp, pci, vr.data(), rows[d], colmap.data(), h_rp.data(), ci.data());
+        for (uint64_t j = 0; j < rows[d]; j++) outdeg[j] = (int32_t)(A->rowptr[vr[j] + 1] - A->rowptr[vr[j]]);
+        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+        GX_TRY(pr_part_build(ctxs[d], n, ndev, d, M.chunk, live[d], h_rp, ci, outdeg, damping, &M.part[d]));
+        const size_t full = M.chunk * (size_t)ndev;
+        GX_TRY(M.xr[d]->alloc(full));
+        GX_TRY(M.xw[d]->alloc(full));
+        GX_TRY(M.xl[d]->alloc(M.chunk));
+        GX_TRY(M.ro[d]->alloc(std::max<uint64_t>(rows[d], 1)));
+        GX_HIP_TRY(hipMemsetAsync(M.xr[d]->p, 0, full * sizeof(double), ctxs[d]->stream));
+        GX_HIP_TRY(hipMemsetAsync(M.xw[d]->p, 0, full * sizeof(double), ctxs[d]->stream));
+    }
+    // init, then per iteration: every device's SpMV, one grouped all-gather
+    for (int d = 0; d < ndev; d++) {
+        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+        GX_TRY(pr_init(M.part[d], M.xl[d]->p, ctxs[d]->stream));
+    }
+    GX_TRY(M.gather(M.xr));
+    for (int it = 0; it < iters; it++) {
+        const bool last = it == iters - 1;
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_TRY(pr_step(M.part[d], M.xr[d]->p, M.xl[d]->p, last ? M.ro[d]->p : nullptr, ctxs[d]->stream));
+        }
+        if (last) break;
+        GX_TRY(M.gather(M.xw));
+        std::swap(M.xr, M.xw);
+    }
+    // scores back in A's vertex order
+    for (int d = 0; d < ndev; d++) {
+        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+        std::vector<double> buf(rows[d]);
+        if (rows[d])
+            GX_HIP_TRY(hipMemcpyAsync(buf.data(), M.ro[d]->p, rows[d] * sizeof(double), hipMemcpyDeviceToHost,
+                                      ctxs[d]->stream));
+        GX_HIP_TRY(hipStreamSynchronize(ctxs[d]->stream));
+        for (uint64_t j = 0; j < rows[d]; j++) rank[mine[d][j]] = buf[j];
+    }
     return GX_SUCCESS;
 }
 

@@ -588,4 +588,73 @@ void host_widen(const int32_t *in, uint64_t n, uint64_t *out) {
     for (int64_t v = 0; v < (int64_t)n; v++) out[v] = (uint64_t)(uint32_t)in[v];
 }
 
+int host_chunk_columns(const uint64_t *ci, uint64_t nnz, const uint64_t *ranges, int nranks, const uint64_t *live,
+                       uint64_t chunk, uint64_t n, int32_t *out) {
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+    for (int64_t k = 0; k < (int64_t)nnz; k++) {
+        const uint64_t c = ci[k];
+        if (c >= n) {
+            bad |= 1;
+            continue;
+        }
+        int owner = 0;   // nranks is small: the last range starting at or before c
+        while (owner + 1 < nranks && ranges[owner + 1] <= c) owner++;
+        const uint64_t local = c - ranges[owner];
+        if (local >= live[owner]) bad |= 2;
+        out[k] = (int32_t)((uint64_t)owner * chunk + local);
+    }
+    return bad;
+}
+
+void host_hub_order(const uint64_t *rp, uint64_t n, uint32_t *order) {
+    uint64_t maxd = 0;
+#pragma omp parallel for schedule(static) reduction(max : maxd)
+    for (int64_t v = 0; v < (int64_t)n; v++) maxd = std::max<uint64_t>(maxd, rp[v + 1] - rp[v]);
+    // stable counting sort by descending degree
+    std::vector<uint64_t> start(maxd + 2, 0);
+    for (uint64_t v = 0; v < n; v++) start[maxd - (rp[v + 1] - rp[v]) + 1]++;
+    for (size_t k = 1; k < start.size(); k++) start[k] += start[k - 1];
+    for (uint64_t v = 0; v < n; v++) order[start[maxd - (rp[v + 1] - rp[v])]++] = (uint32_t)v;
+}
+
+void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows, uint64_t nrows, const int32_t *colmap,
+                    int64_t *out_rp, int32_t *out_ci) {
+    out_rp[0] = 0;
+    for (uint64_t j = 0; j < nrows; j++) out_rp[j + 1] = out_rp[j] + (int64_t)(rp[rows[j] + 1] - rp[rows[j]]);
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int64_t j = 0; j < (int64_t)nrows; j++) {
+        const uint64_t b = rp[rows[j]], e = rp[rows[j] + 1];
+        int32_t *o = out_ci + out_rp[j];
+        for (uint64_t k = b; k < e; k++) o[k - b] = colmap[ci[k]];
+    }
+}
+
+void host_transpose(uint64_t n, const uint64_t *rp, const uint64_t *ci, uint64_t *trp, uint64_t *tci) {
+    const uint64_t nnz = rp[n];
+    std::fill(trp, trp + n + 1, 0);
+    for (uint64_t k = 0; k < nnz; k++) trp[ci[k] + 1]++;
+    for (uint64_t i = 0; i < n; i++) trp[i + 1] += trp[i];
+    std::vector<uint64_t> cur(trp, trp + n);
+    for (uint64_t i = 0; i < n; i++)
+        for (uint64_t k = rp[i]; k < rp[i + 1]; k++) tci[cur[ci[k]]++] = i;
+}
+
 }  // namespace gx
+
+// Host-only: the interleaved hub-first partition of gx_pagerank_multi (include/gx.h).
+extern "C" int gx_pr_partition(uint64_t n, const uint64_t *rowptr, int nparts, uint32_t *order, uint64_t *rows,
+                               uint64_t *live) {
+    if (!rowptr || !order || !rows || !live) return fail(GX_NULL_POINTER, "gx_pr_partition: null argument");
+    if (nparts < 1) return fail(GX_INVALID_VALUE, "gx_pr_partition: nparts < 1");
+    if (n >= (1ull << 32)) return fail(GX_NOT_IMPLEMENTED, "gx_pr_partition: n >= 2^32");
+    gx::host_hub_order(rowptr, n, order);
+    for (int k = 0; k < nparts; k++) {
+        rows[k] = n > (uint64_t)k ? (n - k + nparts - 1) / nparts : 0;
+        live[k] = 0;
+    }
+    // hub-first: degrees descend, so each part's rows with out-edges come first
+    for (uint64_t i = 0; i < n; i++)
+        if (rowptr[order[i] + 1] > rowptr[order[i]]) live[i % nparts]++;
+    return GX_SUCCESS;
+}

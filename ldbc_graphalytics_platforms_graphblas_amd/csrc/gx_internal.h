@@ -27,5 +27,17 @@ bool host_monotone(const uint64_t *rp, uint64_t n);
 void host_levels(const int32_t *in, uint64_t n, int64_t *out);
 // labels: out[i] = (uint64) in[i]
 void host_widen(const int32_t *in, uint64_t n, uint64_t *out);
+// PageRank exchange layout: global column c of rank `owner` (ranges[owner] <= c < ranges[owner+1])
+// -> owner * chunk + (c - ranges[owner]); returns 0, or bit 0 = a column >= n, bit 1 = a column
+// past its owner's live rows
+int host_chunk_columns(const uint64_t *ci, uint64_t nnz, const uint64_t *ranges, int nranks, const uint64_t *live,
+                       uint64_t chunk, uint64_t n, int32_t *out);
+// hub-first order: order[i] = the vertex at position i, out-degree descending, ties by id
+void host_hub_order(const uint64_t *rp, uint64_t n, uint32_t *order);
+// the rows `rows[j]` of (rp, ci) as a local CSR (out_rp from 0) with columns renamed by colmap
+void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows, uint64_t nrows, const int32_t *colmap,
+                    int64_t *out_rp, int32_t *out_ci);
+// CSR of A' (rows sorted)
+void host_transpose(uint64_t n, const uint64_t *rp, const uint64_t *ci, uint64_t *trp, uint64_t *tci);
 
 }  // namespace gx

@@ -1,11 +1,39 @@
 // gx_pr.h -- PageRank pull plan (row blocks of the pull matrix of one rank).
 #pragma once
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "gx_device.h"
 
 namespace gx {
+
+// GX_PLAN_TIMES=1: the host-side phase times of a plan build on stderr (the stream is
+// synchronised at every mark, so device phases are attributed too).  Diagnostics only.
+struct PlanClock {
+    bool on = false;
+    hipStream_t s = nullptr;
+    const char *what = "";
+    std::chrono::steady_clock::time_point t;
+    PlanClock(const char *w, hipStream_t st) : s(st), what(w) {
+        const char *e = std::getenv("GX_PLAN_TIMES");
+        on = e && std::atoi(e) != 0;
+        if (on) {
+            (void)hipStreamSynchronize(s);
+            t = std::chrono::steady_clock::now();
+        }
+    }
+    void mark(const char *phase) {
+        if (!on) return;
+        (void)hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[plan %s] %-28s %8.2f ms\n", what, phase,
+                     std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
 
 // One workgroup's share of the pull SpMV (the CSR-Adaptive split):
 //   split <  0 : STREAM  -- rows [row_begin, row_end), all of them short, <= kStreamNnz
@@ -20,22 +48,6 @@ struct RowBlock {
     int32_t row_end;
     int32_t split;      // -1 stream; else index into the per-long-row ticket/partials
     int32_t seg;        // segment number within the long row
-};
-
-// One wave's share of the hub-cached pull SpMV (k_pr_pull_hub):
-//   split <  0 : rows [row_begin, row_end) of similar length (hub-first order), `lanes`
-//                lanes per row, 64 / lanes rows in flight per pass.
-//   split >= 0 : entries [nz_begin, nz_end) of the long row row_begin (all 64 lanes);
-//                partial sums of a row's segments are combined by the last arriver.
-struct WaveItem {
-    int64_t nz_begin;
-    int64_t nz_end;
-    int32_t row_begin;
-    int32_t row_end;
-    int32_t split;
-    int32_t seg;
-    int32_t lanes;
-    int32_t pad;
 };
 
 // One workgroup's share of a column-sorted block (k_pr_pull_units, gx_pr_sorted.hip): the
@@ -63,11 +75,6 @@ __device__ __forceinline__ void store_x(double *x_out, double *xd, int64_t live,
     else xd[row - live] = v;
 }
 
-constexpr int kHubBlock = 1024;       // one 16-wave workgroup per CU
-constexpr int kItemNnz = 2048;        // entries per wave item
-constexpr int kItemRows = 512;        // rows per wave item
-constexpr int kHubSegNnz = 4096;      // entries per long-row segment item
-
 constexpr int kPullBlock = 256;      // 4 waves
 constexpr int kStreamNnz = 2048;     // LDS stage: 16 KiB of fp64 per workgroup
 constexpr int kStreamRows = 256;     // at most one row per lane in stream mode
@@ -93,8 +100,6 @@ struct PrPart {
     DBuf<RowBlock> blocks;
     uint32_t nblocks = 0;
     uint32_t nlong_blocks = 0;   // LONG blocks come first in `blocks`
-    int stream_nnz = kStreamNnz; // LDS stage of a STREAM block: 1024, 2048 or 4096 entries
-    int only = 0;                // tuning/debug: 1 = launch LONG blocks only, 2 = STREAM only
     DBuf<int32_t> long_first;  // per long row: index of its first partial
     DBuf<int32_t> long_nseg;   // per long row: number of segments
     DBuf<double> long_part;    // per segment partial sum
@@ -108,15 +113,14 @@ struct PrPart {
     uint32_t dgrid = 0;
     DBuf<double> dpart;
     DBuf<uint32_t> dticket;
-    // column-sorted blocks (k_pr_pull_sorted, gx_pr_sorted.hip; the default)
+    // column-sorted blocks (k_pr_pull_units, gx_pr_sorted.hip; the default)
     DBuf<int32_t> sci;           // columns sorted within each block
     DBuf<uint32_t> spk;          // packed (column - group base) << 14 | row
     DBuf<uint32_t> gbase;        // base column per 64-entry group (bit 31: escape to sci)
     int sorted_nnz = 65536;      // entries per block
     int sorted_rows = 4096;      // rows per block (LDS accumulators)
-    bool units_mode = false;     // split blocks (k_pr_pull_units)
     int64_t unit_nnz = 0;        // target entries per unit
-    DBuf<SortedUnit> units;      // one-pass mode: one workgroup per unit, after the LONG blocks
+    DBuf<SortedUnit> units;      // one workgroup per unit, after the LONG blocks
     uint32_t nunits = 0;
     DBuf<double> uslab;          // partial row sums of the multi-unit blocks
     DBuf<uint32_t> uticket;      // per multi-unit block: arrivals of the current iteration
@@ -124,35 +128,19 @@ struct PrPart {
     int utimes_launch = 0;
     int long_nnz = 65536;        // longer rows take the LONG segment path
     int sorted_lds = 0;          // dynamic LDS bytes of the launch
-    int sorted_variant = 0;      // tuning: block size / gathers in flight (gx_pr_sorted.hip)
-    int index_x4 = 1;            // units kernel: four entries per 16-B index load (GX_PR_INDEX_X4)
-    int pipe2 = 1;               // X4 units kernel pipelined across rounds (GX_PR_PIPE2, default on)
-    DBuf<int64_t> ssplit;        // per block: first sorted entry in the tail pass
-    DBuf<double> ypart;          // hub-pass row sums
-    int64_t hot_cols = 0;        // columns of the hub pass (0: one pass; GX_PR_HOT_COLS)
-    bool two_pass = false;
-    int slices = 1;              // XCD column slices (k_pr_pull_sliced; GX_PR_SLICES)
-    DBuf<int64_t> sbound;        // per sorted block: slice boundaries
     uint32_t nsorted = 0, nlong_pad = 0;
-    // dangling-score sum fused into the one-pass sorted kernel: blocks holding out-degree-0
-    // rows publish a partial, the last of them adds them up in slot order
+    // rows without entries (a suffix of the hub-first order): row-range workgroups
+    int64_t sfx0 = 0;            // first such row
+    uint32_t nsfx = 0;           // their workgroups
+    int32_t sfx_slot0 = -1;      // their first dangling slot, -1: none dangling
+    // dangling-score sum fused into the kernel: blocks holding out-degree-0 rows publish a
+    // partial, the last of them adds them up in slot order
     bool fused_dangling = false;
     DBuf<int32_t> dslot;         // per block: its partial's slot, -1 = no dangling rows
     DBuf<double> fdpart;
     DBuf<uint32_t> fdticket;
     uint32_t ndblocks = 0;
-    // hub-cached kernel: wave items, LDS hub prefix, fused dangling reduction
-    int kernel = 2;              // 0 = k_pr_pull_hub, 1 = k_pr_pull (CSR-Adaptive), 2 = k_pr_pull_sorted
-    bool int4_loads = false;     // k_pr_pull: 16-B index loads (lane stride 4) instead of lane-consecutive
-    DBuf<WaveItem> items;
-    uint32_t nitems = 0;
-    DBuf<int32_t> hlong_first, hlong_nseg;
-    DBuf<double> hlong_part;
-    DBuf<uint32_t> hlong_ticket;
-    uint32_t hub_grid = 0;       // workgroups (one per CU)
-    int64_t hub_entries = 0;     // x prefix cached in LDS
-    DBuf<double> gpart;          // per-workgroup dangling partial
-    DBuf<uint32_t> gticket;
+    int kernel = 2;              // 1 = k_pr_pull (CSR-Adaptive, GX_PR_KERNEL=adaptive), 2 = k_pr_pull_units
     // single-GPU driver buffers (gx_pagerank): vertices relabelled hub-first
     DBuf<double> xa, xb, rank_out, result;
     DBuf<int32_t> perm;        // old vertex id -> position in the hub-first order
@@ -163,12 +151,7 @@ struct PrPart {
 int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp,
             const int32_t *d_ci, const int32_t *d_outdeg, const std::vector<int32_t> &h_outdeg);
 
-// Wave-item plan of the hub-cached kernel (called by pr_plan).
-int pr_plan_hub(PrPart *p, const std::vector<int64_t> &h_rp);
-// One iteration with k_pr_pull_hub (pull + fused dangling sum).
-int pr_step_hub(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
-
-// Column-sorted block plan (k_pr_pull_sorted) and its iteration (gx_pr_sorted.hip).
+// Column-sorted block plan (k_pr_pull_units) and its iteration (gx_pr_sorted.hip).
 int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vector<int32_t> &h_outdeg);
 int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 // Dangling-score sum of this rank into x_local's last chunk slot.
@@ -178,6 +161,11 @@ int pr_init(PrPart *p, double *x_local, hipStream_t s);
 // gx_pagerank's single-rank plan of a graph: its pull matrix (A' when directed, which must be
 // built) relabelled hub-first, column-sorted blocks, x buffers and the hub-first perm.
 int pr_single_plan(gx_graph *g, PrPart **out);
+// A rank's plan from its local pull rows (h_rp from 0) with columns already in the exchange
+// layout (ci), the out-degree of each row's vertex, and its live prefix (gx_pr_part_create_live).
+int pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint64_t chunk, uint64_t live,
+                  const std::vector<int64_t> &h_rp, const std::vector<int32_t> &ci, const std::vector<int32_t> &h_outdeg,
+                  double damping, PrPart **out);
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 
 }  // namespace gx

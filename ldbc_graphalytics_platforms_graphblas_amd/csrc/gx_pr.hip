@@ -305,75 +305,75 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     p->rows = (uint64_t)rows;
     if (p->live > p->rows) p->live = p->rows;   // no live prefix given: all rows
     if (p->live < p->rows) GX_TRY(p->xd.alloc(p->rows - p->live));
-    // tuning knobs (plan time): GX_PR_STREAM_NNZ = 1024 | 2048 | 4096, GX_PR_ONLY = long | stream
-    if (const char *e = std::getenv("GX_PR_STREAM_NNZ")) {
-        const int v = std::atoi(e);
-        if (v == 1024 || v == 2048 || v == 4096) p->stream_nnz = v;
-    }
-    if (const char *e = std::getenv("GX_PR_ONLY")) p->only = std::strcmp(e, "long") == 0 ? 1 : std::strcmp(e, "stream") == 0 ? 2 : 0;
-    const int64_t NB = p->stream_nnz;
     p->rp = d_rp;
     p->ci = d_ci;
     p->outdeg = d_outdeg;
-    std::vector<RowBlock> longb, streamb;
-    std::vector<int32_t> lfirst, lnseg;
-    int32_t nsegs = 0;
-    std::vector<std::pair<int64_t, int32_t>> longrows;   // (length, row)
-    int64_t r = 0;
-    while (r < rows) {
-        const int64_t len = h_rp[r + 1] - h_rp[r];
-        if (len > NB) {
-            longrows.push_back({len, (int32_t)r});
-            r++;
-            continue;
+    // kernel choice: GX_PR_KERNEL = sorted (default) | adaptive (CSR-Adaptive k_pr_pull: row-order
+    // sums, bitwise deterministic, ~3x slower)
+    if (const char *e = std::getenv("GX_PR_KERNEL")) p->kernel = std::strcmp(e, "adaptive") == 0 ? 1 : 2;
+    PlanClock clk("pr_plan", p->ctx->stream);
+    if (p->kernel == 1) {
+        const int64_t NB = kStreamNnz;
+        std::vector<RowBlock> longb, streamb;
+        std::vector<int32_t> lfirst, lnseg;
+        int32_t nsegs = 0;
+        std::vector<std::pair<int64_t, int32_t>> longrows;   // (length, row)
+        int64_t r = 0;
+        while (r < rows) {
+            const int64_t len = h_rp[r + 1] - h_rp[r];
+            if (len > NB) {
+                longrows.push_back({len, (int32_t)r});
+                r++;
+                continue;
+            }
+            const int64_t start = r;
+            int64_t nz = 0;
+            while (r < rows && r - start < kStreamRows) {
+                const int64_t l = h_rp[r + 1] - h_rp[r];
+                if (l > NB || nz + l > NB) break;
+                nz += l;
+                r++;
+            }
+            streamb.push_back({h_rp[start], h_rp[r], (int32_t)start, (int32_t)r, -1, 0});
         }
-        const int64_t start = r;
-        int64_t nz = 0;
-        while (r < rows && r - start < kStreamRows) {
-            const int64_t l = h_rp[r + 1] - h_rp[r];
-            if (l > NB || nz + l > NB) break;
-            nz += l;
-            r++;
+        // longest rows first: they are the tail of the launch otherwise
+        std::stable_sort(longrows.begin(), longrows.end(),
+                         [](const auto &x, const auto &y) { return x.first > y.first; });
+        for (const auto &lr : longrows) {
+            const int32_t row = lr.second;
+            const int64_t len = lr.first;
+            const int32_t nseg = (int32_t)((len + kSegNnz - 1) / kSegNnz);
+            const int32_t sp = (int32_t)lfirst.size();
+            lfirst.push_back(nsegs);
+            lnseg.push_back(nseg);
+            for (int32_t s = 0; s < nseg; s++) {
+                const int64_t zb = h_rp[row] + (int64_t)s * kSegNnz;
+                const int64_t ze = std::min(zb + kSegNnz, h_rp[row + 1]);
+                longb.push_back({zb, ze, row, row + 1, sp, s});
+            }
+            nsegs += nseg;
         }
-        streamb.push_back({h_rp[start], h_rp[r], (int32_t)start, (int32_t)r, -1, 0});
-    }
-    // longest rows first: they are the tail of the launch otherwise
-    std::stable_sort(longrows.begin(), longrows.end(),
-                     [](const auto &x, const auto &y) { return x.first > y.first; });
-    for (const auto &lr : longrows) {
-        const int32_t row = lr.second;
-        const int64_t len = lr.first;
-        const int32_t nseg = (int32_t)((len + kSegNnz - 1) / kSegNnz);
-        const int32_t sp = (int32_t)lfirst.size();
-        lfirst.push_back(nsegs);
-        lnseg.push_back(nseg);
-        for (int32_t s = 0; s < nseg; s++) {
-            const int64_t zb = h_rp[row] + (int64_t)s * kSegNnz;
-            const int64_t ze = std::min(zb + kSegNnz, h_rp[row + 1]);
-            longb.push_back({zb, ze, row, row + 1, sp, s});
+        std::vector<RowBlock> all;
+        all.reserve(longb.size() + streamb.size());
+        all.insert(all.end(), longb.begin(), longb.end());
+        all.insert(all.end(), streamb.begin(), streamb.end());
+        p->nblocks = (uint32_t)all.size();
+        p->nlong_blocks = (uint32_t)longb.size();
+        p->nlong = (uint32_t)lfirst.size();
+        p->nsegs = (uint32_t)nsegs;
+        GX_TRY(p->blocks.alloc(std::max<size_t>(all.size(), 1)));
+        GX_TRY(p->long_first.alloc(std::max<size_t>(lfirst.size(), 1)));
+        GX_TRY(p->long_nseg.alloc(std::max<size_t>(lnseg.size(), 1)));
+        GX_TRY(p->long_part.alloc(std::max<size_t>(nsegs, 1)));
+        GX_TRY(p->long_ticket.alloc(std::max<size_t>(lfirst.size(), 1)));
+        if (!all.empty())
+            GX_HIP_TRY(hipMemcpy(p->blocks.p, all.data(), all.size() * sizeof(RowBlock), hipMemcpyHostToDevice));
+        if (!lfirst.empty()) {
+            GX_HIP_TRY(hipMemcpy(p->long_first.p, lfirst.data(), lfirst.size() * 4, hipMemcpyHostToDevice));
+            GX_HIP_TRY(hipMemcpy(p->long_nseg.p, lnseg.data(), lnseg.size() * 4, hipMemcpyHostToDevice));
         }
-        nsegs += nseg;
+        GX_HIP_TRY(hipMemset(p->long_ticket.p, 0, p->long_ticket.n * 4));
     }
-    std::vector<RowBlock> all;
-    all.reserve(longb.size() + streamb.size());
-    all.insert(all.end(), longb.begin(), longb.end());
-    all.insert(all.end(), streamb.begin(), streamb.end());
-    p->nblocks = (uint32_t)all.size();
-    p->nlong_blocks = (uint32_t)longb.size();
-    p->nlong = (uint32_t)lfirst.size();
-    p->nsegs = (uint32_t)nsegs;
-    GX_TRY(p->blocks.alloc(std::max<size_t>(all.size(), 1)));
-    GX_TRY(p->long_first.alloc(std::max<size_t>(lfirst.size(), 1)));
-    GX_TRY(p->long_nseg.alloc(std::max<size_t>(lnseg.size(), 1)));
-    GX_TRY(p->long_part.alloc(std::max<size_t>(nsegs, 1)));
-    GX_TRY(p->long_ticket.alloc(std::max<size_t>(lfirst.size(), 1)));
-    if (!all.empty())
-        GX_HIP_TRY(hipMemcpy(p->blocks.p, all.data(), all.size() * sizeof(RowBlock), hipMemcpyHostToDevice));
-    if (!lfirst.empty()) {
-        GX_HIP_TRY(hipMemcpy(p->long_first.p, lfirst.data(), lfirst.size() * 4, hipMemcpyHostToDevice));
-        GX_HIP_TRY(hipMemcpy(p->long_nseg.p, lnseg.data(), lnseg.size() * 4, hipMemcpyHostToDevice));
-    }
-    GX_HIP_TRY(hipMemset(p->long_ticket.p, 0, p->long_ticket.n * 4));
     // dangling rows
     std::vector<int32_t> dl;
     for (int64_t i = 0; i < rows; i++)
@@ -390,11 +390,7 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     GX_TRY(p->dpart.alloc(p->dgrid));
     GX_TRY(p->dticket.alloc(1));
     GX_HIP_TRY(hipMemset(p->dticket.p, 0, 4));
-    // kernel choice: GX_PR_KERNEL = sorted (default) | adaptive | hub
-    if (const char *e = std::getenv("GX_PR_KERNEL"))
-        p->kernel = std::strcmp(e, "hub") == 0 ? 0 : std::strcmp(e, "adaptive") == 0 ? 1 : 2;
-    if (const char *e = std::getenv("GX_PR_INT4")) p->int4_loads = std::atoi(e) != 0;
-    if (p->kernel == 0) GX_TRY(pr_plan_hub(p, h_rp));
+    clk.mark("adaptive blocks + dangling");
     if (p->kernel == 2) GX_TRY(pr_plan_sorted(p, h_rp, h_outdeg));
     return GX_SUCCESS;
 }
@@ -417,7 +413,6 @@ int pr_init(PrPart *p, double *x_local, hipStream_t s) {
 }
 
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s) {
-    if (p->kernel == 0) return pr_step_hub(p, x_full, x_local, rank_out, s);
     if (p->kernel == 2) return pr_step_sorted(p, x_full, x_local, rank_out, s);
     const double dn = (double)p->n_global;
     PullArgs a;
@@ -440,24 +435,10 @@ int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, 
     a.long_ticket = p->long_ticket.p;
     a.xd = p->xd.p;
     a.live = (int64_t)p->live;
-    uint32_t nb = p->nblocks;
     a.block_offset = 0;
-    if (p->only == 1) nb = p->nlong_blocks;
-    if (p->only == 2) {
-        a.block_offset = p->nlong_blocks;
-        nb = p->nblocks - p->nlong_blocks;
-    }
-    if (nb) {
+    if (p->nblocks) {
         KTimer kt(p->ctx, "pr_pull", s);
-        if (p->int4_loads) {
-            hipLaunchKernelGGL((k_pr_pull<2048, false>), dim3(nb), dim3(kPullBlock), 0, s, a);
-        } else if (p->stream_nnz == 1024) {
-            hipLaunchKernelGGL((k_pr_pull<1024, true>), dim3(nb), dim3(kPullBlock), 0, s, a);
-        } else if (p->stream_nnz == 4096) {
-            hipLaunchKernelGGL((k_pr_pull<4096, true>), dim3(nb), dim3(kPullBlock), 0, s, a);
-        } else {
-            hipLaunchKernelGGL((k_pr_pull<2048, true>), dim3(nb), dim3(kPullBlock), 0, s, a);
-        }
+        hipLaunchKernelGGL((k_pr_pull<kStreamNnz, true>), dim3(p->nblocks), dim3(kPullBlock), 0, s, a);
     }
     GX_TRY(check_launch("k_pr_pull"));
     return pr_dangling(p, x_local, s);
@@ -522,9 +503,11 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     gx_ctx *ctx = g->ctx;
     hipStream_t s = ctx->stream;
     DevCSR &P = g->directed ? g->AT : g->A;
+    PlanClock clk("single", s);
     std::vector<int32_t> h_outdeg(n), order, perm;
     for (uint64_t v = 0; v < n; v++) h_outdeg[v] = (int32_t)(g->A.h_rp[v + 1] - g->A.h_rp[v]);
     hub_order(h_outdeg, order, perm);
+    clk.mark("outdeg + hub order (host)");
     std::vector<int64_t> nrp(n + 1, 0);
     std::vector<int32_t> nout(n);
     for (uint64_t i = 0; i < n; i++) {
@@ -553,6 +536,7 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     if (rc == GX_SUCCESS && e == hipSuccess)
         e = hipMemcpyAsync(p->outdeg_own.p, nout.data(), n * 4, hipMemcpyHostToDevice, s);
     if (rc == GX_SUCCESS && e != hipSuccess) rc = fail(GX_DEVICE_ERROR, hipGetErrorString(e));
+    clk.mark("row pointers + uploads");
     if (rc == GX_SUCCESS && P.nnz) {
         DBuf<uint64_t> keys, scratch;
         rc = keys.alloc(P.nnz);
@@ -568,7 +552,9 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
             if (e != hipSuccess) rc = fail(GX_DEVICE_ERROR, hipGetErrorString(e));
         }
     }
+    clk.mark("relabel (keys + sort)");
     if (rc == GX_SUCCESS) rc = pr_plan(p, nrp, p->rp_own.p, p->ci_own.p, p->outdeg_own.p, nout);
+    clk.mark("pr_plan");
     if (rc == GX_SUCCESS) {
         e = hipStreamSynchronize(s);   // host vectors above die at return
         if (e != hipSuccess) rc = fail(GX_DEVICE_ERROR, hipGetErrorString(e));
@@ -656,23 +642,29 @@ extern "C" int gx_pr_part_create_live(gx_ctx *ctx, uint64_t n_global, int nranks
     std::vector<int64_t> h_rp(rows + 1);
     for (uint64_t i = 0; i <= rows; i++) h_rp[i] = (int64_t)rowptr_local[i];
     std::vector<int32_t> ci(nnz);
-    for (uint64_t k = 0; k < nnz; k++) {
-        const uint64_t c = colidx_local[k];
-        if (c >= n_global) return fail(GX_INVALID_INDEX, "column out of range");
-        const int owner = (int)(std::upper_bound(row_ranges, row_ranges + nranks + 1, c) - row_ranges) - 1;
-        if (c - row_ranges[owner] >= live[owner])
-            return fail(GX_INVALID_VALUE, "a column is past its owner's live rows (a vertex without out-edges)");
-        ci[k] = (int32_t)((uint64_t)owner * chunk + (c - row_ranges[owner]));
-    }
+    const int bad = nnz ? host_chunk_columns(colidx_local, nnz, row_ranges, nranks, live.data(), chunk, n_global, ci.data())
+                        : 0;
+    if (bad & 1) return fail(GX_INVALID_INDEX, "column out of range");
+    if (bad & 2) return fail(GX_INVALID_VALUE, "a column is past its owner's live rows (a vertex without out-edges)");
     std::vector<int32_t> h_outdeg(rows);
     for (uint64_t i = 0; i < rows; i++) h_outdeg[i] = (int32_t)outdeg_local[i];
+    PrPart *p = nullptr;
+    GX_TRY(pr_part_build(ctx, n_global, nranks, rank, chunk, live[rank], h_rp, ci, h_outdeg, damping, &p));
+    *out = reinterpret_cast<gx_pr_part *>(p);
+    return GX_SUCCESS;
+}
+
+int gx::pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint64_t chunk, uint64_t live,
+                      const std::vector<int64_t> &h_rp, const std::vector<int32_t> &ci,
+                      const std::vector<int32_t> &h_outdeg, double damping, PrPart **out) {
+    const uint64_t rows = h_rp.size() - 1, nnz = (uint64_t)h_rp[rows];
     auto *p = new PrPart();
     p->ctx = ctx;
     p->n_global = n_global;
     p->nranks = nranks;
     p->rank = rank;
     p->chunk = chunk;
-    p->live = live[rank];
+    p->live = live;
     p->damping = damping;
     int rc = p->rp_own.alloc(rows + 1);
     if (rc == GX_SUCCESS) rc = p->ci_own.alloc(nnz, 16);
@@ -690,7 +682,7 @@ extern "C" int gx_pr_part_create_live(gx_ctx *ctx, uint64_t n_global, int nranks
         delete p;
         return rc;
     }
-    *out = reinterpret_cast<gx_pr_part *>(p);
+    *out = p;
     return GX_SUCCESS;
 }
 

@@ -59,9 +59,11 @@ struct IdsHolder {
 struct CtxHolder {
     gx_ctx *ctx = nullptr;
     gx_graph *g = nullptr;
+    std::vector<gx_ctx *> more;   // GX_NGPUS > 1: the contexts of the other devices
     ~CtxHolder() {
         gx_graph_free(g);
         gx_free(ctx);
+        for (gx_ctx *c : more) gx_free(c);
     }
 };
 
@@ -104,6 +106,15 @@ int Main(int argc, char **argv, Algorithm alg) {
         if (p.thread_num > 0) omp_set_num_threads((int)p.thread_num);
         int device = 0;
         if (const char *d = std::getenv("GX_DEVICE")) device = std::atoi(d);
+        // GX_NGPUS = N: PageRank on devices [GX_DEVICE, GX_DEVICE + N) in this one process
+        // (gx_pagerank_multi: 1-D row blocks, in-process RCCL all-gather); execute-job.sh cannot
+        // pass new flags (execute-job.sh:68-151), so the backend comes from the environment
+        // (SURVEY.md 8b).  The other algorithms run on one GPU.
+        int ngpus = 0;
+        if (const char *g = std::getenv("GX_NGPUS")) ngpus = std::max(1, std::atoi(g));
+        if (ngpus && alg != Algorithm::PR)
+            std::cerr << "GX_NGPUS: only PageRank runs on several GPUs; this algorithm runs on device " << device
+                      << std::endl;
 
         CsrHolder A;
         ReadMatrix(p, &A.csr);
@@ -125,13 +136,20 @@ int Main(int argc, char **argv, Algorithm alg) {
 
         CtxHolder H;
         OK(gx_init(device, &H.ctx), "gx_init");
+        const bool multi = ngpus > 0 && alg == Algorithm::PR;
+        if (multi)
+            for (int k = 1; k < ngpus; k++) {
+                gx_ctx *c = nullptr;
+                OK(gx_init(device + k, &c), "gx_init (GX_NGPUS)");
+                H.more.push_back(c);
+            }
         std::vector<int64_t> level;
         std::vector<double> vals;
         std::vector<uint64_t> labels;
 
         const auto t_start = GetCurrentMilliseconds();
         std::cout << "Processing starts at: " << t_start << std::endl;
-        OK(gx_graph_create(H.ctx, &A.csr, p.directed ? 1 : 0, &H.g), "gx_graph_create");
+        if (!multi) OK(gx_graph_create(H.ctx, &A.csr, p.directed ? 1 : 0, &H.g), "gx_graph_create");
         const auto t_uploaded = GetCurrentMilliseconds();
         switch (alg) {
             case Algorithm::BFS:
@@ -140,7 +158,15 @@ int Main(int argc, char **argv, Algorithm alg) {
                 break;
             case Algorithm::PR:
                 vals.resize(n);
-                OK(gx_pagerank(H.g, p.damping_factor, p.max_iteration, vals.data()), "gx_pagerank");
+                if (multi) {
+                    std::vector<gx_ctx *> ctxs{H.ctx};
+                    ctxs.insert(ctxs.end(), H.more.begin(), H.more.end());
+                    OK(gx_pagerank_multi(ctxs.data(), ngpus, &A.csr, p.directed ? 1 : 0, p.damping_factor,
+                                         p.max_iteration, vals.data()),
+                       "gx_pagerank_multi");
+                } else {
+                    OK(gx_pagerank(H.g, p.damping_factor, p.max_iteration, vals.data()), "gx_pagerank");
+                }
                 break;
             case Algorithm::SSSP:
                 vals.resize(n);

@@ -284,3 +284,51 @@ def test_device_runner_rejects_mismatched_pieces():
     h = C.c_void_p()
     rc = N.lib().gx_pr_dist_create(None, None, 1, C.byref(h))
     assert rc != 0
+
+
+def test_gx_pr_partition_matches_interleaved_relabel():
+    """The host partition of gx_pagerank_multi (libgx, C++) deals the hub-first order exactly
+    as pr_partition.interleaved_relabel does (no GPU needed): same vertex per local row, same
+    row counts and live prefixes."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import live_rows
+    for undirected in (True, False):
+        csr = rmat(11, 6, 13, undirected=undirected)
+        rp = np.ascontiguousarray(csr.rowptr, dtype=np.uint64)
+        for nparts in (1, 2, 3, 8):
+            order = np.zeros(csr.n, dtype=np.uint32)
+            rows = np.zeros(nparts, dtype=np.uint64)
+            live = np.zeros(nparts, dtype=np.uint64)
+            N.check(N.lib().gx_pr_partition(csr.n, N.as_u64p(rp), nparts,
+                                            order.ctypes.data_as(C.POINTER(C.c_uint32)), N.as_u64p(rows),
+                                            N.as_u64p(live)), "gx_pr_partition")
+            perm, hub, bounds = interleaved_relabel(csr, nparts)
+            np.testing.assert_array_equal(rows, np.diff(bounds.astype(np.int64)))
+            np.testing.assert_array_equal(live, live_rows(hub, bounds))
+            # the vertex of local row j of part k sits at position k + j * nparts
+            for k in range(nparts):
+                mine = order[k::nparts].astype(np.int64)
+                np.testing.assert_array_equal(perm[mine], np.arange(int(bounds[k]), int(bounds[k + 1])))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("undirected", [True, False])
+def test_gx_pagerank_multi_one_device(undirected):
+    """gx_pagerank_multi on one device (a size-1 in-process RCCL clique) against the oracle."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    from oracle import oracle as O
+    ctx = Context(0)
+    try:
+        for scale, ef in ((10, 8), (14, 16)):
+            csr = rmat(scale, ef, 5 + scale, undirected=undirected)
+            out = np.zeros(csr.n)
+            arr = (C.c_void_p * 1)(ctx.handle.value)
+            s = csr.as_c()
+            N.check(N.lib().gx_pagerank_multi(arr, 1, C.byref(s), int(not undirected), 0.85, 10, N.as_dp(out)),
+                    "gx_pagerank_multi")
+            np.testing.assert_allclose(out, O.pagerank(csr, not undirected, 0.85, 10), rtol=1e-12, atol=0)
+    finally:
+        ctx.close()

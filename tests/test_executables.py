@@ -106,3 +106,25 @@ def test_source_vertex_not_found(tmp_path_factory, fixture_graphs):
     argv[argv.index("--source-vertex") + 1] = "987654"
     res = subprocess.run(argv, capture_output=True, text=True, timeout=60)
     assert res.returncode != 0 and "Source vertex not found in mapping" in res.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", ["example-directed", "example-undirected", "test-pr-directed", "test-pr-undirected"])
+def test_pagerank_executable_gx_ngpus(graph, tmp_path_factory, fixture_graphs):
+    """bin/exe/pr with GX_NGPUS=1: the single-process multi-GPU path (gx_pagerank_multi: 1-D
+    row blocks, an in-process RCCL clique, grouped all-gathers), equal to the oracle at 1e-12
+    and to the Graphalytics validation file."""
+    import os
+    from oracle import oracle as O
+    d, g = load_dir(tmp_path_factory, graph, fixture_graphs)
+    out = d / "out-pr-multi"
+    env = dict(os.environ, GX_NGPUS="1")
+    res = subprocess.run(job_argv("pr", d, out, g, d), capture_output=True, text=True, timeout=120, env=env)
+    assert res.returncode == 0, res.stderr
+    assert len(re.findall(r"Processing (starts|ends) at: \d+", res.stdout)) == 2
+    ids, vals = parse_output(out, "pr")
+    np.testing.assert_array_equal(ids, g.mapping)
+    got = np.array([float(v) for v in vals])
+    want = O.pagerank(g.csr, g.directed, float(g.param("pr", "damping-factor")), int(g.param("pr", "num-iterations")))
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
+    check_against_validation("PR", g.mapping, list(got), read_validation(FIXTURES / f"{graph}-PR"))

@@ -178,13 +178,13 @@ def test_dense_tiers(ctx):
         np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=4), O.cdlp(csr, directed, 4))
 
 
-@pytest.mark.parametrize("slices", ["1", "4"])
-def test_pagerank_long_row_segments(ctx, monkeypatch, slices):
+@pytest.mark.parametrize("laneperm", ["0", "1"])
+def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
     """A hub row of 150 000 entries, longer than a column-sorted block: LONG segments
-    combined by the last arriver, beside sorted blocks of random edges (with and without XCD
-    column slices)."""
+    combined by the last arriver, beside sorted blocks of random edges (with and without the
+    LDS-bank lane permutation)."""
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
-    monkeypatch.setenv("GX_PR_SLICES", slices)
+    monkeypatch.setenv("GX_PR_LANEPERM", laneperm)
     n = 150001
     rng = np.random.default_rng(3)
     a, b = rng.integers(1, n, 200000), rng.integers(1, n, 200000)
@@ -196,29 +196,21 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, slices):
                                O.pagerank(csr, False, 0.85, 6), rtol=PR_RTOL, atol=0)
 
 
-@pytest.mark.parametrize("env", [{"GX_PR_HOT_COLS": "0"}, {"GX_PR_HOT_COLS": "1024"},
-                                 {"GX_PR_HOT_COLS": "1024", "GX_PR_SORTED_ROWS": "64"},
-                                 {"GX_PR_SORTED_VARIANT": "1"}, {"GX_PR_SORTED_VARIANT": "2"},
-                                 {"GX_PR_SORTED_VARIANT": "4"}, {"GX_PR_INDEX_X4": "0"}, {"GX_PR_UNIT_LDS": "0"},
-                                 {"GX_PR_PIPE2": "0"}, {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536", "GX_PR_PIPE2": "0"},
-                                 {"GX_PR_SLICES": "2"}, {"GX_PR_SLICES": "4"}, {"GX_PR_SLICES": "8"},
-                                 {"GX_PR_SLICES": "8", "GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SLICES": "1"},
+@pytest.mark.parametrize("env", [{}, {"GX_PR_LANEPERM": "0"}, {"GX_PR_SUFFIX": "0"}, {"GX_PR_UNIT_LDS": "0"},
                                  {"GX_PR_KERNEL": "adaptive"},
                                  {"GX_PR_SORTED_ROWS": "16384", "GX_PR_UNIT_NNZ": "16384"},
-                                 {"GX_PR_SORTED_ROWS": "2048", "GX_PR_SLICES": "2"},
-                                 {"GX_PR_SORTED_NNZ": "1024"},
+                                 {"GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SORTED_ROWS": "2048"},
                                  {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536"},
                                  {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "524288"},
                                  {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536", "GX_PR_LONG_NNZ": "1024"},
-                                 {"GX_PR_UNIT_NNZ": "4096", "GX_PR_BLOCK_NNZ": "65536", "GX_PR_SORTED_VARIANT": "3"},
-                                 {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192", "GX_PR_UNIT_LAYOUT": "0"},
+                                 {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192"},
                                  {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192", "GX_PR_SORTED_ROWS": "64",
-                                  "GX_PR_UNIT_LAYOUT": "0"}])
+                                  "GX_PR_LANEPERM": "0"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
-    """One pass, two passes around a small hub slice, tiny blocks, the other block shapes,
-    16 Ki- and 2 Ki-row blocks, split blocks (several workgroups per sorted block, combined through slabs by the last
-    arriver) and the CSR-Adaptive kernel all give the oracle's scores (directed and
-    undirected)."""
+    """The default plan, without the lane permutation, with the rows without entries kept in
+    sorted blocks, two workgroups per CU, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
+    blocks (several workgroups per sorted block, combined through slabs by the last arriver)
+    and the CSR-Adaptive kernel all give the oracle's scores (directed and undirected)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     for g in (_rmat(14, 16, 4), _rmat(11, 8, 3, undirected=False)):
@@ -228,7 +220,8 @@ def test_pagerank_plan_variants(ctx, monkeypatch, env):
 
 def test_pagerank_escape_groups(ctx, monkeypatch):
     """A perfect matching on 2^21 + 64 vertices in 64-row blocks: the 64 columns of a group
-    span more than 2^20 ids, so the groups escape to plain column ids; two passes."""
+    span more than 2^20 ids, so the groups escape to plain column ids (permuted with the rest
+    of the group by the lane permutation)."""
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
     monkeypatch.setenv("GX_PR_SORTED_ROWS", "64")
     n = (1 << 21) + 64
@@ -401,16 +394,12 @@ def test_cdlp_row_order_and_sparse(ctx, monkeypatch, first_sorted, sparse, only)
         np.testing.assert_array_equal(gpu_run(ctx, _G(t, True), "CDLP", iters=iters), O.cdlp(t, True, iters))
 
 
-@pytest.mark.parametrize("relabel,stage,streams", [("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("0", "1", "1"),
-                                                   ("1", "0", "1")])
-def test_cdlp_layouts(ctx, monkeypatch, relabel, stage, streams):
+@pytest.mark.parametrize("relabel", ["1", "0"])
+def test_cdlp_layouts(ctx, monkeypatch, relabel):
     """gx_cdlp on the hub-first relabelled graph (GX_CDLP_RELABEL, the default) or the caller's
-    order, with labels gathered by the tier kernels or staged in column-sorted blocks
-    (GX_CDLP_STAGE=1), tiers on one stream or three (GX_CDLP_STREAMS=1): label values stay the
-    caller's vertex ids, so every layout matches the oracle exactly."""
+    order: label values stay the caller's vertex ids, so both layouts match the oracle
+    exactly."""
     monkeypatch.setenv("GX_CDLP_RELABEL", relabel)
-    monkeypatch.setenv("GX_CDLP_STAGE", stage)
-    monkeypatch.setenv("GX_CDLP_STREAMS", streams)
     for g in (_rmat(12, 16, 2), _rmat(11, 8, 3, undirected=False), _G(_tier_graph(False), False),
               _G(_tier_graph(True), True)):
         for iters in (1, 3, 10):
