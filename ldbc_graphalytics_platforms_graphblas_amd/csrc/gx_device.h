@@ -116,7 +116,7 @@ namespace gx {
 int ensure_aux_streams(gx_ctx *ctx);
 // Device -> host copy of `count` elements through the context's pinned staging buffers, the
 // conversion of each chunk (parallel, on the host) overlapping the next chunk's DMA.
-enum class Xfer { Raw64, Levels, Widen32 };   // f64/u64 as is; int32 level -> int64 (INF); int32 -> uint64
+enum class Xfer { Raw64, Raw32, Levels, Widen32 };   // 8 / 4 B as is; int32 level -> int64 (INF); int32 -> uint64
 int download(gx_ctx *ctx, void *dst, const void *src_dev, uint64_t count, Xfer kind);
 // SSSP edge layout: every row of A split into its light (w < delta) edges, then its heavy
 // ones; built once per graph and delta by gx_sssp.
@@ -213,6 +213,13 @@ int device_end(gx_ctx *ctx);
 // Radix sort of (u64 key, u32 value) pairs on bits [0, end_bit) of the key, into k_out / v_out.
 int sort_pairs_u64_u32(uint64_t *k_in, uint64_t *k_out, uint32_t *v_in, uint32_t *v_out, size_t m, int end_bit,
                        hipStream_t s);
+// Radix sorts / scan on the context's stream (rocPRIM), each synchronising before it returns.
+int sort_keys_u64(uint64_t *k_in, uint64_t *k_out, size_t m, int end_bit, hipStream_t s);
+int sort_pairs_u32_u16(uint32_t *k_in, uint32_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
+                       hipStream_t s);
+int sort_pairs_u64_u16(uint64_t *k_in, uint64_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
+                       hipStream_t s);
+int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s);
 int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,
                      int32_t *ci, hipStream_t s);
 

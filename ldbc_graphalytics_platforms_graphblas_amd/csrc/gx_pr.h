@@ -129,10 +129,6 @@ struct PrPart {
     int long_nnz = 65536;        // longer rows take the LONG segment path
     int sorted_lds = 0;          // dynamic LDS bytes of the launch
     uint32_t nsorted = 0, nlong_pad = 0;
-    // rows without entries (a suffix of the hub-first order): row-range workgroups
-    int64_t sfx0 = 0;            // first such row
-    uint32_t nsfx = 0;           // their workgroups
-    int32_t sfx_slot0 = -1;      // their first dangling slot, -1: none dangling
     // dangling-score sum fused into the kernel: blocks holding out-degree-0 rows publish a
     // partial, the last of them adds them up in slot order
     bool fused_dangling = false;
@@ -141,6 +137,14 @@ struct PrPart {
     DBuf<uint32_t> fdticket;
     uint32_t ndblocks = 0;
     int kernel = 2;              // 1 = k_pr_pull (CSR-Adaptive, GX_PR_KERNEL=adaptive), 2 = k_pr_pull_units
+    // where the sorted plan reads its entries: local row i is row order[i] of (src_rp, src_ci)
+    // with every column c renamed perm[c] (gx_pagerank's hub-first plan), or row i itself with
+    // its columns as stored (order / perm null: a partition already in its final order)
+    const int64_t *src_rp = nullptr;
+    const int32_t *src_ci = nullptr;
+    const int32_t *src_order = nullptr;
+    const int32_t *src_perm = nullptr;
+    DBuf<int32_t> order;       // hub-first position -> old vertex id (gx_pagerank)
     // single-GPU driver buffers (gx_pagerank): vertices relabelled hub-first
     DBuf<double> xa, xb, rank_out, result;
     DBuf<int32_t> perm;        // old vertex id -> position in the hub-first order

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <numeric>
 
 #include "gx_pr.h"
@@ -374,14 +375,21 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
         }
         GX_HIP_TRY(hipMemset(p->long_ticket.p, 0, p->long_ticket.n * 4));
     }
-    // dangling rows
-    std::vector<int32_t> dl;
+    // dangling rows: one contiguous range (hub-first orders put them last), or a list
+    int64_t nd = 0, dfirst = -1, dlast = -1;
     for (int64_t i = 0; i < rows; i++)
-        if (h_outdeg[i] == 0) dl.push_back((int32_t)i);
-    p->nd = dl.size();
-    p->d_range = !dl.empty() && (int64_t)dl.back() - dl.front() + 1 == (int64_t)dl.size();
-    p->d0 = dl.empty() ? 0 : dl.front();
+        if (h_outdeg[i] == 0) {
+            nd++;
+            if (dfirst < 0) dfirst = i;
+            dlast = i;
+        }
+    p->nd = (uint64_t)nd;
+    p->d_range = nd > 0 && dlast - dfirst + 1 == nd;
+    p->d0 = nd > 0 ? dfirst : 0;
     if (!p->d_range) {
+        std::vector<int32_t> dl;
+        for (int64_t i = 0; i < rows; i++)
+            if (h_outdeg[i] == 0) dl.push_back((int32_t)i);
         GX_TRY(p->dlist.alloc(std::max<size_t>(dl.size(), 1)));
         if (!dl.empty())
             GX_HIP_TRY(hipMemcpy(p->dlist.p, dl.data(), dl.size() * 4, hipMemcpyHostToDevice));
@@ -477,6 +485,31 @@ __global__ void k_gather_perm(const double *__restrict__ in, const int32_t *__re
         out[v] = in[perm[v]];
 }
 
+// Device hub-first order: keys (2^31 - 1 - outdeg) << 32 | v sort ascending into out-degree
+// descending, ties by id (the host hub_order's order, which the adaptive kernel's plan keeps).
+__global__ void k_hub_keys(const int32_t *__restrict__ outdeg, int64_t n, uint64_t *__restrict__ keys) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        keys[v] = ((uint64_t)(0x7fffffffu - (uint32_t)outdeg[v]) << 32) | (uint64_t)v;
+}
+
+// order[i] = v, perm[v] = i, the hub-first row's out-degree and pull length (plen[n] = 0, so an
+// exclusive scan of n + 1 values gives the relabelled row pointers)
+__global__ void k_hub_apply(const uint64_t *__restrict__ keys, int64_t n, const int32_t *__restrict__ outdeg,
+                            const int64_t *__restrict__ prp, int32_t *__restrict__ order, int32_t *__restrict__ perm,
+                            int32_t *__restrict__ nout, int64_t *__restrict__ plen) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i == n) {
+            plen[n] = 0;
+            continue;
+        }
+        const int32_t v = (int32_t)(uint32_t)keys[i];
+        order[i] = v;
+        perm[v] = (int32_t)i;
+        nout[i] = outdeg[v];
+        plen[i] = prp[v + 1] - prp[v];
+    }
+}
+
 // Hub-first order: vertices by out-degree descending, ties by id (stable counting sort).
 // The pull SpMV gathers x(u) once per out-edge of u, so this packs the most gathered
 // entries of x into its first few MiB, which stay resident in each XCD's 4 MiB L2.
@@ -498,7 +531,9 @@ void hub_order(const std::vector<int32_t> &outdeg, std::vector<int32_t> &order, 
 
 }  // namespace
 
-int gx::pr_single_plan(gx_graph *g, PrPart **out) {
+// The CSR-Adaptive kernel's plan (GX_PR_KERNEL=adaptive): the hub-first relabelled pull CSR
+// itself, built by a radix sort of (perm[row] << 32 | perm[col]) keys.
+static int pr_single_plan_adaptive(gx_graph *g, PrPart **out) {
     const uint64_t n = g->n;
     gx_ctx *ctx = g->ctx;
     hipStream_t s = ctx->stream;
@@ -564,6 +599,67 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
         return rc;
     }
     *out = p;
+    return GX_SUCCESS;
+}
+
+// gx_pagerank's plan: the hub-first order on the device (a radix sort of n keys), the
+// relabelled row pointers by a scan, then the column-sorted blocks read straight from the
+// caller's pull matrix through order / perm (pr_plan_sorted's one radix sort): no relabelled
+// CSR is materialised.  The host sees only the row pointers and out-degrees it plans blocks
+// from.  Replaces LAGraph_Cached_OutDegree / LAGraph_Cached_AT's share of processing time
+// (pr.cpp:58-60).
+int gx::pr_single_plan(gx_graph *g, PrPart **out) {
+    if (const char *e = std::getenv("GX_PR_KERNEL"))
+        if (std::strcmp(e, "adaptive") == 0) return pr_single_plan_adaptive(g, out);
+    const uint64_t n = g->n;
+    gx_ctx *ctx = g->ctx;
+    hipStream_t s = ctx->stream;
+    DevCSR &P = g->directed ? g->AT : g->A;
+    PlanClock clk("single", s);
+    GX_TRY(ensure_outdeg(g));
+    std::unique_ptr<PrPart> p(new PrPart());
+    p->ctx = ctx;
+    p->n_global = n;
+    p->nranks = 1;
+    p->rank = 0;
+    p->chunk = round_up(n + 1, 32);
+    GX_TRY(p->perm.alloc(n));
+    GX_TRY(p->order.alloc(n));
+    GX_TRY(p->rp_own.alloc(n + 1));
+    GX_TRY(p->outdeg_own.alloc(n));
+    GX_TRY(p->xa.alloc(p->chunk));
+    GX_TRY(p->xb.alloc(p->chunk));
+    GX_TRY(p->rank_out.alloc(n));
+    GX_TRY(p->result.alloc(n));
+    {
+        DBuf<uint64_t> k0, k1;
+        DBuf<int64_t> plen;
+        GX_TRY(k0.alloc(n));
+        GX_TRY(k1.alloc(n));
+        GX_TRY(plen.alloc(n + 1));
+        const unsigned grid = grid_for(n + 1, 256, 8192);
+        hipLaunchKernelGGL(k_hub_keys, dim3(grid), dim3(256), 0, s, g->outdeg.p, (int64_t)n, k0.p);
+        GX_TRY(check_launch("k_hub_keys"));
+        GX_TRY(sort_keys_u64(k0.p, k1.p, n, 64, s));
+        hipLaunchKernelGGL(k_hub_apply, dim3(grid), dim3(256), 0, s, k1.p, (int64_t)n, g->outdeg.p, P.rp.p, p->order.p,
+                           p->perm.p, p->outdeg_own.p, plen.p);
+        GX_TRY(check_launch("k_hub_apply"));
+        GX_TRY(scan_exclusive_i64(plen.p, p->rp_own.p, n + 1, s));
+    }
+    clk.mark("hub order + row pointers (device)");
+    std::vector<int64_t> nrp(n + 1);
+    std::vector<int32_t> nout(n);
+    GX_TRY(download(ctx, nrp.data(), p->rp_own.p, n + 1, Xfer::Raw64));
+    GX_TRY(download(ctx, nout.data(), p->outdeg_own.p, n, Xfer::Raw32));
+    clk.mark("row pointers to the host");
+    p->src_rp = P.rp.p;
+    p->src_ci = P.ci.p;
+    p->src_order = p->order.p;
+    p->src_perm = p->perm.p;
+    GX_TRY(pr_plan(p.get(), nrp, p->rp_own.p, nullptr, p->outdeg_own.p, nout));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors above die at return
+    clk.mark("pr_plan");
+    *out = p.release();
     return GX_SUCCESS;
 }
 
@@ -677,6 +773,8 @@ int gx::pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint
         e = hipMemcpy(p->outdeg_own.p, h_outdeg.data(), rows * 4, hipMemcpyHostToDevice);
     if (rc == GX_SUCCESS && e != hipSuccess)
         rc = fail(GX_DEVICE_ERROR, std::string("gx_pr_part_create upload: ") + hipGetErrorString(e));
+    p->src_rp = p->rp_own.p;
+    p->src_ci = p->ci_own.p;
     if (rc == GX_SUCCESS) rc = pr_plan(p, h_rp, p->rp_own.p, p->ci_own.p, p->outdeg_own.p, h_outdeg);
     if (rc != GX_SUCCESS) {
         delete p;

@@ -25,10 +25,10 @@
 // Each sorted block is cut into interleaved units (one workgroup each, LDS accumulators for
 // every row of the block); a multi-unit block's units combine through write-through slabs and
 // an arrival ticket.  Rows longer than `long_nnz` take the LONG path (a workgroup per
-// 8192-entry segment, in row order); their workgroups come first.  Rows without any entry
-// (the isolated vertices of an undirected graph, 29.5 % of SYN-7_5; rows without in-edges of
-// a directed one) form the plan's suffix and are handled by a few row-range workgroups at the
-// end of the grid: r = teleport, no LDS, no gathers.
+// 8192-entry segment, in row order); their workgroups come first.  A block without any entry
+// (isolated vertices: 29.5 % of SYN-7_5's rows) runs only the epilogue.  Its rows were also
+// tried as 64 Ki-row blocks at the end of the grid: a CU streams one such block's epilogue at
+// ~100 GB/s, ~15 us, which lengthened the launch (SYN-7_5 100-104 us against 85-86).
 #include <algorithm>
 #include <functional>
 #include <queue>
@@ -45,7 +45,6 @@ constexpr int kRowBits = 14;     // packed entry: (column - group base) << kRowB
 constexpr int kBS = 1024;        // threads of a k_pr_pull_units workgroup (16 waves, one per CU)
 constexpr int kU = 8;            // entries per lane and round (two 16-B index loads)
 constexpr int kRound = kBS * kU; // entries of one round of a workgroup
-constexpr int kSfxRows = 64 * kBS;   // suffix rows per row-range workgroup
 
 struct SortedArgs {
     const RowBlock *blocks;
@@ -76,9 +75,6 @@ struct SortedArgs {
     uint32_t nunits;
     double *uslab;
     uint32_t *uticket;
-    // rows without entries: [sfx0, rows), kSfxRows per workgroup after the units
-    int64_t sfx0, rows;
-    int32_t sfx_slot0;       // their dangling slots (sfx_slot0 + k), -1: none
     uint64_t *utimes;        // debug (GX_PR_UNIT_TIMES): per workgroup start, gather end, end, XCC
     double *xd;              // x of the rows past `live` (store_x, gx_pr.h)
     int64_t live;
@@ -310,8 +306,7 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
 }
 
 // One iteration's SpMV over split blocks.  Grid: [0, nlong_pad) LONG row segments (padded to a
-// multiple of 8), then the units (largest first), then the row-range workgroups of the rows
-// without entries.  A multi-unit block's units store their row sums write-through (sc1) to
+// multiple of 8), then the units (largest first; the blocks of rows without entries last).  A multi-unit block's units store their row sums write-through (sc1) to
 // their own slab, drain them (vmcnt(0)) and take a ticket; the last arriver adds the slabs in
 // unit order with sc1 loads and runs the epilogue (MI355X_MICROARCH.md "Valid forms": sc1 stores
 // drained before the counter add, sc1 loads by the workgroup whose add came last).
@@ -343,24 +338,18 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
         stamp();
         return;
     }
-    if (w >= a.nlong_pad + a.nunits) {
-        // rows without entries: r = teleport
-        const int64_t k = w - a.nlong_pad - a.nunits;
-        const int64_t r0 = a.sfx0 + k * kSfxRows, r1 = min(r0 + kSfxRows, a.rows);
-        double d = 0.0;
-        for (int64_t r = r0 + tid; r < r1; r += kBS) d += sorted_epilogue(a, r, 0.0, teleport);
-        if (a.dslot && a.sfx_slot0 >= 0) dangling_publish(a, a.sfx_slot0 + (int32_t)k, d, wred, &last);
-        if (TIMES && tid == 0) ts[1] = ts[0];
-        stamp();
-        return;
-    }
     const SortedUnit u = a.units[w - a.nlong_pad];
     const RowBlock b = a.blocks[u.blk];
     const int nrows = b.row_end - b.row_begin;
-    for (int i = tid; i < nrows; i += kBS) acc[i] = 0.0;
-    __syncthreads();
-    gather_units<PROBE>(a, b, u.lo, u.hi, acc, u.step);
-    __syncthreads();
+    // a block without entries (the isolated vertices a hub-first undirected graph puts last):
+    // r = teleport, no accumulators, no gathers
+    const bool empty = b.nz_begin == b.nz_end;
+    if (!empty) {
+        for (int i = tid; i < nrows; i += kBS) acc[i] = 0.0;
+        __syncthreads();
+        gather_units<PROBE>(a, b, u.lo, u.hi, acc, u.step);
+        __syncthreads();
+    }
     if (TIMES && tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
     if (u.nunits > 1) {
         double *mine = a.uslab + u.slab + (int64_t)u.unit * nrows;
@@ -400,7 +389,10 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
         // each thread reads back only the acc entries it wrote: no barrier needed
     }
     double d = 0.0;
-    for (int i = tid; i < nrows; i += kBS) d += sorted_epilogue(a, b.row_begin + i, acc[i], teleport);
+    if (empty)
+        for (int i = tid; i < nrows; i += kBS) d += sorted_epilogue(a, b.row_begin + i, 0.0, teleport);
+    else
+        for (int i = tid; i < nrows; i += kBS) d += sorted_epilogue(a, b.row_begin + i, acc[i], teleport);
     if (a.dslot) {
         const int32_t slot = a.dslot[u.blk];
         if (slot >= 0) dangling_publish(a, slot, d, wred, &last);
@@ -408,41 +400,85 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
     stamp();
 }
 
-// keys[coff + t] = (block << 32) | column, vals = block-relative row, for the t-th entry of
-// sorted block `blockIdx.x` (one workgroup per block, a wave per row).
-__global__ __launch_bounds__(256) void k_sorted_keys(const RowBlock *__restrict__ blocks, const int64_t *__restrict__ coff,
-                                                     const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
-                                                     uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
-    const RowBlock b = blocks[blockIdx.x];
-    const int64_t base = coff[blockIdx.x] - b.nz_begin;
-    const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-    for (int32_t i = wave; i < b.row_end - b.row_begin; i += 256 / kWave) {
-        const int32_t row = b.row_begin + i;
-        for (int64_t e = rp[row] + lane; e < rp[row + 1]; e += kWave) {
-            keys[base + e] = ((uint64_t)blockIdx.x << 32) | (uint32_t)ci[e];
-            vals[base + e] = (uint32_t)i;
+// The plan's one radix sort.  The rows are cut into segments, in row order: the sorted blocks
+// and each LONG row (a sorted block's rows, or one LONG row).  Entry e of local row i gets key
+// (segment << colbits) | column and value i - (its segment's first row); sorted, every
+// segment's entries keep its CSR range [rp[row_begin], rp[row_end]) and come out in column
+// order.  Local row i is row order[i] of the source CSR with columns renamed perm[c]
+// (gx_pagerank's hub-first relabelling, never materialised), or row i itself (order / perm
+// null).  Sixteen entries per thread, the row found once by a binary search of the row
+// pointers.
+struct KeySrc {
+    const int64_t *rp;          // local row pointers (the plan's, row order)
+    int64_t rows;
+    const int64_t *srp;         // source CSR
+    const int32_t *sci;
+    const int32_t *order;       // null: identity
+    const int32_t *perm;        // null: columns as stored
+    const int32_t *seg_row;     // nseg + 1 segment row starts
+    int32_t nseg;
+    int colbits;
+};
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_sorted_keys(KeySrc k, int64_t nnz, K *__restrict__ keys, uint16_t *__restrict__ vals) {
+    constexpr int kPer = 16;
+    const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPer;
+    if (e0 >= nnz) return;
+    const int64_t e1 = min(e0 + kPer, nnz);
+    int64_t i = row_of_edge(k.rp, k.rows, e0);
+    int lo = 0, hi = k.nseg;   // segment of row i: seg_row[lo] <= i < seg_row[lo + 1]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (k.seg_row[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    for (int64_t e = e0; e < e1; e++) {
+        while (k.rp[i + 1] <= e) {
+            i++;
+            while (lo + 1 < k.nseg && k.seg_row[lo + 1] <= i) lo++;
         }
+        const int64_t v = k.order ? k.order[i] : i;
+        const int32_t c0 = k.sci[k.srp[v] + (e - k.rp[i])];
+        const uint32_t c = (uint32_t)(k.perm ? k.perm[c0] : c0);
+        keys[e] = ((K)lo << k.colbits) | (K)c;
+        vals[e] = (uint16_t)(i - k.seg_row[lo]);
     }
 }
 
-// spk / sci / gbase of the sorted block `blockIdx.x` straight from the sorted (key, row) pairs:
-// 64-entry groups aligned to the block's first entry (the kernel's wave-instructions).
-__global__ __launch_bounds__(256) void k_sorted_pack(const RowBlock *__restrict__ blocks, const int64_t *__restrict__ coff,
-                                                     const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
-                                                     int32_t *__restrict__ sci, uint32_t *__restrict__ spk,
-                                                     uint32_t *__restrict__ gbase) {
-    const RowBlock b = blocks[blockIdx.x];
-    const int64_t c0 = coff[blockIdx.x], E = b.nz_end - b.nz_begin;
-    for (int64_t t = threadIdx.x; t < E; t += 256) {
-        const int64_t g = t >> 6;
-        const uint32_t col = (uint32_t)keys[c0 + t];
-        const uint32_t base = (uint32_t)keys[c0 + (g << 6)];
-        const uint32_t lastc = (uint32_t)keys[c0 + min((g << 6) + 63, E - 1)];
+// sci / spk / gbase from the sorted (key, row) pairs: every entry's column into sci (the LONG
+// path and the escape groups read it), and for the sorted blocks (segments with gseg >= 0) the
+// packed entries and the base of each 64-entry group, aligned to the block's first entry (the
+// kernel's wave-instructions).
+struct SegDesc {
+    int64_t z0, z1;
+    int32_t gseg;   // the block's first group in gbase, -1 for a LONG row
+    int32_t pad;
+};
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_sorted_pack(const SegDesc *__restrict__ segs, int32_t nseg, int64_t nnz,
+                                                     const K *__restrict__ keys, const uint16_t *__restrict__ vals,
+                                                     uint32_t colmask, int32_t *__restrict__ sci,
+                                                     uint32_t *__restrict__ spk, uint32_t *__restrict__ gbase) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = nseg;   // the segment holding e: segs[lo].z0 <= e < segs[lo].z1
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (segs[mid].z0 <= e) lo = mid;
+            else hi = mid;
+        }
+        const SegDesc sg = segs[lo];
+        const uint32_t col = (uint32_t)keys[e] & colmask;
+        sci[e] = (int32_t)col;
+        if (sg.gseg < 0) continue;
+        const int64_t t = e - sg.z0, g = t >> 6;
+        const uint32_t base = (uint32_t)keys[sg.z0 + (g << 6)] & colmask;
+        const uint32_t lastc = (uint32_t)keys[min(sg.z0 + (g << 6) + 63, sg.z1 - 1)] & colmask;
         const bool esc = lastc - base >= (1u << (32 - kRowBits));
-        const uint32_t row = vals[c0 + t];
-        sci[b.nz_begin + t] = (int32_t)col;
-        spk[b.nz_begin + t] = esc ? row : ((col - base) << kRowBits) | row;
-        if ((t & 63) == 0) gbase[b.seg + g] = esc ? (base | 0x80000000u) : base;
+        const uint32_t row = vals[e];
+        spk[e] = esc ? row : ((col - base) << kRowBits) | row;
+        if ((t & 63) == 0) gbase[sg.gseg + g] = esc ? (base | 0x80000000u) : base;
     }
 }
 
@@ -554,18 +590,12 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     p->sorted_nnz = (int)B;
     PlanClock clk("sorted", p->ctx->stream);
     const int64_t R = p->sorted_rows, LT = std::max<int64_t>(p->long_nnz, 1);
-    // the trailing rows without entries (isolated vertices of a hub-first undirected graph);
-    // GX_PR_SUFFIX=0 keeps them in sorted blocks
-    int64_t sfx0 = rows;
-    while (sfx0 > 0 && h_rp[sfx0 - 1] == h_rp[rows]) sfx0--;
-    if (env_int("GX_PR_SUFFIX", 1, 0, 1) == 0) sfx0 = rows;
-    p->sfx0 = sfx0;
     std::vector<RowBlock> longb, sortb;
     std::vector<int32_t> lfirst, lnseg;
     std::vector<std::pair<int64_t, int32_t>> longrows;
     int32_t nsegs = 0;
     int64_t r = 0;
-    while (r < sfx0) {
+    while (r < rows) {
         const int64_t len = h_rp[r + 1] - h_rp[r];
         if (len > LT) {
             longrows.push_back({len, (int32_t)r});
@@ -574,7 +604,7 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         }
         const int64_t start = r;
         int64_t nz = 0;
-        while (r < sfx0 && r - start < R) {
+        while (r < rows && r - start < R) {
             const int64_t l = h_rp[r + 1] - h_rp[r];
             if (l > LT || nz + l > B) break;
             nz += l;
@@ -582,6 +612,8 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         }
         sortb.push_back({h_rp[start], h_rp[r], (int32_t)start, (int32_t)r, -1, 0});
     }
+    int64_t maxrows = 1;   // LDS accumulators
+    for (const RowBlock &b : sortb) maxrows = std::max<int64_t>(maxrows, b.row_end - b.row_begin);
     // seg of a sorted block = index of its first 64-entry group in gbase
     int64_t ngroups = 0;
     for (RowBlock &b : sortb) {
@@ -601,8 +633,6 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         }
         nsegs += nseg;
     }
-    int64_t maxrows = 1;
-    for (const RowBlock &b : sortb) maxrows = std::max<int64_t>(maxrows, b.row_end - b.row_begin);
     p->sorted_lds = (int)(maxrows * sizeof(double));
     std::vector<RowBlock> all(longb);
     all.insert(all.end(), sortb.begin(), sortb.end());
@@ -624,45 +654,76 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     GX_HIP_TRY(hipMemset(p->long_ticket.p, 0, p->long_ticket.n * 4));
     clk.mark("blocks (host)");
 
-    // block-sorted columns and packed entries (entries of LONG rows stay unused there)
+    // block-sorted columns and packed entries, by one radix sort of (segment, column) keys
     GX_TRY(p->sci.alloc(std::max<uint64_t>(nnz, 1), 16));
     GX_TRY(p->spk.alloc(std::max<uint64_t>(nnz, 1), 16));
     GX_TRY(p->gbase.alloc(std::max<int64_t>(ngroups, 1), 16));
     hipStream_t s = p->ctx->stream;
-    std::vector<int64_t> coff(sortb.size());
-    int64_t m = 0;
-    for (size_t j = 0; j < sortb.size(); j++) {
-        coff[j] = m;
-        m += sortb[j].nz_end - sortb[j].nz_begin;
-    }
     const RowBlock *d_sort = p->blocks.p + longb.size();
-    if (m > 0) {
-        DBuf<int64_t> d_coff;
-        DBuf<uint64_t> k0, k1;
-        DBuf<uint32_t> v0, v1;
-        GX_TRY(d_coff.alloc(coff.size()));
-        GX_TRY(k0.alloc(m));
-        GX_TRY(k1.alloc(m));
-        GX_TRY(v0.alloc(m));
-        GX_TRY(v1.alloc(m));
-        GX_HIP_TRY(hipMemcpy(d_coff.p, coff.data(), coff.size() * 8, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(k_sorted_keys, dim3((unsigned)sortb.size()), dim3(256), 0, s, d_sort, d_coff.p, p->rp, p->ci,
-                           k0.p, v0.p);
-        GX_TRY(check_launch("k_sorted_keys"));
-        int bits = 1;
-        while ((1ull << bits) < sortb.size()) bits++;
-        GX_TRY(sort_pairs_u64_u32(k0.p, k1.p, v0.p, v1.p, (size_t)m, 32 + bits, s));
-        hipLaunchKernelGGL(k_sorted_pack, dim3((unsigned)sortb.size()), dim3(256), 0, s, d_sort, d_coff.p, k1.p, v1.p,
-                           p->sci.p, p->spk.p, p->gbase.p);
+    if (nnz > 0) {
+        // segments in row order: the sorted blocks and the LONG rows
+        std::vector<std::pair<int32_t, int32_t>> order_;   // (first row, index: block i >= 0, LONG row -1 - j)
+        for (size_t i = 0; i < sortb.size(); i++) order_.push_back({sortb[i].row_begin, (int32_t)i});
+        for (size_t j = 0; j < longrows.size(); j++) order_.push_back({longrows[j].second, -1 - (int32_t)j});
+        std::sort(order_.begin(), order_.end());
+        std::vector<int32_t> seg_row;
+        std::vector<SegDesc> segd;
+        for (const auto &o : order_) {
+            const int32_t r0 = o.first;
+            const bool blk = o.second >= 0;
+            const int32_t r1 = blk ? sortb[o.second].row_end : r0 + 1;
+            seg_row.push_back(r0);
+            segd.push_back({h_rp[r0], h_rp[r1], blk ? sortb[o.second].seg : -1, 0});
+        }
+        seg_row.push_back((int32_t)rows);
+        int colbits = 1;
+        const uint64_t ncols = p->chunk * (uint64_t)p->nranks;
+        while ((1ull << colbits) < ncols) colbits++;
+        int segbits = 1;
+        while ((1ull << segbits) < segd.size()) segbits++;
+        DBuf<int32_t> d_seg_row;
+        DBuf<SegDesc> d_segd;
+        GX_TRY(d_seg_row.alloc(seg_row.size()));
+        GX_TRY(d_segd.alloc(segd.size()));
+        GX_HIP_TRY(hipMemcpyAsync(d_seg_row.p, seg_row.data(), seg_row.size() * 4, hipMemcpyHostToDevice, s));
+        GX_HIP_TRY(hipMemcpyAsync(d_segd.p, segd.data(), segd.size() * sizeof(SegDesc), hipMemcpyHostToDevice, s));
+        const KeySrc ks{p->rp, rows, p->src_rp, p->src_ci, p->src_order, p->src_perm, d_seg_row.p,
+                        (int32_t)segd.size(), colbits};
+        const unsigned kgrid = grid_for((nnz + 15) / 16, 256, 1u << 30);
+        const unsigned pgrid = grid_for(nnz, 256, 1u << 20);
+        const uint32_t colmask = (uint32_t)((1ull << colbits) - 1);
+        DBuf<uint16_t> v0, v1;
+        GX_TRY(v0.alloc(nnz));
+        GX_TRY(v1.alloc(nnz));
+        if (segbits + colbits <= 32) {   // 4-byte keys: fewer radix passes, half the key bytes
+            DBuf<uint32_t> k0, k1;
+            GX_TRY(k0.alloc(nnz));
+            GX_TRY(k1.alloc(nnz));
+            hipLaunchKernelGGL(k_sorted_keys<uint32_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, k0.p, v0.p);
+            GX_TRY(check_launch("k_sorted_keys"));
+            GX_TRY(sort_pairs_u32_u16(k0.p, k1.p, v0.p, v1.p, (size_t)nnz, segbits + colbits, s));
+            hipLaunchKernelGGL(k_sorted_pack<uint32_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
+                               (int64_t)nnz, k1.p, v1.p, colmask, p->sci.p, p->spk.p, p->gbase.p);
+        } else {
+            DBuf<uint64_t> k0, k1;
+            GX_TRY(k0.alloc(nnz));
+            GX_TRY(k1.alloc(nnz));
+            hipLaunchKernelGGL(k_sorted_keys<uint64_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, k0.p, v0.p);
+            GX_TRY(check_launch("k_sorted_keys"));
+            GX_TRY(sort_pairs_u64_u16(k0.p, k1.p, v0.p, v1.p, (size_t)nnz, segbits + colbits, s));
+            hipLaunchKernelGGL(k_sorted_pack<uint64_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
+                               (int64_t)nnz, k1.p, v1.p, colmask, p->sci.p, p->spk.p, p->gbase.p);
+        }
         GX_TRY(check_launch("k_sorted_pack"));
         // GX_PR_LANEPERM=0 keeps every group in column order
-        if (env_int("GX_PR_LANEPERM", 1, 0, 1)) {
+        if (env_int("GX_PR_LANEPERM", 1, 0, 1) && !sortb.empty()) {
             hipLaunchKernelGGL(k_sorted_laneperm, dim3(64, (unsigned)sortb.size()), dim3(256), 0, s, d_sort, p->spk.p,
                                p->sci.p);
             GX_TRY(check_launch("k_sorted_laneperm"));
         }
         GX_HIP_TRY(hipStreamSynchronize(s));   // the key buffers are freed at return
     }
+    p->ci = p->sci.p;   // the LONG rows read their (column-sorted) entries there
     clk.mark("keys + sort + pack + laneperm");
     p->nsorted = (uint32_t)sortb.size();
     p->nlong_pad = (p->nlong_blocks + 7u) & ~7u;
@@ -688,8 +749,10 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
             for (const RowBlock &b : longb) lsegs.push_back(b.nz_end - b.nz_begin);
             double best = 0.0;
             const int64_t emax = *std::max_element(ents.begin(), ents.end());
+            // candidates: every round up to 64 rounds, then 4 % apart (the makespan curve is
+            // flat there; every round up to emax cost ~16 ms of host time on SYN-8_5)
             for (int64_t t = kRound; t <= std::max<int64_t>(kRound, emax);
-                 t += t < 256 * kRound ? kRound : 16 * kRound) {
+                 t = t < 64 * kRound ? t + kRound : (t + t / 25 + kRound - 1) / kRound * kRound) {
                 const double ms = pr_unit_makespan(ents, rws, lsegs, t, (int)cus);
                 if (T == 0 || ms < best * 0.999) {
                     best = ms;
@@ -732,17 +795,17 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         // stay adjacent.
         auto cost = [&](const SortedUnit &u) {
             const RowBlock &b = sortb[u.blk - longb.size()];
-            const int64_t E = b.nz_end - b.nz_begin;
-            return (E + u.nunits - 1) / u.nunits + 4 * (int64_t)(b.row_end - b.row_begin);
+            const int64_t E = b.nz_end - b.nz_begin, R = b.row_end - b.row_begin;
+            return (E + u.nunits - 1) / u.nunits + 4 * R;
         };
         std::stable_sort(units.begin(), units.end(),
                          [&](const SortedUnit &x, const SortedUnit &y) { return cost(x) > cost(y); });
         p->nunits = (uint32_t)units.size();
         if (env_int("GX_PR_VERBOSE", 0, 0, 1))
-            std::fprintf(stderr, "[gx_pr] plan: rows %lld (%lld without entries) nnz %llu unit_nnz %lld block_nnz %d "
+            std::fprintf(stderr, "[gx_pr] plan: rows %lld nnz %llu unit_nnz %lld block_nnz %d "
                          "long_nnz %d: %zu sorted blocks, %u LONG blocks (%u rows), %u units, %d multi-unit blocks, "
                          "slab %lld doubles\n",
-                         (long long)rows, (long long)(rows - sfx0), (unsigned long long)nnz, (long long)T,
+                         (long long)rows, (unsigned long long)nnz, (long long)T,
                          p->sorted_nnz, p->long_nnz, sortb.size(), p->nlong_blocks, p->nlong, p->nunits, parts,
                          (long long)slab);
         GX_TRY(p->units.alloc(units.size()));
@@ -752,10 +815,9 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         GX_HIP_TRY(hipMemset(p->uticket.p, 0, p->uticket.n * 4));
     }
     p->unit_nnz = T;
-    p->nsfx = (uint32_t)((rows - sfx0 + kSfxRows - 1) / kSfxRows);
     clk.mark("units");
-    // fused dangling sum: every dangling row in a sorted block or the suffix (none in a LONG
-    // block), slots: the blocks holding dangling rows, then one per suffix workgroup
+    // fused dangling sum: every dangling row in a sorted block (none in a LONG block), one slot
+    // per block holding dangling rows
     {
         std::vector<int32_t> slot(all.size(), -1);
         bool long_dangling = false;
@@ -766,10 +828,6 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
             for (int32_t r2 = all[i].row_begin; r2 < all[i].row_end && !any; r2++) any = h_outdeg[r2] == 0;
             if (any) slot[i] = (int32_t)nd++;
         }
-        bool sfx_dangling = false;
-        for (int64_t r2 = sfx0; r2 < rows && !sfx_dangling; r2++) sfx_dangling = h_outdeg[r2] == 0;
-        p->sfx_slot0 = sfx_dangling ? (int32_t)nd : -1;
-        if (sfx_dangling) nd += p->nsfx;
         p->fused_dangling = p->nd > 0 && nd > 0 && !long_dangling;
         p->ndblocks = nd;
         if (p->fused_dangling) {
@@ -816,14 +874,11 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.nunits = p->nunits;
     a.uslab = p->uslab.p;
     a.uticket = p->uticket.p;
-    a.sfx0 = p->sfx0;
-    a.rows = (int64_t)p->rows;
-    a.sfx_slot0 = p->sfx_slot0;
     a.xd = p->xd.p;
     a.live = (int64_t)p->live;
     a.utimes = nullptr;
     const char *times_path = std::getenv("GX_PR_UNIT_TIMES");   // debug: not under graph capture
-    const uint32_t nw = p->nlong_pad + p->nunits + p->nsfx;
+    const uint32_t nw = p->nlong_pad + p->nunits;
     if (times_path && nw) {
         if (!p->utimes.p) GX_TRY(p->utimes.alloc(4 * (size_t)nw));
         a.utimes = p->utimes.p;
@@ -863,16 +918,12 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                 for (size_t w = 0; w < nw; w++) {
                     if (w >= p->nlong_blocks && w < p->nlong_pad) continue;
                     const bool lng = w < p->nlong_blocks;
-                    const bool sfx = w >= (size_t)p->nlong_pad + p->nunits;
                     long long ents = 0, nrows = 0;
                     int blk = -1, unit = 0, nunits = 1;
                     if (lng) {
                         ents = bs[w].nz_end - bs[w].nz_begin;
                         nrows = 1;
                         blk = (int)w;
-                    } else if (sfx) {
-                        const int64_t k = (int64_t)w - p->nlong_pad - p->nunits;
-                        nrows = std::min<int64_t>(kSfxRows, (int64_t)p->rows - p->sfx0 - k * kSfxRows);
                     } else {
                         const SortedUnit &u = us[w - p->nlong_pad];
                         for (int64_t k0 = u.lo; k0 < u.hi; k0 += u.step) ents += std::min<int64_t>(u.step / u.nunits, u.hi - k0);
@@ -882,7 +933,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                         nrows = bs[u.blk].row_end - bs[u.blk].row_begin;
                     }
                     std::fprintf(f, "%zu %s %d %d %d %lld %lld %llu %llu %llu %llu\n", w,
-                                 lng ? "long" : sfx ? "rows" : "unit", blk, unit, nunits, ents, nrows,
+                                 lng ? "long" : "unit", blk, unit, nunits, ents, nrows,
                                  (unsigned long long)t[4 * w], (unsigned long long)t[4 * w + 1],
                                  (unsigned long long)t[4 * w + 2], (unsigned long long)t[4 * w + 3]);
                 }

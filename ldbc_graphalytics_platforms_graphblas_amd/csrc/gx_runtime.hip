@@ -151,13 +151,16 @@ int slab_rows(const int64_t *rp, int64_t n, int64_t nslabs, int64_t *srow, hipSt
 }
 
 int download(gx_ctx *ctx, void *dst, const void *src_dev, uint64_t count, Xfer kind) {
-    const size_t elem = kind == Xfer::Raw64 ? 8 : 4;
+    const size_t elem = kind == Xfer::Raw64 ? 8 : 4;   // Raw32: 4 as well
     const uint64_t chunk = gx_ctx::kStageBytes / elem;
     hipStream_t s = ctx->stream;
     auto convert = [&](uint64_t off, uint64_t cnt, const void *buf) {
         switch (kind) {
             case Xfer::Raw64:
                 host_copy(static_cast<char *>(dst) + off * 8, buf, cnt * 8);
+                break;
+            case Xfer::Raw32:
+                host_copy(static_cast<char *>(dst) + off * 4, buf, cnt * 4);
                 break;
             case Xfer::Levels:
                 host_levels(static_cast<const int32_t *>(buf), cnt, static_cast<int64_t *>(dst) + off);
@@ -553,6 +556,50 @@ int sort_pairs_u64_u32(uint64_t *k_in, uint64_t *k_out, uint32_t *v_in, uint32_t
     DBuf<char> tmp;
     GX_TRY(tmp.alloc(tmp_bytes));
     GX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+    return GX_SUCCESS;
+}
+
+int sort_keys_u64(uint64_t *k_in, uint64_t *k_out, size_t m, int end_bit, hipStream_t s) {
+    if (!m) return GX_SUCCESS;
+    size_t tmp_bytes = 0;
+    GX_HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, k_in, k_out, m, 0, end_bit, s));
+    DBuf<char> tmp;
+    GX_TRY(tmp.alloc(tmp_bytes));
+    GX_HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, k_in, k_out, m, 0, end_bit, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+    return GX_SUCCESS;
+}
+
+template <typename K>
+static int sort_pairs_k_u16(K *k_in, K *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit, hipStream_t s) {
+    if (!m) return GX_SUCCESS;
+    size_t tmp_bytes = 0;
+    GX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
+    DBuf<char> tmp;
+    GX_TRY(tmp.alloc(tmp_bytes));
+    GX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+    return GX_SUCCESS;
+}
+
+int sort_pairs_u32_u16(uint32_t *k_in, uint32_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
+                       hipStream_t s) {
+    return sort_pairs_k_u16(k_in, k_out, v_in, v_out, m, end_bit, s);
+}
+
+int sort_pairs_u64_u16(uint64_t *k_in, uint64_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
+                       hipStream_t s) {
+    return sort_pairs_k_u16(k_in, k_out, v_in, v_out, m, end_bit, s);
+}
+
+int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s) {
+    if (!m) return GX_SUCCESS;
+    size_t tmp_bytes = 0;
+    GX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, in, out, (int64_t)0, m, rocprim::plus<int64_t>(), s));
+    DBuf<char> tmp;
+    GX_TRY(tmp.alloc(tmp_bytes));
+    GX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tmp_bytes, in, out, (int64_t)0, m, rocprim::plus<int64_t>(), s));
     GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
     return GX_SUCCESS;
 }

@@ -196,7 +196,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                O.pagerank(csr, False, 0.85, 6), rtol=PR_RTOL, atol=0)
 
 
-@pytest.mark.parametrize("env", [{}, {"GX_PR_LANEPERM": "0"}, {"GX_PR_SUFFIX": "0"}, {"GX_PR_UNIT_LDS": "0"},
+@pytest.mark.parametrize("env", [{}, {"GX_PR_LANEPERM": "0"}, {"GX_PR_UNIT_LDS": "0"},
                                  {"GX_PR_KERNEL": "adaptive"},
                                  {"GX_PR_SORTED_ROWS": "16384", "GX_PR_UNIT_NNZ": "16384"},
                                  {"GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SORTED_ROWS": "2048"},
@@ -207,8 +207,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                  {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192", "GX_PR_SORTED_ROWS": "64",
                                   "GX_PR_LANEPERM": "0"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
-    """The default plan, without the lane permutation, with the rows without entries kept in
-    sorted blocks, two workgroups per CU, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
+    """The default plan, without the lane permutation, two workgroups per CU, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
     blocks (several workgroups per sorted block, combined through slabs by the last arriver)
     and the CSR-Adaptive kernel all give the oracle's scores (directed and undirected)."""
     for k, v in env.items():
