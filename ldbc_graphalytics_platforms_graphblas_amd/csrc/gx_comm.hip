@@ -284,6 +284,9 @@ extern "C" int gx_pr_dist_create(gx_comm *comm, gx_pr_part *const *parts, int np
     for (int p = 0; p < npieces && rc == GX_SUCCESS; p++) {
         rc = d.xl[p]->alloc(d.chunk);
         if (rc == GX_SUCCESS) rc = d.ro[p]->alloc(std::max<uint64_t>(d.pieces[p]->rows, 1));
+        // the padding slots (the kernel's zero column among them) stay 0.0 through the exchange
+        if (rc == GX_SUCCESS && hipMemset(d.xl[p]->p, 0, d.chunk * sizeof(double)) != hipSuccess)
+            rc = fail(GX_DEVICE_ERROR, "hipMemset");
     }
     hipError_t e = hipSuccess;
     if (rc == GX_SUCCESS) e = hipMemset(d.xa.p, 0, full * sizeof(double));
@@ -412,7 +415,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     for (int d = 0; d < ndev; d++) maxlive = std::max(maxlive, live[d]);
     MultiRun M;
     M.ndev = ndev;
-    M.chunk = (maxlive + 1 + 31) / 32 * 32;   // + the dangling slot
+    M.chunk = (maxlive + 2 + 31) / 32 * 32;   // + the zero padding slot and the dangling slot
     if (M.chunk * (uint64_t)ndev >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
     // column map: vertex -> its place in the exchanged vector (owner * chunk + local row)
     std::vector<int32_t> colmap(n);
@@ -447,6 +450,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         GX_TRY(M.xw[d]->alloc(full));
         GX_TRY(M.xl[d]->alloc(M.chunk));
         GX_TRY(M.ro[d]->alloc(std::max<uint64_t>(rows[d], 1)));
+        GX_HIP_TRY(hipMemsetAsync(M.xl[d]->p, 0, M.chunk * sizeof(double), ctxs[d]->stream));
         GX_HIP_TRY(hipMemsetAsync(M.xr[d]->p, 0, full * sizeof(double), ctxs[d]->stream));
         GX_HIP_TRY(hipMemsetAsync(M.xw[d]->p, 0, full * sizeof(double), ctxs[d]->stream));
     }

@@ -555,7 +555,7 @@ static int pr_single_plan_adaptive(gx_graph *g, PrPart **out) {
     p->n_global = n;
     p->nranks = 1;
     p->rank = 0;
-    p->chunk = round_up(n + 1, 32);
+    p->chunk = round_up(n + 2, 32);   // + a zero padding slot (chunk - 2) and the dangling slot
     int rc = p->perm.alloc(n);
     if (rc == GX_SUCCESS) rc = p->rp_own.alloc(n + 1);
     if (rc == GX_SUCCESS) rc = p->ci_own.alloc(P.nnz, 16);
@@ -565,7 +565,9 @@ static int pr_single_plan_adaptive(gx_graph *g, PrPart **out) {
     if (rc == GX_SUCCESS) rc = p->rank_out.alloc(n);
     if (rc == GX_SUCCESS) rc = p->result.alloc(n);
     hipError_t e = hipSuccess;
-    if (rc == GX_SUCCESS) e = hipMemcpyAsync(p->perm.p, perm.data(), n * 4, hipMemcpyHostToDevice, s);
+    if (rc == GX_SUCCESS) e = hipMemsetAsync(p->xa.p, 0, p->chunk * sizeof(double), s);
+    if (rc == GX_SUCCESS && e == hipSuccess) e = hipMemsetAsync(p->xb.p, 0, p->chunk * sizeof(double), s);
+    if (rc == GX_SUCCESS && e == hipSuccess) e = hipMemcpyAsync(p->perm.p, perm.data(), n * 4, hipMemcpyHostToDevice, s);
     if (rc == GX_SUCCESS && e == hipSuccess)
         e = hipMemcpyAsync(p->rp_own.p, nrp.data(), (n + 1) * 8, hipMemcpyHostToDevice, s);
     if (rc == GX_SUCCESS && e == hipSuccess)
@@ -622,13 +624,15 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     p->n_global = n;
     p->nranks = 1;
     p->rank = 0;
-    p->chunk = round_up(n + 1, 32);
+    p->chunk = round_up(n + 2, 32);   // + a zero padding slot (chunk - 2) and the dangling slot
     GX_TRY(p->perm.alloc(n));
     GX_TRY(p->order.alloc(n));
     GX_TRY(p->rp_own.alloc(n + 1));
     GX_TRY(p->outdeg_own.alloc(n));
     GX_TRY(p->xa.alloc(p->chunk));
     GX_TRY(p->xb.alloc(p->chunk));
+    GX_HIP_TRY(hipMemsetAsync(p->xa.p, 0, p->chunk * sizeof(double), s));   // padding: the zero column
+    GX_HIP_TRY(hipMemsetAsync(p->xb.p, 0, p->chunk * sizeof(double), s));
     GX_TRY(p->rank_out.alloc(n));
     GX_TRY(p->result.alloc(n));
     {
@@ -728,7 +732,7 @@ extern "C" int gx_pr_part_create_live(gx_ctx *ctx, uint64_t n_global, int nranks
         }
         maxlive = std::max(maxlive, live[k]);
     }
-    const uint64_t chunk = round_up(maxlive + 1, 32);
+    const uint64_t chunk = round_up(maxlive + 2, 32);   // + the zero padding slot and the dangling slot
     if (chunk * (uint64_t)nranks >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "partition too large");
     const uint64_t rows = row_ranges[rank + 1] - row_ranges[rank];
     const uint64_t nnz = rowptr_local[rows];

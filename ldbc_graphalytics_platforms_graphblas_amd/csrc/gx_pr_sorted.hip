@@ -59,6 +59,7 @@ struct SortedArgs {
     int64_t chunk;
     int nranks;
     int zero_slot;
+    int32_t zero_col;        // a padding slot of x that holds 0.0 (chunk - 2)
     double teleport0, damping_over_n, damping;
     const int32_t *long_first;
     const int32_t *long_nseg;
@@ -174,133 +175,162 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 
 // Adds x(column) of the sorted entries [lo, hi) of block b into the LDS row accumulators,
 // taking every (step / kRound)-th round of kRound entries from the one holding lo (the
-// interleaved units of a split block), starting at lo's 64-entry group.
+// interleaved units of a split block; lo - nz_begin is a multiple of kRound).
 //
 // Four entries per lane from one 16-B index load (X4): what bounds the launch is the CU's
-// vector memory and LDS instruction stream, not cache lines (timing probes).  Wave
-// w takes the kU / 4 256-entry supergroups [R + 256 (w kU/4 + v), +256) of round R; lane l
-// holds entries 4l .. 4l+3 of each, all in 64-entry group l / 16 of the supergroup, and the
-// group's four bases are scalar loads selected per lane.  Pipelined across rounds: round k+1's
-// gathers are issued before round k's LDS adds, the index loads two rounds ahead, buffers A/B
-// alternating (a copy of a pending load would wait for it).
+// vector memory and LDS instruction stream (timing probes).  Wave w takes the
+// kU / 4 256-entry supergroups [R + 256 (w kU/4 + v), +256) of round R; lane l holds entries
+// 4l .. 4l+3 of each.  A supergroup has one base column, a scalar load, so a lane's columns are
+// base + (entry >> 14) with no per-lane select.  Pipelined across rounds: round k+1's gathers
+// are issued before round k's LDS adds, the index loads two rounds ahead, buffers A/B
+// alternating (a copy of a pending load would wait for it).  Positions are block-relative
+// 32-bit values.  An entry outside [lo, hi) gathers the zero padding slot x[zero_col] and adds
+// 0.0 to whatever row its (clamped or neighbouring) index word names -- below 16 Ki, and the
+// launch reserves 16 Ki accumulators -- so the hot path has no 64-bit compares or masks.  The
+// columns of escape supergroups (spanning >= 2^18 ids) come from sci inside a uniform branch
+// that consumes its loads there: a load merged into the columns after the branch made the
+// compiler drain every outstanding load (s_waitcnt vmcnt(0)) each round.
 //
 // PROBE (diagnostic builds only, -DGX_PR_PROBES, tools/pr_probe.sh; wrong results by design):
 // 1 no LDS adds (register sum), 2 no gathers, 3 neither, 4 gathers folded into x[c & 4095]
 // (L1 hits), 5 no gathers + conflict-free LDS adds (acc[tid]), 6 gathers + conflict-free LDS
-// adds, 7 no index loads (entries synthesised from the position, columns = the group base).
+// adds, 7 no index loads (entries synthesised from the position, columns = the base).
 template <int PROBE>
-__device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo, int64_t hi,
-                                             double *acc, int64_t step) {
+__device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
+                                             double *acc, int64_t step64) {
     const int tid = threadIdx.x;
-    const int64_t z0 = b.nz_begin, z1 = b.nz_end;
+    const int64_t z0 = b.nz_begin;
+    const int32_t lo = (int32_t)(lo64 - z0), hi = (int32_t)(hi64 - z0), step = (int32_t)step64;
     if (lo >= hi) return;
-    const int64_t glast = (z1 - 1 - z0) >> 6;
-    const int64_t start = z0 + ((lo - z0) & ~(int64_t)(kWave - 1));   // 64-entry group aligned
+    const int32_t last = (int32_t)(b.nz_end - z0) - 1;
+    const int32_t nsg = (last >> 8) + 1;   // supergroups of the block
+    const uint32_t span = (uint32_t)(hi - lo);
+    const uint32_t *spk = a.spk + z0;
+    const int32_t *sci = a.sci + z0;
+    const uint32_t *sgb = a.gbase + b.seg;
+    const int32_t zc = a.zero_col;
+    const char *xb = reinterpret_cast<const char *>(a.x_in);
     const int lane = tid & (kWave - 1);
     constexpr int V = kU / 4;
     const int wave = tid >> 6;
-    const int sub = lane >> 4;
     struct Rd {
         uint4 q[V];
-        uint32_t gbs[V][4];
+        uint32_t bq;   // lane l: the base of supergroup l mod V (a vector load, see below)
     };
     struct Gt {
         double g[kU];
         uint32_t r[kU];
-        bool ok[kU];
     };
-    auto load = [&](Rd &d, int64_t R) {
+    // The supergroup bases come in through one vector load per round (lanes l mod V) read back
+    // with v_readlane: a scalar load's wait (lgkmcnt) would also wait for the LDS adds in flight.
+    auto load = [&](Rd &d, int32_t R) {
+        const int32_t sg0 = R + wave * V * 256;
 #pragma unroll
         for (int v = 0; v < V; v++) {
-            const int64_t sg = R + (int64_t)(wave * V + v) * 256;
+            const int32_t sg = sg0 + v * 256;
             if constexpr (PROBE == 7) {
-                const uint32_t e0 = (uint32_t)(sg + 4 * lane - z0) & 4095u;
+                const uint32_t e0 = (uint32_t)(sg + 4 * lane) & 4095u;
                 d.q[v] = make_uint4(e0, (e0 + 1) & 4095u, (e0 + 2) & 4095u, (e0 + 3) & 4095u);
             } else {
-                // clamped into the block; spk's allocation slack covers the 3 entries past z1 - 1;
+                // clamped into the block; spk's allocation slack covers the 3 entries past `last`;
                 // the address is a CSR offset, only 4-B aligned (gx_u32x4)
-                const gx_u32x4 q4 = *reinterpret_cast<const gx_u32x4 *>(a.spk + min(sg + 4 * lane, z1 - 1));
+                const gx_u32x4 q4 = *reinterpret_cast<const gx_u32x4 *>(spk + min(sg + 4 * lane, last));
                 d.q[v] = make_uint4(q4.x, q4.y, q4.z, q4.w);
             }
-            // readfirstlane is convergent, so the loads cannot sink into the select's branches.
-            // A supergroup past the block's end reads the last group's bases; the up to 3 groups
-            // past the last read the next block's bases or gbase's allocation slack, for entries
-            // that ok[] masks.
-            const int g = __builtin_amdgcn_readfirstlane((int)(b.seg + min((sg - z0) >> 6, glast)));
-#pragma unroll
-            for (int k = 0; k < 4; k++) d.gbs[v][k] = __builtin_amdgcn_readfirstlane(a.gbase[g + k]);
         }
+        d.bq = sgb[min((sg0 >> 8) + (lane & (V - 1)), nsg - 1)];
     };
-    auto issue = [&](const Rd &d, int64_t R, Gt &t) {
+    auto issue = [&](const Rd &d, int32_t R, Gt &t) {
         int32_t c[kU];
-        uint32_t esc = 0, gb[V];
+        uint32_t sb[V], esc = 0;
 #pragma unroll
         for (int v = 0; v < V; v++) {
-            gb[v] = sub == 0 ? d.gbs[v][0] : sub == 1 ? d.gbs[v][1] : sub == 2 ? d.gbs[v][2] : d.gbs[v][3];
+            sb[v] = __builtin_amdgcn_readlane(d.bq, v);
+            esc |= sb[v];
+        }
+#pragma unroll
+        for (int v = 0; v < V; v++) {
             const uint32_t w4[4] = {d.q[v].x, d.q[v].y, d.q[v].z, d.q[v].w};
-            const int64_t e4 = R + (int64_t)(wave * V + v) * 256 + 4 * lane;
+            const int32_t d0 = R + (wave * V + v) * 256 + 4 * lane - lo;
+            const uint32_t base = sb[v] & 0x7fffffffu;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                // entries outside [lo, hi) (and whatever the clamped load brought) gather x(0) and
-                // add 0.0 to row 0
                 const int i = 4 * v + j;
-                t.ok[i] = e4 + j >= lo && e4 + j < hi;
-                t.r[i] = t.ok[i] ? (w4[j] & ((1u << kRowBits) - 1)) : 0u;
-                if constexpr (PROBE == 7) c[i] = t.ok[i] ? (int32_t)(gb[v] & 0x7fffffffu) : 0;
-                else c[i] = t.ok[i] ? (int32_t)(gb[v] + (w4[j] >> kRowBits)) : 0;
+                const bool ok = (uint32_t)(d0 + j) < span;
+                t.r[i] = w4[j] & ((1u << kRowBits) - 1);
+                // materialised here: sunk to the adds, the rows would keep this buffer's index
+                // registers live past its reload, and the allocator copies at the loop latch
+                asm volatile("" : "+v"(t.r[i]));
+                if constexpr (PROBE == 7) c[i] = ok ? (int32_t)base : zc;
+                else c[i] = ok ? (int32_t)(base + (w4[j] >> kRowBits)) : zc;
             }
-            esc |= gb[v];
         }
-        if (PROBE != 7 && __builtin_amdgcn_readfirstlane(__ballot(esc & 0x80000000u) != 0)) {   // an escape group
+        if (PROBE != 7 && (esc & 0x80000000u)) {   // uniform: an escape supergroup in this round
 #pragma unroll
-            for (int v = 0; v < V; v++)
+            for (int v = 0; v < V; v++) {
+                if (!(sb[v] & 0x80000000u)) continue;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const int i = 4 * v + j;
-                    const int64_t e = R + (int64_t)(wave * V + v) * 256 + 4 * lane + j;
-                    if ((gb[v] & 0x80000000u) && t.ok[i]) c[i] = a.sci[e];
+                    const int32_t pos = R + (wave * V + v) * 256 + 4 * lane + j;
+                    if ((uint32_t)(pos - lo) < span) c[i] = sci[pos];
                 }
+            }
+            // consume the loads here: a column register still waiting on one at the branch's end
+            // makes the compiler wait for every load in flight (vmcnt(0)) on both paths
+            __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
         }
 #pragma unroll
         for (int i = 0; i < kU; i++) {
             if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5) t.g[i] = (double)c[i];
             else if constexpr (PROBE == 4) t.g[i] = a.x_in[c[i] & 4095];
-            else t.g[i] = a.x_in[c[i]];
+            else t.g[i] = *reinterpret_cast<const double *>(xb + ((uint32_t)c[i] << 3));
         }
     };
     double rsum = 0.0;   // PROBE 1 / 3
     auto add = [&](const Gt &t) {
 #pragma unroll
         for (int i = 0; i < kU; i++) {
-            if constexpr (PROBE == 1 || PROBE == 3) rsum += t.ok[i] ? t.g[i] : 0.0;
-            else if constexpr (PROBE == 5 || PROBE == 6) atomicAdd(&acc[tid], t.ok[i] ? t.g[i] : 0.0);
-            else atomicAdd(&acc[t.r[i]], t.ok[i] ? t.g[i] : 0.0);
+            if constexpr (PROBE == 1 || PROBE == 3) rsum += t.g[i];
+            else if constexpr (PROBE == 5 || PROBE == 6) atomicAdd(&acc[tid], t.g[i]);
+            else atomicAdd(&acc[t.r[i]], t.g[i]);
         }
     };
+    // Two rounds per trip of a counted loop with a single exit.  The stages are fenced from
+    // the scheduler and the exits are not shared: a load hoisted above the issue that still
+    // reads its buffer, or one exit block adding "tA or tB", makes the register allocator copy
+    // a buffer at the loop latch, and a copy waits for the loads in flight.
+    const int32_t nr = (hi - lo + step - 1) / step;   // rounds of this unit
     Rd dA, dB;
     Gt tA, tB;
-    int64_t R = start;
+    int32_t R = lo;
     load(dA, R);
     load(dB, R + step);
     issue(dA, R, tA);
+    __builtin_amdgcn_sched_barrier(0);
     load(dA, R + 2 * step);
-    for (;;) {
-        if (R + step >= hi) {
-            add(tA);
-            break;
-        }
+    int32_t k = 1;
+    for (; k + 1 < nr; k += 2) {
+        __builtin_amdgcn_sched_barrier(0);
         issue(dB, R + step, tB);
+        __builtin_amdgcn_sched_barrier(0);
         load(dB, R + 3 * step);
+        __builtin_amdgcn_sched_barrier(0);
         add(tA);
-        R += step;
-        if (R + step >= hi) {
-            add(tB);
-            break;
-        }
-        issue(dA, R + step, tA);
-        load(dA, R + 3 * step);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(dA, R + 2 * step, tA);
+        __builtin_amdgcn_sched_barrier(0);
+        load(dA, R + 4 * step);
+        __builtin_amdgcn_sched_barrier(0);
         add(tB);
-        R += step;
+        R += 2 * step;
+    }
+    if (k < nr) {
+        issue(dB, R + step, tB);
+        add(tA);
+        add(tB);
+    } else {
+        add(tA);
     }
     if constexpr (PROBE == 1 || PROBE == 3) atomicAdd(&acc[tid], rsum);
 }
@@ -447,12 +477,12 @@ __global__ __launch_bounds__(256) void k_sorted_keys(KeySrc k, int64_t nnz, K *_
 }
 
 // sci / spk / gbase from the sorted (key, row) pairs: every entry's column into sci (the LONG
-// path and the escape groups read it), and for the sorted blocks (segments with gseg >= 0) the
-// packed entries and the base of each 64-entry group, aligned to the block's first entry (the
-// kernel's wave-instructions).
+// path and the escape supergroups read it), and for the sorted blocks (segments with gseg >= 0)
+// the packed entries and the base column of each 256-entry supergroup, aligned to the block's
+// first entry (the kernel's rounds).
 struct SegDesc {
     int64_t z0, z1;
-    int32_t gseg;   // the block's first group in gbase, -1 for a LONG row
+    int32_t gseg;   // the block's first supergroup in gbase, -1 for a LONG row
     int32_t pad;
 };
 
@@ -472,13 +502,13 @@ __global__ __launch_bounds__(256) void k_sorted_pack(const SegDesc *__restrict__
         const uint32_t col = (uint32_t)keys[e] & colmask;
         sci[e] = (int32_t)col;
         if (sg.gseg < 0) continue;
-        const int64_t t = e - sg.z0, g = t >> 6;
-        const uint32_t base = (uint32_t)keys[sg.z0 + (g << 6)] & colmask;
-        const uint32_t lastc = (uint32_t)keys[min(sg.z0 + (g << 6) + 63, sg.z1 - 1)] & colmask;
+        const int64_t t = e - sg.z0, q = t >> 8;
+        const uint32_t base = (uint32_t)keys[sg.z0 + (q << 8)] & colmask;
+        const uint32_t lastc = (uint32_t)keys[min(sg.z0 + (q << 8) + 255, sg.z1 - 1)] & colmask;
         const bool esc = lastc - base >= (1u << (32 - kRowBits));
         const uint32_t row = vals[e];
         spk[e] = esc ? row : ((col - base) << kRowBits) | row;
-        if ((t & 63) == 0) gbase[sg.gseg + g] = esc ? (base | 0x80000000u) : base;
+        if ((t & 255) == 0) gbase[sg.gseg + q] = esc ? (base | 0x80000000u) : base;
     }
 }
 
@@ -614,11 +644,11 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     }
     int64_t maxrows = 1;   // LDS accumulators
     for (const RowBlock &b : sortb) maxrows = std::max<int64_t>(maxrows, b.row_end - b.row_begin);
-    // seg of a sorted block = index of its first 64-entry group in gbase
+    // seg of a sorted block = index of its first 256-entry supergroup in gbase
     int64_t ngroups = 0;
     for (RowBlock &b : sortb) {
         b.seg = (int32_t)ngroups;
-        ngroups += (b.nz_end - b.nz_begin + 63) / 64;
+        ngroups += (b.nz_end - b.nz_begin + 255) / 256;
     }
     std::stable_sort(longrows.begin(), longrows.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
     for (const auto &lr : longrows) {
@@ -800,6 +830,9 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         };
         std::stable_sort(units.begin(), units.end(),
                          [&](const SortedUnit &x, const SortedUnit &y) { return cost(x) > cost(y); });
+        // (Co-scheduling similar units on one XCD -- slices of 32 dealt to 8 queues, grid slot
+        // 8 i + q -- cut the fabric reads of SYN-8_5 by 9 % and still ran slower: 955 against
+        // 925 us per launch, SYN-7_5 100 against 84; round 3)
         p->nunits = (uint32_t)units.size();
         if (env_int("GX_PR_VERBOSE", 0, 0, 1))
             std::fprintf(stderr, "[gx_pr] plan: rows %lld nnz %llu unit_nnz %lld block_nnz %d "
@@ -857,6 +890,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.chunk = (int64_t)p->chunk;
     a.nranks = p->nranks;
     a.zero_slot = p->nd == 0 ? 1 : 0;
+    a.zero_col = (int32_t)p->chunk - 2;
     a.teleport0 = (1.0 - p->damping) / dn;
     a.damping_over_n = p->damping / dn;
     a.damping = p->damping;
@@ -885,11 +919,11 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     }
     if (nw) {
         KTimer kt(p->ctx, "pr_pull", s);   // one iteration's SpMV (+ fused dangling sum)
-        // One 1024-thread workgroup per CU (GX_PR_UNIT_LDS, bytes: the LDS reserved per
-        // workgroup).  Fewer concurrent sweeps keep the XCD's L2 window of x smaller: SYN-7_5
-        // one per CU 100-104 us per launch against 109-125 with two (tools/pr_units_sweep.sh).
-        const size_t lds = std::max<size_t>((size_t)p->sorted_lds, (size_t)env_int("GX_PR_UNIT_LDS", 96 * 1024, 0,
-                                                                                    160 * 1024 - 4096));
+        // One 1024-thread workgroup per CU, 16 Ki accumulators (128 KiB of LDS) whatever the block's
+        // rows: an entry outside its unit's range adds 0.0 to any row below 16 Ki (gather_units).
+        // One workgroup per CU also keeps fewer concurrent sweeps of x: SYN-7_5 ran 100-104 us per
+        // launch against 109-125 with two (round 2, tools/pr_units_sweep.sh).
+        const size_t lds = (size_t)(1 << kRowBits) * sizeof(double);
         if (a.utimes) {
             hipLaunchKernelGGL((k_pr_pull_units<true>), dim3(nw), dim3(kBS), lds, s, a);
         } else {

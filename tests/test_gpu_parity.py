@@ -196,7 +196,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                O.pagerank(csr, False, 0.85, 6), rtol=PR_RTOL, atol=0)
 
 
-@pytest.mark.parametrize("env", [{}, {"GX_PR_LANEPERM": "0"}, {"GX_PR_UNIT_LDS": "0"},
+@pytest.mark.parametrize("env", [{}, {"GX_PR_LANEPERM": "0"}, {"GX_PR_BLOCK_NNZ": "2097152", "GX_PR_UNIT_NNZ": "16384"},
                                  {"GX_PR_KERNEL": "adaptive"},
                                  {"GX_PR_SORTED_ROWS": "16384", "GX_PR_UNIT_NNZ": "16384"},
                                  {"GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SORTED_ROWS": "2048"},
@@ -207,7 +207,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                  {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192", "GX_PR_SORTED_ROWS": "64",
                                   "GX_PR_LANEPERM": "0"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
-    """The default plan, without the lane permutation, two workgroups per CU, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
+    """The default plan, without the lane permutation, blocks cut into many units, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
     blocks (several workgroups per sorted block, combined through slabs by the last arriver)
     and the CSR-Adaptive kernel all give the oracle's scores (directed and undirected)."""
     for k, v in env.items():
@@ -218,14 +218,33 @@ def test_pagerank_plan_variants(ctx, monkeypatch, env):
 
 
 def test_pagerank_escape_groups(ctx, monkeypatch):
-    """A perfect matching on 2^21 + 64 vertices in 64-row blocks: the 64 columns of a group
-    span more than 2^20 ids, so the groups escape to plain column ids (permuted with the rest
-    of the group by the lane permutation)."""
+    """A perfect matching on 2^21 + 64 vertices in 64-row blocks: the columns of a block's one
+    256-entry supergroup span more than 2^18 ids, so it escapes to plain column ids (permuted
+    with the rest of its 64-entry groups by the lane permutation)."""
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
     monkeypatch.setenv("GX_PR_SORTED_ROWS", "64")
     n = (1 << 21) + 64
     perm = np.random.default_rng(9).permutation(n)
     csr = csr_from_edges(n, perm[0::2], perm[1::2], None, symmetric=True)
+    np.testing.assert_allclose(gpu_run(ctx, _G(csr, False), "PR", damping=0.85, iters=4),
+                               O.pagerank(csr, False, 0.85, 4), rtol=PR_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("laneperm", ["1", "0"])
+def test_pagerank_mixed_escape_rounds(ctx, monkeypatch, laneperm):
+    """Escape and packed supergroups in the same round: 1 Ki rows each linked to the 96 lowest
+    ids (packed supergroups) and to a partner far away (a perfect matching over 2^20 ids: the
+    tail supergroups of a block escape), in 1 Ki-row blocks cut into 8 Ki-entry units."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    monkeypatch.setenv("GX_PR_SORTED_ROWS", "1024")
+    monkeypatch.setenv("GX_PR_UNIT_NNZ", "8192")
+    monkeypatch.setenv("GX_PR_LANEPERM", laneperm)
+    n = 1 << 20
+    perm = np.random.default_rng(10).permutation(n)
+    dense_r = np.repeat(np.arange(96, 4096, dtype=np.int64), 96)
+    dense_c = np.tile(np.arange(96, dtype=np.int64), 4096 - 96)
+    csr = csr_from_edges(n, np.concatenate([perm[0::2], dense_r]), np.concatenate([perm[1::2], dense_c]), None,
+                         symmetric=True)
     np.testing.assert_allclose(gpu_run(ctx, _G(csr, False), "PR", damping=0.85, iters=4),
                                O.pagerank(csr, False, 0.85, 4), rtol=PR_RTOL, atol=0)
 
