@@ -237,6 +237,22 @@ def run_algorithm(args):
         unit = "edges/s"
     if alg != "lcc":
         ref_model_bytes = None
+    split = None
+    if alg == "sssp":
+        # config 4's multi-GPU SSSP path (1-D split, gx_sssp_split) at N = 1: the same rounds,
+        # no exchange -- its device time against gx_sssp's
+        sp = A.SsspSplit(G)
+        try:
+            sp.run(src)
+            sms = []
+            for _ in range(max(1, min(args.steps, 5))):
+                d_split = sp.run(src)
+                sms.append(ctx.last_device_ms())
+            split = {"path": "gx_sssp_split_run (1 rank owning every vertex)", "ms": float(np.median(sms)),
+                     "ratio_vs_gx_sssp": float(np.median(sms)) / (t_dev * 1e3),
+                     "equal_to_gx_sssp": bool(np.array_equal(d_split, out))}
+        finally:
+            sp.close()
     # Graphalytics processing time: upload + the first call (transpose /
     # closure / layout built inside it), as the executables' markers bracket it
     proc_ms = t_up * 1e3 + first_ms
@@ -285,7 +301,7 @@ def run_algorithm(args):
                      "stream_copy_gbs": copy_gbs, "frac_of_stream": nbytes / t_dev / 1e9 / copy_gbs},
         "processing_ms": proc_ms,
         "evps": (n + (nnz if directed else nnz // 2)) / (proc_ms / 1e3),
-        "cpu_baseline": cpu, "parity_vs_oracle": parity, "first_call_ms": first_ms,
+        "cpu_baseline": cpu, "parity_vs_oracle": parity, "first_call_ms": first_ms, "split_n1": split,
         "wall_ms_per_call_incl_d2h": wall * 1e3 / args.steps, "graph_gen_s": t_gen,
     }
     print(json.dumps(line), flush=True)
@@ -430,7 +446,9 @@ def measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True):
     # ranks, so each owns n / (N * pieces) rows AND ~nnz / (N * pieces) entries and the
     # exchanged vector is ~n long (interleaved_relabel); GX_PR_PARTITION=ranges keeps the
     # round-1 contiguous hub-first ranges balanced by entries.
-    pieces = max(1, int(os.environ.get("GX_PR_PIECES", "1"))) if dist else 1
+    # (at N = 1, GX_PR_PIECES = 8 runs the 8 rank shares of config 4 on one GPU back to back:
+    # the per-piece launch against 1/8 of the whole-graph launch is the per-rank efficiency)
+    pieces = max(1, int(os.environ.get("GX_PR_PIECES", "1")))
     vranks = world * pieces
     partition = os.environ.get("GX_PR_PARTITION", "interleave")
     if partition == "ranges":

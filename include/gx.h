@@ -300,9 +300,15 @@ int gx_pr_partition(uint64_t n, const uint64_t *rowptr, int nparts, uint32_t *or
  * WCC  : init(parent); per round: zero changed; hook(owned rows' edges, then compress);
  *        all-reduce MIN(parent); compress; all-reduce MAX(changed); stop when 0.
  *        parent[v] is then the smallest vertex id of v's component.
- * SSSP : init(dist, prev); per round: zero active; round(owned); all-reduce MIN(dist as
- *        int64); all-reduce SUM(active); stop when active == 0.  dist holds fp64 bit
- *        patterns (+inf = unreached).
+ * SSSP : split_create(owned targets [v0, v1)) once -- the edges into owned vertices, by
+ *        source, light first; split_start(src); per round: split_relax(-> this rank's
+ *        improved owned vertices as (vertex, fp64 bits) pairs + count[2] = {pairs, done});
+ *        all-gather the count words; stop when done; all-gather the first 2 max-count words
+ *        of every rank's pairs; split_apply(all ranks' pairs, the gathered counts, nranks,
+ *        stride = max count).  The distance vector is replicated: every rank applies every
+ *        improvement and takes the same delta-stepping decisions.  split_distances copies it
+ *        out (fp64, +inf = unreached).  split_run: one rank owning every vertex, rounds on the
+ *        device with no exchange.
  * CDLP : part_create(range) once; part_init(labels); per iteration: zero changed;
  *        part_step(labels -> next, owned range written); exchange the owned slices of next
  *        into every rank's labels (all-gather); all-reduce MAX(changed); stop when 0 or
@@ -321,9 +327,18 @@ int gx_wcc_part_init(gx_graph *g, int32_t *parent, void *stream);
 int gx_wcc_part_hook(gx_graph *g, uint64_t v0, uint64_t v1, int32_t *parent, int *changed, void *stream);
 int gx_wcc_part_compress(gx_graph *g, int32_t *parent, void *stream);
 
-int gx_sssp_part_init(gx_graph *g, uint64_t src, uint64_t *dist, uint64_t *prev, void *stream);
-int gx_sssp_part_round(gx_graph *g, uint64_t v0, uint64_t v1, uint64_t *dist, uint64_t *prev,
-                       uint8_t *flag, uint64_t *active, void *stream);
+typedef struct gx_sssp_split gx_sssp_split;
+int gx_sssp_split_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_sssp_split **part);
+int gx_sssp_split_delta(gx_sssp_split *part, double *delta);
+int gx_sssp_split_start(gx_sssp_split *part, uint64_t src, void *stream);
+/* pairs: device buffer of 2 (v1 - v0) uint64; count: device uint64[2] */
+int gx_sssp_split_relax(gx_sssp_split *part, uint64_t *pairs, uint64_t *count, void *stream);
+/* rank r's pairs at pairs + 2 r stride, its count words at counts + 2 r */
+int gx_sssp_split_apply(gx_sssp_split *part, const uint64_t *pairs, const uint64_t *counts, int nranks,
+                        uint64_t stride, void *stream);
+int gx_sssp_split_distances(gx_sssp_split *part, double *dist, void *stream);
+int gx_sssp_split_run(gx_sssp_split *part, uint64_t src, double *dist);
+int gx_sssp_split_free(gx_sssp_split *part);
 
 typedef struct gx_cdlp_part gx_cdlp_part;
 int gx_cdlp_part_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_cdlp_part **part);

@@ -96,8 +96,14 @@ SIGNATURES = [
     ("gx_wcc_part_init", C.c_int, [_P, _P, _P]),
     ("gx_wcc_part_hook", C.c_int, [_P, C.c_uint64, C.c_uint64, _P, _P, _P]),
     ("gx_wcc_part_compress", C.c_int, [_P, _P, _P]),
-    ("gx_sssp_part_init", C.c_int, [_P, C.c_uint64, _P, _P, _P]),
-    ("gx_sssp_part_round", C.c_int, [_P, C.c_uint64, C.c_uint64, _P, _P, _P, _P, _P]),
+    ("gx_sssp_split_create", C.c_int, [_P, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
+    ("gx_sssp_split_delta", C.c_int, [_P, _DP]),
+    ("gx_sssp_split_start", C.c_int, [_P, C.c_uint64, _P]),
+    ("gx_sssp_split_relax", C.c_int, [_P, _P, _P, _P]),
+    ("gx_sssp_split_apply", C.c_int, [_P, _P, _P, C.c_int, C.c_uint64, _P]),
+    ("gx_sssp_split_distances", C.c_int, [_P, _P, _P]),
+    ("gx_sssp_split_run", C.c_int, [_P, C.c_uint64, _DP]),
+    ("gx_sssp_split_free", C.c_int, [_P]),
     ("gx_cdlp_part_create", C.c_int, [_P, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
     ("gx_cdlp_part_init", C.c_int, [_P, _P, _P]),
     ("gx_cdlp_part_step", C.c_int, [_P, _P, _P, _P, _P]),

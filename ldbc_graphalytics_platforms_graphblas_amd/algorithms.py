@@ -118,6 +118,26 @@ def LA_SSSP(G: Graph, source_vertex: int) -> np.ndarray:
     return out
 
 
+class SsspSplit:
+    """gx_sssp_split on one device owning every vertex: the multi-GPU SSSP's per-rank path
+    (1-D split, gx_sssp_split.hip) with no exchange; run(src) -> fp64 distances."""
+
+    def __init__(self, G: Graph):
+        self.G = G
+        self.h = C.c_void_p()
+        N.check(N.lib().gx_sssp_split_create(G.handle, 0, G.n, C.byref(self.h)), "gx_sssp_split_create")
+
+    def run(self, source_vertex: int) -> np.ndarray:
+        out = np.empty(self.G.n, dtype=np.float64)
+        N.check(N.lib().gx_sssp_split_run(self.h, int(source_vertex), N.as_dp(out)), "gx_sssp_split_run")
+        return out
+
+    def close(self):
+        if self.h:
+            N.lib().gx_sssp_split_free(self.h)
+            self.h = C.c_void_p()
+
+
 def WeaklyConnectedComponents(G: Graph) -> np.ndarray:
     """wcc.cpp:39-66: component label = smallest internal vertex id of the component."""
     out = np.empty(G.n, dtype=np.uint64)

@@ -341,6 +341,7 @@ hipError_t warm_cdlp(hipStream_t s);
 hipError_t warm_lcc(hipStream_t s);
 hipError_t warm_ops(hipStream_t s);
 hipError_t warm_part(hipStream_t s);
+hipError_t warm_sssp_split(hipStream_t s);
 hipError_t warm_pr(hipStream_t s);
 hipError_t warm_pr_sorted(hipStream_t s);
 hipError_t warm_runtime(hipStream_t s);

@@ -1,4 +1,5 @@
-// gx_part.hip -- per-rank steps of the multi-GPU BFS, WCC and SSSP.
+// gx_part.hip -- per-rank steps of the multi-GPU BFS and WCC (SSSP's 1-D split
+// is gx_sssp_split.hip).
 //
 // The graph is replicated on every rank (it fits: 8_5-fb is ~8 GB of CSR against 288 GB of
 // HBM); ranks own contiguous vertex ranges [v0, v1) balanced by stored entries and work
@@ -8,12 +9,8 @@
 //          commit: level[v] = cur+1 for newly reached v (every rank, same result)
 //   WCC  : hook the edges of owned rows into the parent forest             -> all-reduce MIN
 //          compress (pointer jumping) on every rank
-//   SSSP : relax the out-edges of owned vertices whose distance dropped last round
-//                                                                          -> all-reduce MIN
-//          (distances as IEEE bit patterns: signed-int64 MIN is the numeric min)
 // The reference has no distributed path ("Collective call sites: none").
-// Results equal the single-GPU ones: BFS levels and WCC min-root labels are unique, and SSSP
-// reaches the relaxation fixed point (the Dijkstra values bit for bit).
+// Results equal the single-GPU ones: BFS levels and WCC min-root labels are unique.
 #include "gx_device.h"
 
 namespace gx {
@@ -21,7 +18,6 @@ namespace {
 
 constexpr int kPartBlock = 256;
 constexpr int64_t kInfLevel = INT64_MAX;
-constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;   // +infinity
 
 // Visit the owned vertices [v0, v1) 64 at a time; `pick` selects the ones whose out-edges the
 // wave then walks together (lane-strided), calling `edge(u, v, k)` for each.
@@ -113,47 +109,6 @@ __global__ __launch_bounds__(kPartBlock) void k_wccp_compress(int32_t *parent, i
         parent[v] = find_root_p(parent, (int32_t)v);
 }
 
-__global__ __launch_bounds__(kPartBlock) void k_ssspp_init(unsigned long long *dist, unsigned long long *prev,
-                                                           int64_t n, int64_t src) {
-    for (int64_t v = (int64_t)blockIdx.x * kPartBlock + threadIdx.x; v < n; v += (int64_t)gridDim.x * kPartBlock) {
-        dist[v] = v == src ? 0ull : kInfBits;
-        prev[v] = kInfBits;
-    }
-}
-
-// Marks the owned vertices whose distance dropped since `prev` was taken and counts them.
-__global__ __launch_bounds__(kPartBlock) void k_ssspp_mark(const unsigned long long *__restrict__ dist,
-                                                           const unsigned long long *__restrict__ prev, int64_t v0,
-                                                           int64_t v1, uint8_t *flag, unsigned long long *active) {
-    unsigned long long c = 0;
-    for (int64_t v = v0 + (int64_t)blockIdx.x * kPartBlock + threadIdx.x; v < v1;
-         v += (int64_t)gridDim.x * kPartBlock) {
-        const bool f = dist[v] < prev[v];
-        flag[v] = f;
-        c += f;
-    }
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, kWave);
-    if ((threadIdx.x & (kWave - 1)) == 0 && c) atomicAdd(active, c);
-}
-
-__global__ __launch_bounds__(kPartBlock) void k_ssspp_relax(const int64_t *__restrict__ rp,
-                                                            const int32_t *__restrict__ ci,
-                                                            const double *__restrict__ w, int64_t v0, int64_t v1,
-                                                            const uint8_t *__restrict__ flag,
-                                                            const unsigned long long *__restrict__ prev,
-                                                            unsigned long long *dist) {
-    // the source distance is the snapshot taken before this round (prev == dist at that
-    // time), so every relaxation of the round uses one consistent value per vertex
-    for_owned_rows(
-        rp, ci, v0, v1, [&](int64_t u) { return flag[u] != 0; },
-        [&](int64_t u, int64_t v, int64_t k) {
-            const double nd = __longlong_as_double((long long)prev[u]) + w[k];
-            const unsigned long long b = (unsigned long long)__double_as_longlong(nd);
-            if (b < __hip_atomic_load(&dist[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                __hip_atomic_fetch_min(&dist[v], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        });
-}
-
 // NULL is the null (default) stream -- torch's default stream -- not the context's stream.
 hipStream_t pick_stream(gx_graph *, void *stream) { return (hipStream_t)stream; }
 
@@ -226,37 +181,6 @@ extern "C" int gx_wcc_part_compress(gx_graph *g, int32_t *parent, void *stream) 
     hipLaunchKernelGGL(k_wccp_compress, dim3(grid_for(g->n, kPartBlock, 8192)), dim3(kPartBlock), 0,
                        pick_stream(g, stream), parent, (int64_t)g->n);
     return check_launch("k_wccp_compress");
-}
-
-extern "C" int gx_sssp_part_init(gx_graph *g, uint64_t src, uint64_t *dist, uint64_t *prev, void *stream) {
-    if (!g || !dist || !prev) return fail(GX_NULL_POINTER, "gx_sssp_part_init: null argument");
-    if (!g->weighted) return fail(GX_INVALID_VALUE, "gx_sssp_part_init: graph has no edge weights");
-    if (src >= g->n) return fail(GX_INVALID_INDEX, "gx_sssp_part_init: source out of range");
-    GX_HIP_TRY(hipSetDevice(g->ctx->device));
-    hipLaunchKernelGGL(k_ssspp_init, dim3(grid_for(g->n, kPartBlock, 8192)), dim3(kPartBlock), 0,
-                       pick_stream(g, stream), (unsigned long long *)dist, (unsigned long long *)prev, (int64_t)g->n,
-                       (int64_t)src);
-    return check_launch("k_ssspp_init");
-}
-
-extern "C" int gx_sssp_part_round(gx_graph *g, uint64_t v0, uint64_t v1, uint64_t *dist, uint64_t *prev,
-                                  uint8_t *flag, uint64_t *active, void *stream) {
-    if (!g || !dist || !prev || !flag || !active) return fail(GX_NULL_POINTER, "gx_sssp_part_round: null argument");
-    if (!g->weighted) return fail(GX_INVALID_VALUE, "gx_sssp_part_round: graph has no edge weights");
-    GX_TRY(check_range(g, v0, v1, "gx_sssp_part_round"));
-    GX_HIP_TRY(hipSetDevice(g->ctx->device));
-    hipStream_t s = pick_stream(g, stream);
-    auto *d = (unsigned long long *)dist;
-    auto *p = (unsigned long long *)prev;
-    if (v1 > v0)
-        hipLaunchKernelGGL(k_ssspp_mark, dim3(grid_for(v1 - v0, kPartBlock, 8192)), dim3(kPartBlock), 0, s, d, p,
-                           (int64_t)v0, (int64_t)v1, flag, (unsigned long long *)active);
-    GX_TRY(check_launch("k_ssspp_mark"));
-    GX_HIP_TRY(hipMemcpyAsync(p, d, g->n * 8, hipMemcpyDeviceToDevice, s));
-    if (v1 > v0)
-        hipLaunchKernelGGL(k_ssspp_relax, dim3(grid_for(v1 - v0, kPartBlock, 8192)), dim3(kPartBlock), 0, s,
-                           g->A.rp.p, g->A.ci.p, g->A.w.p, (int64_t)v0, (int64_t)v1, flag, p, d);
-    return check_launch("k_ssspp_relax");
 }
 
 GX_MODULE_WARMER(part)

@@ -65,7 +65,7 @@ extern "C" int gx_init(int device, gx_ctx **out) {
         if (e == hipSuccess) e = hipMemcpyAsync(ctx->staging[1], d, 1 << 20, hipMemcpyDeviceToHost, ctx->stream);
         // load every kernel module now (see GX_MODULE_WARMER)
         for (auto warm : {warm_bfs, warm_cdlp, warm_lcc, warm_ops, warm_part, warm_pr, warm_pr_sorted,
-                          warm_runtime, warm_sssp, warm_wcc})
+                          warm_runtime, warm_sssp, warm_sssp_split, warm_wcc})
             if (e == hipSuccess) e = warm(ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
         if (d) (void)hipFree(d);

@@ -14,7 +14,8 @@ points of libgx (include/gx.h).  Every state array is full length on every rank:
 
     BFS  : expand owned frontier rows -> next (uint8)   all-reduce MAX, commit levels
     WCC  : hook owned rows' edges     -> parent (int32) all-reduce MIN, compress
-    SSSP : relax owned dropped rows   -> dist (int64 bit patterns of fp64) all-reduce MIN
+    SSSP : 1-D split (gx_sssp_split): relax the edges into owned vertices -> the improved
+           owned vertices as (vertex, fp64 bits) pairs, all-gathered (sparse, per round)
     CDLP : new labels of owned rows   -> all-gather of the owned slices
     LCC  : triangle counts of owned orientation sources -> all-reduce SUM, finish
 
@@ -130,19 +131,43 @@ class GpuBackend:
     def wcc_compress(self, parent):
         self.N.check(self.lib.gx_wcc_part_compress(self.g, self._p(parent), self._s()), "gx_wcc_part_compress")
 
-    def sssp_init(self, src, dist, prev):
-        self.N.check(self.lib.gx_sssp_part_init(self.g, src, self._p(dist), self._p(prev), self._s()),
-                     "gx_sssp_part_init")
-
-    def sssp_round(self, v0, v1, dist, prev, flag, active):
-        self.N.check(self.lib.gx_sssp_part_round(self.g, v0, v1, self._p(dist), self._p(prev), self._p(flag),
-                                                 self._p(active), self._s()), "gx_sssp_part_round")
+    def sssp_split(self, v0, v1):
+        return _GpuSsspSplit(self, v0, v1)
 
     def cdlp_part(self, v0, v1):
         return _GpuCdlpPart(self, v0, v1)
 
     def lcc_part(self):
         return _GpuLccPart(self)
+
+
+class _GpuSsspSplit:
+    """gx_sssp_split_* for one rank: owned targets [v0, v1)."""
+
+    def __init__(self, be: GpuBackend, v0: int, v1: int):
+        self.be = be
+        self.h = C.c_void_p()
+        be.N.check(be.lib.gx_sssp_split_create(be.g, v0, v1, C.byref(self.h)), "gx_sssp_split_create")
+
+    def start(self, src):
+        self.be.N.check(self.be.lib.gx_sssp_split_start(self.h, src, self.be._s()), "gx_sssp_split_start")
+
+    def relax(self, pairs, count):
+        self.be.N.check(self.be.lib.gx_sssp_split_relax(self.h, self.be._p(pairs), self.be._p(count), self.be._s()),
+                        "gx_sssp_split_relax")
+
+    def apply(self, pairs, counts, nranks, stride):
+        self.be.N.check(self.be.lib.gx_sssp_split_apply(self.h, self.be._p(pairs), self.be._p(counts), nranks, stride,
+                                                        self.be._s()), "gx_sssp_split_apply")
+
+    def distances(self, out):
+        self.be.N.check(self.be.lib.gx_sssp_split_distances(self.h, self.be._p(out), self.be._s()),
+                        "gx_sssp_split_distances")
+
+    def close(self):
+        if self.h:
+            self.be.lib.gx_sssp_split_free(self.h)
+            self.h = C.c_void_p()
 
 
 class _GpuCdlpPart:
@@ -252,23 +277,40 @@ def wcc(ranks: List[LocalRank], comm, n: int):
 
 
 def sssp(ranks: List[LocalRank], comm, n: int, src: int):
-    """Frontier Bellman-Ford over owned rows + MIN exchange of the distance bits; returns the
-    distances (float64, inf = unreached)."""
+    """Delta-stepping on the 1-D split (gx_sssp_split): each rank relaxes the edges into its
+    owned vertices; per round the count words {pairs, done} are all-gathered (one host read),
+    then the improved owned vertices as (vertex, fp64 bits) pairs, max-count words from every
+    rank.  Returns the distances (float64, inf = unreached)."""
     import torch
-    dist = [_zeros(r, n, torch.int64) for r in ranks]
-    prev = [_zeros(r, n, torch.int64) for r in ranks]
-    flag = [_zeros(r, n, torch.uint8) for r in ranks]
-    for r, d, p in zip(ranks, dist, prev):
-        r.backend.sssp_init(src, d, p)
-    while True:
-        active = [_zeros(r, 1, torch.int64) for r in ranks]
-        for r, d, p, f, a in zip(ranks, dist, prev, flag, active):
-            r.backend.sssp_round(r.v0, r.v1, d, p, f, a)
-        comm.all_reduce(dist, "min")
-        comm.all_reduce(active, "sum")
-        if int(active[0].item()) == 0:
-            break
-    return dist[0].view(torch.float64)
+    nranks = getattr(comm, "world_size", None) or len(ranks)
+    parts = [r.backend.sssp_split(r.v0, r.v1) for r in ranks]
+    try:
+        pairs = [_zeros(r, 2 * max(1, r.v1 - r.v0), torch.int64) for r in ranks]
+        count = [_zeros(r, 2, torch.int64) for r in ranks]
+        counts = [_zeros(r, 2 * nranks, torch.int64) for r in ranks]
+        for p in parts:
+            p.start(src)
+        while True:
+            for p, pr, c in zip(parts, pairs, count):
+                p.relax(pr, c)
+            comm.all_gather(counts, count)
+            cw = counts[0].cpu().numpy()   # identical on every rank
+            if int(cw[1]):   # done (the same flag on every rank)
+                break
+            m = int(cw[0::2].max())
+            if m:
+                gathered = [_zeros(r, 2 * m * nranks, torch.int64) for r in ranks]
+                comm.all_gather(gathered, [pr[:2 * m] for pr in pairs])
+            else:
+                gathered = pairs
+            for p, g, cs in zip(parts, gathered, counts):
+                p.apply(g, cs, nranks, m)
+        out = _zeros(ranks[0], n, torch.float64)
+        parts[0].distances(out)
+        return out
+    finally:
+        for p in parts:
+            p.close()
 
 
 def cdlp(ranks: List[LocalRank], comm, n: int, iters: int, ranges: np.ndarray):

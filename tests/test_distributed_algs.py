@@ -84,22 +84,8 @@ class NumpyBackend:
             p[v] = self._root(p, v)
 
     # SSSP
-    def sssp_init(self, src, dist_, prev):
-        d, pv = dist_.numpy().view(np.float64), prev.numpy().view(np.float64)
-        d[:] = np.inf
-        d[src] = 0.0
-        pv[:] = np.inf
-
-    def sssp_round(self, v0, v1, dist_, prev, flag, active):
-        d, pv = dist_.numpy().view(np.float64), prev.numpy().view(np.float64)
-        f = flag.numpy()
-        f[v0:v1] = d[v0:v1] < pv[v0:v1]
-        active.numpy()[0] += int(f[v0:v1].sum())
-        pv[:] = d
-        pick = np.zeros(self.n, bool)
-        pick[v0:v1] = f[v0:v1] != 0
-        rows, cols, eid = self._owned_edges(v0, v1, pick)
-        np.minimum.at(d, cols, pv[rows] + self.w[eid])
+    def sssp_split(self, v0, v1):
+        return _NpSsspSplit(self, v0, v1)
 
     # CDLP
     def cdlp_part(self, v0, v1):
@@ -108,6 +94,96 @@ class NumpyBackend:
     # LCC
     def lcc_part(self):
         return _NpLcc(self)
+
+
+class _NpSsspSplit:
+    """numpy restatement of gx_sssp_split's protocol (gx_sssp_split.hip): the edges into
+    [v0, v1) by source, a replicated distance vector, the same plan (LIGHT / HEAVY / ADVANCE /
+    done) from the same replicated counts, (vertex, fp64 bits) pairs of the improved owned
+    vertices."""
+
+    def __init__(self, be, v0, v1):
+        self.be, self.v0, self.v1 = be, v0, v1
+        w = be.w
+        mean_deg = max(1.0, len(be.ci) / max(1, be.n))
+        self.delta = 4.0 * float(w.mean() if len(w) else 1.0) / mean_deg
+        own = (be.ci >= v0) & (be.ci < v1)
+        self.light = [[] for _ in range(be.n)]
+        self.heavy = [[] for _ in range(be.n)]
+        for e in np.flatnonzero(own):
+            (self.light if w[e] < self.delta else self.heavy)[be.rows[e]].append((int(be.ci[e]), float(w[e])))
+
+    def _b(self, d):
+        return int(min(d / self.delta, 4.0e18))
+
+    def _queue(self, v, d):
+        self.lrel[v] = d
+        self.f_next.append(v)
+        if self.sstamp[v] != self.epoch:
+            self.sstamp[v] = self.epoch
+            self.S.append(v)
+
+    def start(self, src):
+        n = self.be.n
+        self.dist = np.full(n, np.inf)
+        self.dist[src] = 0.0
+        self.lrel = np.full(n, np.inf)
+        self.sstamp = np.zeros(n, np.int64)
+        self.epoch, self.cur, self.done, self.mode = 1, 0, False, 0
+        self.f_next, self.S, self.s_done, self.P = [], [], 0, set()
+        self._queue(src, 0.0)
+
+    def relax(self, pairs, count):
+        work, edges = [], self.light
+        if self.done:
+            self.mode = 0
+        elif self.f_next:
+            self.mode, work, self.f_next = 1, self.f_next, []
+        elif len(self.S) > self.s_done:
+            self.mode, work, edges = 2, self.S[self.s_done:], self.heavy
+            self.s_done = len(self.S)
+        elif self.P:
+            self.mode = 3
+            self.epoch += 1
+            self.S, self.s_done = [], 0
+            pend = [v for v in self.P if self.dist[v] < self.lrel[v]]
+            cb = min((self._b(self.dist[v]) for v in pend), default=int(4e18))
+            self.P = {v for v in pend if self._b(self.dist[v]) > cb}
+            for v in sorted(v for v in pend if self._b(self.dist[v]) <= cb):
+                self._queue(v, self.dist[v])
+            self.cur = cb
+            work, self.f_next = self.f_next, []
+        else:
+            self.done, self.mode = True, 0
+        before = self.dist.copy()
+        for u in work:
+            for v, x in edges[u]:
+                self.dist[v] = min(self.dist[v], self.dist[u] + x)
+        imp = np.flatnonzero(self.dist[self.v0:self.v1] < before[self.v0:self.v1]) + self.v0
+        pr = pairs.numpy()
+        pr[0:2 * len(imp):2] = imp
+        pr[1:2 * len(imp):2] = self.dist[imp].view(np.int64)
+        count.numpy()[:] = [len(imp), int(self.done)]
+
+    def apply(self, pairs, counts, nranks, stride):
+        if self.mode == 0:
+            return
+        pr, cw = pairs.numpy(), counts.numpy()
+        for r in range(nranks):
+            for i in range(int(cw[2 * r])):
+                v = int(pr[2 * (r * stride + i)])
+                d = float(pr[2 * (r * stride + i) + 1:2 * (r * stride + i) + 2].view(np.float64)[0])
+                self.dist[v] = min(self.dist[v], d)
+                if self._b(d) <= self.cur:
+                    self._queue(v, d)
+                else:
+                    self.P.add(v)
+
+    def distances(self, out):
+        out.numpy()[:] = self.dist
+
+    def close(self):
+        pass
 
 
 class _NpCdlp:
