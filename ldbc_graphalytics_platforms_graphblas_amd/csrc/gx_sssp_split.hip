@@ -418,9 +418,9 @@ struct gx_sssp_split {
     }
 };
 
-static hipStream_t split_stream(gx_sssp_split *p, void *stream) {
-    return stream ? (hipStream_t)stream : p->g->ctx->stream;
-}
+// as the other *_part_* steps (gx.h): NULL is the null (default) stream -- torch's -- so the
+// steps order with the tensors and collectives issued there
+static hipStream_t split_stream(gx_sssp_split *, void *stream) { return (hipStream_t)stream; }
 
 // plan -> minb -> take -> relax -> pairs (this rank's improved owned vertices)
 static int split_relax(gx_sssp_split *p, uint64_t *pairs, uint64_t *count, hipStream_t s) {

@@ -285,7 +285,9 @@ def sssp(ranks: List[LocalRank], comm, n: int, src: int):
     nranks = getattr(comm, "world_size", None) or len(ranks)
     parts = [r.backend.sssp_split(r.v0, r.v1) for r in ranks]
     try:
-        pairs = [_zeros(r, 2 * max(1, r.v1 - r.v0), torch.int64) for r in ranks]
+        # n pairs of room on every rank: the all-gather sends max-count pairs from each, which
+        # may exceed what a small range could ever fill
+        pairs = [_zeros(r, 2 * max(1, n), torch.int64) for r in ranks]
         count = [_zeros(r, 2, torch.int64) for r in ranks]
         counts = [_zeros(r, 2 * nranks, torch.int64) for r in ranks]
         for p in parts:
