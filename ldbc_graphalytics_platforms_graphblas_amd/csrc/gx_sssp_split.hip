@@ -7,17 +7,23 @@
 // every rank holds dist[n] and applies every improvement, so every rank takes the same
 // scheduling decisions from the same counts.
 //
-// Round (bulk synchronous, delta-stepping after Meyer & Sanders):
-//   plan   one thread: LIGHT (relax the frontier queued last round), HEAVY (relax the heavy
-//          edges of the vertices settled in the current bucket since the last HEAVY), ADVANCE
-//          (open the smallest pending bucket: minb + take move its vertices to the frontier),
-//          or done -- decided from the replicated vertex counts only;
-//   relax  one wave per (vertex, 256-edge chunk) item of this rank's slice; a target whose
-//          distance drops is claimed once per round onto the improved list;
+// Round (bulk synchronous, delta-stepping after Meyer & Sanders; the bucket ring, fusion and
+// pulled heavy phase of gx_sssp.hip restated for replicated state):
+//   plan   one thread, from the replicated counts only: LIGHT (relax the frontier queued last
+//          round), HEAVY / PULL (the heavy edges of the vertices settled since the last time:
+//          pushed, or -- undirected, batch >= 1/8 of the vertices with edges -- pulled by the
+//          owned vertices above fl(min settled distance + delta)), ADVANCE (open the next
+//          non-empty slot of the 32-bucket ring, fused with the following ones while they hold
+//          <= n/16 vertices), SPLIT (the overflow into a new ring window) or done;
+//   prep   ADVANCE: the opened slots' pending vertices -> this round's frontier; SPLIT: the
+//          overflow -> ring / new overflow; HEAVY / PULL: the batch marked (PULL: its minimum);
+//   cand   PULL: the owned vertices a batch neighbour could still improve;
+//   relax  one wave per (vertex, 256-edge chunk) item of this rank's slice, or per PULL
+//          candidate; a target whose distance drops is claimed once per round;
 //   pairs  (vertex, distance bits) of the improved owned vertices + {count, done};
 //   -- the caller all-gathers the pairs of every rank (gx_sssp_split_run: one rank, none) --
-//   apply  every rank's pairs: dist = min, then the vertex goes to the next frontier when its
-//          bucket is <= cur (and to the current bucket's settled set), else to the pending set.
+//   apply  every rank's pairs: dist = min, then the vertex joins the next frontier when its
+//          bucket is <= cur (and the epoch's settled set), else its ring slot or the overflow.
 // Distances are the relaxation fixed point, bitwise the oracle's and gx_sssp's whatever the
 // split or delta (gx_sssp.hip header).
 #include <algorithm>
@@ -36,24 +42,37 @@ namespace {
 
 constexpr int kSB = 256;        // threads per block
 constexpr int kSChunk = 256;    // edges per relax item
+constexpr int kW = 32;          // bucket ring slots
 constexpr unsigned long long kInf = 0x7FF0000000000000ull;   // +inf bits
 
-enum : int32_t { kNone = 0, kLight = 1, kHeavy = 2, kAdvance = 3 };
+enum : int32_t { kNone = 0, kLight = 1, kHeavy = 2, kAdvance = 3, kPull = 4, kSplit = 5 };
 
 // Replicated decision state (identical on every rank after every apply) + this rank's item
 // counters (which differ by rank and never enter a decision).
 struct SplitState {
-    int64_t cur;                  // bucket being settled
-    unsigned long long pminb;     // ADVANCE: smallest bucket on the pending list
+    int64_t cur;                  // last bucket of the group being settled
+    int64_t win_base;             // ring window [win_base, win_base + kW)
+    unsigned long long ovf_minb;  // smallest bucket on the overflow list being filled
+    unsigned long long smin;      // PULL: smallest distance of the settled batch
     int32_t mode, round, epoch, done;
     int32_t fc;                   // frontier list relaxed this round (LIGHT / ADVANCE)
-    int32_t pin;                  // pending list appended to
+    int32_t oe;                   // overflow list being filled; SPLIT reads oe ^ 1
+    int32_t ostamp_tag;           // overflow dedupe tag (one per overflow generation)
+    int32_t slot0, nslots;        // ADVANCE: ring slots opened
+    int32_t consume, consume_n;   // ring slots to clear at the next plan
     uint32_t fv[2], fi[2];        // frontier vertices (replicated) / items (rank-local)
     uint32_t sv, sv_done;         // settled vertices of this epoch / heavy-relaxed so far
     uint32_t si, si_done;         // their heavy items (rank-local) / relaxed so far
-    uint32_t hs0, hs1;            // HEAVY: items [hs0, hs1) of the settled list
-    uint32_t pcnt[2];             // pending vertices
+    uint32_t hs0, hs1;            // HEAVY: items [hs0, hs1); HEAVY / PULL: vertices [sb0, sb1)
+    uint32_t sb0, sb1;
+    uint32_t ring_cnt[kW];
+    uint32_t ovf_cnt[2];
+    uint32_t ncand;               // PULL candidates (rank-local)
     uint32_t nimp;                // improved owned vertices this round (rank-local)
+    uint32_t pull_min;            // settled batch size from which the heavy phase is pulled (0: never)
+    uint32_t fuse;                // ADVANCE opens further slots while the vertices stay <= fuse
+    uint32_t nmode[6];            // rounds per mode (GX_SPLIT_VERBOSE)
+    unsigned long long nitems[6]; // items / candidates per mode (rank-local)
 };
 
 struct SplitBufs {
@@ -61,15 +80,27 @@ struct SplitBufs {
     const int64_t *slend;
     const int32_t *sci;           // owned target - v0
     const double *sw;
+    const int64_t *orp;           // owned rows' heavy in-edges (PULL; undirected graphs)
+    const int32_t *oci;
+    const double *ow;
     unsigned long long *dist;     // replicated distances (fp64 bits)
-    unsigned long long *lrel;     // distance u's light edges were queued for relaxing with
-    int32_t *sstamp, *pstamp, *istamp;   // settled epoch / pending flag / improved round
+    unsigned long long *lrel;     // distance v's light edges were queued for relaxing with
+    int32_t *sstamp;              // epoch v joined the settled set
+    int32_t *hdone;               // epoch v's heavy edges were relaxed (0: pending)
+    int32_t *hmark;               // PULL: round v is in the settled batch
+    int32_t *qstamp;              // ADVANCE: round v was taken from the ring
+    int32_t *bstamp;              // bucket v was last put into a ring slot for (low 32 bits + 1)
+    int32_t *ostamp;              // overflow tag v was last put on the overflow with
+    int32_t *istamp;              // round an owned vertex was last claimed as improved
     uint64_t *fitems[2];          // (u << 32 | chunk)
     uint64_t *sitems;             // heavy items of the settled vertices
-    int32_t *plist[2];
+    int32_t *sverts;              // settled vertices of the epoch (replicated set)
+    int32_t *ring;                // kW slots of n vertices
+    int32_t *ovf[2];
+    int32_t *cand;                // PULL candidates (owned vertices)
     int32_t *imp;                 // improved owned vertices (global ids)
     int64_t n, v0, v1;
-    double inv_delta;
+    double delta, inv_delta;
     SplitState *st;
 };
 
@@ -78,47 +109,110 @@ __device__ __forceinline__ int64_t sbucket(unsigned long long bits, double inv_d
     return q < 4.0e18 ? (int64_t)q : (int64_t)4000000000000000000ll;
 }
 
-// Wave-aggregated reservation: lane with c items gets its first slot; one atomic per wave.
-// Every lane of the wave must call it.
-__device__ __forceinline__ uint32_t wave_reserve(uint32_t *counter, uint32_t c) {
-    const int lane = threadIdx.x & (kWave - 1);
-    uint32_t x = c;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, kWave);
-        if (lane >= off) x += y;
-    }
-    const uint32_t tot = __shfl(x, kWave - 1, kWave);
-    uint32_t base = 0;
-    if (lane == kWave - 1 && tot) base = atomicAdd(counter, tot);
-    base = __shfl(base, kWave - 1, kWave);
-    return base + x - c;
-}
-
 __device__ __forceinline__ uint32_t nchunks(int64_t len) { return (uint32_t)max<int64_t>(1, (len + kSChunk - 1) / kSChunk); }
 
-// Queue v (distance d) for the next light relaxation of `list` and into the epoch's settled
-// set; `take` lanes only (every lane calls).
-__device__ __forceinline__ void queue_frontier(const SplitBufs &B, bool take, int64_t v, unsigned long long d, int list,
-                                               int32_t epoch) {
-    SplitState *st = B.st;
-    uint32_t nl = 0, nh = 0, isv = 0;
+// ---- tile reservations ----
+// A kernel that queues vertices works in tiles of kTile elements per workgroup: each element
+// takes its offsets inside the tile from LDS atomics, then one thread per queue reserves the
+// tile's range with one global atomic.  A shared counter then sees one atomic per queue and
+// tile instead of one per wave (same-address atomics serialise at ~11-20 ns each: the first
+// version of this file spent most of its time there).
+constexpr int kPer = 8;                    // elements per thread and tile
+constexpr int kTile = kSB * kPer;
+enum : int { kQFv = 0, kQFi, kQSv, kQSi, kQOvf, kQRing, kQCat = kQRing + kW };
+
+struct Tile {
+    uint32_t cnt[kQCat];
+    uint32_t base[kQCat];
+    unsigned long long ominb;
+};
+
+// One element's pushes: the frontier (with its light items) and the settled set (with its
+// heavy items) for `take`; the ring slot or overflow for `far`.
+struct Push {
+    int32_t v;
+    uint32_t nl, offi, nh, offs, offsv, offr;
+    int8_t isv, q;   // q: -1 none, kQOvf, or kQRing + slot
+    uint8_t take;
+};
+
+__device__ __forceinline__ void tile_begin(Tile &T) {
+    for (int c = threadIdx.x; c < kQCat; c += kSB) T.cnt[c] = 0;
+    if (threadIdx.x == 0) T.ominb = ~0ull;
+    __syncthreads();
+}
+
+// Stage element v (distance d): frontier/settled when take, ring/overflow (bucket b) when far.
+__device__ __forceinline__ void tile_stage(const SplitBufs &B, Tile &T, Push &P, bool take, bool far, int64_t v,
+                                           unsigned long long d, int64_t b, int32_t epoch) {
+    const SplitState *st = B.st;
+    P.v = (int32_t)v;
+    P.take = take;
+    P.isv = 0;
+    P.q = -1;
+    P.nl = P.nh = 0;
     if (take) {
         B.lrel[v] = d;
-        nl = nchunks(B.slend[v] - B.srp[v]);
-        if (B.sstamp[v] != epoch) {
-            B.sstamp[v] = epoch;   // the vertex is claimed by this lane alone (unique per round)
-            isv = 1;
-            nh = nchunks(B.srp[v + 1] - B.slend[v]);
+        P.nl = nchunks(B.slend[v] - B.srp[v]);
+        atomicAdd(&T.cnt[kQFv], 1u);
+        P.offi = atomicAdd(&T.cnt[kQFi], P.nl);
+        if (B.sstamp[v] != epoch || B.hdone[v] == epoch) {
+            B.sstamp[v] = epoch;
+            B.hdone[v] = 0;
+            P.isv = 1;
+            P.nh = nchunks(B.srp[v + 1] - B.slend[v]);
+            P.offsv = atomicAdd(&T.cnt[kQSv], 1u);
+            P.offs = atomicAdd(&T.cnt[kQSi], P.nh);
         }
     }
-    const uint32_t fvb = wave_reserve(&st->fv[list], take ? 1u : 0u);
-    (void)fvb;
-    const uint32_t fib = wave_reserve(&st->fi[list], nl);
-    wave_reserve(&st->sv, isv);
-    const uint32_t sib = wave_reserve(&st->si, nh);
-    for (uint32_t j = 0; j < nl; j++) B.fitems[list][fib + j] = ((uint64_t)(uint32_t)v << 32) | j;
-    for (uint32_t j = 0; j < nh; j++) B.sitems[sib + j] = ((uint64_t)(uint32_t)v << 32) | j;
+    if (far) {
+        if (b < st->win_base + kW) {
+            const int32_t btag = (int32_t)(uint32_t)b + 1;
+            if (B.bstamp[v] != btag) {
+                B.bstamp[v] = btag;
+                P.q = (int8_t)(kQRing + (int)(b % kW));
+                P.offr = atomicAdd(&T.cnt[P.q], 1u);
+            }
+        } else {
+            // the bound counts every overflow vertex, also one already listed whose bucket dropped
+            atomicMin(&T.ominb, (unsigned long long)b);
+            if (B.ostamp[v] != st->ostamp_tag) {
+                B.ostamp[v] = st->ostamp_tag;
+                P.q = kQOvf;
+                P.offr = atomicAdd(&T.cnt[kQOvf], 1u);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t *tile_counter(SplitState *st, int c, int list) {
+    switch (c) {
+    case kQFv: return &st->fv[list];
+    case kQFi: return &st->fi[list];
+    case kQSv: return &st->sv;
+    case kQSi: return &st->si;
+    case kQOvf: return &st->ovf_cnt[st->oe];
+    default: return &st->ring_cnt[c - kQRing];
+    }
+}
+
+__device__ __forceinline__ void tile_reserve(SplitState *st, Tile &T, int list) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < kQCat; c += kSB) T.base[c] = T.cnt[c] ? atomicAdd(tile_counter(st, c, list), T.cnt[c]) : 0u;
+    if (threadIdx.x == 0 && T.ominb != ~0ull) atomicMin(&st->ovf_minb, T.ominb);
+    __syncthreads();
+}
+
+__device__ __forceinline__ void tile_write(const SplitBufs &B, const Tile &T, const Push &P, int list) {
+    const int64_t v = P.v;
+    if (P.take)
+        for (uint32_t j = 0; j < P.nl; j++) B.fitems[list][T.base[kQFi] + P.offi + j] = ((uint64_t)(uint32_t)v << 32) | j;
+    if (P.isv) {
+        B.sverts[T.base[kQSv] + P.offsv] = (int32_t)v;
+        for (uint32_t j = 0; j < P.nh; j++) B.sitems[T.base[kQSi] + P.offs + j] = ((uint64_t)(uint32_t)v << 32) | j;
+    }
+    if (P.q == kQOvf) B.ovf[B.st->oe][T.base[kQOvf] + P.offr] = (int32_t)v;
+    else if (P.q >= kQRing) B.ring[(uint64_t)(P.q - kQRing) * (uint64_t)B.n + T.base[P.q] + P.offr] = (int32_t)v;
 }
 
 __global__ void k_split_start(SplitBufs B, int64_t src) {
@@ -127,138 +221,340 @@ __global__ void k_split_start(SplitBufs B, int64_t src) {
         B.dist[v] = v == src ? 0ull : kInf;
         B.lrel[v] = kInf;
         B.sstamp[v] = 0;
-        B.pstamp[v] = 0;
+        B.hdone[v] = 0;
+        B.hmark[v] = 0;
+        B.qstamp[v] = 0;
+        B.bstamp[v] = 0;
+        B.ostamp[v] = 0;
     }
     for (int64_t v = i; v < B.v1 - B.v0; v += (int64_t)gridDim.x * kSB) B.istamp[v] = 0;
 }
 
-__global__ void k_split_seed(SplitBufs B, int64_t src) {
+__global__ void k_split_seed(SplitBufs B, int64_t src, uint32_t pull_min, uint32_t fuse) {
     SplitState *st = B.st;
     if (threadIdx.x == 0) {
         memset(st, 0, sizeof(SplitState));
         st->epoch = 1;
-        st->fc = 0;
+        st->ostamp_tag = 1;
+        st->consume = -1;
+        st->ovf_minb = ~0ull;
+        st->pull_min = pull_min;
+        st->fuse = fuse;
     }
     __syncthreads();
-    // first wave queues the source into list 1 (the next frontier)
-    if (threadIdx.x < kWave) queue_frontier(B, threadIdx.x == 0, src, 0ull, 1, 1);
+    // the source -> list 1 (the next frontier)
+    __shared__ Tile T;
+    tile_begin(T);
+    Push P;
+    tile_stage(B, T, P, threadIdx.x == 0, false, src, 0ull, 0, 1);
+    tile_reserve(st, T, 1);
+    tile_write(B, T, P, 1);
 }
 
 __global__ void k_split_plan(SplitState *st) {
     st->nimp = 0;
+    st->ncand = 0;
     if (st->done) {
         st->mode = kNone;
         return;
     }
     st->round++;
+    if (st->consume >= 0) {
+        for (int j = 0; j < st->consume_n; j++) st->ring_cnt[(st->consume + j) % kW] = 0;
+        st->consume = -1;
+    }
     const int nx = st->fc ^ 1;
-    if (st->fv[nx] > 0) {
+    if (st->fv[nx] > 0) {   // the frontier queued last round
         st->mode = kLight;
         st->fc = nx;
         st->fv[nx ^ 1] = 0;
         st->fi[nx ^ 1] = 0;
+        st->nmode[kLight]++;
+        st->nitems[kLight] += st->fi[nx];
         return;
     }
-    if (st->sv > st->sv_done) {
-        st->mode = kHeavy;
+    st->fv[nx] = st->fi[nx] = 0;
+    if (st->sv > st->sv_done) {   // heavy edges of the vertices settled since the last time
+        st->sb0 = st->sv_done;
+        st->sb1 = st->sv;
         st->hs0 = st->si_done;
         st->hs1 = st->si;
-        st->si_done = st->si;
         st->sv_done = st->sv;
+        st->si_done = st->si;
+        st->mode = st->pull_min && st->sb1 - st->sb0 >= st->pull_min ? kPull : kHeavy;
+        st->smin = ~0ull;
+        st->nmode[st->mode]++;
+        st->nitems[kHeavy] += st->mode == kHeavy ? st->hs1 - st->hs0 : 0;
         return;
     }
-    if (st->pcnt[st->pin] > 0) {
+    // open the next non-empty ring bucket, with the following ones while the vertices stay
+    // within `fuse` (bucket fusion; any grouping reaches the same fixed point)
+    const int64_t lim = st->win_base + kW;
+    for (int64_t b = st->cur + 1; b < lim; b++) {
+        const uint32_t c0 = st->ring_cnt[b % kW];
+        if (c0 == 0) continue;
+        uint32_t tot = c0;
+        int64_t last = b;
+        for (int64_t b2 = b + 1; b2 < lim; b2++) {
+            const uint32_t c = st->ring_cnt[b2 % kW];
+            if (tot + c > st->fuse) break;
+            tot += c;
+            last = b2;
+        }
         st->mode = kAdvance;
+        st->cur = last;
+        st->slot0 = (int32_t)(b % kW);
+        st->nslots = (int32_t)(last - b + 1);
+        st->consume = st->slot0;
+        st->consume_n = st->nslots;
         st->epoch++;
         st->sv = st->sv_done = st->si = st->si_done = 0;
-        st->pin ^= 1;
-        st->pcnt[st->pin] = 0;
-        st->pminb = ~0ull;
-        st->fc ^= 1;   // take fills list fc, apply the other
+        st->fc = nx;   // take fills list fc, apply the other
         st->fv[0] = st->fv[1] = st->fi[0] = st->fi[1] = 0;
+        st->nmode[kAdvance]++;
+        return;
+    }
+    const int src = st->oe;
+    if (st->ovf_cnt[src] > 0) {   // new ring window from the overflow
+        const int64_t mb = (int64_t)min(st->ovf_minb, 4000000000000000000ull);
+        st->win_base = max(st->cur + 1, mb);
+        st->cur = st->win_base - 1;
+        st->oe = src ^ 1;
+        st->ovf_cnt[st->oe] = 0;
+        st->ovf_minb = ~0ull;
+        st->ostamp_tag++;
+        st->mode = kSplit;
+        st->nmode[kSplit]++;
         return;
     }
     st->done = 1;
     st->mode = kNone;
 }
 
-// ADVANCE: the smallest bucket among the still pending vertices of the old pending list.
-__global__ __launch_bounds__(kSB) void k_split_minb(SplitBufs B) {
+// ADVANCE: the opened ring slots' still pending vertices -> this round's frontier;
+// SPLIT: the old overflow -> ring slots of the new window / the new overflow;
+// HEAVY / PULL: the settled batch's heavy edges are now relaxed (PULL: marked, and its
+// smallest distance taken).
+__global__ __launch_bounds__(kSB) void k_split_prep(SplitBufs B) {
     SplitState *st = B.st;
-    if (st->mode != kAdvance) return;
-    const int32_t *pl = B.plist[st->pin ^ 1];
-    const uint32_t cnt = st->pcnt[st->pin ^ 1];
-    unsigned long long m = ~0ull;
-    for (uint32_t i = blockIdx.x * kSB + threadIdx.x; i < cnt; i += gridDim.x * kSB) {
-        const int32_t v = pl[i];
-        const unsigned long long d = B.dist[v];
-        if (d < B.lrel[v]) m = min(m, (unsigned long long)sbucket(d, B.inv_delta));
+    const int32_t mode = st->mode;
+    __shared__ Tile T;
+    if (mode == kAdvance) {
+        const int64_t cur = st->cur;
+        const int32_t round = st->round, epoch = st->epoch, fc = st->fc;
+        // the opened slots' entries as one index space
+        uint32_t tot = 0;
+        for (int j = 0; j < st->nslots; j++) tot += st->ring_cnt[(st->slot0 + j) % kW];
+        for (uint32_t t0 = blockIdx.x * kTile; t0 < tot; t0 += gridDim.x * kTile) {
+            tile_begin(T);
+            Push P[kPer];
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                uint32_t i = t0 + k * kSB + threadIdx.x;
+                const bool valid = i < tot;
+                int32_t v = 0;
+                if (valid) {
+                    int j = 0;
+                    uint32_t c = st->ring_cnt[st->slot0 % kW];
+                    while (i >= c) {
+                        i -= c;
+                        j++;
+                        c = st->ring_cnt[(st->slot0 + j) % kW];
+                    }
+                    v = B.ring[(uint64_t)((st->slot0 + j) % kW) * (uint64_t)B.n + i];
+                }
+                const unsigned long long d = valid ? B.dist[v] : kInf;
+                bool now = valid && d < B.lrel[v] && sbucket(d, B.inv_delta) <= cur;
+                if (now) now = B.qstamp[v] != round && atomicExch(&B.qstamp[v], round) != round;
+                tile_stage(B, T, P[k], now, false, v, d, 0, epoch);
+            }
+            tile_reserve(st, T, fc);
+#pragma unroll
+            for (int k = 0; k < kPer; k++) tile_write(B, T, P[k], fc);
+            __syncthreads();
+        }
+    } else if (mode == kSplit) {
+        const int src = st->oe ^ 1;
+        const uint32_t cnt = st->ovf_cnt[src];
+        for (uint32_t t0 = blockIdx.x * kTile; t0 < cnt; t0 += gridDim.x * kTile) {
+            tile_begin(T);
+            Push P[kPer];
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                const uint32_t i = t0 + k * kSB + threadIdx.x;
+                const bool valid = i < cnt;
+                const int32_t v = valid ? B.ovf[src][i] : 0;
+                const unsigned long long d = valid ? B.dist[v] : kInf;
+                const bool pend = valid && d < B.lrel[v];
+                tile_stage(B, T, P[k], false, pend, v, d, pend ? sbucket(d, B.inv_delta) : 0, 0);
+            }
+            tile_reserve(st, T, 0);
+#pragma unroll
+            for (int k = 0; k < kPer; k++) tile_write(B, T, P[k], 0);
+            __syncthreads();
+        }
+    } else if (mode == kHeavy || mode == kPull) {
+        const int32_t epoch = st->epoch, round = st->round;
+        unsigned long long m = ~0ull;
+        for (uint32_t i = st->sb0 + blockIdx.x * kSB + threadIdx.x; i < st->sb1; i += gridDim.x * kSB) {
+            const int32_t u = B.sverts[i];
+            B.hdone[u] = epoch;
+            if (mode == kPull) {
+                B.hmark[u] = round;
+                m = min(m, B.dist[u]);
+            }
+        }
+        if (mode == kPull) {
+            for (int off = 32; off > 0; off >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, off, kWave));
+            if ((threadIdx.x & (kWave - 1)) == 0 && m != ~0ull) atomicMin(&st->smin, m);
+        }
     }
-    for (int off = 32; off > 0; off >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, off, kWave));
-    if ((threadIdx.x & (kWave - 1)) == 0 && m != ~0ull) atomicMin(&st->pminb, m);
 }
 
-// ADVANCE: the pending vertices of bucket <= pminb go to the frontier relaxed this round,
-// the other still pending ones to the new pending list; relaxed ones are dropped.
-__global__ __launch_bounds__(kSB) void k_split_take(SplitBufs B) {
+// PULL: the owned vertices a settled neighbour could still improve (distance above
+// fl(smin + delta): a heavy edge adds at least delta).
+__global__ __launch_bounds__(kSB) void k_split_cand(SplitBufs B) {
     SplitState *st = B.st;
-    if (st->mode != kAdvance) return;
-    const int32_t *pl = B.plist[st->pin ^ 1];
-    const uint32_t cnt = st->pcnt[st->pin ^ 1];
-    const unsigned long long cb = st->pminb;
-    const int32_t epoch = st->epoch, fc = st->fc, pin = st->pin;
-    const uint32_t span = (cnt + kSB - 1) / kSB * kSB;   // whole waves iterate together
-    for (uint32_t i = blockIdx.x * kSB + threadIdx.x; i < span; i += gridDim.x * kSB) {
-        const bool valid = i < cnt;
-        const int32_t v = valid ? pl[i] : 0;
-        const unsigned long long d = valid ? B.dist[v] : kInf;
-        const bool pend = valid && d < B.lrel[v];
-        const bool now = pend && (unsigned long long)sbucket(d, B.inv_delta) <= cb;
-        const bool keep = pend && !now;
-        if (valid && !keep) B.pstamp[v] = 0;
-        const uint32_t at = wave_reserve(&st->pcnt[pin], keep ? 1u : 0u);
-        if (keep) B.plist[pin][at] = v;
-        queue_frontier(B, now, v, d, fc, epoch);
+    if (st->mode != kPull) return;
+    const unsigned long long lim =
+        (unsigned long long)__double_as_longlong(__longlong_as_double((long long)st->smin) + B.delta);
+    const int64_t own = B.v1 - B.v0;
+    __shared__ uint32_t lcnt, lbase;
+    for (int64_t t0 = (int64_t)blockIdx.x * kTile; t0 < own; t0 += (int64_t)gridDim.x * kTile) {
+        if (threadIdx.x == 0) lcnt = 0;
+        __syncthreads();
+        uint32_t off[kPer];
+        bool c[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int64_t i = t0 + k * kSB + threadIdx.x;
+            c[k] = i < own && B.dist[B.v0 + i] > lim && B.orp[i + 1] > B.orp[i];
+            off[k] = c[k] ? atomicAdd(&lcnt, 1u) : 0u;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) lbase = lcnt ? atomicAdd(&st->ncand, lcnt) : 0u;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPer; k++)
+            if (c[k]) B.cand[lbase + off[k]] = (int32_t)(t0 + k * kSB + threadIdx.x);
+        __syncthreads();
     }
 }
 
-// One wave per item of the list this round relaxes.
+// LIGHT / ADVANCE: the frontier's light edges; HEAVY: the settled batch's heavy edges.  A wave
+// takes 64 items (vertex, 256-edge chunk) and walks their concatenated edges 64 at a time,
+// each lane finding its item by a shuffle binary search over the items' edge prefix -- a
+// frontier of low-degree vertices fills the lanes.  PULL: one wave per candidate, its heavy
+// in-edges from the settled batch, minimum in registers, written by the wave.  Improved owned
+// vertices are claimed once per round, staged in LDS and appended once per workgroup.
+constexpr int kStageCap = 2048;
+
 __global__ __launch_bounds__(kSB) void k_split_relax(SplitBufs B) {
     SplitState *st = B.st;
     const int32_t mode = st->mode;
-    if (mode == kNone) return;
-    if (mode == kAdvance && blockIdx.x == 0 && threadIdx.x == 0) st->cur = (int64_t)min(st->pminb, 4000000000000000000ull);
-    const bool heavy = mode == kHeavy;
-    const uint64_t *items = heavy ? B.sitems : B.fitems[st->fc];
-    const uint32_t i0 = heavy ? st->hs0 : 0u, i1 = heavy ? st->hs1 : st->fi[st->fc];
+    if (mode == kNone || mode == kSplit) return;
+    __shared__ int32_t stage[kStageCap];
+    __shared__ uint32_t scnt, sbase;
+    if (threadIdx.x == 0) scnt = 0;
+    __syncthreads();
     const int32_t round = st->round;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = (blockIdx.x * kSB + threadIdx.x) / kWave, nw = gridDim.x * (kSB / kWave);
-    for (uint32_t it = i0 + wid; it < i1; it += nw) {
-        const uint64_t x = items[it];
-        const int64_t u = (int64_t)(x >> 32);
-        const int64_t j = (int64_t)(x & 0xffffffffu);
-        const int64_t a = heavy ? B.slend[u] : B.srp[u], b = heavy ? B.srp[u + 1] : B.slend[u];
-        const int64_t e0 = a + j * kSChunk, e1 = min(b, e0 + kSChunk);
-        const double du = __longlong_as_double((long long)B.dist[u]);
-        for (int64_t eb = e0; eb < e1; eb += kWave) {
-            const int64_t e = eb + lane;
-            bool won = false;
-            int32_t t = 0;
-            if (e < e1) {
-                t = B.sci[e];
-                const unsigned long long nd = (unsigned long long)__double_as_longlong(du + B.sw[e]);
-                unsigned long long *dv = &B.dist[B.v0 + t];
-                if (nd < __hip_atomic_load(dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    const unsigned long long old =
-                        __hip_atomic_fetch_min(dv, nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    won = nd < old && B.istamp[t] != round && atomicExch(&B.istamp[t], round) != round;
+    auto claim = [&](bool won, int32_t v) {   // every lane of the wave calls
+        const uint64_t m = __ballot(won);
+        if (!m) return;
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(&scnt, (uint32_t)__popcll(m));
+        at = __shfl(at, 0, kWave) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (won) {
+            if (at < kStageCap) stage[at] = v;
+            else B.imp[atomicAdd(&st->nimp, 1u)] = v;   // stage full: straight out
+        }
+    };
+    if (mode == kPull) {
+        const uint32_t nc = st->ncand;
+        for (uint32_t it = wid; it < nc; it += nw) {
+            const int64_t i = B.cand[it];
+            unsigned long long best = kInf;
+            for (int64_t e = B.orp[i] + lane; e < B.orp[i + 1]; e += kWave) {
+                const int32_t u = B.oci[e];
+                if (B.hmark[u] == round) {
+                    const unsigned long long nd =
+                        (unsigned long long)__double_as_longlong(__longlong_as_double((long long)B.dist[u]) + B.ow[e]);
+                    best = min(best, nd);
                 }
             }
-            const uint32_t at = wave_reserve(&st->nimp, won ? 1u : 0u);
-            if (won) B.imp[at] = (int32_t)(B.v0 + t);
+            for (int off = 32; off > 0; off >>= 1) best = min(best, (unsigned long long)__shfl_xor(best, off, kWave));
+            bool won = false;
+            if (lane == 0 && best < B.dist[B.v0 + i]) {
+                B.dist[B.v0 + i] = best;   // this wave alone writes the vertex this round
+                won = true;                // one candidate per wave: no claim needed
+            }
+            claim(won, (int32_t)(B.v0 + i));
+        }
+    } else {
+        const bool heavy = mode == kHeavy;
+        const uint64_t *items = heavy ? B.sitems : B.fitems[st->fc];
+        const uint32_t i0 = heavy ? st->hs0 : 0u, i1 = heavy ? st->hs1 : st->fi[st->fc];
+        for (uint32_t g0 = i0 + wid * kWave; g0 < i1; g0 += nw * kWave) {
+            // lane l: item g0 + l
+            const uint32_t gi = g0 + lane;
+            int64_t e0 = 0, len = 0;
+            unsigned long long du = 0;
+            if (gi < i1) {
+                const uint64_t x = items[gi];
+                const int64_t u = (int64_t)(x >> 32), j = (int64_t)(x & 0xffffffffu);
+                const int64_t a = heavy ? B.slend[u] : B.srp[u], b = heavy ? B.srp[u + 1] : B.slend[u];
+                e0 = a + j * kSChunk;
+                len = max<int64_t>(0, min(b, e0 + kSChunk) - e0);
+                du = B.dist[u];
+            }
+            // exclusive prefix of the items' lengths (<= 64 x 256: 32 bits)
+            uint32_t x = (uint32_t)len;
+#pragma unroll
+            for (int off = 1; off < kWave; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off, kWave);
+                if (lane >= off) x += y;
+            }
+            const uint32_t total = __shfl(x, kWave - 1, kWave);
+            const uint32_t pre = x - (uint32_t)len;
+            for (uint32_t k0 = 0; k0 < total; k0 += kWave) {
+                const uint32_t k = k0 + lane;
+                // the item holding edge k: the last lane whose prefix is <= k (lanes past the
+                // group have len 0 and prefix = total, never <= k < total)
+                int lo = 0;
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1) {
+                    const int c = lo + step;
+                    const uint32_t pc = __shfl(pre, c < kWave ? c : kWave - 1, kWave);
+                    if (c < kWave && pc <= k) lo = c;
+                }
+                const int64_t eo = __shfl(e0, lo, kWave);
+                const uint32_t po = __shfl(pre, lo, kWave);
+                const unsigned long long dbits = __shfl(du, lo, kWave);
+                bool won = false;
+                int32_t t = 0;
+                if (k < total) {
+                    const int64_t e = eo + (int64_t)(k - po);
+                    t = B.sci[e];
+                    const unsigned long long nd =
+                        (unsigned long long)__double_as_longlong(__longlong_as_double((long long)dbits) + B.sw[e]);
+                    unsigned long long *dv = &B.dist[B.v0 + t];
+                    if (nd < __hip_atomic_load(dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        // no return: the load decided that the vertex improves this round
+                        __hip_atomic_fetch_min(dv, nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        won = B.istamp[t] != round && atomicExch(&B.istamp[t], round) != round;
+                    }
+                }
+                claim(won, (int32_t)(B.v0 + t));
+            }
         }
     }
+    __syncthreads();
+    const uint32_t n_st = min(scnt, (uint32_t)kStageCap);
+    if (threadIdx.x == 0) sbase = n_st ? atomicAdd(&st->nimp, n_st) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n_st; i += kSB) B.imp[sbase + i] = stage[i];
 }
 
 // (vertex, distance bits) of the improved owned vertices, then {count, done}.
@@ -276,29 +572,45 @@ __global__ __launch_bounds__(kSB) void k_split_pairs(SplitBufs B, uint64_t *pair
     }
 }
 
-// Every rank's pairs (rank r's at pairs + 2 r stride, their number at counts[2 r]).
+// Every rank's pairs (rank r's at pairs + 2 r stride, their number at counts[2 r]), as one
+// index space cut into tiles.
 __global__ __launch_bounds__(kSB) void k_split_apply(SplitBufs B, const uint64_t *pairs, const uint64_t *counts,
                                                      int nranks, uint64_t stride) {
     SplitState *st = B.st;
-    if (st->mode == kNone) return;
+    if (st->mode == kNone || st->mode == kSplit) return;
     const int64_t cur = st->cur;
-    const int32_t epoch = st->epoch, nx = st->fc ^ 1, pin = st->pin;
-    for (int r = 0; r < nranks; r++) {
-        const uint64_t cnt = counts[2 * r];
-        const uint64_t *pr = pairs + 2 * (uint64_t)r * stride;
-        const uint64_t span = (cnt + kSB - 1) / kSB * kSB;
-        for (uint64_t i = (uint64_t)blockIdx.x * kSB + threadIdx.x; i < span; i += (uint64_t)gridDim.x * kSB) {
-            const bool valid = i < cnt;
-            const int64_t v = valid ? (int64_t)pr[2 * i] : 0;
-            const unsigned long long d = valid ? pr[2 * i + 1] : kInf;
-            if (valid && d < B.dist[v]) B.dist[v] = d;   // one pair per vertex and round
-            const bool near = valid && sbucket(d, B.inv_delta) <= cur;
-            const bool far = valid && !near && B.pstamp[v] == 0;
-            if (far) B.pstamp[v] = 1;
-            const uint32_t at = wave_reserve(&st->pcnt[pin], far ? 1u : 0u);
-            if (far) B.plist[pin][at] = (int32_t)v;
-            queue_frontier(B, near, v, d, nx, epoch);
+    const int32_t epoch = st->epoch, nx = st->fc ^ 1;
+    uint64_t tot = 0;
+    for (int r = 0; r < nranks; r++) tot += counts[2 * r];
+    __shared__ Tile T;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kTile; t0 < tot; t0 += (uint64_t)gridDim.x * kTile) {
+        tile_begin(T);
+        Push P[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            uint64_t i = t0 + (uint64_t)k * kSB + threadIdx.x;
+            const bool valid = i < tot;
+            int64_t v = 0;
+            unsigned long long d = kInf;
+            if (valid) {
+                int r = 0;
+                while (i >= counts[2 * r]) {
+                    i -= counts[2 * r];
+                    r++;
+                }
+                const uint64_t *pr = pairs + 2 * ((uint64_t)r * stride + i);
+                v = (int64_t)pr[0];
+                d = pr[1];
+                if (d < B.dist[v]) B.dist[v] = d;   // one pair per vertex and round
+            }
+            const int64_t b = valid ? sbucket(d, B.inv_delta) : 0;
+            const bool near = valid && b <= cur;
+            tile_stage(B, T, P[k], near, valid && !near, v, d, b, epoch);
         }
+        tile_reserve(st, T, nx);
+#pragma unroll
+        for (int k = 0; k < kPer; k++) tile_write(B, T, P[k], nx);
+        __syncthreads();
     }
 }
 
@@ -364,6 +676,44 @@ __global__ __launch_bounds__(kSB) void k_slice_scatter(const int64_t *__restrict
     }
 }
 
+// PULL layout: the heavy entries (w >= delta) of the owned rows of A (an undirected graph's
+// in-edges), row order kept.  Wave per row.
+__global__ __launch_bounds__(kSB) void k_own_count(const int64_t *__restrict__ rp, const double *__restrict__ w,
+                                                   int64_t v0, int64_t v1, double delta, int64_t *cnt) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * (kSB / kWave), own = v1 - v0;
+    for (int64_t i = ((int64_t)blockIdx.x * kSB + threadIdx.x) / kWave; i < own; i += nw) {
+        uint32_t h = 0;
+        for (int64_t e = rp[v0 + i] + lane; e < rp[v0 + i + 1]; e += kWave) h += !(w[e] < delta);
+        for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off, kWave);
+        if (lane == 0) cnt[i] = h;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[own] = 0;
+}
+
+__global__ __launch_bounds__(kSB) void k_own_scatter(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                     const double *__restrict__ w, int64_t v0, int64_t v1, double delta,
+                                                     const int64_t *__restrict__ orp, int32_t *oci, double *ow) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * (kSB / kWave), own = v1 - v0;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int64_t i = ((int64_t)blockIdx.x * kSB + threadIdx.x) / kWave; i < own; i += nw) {
+        int64_t at = orp[i];
+        const int64_t r0 = rp[v0 + i], r1 = rp[v0 + i + 1];
+        for (int64_t eb = r0; eb < r1; eb += kWave) {
+            const int64_t e = eb + lane;
+            const bool hv = e < r1 && !(w[e] < delta);
+            const uint64_t m = __ballot(hv);
+            if (hv) {
+                const int64_t q = at + __popcll(m & below);
+                oci[q] = ci[e];
+                ow[q] = w[e];
+            }
+            at += __popcll(m);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_split_sum_w(const double *__restrict__ w, int64_t m, double *sum) {
     double acc = 0.0;
     for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < m; k += (int64_t)gridDim.x * 256) acc += w[k];
@@ -378,13 +728,14 @@ using namespace gx;
 
 struct gx_sssp_split {
     gx_graph *g = nullptr;
-    int64_t n = 0, v0 = 0, v1 = 0, snnz = 0;
+    int64_t n = 0, v0 = 0, v1 = 0, snnz = 0, onnz = 0;
     double delta = 1.0;
-    DBuf<int64_t> srp, slend;
-    DBuf<int32_t> sci;
-    DBuf<double> sw;
+    uint32_t pull_min = 0, fuse = 0;
+    DBuf<int64_t> srp, slend, orp;
+    DBuf<int32_t> sci, oci;
+    DBuf<double> sw, ow;
     DBuf<unsigned long long> dist, lrel;
-    DBuf<int32_t> sstamp, pstamp, istamp, plist0, plist1, imp;
+    DBuf<int32_t> sstamp, hdone, hmark, qstamp, bstamp, ostamp, istamp, sverts, ring, ovf0, ovf1, cand, imp;
     DBuf<uint64_t> fitems0, fitems1, sitems, own_pairs, own_count;
     DBuf<SplitState> st;
     int32_t *h_done = nullptr;
@@ -398,20 +749,31 @@ struct gx_sssp_split {
         B.slend = slend.p;
         B.sci = sci.p;
         B.sw = sw.p;
+        B.orp = orp.p;
+        B.oci = oci.p;
+        B.ow = ow.p;
         B.dist = dist.p;
         B.lrel = lrel.p;
         B.sstamp = sstamp.p;
-        B.pstamp = pstamp.p;
+        B.hdone = hdone.p;
+        B.hmark = hmark.p;
+        B.qstamp = qstamp.p;
+        B.bstamp = bstamp.p;
+        B.ostamp = ostamp.p;
         B.istamp = istamp.p;
         B.fitems[0] = fitems0.p;
         B.fitems[1] = fitems1.p;
         B.sitems = sitems.p;
-        B.plist[0] = plist0.p;
-        B.plist[1] = plist1.p;
+        B.sverts = sverts.p;
+        B.ring = ring.p;
+        B.ovf[0] = ovf0.p;
+        B.ovf[1] = ovf1.p;
+        B.cand = cand.p;
         B.imp = imp.p;
         B.n = n;
         B.v0 = v0;
         B.v1 = v1;
+        B.delta = delta;
         B.inv_delta = 1.0 / delta;
         B.st = st.p;
         return B;
@@ -422,12 +784,12 @@ struct gx_sssp_split {
 // steps order with the tensors and collectives issued there
 static hipStream_t split_stream(gx_sssp_split *, void *stream) { return (hipStream_t)stream; }
 
-// plan -> minb -> take -> relax -> pairs (this rank's improved owned vertices)
+// plan -> prep -> cand -> relax -> pairs (this rank's improved owned vertices)
 static int split_relax(gx_sssp_split *p, uint64_t *pairs, uint64_t *count, hipStream_t s) {
     const SplitBufs B = p->bufs();
     hipLaunchKernelGGL(k_split_plan, dim3(1), dim3(1), 0, s, B.st);
-    hipLaunchKernelGGL(k_split_minb, dim3(p->grid), dim3(kSB), 0, s, B);
-    hipLaunchKernelGGL(k_split_take, dim3(p->grid), dim3(kSB), 0, s, B);
+    hipLaunchKernelGGL(k_split_prep, dim3(p->grid), dim3(kSB), 0, s, B);
+    hipLaunchKernelGGL(k_split_cand, dim3(p->grid), dim3(kSB), 0, s, B);
     hipLaunchKernelGGL(k_split_relax, dim3(p->grid), dim3(kSB), 0, s, B);
     hipLaunchKernelGGL(k_split_pairs, dim3(p->grid), dim3(kSB), 0, s, B, pairs, count);
     return check_launch("k_split_relax");
@@ -443,7 +805,7 @@ extern "C" int gx_sssp_split_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_ss
     if (!g || !out) return fail(GX_NULL_POINTER, "gx_sssp_split_create: null argument");
     if (!g->weighted) return fail(GX_INVALID_VALUE, "gx_sssp_split_create: graph has no edge weights");
     if (v0 > v1 || v1 > g->n) return fail(GX_INVALID_INDEX, "gx_sssp_split_create: bad vertex range");
-    if (g->n >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_sssp_split_create: more than 2^31 vertices");
+    if (g->n >= (1ull << 31) / kW) return fail(GX_NOT_IMPLEMENTED, "gx_sssp_split_create: more than 2^26 vertices");
     GX_HIP_TRY(hipSetDevice(g->ctx->device));
     hipStream_t s = g->ctx->stream;
     std::unique_ptr<gx_sssp_split> p(new gx_sssp_split());
@@ -473,6 +835,20 @@ extern "C" int gx_sssp_split_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_ss
     if (!(delta > 0.0)) delta = scale * mean / std::max(1.0, (double)g->nnz / std::max<double>(1.0, (double)n));
     if (!(delta > 0.0) || !std::isfinite(delta)) delta = 1.0;
     p->delta = delta;
+    // the heavy phase is pulled (undirected graphs) once the settled batch holds 1/8 of the
+    // vertices with edges (gx_sssp's rule; GX_SSSP_PULL = 0 never, 2 always); buckets are fused
+    // while they hold at most n / 16 vertices (GX_SSSP_FUSE)
+    int64_t nonisolated = n;
+    if ((int64_t)g->A.h_rp.size() == n + 1) {
+        nonisolated = 0;
+        for (int64_t v = 0; v < n; v++) nonisolated += g->A.h_rp[v + 1] != g->A.h_rp[v];
+    }
+    const int pull_mode = std::getenv("GX_SSSP_PULL") ? std::atoi(std::getenv("GX_SSSP_PULL")) : 1;
+    const bool can_pull = !g->directed && pull_mode != 0;
+    p->pull_min = !can_pull ? 0u : pull_mode == 2 ? 1u : (uint32_t)std::max<int64_t>(1, nonisolated / 8);
+    p->fuse = std::getenv("GX_SSSP_FUSE") ? (uint32_t)std::max(1, std::atoi(std::getenv("GX_SSSP_FUSE")))
+                                          : (uint32_t)std::max<int64_t>(1024, n / 16);
+    const unsigned wg_all = grid_for((uint64_t)std::max<int64_t>(n, 1) * kWave, kSB, 16384);
     // slice: count, scan, scatter
     GX_TRY(p->srp.alloc(n + 1));
     GX_TRY(p->slend.alloc(std::max<int64_t>(n, 1)));
@@ -480,10 +856,9 @@ extern "C" int gx_sssp_split_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_ss
         DBuf<int64_t> lc, tc;
         GX_TRY(lc.alloc(std::max<int64_t>(n, 1)));
         GX_TRY(tc.alloc(n + 1));
-        const unsigned wg = grid_for((uint64_t)n * kWave, kSB, 16384);
         if (n) {
-            hipLaunchKernelGGL(k_slice_count, dim3(wg), dim3(kSB), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, n, p->v0, p->v1,
-                               delta, lc.p, tc.p);
+            hipLaunchKernelGGL(k_slice_count, dim3(wg_all), dim3(kSB), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, n, p->v0,
+                               p->v1, delta, lc.p, tc.p);
             GX_TRY(check_launch("k_slice_count"));
         } else {
             GX_HIP_TRY(hipMemsetAsync(tc.p, 0, sizeof(int64_t), s));
@@ -494,26 +869,50 @@ extern "C" int gx_sssp_split_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_ss
         GX_TRY(p->sci.alloc(std::max<int64_t>(p->snnz, 1)));
         GX_TRY(p->sw.alloc(std::max<int64_t>(p->snnz, 1)));
         if (n) {
-            hipLaunchKernelGGL(k_slice_scatter, dim3(wg), dim3(kSB), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, n, p->v0,
+            hipLaunchKernelGGL(k_slice_scatter, dim3(wg_all), dim3(kSB), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, n, p->v0,
                                p->v1, delta, p->srp.p, lc.p, p->slend.p, p->sci.p, p->sw.p);
             GX_TRY(check_launch("k_slice_scatter"));
         }
         GX_HIP_TRY(hipStreamSynchronize(s));   // lc / tc die here
     }
+    // owned rows' heavy in-edges (PULL)
+    GX_TRY(p->orp.alloc(own + 1));
+    if (can_pull) {
+        DBuf<int64_t> cnt;
+        GX_TRY(cnt.alloc(own + 1));
+        const unsigned wg_own = grid_for((uint64_t)std::max<int64_t>(own, 1) * kWave, kSB, 16384);
+        hipLaunchKernelGGL(k_own_count, dim3(wg_own), dim3(kSB), 0, s, g->A.rp.p, g->A.w.p, p->v0, p->v1, delta, cnt.p);
+        GX_TRY(check_launch("k_own_count"));
+        GX_TRY(scan_exclusive_i64(cnt.p, p->orp.p, (size_t)(own + 1), s));
+        GX_HIP_TRY(hipMemcpyAsync(&p->onnz, p->orp.p + own, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+        GX_TRY(p->oci.alloc(std::max<int64_t>(p->onnz, 1)));
+        GX_TRY(p->ow.alloc(std::max<int64_t>(p->onnz, 1)));
+        if (own) {
+            hipLaunchKernelGGL(k_own_scatter, dim3(wg_own), dim3(kSB), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, p->v0, p->v1,
+                               delta, p->orp.p, p->oci.p, p->ow.p);
+            GX_TRY(check_launch("k_own_scatter"));
+        }
+        GX_HIP_TRY(hipStreamSynchronize(s));
+    } else {
+        GX_HIP_TRY(hipMemset(p->orp.p, 0, (own + 1) * sizeof(int64_t)));
+    }
     // state: item lists hold at most one item per vertex plus one per 256 slice entries
     const uint64_t icap = (uint64_t)n + (uint64_t)p->snnz / kSChunk + 64;
-    GX_TRY(p->dist.alloc(std::max<int64_t>(n, 1)));
-    GX_TRY(p->lrel.alloc(std::max<int64_t>(n, 1)));
-    GX_TRY(p->sstamp.alloc(std::max<int64_t>(n, 1)));
-    GX_TRY(p->pstamp.alloc(std::max<int64_t>(n, 1)));
-    GX_TRY(p->istamp.alloc(std::max<int64_t>(own, 1)));
-    GX_TRY(p->plist0.alloc(std::max<int64_t>(n, 1)));
-    GX_TRY(p->plist1.alloc(std::max<int64_t>(n, 1)));
-    GX_TRY(p->imp.alloc(std::max<int64_t>(own, 1)));
+    const int64_t n1 = std::max<int64_t>(n, 1), own1 = std::max<int64_t>(own, 1);
+    GX_TRY(p->dist.alloc(n1));
+    GX_TRY(p->lrel.alloc(n1));
+    for (DBuf<int32_t> *b : {&p->sstamp, &p->hdone, &p->hmark, &p->qstamp, &p->bstamp, &p->ostamp, &p->sverts,
+                             &p->ovf0, &p->ovf1})
+        GX_TRY(b->alloc(n1));
+    GX_TRY(p->ring.alloc((uint64_t)n1 * kW));
+    GX_TRY(p->istamp.alloc(own1));
+    GX_TRY(p->cand.alloc(own1));
+    GX_TRY(p->imp.alloc(own1));
     GX_TRY(p->fitems0.alloc(icap));
     GX_TRY(p->fitems1.alloc(icap));
     GX_TRY(p->sitems.alloc(icap));
-    GX_TRY(p->own_pairs.alloc(2 * (uint64_t)std::max<int64_t>(own, 1)));
+    GX_TRY(p->own_pairs.alloc(2 * (uint64_t)own1));
     GX_TRY(p->own_count.alloc(2));
     GX_TRY(p->st.alloc(1));
     GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&p->h_done), 2 * sizeof(int32_t), hipHostMallocDefault));
@@ -544,7 +943,7 @@ extern "C" int gx_sssp_split_start(gx_sssp_split *p, uint64_t src, void *stream)
     const SplitBufs B = p->bufs();
     hipLaunchKernelGGL(k_split_start, dim3(grid_for(std::max<int64_t>(p->n, 1), kSB, 8192)), dim3(kSB), 0, s, B,
                        (int64_t)src);
-    hipLaunchKernelGGL(k_split_seed, dim3(1), dim3(kSB), 0, s, B, (int64_t)src);
+    hipLaunchKernelGGL(k_split_seed, dim3(1), dim3(kSB), 0, s, B, (int64_t)src, p->pull_min, p->fuse);
     return check_launch("k_split_seed");
 }
 
@@ -591,6 +990,15 @@ extern "C" int gx_sssp_split_run(gx_sssp_split *p, uint64_t src, double *dist_ho
         if (guard > 4 * (p->n + 16)) return fail(GX_DEVICE_ERROR, "gx_sssp_split_run: no fixed point");
     }
     GX_TRY(device_end(ctx));
+    if (std::getenv("GX_SPLIT_VERBOSE")) {
+        SplitState h;
+        GX_HIP_TRY(hipMemcpy(&h, p->st.p, sizeof(h), hipMemcpyDeviceToHost));
+        std::fprintf(stderr,
+                     "[gx_sssp_split] delta %.4g rounds %d: light %u (items %llu), heavy push %u (items %llu), "
+                     "pull %u, advance %u, split %u\n",
+                     p->delta, h.round, h.nmode[kLight], h.nitems[kLight], h.nmode[kHeavy], h.nitems[kHeavy],
+                     h.nmode[kPull], h.nmode[kAdvance], h.nmode[kSplit]);
+    }
     GX_HIP_TRY(hipMemcpy(dist_host, p->dist.p, (size_t)p->n * 8, hipMemcpyDeviceToHost));
     return GX_SUCCESS;
 }

@@ -32,12 +32,18 @@ def _src(csr):
 GRAPHS = [(10, 8, 1, True), (13, 16, 2, True), (12, 8, 3, False), (14, 6, 4, False)]
 
 
+ENVS = [{}, {"GX_SSSP_DSCALE": "0.25"}, {"GX_SSSP_DSCALE": "40"}, {"GX_SSSP_PULL": "2"}, {"GX_SSSP_PULL": "0"},
+        {"GX_SSSP_FUSE": "1"}, {"GX_SSSP_FUSE": "1", "GX_SSSP_DSCALE": "0.05"}]
+
+
 @pytest.mark.parametrize("scale,ef,seed,und", GRAPHS)
-@pytest.mark.parametrize("dscale", [None, "0.25", "40"])
-def test_split_run_one_rank(ctx, monkeypatch, scale, ef, seed, und, dscale):
+@pytest.mark.parametrize("env", ENVS)
+def test_split_run_one_rank(ctx, monkeypatch, scale, ef, seed, und, env):
+    """Every schedule: bucket widths (0.05 x the default puts most vertices past the 32-bucket
+    ring window, through the overflow), pulled / pushed heavy phases, no bucket fusion."""
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
-    if dscale:
-        monkeypatch.setenv("GX_SSSP_DSCALE", dscale)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     csr = rmat(scale, ef, seed, undirected=und, weighted=True)
     G = A.Graph(ctx, csr, not und)
     sp = A.SsspSplit(G)
@@ -71,11 +77,14 @@ def test_split_run_unreachable_and_isolated(ctx):
         G.close()
 
 
-@pytest.mark.parametrize("nranks", [2, 4, 5])
-def test_split_simulated_ranks(ctx, nranks):
+@pytest.mark.parametrize("nranks,env", [(2, {}), (4, {}), (5, {}), (3, {"GX_SSSP_PULL": "2"}),
+                                        (3, {"GX_SSSP_FUSE": "1", "GX_SSSP_DSCALE": "0.05"})])
+def test_split_simulated_ranks(ctx, monkeypatch, nranks, env):
     """The per-round protocol with 2, 4 and 5 ranks on one device (rank ranges balanced by
-    entries; with 5 ranks on a graph whose hubs sit in the first range, one range is tiny)."""
+    entries), also with an always-pulled heavy phase and through the overflow."""
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Graph
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     dev = torch.device("cuda", 0)
     for csr, directed in [(rmat(13, 8, 31, undirected=True, weighted=True), False),
                           (rmat(12, 6, 32, undirected=False, weighted=True), True)]:
