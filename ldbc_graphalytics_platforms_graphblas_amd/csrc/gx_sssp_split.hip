@@ -73,6 +73,7 @@ struct SplitState {
     uint32_t fuse;                // ADVANCE opens further slots while the vertices stay <= fuse
     uint32_t nmode[6];            // rounds per mode (GX_SPLIT_VERBOSE)
     unsigned long long nitems[6]; // items / candidates per mode (rank-local)
+    int8_t modelog[256];          // mode of rounds 1..256 (GX_SPLIT_VERBOSE)
 };
 
 struct SplitBufs {
@@ -251,6 +252,8 @@ __global__ void k_split_seed(SplitBufs B, int64_t src, uint32_t pull_min, uint32
     tile_write(B, T, P, 1);
 }
 
+__device__ void k_split_plan_body(SplitState *st);
+
 __global__ void k_split_plan(SplitState *st) {
     st->nimp = 0;
     st->ncand = 0;
@@ -259,6 +262,11 @@ __global__ void k_split_plan(SplitState *st) {
         return;
     }
     st->round++;
+    k_split_plan_body(st);
+    if (st->round <= 256) st->modelog[st->round - 1] = (int8_t)st->mode;
+}
+
+__device__ void k_split_plan_body(SplitState *st) {
     if (st->consume >= 0) {
         for (int j = 0; j < st->consume_n; j++) st->ring_cnt[(st->consume + j) % kW] = 0;
         st->consume = -1;
@@ -727,7 +735,9 @@ __global__ __launch_bounds__(256) void k_split_sum_w(const double *__restrict__ 
 using namespace gx;
 
 struct gx_sssp_split {
-    gx_graph *g = nullptr;
+    gx_graph *g = nullptr;        // the graph the slice is built on (a single rank: its hub-first copy)
+    gx_graph *caller = nullptr;   // the graph gx_sssp_split_create was given
+    bool hub_checked = false;     // gx_sssp_split_run looked for the hub-first copy
     int64_t n = 0, v0 = 0, v1 = 0, snnz = 0, onnz = 0;
     double delta = 1.0;
     uint32_t pull_min = 0, fuse = 0;
@@ -801,18 +811,29 @@ static int split_apply(gx_sssp_split *p, const uint64_t *pairs, const uint64_t *
     return check_launch("k_split_apply");
 }
 
+static int split_build(gx_sssp_split *p, gx_graph *g);
+
 extern "C" int gx_sssp_split_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_sssp_split **out) {
     if (!g || !out) return fail(GX_NULL_POINTER, "gx_sssp_split_create: null argument");
     if (!g->weighted) return fail(GX_INVALID_VALUE, "gx_sssp_split_create: graph has no edge weights");
     if (v0 > v1 || v1 > g->n) return fail(GX_INVALID_INDEX, "gx_sssp_split_create: bad vertex range");
     if (g->n >= (1ull << 31) / kW) return fail(GX_NOT_IMPLEMENTED, "gx_sssp_split_create: more than 2^26 vertices");
     GX_HIP_TRY(hipSetDevice(g->ctx->device));
-    hipStream_t s = g->ctx->stream;
     std::unique_ptr<gx_sssp_split> p(new gx_sssp_split());
-    p->g = g;
-    p->n = (int64_t)g->n;
+    p->caller = g;
     p->v0 = (int64_t)v0;
     p->v1 = (int64_t)v1;
+    GX_TRY(split_build(p.get(), g));
+    *out = p.release();
+    return GX_SUCCESS;
+}
+
+// The slice, the PULL layout and the work buffers of p for graph g (the caller's graph, or
+// for gx_sssp_split_run its hub-first copy); earlier buffers are released.
+static int split_build(gx_sssp_split *p, gx_graph *g) {
+    hipStream_t s = g->ctx->stream;
+    p->g = g;
+    p->n = (int64_t)g->n;
     const int64_t n = p->n, own = p->v1 - p->v0;
     // bucket width: gx_sssp's rule (scale x mean weight / mean degree; GX_SSSP_DELTA and
     // GX_SSSP_DSCALE override) -- any positive value gives the same distances
@@ -915,9 +936,9 @@ extern "C" int gx_sssp_split_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_ss
     GX_TRY(p->own_pairs.alloc(2 * (uint64_t)own1));
     GX_TRY(p->own_count.alloc(2));
     GX_TRY(p->st.alloc(1));
-    GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&p->h_done), 2 * sizeof(int32_t), hipHostMallocDefault));
+    if (!p->h_done)
+        GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&p->h_done), 2 * sizeof(int32_t), hipHostMallocDefault));
     p->grid = (unsigned)std::max(1, g->ctx->num_cus) * 8;
-    *out = p.release();
     return GX_SUCCESS;
 }
 
@@ -938,6 +959,7 @@ extern "C" int gx_sssp_split_delta(gx_sssp_split *p, double *delta) {
 extern "C" int gx_sssp_split_start(gx_sssp_split *p, uint64_t src, void *stream) {
     if (!p) return fail(GX_NULL_POINTER, "gx_sssp_split_start: null argument");
     if (src >= (uint64_t)p->n) return fail(GX_INVALID_INDEX, "gx_sssp_split_start: source out of range");
+    if (p->g != p->caller) src = (uint64_t)p->caller->h_hub_perm[src];
     GX_HIP_TRY(hipSetDevice(p->g->ctx->device));
     hipStream_t s = split_stream(p, stream);
     const SplitBufs B = p->bufs();
@@ -964,7 +986,10 @@ extern "C" int gx_sssp_split_apply(gx_sssp_split *p, const uint64_t *pairs, cons
 extern "C" int gx_sssp_split_distances(gx_sssp_split *p, double *dist, void *stream) {
     if (!p || !dist) return fail(GX_NULL_POINTER, "gx_sssp_split_distances: null argument");
     GX_HIP_TRY(hipSetDevice(p->g->ctx->device));
-    GX_HIP_TRY(hipMemcpyAsync(dist, p->dist.p, (size_t)p->n * 8, hipMemcpyDeviceToDevice, split_stream(p, stream)));
+    hipStream_t s = split_stream(p, stream);
+    const void *res = nullptr;
+    GX_TRY(remap_out(p->g, p->dist.p, 8, s, &res));   // hub-first copy -> the caller's order
+    GX_HIP_TRY(hipMemcpyAsync(dist, res, (size_t)p->n * 8, hipMemcpyDeviceToDevice, s));
     return GX_SUCCESS;
 }
 
@@ -976,6 +1001,14 @@ extern "C" int gx_sssp_split_run(gx_sssp_split *p, uint64_t src, double *dist_ho
     gx_ctx *ctx = p->g->ctx;
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
+    if (!p->hub_checked) {
+        // one rank owning every vertex: the hub-first copy of an undirected graph, as gx_sssp
+        // runs from its second call (gx_runtime.hip hub_for; GX_HUB=0 keeps the caller's order)
+        p->hub_checked = true;
+        gx_graph *h = nullptr;
+        GX_TRY(hub_for(p->caller, 2, &h, nullptr));
+        if (h && h != p->g) GX_TRY(split_build(p, h));
+    }
     GX_TRY(device_begin(ctx));
     GX_TRY(gx_sssp_split_start(p, src, s));
     constexpr int kBatch = 16;
@@ -998,8 +1031,14 @@ extern "C" int gx_sssp_split_run(gx_sssp_split *p, uint64_t src, double *dist_ho
                      "pull %u, advance %u, split %u\n",
                      p->delta, h.round, h.nmode[kLight], h.nitems[kLight], h.nmode[kHeavy], h.nitems[kHeavy],
                      h.nmode[kPull], h.nmode[kAdvance], h.nmode[kSplit]);
+        std::fprintf(stderr, "[gx_sssp_split] modes:");
+        for (int i = 0; i < std::min(h.round, 256); i++) std::fprintf(stderr, " %d", (int)h.modelog[i]);
+        std::fprintf(stderr, "\n");
     }
-    GX_HIP_TRY(hipMemcpy(dist_host, p->dist.p, (size_t)p->n * 8, hipMemcpyDeviceToHost));
+    const void *res = nullptr;
+    GX_TRY(remap_out(p->g, p->dist.p, 8, s, &res));   // hub-first copy -> the caller's order
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    GX_HIP_TRY(hipMemcpy(dist_host, res, (size_t)p->n * 8, hipMemcpyDeviceToHost));
     return GX_SUCCESS;
 }
 
