@@ -43,6 +43,7 @@ namespace {
 constexpr int kSB = 256;        // threads per block
 constexpr int kSChunk = 256;    // edges per relax item
 constexpr int kW = 32;          // bucket ring slots
+constexpr int kSmallDeg = 32;   // PULL: candidates up to this many heavy in-edges take a thread
 constexpr unsigned long long kInf = 0x7FF0000000000000ull;   // +inf bits
 
 enum : int32_t { kNone = 0, kLight = 1, kHeavy = 2, kAdvance = 3, kPull = 4, kSplit = 5 };
@@ -55,6 +56,7 @@ struct SplitState {
     unsigned long long ovf_minb;  // smallest bucket on the overflow list being filled
     unsigned long long smin;      // PULL: smallest distance of the settled batch
     int32_t mode, round, epoch, done;
+    int32_t epoch_round;          // round that opened the current epoch
     int32_t fc;                   // frontier list relaxed this round (LIGHT / ADVANCE)
     int32_t oe;                   // overflow list being filled; SPLIT reads oe ^ 1
     int32_t ostamp_tag;           // overflow dedupe tag (one per overflow generation)
@@ -67,7 +69,7 @@ struct SplitState {
     uint32_t sb0, sb1;
     uint32_t ring_cnt[kW];
     uint32_t ovf_cnt[2];
-    uint32_t ncand;               // PULL candidates (rank-local)
+    uint32_t ncand, ncand_big;    // PULL candidates with <= kSmallDeg heavy in-edges / more (rank-local)
     uint32_t nimp;                // improved owned vertices this round (rank-local)
     uint32_t pull_min;            // settled batch size from which the heavy phase is pulled (0: never)
     uint32_t fuse;                // ADVANCE opens further slots while the vertices stay <= fuse
@@ -87,8 +89,7 @@ struct SplitBufs {
     unsigned long long *dist;     // replicated distances (fp64 bits)
     unsigned long long *lrel;     // distance v's light edges were queued for relaxing with
     int32_t *sstamp;              // epoch v joined the settled set
-    int32_t *hdone;               // epoch v's heavy edges were relaxed (0: pending)
-    int32_t *hmark;               // PULL: round v is in the settled batch
+    int32_t *hmark;               // round of the HEAVY / PULL phase that relaxed v's heavy edges (0: pending)
     int32_t *qstamp;              // ADVANCE: round v was taken from the ring
     int32_t *bstamp;              // bucket v was last put into a ring slot for (low 32 bits + 1)
     int32_t *ostamp;              // overflow tag v was last put on the overflow with
@@ -98,7 +99,7 @@ struct SplitBufs {
     int32_t *sverts;              // settled vertices of the epoch (replicated set)
     int32_t *ring;                // kW slots of n vertices
     int32_t *ovf[2];
-    int32_t *cand;                // PULL candidates (owned vertices)
+    int32_t *cand, *cand_big;     // PULL candidates (owned vertices - v0): thread / wave each
     int32_t *imp;                 // improved owned vertices (global ids)
     int64_t n, v0, v1;
     double delta, inv_delta;
@@ -121,6 +122,14 @@ __device__ __forceinline__ uint32_t nchunks(int64_t len) { return (uint32_t)max<
 constexpr int kPer = 8;                    // elements per thread and tile
 constexpr int kTile = kSB * kPer;
 enum : int { kQFv = 0, kQFi, kQSv, kQSi, kQOvf, kQRing, kQCat = kQRing + kW };
+
+// elements per thread for `tot` elements over the grid: the full kPer only when the input
+// fills every workgroup's tiles (a small input on few workgroups would run kPer dependent
+// element chains per thread in series)
+__device__ __forceinline__ uint32_t tile_per(uint64_t tot) {
+    const uint64_t per = (tot + (uint64_t)gridDim.x * kSB - 1) / ((uint64_t)gridDim.x * kSB);
+    return (uint32_t)max<uint64_t>(1, min<uint64_t>(kPer, per));
+}
 
 struct Tile {
     uint32_t cnt[kQCat];
@@ -157,9 +166,9 @@ __device__ __forceinline__ void tile_stage(const SplitBufs &B, Tile &T, Push &P,
         P.nl = nchunks(B.slend[v] - B.srp[v]);
         atomicAdd(&T.cnt[kQFv], 1u);
         P.offi = atomicAdd(&T.cnt[kQFi], P.nl);
-        if (B.sstamp[v] != epoch || B.hdone[v] == epoch) {
+        if (B.sstamp[v] != epoch || B.hmark[v] >= st->epoch_round) {
             B.sstamp[v] = epoch;
-            B.hdone[v] = 0;
+            B.hmark[v] = 0;
             P.isv = 1;
             P.nh = nchunks(B.srp[v + 1] - B.slend[v]);
             P.offsv = atomicAdd(&T.cnt[kQSv], 1u);
@@ -222,7 +231,6 @@ __global__ void k_split_start(SplitBufs B, int64_t src) {
         B.dist[v] = v == src ? 0ull : kInf;
         B.lrel[v] = kInf;
         B.sstamp[v] = 0;
-        B.hdone[v] = 0;
         B.hmark[v] = 0;
         B.qstamp[v] = 0;
         B.bstamp[v] = 0;
@@ -236,6 +244,7 @@ __global__ void k_split_seed(SplitBufs B, int64_t src, uint32_t pull_min, uint32
     if (threadIdx.x == 0) {
         memset(st, 0, sizeof(SplitState));
         st->epoch = 1;
+        st->epoch_round = 1;
         st->ostamp_tag = 1;
         st->consume = -1;
         st->ovf_minb = ~0ull;
@@ -256,7 +265,7 @@ __device__ void k_split_plan_body(SplitState *st);
 
 __global__ void k_split_plan(SplitState *st) {
     st->nimp = 0;
-    st->ncand = 0;
+    st->ncand = st->ncand_big = 0;
     if (st->done) {
         st->mode = kNone;
         return;
@@ -316,6 +325,7 @@ __device__ void k_split_plan_body(SplitState *st) {
         st->consume = st->slot0;
         st->consume_n = st->nslots;
         st->epoch++;
+        st->epoch_round = st->round;
         st->sv = st->sv_done = st->si = st->si_done = 0;
         st->fc = nx;   // take fills list fc, apply the other
         st->fv[0] = st->fv[1] = st->fi[0] = st->fi[1] = 0;
@@ -353,13 +363,14 @@ __global__ __launch_bounds__(kSB) void k_split_prep(SplitBufs B) {
         // the opened slots' entries as one index space
         uint32_t tot = 0;
         for (int j = 0; j < st->nslots; j++) tot += st->ring_cnt[(st->slot0 + j) % kW];
-        for (uint32_t t0 = blockIdx.x * kTile; t0 < tot; t0 += gridDim.x * kTile) {
+        const uint32_t per = tile_per(tot), tile = per * kSB;
+        for (uint32_t t0 = blockIdx.x * tile; t0 < tot; t0 += gridDim.x * tile) {
             tile_begin(T);
             Push P[kPer];
 #pragma unroll
             for (int k = 0; k < kPer; k++) {
                 uint32_t i = t0 + k * kSB + threadIdx.x;
-                const bool valid = i < tot;
+                const bool valid = k < (int)per && i < tot;
                 int32_t v = 0;
                 if (valid) {
                     int j = 0;
@@ -384,13 +395,14 @@ __global__ __launch_bounds__(kSB) void k_split_prep(SplitBufs B) {
     } else if (mode == kSplit) {
         const int src = st->oe ^ 1;
         const uint32_t cnt = st->ovf_cnt[src];
-        for (uint32_t t0 = blockIdx.x * kTile; t0 < cnt; t0 += gridDim.x * kTile) {
+        const uint32_t per = tile_per(cnt), tile = per * kSB;
+        for (uint32_t t0 = blockIdx.x * tile; t0 < cnt; t0 += gridDim.x * tile) {
             tile_begin(T);
             Push P[kPer];
 #pragma unroll
             for (int k = 0; k < kPer; k++) {
                 const uint32_t i = t0 + k * kSB + threadIdx.x;
-                const bool valid = i < cnt;
+                const bool valid = k < (int)per && i < cnt;
                 const int32_t v = valid ? B.ovf[src][i] : 0;
                 const unsigned long long d = valid ? B.dist[v] : kInf;
                 const bool pend = valid && d < B.lrel[v];
@@ -402,15 +414,12 @@ __global__ __launch_bounds__(kSB) void k_split_prep(SplitBufs B) {
             __syncthreads();
         }
     } else if (mode == kHeavy || mode == kPull) {
-        const int32_t epoch = st->epoch, round = st->round;
+        const int32_t round = st->round;
         unsigned long long m = ~0ull;
         for (uint32_t i = st->sb0 + blockIdx.x * kSB + threadIdx.x; i < st->sb1; i += gridDim.x * kSB) {
             const int32_t u = B.sverts[i];
-            B.hdone[u] = epoch;
-            if (mode == kPull) {
-                B.hmark[u] = round;
-                m = min(m, B.dist[u]);
-            }
+            B.hmark[u] = round;
+            if (mode == kPull) m = min(m, B.dist[u]);
         }
         if (mode == kPull) {
             for (int off = 32; off > 0; off >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, off, kWave));
@@ -427,30 +436,36 @@ __global__ __launch_bounds__(kSB) void k_split_cand(SplitBufs B) {
     const unsigned long long lim =
         (unsigned long long)__double_as_longlong(__longlong_as_double((long long)st->smin) + B.delta);
     const int64_t own = B.v1 - B.v0;
-    __shared__ uint32_t lcnt, lbase;
-    for (int64_t t0 = (int64_t)blockIdx.x * kTile; t0 < own; t0 += (int64_t)gridDim.x * kTile) {
-        if (threadIdx.x == 0) lcnt = 0;
+    __shared__ uint32_t lcnt[2], lbase[2];
+    const uint32_t per = tile_per((uint64_t)own), tile = per * kSB;
+    for (int64_t t0 = (int64_t)blockIdx.x * tile; t0 < own; t0 += (int64_t)gridDim.x * tile) {
+        if (threadIdx.x < 2) lcnt[threadIdx.x] = 0;
         __syncthreads();
         uint32_t off[kPer];
-        bool c[kPer];
+        int8_t c[kPer];   // -1 none, 0 small, 1 big
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int64_t i = t0 + k * kSB + threadIdx.x;
-            c[k] = i < own && B.dist[B.v0 + i] > lim && B.orp[i + 1] > B.orp[i];
-            off[k] = c[k] ? atomicAdd(&lcnt, 1u) : 0u;
+            c[k] = -1;
+            if (k < (int)per && i < own && B.dist[B.v0 + i] > lim) {
+                const int64_t deg = B.orp[i + 1] - B.orp[i];
+                if (deg > 0) c[k] = deg > kSmallDeg ? 1 : 0;
+            }
+            off[k] = c[k] >= 0 ? atomicAdd(&lcnt[c[k]], 1u) : 0u;
         }
         __syncthreads();
-        if (threadIdx.x == 0) lbase = lcnt ? atomicAdd(&st->ncand, lcnt) : 0u;
+        if (threadIdx.x < 2)
+            lbase[threadIdx.x] = lcnt[threadIdx.x] ? atomicAdd(threadIdx.x ? &st->ncand_big : &st->ncand, lcnt[threadIdx.x]) : 0u;
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kPer; k++)
-            if (c[k]) B.cand[lbase + off[k]] = (int32_t)(t0 + k * kSB + threadIdx.x);
+            if (c[k] >= 0) (c[k] ? B.cand_big : B.cand)[lbase[c[k]] + off[k]] = (int32_t)(t0 + k * kSB + threadIdx.x);
         __syncthreads();
     }
 }
 
 // LIGHT / ADVANCE: the frontier's light edges; HEAVY: the settled batch's heavy edges.  A wave
-// takes 64 items (vertex, 256-edge chunk) and walks their concatenated edges 64 at a time,
+// takes up to 64 items (vertex, 256-edge chunk) and walks their concatenated edges 64 at a time,
 // each lane finding its item by a shuffle binary search over the items' edge prefix -- a
 // frontier of low-degree vertices fills the lanes.  PULL: one wave per candidate, its heavy
 // in-edges from the settled batch, minimum in registers, written by the wave.  Improved owned
@@ -480,9 +495,33 @@ __global__ __launch_bounds__(kSB) void k_split_relax(SplitBufs B) {
         }
     };
     if (mode == kPull) {
-        const uint32_t nc = st->ncand;
+        // low-degree candidates: a thread each (the loop trip count is uniform per wave)
+        const uint32_t ns = st->ncand;
+        const uint32_t nth = gridDim.x * kSB, span = (ns + kWave - 1) / kWave * kWave;
+        for (uint32_t it = blockIdx.x * kSB + threadIdx.x; it < span; it += nth) {
+            bool won = false;
+            int64_t i = 0;
+            if (it < ns) {
+                i = B.cand[it];
+                unsigned long long best = kInf;
+                for (int64_t e = B.orp[i]; e < B.orp[i + 1]; e++) {
+                    const int32_t u = B.oci[e];
+                    if (B.hmark[u] == round) {
+                        const unsigned long long nd = (unsigned long long)__double_as_longlong(
+                            __longlong_as_double((long long)B.dist[u]) + B.ow[e]);
+                        best = min(best, nd);
+                    }
+                }
+                if (best < B.dist[B.v0 + i]) {
+                    B.dist[B.v0 + i] = best;   // this thread alone writes the vertex this round
+                    won = true;
+                }
+            }
+            claim(won, (int32_t)(B.v0 + i));
+        }
+        const uint32_t nc = st->ncand_big;
         for (uint32_t it = wid; it < nc; it += nw) {
-            const int64_t i = B.cand[it];
+            const int64_t i = B.cand_big[it];
             unsigned long long best = kInf;
             for (int64_t e = B.orp[i] + lane; e < B.orp[i + 1]; e += kWave) {
                 const int32_t u = B.oci[e];
@@ -504,12 +543,15 @@ __global__ __launch_bounds__(kSB) void k_split_relax(SplitBufs B) {
         const bool heavy = mode == kHeavy;
         const uint64_t *items = heavy ? B.sitems : B.fitems[st->fc];
         const uint32_t i0 = heavy ? st->hs0 : 0u, i1 = heavy ? st->hs1 : st->fi[st->fc];
-        for (uint32_t g0 = i0 + wid * kWave; g0 < i1; g0 += nw * kWave) {
-            // lane l: item g0 + l
+        // G = ceil(items / waves) <= 64 items per wave: a short list (a hub's chunks) spreads
+        // over as many waves as it has items instead of filling a few waves' lanes
+        const uint32_t G = max(1u, min((uint32_t)kWave, (i1 - i0 + nw - 1) / nw));
+        for (uint32_t g0 = i0 + wid * G; g0 < i1; g0 += nw * G) {
+            // lane l < G: item g0 + l
             const uint32_t gi = g0 + lane;
             int64_t e0 = 0, len = 0;
             unsigned long long du = 0;
-            if (gi < i1) {
+            if (lane < (int)G && gi < i1) {
                 const uint64_t x = items[gi];
                 const int64_t u = (int64_t)(x >> 32), j = (int64_t)(x & 0xffffffffu);
                 const int64_t a = heavy ? B.slend[u] : B.srp[u], b = heavy ? B.srp[u + 1] : B.slend[u];
@@ -591,13 +633,14 @@ __global__ __launch_bounds__(kSB) void k_split_apply(SplitBufs B, const uint64_t
     uint64_t tot = 0;
     for (int r = 0; r < nranks; r++) tot += counts[2 * r];
     __shared__ Tile T;
-    for (uint64_t t0 = (uint64_t)blockIdx.x * kTile; t0 < tot; t0 += (uint64_t)gridDim.x * kTile) {
+    const uint32_t per = tile_per(tot), tile = per * kSB;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * tile; t0 < tot; t0 += (uint64_t)gridDim.x * tile) {
         tile_begin(T);
         Push P[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             uint64_t i = t0 + (uint64_t)k * kSB + threadIdx.x;
-            const bool valid = i < tot;
+            const bool valid = k < (int)per && i < tot;
             int64_t v = 0;
             unsigned long long d = kInf;
             if (valid) {
@@ -745,7 +788,7 @@ struct gx_sssp_split {
     DBuf<int32_t> sci, oci;
     DBuf<double> sw, ow;
     DBuf<unsigned long long> dist, lrel;
-    DBuf<int32_t> sstamp, hdone, hmark, qstamp, bstamp, ostamp, istamp, sverts, ring, ovf0, ovf1, cand, imp;
+    DBuf<int32_t> sstamp, hmark, qstamp, bstamp, ostamp, istamp, sverts, ring, ovf0, ovf1, cand, cand_big, imp;
     DBuf<uint64_t> fitems0, fitems1, sitems, own_pairs, own_count;
     DBuf<SplitState> st;
     int32_t *h_done = nullptr;
@@ -765,7 +808,6 @@ struct gx_sssp_split {
         B.dist = dist.p;
         B.lrel = lrel.p;
         B.sstamp = sstamp.p;
-        B.hdone = hdone.p;
         B.hmark = hmark.p;
         B.qstamp = qstamp.p;
         B.bstamp = bstamp.p;
@@ -779,6 +821,7 @@ struct gx_sssp_split {
         B.ovf[0] = ovf0.p;
         B.ovf[1] = ovf1.p;
         B.cand = cand.p;
+        B.cand_big = cand_big.p;
         B.imp = imp.p;
         B.n = n;
         B.v0 = v0;
@@ -923,12 +966,13 @@ static int split_build(gx_sssp_split *p, gx_graph *g) {
     const int64_t n1 = std::max<int64_t>(n, 1), own1 = std::max<int64_t>(own, 1);
     GX_TRY(p->dist.alloc(n1));
     GX_TRY(p->lrel.alloc(n1));
-    for (DBuf<int32_t> *b : {&p->sstamp, &p->hdone, &p->hmark, &p->qstamp, &p->bstamp, &p->ostamp, &p->sverts,
+    for (DBuf<int32_t> *b : {&p->sstamp, &p->hmark, &p->qstamp, &p->bstamp, &p->ostamp, &p->sverts,
                              &p->ovf0, &p->ovf1})
         GX_TRY(b->alloc(n1));
     GX_TRY(p->ring.alloc((uint64_t)n1 * kW));
     GX_TRY(p->istamp.alloc(own1));
     GX_TRY(p->cand.alloc(own1));
+    GX_TRY(p->cand_big.alloc(own1));
     GX_TRY(p->imp.alloc(own1));
     GX_TRY(p->fitems0.alloc(icap));
     GX_TRY(p->fitems1.alloc(icap));
