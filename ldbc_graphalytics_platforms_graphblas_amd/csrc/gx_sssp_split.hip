@@ -17,9 +17,9 @@
 //          <= n/16 vertices), SPLIT (the overflow into a new ring window) or done;
 //   prep   ADVANCE: the opened slots' pending vertices -> this round's frontier; SPLIT: the
 //          overflow -> ring / new overflow; HEAVY / PULL: the batch marked (PULL: its minimum);
-//   cand   PULL: the owned vertices a batch neighbour could still improve;
-//   relax  one wave per (vertex, 256-edge chunk) item of this rank's slice, or per PULL
-//          candidate; a target whose distance drops is claimed once per round;
+//   relax  up to 64 (vertex, 256-edge chunk) items of this rank's slice per wave; PULL: the
+//          owned vertices a batch neighbour could still improve, a thread each (a wave for
+//          rows past 32 heavy in-edges); a target whose distance drops is claimed once;
 //   pairs  (vertex, distance bits) of the improved owned vertices + {count, done};
 //   -- the caller all-gathers the pairs of every rank (gx_sssp_split_run: one rank, none) --
 //   apply  every rank's pairs: dist = min, then the vertex joins the next frontier when its
@@ -44,6 +44,7 @@ constexpr int kSB = 256;        // threads per block
 constexpr int kSChunk = 256;    // edges per relax item
 constexpr int kW = 32;          // bucket ring slots
 constexpr int kSmallDeg = 32;   // PULL: candidates up to this many heavy in-edges take a thread
+constexpr int kBigCap = 1024;   // PULL: larger candidates listed per workgroup for its waves
 constexpr unsigned long long kInf = 0x7FF0000000000000ull;   // +inf bits
 
 enum : int32_t { kNone = 0, kLight = 1, kHeavy = 2, kAdvance = 3, kPull = 4, kSplit = 5 };
@@ -69,7 +70,6 @@ struct SplitState {
     uint32_t sb0, sb1;
     uint32_t ring_cnt[kW];
     uint32_t ovf_cnt[2];
-    uint32_t ncand, ncand_big;    // PULL candidates with <= kSmallDeg heavy in-edges / more (rank-local)
     uint32_t nimp;                // improved owned vertices this round (rank-local)
     uint32_t pull_min;            // settled batch size from which the heavy phase is pulled (0: never)
     uint32_t fuse;                // ADVANCE opens further slots while the vertices stay <= fuse
@@ -78,9 +78,21 @@ struct SplitState {
     int8_t modelog[256];          // mode of rounds 1..256 (GX_SPLIT_VERBOSE)
 };
 
+// Per-vertex records, one 16-B line each: the slice row (light entries [start, start + nl),
+// heavy [start + nl, start + nl + nh)), and the vertex's stamps.
+struct alignas(16) VRec {
+    int64_t start;
+    uint32_t nl, nh;
+};
+struct alignas(16) SRec {
+    int32_t sstamp;   // epoch v joined the settled set
+    int32_t hmark;    // round of the HEAVY / PULL phase that relaxed v's heavy edges (0: pending)
+    int32_t bstamp;   // bucket v was last put into a ring slot for (low 32 bits + 1)
+    int32_t ostamp;   // overflow tag v was last put on the overflow with
+};
+
 struct SplitBufs {
-    const int64_t *srp;           // slice rows: [srp[u], slend[u]) light, [slend[u], srp[u+1]) heavy
-    const int64_t *slend;
+    const VRec *vrec;
     const int32_t *sci;           // owned target - v0
     const double *sw;
     const int64_t *orp;           // owned rows' heavy in-edges (PULL; undirected graphs)
@@ -88,18 +100,14 @@ struct SplitBufs {
     const double *ow;
     unsigned long long *dist;     // replicated distances (fp64 bits)
     unsigned long long *lrel;     // distance v's light edges were queued for relaxing with
-    int32_t *sstamp;              // epoch v joined the settled set
-    int32_t *hmark;               // round of the HEAVY / PULL phase that relaxed v's heavy edges (0: pending)
+    SRec *srec;
     int32_t *qstamp;              // ADVANCE: round v was taken from the ring
-    int32_t *bstamp;              // bucket v was last put into a ring slot for (low 32 bits + 1)
-    int32_t *ostamp;              // overflow tag v was last put on the overflow with
     int32_t *istamp;              // round an owned vertex was last claimed as improved
     uint64_t *fitems[2];          // (u << 32 | chunk)
     uint64_t *sitems;             // heavy items of the settled vertices
     int32_t *sverts;              // settled vertices of the epoch (replicated set)
     int32_t *ring;                // kW slots of n vertices
     int32_t *ovf[2];
-    int32_t *cand, *cand_big;     // PULL candidates (owned vertices - v0): thread / wave each
     int32_t *imp;                 // improved owned vertices (global ids)
     int64_t n, v0, v1;
     double delta, inv_delta;
@@ -161,16 +169,19 @@ __device__ __forceinline__ void tile_stage(const SplitBufs &B, Tile &T, Push &P,
     P.isv = 0;
     P.q = -1;
     P.nl = P.nh = 0;
+    if (!take && !far) return;
+    SRec r = B.srec[v];
     if (take) {
         B.lrel[v] = d;
-        P.nl = nchunks(B.slend[v] - B.srp[v]);
+        const VRec vr = B.vrec[v];
+        P.nl = nchunks(vr.nl);
         atomicAdd(&T.cnt[kQFv], 1u);
         P.offi = atomicAdd(&T.cnt[kQFi], P.nl);
-        if (B.sstamp[v] != epoch || B.hmark[v] >= st->epoch_round) {
-            B.sstamp[v] = epoch;
-            B.hmark[v] = 0;
+        if (r.sstamp != epoch || r.hmark >= st->epoch_round) {
+            B.srec[v].sstamp = epoch;
+            B.srec[v].hmark = 0;
             P.isv = 1;
-            P.nh = nchunks(B.srp[v + 1] - B.slend[v]);
+            P.nh = nchunks(vr.nh);
             P.offsv = atomicAdd(&T.cnt[kQSv], 1u);
             P.offs = atomicAdd(&T.cnt[kQSi], P.nh);
         }
@@ -178,16 +189,16 @@ __device__ __forceinline__ void tile_stage(const SplitBufs &B, Tile &T, Push &P,
     if (far) {
         if (b < st->win_base + kW) {
             const int32_t btag = (int32_t)(uint32_t)b + 1;
-            if (B.bstamp[v] != btag) {
-                B.bstamp[v] = btag;
+            if (r.bstamp != btag) {
+                B.srec[v].bstamp = btag;
                 P.q = (int8_t)(kQRing + (int)(b % kW));
                 P.offr = atomicAdd(&T.cnt[P.q], 1u);
             }
         } else {
             // the bound counts every overflow vertex, also one already listed whose bucket dropped
             atomicMin(&T.ominb, (unsigned long long)b);
-            if (B.ostamp[v] != st->ostamp_tag) {
-                B.ostamp[v] = st->ostamp_tag;
+            if (r.ostamp != st->ostamp_tag) {
+                B.srec[v].ostamp = st->ostamp_tag;
                 P.q = kQOvf;
                 P.offr = atomicAdd(&T.cnt[kQOvf], 1u);
             }
@@ -230,11 +241,8 @@ __global__ void k_split_start(SplitBufs B, int64_t src) {
     for (int64_t v = i; v < B.n; v += (int64_t)gridDim.x * kSB) {
         B.dist[v] = v == src ? 0ull : kInf;
         B.lrel[v] = kInf;
-        B.sstamp[v] = 0;
-        B.hmark[v] = 0;
+        B.srec[v] = SRec{0, 0, 0, 0};
         B.qstamp[v] = 0;
-        B.bstamp[v] = 0;
-        B.ostamp[v] = 0;
     }
     for (int64_t v = i; v < B.v1 - B.v0; v += (int64_t)gridDim.x * kSB) B.istamp[v] = 0;
 }
@@ -265,7 +273,6 @@ __device__ void k_split_plan_body(SplitState *st);
 
 __global__ void k_split_plan(SplitState *st) {
     st->nimp = 0;
-    st->ncand = st->ncand_big = 0;
     if (st->done) {
         st->mode = kNone;
         return;
@@ -418,7 +425,7 @@ __global__ __launch_bounds__(kSB) void k_split_prep(SplitBufs B) {
         unsigned long long m = ~0ull;
         for (uint32_t i = st->sb0 + blockIdx.x * kSB + threadIdx.x; i < st->sb1; i += gridDim.x * kSB) {
             const int32_t u = B.sverts[i];
-            B.hmark[u] = round;
+            B.srec[u].hmark = round;
             if (mode == kPull) m = min(m, B.dist[u]);
         }
         if (mode == kPull) {
@@ -428,47 +435,11 @@ __global__ __launch_bounds__(kSB) void k_split_prep(SplitBufs B) {
     }
 }
 
-// PULL: the owned vertices a settled neighbour could still improve (distance above
-// fl(smin + delta): a heavy edge adds at least delta).
-__global__ __launch_bounds__(kSB) void k_split_cand(SplitBufs B) {
-    SplitState *st = B.st;
-    if (st->mode != kPull) return;
-    const unsigned long long lim =
-        (unsigned long long)__double_as_longlong(__longlong_as_double((long long)st->smin) + B.delta);
-    const int64_t own = B.v1 - B.v0;
-    __shared__ uint32_t lcnt[2], lbase[2];
-    const uint32_t per = tile_per((uint64_t)own), tile = per * kSB;
-    for (int64_t t0 = (int64_t)blockIdx.x * tile; t0 < own; t0 += (int64_t)gridDim.x * tile) {
-        if (threadIdx.x < 2) lcnt[threadIdx.x] = 0;
-        __syncthreads();
-        uint32_t off[kPer];
-        int8_t c[kPer];   // -1 none, 0 small, 1 big
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const int64_t i = t0 + k * kSB + threadIdx.x;
-            c[k] = -1;
-            if (k < (int)per && i < own && B.dist[B.v0 + i] > lim) {
-                const int64_t deg = B.orp[i + 1] - B.orp[i];
-                if (deg > 0) c[k] = deg > kSmallDeg ? 1 : 0;
-            }
-            off[k] = c[k] >= 0 ? atomicAdd(&lcnt[c[k]], 1u) : 0u;
-        }
-        __syncthreads();
-        if (threadIdx.x < 2)
-            lbase[threadIdx.x] = lcnt[threadIdx.x] ? atomicAdd(threadIdx.x ? &st->ncand_big : &st->ncand, lcnt[threadIdx.x]) : 0u;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kPer; k++)
-            if (c[k] >= 0) (c[k] ? B.cand_big : B.cand)[lbase[c[k]] + off[k]] = (int32_t)(t0 + k * kSB + threadIdx.x);
-        __syncthreads();
-    }
-}
-
 // LIGHT / ADVANCE: the frontier's light edges; HEAVY: the settled batch's heavy edges.  A wave
 // takes up to 64 items (vertex, 256-edge chunk) and walks their concatenated edges 64 at a time,
 // each lane finding its item by a shuffle binary search over the items' edge prefix -- a
-// frontier of low-degree vertices fills the lanes.  PULL: one wave per candidate, its heavy
-// in-edges from the settled batch, minimum in registers, written by the wave.  Improved owned
+// frontier of low-degree vertices fills the lanes.  PULL: a thread (a wave past kSmallDeg
+// in-edges) per candidate, its heavy in-edges from the settled batch, minimum in registers.  Improved owned
 // vertices are claimed once per round, staged in LDS and appended once per workgroup.
 constexpr int kStageCap = 2048;
 
@@ -495,37 +466,59 @@ __global__ __launch_bounds__(kSB) void k_split_relax(SplitBufs B) {
         }
     };
     if (mode == kPull) {
-        // low-degree candidates: a thread each (the loop trip count is uniform per wave)
-        const uint32_t ns = st->ncand;
-        const uint32_t nth = gridDim.x * kSB, span = (ns + kWave - 1) / kWave * kWave;
-        for (uint32_t it = blockIdx.x * kSB + threadIdx.x; it < span; it += nth) {
-            bool won = false;
-            int64_t i = 0;
-            if (it < ns) {
-                i = B.cand[it];
-                unsigned long long best = kInf;
-                for (int64_t e = B.orp[i]; e < B.orp[i + 1]; e++) {
-                    const int32_t u = B.oci[e];
-                    if (B.hmark[u] == round) {
-                        const unsigned long long nd = (unsigned long long)__double_as_longlong(
-                            __longlong_as_double((long long)B.dist[u]) + B.ow[e]);
-                        best = min(best, nd);
-                    }
+        // candidates found here: an owned vertex above fl(smin + delta) with heavy in-edges;
+        // up to kSmallDeg of them a thread pulls at once, larger rows go to the workgroup's
+        // LDS list for its waves (the loop trip count is uniform per wave)
+        __shared__ int32_t bigs[kBigCap];
+        __shared__ uint32_t nbig;
+        if (threadIdx.x == 0) nbig = 0;
+        __syncthreads();
+        const unsigned long long lim =
+            (unsigned long long)__double_as_longlong(__longlong_as_double((long long)st->smin) + B.delta);
+        auto pull_row = [&](int64_t i) {
+            unsigned long long best = kInf;
+            for (int64_t e = B.orp[i]; e < B.orp[i + 1]; e++) {
+                const int32_t u = B.oci[e];
+                if (B.srec[u].hmark == round) {
+                    const unsigned long long nd =
+                        (unsigned long long)__double_as_longlong(__longlong_as_double((long long)B.dist[u]) + B.ow[e]);
+                    best = min(best, nd);
                 }
-                if (best < B.dist[B.v0 + i]) {
-                    B.dist[B.v0 + i] = best;   // this thread alone writes the vertex this round
-                    won = true;
+            }
+            return best;
+        };
+        const int64_t own = B.v1 - B.v0;
+        const int64_t nth = (int64_t)gridDim.x * kSB, span = (own + kWave - 1) / kWave * kWave;
+        for (int64_t i = (int64_t)blockIdx.x * kSB + threadIdx.x; i < span; i += nth) {
+            bool won = false;
+            if (i < own) {
+                const unsigned long long d = B.dist[B.v0 + i];
+                const int64_t deg = d > lim ? B.orp[i + 1] - B.orp[i] : 0;
+                bool listed = false;
+                if (deg > kSmallDeg) {
+                    const uint32_t at = atomicAdd(&nbig, 1u);
+                    listed = at < (uint32_t)kBigCap;
+                    if (listed) bigs[at] = (int32_t)i;
+                }
+                if (deg > 0 && !listed) {
+                    // (a full list: the thread pulls the row itself)
+                    const unsigned long long best = pull_row(i);
+                    if (best < d) {
+                        B.dist[B.v0 + i] = best;   // this thread alone writes the vertex this round
+                        won = true;
+                    }
                 }
             }
             claim(won, (int32_t)(B.v0 + i));
         }
-        const uint32_t nc = st->ncand_big;
-        for (uint32_t it = wid; it < nc; it += nw) {
-            const int64_t i = B.cand_big[it];
+        __syncthreads();
+        const uint32_t nb = min(nbig, (uint32_t)kBigCap);
+        for (uint32_t it = threadIdx.x / kWave; it < nb; it += kSB / kWave) {
+            const int64_t i = bigs[it];
             unsigned long long best = kInf;
             for (int64_t e = B.orp[i] + lane; e < B.orp[i + 1]; e += kWave) {
                 const int32_t u = B.oci[e];
-                if (B.hmark[u] == round) {
+                if (B.srec[u].hmark == round) {
                     const unsigned long long nd =
                         (unsigned long long)__double_as_longlong(__longlong_as_double((long long)B.dist[u]) + B.ow[e]);
                     best = min(best, nd);
@@ -535,7 +528,7 @@ __global__ __launch_bounds__(kSB) void k_split_relax(SplitBufs B) {
             bool won = false;
             if (lane == 0 && best < B.dist[B.v0 + i]) {
                 B.dist[B.v0 + i] = best;   // this wave alone writes the vertex this round
-                won = true;                // one candidate per wave: no claim needed
+                won = true;
             }
             claim(won, (int32_t)(B.v0 + i));
         }
@@ -554,7 +547,8 @@ __global__ __launch_bounds__(kSB) void k_split_relax(SplitBufs B) {
             if (lane < (int)G && gi < i1) {
                 const uint64_t x = items[gi];
                 const int64_t u = (int64_t)(x >> 32), j = (int64_t)(x & 0xffffffffu);
-                const int64_t a = heavy ? B.slend[u] : B.srp[u], b = heavy ? B.srp[u + 1] : B.slend[u];
+                const VRec vr = B.vrec[u];
+                const int64_t a = heavy ? vr.start + vr.nl : vr.start, b = a + (heavy ? vr.nh : vr.nl);
                 e0 = a + j * kSChunk;
                 len = max<int64_t>(0, min(b, e0 + kSChunk) - e0);
                 du = B.dist[u];
@@ -631,7 +625,9 @@ __global__ __launch_bounds__(kSB) void k_split_apply(SplitBufs B, const uint64_t
     const int64_t cur = st->cur;
     const int32_t epoch = st->epoch, nx = st->fc ^ 1;
     uint64_t tot = 0;
-    for (int r = 0; r < nranks; r++) tot += counts[2 * r];
+    if (!pairs) tot = st->nimp;
+    else
+        for (int r = 0; r < nranks; r++) tot += counts[2 * r];
     __shared__ Tile T;
     const uint32_t per = tile_per(tot), tile = per * kSB;
     for (uint64_t t0 = (uint64_t)blockIdx.x * tile; t0 < tot; t0 += (uint64_t)gridDim.x * tile) {
@@ -643,7 +639,10 @@ __global__ __launch_bounds__(kSB) void k_split_apply(SplitBufs B, const uint64_t
             const bool valid = k < (int)per && i < tot;
             int64_t v = 0;
             unsigned long long d = kInf;
-            if (valid) {
+            if (valid && !pairs) {   // this rank's own improved list (a single rank)
+                v = B.imp[i];
+                d = B.dist[v];
+            } else if (valid) {
                 int r = 0;
                 while (i >= counts[2 * r]) {
                     i -= counts[2 * r];
@@ -727,6 +726,12 @@ __global__ __launch_bounds__(kSB) void k_slice_scatter(const int64_t *__restrict
     }
 }
 
+__global__ __launch_bounds__(kSB) void k_slice_vrec(const int64_t *__restrict__ srp, const int64_t *__restrict__ slend,
+                                                    int64_t n, VRec *vrec) {
+    for (int64_t u = (int64_t)blockIdx.x * kSB + threadIdx.x; u < n; u += (int64_t)gridDim.x * kSB)
+        vrec[u] = VRec{srp[u], (uint32_t)(slend[u] - srp[u]), (uint32_t)(srp[u + 1] - slend[u])};
+}
+
 // PULL layout: the heavy entries (w >= delta) of the owned rows of A (an undirected graph's
 // in-edges), row order kept.  Wave per row.
 __global__ __launch_bounds__(kSB) void k_own_count(const int64_t *__restrict__ rp, const double *__restrict__ w,
@@ -781,14 +786,17 @@ struct gx_sssp_split {
     gx_graph *g = nullptr;        // the graph the slice is built on (a single rank: its hub-first copy)
     gx_graph *caller = nullptr;   // the graph gx_sssp_split_create was given
     bool hub_checked = false;     // gx_sssp_split_run looked for the hub-first copy
+    int rounds_hint = 0;          // rounds the last gx_sssp_split_run took
     int64_t n = 0, v0 = 0, v1 = 0, snnz = 0, onnz = 0;
     double delta = 1.0;
     uint32_t pull_min = 0, fuse = 0;
-    DBuf<int64_t> srp, slend, orp;
+    DBuf<VRec> vrec;
+    DBuf<SRec> srec;
+    DBuf<int64_t> orp;
     DBuf<int32_t> sci, oci;
     DBuf<double> sw, ow;
     DBuf<unsigned long long> dist, lrel;
-    DBuf<int32_t> sstamp, hmark, qstamp, bstamp, ostamp, istamp, sverts, ring, ovf0, ovf1, cand, cand_big, imp;
+    DBuf<int32_t> qstamp, istamp, sverts, ring, ovf0, ovf1, imp;
     DBuf<uint64_t> fitems0, fitems1, sitems, own_pairs, own_count;
     DBuf<SplitState> st;
     int32_t *h_done = nullptr;
@@ -798,8 +806,7 @@ struct gx_sssp_split {
     }
     SplitBufs bufs() {
         SplitBufs B;
-        B.srp = srp.p;
-        B.slend = slend.p;
+        B.vrec = vrec.p;
         B.sci = sci.p;
         B.sw = sw.p;
         B.orp = orp.p;
@@ -807,11 +814,8 @@ struct gx_sssp_split {
         B.ow = ow.p;
         B.dist = dist.p;
         B.lrel = lrel.p;
-        B.sstamp = sstamp.p;
-        B.hmark = hmark.p;
+        B.srec = srec.p;
         B.qstamp = qstamp.p;
-        B.bstamp = bstamp.p;
-        B.ostamp = ostamp.p;
         B.istamp = istamp.p;
         B.fitems[0] = fitems0.p;
         B.fitems[1] = fitems1.p;
@@ -820,8 +824,6 @@ struct gx_sssp_split {
         B.ring = ring.p;
         B.ovf[0] = ovf0.p;
         B.ovf[1] = ovf1.p;
-        B.cand = cand.p;
-        B.cand_big = cand_big.p;
         B.imp = imp.p;
         B.n = n;
         B.v0 = v0;
@@ -837,14 +839,14 @@ struct gx_sssp_split {
 // steps order with the tensors and collectives issued there
 static hipStream_t split_stream(gx_sssp_split *, void *stream) { return (hipStream_t)stream; }
 
-// plan -> prep -> cand -> relax -> pairs (this rank's improved owned vertices)
+// plan -> prep -> relax -> pairs (this rank's improved owned vertices; a single rank's device
+// loop skips the pairs: its apply reads the improved list)
 static int split_relax(gx_sssp_split *p, uint64_t *pairs, uint64_t *count, hipStream_t s) {
     const SplitBufs B = p->bufs();
     hipLaunchKernelGGL(k_split_plan, dim3(1), dim3(1), 0, s, B.st);
     hipLaunchKernelGGL(k_split_prep, dim3(p->grid), dim3(kSB), 0, s, B);
-    hipLaunchKernelGGL(k_split_cand, dim3(p->grid), dim3(kSB), 0, s, B);
     hipLaunchKernelGGL(k_split_relax, dim3(p->grid), dim3(kSB), 0, s, B);
-    hipLaunchKernelGGL(k_split_pairs, dim3(p->grid), dim3(kSB), 0, s, B, pairs, count);
+    if (pairs) hipLaunchKernelGGL(k_split_pairs, dim3(p->grid), dim3(kSB), 0, s, B, pairs, count);
     return check_launch("k_split_relax");
 }
 
@@ -914,10 +916,11 @@ static int split_build(gx_sssp_split *p, gx_graph *g) {
                                           : (uint32_t)std::max<int64_t>(1024, n / 16);
     const unsigned wg_all = grid_for((uint64_t)std::max<int64_t>(n, 1) * kWave, kSB, 16384);
     // slice: count, scan, scatter
-    GX_TRY(p->srp.alloc(n + 1));
-    GX_TRY(p->slend.alloc(std::max<int64_t>(n, 1)));
+    GX_TRY(p->vrec.alloc(std::max<int64_t>(n, 1)));
     {
-        DBuf<int64_t> lc, tc;
+        DBuf<int64_t> lc, tc, srp, slend;
+        GX_TRY(srp.alloc(n + 1));
+        GX_TRY(slend.alloc(std::max<int64_t>(n, 1)));
         GX_TRY(lc.alloc(std::max<int64_t>(n, 1)));
         GX_TRY(tc.alloc(n + 1));
         if (n) {
@@ -927,15 +930,17 @@ static int split_build(gx_sssp_split *p, gx_graph *g) {
         } else {
             GX_HIP_TRY(hipMemsetAsync(tc.p, 0, sizeof(int64_t), s));
         }
-        GX_TRY(scan_exclusive_i64(tc.p, p->srp.p, (size_t)(n + 1), s));
-        GX_HIP_TRY(hipMemcpyAsync(&p->snnz, p->srp.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        GX_TRY(scan_exclusive_i64(tc.p, srp.p, (size_t)(n + 1), s));
+        GX_HIP_TRY(hipMemcpyAsync(&p->snnz, srp.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         GX_HIP_TRY(hipStreamSynchronize(s));
         GX_TRY(p->sci.alloc(std::max<int64_t>(p->snnz, 1)));
         GX_TRY(p->sw.alloc(std::max<int64_t>(p->snnz, 1)));
         if (n) {
             hipLaunchKernelGGL(k_slice_scatter, dim3(wg_all), dim3(kSB), 0, s, g->A.rp.p, g->A.ci.p, g->A.w.p, n, p->v0,
-                               p->v1, delta, p->srp.p, lc.p, p->slend.p, p->sci.p, p->sw.p);
+                               p->v1, delta, srp.p, lc.p, slend.p, p->sci.p, p->sw.p);
             GX_TRY(check_launch("k_slice_scatter"));
+            hipLaunchKernelGGL(k_slice_vrec, dim3(grid_for(n, kSB, 8192)), dim3(kSB), 0, s, srp.p, slend.p, n, p->vrec.p);
+            GX_TRY(check_launch("k_slice_vrec"));
         }
         GX_HIP_TRY(hipStreamSynchronize(s));   // lc / tc die here
     }
@@ -966,13 +971,10 @@ static int split_build(gx_sssp_split *p, gx_graph *g) {
     const int64_t n1 = std::max<int64_t>(n, 1), own1 = std::max<int64_t>(own, 1);
     GX_TRY(p->dist.alloc(n1));
     GX_TRY(p->lrel.alloc(n1));
-    for (DBuf<int32_t> *b : {&p->sstamp, &p->hmark, &p->qstamp, &p->bstamp, &p->ostamp, &p->sverts,
-                             &p->ovf0, &p->ovf1})
-        GX_TRY(b->alloc(n1));
+    for (DBuf<int32_t> *b : {&p->qstamp, &p->sverts, &p->ovf0, &p->ovf1}) GX_TRY(b->alloc(n1));
+    GX_TRY(p->srec.alloc(n1));
     GX_TRY(p->ring.alloc((uint64_t)n1 * kW));
     GX_TRY(p->istamp.alloc(own1));
-    GX_TRY(p->cand.alloc(own1));
-    GX_TRY(p->cand_big.alloc(own1));
     GX_TRY(p->imp.alloc(own1));
     GX_TRY(p->fitems0.alloc(icap));
     GX_TRY(p->fitems1.alloc(icap));
@@ -1055,16 +1057,24 @@ extern "C" int gx_sssp_split_run(gx_sssp_split *p, uint64_t src, double *dist_ho
     }
     GX_TRY(device_begin(ctx));
     GX_TRY(gx_sssp_split_start(p, src, s));
-    constexpr int kBatch = 16;
+    // the first batch queues as many rounds as the last run took (+2), then batches of 8; a
+    // round past the end is four launches that return at once
+    int batch = p->rounds_hint > 0 ? std::min(p->rounds_hint + 2, 512) : 16;
     for (int64_t guard = 0;; guard++) {
-        for (int k = 0; k < kBatch; k++) {
-            GX_TRY(split_relax(p, p->own_pairs.p, p->own_count.p, s));
-            GX_TRY(split_apply(p, p->own_pairs.p, p->own_count.p, 1, (uint64_t)std::max<int64_t>(p->n, 1), s));
+        for (int k = 0; k < batch; k++) {
+            GX_TRY(split_relax(p, nullptr, nullptr, s));
+            GX_TRY(split_apply(p, nullptr, nullptr, 1, 0, s));
         }
-        GX_HIP_TRY(hipMemcpyAsync(p->h_done, &p->st.p->done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipMemcpyAsync(p->h_done, &p->st.p->done, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
         GX_HIP_TRY(hipStreamSynchronize(s));
-        if (*p->h_done) break;
+        if (p->h_done[0]) break;
+        batch = 8;
         if (guard > 4 * (p->n + 16)) return fail(GX_DEVICE_ERROR, "gx_sssp_split_run: no fixed point");
+    }
+    {
+        int32_t rounds = 0;
+        GX_HIP_TRY(hipMemcpy(&rounds, &p->st.p->round, sizeof(int32_t), hipMemcpyDeviceToHost));
+        p->rounds_hint = rounds;
     }
     GX_TRY(device_end(ctx));
     if (std::getenv("GX_SPLIT_VERBOSE")) {
