@@ -562,35 +562,55 @@ __global__ __launch_bounds__(kSB) void k_split_relax(SplitBufs B) {
             }
             const uint32_t total = __shfl(x, kWave - 1, kWave);
             const uint32_t pre = x - (uint32_t)len;
-            for (uint32_t k0 = 0; k0 < total; k0 += kWave) {
-                const uint32_t k = k0 + lane;
-                // the item holding edge k: the last lane whose prefix is <= k (lanes past the
-                // group have len 0 and prefix = total, never <= k < total)
-                int lo = 0;
+            // four edges per lane and pass, each step issued for all four before any result is
+            // used (the edge, target and claim loads of one edge are a dependent chain)
+            constexpr int kQ = 4;
+            for (uint32_t k0 = 0; k0 < total; k0 += kQ * kWave) {
+                int32_t t[kQ];
+                unsigned long long nd[kQ];
+                bool live[kQ], won[kQ];
 #pragma unroll
-                for (int step = 32; step > 0; step >>= 1) {
-                    const int c = lo + step;
-                    const uint32_t pc = __shfl(pre, c < kWave ? c : kWave - 1, kWave);
-                    if (c < kWave && pc <= k) lo = c;
-                }
-                const int64_t eo = __shfl(e0, lo, kWave);
-                const uint32_t po = __shfl(pre, lo, kWave);
-                const unsigned long long dbits = __shfl(du, lo, kWave);
-                bool won = false;
-                int32_t t = 0;
-                if (k < total) {
-                    const int64_t e = eo + (int64_t)(k - po);
-                    t = B.sci[e];
-                    const unsigned long long nd =
-                        (unsigned long long)__double_as_longlong(__longlong_as_double((long long)dbits) + B.sw[e]);
-                    unsigned long long *dv = &B.dist[B.v0 + t];
-                    if (nd < __hip_atomic_load(dv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        // no return: the load decided that the vertex improves this round
-                        __hip_atomic_fetch_min(dv, nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        won = B.istamp[t] != round && atomicExch(&B.istamp[t], round) != round;
+                for (int q = 0; q < kQ; q++) {
+                    const uint32_t k = k0 + q * kWave + lane;
+                    // the item holding edge k: the last lane whose prefix is <= k (lanes past
+                    // the group have len 0 and prefix = total, never <= k < total)
+                    int lo = 0;
+#pragma unroll
+                    for (int step = 32; step > 0; step >>= 1) {
+                        const int c = lo + step;
+                        const uint32_t pc = __shfl(pre, c < kWave ? c : kWave - 1, kWave);
+                        if (c < kWave && pc <= k) lo = c;
+                    }
+                    const int64_t eo = __shfl(e0, lo, kWave);
+                    const uint32_t po = __shfl(pre, lo, kWave);
+                    const unsigned long long dbits = __shfl(du, lo, kWave);
+                    live[q] = k < total;
+                    t[q] = 0;
+                    nd[q] = kInf;
+                    if (live[q]) {
+                        const int64_t e = eo + (int64_t)(k - po);
+                        t[q] = B.sci[e];
+                        nd[q] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)dbits) + B.sw[e]);
                     }
                 }
-                claim(won, (int32_t)(B.v0 + t));
+                unsigned long long cur[kQ];
+#pragma unroll
+                for (int q = 0; q < kQ; q++)
+                    cur[q] = live[q] ? __hip_atomic_load(&B.dist[B.v0 + t[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0ull;
+                int32_t stamp[kQ];
+#pragma unroll
+                for (int q = 0; q < kQ; q++) {
+                    won[q] = live[q] && nd[q] < cur[q];
+                    // no return: the load decided that the vertex improves this round
+                    if (won[q]) __hip_atomic_fetch_min(&B.dist[B.v0 + t[q]], nd[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stamp[q] = won[q] ? B.istamp[t[q]] : round;
+                }
+#pragma unroll
+                for (int q = 0; q < kQ; q++) {
+                    won[q] = won[q] && stamp[q] != round && atomicExch(&B.istamp[t[q]], round) != round;
+                    claim(won[q], (int32_t)(B.v0 + t[q]));
+                }
             }
         }
     }
