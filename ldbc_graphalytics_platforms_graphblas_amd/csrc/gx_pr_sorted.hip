@@ -450,29 +450,33 @@ struct KeySrc {
     int colbits;
 };
 
+// One wave per 64-entry slab of the plan's rows, lane = entry (coalesced key / row writes and
+// row-contiguous column reads; the row by the slab shuffle search, gx_device.h slab_row_of).
 template <typename K>
-__global__ __launch_bounds__(256) void k_sorted_keys(KeySrc k, int64_t nnz, K *__restrict__ keys, uint16_t *__restrict__ vals) {
-    constexpr int kPer = 16;
-    const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPer;
-    if (e0 >= nnz) return;
-    const int64_t e1 = min(e0 + kPer, nnz);
-    int64_t i = row_of_edge(k.rp, k.rows, e0);
-    int lo = 0, hi = k.nseg;   // segment of row i: seg_row[lo] <= i < seg_row[lo + 1]
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (k.seg_row[mid] <= i) lo = mid;
-        else hi = mid;
-    }
-    for (int64_t e = e0; e < e1; e++) {
-        while (k.rp[i + 1] <= e) {
-            i++;
-            while (lo + 1 < k.nseg && k.seg_row[lo + 1] <= i) lo++;
+__global__ __launch_bounds__(256) void k_sorted_keys(KeySrc k, int64_t nnz, const int64_t *__restrict__ srow,
+                                                     int64_t nslabs, K *__restrict__ keys, uint16_t *__restrict__ vals) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
+    for (int64_t sl = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; sl < nslabs; sl += nw) {
+        const int64_t e = sl * kWave + lane;
+        const bool valid = e < nnz;
+        const int64_t i = slab_row_of(k.rp, srow, k.rows, sl, valid ? e : nnz - 1, lane);
+        // the segment of the slab's first row (uniform search), then forward per lane
+        const int64_t r0 = srow[sl];
+        int lo = 0, hi = k.nseg;   // seg_row[lo] <= r0 < seg_row[lo + 1]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (k.seg_row[mid] <= r0) lo = mid;
+            else hi = mid;
         }
-        const int64_t v = k.order ? k.order[i] : i;
-        const int32_t c0 = k.sci[k.srp[v] + (e - k.rp[i])];
-        const uint32_t c = (uint32_t)(k.perm ? k.perm[c0] : c0);
-        keys[e] = ((K)lo << k.colbits) | (K)c;
-        vals[e] = (uint16_t)(i - k.seg_row[lo]);
+        while (lo + 1 < k.nseg && k.seg_row[lo + 1] <= i) lo++;
+        if (valid) {
+            const int64_t v = k.order ? k.order[i] : i;
+            const int32_t c0 = k.sci[k.srp[v] + (e - k.rp[i])];
+            const uint32_t c = (uint32_t)(k.perm ? k.perm[c0] : c0);
+            keys[e] = ((K)lo << k.colbits) | (K)c;
+            vals[e] = (uint16_t)(i - k.seg_row[lo]);
+        }
     }
 }
 
@@ -702,12 +706,15 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
             const int32_t r0 = o.first;
             const bool blk = o.second >= 0;
             const int32_t r1 = blk ? sortb[o.second].row_end : r0 + 1;
+            if (h_rp[r0] == h_rp[r1]) continue;   // no entries: no key names it (fewer segment bits)
             seg_row.push_back(r0);
             segd.push_back({h_rp[r0], h_rp[r1], blk ? sortb[o.second].seg : -1, 0});
         }
         seg_row.push_back((int32_t)rows);
+        // column bits from the columns that occur: one rank's plan holds vertex ids < n (the
+        // chunk's padding slots are never a column), a partition's the chunk layout
         int colbits = 1;
-        const uint64_t ncols = p->chunk * (uint64_t)p->nranks;
+        const uint64_t ncols = p->nranks == 1 ? std::max<uint64_t>(p->n_global, 1) : p->chunk * (uint64_t)p->nranks;
         while ((1ull << colbits) < ncols) colbits++;
         int segbits = 1;
         while ((1ull << segbits) < segd.size()) segbits++;
@@ -719,7 +726,11 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         GX_HIP_TRY(hipMemcpyAsync(d_segd.p, segd.data(), segd.size() * sizeof(SegDesc), hipMemcpyHostToDevice, s));
         const KeySrc ks{p->rp, rows, p->src_rp, p->src_ci, p->src_order, p->src_perm, d_seg_row.p,
                         (int32_t)segd.size(), colbits};
-        const unsigned kgrid = grid_for((nnz + 15) / 16, 256, 1u << 30);
+        const int64_t nslabs = (int64_t)((nnz + kWave - 1) / kWave);
+        DBuf<int64_t> srow;
+        GX_TRY(srow.alloc(nslabs + 1));
+        GX_TRY(slab_rows(p->rp, rows, nslabs, srow.p, s));
+        const unsigned kgrid = grid_for((uint64_t)nslabs * kWave, 256, 16384);
         const unsigned pgrid = grid_for(nnz, 256, 1u << 20);
         const uint32_t colmask = (uint32_t)((1ull << colbits) - 1);
         DBuf<uint16_t> v0, v1;
@@ -729,7 +740,8 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
             DBuf<uint32_t> k0, k1;
             GX_TRY(k0.alloc(nnz));
             GX_TRY(k1.alloc(nnz));
-            hipLaunchKernelGGL(k_sorted_keys<uint32_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, k0.p, v0.p);
+            hipLaunchKernelGGL(k_sorted_keys<uint32_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs, k0.p,
+                               v0.p);
             GX_TRY(check_launch("k_sorted_keys"));
             GX_TRY(sort_pairs_u32_u16(k0.p, k1.p, v0.p, v1.p, (size_t)nnz, segbits + colbits, s));
             hipLaunchKernelGGL(k_sorted_pack<uint32_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
@@ -738,7 +750,8 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
             DBuf<uint64_t> k0, k1;
             GX_TRY(k0.alloc(nnz));
             GX_TRY(k1.alloc(nnz));
-            hipLaunchKernelGGL(k_sorted_keys<uint64_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, k0.p, v0.p);
+            hipLaunchKernelGGL(k_sorted_keys<uint64_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs, k0.p,
+                               v0.p);
             GX_TRY(check_launch("k_sorted_keys"));
             GX_TRY(sort_pairs_u64_u16(k0.p, k1.p, v0.p, v1.p, (size_t)nnz, segbits + colbits, s));
             hipLaunchKernelGGL(k_sorted_pack<uint64_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
