@@ -284,6 +284,7 @@ def run_algorithm(args):
         ref = {"bfs": lambda: O.bfs(csr, src), "wcc": lambda: O.wcc(csr), "sssp": lambda: O.sssp(csr, src)}.get(
             alg, lambda: base)()
         parity = "bit-exact" if np.array_equal(out, ref) else f"MISMATCH ({int((out != ref).sum())} vertices)"
+    traffic, traffic_src = pmc_alg_traffic(alg, f"{alg.upper()} {gname}")
     line = {
         "metric": METRIC, "value": work / t_dev, "unit": unit, "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": t_dev * 1e3, "higher_is_better": True, "scaling": "weak",
@@ -294,7 +295,8 @@ def run_algorithm(args):
                    "parallelism": "single", "device": dev_name, "cus": cus},
         "roofline": {"kernel": f"{alg} (whole device time)", "dominant_kernel": " + ".join(DOMINANT[alg]), "bound": "hbm",
                      "achieved": nbytes / t_dev / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": nbytes / t_dev / 1e9 / HBM_PEAK_GBS, "traffic": None, "bytes_per_run": nbytes,
+                     "frac": nbytes / t_dev / 1e9 / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "bytes_per_run": nbytes,
                      "dominant_kernel_ms_per_run": kms / max(1, args.steps), "dominant_launches": kl,
                      "kernels": per_kernel,
                      "survey_8d_bytes_per_run": ref_model_bytes,
@@ -307,6 +309,19 @@ def run_algorithm(args):
     print(json.dumps(line), flush=True)
     G.close()
     ctx.close()
+
+
+def pmc_alg_traffic(alg: str, workload: str):
+    """Per-run HBM bytes of an algorithm's per-run kernels from the committed rocprofv3 PMC
+    summary (tools/alg_pmc.sh + tools/alg_pmc_json.py), if it covers this workload."""
+    for p in sorted((ROOT / "profiles").glob("r*_pmc_algorithms.json"), reverse=True):
+        try:
+            a = json.loads(p.read_text())["algorithms"].get(alg)
+        except Exception:
+            continue
+        if a and a.get("workload") == workload:
+            return a.get("hbm_bytes_per_run"), p.name
+    return None, None
 
 
 def pmc_traffic(workload: str):
