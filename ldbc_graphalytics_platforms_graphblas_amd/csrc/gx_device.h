@@ -219,7 +219,11 @@ int sort_pairs_u32_u16(uint32_t *k_in, uint32_t *k_out, uint16_t *v_in, uint16_t
                        hipStream_t s);
 int sort_pairs_u64_u16(uint64_t *k_in, uint64_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
                        hipStream_t s);
+// stable descending sort of (key, value) pairs, all 32 key bits
+int sort_pairs_desc_u32_i32(uint32_t *k_in, uint32_t *k_out, int32_t *v_in, int32_t *v_out, size_t m, hipStream_t s);
 int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s);
+// grow-only device scratch of the current device, kept between calls (gx_runtime.hip)
+int plan_scratch(size_t bytes, void **p);
 int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,
                      int32_t *ci, hipStream_t s);
 

@@ -487,14 +487,19 @@ __global__ void k_gather_perm(const double *__restrict__ in, const int32_t *__re
 
 // Device hub-first order: keys (2^31 - 1 - outdeg) << 32 | v sort ascending into out-degree
 // descending, ties by id (the host hub_order's order, which the adaptive kernel's plan keeps).
-__global__ void k_hub_keys(const int32_t *__restrict__ outdeg, int64_t n, uint64_t *__restrict__ keys) {
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
-        keys[v] = ((uint64_t)(0x7fffffffu - (uint32_t)outdeg[v]) << 32) | (uint64_t)v;
+// (out-degree, vertex) pairs; a stable descending sort of the degrees gives the hub-first order
+// (degree descending, ties by id)
+__global__ void k_hub_keys(const int32_t *__restrict__ outdeg, int64_t n, uint32_t *__restrict__ deg,
+                           int32_t *__restrict__ ids) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        deg[v] = (uint32_t)outdeg[v];
+        ids[v] = (int32_t)v;
+    }
 }
 
 // order[i] = v, perm[v] = i, the hub-first row's out-degree and pull length (plen[n] = 0, so an
 // exclusive scan of n + 1 values gives the relabelled row pointers)
-__global__ void k_hub_apply(const uint64_t *__restrict__ keys, int64_t n, const int32_t *__restrict__ outdeg,
+__global__ void k_hub_apply(const int32_t *__restrict__ sorted_ids, int64_t n, const int32_t *__restrict__ outdeg,
                             const int64_t *__restrict__ prp, int32_t *__restrict__ order, int32_t *__restrict__ perm,
                             int32_t *__restrict__ nout, int64_t *__restrict__ plen) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -502,7 +507,7 @@ __global__ void k_hub_apply(const uint64_t *__restrict__ keys, int64_t n, const 
             plen[n] = 0;
             continue;
         }
-        const int32_t v = (int32_t)(uint32_t)keys[i];
+        const int32_t v = sorted_ids[i];
         order[i] = v;
         perm[v] = (int32_t)i;
         nout[i] = outdeg[v];
@@ -636,19 +641,23 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     GX_TRY(p->rank_out.alloc(n));
     GX_TRY(p->result.alloc(n));
     {
-        DBuf<uint64_t> k0, k1;
+        DBuf<uint32_t> d0, d1;
+        DBuf<int32_t> i0, i1;
         DBuf<int64_t> plen;
-        GX_TRY(k0.alloc(n));
-        GX_TRY(k1.alloc(n));
+        GX_TRY(d0.alloc(n));
+        GX_TRY(d1.alloc(n));
+        GX_TRY(i0.alloc(n));
+        GX_TRY(i1.alloc(n));
         GX_TRY(plen.alloc(n + 1));
         const unsigned grid = grid_for(n + 1, 256, 8192);
-        hipLaunchKernelGGL(k_hub_keys, dim3(grid), dim3(256), 0, s, g->outdeg.p, (int64_t)n, k0.p);
+        hipLaunchKernelGGL(k_hub_keys, dim3(grid), dim3(256), 0, s, g->outdeg.p, (int64_t)n, d0.p, i0.p);
         GX_TRY(check_launch("k_hub_keys"));
-        GX_TRY(sort_keys_u64(k0.p, k1.p, n, 64, s));
-        hipLaunchKernelGGL(k_hub_apply, dim3(grid), dim3(256), 0, s, k1.p, (int64_t)n, g->outdeg.p, P.rp.p, p->order.p,
+        GX_TRY(sort_pairs_desc_u32_i32(d0.p, d1.p, i0.p, i1.p, n, s));
+        hipLaunchKernelGGL(k_hub_apply, dim3(grid), dim3(256), 0, s, i1.p, (int64_t)n, g->outdeg.p, P.rp.p, p->order.p,
                            p->perm.p, p->outdeg_own.p, plen.p);
         GX_TRY(check_launch("k_hub_apply"));
         GX_TRY(scan_exclusive_i64(plen.p, p->rp_own.p, n + 1, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries are freed at the end of the block
     }
     clk.mark("hub order + row pointers (device)");
     std::vector<int64_t> nrp(n + 1);

@@ -730,32 +730,37 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         DBuf<int64_t> srow;
         GX_TRY(srow.alloc(nslabs + 1));
         GX_TRY(slab_rows(p->rp, rows, nslabs, srow.p, s));
+        clk.mark("segments + slab rows");
         const unsigned kgrid = grid_for((uint64_t)nslabs * kWave, 256, 16384);
         const unsigned pgrid = grid_for(nnz, 256, 1u << 20);
         const uint32_t colmask = (uint32_t)((1ull << colbits) - 1);
-        DBuf<uint16_t> v0, v1;
-        GX_TRY(v0.alloc(nnz));
-        GX_TRY(v1.alloc(nnz));
-        if (segbits + colbits <= 32) {   // 4-byte keys: fewer radix passes, half the key bytes
-            DBuf<uint32_t> k0, k1;
-            GX_TRY(k0.alloc(nnz));
-            GX_TRY(k1.alloc(nnz));
-            hipLaunchKernelGGL(k_sorted_keys<uint32_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs, k0.p,
-                               v0.p);
+        // keys and values in the kept plan scratch: [k0 | k1 | v0 | v1]
+        const bool narrow = segbits + colbits <= 32;   // 4-byte keys: fewer radix passes, half the key bytes
+        const size_t kb = narrow ? 4 : 8, align = 256;
+        auto up = [&](size_t x) { return (x + align - 1) / align * align; };
+        const size_t kbytes = up((size_t)nnz * kb), vbytes = up((size_t)nnz * 2);
+        char *scr = nullptr;
+        GX_TRY(plan_scratch(2 * kbytes + 2 * vbytes, reinterpret_cast<void **>(&scr)));
+        uint16_t *v0 = reinterpret_cast<uint16_t *>(scr + 2 * kbytes), *v1 = reinterpret_cast<uint16_t *>(scr + 2 * kbytes + vbytes);
+        clk.mark("key buffers");
+        if (narrow) {
+            uint32_t *k0 = reinterpret_cast<uint32_t *>(scr), *k1 = reinterpret_cast<uint32_t *>(scr + kbytes);
+            hipLaunchKernelGGL(k_sorted_keys<uint32_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs, k0,
+                               v0);
             GX_TRY(check_launch("k_sorted_keys"));
-            GX_TRY(sort_pairs_u32_u16(k0.p, k1.p, v0.p, v1.p, (size_t)nnz, segbits + colbits, s));
+            clk.mark("keys");
+            GX_TRY(sort_pairs_u32_u16(k0, k1, v0, v1, (size_t)nnz, segbits + colbits, s));
+            clk.mark("sort");
             hipLaunchKernelGGL(k_sorted_pack<uint32_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
-                               (int64_t)nnz, k1.p, v1.p, colmask, p->sci.p, p->spk.p, p->gbase.p);
+                               (int64_t)nnz, k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
         } else {
-            DBuf<uint64_t> k0, k1;
-            GX_TRY(k0.alloc(nnz));
-            GX_TRY(k1.alloc(nnz));
-            hipLaunchKernelGGL(k_sorted_keys<uint64_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs, k0.p,
-                               v0.p);
+            uint64_t *k0 = reinterpret_cast<uint64_t *>(scr), *k1 = reinterpret_cast<uint64_t *>(scr + kbytes);
+            hipLaunchKernelGGL(k_sorted_keys<uint64_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs, k0,
+                               v0);
             GX_TRY(check_launch("k_sorted_keys"));
-            GX_TRY(sort_pairs_u64_u16(k0.p, k1.p, v0.p, v1.p, (size_t)nnz, segbits + colbits, s));
+            GX_TRY(sort_pairs_u64_u16(k0, k1, v0, v1, (size_t)nnz, segbits + colbits, s));
             hipLaunchKernelGGL(k_sorted_pack<uint64_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
-                               (int64_t)nnz, k1.p, v1.p, colmask, p->sci.p, p->spk.p, p->gbase.p);
+                               (int64_t)nnz, k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
         }
         GX_TRY(check_launch("k_sorted_pack"));
         // GX_PR_LANEPERM=0 keeps every group in column order
@@ -764,7 +769,7 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
                                p->sci.p);
             GX_TRY(check_launch("k_sorted_laneperm"));
         }
-        GX_HIP_TRY(hipStreamSynchronize(s));   // the key buffers are freed at return
+        GX_HIP_TRY(hipStreamSynchronize(s));   // the segment tables are freed at return
     }
     p->ci = p->sci.p;   // the LONG rows read their (column-sorted) entries there
     clk.mark("keys + sort + pack + laneperm");

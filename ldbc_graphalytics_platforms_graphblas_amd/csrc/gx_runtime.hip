@@ -548,59 +548,85 @@ int key_bits(uint64_t n) {
 
 namespace gx {
 
-int sort_pairs_u64_u32(uint64_t *k_in, uint64_t *k_out, uint32_t *v_in, uint32_t *v_out, size_t m, int end_bit,
-                       hipStream_t s) {
-    if (!m) return GX_SUCCESS;
-    size_t tmp_bytes = 0;
-    GX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
-    DBuf<char> tmp;
-    GX_TRY(tmp.alloc(tmp_bytes));
-    GX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
-    GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+// rocPRIM temporary storage: one grow-only buffer per device, reused by every sort and scan,
+// so a call neither allocates, frees nor synchronises (the buffer outlives the stream work
+// that uses it; growing frees the old one, and hipFree waits for the device).  libgx is
+// driven by one host thread per device.
+// (Never destroyed: a static destructor would free after the HIP runtime shut down.)
+static DBuf<char> *const g_tmp = new DBuf<char>[64];
+
+static DBuf<char> *const g_scratch = new DBuf<char>[64];
+
+static int grow_slot(DBuf<char> *slots, size_t bytes, void **p) {
+    int dev = 0;
+    GX_HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(GX_NOT_IMPLEMENTED, "more than 64 devices");
+    DBuf<char> &t = slots[dev];
+    if (t.n < bytes) GX_TRY(t.alloc(std::max<size_t>(bytes, 1 << 20)));
+    *p = t.p;
     return GX_SUCCESS;
 }
+
+static int rocprim_tmp(size_t bytes, void **p) { return grow_slot(g_tmp, bytes, p); }
+
+// Plan-time scratch of the current device (the PageRank plan's sort keys and values): grow-only
+// and kept, so a plan neither frees gigabytes (hipFree waits for the device) nor allocates
+// them again for the next graph.  One user at a time (the plan builders, one host thread).
+int plan_scratch(size_t bytes, void **p) { return grow_slot(g_scratch, bytes, p); }
 
 int sort_keys_u64(uint64_t *k_in, uint64_t *k_out, size_t m, int end_bit, hipStream_t s) {
     if (!m) return GX_SUCCESS;
     size_t tmp_bytes = 0;
     GX_HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, k_in, k_out, m, 0, end_bit, s));
-    DBuf<char> tmp;
-    GX_TRY(tmp.alloc(tmp_bytes));
-    GX_HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, k_in, k_out, m, 0, end_bit, s));
-    GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+    void *tmp = nullptr;
+    GX_TRY(rocprim_tmp(tmp_bytes, &tmp));
+    GX_HIP_TRY(rocprim::radix_sort_keys(tmp, tmp_bytes, k_in, k_out, m, 0, end_bit, s));
     return GX_SUCCESS;
 }
 
-template <typename K>
-static int sort_pairs_k_u16(K *k_in, K *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit, hipStream_t s) {
+template <typename K, typename V>
+static int sort_pairs_kv(K *k_in, K *k_out, V *v_in, V *v_out, size_t m, int end_bit, bool desc, hipStream_t s) {
     if (!m) return GX_SUCCESS;
     size_t tmp_bytes = 0;
-    GX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
-    DBuf<char> tmp;
-    GX_TRY(tmp.alloc(tmp_bytes));
-    GX_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
-    GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+    if (desc)
+        GX_HIP_TRY(rocprim::radix_sort_pairs_desc(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
+    else
+        GX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
+    void *tmp = nullptr;
+    GX_TRY(rocprim_tmp(tmp_bytes, &tmp));
+    if (desc)
+        GX_HIP_TRY(rocprim::radix_sort_pairs_desc(tmp, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
+    else
+        GX_HIP_TRY(rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
     return GX_SUCCESS;
 }
 
 int sort_pairs_u32_u16(uint32_t *k_in, uint32_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
                        hipStream_t s) {
-    return sort_pairs_k_u16(k_in, k_out, v_in, v_out, m, end_bit, s);
+    return sort_pairs_kv(k_in, k_out, v_in, v_out, m, end_bit, false, s);
 }
 
 int sort_pairs_u64_u16(uint64_t *k_in, uint64_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
                        hipStream_t s) {
-    return sort_pairs_k_u16(k_in, k_out, v_in, v_out, m, end_bit, s);
+    return sort_pairs_kv(k_in, k_out, v_in, v_out, m, end_bit, false, s);
+}
+
+int sort_pairs_u64_u32(uint64_t *k_in, uint64_t *k_out, uint32_t *v_in, uint32_t *v_out, size_t m, int end_bit,
+                       hipStream_t s) {
+    return sort_pairs_kv(k_in, k_out, v_in, v_out, m, end_bit, false, s);
+}
+
+int sort_pairs_desc_u32_i32(uint32_t *k_in, uint32_t *k_out, int32_t *v_in, int32_t *v_out, size_t m, hipStream_t s) {
+    return sort_pairs_kv(k_in, k_out, v_in, v_out, m, 32, true, s);
 }
 
 int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s) {
     if (!m) return GX_SUCCESS;
     size_t tmp_bytes = 0;
     GX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, in, out, (int64_t)0, m, rocprim::plus<int64_t>(), s));
-    DBuf<char> tmp;
-    GX_TRY(tmp.alloc(tmp_bytes));
-    GX_HIP_TRY(rocprim::exclusive_scan(tmp.p, tmp_bytes, in, out, (int64_t)0, m, rocprim::plus<int64_t>(), s));
-    GX_HIP_TRY(hipStreamSynchronize(s));   // tmp is freed at return
+    void *tmp = nullptr;
+    GX_TRY(rocprim_tmp(tmp_bytes, &tmp));
+    GX_HIP_TRY(rocprim::exclusive_scan(tmp, tmp_bytes, in, out, (int64_t)0, m, rocprim::plus<int64_t>(), s));
     return GX_SUCCESS;
 }
 
