@@ -7,7 +7,7 @@ bytes, and the one-off plan kernels (built by the first call, cached) listed apa
 2 x FETCH_SIZE (gfx950 tallies a 128-B read request at 64 B, MI355X_MICROARCH.md HBM) +
 WRITE_SIZE; the 32-B share of the read requests is reported so the x2 can be checked.
 
-    python tools/alg_pmc_json.py OUTDIR TAG
+    python tools/alg_pmc_json.py OUTDIR OUTFILE
 """
 import collections
 import csv
@@ -45,7 +45,7 @@ def stats(path):
 
 
 def main():
-    outdir, tag = sys.argv[1], sys.argv[2]
+    outdir, outfile = sys.argv[1], sys.argv[2]
     res = {"how": __doc__.strip().splitlines()[2:8], "algorithms": {}}
     for alg in ("bfs", "wcc", "sssp", "cdlp", "lcc"):
         tr = os.path.join(outdir, f"{alg}_trace")
@@ -79,8 +79,7 @@ def main():
             "hbm_bytes_per_run": hbm, "algorithmic_bytes_per_run": bytes_model,
             "traffic_over_algorithmic": hbm / bytes_model if bytes_model else None,
             "device_us_per_run": sum(e["us_per_run"] for e in per_run.values())}
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", f"{tag}_pmc_algorithms.json")
-    with open(p, "w") as f:
+    with open(outfile, "w") as f:
         json.dump(res, f, indent=1)
     for alg, a in res["algorithms"].items():
         print(alg, a["workload"], "hbm %.1f MB/run" % (a["hbm_bytes_per_run"] / 1e6),
