@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Summarise tools/alg_pmc.sh output into profiles/<tag>_pmc_algorithms.json.
 
-Per algorithm: the kernels launched in every call (dispatch count a multiple of the 8 calls
-bench.py --steps 4 --warmup 1 makes) with their rocprofv3 mean duration and per-run fabric
-bytes, and the one-off plan kernels (built by the first call, cached) listed apart.  Bytes:
+Per algorithm: the kernels launched by (nearly) every one of the 8 calls bench.py --steps 4
+--warmup 1 makes (at least 4 dispatches; totals divided by 8) with their rocprofv3 mean
+duration and per-run fabric bytes, and the one-off plan kernels (built by the first call,
+cached) listed apart.  Bytes:
 2 x FETCH_SIZE (gfx950 tallies a 128-B read request at 64 B, MI355X_MICROARCH.md HBM) +
 WRITE_SIZE; the 32-B share of the read requests is reported so the x2 can be checked.
 
@@ -14,7 +15,14 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
+
+
+def kname(full):
+    """k_* symbol of a rocprof kernel name ("void gx::(anonymous namespace)::k_x<...>(...)")."""
+    m = re.search(r"\b(k_[A-Za-z0-9_]+)", full)
+    return m.group(1) if m else None
 
 CALLS = 8
 
@@ -25,7 +33,9 @@ def pmc(path):
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         seen = set()
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].split("<")[0].strip()
+            k = kname(r["Kernel_Name"])
+            if k is None:
+                continue
             acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
             if (r["Dispatch_Id"], r["Counter_Name"]) not in seen:
                 seen.add((r["Dispatch_Id"], r["Counter_Name"]))
@@ -36,8 +46,8 @@ def stats(path):
     out = {}
     for f in glob.glob(os.path.join(path, "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = r["Name"].split("(")[0].split("<")[0].strip()
-            if k.startswith("k_"):
+            k = kname(r["Name"])
+            if k:
                 d = out.setdefault(k, {"calls": 0, "total_ns": 0.0})
                 d["calls"] += int(r["Calls"])
                 d["total_ns"] += float(r["TotalDurationNs"])
@@ -65,10 +75,10 @@ def main():
                  "write_bytes": f2.get(k, {}).get("WRITE_SIZE", 0.0) * 1024,
                  "ea_rdreq": f3.get(k, {}).get("TCC_EA0_RDREQ_sum", 0.0),
                  "ea_rdreq_32b": f3.get(k, {}).get("TCC_EA0_RDREQ_32B_sum", 0.0)}
-            if d["calls"] % CALLS == 0:
+            if d["calls"] >= CALLS // 2:   # launched by (nearly) every call; plan kernels run once or twice
                 for x in ("fetch_bytes", "write_bytes", "ea_rdreq", "ea_rdreq_32b"):
                     e[x] /= CALLS
-                e["dispatches_per_run"] = d["calls"] // CALLS
+                e["dispatches_per_run"] = d["calls"] / CALLS
                 e["us_per_run"] = d["total_ns"] / CALLS / 1e3
                 per_run[k] = e
             else:
