@@ -19,7 +19,7 @@ for alg in "${ALGS[@]}"; do
   i=0
   for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
     i=$((i+1))
-    timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex '^k_' --output-format csv -d "$OUT/${alg}_pmc$i" -o pmc -- \
+    timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex '::k_' --output-format csv -d "$OUT/${alg}_pmc$i" -o pmc -- \
         python3 bench.py --algorithm "$alg" --steps 4 --warmup 1 --no-cpu-baseline > "$OUT/${alg}_pmc$i.log" 2>&1 || exit 1
   done
   echo "$alg done"

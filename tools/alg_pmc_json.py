@@ -68,14 +68,16 @@ def main():
             workload, bytes_model = line["config"]["workload"], line["roofline"]["bytes_per_run"]
         except Exception:
             workload, bytes_model = alg, None
-        per_run, plan = {}, {}
+        per_run, plan, other = {}, {}, {}
         for k, d in sorted(st.items(), key=lambda kv: -kv[1]["total_ns"]):
             e = {"dispatches": d["calls"], "mean_us": d["total_ns"] / d["calls"] / 1e3,
                  "fetch_bytes": 2.0 * f1.get(k, {}).get("FETCH_SIZE", 0.0) * 1024,
                  "write_bytes": f2.get(k, {}).get("WRITE_SIZE", 0.0) * 1024,
                  "ea_rdreq": f3.get(k, {}).get("TCC_EA0_RDREQ_sum", 0.0),
                  "ea_rdreq_32b": f3.get(k, {}).get("TCC_EA0_RDREQ_32B_sum", 0.0)}
-            if d["calls"] >= CALLS // 2:   # launched by (nearly) every call; plan kernels run once or twice
+            if alg == "sssp" and k.startswith("k_split_"):   # the bench's split-path leg, not gx_sssp
+                other[k] = e
+            elif d["calls"] >= CALLS // 2:   # launched by (nearly) every call; plan kernels run once or twice
                 for x in ("fetch_bytes", "write_bytes", "ea_rdreq", "ea_rdreq_32b"):
                     e[x] /= CALLS
                 e["dispatches_per_run"] = d["calls"] / CALLS
@@ -86,6 +88,7 @@ def main():
         hbm = sum(e["fetch_bytes"] + e["write_bytes"] for e in per_run.values())
         res["algorithms"][alg] = {
             "workload": workload, "calls_profiled": CALLS, "per_run_kernels": per_run, "plan_kernels": plan,
+            "other_path_kernels": other,
             "hbm_bytes_per_run": hbm, "algorithmic_bytes_per_run": bytes_model,
             "traffic_over_algorithmic": hbm / bytes_model if bytes_model else None,
             "device_us_per_run": sum(e["us_per_run"] for e in per_run.values())}
