@@ -128,6 +128,7 @@ struct PrPart {
     int utimes_launch = 0;
     int long_nnz = 65536;        // longer rows take the LONG segment path
     int sorted_lds = 0;          // dynamic LDS bytes of the launch
+    int idx_nt = 0;              // index stream loaded non-temporally (x far larger than the L2s)
     uint32_t nsorted = 0, nlong_pad = 0;
     // dangling-score sum fused into the kernel: blocks holding out-degree-0 rows publish a
     // partial, the last of them adds them up in slot order

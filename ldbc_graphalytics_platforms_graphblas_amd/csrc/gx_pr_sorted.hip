@@ -195,7 +195,7 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // 1 no LDS adds (register sum), 2 no gathers, 3 neither, 4 gathers folded into x[c & 4095]
 // (L1 hits), 5 no gathers + conflict-free LDS adds (acc[tid]), 6 gathers + conflict-free LDS
 // adds, 7 no index loads (entries synthesised from the position, columns = the base).
-template <int PROBE>
+template <int PROBE, int CP>   // CP bit 0: index loads non-temporal
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
                                              double *acc, int64_t step64) {
     const int tid = threadIdx.x;
@@ -234,7 +234,8 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
             } else {
                 // clamped into the block; spk's allocation slack covers the 3 entries past `last`;
                 // the address is a CSR offset, only 4-B aligned (gx_u32x4)
-                const gx_u32x4 q4 = *reinterpret_cast<const gx_u32x4 *>(spk + min(sg + 4 * lane, last));
+                const gx_u32x4 *qa = reinterpret_cast<const gx_u32x4 *>(spk + min(sg + 4 * lane, last));
+                const gx_u32x4 q4 = (CP & 1) ? __builtin_nontemporal_load(qa) : *qa;
                 d.q[v] = make_uint4(q4.x, q4.y, q4.z, q4.w);
             }
         }
@@ -341,7 +342,7 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
 // unit order with sc1 loads and runs the epilogue (MI355X_MICROARCH.md "Valid forms": sc1 stores
 // drained before the counter add, sc1 loads by the workgroup whose add came last).
 // TIMES: debug build with per-workgroup timestamps (GX_PR_UNIT_TIMES).
-template <bool TIMES, int PROBE = 0>
+template <bool TIMES, int PROBE = 0, int CP = 0>
 __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs a) {
     extern __shared__ double acc[];
     __shared__ double wred[kBS / kWave];
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
     if (!empty) {
         for (int i = tid; i < nrows; i += kBS) acc[i] = 0.0;
         __syncthreads();
-        gather_units<PROBE>(a, b, u.lo, u.hi, acc, u.step);
+        gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step);
         __syncthreads();
     }
     if (TIMES && tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
@@ -622,6 +623,11 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     const int64_t B = env_int("GX_PR_BLOCK_NNZ", (int)bdef, 1024, 1 << 30);
     p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)std::max<int64_t>(B / 4, kRound), 1024, 1 << 30);
     p->sorted_nnz = (int)B;
+    // The index stream is read once per launch.  Loaded non-temporally it leaves the XCD's L2 to
+    // x's lines: SYN-8_5 (67 MB of x) 898 -> 871-877 us per launch, SYN-7_5 (8 MB, which the L2s
+    // mostly hold anyway) 83 -> 91 (round 3, tools/r03_cp_ab.sh).  GX_PR_CP=0/1 overrides.
+    const uint64_t xbytes = (uint64_t)p->chunk * (uint64_t)std::max(1, p->nranks) * sizeof(double);
+    p->idx_nt = env_int("GX_PR_CP", xbytes >= (48ull << 20) ? 1 : 0, 0, 1);
     PlanClock clk("sorted", p->ctx->stream);
     const int64_t R = p->sorted_rows, LT = std::max<int64_t>(p->long_nnz, 1);
     std::vector<RowBlock> longb, sortb;
@@ -955,7 +961,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                 }
             } else
 #endif
-            hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
+            if (p->idx_nt) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1>), dim3(nw), dim3(kBS), lds, s, a);
+            else hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
         }
         if (a.utimes && ++p->utimes_launch == env_int("GX_PR_UNIT_TIMES_LAUNCH", 5, 1, 1 << 30)) {
             std::vector<uint64_t> t(4 * (size_t)nw);
