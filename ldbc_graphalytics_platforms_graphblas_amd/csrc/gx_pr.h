@@ -56,15 +56,21 @@ struct RowBlock {
 // column range, so the units of a block move through x together).  A block cut into
 // nunits > 1 units sums its rows through per-unit partial slabs (slab + unit * rows doubles);
 // the last unit to arrive (ticket[part]) adds them in unit order and runs the epilogue.
+// The block's column-sorted prefix of dense columns is stored as narrow 2-byte codes (nbeg,
+// nsg: the block's first code in PrPart::npk and its 512-code supergroups); [lo, hi) is the
+// wide 4-byte remainder.  Unit j of k takes narrow rounds j, j + k, ... as well.
 struct SortedUnit {
     int64_t lo;
     int64_t hi;
     int64_t step;
     int64_t slab;       // first double of the block's slabs in PrPart::uslab
+    int64_t nbeg;       // first narrow code of the block (a multiple of 512)
+    int32_t nsg;        // narrow supergroups (512 codes each) of the block
     int32_t blk;        // index into PrPart::blocks
     int32_t part;       // ticket index of a multi-unit block, -1 when nunits == 1
     int32_t unit;       // this unit's number within the block
     int32_t nunits;
+    int32_t pad;
 };
 
 // x of local row `row`: rows [0, live) sit in the exchanged chunk, the rest (out-degree 0, so
@@ -116,7 +122,14 @@ struct PrPart {
     // column-sorted blocks (k_pr_pull_units, gx_pr_sorted.hip; the default)
     DBuf<int32_t> sci;           // columns sorted within each block
     DBuf<uint32_t> spk;          // packed (column - group base) << 14 | row
-    DBuf<uint32_t> gbase;        // base column per 64-entry group (bit 31: escape to sci)
+    DBuf<uint32_t> gbase;        // base column per 256-entry supergroup (bit 31: escape to sci)
+    // narrow codes (gx_pr_sorted.hip): (column delta 0..3) << 14 | row, per block a 512-aligned
+    // run; the column of a code is its 512-code supergroup's base plus the deltas up to it
+    DBuf<uint16_t> npk;
+    DBuf<uint32_t> nbase;        // per narrow supergroup: the column before its first code
+    uint64_t nnarrow = 0;        // narrow entries (without the delta-only fillers)
+    uint64_t ncodes = 0;         // narrow codes, fillers and padding included
+    uint32_t null_sg = 0;        // an all-padding supergroup gathering x's zero slot
     int sorted_nnz = 65536;      // entries per block
     int sorted_rows = 4096;      // rows per block (LDS accumulators)
     int64_t unit_nnz = 0;        // target entries per unit

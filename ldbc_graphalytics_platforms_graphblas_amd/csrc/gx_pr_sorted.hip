@@ -45,6 +45,9 @@ constexpr int kRowBits = 14;     // packed entry: (column - group base) << kRowB
 constexpr int kBS = 1024;        // threads of a k_pr_pull_units workgroup (16 waves, one per CU)
 constexpr int kU = 8;            // entries per lane and round (two 16-B index loads)
 constexpr int kRound = kBS * kU; // entries of one round of a workgroup
+constexpr int kNSg = 512;        // codes of a narrow supergroup: one wave's 16-B load per lane
+constexpr int kJunkRow = (1 << kRowBits) - kWave;   // accumulators [16320, 16384) absorb fillers
+constexpr int kMaxBlockRows = kJunkRow;             // rows of a sorted block
 
 struct SortedArgs {
     const RowBlock *blocks;
@@ -77,6 +80,9 @@ struct SortedArgs {
     double *uslab;
     uint32_t *uticket;
     uint64_t *utimes;        // debug (GX_PR_UNIT_TIMES): per workgroup start, gather end, end, XCC
+    const uint16_t *npk;     // narrow codes
+    const uint32_t *nbase;   // per narrow supergroup: the column before its first code
+    uint32_t null_sg;        // all-padding supergroup (base = zero_col)
     double *xd;              // x of the rows past `live` (store_x, gx_pr.h)
     int64_t live;
 };
@@ -336,6 +342,106 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
     if constexpr (PROBE == 1 || PROBE == 3) atomicAdd(&acc[tid], rsum);
 }
 
+// Inclusive prefix sum over the 64 lanes by DPP moves (row_shr 1/2/4/8 inside each 16-lane
+// row, then row_bcast:15 and row_bcast:31 across rows); lanes whose source is out of range or
+// whose row is masked add the `old` operand, 0.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
+// The narrow prefix of a block: 2-byte codes (delta << 14) | row, delta = the column step from
+// the previous code (0..3; a larger step is split by filler codes of step 3 whose rows are
+// junk accumulators >= kJunkRow).  A narrow supergroup of 512 codes is one wave-load of 16 B
+// per lane: lane l decodes codes 8l .. 8l+7, their columns are the supergroup's base plus the
+// lane's exclusive wave scan of delta sums plus its own running sum.  Round i of the unit is
+// the workgroup's 16 supergroups (j + i k) * 16 + wave; a supergroup past the block reads the
+// null supergroup (padding codes, base = x's zero slot), so the loop has no range checks.
+// Same pipeline as gather_units: round i+1's gathers issue before round i's LDS adds, the
+// loads two rounds ahead, buffers A/B alternating.
+template <int CP>
+__device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedUnit &u, double *acc) {
+    constexpr int W = kBS / kWave;   // supergroups per round
+    const int32_t nrounds = (u.nsg + W - 1) / W;
+    if (u.unit >= nrounds) return;
+    const int32_t nr = (nrounds - u.unit + u.nunits - 1) / u.nunits;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid >> 6;
+    const uint32_t sg0 = (uint32_t)(u.nbeg / kNSg);
+    const char *xb = reinterpret_cast<const char *>(a.x_in);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // 16-B aligned (512-code runs)
+    struct Rd {
+        u32x4 q;
+        uint32_t base;
+    };
+    struct Gt {
+        double g[kU];
+        uint32_t r[kU];
+    };
+    auto load = [&](Rd &d, int32_t i) {
+        const int32_t sg = (u.unit + i * u.nunits) * W + wave;
+        const uint32_t g = sg < u.nsg ? sg0 + (uint32_t)sg : a.null_sg;
+        const u32x4 *qa = reinterpret_cast<const u32x4 *>(a.npk + (size_t)g * kNSg) + lane;
+        d.q = (CP & 1) ? __builtin_nontemporal_load(qa) : *qa;
+        d.base = a.nbase[g];
+    };
+    auto issue = [&](const Rd &d, Gt &t) {
+        const uint32_t w[4] = {d.q.x, d.q.y, d.q.z, d.q.w};
+        uint32_t pre[kU];
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < kU; k++) {
+            const uint32_t c = (k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu);
+            run += c >> kRowBits;
+            pre[k] = run;
+            t.r[k] = c & ((1u << kRowBits) - 1);
+            asm volatile("" : "+v"(t.r[k]));
+        }
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.base) + (wave_scan_incl(run) - run);
+#pragma unroll
+        for (int k = 0; k < kU; k++) t.g[k] = *reinterpret_cast<const double *>(xb + ((b + pre[k]) << 3));
+    };
+    auto add = [&](const Gt &t) {
+#pragma unroll
+        for (int k = 0; k < kU; k++) atomicAdd(&acc[t.r[k]], t.g[k]);
+    };
+    Rd dA, dB;
+    Gt tA, tB;
+    load(dA, 0);
+    load(dB, 1);
+    issue(dA, tA);
+    __builtin_amdgcn_sched_barrier(0);
+    load(dA, 2);
+    int32_t k = 1;
+    for (; k + 1 < nr; k += 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        issue(dB, tB);
+        __builtin_amdgcn_sched_barrier(0);
+        load(dB, k + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        add(tA);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(dA, tA);
+        __builtin_amdgcn_sched_barrier(0);
+        load(dA, k + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        add(tB);
+    }
+    if (k < nr) {
+        issue(dB, tB);
+        add(tA);
+        add(tB);
+    } else {
+        add(tA);
+    }
+}
+
 // One iteration's SpMV over split blocks.  Grid: [0, nlong_pad) LONG row segments (padded to a
 // multiple of 8), then the units (largest first; the blocks of rows without entries last).  A multi-unit block's units store their row sums write-through (sc1) to
 // their own slab, drain them (vmcnt(0)) and take a ticket; the last arriver adds the slabs in
@@ -378,6 +484,7 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
     if (!empty) {
         for (int i = tid; i < nrows; i += kBS) acc[i] = 0.0;
         __syncthreads();
+        if constexpr (PROBE == 0) gather_narrow<CP>(a, u, acc);
         gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step);
         __syncthreads();
     }
@@ -526,9 +633,11 @@ __global__ __launch_bounds__(256) void k_sorted_pack(const SegDesc *__restrict__
 // goes to instruction k mod 4, slot k / 4: a residue held by m <= 4 entries lands in m
 // different instructions.  The group keeps its column set, so its gathers touch the same lines.
 // One wave per group.
-__global__ __launch_bounds__(256) void k_sorted_laneperm(const RowBlock *__restrict__ blocks, uint32_t *spk, int32_t *sci) {
+// Only the wide part of the block (from its narrow prefix nsplit[block] supergroups on).
+__global__ __launch_bounds__(256) void k_sorted_laneperm(const RowBlock *__restrict__ blocks, const uint32_t *__restrict__ nsplit,
+                                                         uint32_t *spk, int32_t *sci) {
     const RowBlock b = blocks[blockIdx.y];
-    const int64_t z0 = b.nz_begin, ngroups = (b.nz_end - z0) >> 6;   // full groups only
+    const int64_t z0 = b.nz_begin + 256 * (int64_t)nsplit[blockIdx.y], ngroups = (b.nz_end - z0) >> 6;   // full groups only
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
     const int64_t waves = (int64_t)gridDim.x * blockDim.x / kWave;
@@ -548,6 +657,159 @@ __global__ __launch_bounds__(256) void k_sorted_laneperm(const RowBlock *__restr
         const int64_t dst = z0 + (g << 6) + 4 * (rank >> 2) + (rank & 3);
         spk[dst] = p;
         sci[dst] = c;
+    }
+}
+
+// ---- narrow codes (gather_narrow).  A sorted block's entries are column-sorted; its prefix of
+// supergroups where 2-byte codes (fillers included) take fewer bytes than the 4-byte entries is
+// recoded, chosen per block to minimise the index bytes: supergroup g costs 2 (n_g + D_g) bytes
+// narrow against 4 n_g wide, D_g = the fillers its column steps need (a step s > 3 takes
+// ceil(s / 3) - 1).  SYN-8_5: 95 % of the entries, 2.5 % fillers, index bytes 2.51 -> 1.35 GB.
+
+// fillers of the step from the previous entry of the block to entry e (0 for its first)
+__device__ __forceinline__ uint32_t narrow_fillers(const int32_t *sci, int64_t z0, int64_t e, uint32_t *step) {
+    const uint32_t c = (uint32_t)sci[e];
+    const uint32_t s0 = e > z0 ? c - (uint32_t)sci[e - 1] : 0u;
+    *step = s0;
+    return s0 > 3 ? (s0 + 2) / 3 - 1 : 0u;
+}
+
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(v), kWave - 1);
+}
+
+// D_g of every 256-entry supergroup of every sorted block (grid.y = block), one wave each.
+__global__ __launch_bounds__(256) void k_narrow_cost(const RowBlock *__restrict__ blocks, const int32_t *__restrict__ sci,
+                                                     uint32_t *__restrict__ fill) {
+    const RowBlock b = blocks[blockIdx.y];
+    const int64_t z0 = b.nz_begin, N = b.nz_end - z0, ng = (N + 255) >> 8;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t waves = (int64_t)gridDim.x * blockDim.x / kWave;
+    for (int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; g < ng; g += waves) {
+        uint32_t d = 0, st;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t e = (g << 8) + 4 * lane + j;
+            if (e < N) d += narrow_fillers(sci, z0, z0 + e, &st);
+        }
+        d = wave_total(d);
+        if (lane == 0) fill[b.seg + g] = d;
+    }
+}
+
+// Per block (one 1024-thread workgroup): the narrow prefix P (supergroups) maximising
+// sum_{g<P} (n_g - D_g) (0 when `enable` is off), the code offset of every supergroup inside
+// the block's narrow run (exclusive prefix of n_g + D_g), and the block's code count.
+__global__ __launch_bounds__(1024) void k_narrow_split(const RowBlock *__restrict__ blocks, const uint32_t *__restrict__ fill,
+                                                       int enable, uint32_t *__restrict__ nsplit, uint32_t *__restrict__ ncode,
+                                                       uint32_t *__restrict__ noff) {
+    __shared__ int64_t sben[1024], scod[1024];
+    __shared__ int64_t bestv[1024];
+    __shared__ int32_t besti[1024];
+    const RowBlock b = blocks[blockIdx.x];
+    const int64_t N = b.nz_end - b.nz_begin, ng = (N + 255) >> 8;
+    const int t = threadIdx.x;
+    const int64_t per = (ng + 1023) / 1024, g0 = min(ng, t * per), g1 = min(ng, g0 + per);
+    auto cnt = [&](int64_t g) { return min<int64_t>(256, N - (g << 8)); };
+    int64_t ben = 0, cod = 0;
+    for (int64_t g = g0; g < g1; g++) {
+        ben += cnt(g) - (int64_t)fill[b.seg + g];
+        cod += cnt(g) + (int64_t)fill[b.seg + g];
+    }
+    sben[t] = ben;
+    scod[t] = cod;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {   // inclusive scans (Hillis-Steele)
+        const int64_t a1 = t >= o ? sben[t - o] : 0, a2 = t >= o ? scod[t - o] : 0;
+        __syncthreads();
+        sben[t] += a1;
+        scod[t] += a2;
+        __syncthreads();
+    }
+    int64_t pb = sben[t] - ben, pc = scod[t] - cod;
+    int64_t bv = 0;
+    int32_t bi = 0;   // P = 0 is always allowed
+    for (int64_t g = g0; g < g1; g++) {
+        noff[b.seg + g] = (uint32_t)pc;
+        pb += cnt(g) - (int64_t)fill[b.seg + g];
+        pc += cnt(g) + (int64_t)fill[b.seg + g];
+        if (pb > bv) {
+            bv = pb;
+            bi = (int32_t)(g + 1);
+        }
+    }
+    bestv[t] = bv;
+    besti[t] = bi;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {   // max value, then the smallest prefix
+        if (t < o) {
+            const int64_t v2 = bestv[t + o];
+            const int32_t i2 = besti[t + o];
+            if (v2 > bestv[t] || (v2 == bestv[t] && i2 < besti[t])) {
+                bestv[t] = v2;
+                besti[t] = i2;
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const int32_t P = enable ? besti[0] : 0;
+        nsplit[blockIdx.x] = (uint32_t)P;
+        // codes of the prefix: the offset of supergroup P, or all of them
+        ncode[blockIdx.x] = P == 0 ? 0u : (uint32_t)(P < ng ? noff[b.seg + P] : (uint32_t)scod[1023]);
+    }
+}
+
+// Padding codes everywhere (step 0, a junk row by lane) and the null supergroup's base.
+__global__ void k_narrow_fill(uint16_t *__restrict__ npk, uint64_t ncodes, uint32_t *__restrict__ nbase, uint32_t null_sg,
+                              uint32_t zero_col) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < ncodes; p += (uint64_t)gridDim.x * blockDim.x)
+        npk[p] = (uint16_t)(kJunkRow + ((p >> 3) & (kWave - 1)));
+    if (blockIdx.x == 0 && threadIdx.x == 0) nbase[null_sg] = zero_col;
+}
+
+// The codes of the narrow prefix: one wave per 256-entry supergroup g < P of each block; lane
+// l emits entries 4l .. 4l+3, each preceded by its fillers, at the block's run + noff[g] + the
+// lane's exclusive scan of code counts.  Whoever emits the last code of a 512-code supergroup
+// stores the next one's base (the column reached); the block's first base is its first column.
+__global__ __launch_bounds__(256) void k_narrow_emit(const RowBlock *__restrict__ blocks, const int32_t *__restrict__ sci,
+                                                     const uint32_t *__restrict__ spk, const uint32_t *__restrict__ nsplit,
+                                                     const uint32_t *__restrict__ ncode, const uint32_t *__restrict__ noff,
+                                                     const int64_t *__restrict__ nbeg, uint16_t *__restrict__ npk,
+                                                     uint32_t *__restrict__ nbase) {
+    const RowBlock b = blocks[blockIdx.y];
+    const int64_t z0 = b.nz_begin, N = b.nz_end - z0, P = nsplit[blockIdx.y];
+    const int64_t nb = nbeg[blockIdx.y], C = ncode[blockIdx.y];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t waves = (int64_t)gridDim.x * blockDim.x / kWave;
+    if (P > 0 && blockIdx.x == 0 && threadIdx.x == 0) nbase[nb / kNSg] = (uint32_t)sci[z0];
+    for (int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; g < P; g += waves) {
+        uint32_t fl[4], st[4], n = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t e = (g << 8) + 4 * lane + j;
+            fl[j] = e < N ? narrow_fillers(sci, z0, z0 + e, &st[j]) : 0u;
+            n += e < N ? fl[j] + 1 : 0u;
+        }
+        int64_t pos = nb + noff[b.seg + g] + (wave_scan_incl(n) - n);   // absolute code index
+        auto put = [&](uint32_t step, uint32_t row, uint32_t col_after) {
+            npk[pos] = (uint16_t)((step << kRowBits) | row);
+            const int64_t rel = pos - nb + 1;   // codes of the block up to and including this one
+            if ((rel & (kNSg - 1)) == 0 && rel < C) nbase[(pos + 1) / kNSg] = col_after;
+            pos++;
+        };
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t e = (g << 8) + 4 * lane + j;
+            if (e >= N) continue;
+            const uint32_t c = (uint32_t)sci[z0 + e];
+            uint32_t at = c - st[j];
+            for (uint32_t f = 0; f < fl[j]; f++) {
+                at += 3;
+                put(3u, (uint32_t)(kJunkRow + ((pos >> 3) & (kWave - 1))), at);
+            }
+            put(c - at, spk[z0 + e] & ((1u << kRowBits) - 1), c);
+        }
     }
 }
 
@@ -612,7 +874,7 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     // requests (tools/pr_line_model.py) but give the last arriver more slabs per row.
     const double per_cu = std::max(1.0, (double)nnz / (double)cus);
     const bool huge = per_cu > (double)(2 << 20);
-    const int rmax = 1 << kRowBits;   // rows per block (LDS accumulators: 16 Ki rows = 128 KiB)
+    const int rmax = kMaxBlockRows;   // rows per block (LDS accumulators: 16 Ki rows = 128 KiB, the top 64 junk)
     p->sorted_rows = env_int("GX_PR_SORTED_ROWS", huge ? rmax : 4096, 64, rmax);
     // ... and at most 4x the power of two nearest nnz / CUs, so that a small partition (one rank
     // of eight) keeps about 4 units per block: a 1/8 piece of SYN-7_5 with 1 Mi blocks cut into
@@ -700,6 +962,10 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     GX_TRY(p->gbase.alloc(std::max<int64_t>(ngroups, 1), 16));
     hipStream_t s = p->ctx->stream;
     const RowBlock *d_sort = p->blocks.p + longb.size();
+    std::vector<uint32_t> h_nsplit(sortb.size(), 0), h_ncode(sortb.size(), 0);   // narrow prefix per sorted block
+    std::vector<int64_t> h_nbeg(sortb.size(), 0);
+    p->ncodes = 0;
+    p->nnarrow = 0;
     if (nnz > 0) {
         // segments in row order: the sorted blocks and the LONG rows
         std::vector<std::pair<int32_t, int32_t>> order_;   // (first row, index: block i >= 0, LONG row -1 - j)
@@ -769,16 +1035,54 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
                                (int64_t)nnz, k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
         }
         GX_TRY(check_launch("k_sorted_pack"));
+        clk.mark("keys + sort + pack");
+        // the narrow prefixes (GX_PR_NARROW=0: none) and their codes, before the lane permutation
+        DBuf<uint32_t> d_fill, d_noff, d_nsplit, d_ncode;
+        DBuf<int64_t> d_nbeg;
+        if (!sortb.empty()) {
+            const unsigned nsb = (unsigned)sortb.size();
+            GX_TRY(d_fill.alloc(std::max<int64_t>(ngroups, 1)));
+            GX_TRY(d_noff.alloc(std::max<int64_t>(ngroups, 1)));
+            GX_TRY(d_nsplit.alloc(nsb));
+            GX_TRY(d_ncode.alloc(nsb));
+            GX_TRY(d_nbeg.alloc(nsb));
+            hipLaunchKernelGGL(k_narrow_cost, dim3(64, nsb), dim3(256), 0, s, d_sort, p->sci.p, d_fill.p);
+            GX_TRY(check_launch("k_narrow_cost"));
+            hipLaunchKernelGGL(k_narrow_split, dim3(nsb), dim3(1024), 0, s, d_sort, d_fill.p,
+                               env_int("GX_PR_NARROW", 1, 0, 1), d_nsplit.p, d_ncode.p, d_noff.p);
+            GX_TRY(check_launch("k_narrow_split"));
+            GX_HIP_TRY(hipMemcpyAsync(h_nsplit.data(), d_nsplit.p, nsb * 4, hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipMemcpyAsync(h_ncode.data(), d_ncode.p, nsb * 4, hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            uint64_t run = 0;
+            for (size_t i = 0; i < sortb.size(); i++) {
+                h_nbeg[i] = (int64_t)run;
+                run += ((uint64_t)h_ncode[i] + kNSg - 1) / kNSg * kNSg;
+                p->nnarrow += (uint64_t)std::min<int64_t>((int64_t)h_nsplit[i] * 256, sortb[i].nz_end - sortb[i].nz_begin);
+            }
+            p->null_sg = (uint32_t)(run / kNSg);
+            p->ncodes = run + kNSg;
+            GX_TRY(p->npk.alloc(p->ncodes, 16));
+            GX_TRY(p->nbase.alloc(p->ncodes / kNSg));
+            GX_HIP_TRY(hipMemcpyAsync(d_nbeg.p, h_nbeg.data(), nsb * 8, hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(k_narrow_fill, dim3(grid_for(p->ncodes, 256, 16384)), dim3(256), 0, s, p->npk.p, p->ncodes,
+                               p->nbase.p, p->null_sg, (uint32_t)(p->chunk - 2));
+            GX_TRY(check_launch("k_narrow_fill"));
+            hipLaunchKernelGGL(k_narrow_emit, dim3(64, nsb), dim3(256), 0, s, d_sort, p->sci.p, p->spk.p, d_nsplit.p,
+                               d_ncode.p, d_noff.p, d_nbeg.p, p->npk.p, p->nbase.p);
+            GX_TRY(check_launch("k_narrow_emit"));
+            clk.mark("narrow codes");
+        }
         // GX_PR_LANEPERM=0 keeps every group in column order
         if (env_int("GX_PR_LANEPERM", 1, 0, 1) && !sortb.empty()) {
-            hipLaunchKernelGGL(k_sorted_laneperm, dim3(64, (unsigned)sortb.size()), dim3(256), 0, s, d_sort, p->spk.p,
-                               p->sci.p);
+            hipLaunchKernelGGL(k_sorted_laneperm, dim3(64, (unsigned)sortb.size()), dim3(256), 0, s, d_sort, d_nsplit.p,
+                               p->spk.p, p->sci.p);
             GX_TRY(check_launch("k_sorted_laneperm"));
         }
         GX_HIP_TRY(hipStreamSynchronize(s));   // the segment tables are freed at return
     }
     p->ci = p->sci.p;   // the LONG rows read their (column-sorted) entries there
-    clk.mark("keys + sort + pack + laneperm");
+    clk.mark("laneperm");
     p->nsorted = (uint32_t)sortb.size();
     p->nlong_pad = (p->nlong_blocks + 7u) & ~7u;
     // units of the split blocks: ceil(entries / T) per sorted block (at most one per round)
@@ -828,10 +1132,13 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
             const int64_t rows_b = b.row_end - b.row_begin;
             for (int32_t j = 0; j < k; j++) {
                 SortedUnit u;
-                u.lo = b.nz_begin + (int64_t)kRound * j;
+                u.lo = b.nz_begin + 256 * (int64_t)h_nsplit[i] + (int64_t)kRound * j;   // the wide part
                 u.hi = b.nz_end;
                 u.step = (int64_t)kRound * k;
                 u.slab = k > 1 ? slab : 0;
+                u.nbeg = h_nbeg[i];
+                u.nsg = (int32_t)(((int64_t)h_ncode[i] + kNSg - 1) / kNSg);
+                u.pad = 0;
                 u.blk = (int32_t)(longb.size() + i);
                 u.part = k > 1 ? parts : -1;
                 u.unit = j;
@@ -861,10 +1168,10 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         if (env_int("GX_PR_VERBOSE", 0, 0, 1))
             std::fprintf(stderr, "[gx_pr] plan: rows %lld nnz %llu unit_nnz %lld block_nnz %d "
                          "long_nnz %d: %zu sorted blocks, %u LONG blocks (%u rows), %u units, %d multi-unit blocks, "
-                         "slab %lld doubles\n",
+                         "slab %lld doubles; narrow %llu entries in %llu codes\n",
                          (long long)rows, (unsigned long long)nnz, (long long)T,
                          p->sorted_nnz, p->long_nnz, sortb.size(), p->nlong_blocks, p->nlong, p->nunits, parts,
-                         (long long)slab);
+                         (long long)slab, (unsigned long long)p->nnarrow, (unsigned long long)p->ncodes);
         GX_TRY(p->units.alloc(units.size()));
         GX_HIP_TRY(hipMemcpy(p->units.p, units.data(), units.size() * sizeof(SortedUnit), hipMemcpyHostToDevice));
         GX_TRY(p->uslab.alloc(std::max<int64_t>(slab, 1)));
@@ -935,6 +1242,9 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.xd = p->xd.p;
     a.live = (int64_t)p->live;
     a.utimes = nullptr;
+    a.npk = p->npk.p;
+    a.nbase = p->nbase.p;
+    a.null_sg = p->null_sg;
     const char *times_path = std::getenv("GX_PR_UNIT_TIMES");   // debug: not under graph capture
     const uint32_t nw = p->nlong_pad + p->nunits;
     if (times_path && nw) {

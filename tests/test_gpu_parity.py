@@ -197,7 +197,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
 
 
 @pytest.mark.parametrize("env", [{}, {"GX_PR_LANEPERM": "0"}, {"GX_PR_BLOCK_NNZ": "2097152", "GX_PR_UNIT_NNZ": "16384"},
-                                 {"GX_PR_CP": "1"},
+                                 {"GX_PR_CP": "1"}, {"GX_PR_NARROW": "0"}, {"GX_PR_NARROW": "0", "GX_PR_CP": "1"},
                                  {"GX_PR_KERNEL": "adaptive"},
                                  {"GX_PR_SORTED_ROWS": "16384", "GX_PR_UNIT_NNZ": "16384"},
                                  {"GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SORTED_ROWS": "2048"},
@@ -216,6 +216,40 @@ def test_pagerank_plan_variants(ctx, monkeypatch, env):
     for g in (_rmat(14, 16, 4), _rmat(11, 8, 3, undirected=False)):
         np.testing.assert_allclose(gpu_run(ctx, g, "PR", damping=0.85, iters=10),
                                    O.pagerank(g.csr, g.directed, 0.85, 10), rtol=PR_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("unit", [None, "8192"])
+def test_pagerank_narrow_fillers(ctx, monkeypatch, unit):
+    """Narrow 2-byte codes whose column steps need fillers: a 6-regular multiplicative graph
+    (v ~ 5v, 7v, 11v mod n, every degree equal, so the hub-first order is the identity) gives
+    every block column steps of all sizes; the per-block split puts some blocks' prefixes in
+    narrow codes with fillers and leaves the rest wide.  Also with blocks cut into units."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    if unit:
+        monkeypatch.setenv("GX_PR_UNIT_NNZ", unit)
+    n = 200003   # prime: v -> m v is a permutation
+    v = np.arange(1, n, dtype=np.int64)
+    src = np.concatenate([v, v, v])
+    dst = np.concatenate([(5 * v) % n, (7 * v) % n, (11 * v) % n])
+    keep = src != dst
+    csr = csr_from_edges(n, src[keep], dst[keep], None, symmetric=True)
+    np.testing.assert_allclose(gpu_run(ctx, _G(csr, False), "PR", damping=0.85, iters=8),
+                               O.pagerank(csr, False, 0.85, 8), rtol=PR_RTOL, atol=0)
+
+
+def test_pagerank_narrow_exact_supergroups(ctx, monkeypatch):
+    """Blocks whose narrow codes fill whole 512-code supergroups exactly (complete bipartite
+    graph K(512, 1024), 64-row blocks: 65 536 and 32 768 codes, no fillers): the base of the
+    supergroup after a block's last code belongs to the next block and must not be written."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    monkeypatch.setenv("GX_PR_SORTED_ROWS", "64")
+    monkeypatch.setenv("GX_PR_BLOCK_NNZ", "131072")
+    monkeypatch.setenv("GX_PR_UNIT_NNZ", "16384")
+    a = np.repeat(np.arange(512, dtype=np.int64), 1024)
+    b = np.tile(np.arange(512, 1536, dtype=np.int64), 512)
+    csr = csr_from_edges(1536, a, b, None, symmetric=True)
+    np.testing.assert_allclose(gpu_run(ctx, _G(csr, False), "PR", damping=0.85, iters=5),
+                               O.pagerank(csr, False, 0.85, 5), rtol=PR_RTOL, atol=0)
 
 
 def test_pagerank_escape_groups(ctx, monkeypatch):
