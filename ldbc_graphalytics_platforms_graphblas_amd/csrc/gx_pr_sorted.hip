@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <functional>
 #include <queue>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -83,6 +84,7 @@ struct SortedArgs {
     const uint16_t *npk;     // narrow codes
     const uint32_t *nbase;   // per narrow supergroup: the column before its first code
     uint32_t null_sg;        // all-padding supergroup (base = zero_col)
+    uint32_t nt_col;         // CP bit 2: narrow supergroups from this column on gathered non-temporally
     double *xd;              // x of the rows past `live` (store_x, gx_pr.h)
     int64_t live;
 };
@@ -201,7 +203,7 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // 1 no LDS adds (register sum), 2 no gathers, 3 neither, 4 gathers folded into x[c & 4095]
 // (L1 hits), 5 no gathers + conflict-free LDS adds (acc[tid]), 6 gathers + conflict-free LDS
 // adds, 7 no index loads (entries synthesised from the position, columns = the base).
-template <int PROBE, int CP>   // CP bit 0: index loads non-temporal
+template <int PROBE, int CP>   // CP bit 0: index loads non-temporal (bit 2: gather_narrow)
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
                                              double *acc, int64_t step64) {
     const int tid = threadIdx.x;
@@ -358,8 +360,8 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
 // The narrow prefix of a block: 2-byte codes (delta << 14) | row, delta = the column step from
 // the previous code (0..3; a larger step is split by filler codes of step 3 whose rows are
 // junk accumulators >= kJunkRow).  A narrow supergroup of 512 codes is one wave-load of 16 B
-// per lane: lane l decodes codes 8l .. 8l+7, their columns are the supergroup's base plus the
-// lane's exclusive wave scan of delta sums plus its own running sum.  Round i of the unit is
+// per lane (lane l: codes l + 64 k, stored lane-major), decoded by two packed DPP scans (issue
+// below).  Round i of the unit is
 // the workgroup's 16 supergroups (j + i k) * 16 + wave; a supergroup past the block reads the
 // null supergroup (padding codes, base = x's zero slot), so the loop has no range checks.
 // Same pipeline as gather_units: round i+1's gathers issue before round i's LDS adds, the
@@ -391,21 +393,40 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
         d.q = (CP & 1) ? __builtin_nontemporal_load(qa) : *qa;
         d.base = a.nbase[g];
     };
+    // Lane l holds the codes of entries l + 64 k (k < 8) of the supergroup, so instruction k
+    // gathers 64 consecutive sorted entries (3x fewer distinct lines per instruction than 8
+    // consecutive entries per lane on SYN-8_5).  The eight lane scans run packed, four 8-bit
+    // fields per register (a field's sum is at most 64 x 3), in two DPP scans; entry 64 k + l
+    // sits at base + (the column steps of instructions < k) + field k of the scan.
     auto issue = [&](const Rd &d, Gt &t) {
         const uint32_t w[4] = {d.q.x, d.q.y, d.q.z, d.q.w};
-        uint32_t pre[kU];
-        uint32_t run = 0;
+        uint32_t pk[2] = {0u, 0u};
 #pragma unroll
         for (int k = 0; k < kU; k++) {
             const uint32_t c = (k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu);
-            run += c >> kRowBits;
-            pre[k] = run;
+            pk[k >> 2] |= (c >> kRowBits) << (8 * (k & 3));
             t.r[k] = c & ((1u << kRowBits) - 1);
             asm volatile("" : "+v"(t.r[k]));
         }
-        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.base) + (wave_scan_incl(run) - run);
+        const uint32_t s0 = wave_scan_incl(pk[0]), s1 = wave_scan_incl(pk[1]);
+        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)s0, kWave - 1);
+        const uint32_t t1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, kWave - 1);
+        uint32_t bk = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.base);
+        const uint32_t b0 = bk;
+        uint32_t col[kU];
 #pragma unroll
-        for (int k = 0; k < kU; k++) t.g[k] = *reinterpret_cast<const double *>(xb + ((b + pre[k]) << 3));
+        for (int k = 0; k < kU; k++) {
+            const uint32_t sk = k < 4 ? s0 : s1, tk = k < 4 ? t0 : t1;
+            col[k] = bk + ((sk >> (8 * (k & 3))) & 255u);
+            bk += (tk >> (8 * (k & 3))) & 255u;
+        }
+        if ((CP & 4) && b0 >= a.nt_col) {   // past the hub lines: streamed (GX_PR_CP bit 2)
+#pragma unroll
+            for (int k = 0; k < kU; k++) t.g[k] = __builtin_nontemporal_load(reinterpret_cast<const double *>(xb + (col[k] << 3)));
+        } else {
+#pragma unroll
+            for (int k = 0; k < kU; k++) t.g[k] = *reinterpret_cast<const double *>(xb + (col[k] << 3));
+        }
     };
     auto add = [&](const Gt &t) {
 #pragma unroll
@@ -792,8 +813,9 @@ __global__ __launch_bounds__(256) void k_narrow_emit(const RowBlock *__restrict_
             n += e < N ? fl[j] + 1 : 0u;
         }
         int64_t pos = nb + noff[b.seg + g] + (wave_scan_incl(n) - n);   // absolute code index
+        // stored lane-major inside the 512-code supergroup: code e of it at (e mod 64) * 8 + e / 64
         auto put = [&](uint32_t step, uint32_t row, uint32_t col_after) {
-            npk[pos] = (uint16_t)((step << kRowBits) | row);
+            npk[(pos & ~(int64_t)(kNSg - 1)) + (pos & (kWave - 1)) * 8 + ((pos >> 6) & 7)] = (uint16_t)((step << kRowBits) | row);
             const int64_t rel = pos - nb + 1;   // codes of the block up to and including this one
             if ((rel & (kNSg - 1)) == 0 && rel < C) nbase[(pos + 1) / kNSg] = col_after;
             pos++;
@@ -806,7 +828,7 @@ __global__ __launch_bounds__(256) void k_narrow_emit(const RowBlock *__restrict_
             uint32_t at = c - st[j];
             for (uint32_t f = 0; f < fl[j]; f++) {
                 at += 3;
-                put(3u, (uint32_t)(kJunkRow + ((pos >> 3) & (kWave - 1))), at);
+                put(3u, (uint32_t)(kJunkRow + (pos & (kWave - 1))), at);   // the lane's own junk row
             }
             put(c - at, spk[z0 + e] & ((1u << kRowBits) - 1), c);
         }
@@ -885,11 +907,17 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
     const int64_t B = env_int("GX_PR_BLOCK_NNZ", (int)bdef, 1024, 1 << 30);
     p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)std::max<int64_t>(B / 4, kRound), 1024, 1 << 30);
     p->sorted_nnz = (int)B;
-    // The index stream is read once per launch.  Loaded non-temporally it leaves the XCD's L2 to
-    // x's lines: SYN-8_5 (67 MB of x) 898 -> 871-877 us per launch, SYN-7_5 (8 MB, which the L2s
-    // mostly hold anyway) 83 -> 91 (round 3, tools/r03_cp_ab.sh).  GX_PR_CP=0/1 overrides.
+    // Cache policy (round 3, tools/r03_cp_ab.sh, r03_ntx_ab.sh, r03_lanemajor.sh), when x is far
+    // larger than the L2s: the index stream, read once per launch, loaded non-temporally
+    // (bit 0: SYN-8_5, 67 MB of x, 898 -> 871-877 us per launch), and so are the gathers of the
+    // narrow supergroups from column nt_col = 64 Ki on (bit 2: 780 -> 757-760 us), so the XCD's
+    // L2 keeps the hub lines.  Wide (sparse tail) gathers stay cached: non-temporal they ran
+    // 965 us.  SYN-7_5 (8 MB of x) keeps plain loads everywhere: 83 -> 91 us with bit 0, 72.5 ->
+    // 79.6 with bit 2.  GX_PR_CP = 0 / 1 / 5 and GX_PR_NT_COL override.
     const uint64_t xbytes = (uint64_t)p->chunk * (uint64_t)std::max(1, p->nranks) * sizeof(double);
-    p->idx_nt = env_int("GX_PR_CP", xbytes >= (48ull << 20) ? 1 : 0, 0, 1);
+    p->cache_policy = env_int("GX_PR_CP", xbytes >= (48ull << 20) ? 5 : 0, 0, 5);
+    if (p->cache_policy != 0 && p->cache_policy != 1) p->cache_policy = 5;
+    p->nt_col = (uint32_t)env_int("GX_PR_NT_COL", 65536, 0, 1 << 30);
     PlanClock clk("sorted", p->ctx->stream);
     const int64_t R = p->sorted_rows, LT = std::max<int64_t>(p->long_nnz, 1);
     std::vector<RowBlock> longb, sortb;
@@ -1108,15 +1136,27 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
             double best = 0.0;
             const int64_t emax = *std::max_element(ents.begin(), ents.end());
             // candidates: every round up to 64 rounds, then 4 % apart (the makespan curve is
-            // flat there; every round up to emax cost ~16 ms of host time on SYN-8_5)
+            // flat there; every round up to emax cost ~16 ms of host time on SYN-8_5), simulated
+            // on up to 8 host threads (13 ms on one thread for SYN-8_5), then scanned in order
+            std::vector<int64_t> cand;
             for (int64_t t = kRound; t <= std::max<int64_t>(kRound, emax);
-                 t = t < 64 * kRound ? t + kRound : (t + t / 25 + kRound - 1) / kRound * kRound) {
-                const double ms = pr_unit_makespan(ents, rws, lsegs, t, (int)cus);
-                if (T == 0 || ms < best * 0.999) {
-                    best = ms;
-                    T = t;
+                 t = t < 64 * kRound ? t + kRound : (t + t / 25 + kRound - 1) / kRound * kRound)
+                cand.push_back(t);
+            std::vector<double> span(cand.size());
+            const int nth = (int)std::max<size_t>(1, std::min<size_t>({8, cand.size(),
+                                                                       (size_t)std::max(1u, std::thread::hardware_concurrency())}));
+            std::vector<std::thread> th;
+            for (int w = 0; w < nth; w++)
+                th.emplace_back([&, w]() {
+                    for (size_t i = (size_t)w; i < cand.size(); i += (size_t)nth)
+                        span[i] = pr_unit_makespan(ents, rws, lsegs, cand[i], (int)cus);
+                });
+            for (auto &x : th) x.join();
+            for (size_t i = 0; i < cand.size(); i++)
+                if (T == 0 || span[i] < best * 0.999) {
+                    best = span[i];
+                    T = cand[i];
                 }
-            }
             if (env_int("GX_PR_VERBOSE", 0, 0, 1))
                 std::fprintf(stderr, "[gx_pr] unit size %lld: simulated launch %.1f us\n", (long long)T, best);
         }
@@ -1245,6 +1285,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.npk = p->npk.p;
     a.nbase = p->nbase.p;
     a.null_sg = p->null_sg;
+    a.nt_col = p->nt_col;
     const char *times_path = std::getenv("GX_PR_UNIT_TIMES");   // debug: not under graph capture
     const uint32_t nw = p->nlong_pad + p->nunits;
     if (times_path && nw) {
@@ -1271,7 +1312,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                 }
             } else
 #endif
-            if (p->idx_nt) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1>), dim3(nw), dim3(kBS), lds, s, a);
+            if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5>), dim3(nw), dim3(kBS), lds, s, a);
+            else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1>), dim3(nw), dim3(kBS), lds, s, a);
             else hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
         }
         if (a.utimes && ++p->utimes_launch == env_int("GX_PR_UNIT_TIMES_LAUNCH", 5, 1, 1 << 30)) {
