@@ -166,13 +166,24 @@ struct PrPart {
     DBuf<int32_t> perm;        // old vertex id -> position in the hub-first order
 };
 
+// Read-only host array (a std::vector, or a buffer the plan filled without zeroing it).
+template <typename T>
+struct HostView {
+    const T *p = nullptr;
+    size_t n = 0;
+    HostView(const std::vector<T> &v) : p(v.data()), n(v.size()) {}
+    HostView(const T *ptr, size_t count) : p(ptr), n(count) {}
+    size_t size() const { return n; }
+    const T &operator[](size_t i) const { return p[i]; }
+};
+
 // Build the row-block plan and dangling list from a local pull CSR (host row pointers
 // h_rp, device rp/ci) and device out-degrees.  Borrowed device pointers must outlive it.
-int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp,
-            const int32_t *d_ci, const int32_t *d_outdeg, const std::vector<int32_t> &h_outdeg);
+int pr_plan(PrPart *p, HostView<int64_t> h_rp, const int64_t *d_rp,
+            const int32_t *d_ci, const int32_t *d_outdeg, HostView<int32_t> h_outdeg);
 
 // Column-sorted block plan (k_pr_pull_units) and its iteration (gx_pr_sorted.hip).
-int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vector<int32_t> &h_outdeg);
+int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg);
 int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 // Dangling-score sum of this rank into x_local's last chunk slot.
 int pr_dangling(PrPart *p, double *x_local, hipStream_t s);

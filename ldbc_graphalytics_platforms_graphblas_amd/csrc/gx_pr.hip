@@ -300,8 +300,8 @@ __global__ void k_pr_init(const int32_t *__restrict__ outdeg, int64_t rows, doub
 
 }  // namespace
 
-int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, const int32_t *d_ci,
-            const int32_t *d_outdeg, const std::vector<int32_t> &h_outdeg) {
+int pr_plan(PrPart *p, HostView<int64_t> h_rp, const int64_t *d_rp, const int32_t *d_ci,
+            const int32_t *d_outdeg, HostView<int32_t> h_outdeg) {
     const int64_t rows = (int64_t)h_rp.size() - 1;
     p->rows = (uint64_t)rows;
     if (p->live > p->rows) p->live = p->rows;   // no live prefix given: all rows
@@ -377,12 +377,27 @@ int pr_plan(PrPart *p, const std::vector<int64_t> &h_rp, const int64_t *d_rp, co
     }
     // dangling rows: one contiguous range (hub-first orders put them last), or a list
     int64_t nd = 0, dfirst = -1, dlast = -1;
-    for (int64_t i = 0; i < rows; i++)
-        if (h_outdeg[i] == 0) {
-            nd++;
-            if (dfirst < 0) dfirst = i;
-            dlast = i;
+    if (p->src_order) {
+        // gx_pagerank's hub-first rows: out-degrees non-increasing, the dangling rows a suffix
+        int64_t lo = 0, hi = rows;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (h_outdeg[mid] == 0) hi = mid;
+            else lo = mid + 1;
         }
+        nd = rows - lo;
+        if (nd > 0) {
+            dfirst = lo;
+            dlast = rows - 1;
+        }
+    } else {
+        for (int64_t i = 0; i < rows; i++)
+            if (h_outdeg[i] == 0) {
+                nd++;
+                if (dfirst < 0) dfirst = i;
+                dlast = i;
+            }
+    }
     p->nd = (uint64_t)nd;
     p->d_range = nd > 0 && dlast - dfirst + 1 == nd;
     p->d0 = nd > 0 ? dfirst : 0;
@@ -660,16 +675,18 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
         GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries are freed at the end of the block
     }
     clk.mark("hub order + row pointers (device)");
-    std::vector<int64_t> nrp(n + 1);
-    std::vector<int32_t> nout(n);
-    GX_TRY(download(ctx, nrp.data(), p->rp_own.p, n + 1, Xfer::Raw64));
-    GX_TRY(download(ctx, nout.data(), p->outdeg_own.p, n, Xfer::Raw32));
+    // not value-initialised: zeroing 12 n bytes on one thread cost more than the transfer
+    std::unique_ptr<int64_t[]> nrp(new int64_t[n + 1]);
+    std::unique_ptr<int32_t[]> nout(new int32_t[n]);
+    GX_TRY(download(ctx, nrp.get(), p->rp_own.p, n + 1, Xfer::Raw64));
+    GX_TRY(download(ctx, nout.get(), p->outdeg_own.p, n, Xfer::Raw32));
     clk.mark("row pointers to the host");
     p->src_rp = P.rp.p;
     p->src_ci = P.ci.p;
     p->src_order = p->order.p;
     p->src_perm = p->perm.p;
-    GX_TRY(pr_plan(p.get(), nrp, p->rp_own.p, nullptr, p->outdeg_own.p, nout));
+    GX_TRY(pr_plan(p.get(), HostView<int64_t>(nrp.get(), n + 1), p->rp_own.p, nullptr, p->outdeg_own.p,
+                   HostView<int32_t>(nout.get(), n)));
     GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors above die at return
     clk.mark("pr_plan");
     *out = p.release();

@@ -98,6 +98,35 @@ __device__ __forceinline__ double sorted_epilogue(const SortedArgs &a, int64_t r
     return deg > 0 ? 0.0 : r;
 }
 
+// The epilogue of rows [r0, r0 + nrows) of a block, thread tid taking rows tid, tid + kBS, ...:
+// eight out-degree loads issued before any store, since the compiler cannot move a load of
+// outdeg above a store to x_out (they might alias) and the row-by-row loop paid one memory
+// latency per row a thread handles (16 for SYN-8_5's 16 320-row blocks).  acc null: sums 0.
+// Returns the thread's dangling-score sum.
+__device__ __forceinline__ double epilogue_rows(const SortedArgs &a, int64_t r0, int nrows, const double *acc,
+                                                double teleport) {
+    constexpr int kB = 8;
+    double d = 0.0;
+    for (int i0 = threadIdx.x; i0 < nrows; i0 += kB * kBS) {
+        int32_t deg[kB];
+#pragma unroll
+        for (int q = 0; q < kB; q++) {
+            const int i = i0 + q * kBS;
+            deg[q] = i < nrows ? a.outdeg[r0 + i] : 1;
+        }
+#pragma unroll
+        for (int q = 0; q < kB; q++) {
+            const int i = i0 + q * kBS;
+            if (i >= nrows) break;
+            const double r = teleport + (acc ? acc[i] : 0.0);
+            if (a.rank_out) a.rank_out[r0 + i] = r;
+            store_x(a.x_out, a.xd, a.live, r0 + i, deg[q] > 0 ? r / ((double)deg[q] / a.damping) : r);
+            if (deg[q] == 0) d += r;
+        }
+    }
+    return d;
+}
+
 // Fused dangling sum: the block's dangling scores d (one value per thread) are reduced, the
 // block publishes its partial in its slot (agent scope) and takes a ticket; the last of the
 // ndblocks participants adds the partials up with the whole workgroup (thread t takes slots
@@ -549,9 +578,9 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
     }
     double d = 0.0;
     if (empty)
-        for (int i = tid; i < nrows; i += kBS) d += sorted_epilogue(a, b.row_begin + i, 0.0, teleport);
+        d = epilogue_rows(a, b.row_begin, nrows, nullptr, teleport);
     else
-        for (int i = tid; i < nrows; i += kBS) d += sorted_epilogue(a, b.row_begin + i, acc[i], teleport);
+        d = epilogue_rows(a, b.row_begin, nrows, acc, teleport);
     if (a.dslot) {
         const int32_t slot = a.dslot[u.blk];
         if (slot >= 0) dangling_publish(a, slot, d, wred, &last);
@@ -722,7 +751,8 @@ __global__ __launch_bounds__(256) void k_narrow_cost(const RowBlock *__restrict_
 // sum_{g<P} (n_g - D_g) (0 when `enable` is off), the code offset of every supergroup inside
 // the block's narrow run (exclusive prefix of n_g + D_g), and the block's code count.
 __global__ __launch_bounds__(1024) void k_narrow_split(const RowBlock *__restrict__ blocks, const uint32_t *__restrict__ fill,
-                                                       int enable, uint32_t *__restrict__ nsplit, uint32_t *__restrict__ ncode,
+                                                       int enable, int64_t min_entries, uint32_t *__restrict__ nsplit,
+                                                       uint32_t *__restrict__ ncode,
                                                        uint32_t *__restrict__ noff) {
     __shared__ int64_t sben[1024], scod[1024];
     __shared__ int64_t bestv[1024];
@@ -774,7 +804,7 @@ __global__ __launch_bounds__(1024) void k_narrow_split(const RowBlock *__restric
         __syncthreads();
     }
     if (t == 0) {
-        const int32_t P = enable ? besti[0] : 0;
+        const int32_t P = (enable && N >= min_entries) ? besti[0] : 0;
         nsplit[blockIdx.x] = (uint32_t)P;
         // codes of the prefix: the offset of supergroup P, or all of them
         ncode[blockIdx.x] = P == 0 ? 0u : (uint32_t)(P < ng ? noff[b.seg + P] : (uint32_t)scod[1023]);
@@ -881,7 +911,7 @@ double pr_unit_makespan(const std::vector<int64_t> &ents, const std::vector<int6
 // Plan: rows longer than long_nnz -> LONG segment blocks (longest first); runs of the other
 // rows with entries -> blocks of <= block_nnz entries and <= sorted_rows rows, entries sorted
 // by column and cut into units; the trailing rows without entries -> row-range workgroups.
-int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vector<int32_t> &h_outdeg) {
+int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg) {
     const int64_t rows = (int64_t)h_rp.size() - 1;
     const uint64_t nnz = (uint64_t)h_rp[rows];
     const int64_t cus = std::max(1, p->ctx->num_cus);
@@ -1077,7 +1107,8 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
             hipLaunchKernelGGL(k_narrow_cost, dim3(64, nsb), dim3(256), 0, s, d_sort, p->sci.p, d_fill.p);
             GX_TRY(check_launch("k_narrow_cost"));
             hipLaunchKernelGGL(k_narrow_split, dim3(nsb), dim3(1024), 0, s, d_sort, d_fill.p,
-                               env_int("GX_PR_NARROW", 1, 0, 1), d_nsplit.p, d_ncode.p, d_noff.p);
+                               env_int("GX_PR_NARROW", 1, 0, 1), (int64_t)env_int("GX_PR_NARROW_MIN", 0, 0, 1 << 30),
+                               d_nsplit.p, d_ncode.p, d_noff.p);
             GX_TRY(check_launch("k_narrow_split"));
             GX_HIP_TRY(hipMemcpyAsync(h_nsplit.data(), d_nsplit.p, nsb * 4, hipMemcpyDeviceToHost, s));
             GX_HIP_TRY(hipMemcpyAsync(h_ncode.data(), d_ncode.p, nsb * 4, hipMemcpyDeviceToHost, s));
@@ -1194,10 +1225,11 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         // big units start in the first wave and the small ones fill the gaps at the end.  Cost ~
         // entries + 4 per row (zeroing, epilogue).  Ties keep block order, so a block's units
         // stay adjacent.
+        const int64_t rowc = env_int("GX_PR_ROW_COST", 4, 0, 1024);
         auto cost = [&](const SortedUnit &u) {
             const RowBlock &b = sortb[u.blk - longb.size()];
             const int64_t E = b.nz_end - b.nz_begin, R = b.row_end - b.row_begin;
-            return (E + u.nunits - 1) / u.nunits + 4 * R;
+            return (E + u.nunits - 1) / u.nunits + rowc * R;
         };
         std::stable_sort(units.begin(), units.end(),
                          [&](const SortedUnit &x, const SortedUnit &y) { return cost(x) > cost(y); });
@@ -1229,7 +1261,10 @@ int pr_plan_sorted(PrPart *p, const std::vector<int64_t> &h_rp, const std::vecto
         uint32_t nd = 0;
         for (size_t i = longb.size(); i < all.size(); i++) {
             bool any = false;
-            for (int32_t r2 = all[i].row_begin; r2 < all[i].row_end && !any; r2++) any = h_outdeg[r2] == 0;
+            if (p->d_range)   // the dangling rows are [d0, d0 + nd)
+                any = p->nd > 0 && all[i].row_begin < p->d0 + (int64_t)p->nd && all[i].row_end > p->d0;
+            else
+                for (int32_t r2 = all[i].row_begin; r2 < all[i].row_end && !any; r2++) any = h_outdeg[r2] == 0;
             if (any) slot[i] = (int32_t)nd++;
         }
         p->fused_dangling = p->nd > 0 && nd > 0 && !long_dangling;
@@ -1338,6 +1373,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                     } else {
                         const SortedUnit &u = us[w - p->nlong_pad];
                         for (int64_t k0 = u.lo; k0 < u.hi; k0 += u.step) ents += std::min<int64_t>(u.step / u.nunits, u.hi - k0);
+                        for (int64_t r = u.unit; r * 16 < u.nsg; r += u.nunits)   // narrow codes (fillers included)
+                            ents += std::min<int64_t>(16, u.nsg - r * 16) * kNSg;
                         blk = u.blk;
                         unit = u.unit;
                         nunits = u.nunits;

@@ -7,7 +7,7 @@ set -o pipefail
 OUT=$1; G=$2; shift 2
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-env "$@" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${G}_trace" -o trace -- \
+env "$@" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${G}_trace" -o trace -- \
     python3 bench.py --graph "$G" --steps 10 --warmup 2 --no-cpu-baseline --no-secondary > "$OUT/${G}_trace.json" 2> "$OUT/${G}_trace.err" || exit 1
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
