@@ -70,7 +70,9 @@ struct SortedUnit {
     int32_t part;       // ticket index of a multi-unit block, -1 when nunits == 1
     int32_t unit;       // this unit's number within the block
     int32_t nunits;
-    int32_t pad;
+    int32_t seg;        // the block's fields (RowBlock), so a workgroup's first loads are
+    int64_t z0, z1;     //   independent: its block's entries [z0, z1), rows [r0, r1), first
+    int32_t r0, r1;     //   supergroup seg
 };
 
 // x of local row `row`: rows [0, live) sit in the exchanged chunk, the rest (out-degree 0, so

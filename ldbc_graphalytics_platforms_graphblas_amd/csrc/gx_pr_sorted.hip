@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
         return;
     }
     const SortedUnit u = a.units[w - a.nlong_pad];
-    const RowBlock b = a.blocks[u.blk];
+    const RowBlock b = {u.z0, u.z1, u.r0, u.r1, -1, u.seg};
     const int nrows = b.row_end - b.row_begin;
     // a block without entries (the isolated vertices a hub-first undirected graph puts last):
     // r = teleport, no accumulators, no gathers
@@ -1209,7 +1209,11 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                 u.slab = k > 1 ? slab : 0;
                 u.nbeg = h_nbeg[i];
                 u.nsg = (int32_t)(((int64_t)h_ncode[i] + kNSg - 1) / kNSg);
-                u.pad = 0;
+                u.seg = b.seg;
+                u.z0 = b.nz_begin;
+                u.z1 = b.nz_end;
+                u.r0 = b.row_begin;
+                u.r1 = b.row_end;
                 u.blk = (int32_t)(longb.size() + i);
                 u.part = k > 1 ? parts : -1;
                 u.unit = j;
