@@ -106,7 +106,7 @@ class _NpSsspSplit:
         self.be, self.v0, self.v1 = be, v0, v1
         w = be.w
         mean_deg = max(1.0, len(be.ci) / max(1, be.n))
-        self.delta = 4.0 * float(w.mean() if len(w) else 1.0) / mean_deg
+        self.delta = 3.0 * float(w.mean() if len(w) else 1.0) / mean_deg
         own = (be.ci >= v0) & (be.ci < v1)
         self.light = [[] for _ in range(be.n)]
         self.heavy = [[] for _ in range(be.n)]
