@@ -144,7 +144,7 @@ struct PrPart {
     int long_nnz = 65536;        // longer rows take the LONG segment path
     int sorted_lds = 0;          // dynamic LDS bytes of the launch
     int cache_policy = 0;        // k_pr_pull_units CP: 1 index stream non-temporal, 5 also the narrow
-                                 // gathers from column nt_col on (x far larger than the L2s)
+                                 // gathers from column nt_col on (x larger than the L2s)
     uint32_t nt_col = 65536;
     uint32_t nsorted = 0, nlong_pad = 0;
     // dangling-score sum fused into the kernel: blocks holding out-degree-0 rows publish a

@@ -881,14 +881,14 @@ int env_int(const char *name, int dflt, int lo, int hi) {
 // (zeroing, epilogue, slab store), ~1.5 us fixed, and the last arriver's slab reads.  It
 // picks the unit size on large graphs, so that the units of the large blocks land in as few
 // waves as the CUs allow.
-double pr_unit_makespan(const std::vector<int64_t> &ents, const std::vector<int64_t> &rws,
+double pr_unit_makespan(const std::vector<int64_t> &ents, const std::vector<int64_t> &effs, const std::vector<int64_t> &rws,
                         const std::vector<int64_t> &lsegs, int64_t t, int cus) {
     constexpr double kRate = 2900.0, kRow = 0.002, kFixed = 1.5, kSlab = 0.0005;
     std::vector<double> cost;
     for (size_t i = 0; i < ents.size(); i++) {
         const int64_t E = ents[i];
         const int64_t k = std::max<int64_t>(1, std::min((E + kRound - 1) / kRound, (E + t - 1) / t));
-        const double c = (double)E / (double)k / kRate + kRow * (double)rws[i] + kFixed +
+        const double c = (double)effs[i] / (double)k / kRate + kRow * (double)rws[i] + kFixed +
                          (k > 1 ? kSlab * (double)rws[i] * (double)k : 0.0);
         for (int64_t j = 0; j < k; j++) cost.push_back(c);
     }
@@ -937,15 +937,16 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     const int64_t B = env_int("GX_PR_BLOCK_NNZ", (int)bdef, 1024, 1 << 30);
     p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)std::max<int64_t>(B / 4, kRound), 1024, 1 << 30);
     p->sorted_nnz = (int)B;
-    // Cache policy (round 3, tools/r03_cp_ab.sh, r03_ntx_ab.sh, r03_lanemajor.sh), when x is far
-    // larger than the L2s: the index stream, read once per launch, loaded non-temporally
+    // Cache policy (round 3, tools/r03_cp_ab.sh, r03_ntx_ab.sh, r03_lanemajor.sh), when x is
+    // larger than the 32 MiB of all eight L2s (the exchanged chunks: SYN-8_5's live rows are
+    // 44.6 MB): the index stream, read once per launch, loaded non-temporally
     // (bit 0: SYN-8_5, 67 MB of x, 898 -> 871-877 us per launch), and so are the gathers of the
     // narrow supergroups from column nt_col = 64 Ki on (bit 2: 780 -> 757-760 us), so the XCD's
     // L2 keeps the hub lines.  Wide (sparse tail) gathers stay cached: non-temporal they ran
     // 965 us.  SYN-7_5 (8 MB of x) keeps plain loads everywhere: 83 -> 91 us with bit 0, 72.5 ->
     // 79.6 with bit 2.  GX_PR_CP = 0 / 1 / 5 and GX_PR_NT_COL override.
     const uint64_t xbytes = (uint64_t)p->chunk * (uint64_t)std::max(1, p->nranks) * sizeof(double);
-    p->cache_policy = env_int("GX_PR_CP", xbytes >= (48ull << 20) ? 5 : 0, 0, 5);
+    p->cache_policy = env_int("GX_PR_CP", xbytes >= (32ull << 20) ? 5 : 0, 0, 5);
     if (p->cache_policy != 0 && p->cache_policy != 1) p->cache_policy = 5;
     p->nt_col = (uint32_t)env_int("GX_PR_NT_COL", 65536, 0, 1 << 30);
     PlanClock clk("sorted", p->ctx->stream);
@@ -1147,6 +1148,16 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // units of the split blocks: ceil(entries / T) per sorted block (at most one per round)
     int64_t T = 0;
     p->nunits = 0;
+    // the cost of a block's entries in the unit order and the launch simulation: narrow ones 1,
+    // wide (sparse-tail) ones GX_PR_WIDE_COST / 4 each, since their x lines are shared by fewer
+    // entries.  3 on large graphs (SYN-8_5 757-764 -> 755-756 us per launch, tools/r03_wc_ab.sh;
+    // the sparse tail units no longer finish last), 1 otherwise (SYN-7_5: no change)
+    const int64_t wide_cost4 = env_int("GX_PR_WIDE_COST", huge ? 12 : 4, 4, 64);
+    auto eff_entries = [&](int64_t i) -> int64_t {
+        const int64_t E = sortb[i].nz_end - sortb[i].nz_begin;
+        const int64_t En = std::min<int64_t>(E, 256 * (int64_t)h_nsplit[i]);
+        return En + (E - En) * wide_cost4 / 4;
+    };
     if (!sortb.empty()) {
         if (std::getenv("GX_PR_UNIT_NNZ")) {
             T = env_int("GX_PR_UNIT_NNZ", 65536, 1024, 1 << 30);
@@ -1158,9 +1169,10 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         } else {
             // the unit size whose simulated launch is shortest, over multiples of a round
             // (sampled coarsely past 256 rounds: the curve is flat there)
-            std::vector<int64_t> ents, rws, lsegs;
+            std::vector<int64_t> ents, effs, rws, lsegs;
             for (const RowBlock &b : sortb) {
                 ents.push_back(b.nz_end - b.nz_begin);
+                effs.push_back(eff_entries(&b - sortb.data()));
                 rws.push_back(b.row_end - b.row_begin);
             }
             for (const RowBlock &b : longb) lsegs.push_back(b.nz_end - b.nz_begin);
@@ -1180,7 +1192,7 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
             for (int w = 0; w < nth; w++)
                 th.emplace_back([&, w]() {
                     for (size_t i = (size_t)w; i < cand.size(); i += (size_t)nth)
-                        span[i] = pr_unit_makespan(ents, rws, lsegs, cand[i], (int)cus);
+                        span[i] = pr_unit_makespan(ents, effs, rws, lsegs, cand[i], (int)cus);
                 });
             for (auto &x : th) x.join();
             for (size_t i = 0; i < cand.size(); i++)
@@ -1233,7 +1245,8 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         auto cost = [&](const SortedUnit &u) {
             const RowBlock &b = sortb[u.blk - longb.size()];
             const int64_t E = b.nz_end - b.nz_begin, R = b.row_end - b.row_begin;
-            return (E + u.nunits - 1) / u.nunits + rowc * R;
+            (void)E;
+            return (eff_entries(u.blk - (int32_t)longb.size()) + u.nunits - 1) / u.nunits + rowc * R;
         };
         std::stable_sort(units.begin(), units.end(),
                          [&](const SortedUnit &x, const SortedUnit &y) { return cost(x) > cost(y); });
