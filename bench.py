@@ -684,7 +684,9 @@ def main():
                          "ms_per_step": m2["elapsed"] * 1e3 / args.steps,
                          "mean_launch_us": m2["mean_launch_s"] * 1e6, "bytes_per_launch": m2["bytes_per_launch"],
                          "roofline_frac": m2["achieved"] / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(pr_workload("SYN-7_5"))}
+                         "traffic": pmc_traffic(pr_workload("SYN-7_5")),
+                         # bin/exe/pr's processing time on this graph too
+                         "processing": exe_path_pr(csr2, args, ctx)[0]}
 
     if rank == 0:
         achieved = m["achieved"]
