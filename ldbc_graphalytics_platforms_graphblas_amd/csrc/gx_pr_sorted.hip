@@ -606,6 +606,7 @@ struct KeySrc {
     const int32_t *seg_row;     // nseg + 1 segment row starts
     int32_t nseg;
     int colbits;
+    int32_t segmask;            // segment bits kept in the key (its sort group's share)
 };
 
 // One wave per 64-entry slab of the plan's rows, lane = entry (coalesced key / row writes and
@@ -632,7 +633,7 @@ __global__ __launch_bounds__(256) void k_sorted_keys(KeySrc k, int64_t nnz, cons
             const int64_t v = k.order ? k.order[i] : i;
             const int32_t c0 = k.sci[k.srp[v] + (e - k.rp[i])];
             const uint32_t c = (uint32_t)(k.perm ? k.perm[c0] : c0);
-            keys[e] = ((K)lo << k.colbits) | (K)c;
+            keys[e] = ((K)(lo & k.segmask) << k.colbits) | (K)c;
             vals[e] = (uint16_t)(i - k.seg_row[lo]);
         }
     }
@@ -1055,8 +1056,14 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         GX_TRY(d_segd.alloc(segd.size()));
         GX_HIP_TRY(hipMemcpyAsync(d_seg_row.p, seg_row.data(), seg_row.size() * 4, hipMemcpyHostToDevice, s));
         GX_HIP_TRY(hipMemcpyAsync(d_segd.p, segd.data(), segd.size() * sizeof(SegDesc), hipMemcpyHostToDevice, s));
+        // 4-byte keys whenever the columns leave room: segments are contiguous entry ranges, so
+        // groups of 2^(32 - colbits) of them sort independently with the segment's low bits in
+        // the key (SYN-8_5: 556 segments x 2^23 columns = 33 bits, two groups of 32-bit keys
+        // instead of one sort of 64-bit keys)
+        const bool narrow = colbits <= 31 && !env_int("GX_PR_WIDE_KEYS", 0, 0, 1);
+        const int gbits = narrow ? std::min({segbits, 32 - colbits, env_int("GX_PR_SORT_GROUP_BITS", 32, 1, 32)}) : segbits;
         const KeySrc ks{p->rp, rows, p->src_rp, p->src_ci, p->src_order, p->src_perm, d_seg_row.p,
-                        (int32_t)segd.size(), colbits};
+                        (int32_t)segd.size(), colbits, (int32_t)((1ll << gbits) - 1)};
         const int64_t nslabs = (int64_t)((nnz + kWave - 1) / kWave);
         DBuf<int64_t> srow;
         GX_TRY(srow.alloc(nslabs + 1));
@@ -1066,7 +1073,6 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         const unsigned pgrid = grid_for(nnz, 256, 1u << 20);
         const uint32_t colmask = (uint32_t)((1ull << colbits) - 1);
         // keys and values in the kept plan scratch: [k0 | k1 | v0 | v1]
-        const bool narrow = segbits + colbits <= 32;   // 4-byte keys: fewer radix passes, half the key bytes
         const size_t kb = narrow ? 4 : 8, align = 256;
         auto up = [&](size_t x) { return (x + align - 1) / align * align; };
         const size_t kbytes = up((size_t)nnz * kb), vbytes = up((size_t)nnz * 2);
@@ -1080,7 +1086,12 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                                v0);
             GX_TRY(check_launch("k_sorted_keys"));
             clk.mark("keys");
-            GX_TRY(sort_pairs_u32_u16(k0, k1, v0, v1, (size_t)nnz, segbits + colbits, s));
+            const size_t G = (size_t)1 << gbits;
+            for (size_t g0 = 0; g0 < segd.size(); g0 += G) {
+                const size_t g1 = std::min(segd.size(), g0 + G) - 1;
+                const int64_t z0 = segd[g0].z0, z1 = segd[g1].z1;
+                GX_TRY(sort_pairs_u32_u16(k0 + z0, k1 + z0, v0 + z0, v1 + z0, (size_t)(z1 - z0), gbits + colbits, s));
+            }
             clk.mark("sort");
             hipLaunchKernelGGL(k_sorted_pack<uint32_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
                                (int64_t)nnz, k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
@@ -1250,6 +1261,9 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         };
         std::stable_sort(units.begin(), units.end(),
                          [&](const SortedUnit &x, const SortedUnit &y) { return cost(x) > cost(y); });
+        // (Smallest first, or largest and smallest alternating, ran 88 and 120 us against 72 on
+        // SYN-7_5 and 1133 against 753 on SYN-8_5: a block's interleaved units must run
+        // together, tools/r03_order_ab.sh.)
         // (Co-scheduling similar units on one XCD -- slices of 32 dealt to 8 queues, grid slot
         // 8 i + q -- cut the fabric reads of SYN-8_5 by 9 % and still ran slower: 955 against
         // 925 us per launch, SYN-7_5 100 against 84; round 3)

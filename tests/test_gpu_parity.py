@@ -198,7 +198,8 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
 
 @pytest.mark.parametrize("env", [{}, {"GX_PR_LANEPERM": "0"}, {"GX_PR_BLOCK_NNZ": "2097152", "GX_PR_UNIT_NNZ": "16384"},
                                  {"GX_PR_CP": "1"}, {"GX_PR_CP": "5", "GX_PR_NT_COL": "1000"}, {"GX_PR_NARROW": "0"},
-                                 {"GX_PR_NARROW": "0", "GX_PR_CP": "5"},
+                                 {"GX_PR_NARROW": "0", "GX_PR_CP": "5"}, {"GX_PR_SORT_GROUP_BITS": "1"},
+                                 {"GX_PR_WIDE_KEYS": "1"},
                                  {"GX_PR_KERNEL": "adaptive"},
                                  {"GX_PR_SORTED_ROWS": "16384", "GX_PR_UNIT_NNZ": "16384"},
                                  {"GX_PR_SORTED_ROWS": "64"}, {"GX_PR_SORTED_ROWS": "2048"},
@@ -209,7 +210,7 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                  {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192", "GX_PR_SORTED_ROWS": "64",
                                   "GX_PR_LANEPERM": "0"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
-    """The default plan, non-temporal index loads and sparse narrow gathers (GX_PR_CP=1 / 5, the large-graph default), without the lane permutation, blocks cut into many units, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
+    """The default plan, non-temporal index loads and sparse narrow gathers (GX_PR_CP=1 / 5, the large-graph default), the plan's key sort in groups of two segments or with 64-bit keys, without the lane permutation, blocks cut into many units, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
     blocks (several workgroups per sorted block, combined through slabs by the last arriver)
     and the CSR-Adaptive kernel all give the oracle's scores (directed and undirected)."""
     for k, v in env.items():
