@@ -1378,6 +1378,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                 }
             } else
 #endif
+            // (narrow gathers three rounds deep ran the same: SYN-8_5 752-753 against 753-754
+            // us, SYN-7_5 72.1-73.2 against 71.5-72.4; tools/r03_depth_ab.sh)
             if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5>), dim3(nw), dim3(kBS), lds, s, a);
             else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1>), dim3(nw), dim3(kBS), lds, s, a);
             else hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
