@@ -390,10 +390,11 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     }
     if (n >= (1ull << 31) - 64) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: n >= 2^31");
     for (int d = 0; d < ndev; d++)
+        if (!ctxs[d]) return fail(GX_NULL_POINTER, "gx_pagerank_multi: null context");
+    for (int d = 0; d < ndev; d++)
         for (int e = 0; e < d; e++)
-            if (!ctxs[d] || ctxs[d]->device == ctxs[e]->device)
+            if (ctxs[d]->device == ctxs[e]->device)
                 return fail(GX_INVALID_VALUE, "gx_pagerank_multi: one context per distinct device");
-    if (!ctxs[0]) return fail(GX_NULL_POINTER, "gx_pagerank_multi: null context");
     const Rccl &r = rccl();
     if (!r.ok) return fail(GX_NOT_IMPLEMENTED, r.error);
     // the pull matrix: A' for a directed graph (LAGraph_Cached_AT, pr.cpp:60), A itself else

@@ -790,11 +790,21 @@ __global__ __launch_bounds__(kSB) void k_own_scatter(const int64_t *__restrict__
     }
 }
 
-__global__ __launch_bounds__(256) void k_split_sum_w(const double *__restrict__ w, int64_t m, double *sum) {
+// Per-block partial sums of the weights in a fixed order (grid-stride per thread, butterfly per
+// wave, waves in index order), so the bucket width derived from them is bitwise the same on
+// every rank that holds the same graph: the ranks' scheduling decisions must agree.
+__global__ __launch_bounds__(256) void k_split_sum_w(const double *__restrict__ w, int64_t m, double *part) {
+    __shared__ double wsum[256 / kWave];
     double acc = 0.0;
     for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < m; k += (int64_t)gridDim.x * 256) acc += w[k];
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
-    if ((threadIdx.x & (kWave - 1)) == 0) atomicAdd(sum, acc);
+    if ((threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < 256 / kWave; i++) t += wsum[i];
+        part[blockIdx.x] = t;
+    }
 }
 
 }  // namespace
@@ -904,16 +914,17 @@ static int split_build(gx_sssp_split *p, gx_graph *g) {
     // GX_SSSP_DSCALE override) -- any positive value gives the same distances
     double mean = 1.0;
     if (g->nnz) {
-        DBuf<double> sum;
-        GX_TRY(sum.alloc(1));
-        GX_HIP_TRY(hipMemsetAsync(sum.p, 0, sizeof(double), s));
-        hipLaunchKernelGGL(k_split_sum_w, dim3(grid_for(g->nnz, 256, 4096)), dim3(256), 0, s, g->A.w.p,
-                           (int64_t)g->nnz, sum.p);
+        const unsigned sgrid = grid_for(g->nnz, 256, 4096);
+        DBuf<double> part;
+        GX_TRY(part.alloc(sgrid));
+        hipLaunchKernelGGL(k_split_sum_w, dim3(sgrid), dim3(256), 0, s, g->A.w.p, (int64_t)g->nnz, part.p);
         GX_TRY(check_launch("k_split_sum_w"));
-        double h = 0.0;
-        GX_HIP_TRY(hipMemcpyAsync(&h, sum.p, sizeof(double), hipMemcpyDeviceToHost, s));
+        std::vector<double> h(sgrid);
+        GX_HIP_TRY(hipMemcpyAsync(h.data(), part.p, sgrid * sizeof(double), hipMemcpyDeviceToHost, s));
         GX_HIP_TRY(hipStreamSynchronize(s));
-        mean = h / (double)g->nnz;
+        double t = 0.0;
+        for (double x : h) t += x;   // block order: deterministic for a given graph
+        mean = t / (double)g->nnz;
     }
     double scale = g->directed ? 0.5 : 3.0, delta = 0.0;   // SYN-8_5 N = 1: 9.3-9.4 ms at 3, 9.7 at 4
     if (const char *e = std::getenv("GX_SSSP_DSCALE")) scale = std::atof(e);

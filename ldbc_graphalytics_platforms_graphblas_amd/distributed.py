@@ -297,7 +297,12 @@ def sssp(ranks: List[LocalRank], comm, n: int, src: int):
                 p.relax(pr, c)
             comm.all_gather(counts, count)
             cw = counts[0].cpu().numpy()   # identical on every rank
-            if int(cw[1]):   # done (the same flag on every rank)
+            done = cw[1::2]
+            if done.any():
+                # every rank takes the same decisions from replicated counts; a rank that stops
+                # alone would leave the others' relaxations unapplied
+                if not done.all():
+                    raise RuntimeError(f"sssp: ranks disagree on termination (done words {done.tolist()})")
                 break
             m = int(cw[0::2].max())
             if m:

@@ -60,6 +60,32 @@ def test_converter_roundtrip(tmp_path_factory, fixture_graphs):
             np.testing.assert_array_equal(back.vals, g.csr.vals)
 
 
+def test_relabel_standalone_load_graph_flags(tmp_path, fixture_graphs):
+    """relabel.py copied alone into a reference-like checkout, run with
+    the abbreviated flags load-graph.sh:51-58 passes (--input-vertex / --input-edge), gives
+    the same files as the package's restatement, for every fixture graph."""
+    import shutil
+    from ldbc_graphalytics_platforms_graphblas_amd import graphio
+    ref_py = tmp_path / "ref" / "bin" / "py"
+    ref_py.mkdir(parents=True)
+    shutil.copy(RELABEL, ref_py / "relabel.py")
+    graphs = sorted({p.stem for p in FIXTURES.glob("*.properties")})
+    assert len(graphs) == 14
+    for graph in graphs:
+        g = fixture_graphs(graph)
+        out, want = tmp_path / "out" / graph, tmp_path / "want" / graph
+        subprocess.check_call([sys.executable, str(ref_py / "relabel.py"), "--graph-name", graph,
+                               "--input-vertex", str(FIXTURES / f"{graph}.v"),
+                               "--input-edge", str(FIXTURES / f"{graph}.e"),
+                               "--output-path", str(out), "--weighted", str(g.weighted).lower(),
+                               "--directed", str(g.directed).lower()],
+                              stdout=subprocess.DEVNULL, cwd=tmp_path, env={"PATH": "/usr/bin:/bin"})
+        m, s, d_, w = graphio.relabel(FIXTURES / f"{graph}.v", FIXTURES / f"{graph}.e", g.directed, g.weighted)
+        graphio.write_vtx_mtx(want, m, s, d_, w, g.directed)
+        for f in ("graph.vtx", "graph.mtx"):
+            assert (out / f).read_text() == (want / f).read_text(), f"{graph}/{f}"
+
+
 def parse_output(path, alg):
     ids, vals = [], []
     for line in path.read_text().splitlines():

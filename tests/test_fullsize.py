@@ -1,11 +1,16 @@
-"""Full-size parity on config 4's graph (SYN-8_5: the seeded R-MAT stand-in for
-datagen-8_5-fb, scale 23, edgefactor 40, 8.4 M vertices, 628 M stored entries).
+"""Full-size parity on every BASELINE config's graph (SURVEY.md 8d stand-ins; no network for
+the real datasets):
+- config 4, SYN-8_5 (datagen-8_5-fb: R-MAT scale 23, ef 40, seed 85; 8.4 M vertices, 628 M
+  entries): PageRank rtol 1e-12; SSSP bit-exact (gx_sssp and the 1-D split's single-rank loop);
+- config 2, SYN-7_5 (datagen-7_5-fb: scale 20, ef 32, seed 75): PageRank rtol 1e-12 with the
+  default plan (1 Mi-entry blocks cut into units, narrow codes, CP=0); CDLP x10 bit-exact (the
+  north-star's CDLP workload);
+- config 3, SYN-g500-22 (graph500-22: scale 22, ef 16, seed 22): BFS and WCC bit-exact on the
+  first call and the later ones (the hub-first copy serves from the second call);
+- config 5, SYN-cit (cit-Patents: directed, scale 22, ef 4, seed 3): LCC bit-exact.
 
-One bounded case per path on the MI355X, against the oracle's multithreaded restatements
-(oracle/gx_oracle.c; their equality with the serial ones is tests/test_oracle_parallel.py):
-- PageRank (gx_pagerank, 10 iterations): rtol 1e-12 of the fp64 oracle;
-- SSSP (gx_sssp and the 1-D split's single-rank loop gx_sssp_split_run): bit-exact.
-The graph is generated once (~16 s), the oracle runs on the box's host cores.
+Each case runs against the oracle's multithreaded restatements (oracle/gx_oracle.c; their
+equality with the serial ones is tests/test_oracle_parallel.py) on the box's host cores.
 """
 import numpy as np
 import pytest
@@ -15,19 +20,52 @@ from oracle import oracle as O
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
-PR_RTOL = 1e-12
+PR_RTOL = 1e-12   # fp64 PageRank: row sums in a different order than the oracle's
+
+
+def _graph(scale, ef, seed, undirected, weighted=False):
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context, Graph
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
+    csr = rmat(scale, ef, seed, undirected=undirected, weighted=weighted)
+    ctx = Context(0)
+    G = Graph(ctx, csr, not undirected)
+    return csr, ctx, G
 
 
 @pytest.fixture(scope="module")
 def syn85():
-    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context, Graph
-    from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
-    csr = rmat(23, 40, 85, undirected=True, weighted=True)
-    ctx = Context(0)
-    G = Graph(ctx, csr, False)
+    csr, ctx, G = _graph(23, 40, 85, True, weighted=True)
     yield csr, G
     G.close()
     ctx.close()
+
+
+@pytest.fixture(scope="module")
+def syn75():
+    csr, ctx, G = _graph(20, 32, 75, True)
+    yield csr, G
+    G.close()
+    ctx.close()
+
+
+@pytest.fixture(scope="module")
+def g500():
+    csr, ctx, G = _graph(22, 16, 22, True)
+    yield csr, G
+    G.close()
+    ctx.close()
+
+
+@pytest.fixture(scope="module")
+def syncit():
+    csr, ctx, G = _graph(22, 4, 3, False)
+    yield csr, G
+    G.close()
+    ctx.close()
+
+
+def _maxdeg(csr):
+    return int(np.argmax(np.diff(csr.rowptr.astype(np.int64))))
 
 
 def test_pagerank_syn85(syn85):
@@ -41,11 +79,82 @@ def test_pagerank_syn85(syn85):
 def test_sssp_syn85(syn85):
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
     csr, G = syn85
-    src = int(np.argmax(np.diff(csr.rowptr.astype(np.int64))))
+    src = _maxdeg(csr)
     ref = O.sssp_par(csr, src, 0.0, nthreads=O.max_threads())
     assert np.array_equal(A.LA_SSSP(G, src), ref)
+    assert np.array_equal(A.LA_SSSP(G, src), ref)   # second call: the hub-first copy
     sp = A.SsspSplit(G)
     try:
         assert np.array_equal(sp.run(src), ref)
     finally:
         sp.close()
+
+
+def test_pagerank_syn75(syn75):
+    """Config 2 (pr.cpp:61): the default plan at full size, first and warm call."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    csr, G = syn75
+    ref = O.pagerank(csr, False, 0.85, 10, nthreads=O.max_threads())
+    for _ in range(2):
+        np.testing.assert_allclose(A.LA_PR(G, 0.85, 10), ref, rtol=PR_RTOL, atol=0)
+
+
+def test_cdlp_syn75(syn75):
+    """The north-star CDLP workload (cdlp.cpp:54-81, LAGraph_cdlp.c:264-333): 10 iterations,
+    bit-exact, on the caller's order (first call) and the hub-first relabelled copy (later)."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    csr, G = syn75
+    ref = O.cdlp(csr, False, 10, nthreads=O.max_threads())
+    for call in range(3):
+        got = A.LA_CDLP(G, 10)
+        assert np.array_equal(got, ref), f"call {call}: {int((got != ref).sum())} labels differ"
+
+
+def test_bfs_g500(g500):
+    """Config 3 BFS (bfs.cpp:80) from the max-degree vertex and from a low-degree one."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    csr, G = g500
+    deg = np.diff(csr.rowptr.astype(np.int64))
+    srcs = [_maxdeg(csr), int(np.flatnonzero(deg == 1)[0])]
+    for src in srcs:
+        ref = O.bfs_par(csr, src, True, nthreads=O.max_threads())
+        for call in range(3):
+            got = A.LA_BFS(G, src)
+            assert np.array_equal(got, ref), f"src {src} call {call}: {int((got != ref).sum())} differ"
+
+
+def test_wcc_g500(g500):
+    """Config 3 WCC (wcc.cpp:61): canonical min-id labels, first and later calls."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    csr, G = g500
+    ref = O.wcc_par(csr, nthreads=O.max_threads())
+    for call in range(3):
+        got = A.WeaklyConnectedComponents(G)
+        assert np.array_equal(got, ref), f"call {call}: {int((got != ref).sum())} labels differ"
+
+
+def test_lcc_syncit(syncit):
+    """Config 5 (lcc.cpp:68): directed LCC over N(v) = in u out, bit-exact (integer counts
+    and one division)."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    csr, G = syncit
+    ref = O.lcc(csr, True, nthreads=O.max_threads())
+    for call in range(2):
+        got = A.LA_LCC(G)
+        assert np.array_equal(got, ref), f"call {call}: {int((got != ref).sum())} values differ"
+
+
+def test_bfs_wcc_cdlp_syncit(syncit):
+    """The directed paths at config 5's size: BFS (Aᵀ built from the second call), WCC and CDLP
+    (in + out multiset, reciprocal edges twice)."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    csr, G = syncit
+    src = _maxdeg(csr)
+    ref = O.bfs_par(csr, src, False, nthreads=O.max_threads())
+    for call in range(2):
+        assert np.array_equal(A.LA_BFS(G, src), ref), f"bfs call {call}"
+    ref = O.wcc_par(csr, nthreads=O.max_threads())
+    assert np.array_equal(A.WeaklyConnectedComponents(G), ref)
+    ref = O.cdlp(csr, True, 10, nthreads=O.max_threads())
+    for call in range(2):
+        assert np.array_equal(A.LA_CDLP(G, 10), ref), f"cdlp call {call}"
