@@ -281,6 +281,14 @@ int gx_pr_dist_free(gx_pr_dist *dist);
 int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, double damping, int iters,
                       double *rank);
 int gx_pr_partition(uint64_t n, const uint64_t *rowptr, int nparts, uint32_t *order, uint64_t *rows, uint64_t *live);
+/* gx_sssp_multi: single-source shortest paths of the weighted host CSR A (vals = fp64) from
+ * src on the ndev devices of `ctxs`, in one process (bin/exe/sssp with GX_NGPUS=N; config 4 is
+ * "PageRank + SSSP on datagen-8_5-fb, 8 GPUs, 1-D row partition + RCCL allgather").  Every
+ * device holds A and owns a contiguous target range of ~nnz / ndev entries (gx_sssp_split);
+ * per round the 2-word counts and then the improved (vertex, distance) pairs are all-gathered
+ * by an in-process RCCL clique.  dist[v] in A's vertex order, +inf = unreached, bit-identical
+ * to gx_sssp.  Replaces LA_SSSP (sssp.cpp:53-81) when it runs on several GPUs. */
+int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, uint64_t src, double *dist);
 
 /* ---------------------------------------------------------------------------------
  * Multi-GPU steps for the other algorithms.  The graph is replicated on

@@ -30,9 +30,12 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "gx_pr.h"
@@ -374,13 +377,69 @@ struct MultiRun {
     }
 };
 
+// Run fn(d) for every device on a host thread of its own (its device current, an equal share
+// of the host's OpenMP threads), so the devices' uploads and plans overlap; one device runs
+// inline.  The first failure's code and message come back on the calling thread.
+template <class F>
+int per_device(gx_ctx *const *ctxs, int ndev, F fn) {
+    if (ndev == 1) {
+        GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+        return fn(0);
+    }
+    std::vector<int> rc(ndev, GX_SUCCESS);
+    std::vector<std::string> msg(ndev);
+    std::vector<std::thread> th;
+    const int share = std::max(1, host_threads() / ndev);
+    for (int d = 0; d < ndev; d++)
+        th.emplace_back([&, d] {
+            host_set_threads(share);
+            const hipError_t e = hipSetDevice(ctxs[d]->device);
+            rc[d] = e == hipSuccess ? fn(d) : fail(GX_DEVICE_ERROR, hipGetErrorString(e));
+            if (rc[d] != GX_SUCCESS) msg[d] = gx_last_error();
+        });
+    for (auto &t : th) t.join();
+    for (int d = 0; d < ndev; d++)
+        if (rc[d] != GX_SUCCESS) return fail(rc[d], "device " + std::to_string(ctxs[d]->device) + ": " + msg[d]);
+    return GX_SUCCESS;
+}
+
+int check_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, const char *who) {
+    if (!ctxs || !A || (A->nnz && !A->colidx) || !A->rowptr) return fail(GX_NULL_POINTER, std::string(who) + ": null argument");
+    if (ndev < 1) return fail(GX_INVALID_VALUE, std::string(who) + ": ndev < 1");
+    for (int d = 0; d < ndev; d++)
+        if (!ctxs[d]) return fail(GX_NULL_POINTER, std::string(who) + ": null context");
+    for (int d = 0; d < ndev; d++)
+        for (int e = 0; e < d; e++)
+            if (ctxs[d]->device == ctxs[e]->device)
+                return fail(GX_INVALID_VALUE, std::string(who) + ": one context per distinct device");
+    const Rccl &r = rccl();
+    if (!r.ok) return fail(GX_NOT_IMPLEMENTED, r.error);
+    return GX_SUCCESS;
+}
+
+// The graphs of a multi-device call: A on every device (gx_graph_create validates it there),
+// freed with their contexts' streams drained.
+struct MultiGraphs {
+    std::vector<gx_graph *> g;
+    ~MultiGraphs() {
+        for (gx_graph *x : g) (void)gx_graph_free(x);
+    }
+};
+
+int comm_init_all(gx_ctx *const *ctxs, int ndev, std::vector<ncclComm_t> &comm) {
+    std::vector<int> devs(ndev);
+    for (int d = 0; d < ndev; d++) devs[d] = ctxs[d]->device;
+    comm.assign(ndev, nullptr);
+    GX_NCCL_TRY("ncclCommInitAll", rccl().comm_init_all(comm.data(), ndev, devs.data()));
+    return GX_SUCCESS;
+}
+
 }  // namespace
 
 extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, double damping,
                                  int iters, double *rank) {
-    if (!ctxs || !A || !rank || (A->nnz && !A->colidx) || !A->rowptr)
-        return fail(GX_NULL_POINTER, "gx_pagerank_multi: null argument");
-    if (ndev < 1) return fail(GX_INVALID_VALUE, "gx_pagerank_multi: ndev < 1");
+    GX_TRY(check_multi(ctxs, ndev, A, "gx_pagerank_multi"));
+    if (!rank) return fail(GX_NULL_POINTER, "gx_pagerank_multi: null argument");
     if (iters < 0) return fail(GX_INVALID_VALUE, "gx_pagerank_multi: negative iteration count");
     const uint64_t n = A->n;
     if (n == 0) return GX_SUCCESS;
@@ -389,40 +448,17 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         return GX_SUCCESS;
     }
     if (n >= (1ull << 31) - 64) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: n >= 2^31");
-    for (int d = 0; d < ndev; d++)
-        if (!ctxs[d]) return fail(GX_NULL_POINTER, "gx_pagerank_multi: null context");
-    for (int d = 0; d < ndev; d++)
-        for (int e = 0; e < d; e++)
-            if (ctxs[d]->device == ctxs[e]->device)
-                return fail(GX_INVALID_VALUE, "gx_pagerank_multi: one context per distinct device");
-    const Rccl &r = rccl();
-    if (!r.ok) return fail(GX_NOT_IMPLEMENTED, r.error);
-    // the pull matrix: A' for a directed graph (LAGraph_Cached_AT, pr.cpp:60), A itself else
-    const uint64_t *prp = A->rowptr, *pci = A->colidx;
-    std::vector<uint64_t> trp, tci;
-    if (directed) {
-        trp.resize(n + 1);
-        tci.resize(std::max<uint64_t>(A->nnz, 1));
-        host_transpose(n, A->rowptr, A->colidx, trp.data(), tci.data());
-        prp = trp.data();
-        pci = tci.data();
-    }
-    // interleaved hub-first partition (gx_pr_partition; pr_partition.interleaved_relabel):
-    // position i of the hub-first order goes to device i % ndev as its local row i / ndev
-    std::vector<uint32_t> order(n);
-    std::vector<uint64_t> rows(ndev), live(ndev);
-    GX_TRY(gx_pr_partition(n, A->rowptr, ndev, order.data(), rows.data(), live.data()));
-    uint64_t maxlive = 0;
-    for (int d = 0; d < ndev; d++) maxlive = std::max(maxlive, live[d]);
+    // interleaved hub-first partition (pr_partition.interleaved_relabel): hub-first position i
+    // goes to device i % ndev as its local row i / ndev.  The vertices with out-edges come
+    // first in that order, so device 0 holds the most live rows, ceil(nlive / ndev): the
+    // chunk every device exchanges (+ the zero padding slot and the dangling slot).
+    uint64_t nlive = 0;
+    for (uint64_t v = 0; v < n; v++) nlive += A->rowptr[v + 1] != A->rowptr[v];
     MultiRun M;
     M.ndev = ndev;
-    M.chunk = (maxlive + 2 + 31) / 32 * 32;   // + the zero padding slot and the dangling slot
+    M.chunk = ((nlive + ndev - 1) / ndev + 2 + 31) / 32 * 32;
     if (M.chunk * (uint64_t)ndev >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
-    // column map: vertex -> its place in the exchanged vector (owner * chunk + local row)
-    std::vector<int32_t> colmap(n);
-    for (uint64_t i = 0; i < n; i++) colmap[order[i]] = (int32_t)((i % ndev) * M.chunk + i / ndev);
     M.ctx.assign(ctxs, ctxs + ndev);
-    M.comm.assign(ndev, nullptr);
     M.part.assign(ndev, nullptr);
     for (int d = 0; d < ndev; d++) {
         M.xr.emplace_back(new DBuf<double>());
@@ -430,31 +466,28 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         M.xl.emplace_back(new DBuf<double>());
         M.ro.emplace_back(new DBuf<double>());
     }
-    std::vector<int> devs(ndev);
-    for (int d = 0; d < ndev; d++) devs[d] = ctxs[d]->device;
-    GX_NCCL_TRY("ncclCommInitAll", r.comm_init_all(M.comm.data(), ndev, devs.data()));
-    std::vector<std::vector<uint32_t>> mine(ndev);
-    for (int d = 0; d < ndev; d++) {
-        std::vector<uint32_t> &vr = mine[d];
-        vr.resize(rows[d]);
-        for (uint64_t j = 0; j < rows[d]; j++) vr[j] = order[(uint64_t)d + j * ndev];
-        std::vector<int64_t> h_rp(rows[d] + 1);
-        uint64_t nz = 0;
-        for (uint64_t j = 0; j < rows[d]; j++) nz += prp[vr[j] + 1] - prp[vr[j]];
-        std::vector<int32_t> ci(nz), outdeg(rows[d]);
-        host_pick_rows(prp, pci, vr.data(), rows[d], colmap.data(), h_rp.data(), ci.data());
-        for (uint64_t j = 0; j < rows[d]; j++) outdeg[j] = (int32_t)(A->rowptr[vr[j] + 1] - A->rowptr[vr[j]]);
-        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
-        GX_TRY(pr_part_build(ctxs[d], n, ndev, d, M.chunk, live[d], h_rp, ci, outdeg, damping, &M.part[d]));
+    MultiGraphs G;
+    G.g.assign(ndev, nullptr);
+    std::vector<uint64_t> rows(ndev);
+    // per device, on the device: upload A, A' if directed (LAGraph_Cached_AT, pr.cpp:60), the
+    // hub-first order and this device's plan (pr_multi_plan), the exchange buffers
+    GX_TRY(per_device(ctxs, ndev, [&](int d) -> int {
+        GX_TRY(gx_graph_create(ctxs[d], A, directed, &G.g[d]));
+        if (directed) GX_TRY(ensure_transpose(G.g[d]));
+        GX_TRY(pr_multi_plan(G.g[d], ndev, d, M.chunk, damping, &M.part[d]));
+        rows[d] = M.part[d]->rows;
         const size_t full = M.chunk * (size_t)ndev;
+        hipStream_t s = ctxs[d]->stream;
         GX_TRY(M.xr[d]->alloc(full));
         GX_TRY(M.xw[d]->alloc(full));
         GX_TRY(M.xl[d]->alloc(M.chunk));
         GX_TRY(M.ro[d]->alloc(std::max<uint64_t>(rows[d], 1)));
-        GX_HIP_TRY(hipMemsetAsync(M.xl[d]->p, 0, M.chunk * sizeof(double), ctxs[d]->stream));
-        GX_HIP_TRY(hipMemsetAsync(M.xr[d]->p, 0, full * sizeof(double), ctxs[d]->stream));
-        GX_HIP_TRY(hipMemsetAsync(M.xw[d]->p, 0, full * sizeof(double), ctxs[d]->stream));
-    }
+        GX_HIP_TRY(hipMemsetAsync(M.xl[d]->p, 0, M.chunk * sizeof(double), s));
+        GX_HIP_TRY(hipMemsetAsync(M.xr[d]->p, 0, full * sizeof(double), s));
+        GX_HIP_TRY(hipMemsetAsync(M.xw[d]->p, 0, full * sizeof(double), s));
+        return GX_SUCCESS;
+    }));
+    GX_TRY(comm_init_all(ctxs, ndev, M.comm));
     // init, then per iteration: every device's SpMV, one grouped all-gather
     for (int d = 0; d < ndev; d++) {
         GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
@@ -471,16 +504,138 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         GX_TRY(M.gather(M.xw));
         std::swap(M.xr, M.xw);
     }
-    // scores back in A's vertex order
+    // scores back in A's vertex order: device d's local row j is vertex order_d[j]
     for (int d = 0; d < ndev; d++) {
         GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
         std::vector<double> buf(rows[d]);
-        if (rows[d])
+        std::vector<int32_t> who(rows[d]);
+        if (rows[d]) {
             GX_HIP_TRY(hipMemcpyAsync(buf.data(), M.ro[d]->p, rows[d] * sizeof(double), hipMemcpyDeviceToHost,
                                       ctxs[d]->stream));
+            GX_HIP_TRY(hipMemcpyAsync(who.data(), M.part[d]->order.p, rows[d] * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, ctxs[d]->stream));
+        }
         GX_HIP_TRY(hipStreamSynchronize(ctxs[d]->stream));
-        for (uint64_t j = 0; j < rows[d]; j++) rank[mine[d][j]] = buf[j];
+        for (uint64_t j = 0; j < rows[d]; j++) rank[who[j]] = buf[j];
     }
+    return GX_SUCCESS;
+}
+
+// Multi-device SSSP in one process (bin/exe/sssp with GX_NGPUS; config 4's other half): the
+// 1-D split of gx_sssp_split on every device, the rounds exchanged by in-process RCCL.
+// Device d owns the targets [ranges[d], ranges[d+1]) (contiguous, ~nnz / ndev stored entries
+// each); per round: every device relaxes into its owned vertices, the 2-word counts
+// {pairs, done} are all-gathered and read by the host (the only host read of a round), then
+// max-count pairs of every device are all-gathered and applied everywhere.  The decisions
+// come from replicated state, so every device stops at the same round; a disagreement is an
+// error, not a silent stop.
+extern "C" int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, uint64_t src,
+                             double *dist) {
+    GX_TRY(check_multi(ctxs, ndev, A, "gx_sssp_multi"));
+    if (!dist) return fail(GX_NULL_POINTER, "gx_sssp_multi: null argument");
+    if (!A->vals) return fail(GX_INVALID_VALUE, "gx_sssp_multi: graph has no edge weights");
+    const uint64_t n = A->n, nnz = A->nnz;
+    if (src >= n) return fail(GX_INVALID_INDEX, "gx_sssp_multi: source out of range");
+    std::vector<uint64_t> ranges(ndev + 1, 0);
+    for (int k = 1; k < ndev; k++) {   // pr_partition.partition_rows: ~nnz / ndev entries each
+        const uint64_t target = nnz / ndev * k + nnz % ndev * k / ndev;
+        const uint64_t r = (uint64_t)(std::lower_bound(A->rowptr, A->rowptr + n + 1, target) - A->rowptr);
+        ranges[k] = std::min(std::max(r, ranges[k - 1]), n);
+    }
+    ranges[ndev] = n;
+    uint64_t maxown = 1;
+    for (int d = 0; d < ndev; d++) maxown = std::max(maxown, ranges[d + 1] - ranges[d]);
+    MultiGraphs G;
+    G.g.assign(ndev, nullptr);
+    struct Dev {
+        gx_sssp_split *sp = nullptr;
+        DBuf<uint64_t> pairs, count, counts, all;
+    };
+    std::vector<Dev> D(ndev);
+    std::vector<ncclComm_t> comm;
+    uint64_t *hc = nullptr;
+    // released in this order on every exit: the splits and buffers on their devices, the
+    // communicators, the pinned words (the graphs go last, with G)
+    struct Cleanup {
+        gx_ctx *const *ctxs;
+        std::vector<Dev> &D;
+        std::vector<ncclComm_t> &comm;
+        uint64_t *&hc;
+        ~Cleanup() {
+            for (size_t d = 0; d < D.size(); d++) {
+                (void)hipSetDevice(ctxs[d]->device);
+                (void)hipStreamSynchronize(ctxs[d]->stream);
+                (void)gx_sssp_split_free(D[d].sp);
+                D[d].sp = nullptr;
+                D[d].pairs.release();
+                D[d].count.release();
+                D[d].counts.release();
+                D[d].all.release();
+            }
+            for (ncclComm_t c : comm)
+                if (c) (void)rccl().comm_destroy(c);
+            if (hc) (void)hipHostFree(hc);
+        }
+    } cleanup{ctxs, D, comm, hc};
+    GX_TRY(per_device(ctxs, ndev, [&](int d) -> int {
+        GX_TRY(gx_graph_create(ctxs[d], A, directed, &G.g[d]));
+        GX_TRY(gx_sssp_split_create(G.g[d], ranges[d], ranges[d + 1], &D[d].sp));
+        GX_TRY(D[d].pairs.alloc(2 * maxown));
+        GX_TRY(D[d].count.alloc(2));
+        GX_TRY(D[d].counts.alloc(2 * (uint64_t)ndev));
+        GX_TRY(D[d].all.alloc(2 * maxown * (uint64_t)ndev));
+        return GX_SUCCESS;
+    }));
+    GX_TRY(comm_init_all(ctxs, ndev, comm));
+    GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+    GX_HIP_TRY(hipHostMalloc((void **)&hc, 2 * (size_t)ndev * sizeof(uint64_t), hipHostMallocDefault));
+    const Rccl &r = rccl();
+    auto gather = [&](auto send, auto recv, size_t words) -> int {
+        GX_NCCL_TRY("ncclGroupStart", r.group_start());
+        for (int d = 0; d < ndev; d++) {
+            const ncclResult_t e = r.all_gather(send(d), recv(d), words, ncclUint64, comm[d], ctxs[d]->stream);
+            if (e != ncclSuccess) {
+                (void)r.group_end();
+                return rccl_fail("ncclAllGather", e);
+            }
+        }
+        GX_NCCL_TRY("ncclGroupEnd", r.group_end());
+        return GX_SUCCESS;
+    };
+    for (int d = 0; d < ndev; d++) GX_TRY(gx_sssp_split_start(D[d].sp, src, ctxs[d]->stream));
+    for (uint64_t round = 0;; round++) {
+        if (round > 4 * (n + 16)) return fail(GX_DEVICE_ERROR, "gx_sssp_multi: no fixed point");
+        for (int d = 0; d < ndev; d++)
+            GX_TRY(gx_sssp_split_relax(D[d].sp, D[d].pairs.p, D[d].count.p, ctxs[d]->stream));
+        GX_TRY(gather([&](int d) { return (const void *)D[d].count.p; }, [&](int d) { return (void *)D[d].counts.p; },
+                      2));
+        GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+        GX_HIP_TRY(hipMemcpyAsync(hc, D[0].counts.p, 2 * (size_t)ndev * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                  ctxs[0]->stream));
+        GX_HIP_TRY(hipStreamSynchronize(ctxs[0]->stream));
+        int ndone = 0;
+        uint64_t m = 0;
+        for (int d = 0; d < ndev; d++) {
+            ndone += hc[2 * d + 1] != 0;
+            m = std::max(m, hc[2 * d]);
+        }
+        if (ndone == ndev) break;
+        if (ndone) return fail(GX_DEVICE_ERROR, "gx_sssp_multi: devices disagree on termination");
+        if (m > maxown) return fail(GX_DEVICE_ERROR, "gx_sssp_multi: pair count beyond the owned range");
+        if (m)
+            GX_TRY(gather([&](int d) { return (const void *)D[d].pairs.p; }, [&](int d) { return (void *)D[d].all.p; },
+                          2 * m));
+        for (int d = 0; d < ndev; d++)
+            GX_TRY(gx_sssp_split_apply(D[d].sp, m ? D[d].all.p : D[d].pairs.p, D[d].counts.p, ndev, m,
+                                       ctxs[d]->stream));
+    }
+    // the distance vector is replicated: device 0's, in A's vertex order
+    GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+    DBuf<double> out;
+    GX_TRY(out.alloc(std::max<uint64_t>(n, 1)));
+    GX_TRY(gx_sssp_split_distances(D[0].sp, out.p, ctxs[0]->stream));
+    GX_HIP_TRY(hipStreamSynchronize(ctxs[0]->stream));
+    GX_TRY(download(ctxs[0], dist, out.p, n, Xfer::Raw64));
     return GX_SUCCESS;
 }
 

@@ -571,6 +571,10 @@ void host_copy(void *dst, const void *src, size_t bytes) {
     }
 }
 
+int host_threads() { return omp_get_max_threads(); }
+
+void host_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
+
 bool host_monotone(const uint64_t *rp, uint64_t n) {
     int bad = 0;
 #pragma omp parallel for schedule(static) reduction(| : bad)

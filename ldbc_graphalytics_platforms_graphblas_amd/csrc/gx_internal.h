@@ -38,6 +38,9 @@ void host_hub_order(const uint64_t *rp, uint64_t n, uint32_t *order);
 void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows, uint64_t nrows, const int32_t *colmap,
                     int64_t *out_rp, int32_t *out_ci);
 // CSR of A' (rows sorted)
+// OpenMP threads of the calling host thread (gx_*_multi gives each device's thread a share)
+int host_threads();
+void host_set_threads(int n);
 void host_transpose(uint64_t n, const uint64_t *rp, const uint64_t *ci, uint64_t *trp, uint64_t *tci);
 
 }  // namespace gx

@@ -194,6 +194,9 @@ int pr_init(PrPart *p, double *x_local, hipStream_t s);
 // gx_pagerank's single-rank plan of a graph: its pull matrix (A' when directed, which must be
 // built) relabelled hub-first, column-sorted blocks, x buffers and the hub-first perm.
 int pr_single_plan(gx_graph *g, PrPart **out);
+// gx_pagerank_multi's plan of device d of ndev from its copy of the graph (A' built when
+// directed): hub-first positions d, d + ndev, ... as rows, columns in the exchange layout.
+int pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double damping, PrPart **out);
 // A rank's plan from its local pull rows (h_rp from 0) with columns already in the exchange
 // layout (ci), the out-degree of each row's vertex, and its live prefix (gx_pr_part_create_live).
 int pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint64_t chunk, uint64_t live,

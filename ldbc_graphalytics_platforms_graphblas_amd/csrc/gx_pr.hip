@@ -530,6 +530,34 @@ __global__ void k_hub_apply(const int32_t *__restrict__ sorted_ids, int64_t n, c
     }
 }
 
+// Device `d` of `ndev` (gx_pagerank_multi's interleaved partition): its local row j is hub-first
+// position i = d + j ndev; the row's source vertex, out-degree and pull length (plen[rows] = 0
+// for the exclusive scan).
+__global__ void k_multi_pick(const int32_t *__restrict__ order, const int32_t *__restrict__ nout,
+                             const int64_t *__restrict__ plen, int ndev, int d, int64_t rows,
+                             int32_t *__restrict__ my_order, int32_t *__restrict__ my_out,
+                             int64_t *__restrict__ my_plen) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= rows; j += (int64_t)gridDim.x * blockDim.x) {
+        if (j == rows) {
+            my_plen[rows] = 0;
+            continue;
+        }
+        const int64_t i = (int64_t)d + j * ndev;
+        my_order[j] = order[i];
+        my_out[j] = nout[i];
+        my_plen[j] = plen[i];
+    }
+}
+
+// vertex -> its slot in the exchanged vector: owner (i mod ndev) * chunk + local row (i / ndev)
+__global__ void k_multi_colmap(const int32_t *__restrict__ perm, int64_t n, int ndev, int64_t chunk,
+                               int32_t *__restrict__ colmap) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = perm[v];
+        colmap[v] = (int32_t)((i % ndev) * chunk + i / ndev);
+    }
+}
+
 // Hub-first order: vertices by out-degree descending, ties by id (stable counting sort).
 // The pull SpMV gathers x(u) once per out-edge of u, so this packs the most gathered
 // entries of x into its first few MiB, which stay resident in each XCD's 4 MiB L2.
@@ -687,6 +715,85 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     p->src_perm = p->perm.p;
     GX_TRY(pr_plan(p.get(), HostView<int64_t>(nrp.get(), n + 1), p->rp_own.p, nullptr, p->outdeg_own.p,
                    HostView<int32_t>(nout.get(), n)));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors above die at return
+    clk.mark("pr_plan");
+    *out = p.release();
+    return GX_SUCCESS;
+}
+
+// gx_pagerank_multi's plan of device `d` of `ndev`, all on that device from its copy of the
+// graph: the hub-first order (the same radix sort on every device, so every device derives
+// the same partition), the device's rows (hub-first positions d, d + ndev, ...) as the sorted
+// plan's source rows, and the column map into the exchange layout as its column renaming.
+// Replaces the host transpose / row picking / column remapping of round 3.
+int gx::pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double damping, PrPart **out) {
+    const uint64_t n = g->n;
+    gx_ctx *ctx = g->ctx;
+    hipStream_t s = ctx->stream;
+    DevCSR &P = g->directed ? g->AT : g->A;
+    PlanClock clk("multi", s);
+    GX_TRY(ensure_outdeg(g));
+    const uint64_t rows = n > (uint64_t)d ? (n - (uint64_t)d + ndev - 1) / ndev : 0;
+    std::unique_ptr<PrPart> p(new PrPart());
+    p->ctx = ctx;
+    p->n_global = n;
+    p->nranks = ndev;
+    p->rank = d;
+    p->chunk = chunk;
+    p->damping = damping;
+    GX_TRY(p->order.alloc(std::max<uint64_t>(rows, 1)));
+    GX_TRY(p->perm.alloc(n));   // the column map
+    GX_TRY(p->rp_own.alloc(rows + 1));
+    GX_TRY(p->outdeg_own.alloc(std::max<uint64_t>(rows, 1)));
+    {
+        DBuf<uint32_t> d0, d1;
+        DBuf<int32_t> i0, i1, ord, nout;
+        DBuf<int64_t> plen, myplen;
+        GX_TRY(d0.alloc(n));
+        GX_TRY(d1.alloc(n));
+        GX_TRY(i0.alloc(n));
+        GX_TRY(i1.alloc(n));
+        GX_TRY(ord.alloc(n));
+        GX_TRY(nout.alloc(n));
+        GX_TRY(plen.alloc(n + 1));
+        GX_TRY(myplen.alloc(rows + 1));
+        const unsigned grid = grid_for(n + 1, 256, 8192);
+        hipLaunchKernelGGL(k_hub_keys, dim3(grid), dim3(256), 0, s, g->outdeg.p, (int64_t)n, d0.p, i0.p);
+        GX_TRY(check_launch("k_hub_keys"));
+        GX_TRY(sort_pairs_desc_u32_i32(d0.p, d1.p, i0.p, i1.p, n, s));
+        // i0 is free after the sort: it takes the full perm
+        hipLaunchKernelGGL(k_hub_apply, dim3(grid), dim3(256), 0, s, i1.p, (int64_t)n, g->outdeg.p, P.rp.p, ord.p,
+                           i0.p, nout.p, plen.p);
+        GX_TRY(check_launch("k_hub_apply"));
+        hipLaunchKernelGGL(k_multi_pick, dim3(grid_for(rows + 1, 256, 8192)), dim3(256), 0, s, ord.p, nout.p, plen.p,
+                           ndev, d, (int64_t)rows, p->order.p, p->outdeg_own.p, myplen.p);
+        GX_TRY(check_launch("k_multi_pick"));
+        hipLaunchKernelGGL(k_multi_colmap, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, i0.p, (int64_t)n, ndev,
+                           (int64_t)chunk, p->perm.p);
+        GX_TRY(check_launch("k_multi_colmap"));
+        GX_TRY(scan_exclusive_i64(myplen.p, p->rp_own.p, rows + 1, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries are freed at the end of the block
+    }
+    clk.mark("hub order + partition rows (device)");
+    std::unique_ptr<int64_t[]> nrp(new int64_t[rows + 1]);
+    std::unique_ptr<int32_t[]> nout(new int32_t[std::max<uint64_t>(rows, 1)]);
+    GX_TRY(download(ctx, nrp.get(), p->rp_own.p, rows + 1, Xfer::Raw64));
+    if (rows) GX_TRY(download(ctx, nout.get(), p->outdeg_own.p, rows, Xfer::Raw32));
+    // the live prefix: rows with out-edges (hub-first, so a prefix of the device's rows)
+    uint64_t lo = 0, hi = rows;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (nout[mid] > 0) lo = mid + 1;
+        else hi = mid;
+    }
+    p->live = lo;
+    clk.mark("row pointers to the host");
+    p->src_rp = P.rp.p;
+    p->src_ci = P.ci.p;
+    p->src_order = p->order.p;
+    p->src_perm = p->perm.p;
+    GX_TRY(pr_plan(p.get(), HostView<int64_t>(nrp.get(), rows + 1), p->rp_own.p, nullptr, p->outdeg_own.p,
+                   HostView<int32_t>(nout.get(), rows)));
     GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors above die at return
     clk.mark("pr_plan");
     *out = p.release();

@@ -231,7 +231,10 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // PROBE (diagnostic builds only, -DGX_PR_PROBES, tools/pr_probe.sh; wrong results by design):
 // 1 no LDS adds (register sum), 2 no gathers, 3 neither, 4 gathers folded into x[c & 4095]
 // (L1 hits), 5 no gathers + conflict-free LDS adds (acc[tid]), 6 gathers + conflict-free LDS
-// adds, 7 no index loads (entries synthesised from the position, columns = the base).
+// adds, 7 no index loads (entries synthesised from the position, columns = the base),
+// 8 gathers of columns >= 512 Ki folded into the first 512 Ki (the sparse tail as local as the
+// hub lines), 9 every gather folded into the first 64 Ki columns.  gather_narrow takes 2, 4,
+// 8 and 9 (the others run it unchanged).
 template <int PROBE, int CP>   // CP bit 0: index loads non-temporal (bit 2: gather_narrow)
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
                                              double *acc, int64_t step64) {
@@ -322,6 +325,8 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
         for (int i = 0; i < kU; i++) {
             if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5) t.g[i] = (double)c[i];
             else if constexpr (PROBE == 4) t.g[i] = a.x_in[c[i] & 4095];
+            else if constexpr (PROBE == 8) t.g[i] = a.x_in[c[i] >= (1 << 19) ? (c[i] & ((1 << 19) - 1)) : c[i]];
+            else if constexpr (PROBE == 9) t.g[i] = a.x_in[c[i] & 65535];
             else t.g[i] = *reinterpret_cast<const double *>(xb + ((uint32_t)c[i] << 3));
         }
     };
@@ -395,7 +400,7 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
 // null supergroup (padding codes, base = x's zero slot), so the loop has no range checks.
 // Same pipeline as gather_units: round i+1's gathers issue before round i's LDS adds, the
 // loads two rounds ahead, buffers A/B alternating.
-template <int CP>
+template <int CP, int PROBE = 0>
 __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedUnit &u, double *acc) {
     constexpr int W = kBS / kWave;   // supergroups per round
     const int32_t nrounds = (u.nsg + W - 1) / W;
@@ -449,7 +454,17 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
             col[k] = bk + ((sk >> (8 * (k & 3))) & 255u);
             bk += (tk >> (8 * (k & 3))) & 255u;
         }
-        if ((CP & 4) && b0 >= a.nt_col) {   // past the hub lines: streamed (GX_PR_CP bit 2)
+        if constexpr (PROBE == 2 || PROBE == 4 || PROBE == 8 || PROBE == 9) {
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                const uint32_t c = col[k];
+                if constexpr (PROBE == 2) t.g[k] = (double)c;
+                else if constexpr (PROBE == 4) t.g[k] = a.x_in[c & 4095u];
+                else if constexpr (PROBE == 8) t.g[k] = a.x_in[c >= (1u << 19) ? (c & ((1u << 19) - 1)) : c];
+                else t.g[k] = a.x_in[c & 65535u];
+            }
+            (void)b0;
+        } else if ((CP & 4) && b0 >= a.nt_col) {   // past the hub lines: streamed (GX_PR_CP bit 2)
 #pragma unroll
             for (int k = 0; k < kU; k++) t.g[k] = __builtin_nontemporal_load(reinterpret_cast<const double *>(xb + (col[k] << 3)));
         } else {
@@ -534,7 +549,7 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
     if (!empty) {
         for (int i = tid; i < nrows; i += kBS) acc[i] = 0.0;
         __syncthreads();
-        if constexpr (PROBE == 0) gather_narrow<CP>(a, u, acc);
+        gather_narrow<CP, PROBE>(a, u, acc);
         gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step);
         __syncthreads();
     }
@@ -1371,8 +1386,11 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
 #ifdef GX_PR_PROBES
             if (const char *pe = std::getenv("GX_PR_PROBE")) {
                 switch (std::atoi(pe)) {
-#define GX_PROBE_CASE(k) case k: hipLaunchKernelGGL((k_pr_pull_units<false, k>), dim3(nw), dim3(kBS), lds, s, a); break;
+// the probes run under the plan's cache policy (0, or 5 for a large x)
+#define GX_PROBE_CASE(k) case k: if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, k, 5>), dim3(nw), dim3(kBS), lds, s, a); \
+                                 else hipLaunchKernelGGL((k_pr_pull_units<false, k>), dim3(nw), dim3(kBS), lds, s, a); break;
                 GX_PROBE_CASE(1) GX_PROBE_CASE(2) GX_PROBE_CASE(3) GX_PROBE_CASE(4) GX_PROBE_CASE(5) GX_PROBE_CASE(6) GX_PROBE_CASE(7)
+                GX_PROBE_CASE(8) GX_PROBE_CASE(9)
 #undef GX_PROBE_CASE
                 default: hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
                 }

@@ -98,6 +98,20 @@ struct OutFile {
 // "%.16e" == ostream precision(16) + std::scientific (pr.cpp:26-27)
 void PutDouble(FILE *f, uint64_t id, double x) { std::fprintf(f, "%" PRIu64 " %.16e\n", id, x); }
 
+// the names the reference's wrappers give their ComputationTimer (bfs.cpp:71, pr.cpp:48,
+// sssp.cpp:64, wcc.cpp:40, cdlp.cpp:59, lcc.cpp:65)
+const char *TimerName(Algorithm alg) {
+    switch (alg) {
+        case Algorithm::BFS: return "BFS";
+        case Algorithm::PR: return "PageRank";
+        case Algorithm::SSSP: return "SSSP";
+        case Algorithm::WCC: return "WeaklyConnectedComponents";
+        case Algorithm::CDLP: return "CDLP";
+        case Algorithm::LCC: return "LCC";
+    }
+    return "?";
+}
+
 }  // namespace
 
 int Main(int argc, char **argv, Algorithm alg) {
@@ -106,15 +120,16 @@ int Main(int argc, char **argv, Algorithm alg) {
         if (p.thread_num > 0) omp_set_num_threads((int)p.thread_num);
         int device = 0;
         if (const char *d = std::getenv("GX_DEVICE")) device = std::atoi(d);
-        // GX_NGPUS = N: PageRank on devices [GX_DEVICE, GX_DEVICE + N) in this one process
-        // (gx_pagerank_multi: 1-D row blocks, in-process RCCL all-gather); execute-job.sh cannot
-        // pass new flags (execute-job.sh:68-151), so the backend comes from the environment
-        // (SURVEY.md 8b).  The other algorithms run on one GPU.
+        // GX_NGPUS = N: PageRank and SSSP (BASELINE config 4) on devices [GX_DEVICE,
+        // GX_DEVICE + N) in this one process (gx_pagerank_multi / gx_sssp_multi: 1-D row
+        // partition, in-process RCCL all-gathers); execute-job.sh cannot pass new flags
+        // (execute-job.sh:68-151), so the backend comes from the environment.
+        // The other algorithms run on one GPU.
         int ngpus = 0;
         if (const char *g = std::getenv("GX_NGPUS")) ngpus = std::max(1, std::atoi(g));
-        if (ngpus && alg != Algorithm::PR)
-            std::cerr << "GX_NGPUS: only PageRank runs on several GPUs; this algorithm runs on device " << device
-                      << std::endl;
+        if (ngpus && alg != Algorithm::PR && alg != Algorithm::SSSP)
+            std::cerr << "GX_NGPUS: only PageRank and SSSP run on several GPUs; this algorithm runs on device "
+                      << device << std::endl;
 
         CsrHolder A;
         ReadMatrix(p, &A.csr);
@@ -136,7 +151,7 @@ int Main(int argc, char **argv, Algorithm alg) {
 
         CtxHolder H;
         OK(gx_init(device, &H.ctx), "gx_init");
-        const bool multi = ngpus > 0 && alg == Algorithm::PR;
+        const bool multi = ngpus > 0 && (alg == Algorithm::PR || alg == Algorithm::SSSP);
         if (multi)
             for (int k = 1; k < ngpus; k++) {
                 gx_ctx *c = nullptr;
@@ -149,6 +164,8 @@ int Main(int argc, char **argv, Algorithm alg) {
 
         const auto t_start = GetCurrentMilliseconds();
         std::cout << "Processing starts at: " << t_start << std::endl;
+        std::cout << TimerName(alg) << " starts" << std::endl;   // ComputationTimer's constructor line
+        const auto wall0 = std::chrono::high_resolution_clock::now();
         if (!multi) OK(gx_graph_create(H.ctx, &A.csr, p.directed ? 1 : 0, &H.g), "gx_graph_create");
         const auto t_uploaded = GetCurrentMilliseconds();
         switch (alg) {
@@ -170,7 +187,14 @@ int Main(int argc, char **argv, Algorithm alg) {
                 break;
             case Algorithm::SSSP:
                 vals.resize(n);
-                OK(gx_sssp(H.g, src, vals.data()), "gx_sssp");
+                if (multi) {
+                    std::vector<gx_ctx *> ctxs{H.ctx};
+                    ctxs.insert(ctxs.end(), H.more.begin(), H.more.end());
+                    OK(gx_sssp_multi(ctxs.data(), ngpus, &A.csr, p.directed ? 1 : 0, src, vals.data()),
+                       "gx_sssp_multi");
+                } else {
+                    OK(gx_sssp(H.g, src, vals.data()), "gx_sssp");
+                }
                 break;
             case Algorithm::WCC:
                 labels.resize(n);
@@ -186,6 +210,13 @@ int Main(int argc, char **argv, Algorithm alg) {
                 break;
         }
         const auto t_end = GetCurrentMilliseconds();
+        {
+            // ComputationTimer's line (computation_timer.hpp:38-49; "PageRank" at pr.cpp:48,
+            // "SSSP" at sssp.cpp:64, ...): the scope's seconds rounded to milliseconds
+            using namespace std::chrono;
+            const duration<double> d = round<milliseconds>(high_resolution_clock::now() - wall0);
+            std::cout << TimerName(alg) << " duration: " << d.count() << "s" << std::endl;
+        }
         std::cout << "Processing ends at: " << t_end << std::endl;
         double dev_ms = 0;
         gx_last_device_ms(H.ctx, &dev_ms);

@@ -332,3 +332,42 @@ def test_gx_pagerank_multi_one_device(undirected):
             np.testing.assert_allclose(out, O.pagerank(csr, not undirected, 0.85, 10), rtol=1e-12, atol=0)
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("undirected", [True, False])
+def test_gx_sssp_multi_one_device(undirected):
+    """gx_sssp_multi (bin/exe/sssp's GX_NGPUS path) on one device: the full exchange protocol
+    over a size-1 in-process RCCL clique, bit-exact against the oracle and gx_sssp."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    from oracle import oracle as O
+    ctx = A.Context(0)
+    try:
+        for scale, ef in ((10, 8), (14, 16)):
+            csr = rmat(scale, ef, 7 + scale, undirected=undirected, weighted=True)
+            deg = np.diff(csr.rowptr.astype(np.int64))
+            for src in (int(np.argmax(deg)), int(np.flatnonzero(deg == 0)[0]) if (deg == 0).any() else 0):
+                out = np.zeros(csr.n)
+                arr = (C.c_void_p * 1)(ctx.handle.value)
+                s = csr.as_c()
+                N.check(N.lib().gx_sssp_multi(arr, 1, C.byref(s), int(not undirected), src, N.as_dp(out)),
+                        "gx_sssp_multi")
+                assert np.array_equal(out, O.sssp(csr, src)), (scale, src)
+    finally:
+        ctx.close()
+
+
+def test_gx_sssp_multi_rejects_bad_arguments():
+    """Argument checks run before any device work (no GPU needed): unweighted graph, null
+    contexts, source out of range."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    csr = rmat(6, 4, 1, undirected=True)
+    s = csr.as_c()
+    out = np.zeros(csr.n)
+    arr = (C.c_void_p * 1)(None)
+    assert N.lib().gx_sssp_multi(arr, 1, C.byref(s), 0, 0, N.as_dp(out)) != 0
+    assert N.lib().gx_sssp_multi(None, 1, C.byref(s), 0, 0, N.as_dp(out)) != 0
+    assert N.lib().gx_pagerank_multi(arr, 1, C.byref(s), 0, 0.85, 10, N.as_dp(out)) != 0

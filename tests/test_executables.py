@@ -107,6 +107,11 @@ def test_executable_matches_validation(name, tmp_path_factory, fixture_graphs):
     starts = re.findall(r"Processing starts at: (\d+)", res.stdout)
     ends = re.findall(r"Processing ends at: (\d+)", res.stdout)
     assert len(starts) == 1 and len(ends) == 1 and int(ends[0]) >= int(starts[0])
+    # ComputationTimer's lines (computation_timer.hpp:17-50), inside the markers
+    tname = {"BFS": "BFS", "PR": "PageRank", "SSSP": "SSSP", "WCC": "WeaklyConnectedComponents", "CDLP": "CDLP",
+             "LCC": "LCC"}[ALG]
+    assert re.search(rf"^{tname} starts$", res.stdout, re.M), res.stdout
+    assert re.search(rf"^{tname} duration: \d+(\.\d+)?s$", res.stdout, re.M), res.stdout
     ids, vals = parse_output(out, alg)
     np.testing.assert_array_equal(ids, g.mapping)
     expected = read_validation(FIXTURES / name)
@@ -154,3 +159,27 @@ def test_pagerank_executable_gx_ngpus(graph, tmp_path_factory, fixture_graphs):
     want = O.pagerank(g.csr, g.directed, float(g.param("pr", "damping-factor")), int(g.param("pr", "num-iterations")))
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
     check_against_validation("PR", g.mapping, list(got), read_validation(FIXTURES / f"{graph}-PR"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", ["example-directed", "example-undirected", "test-sssp-directed",
+                                   "test-sssp-undirected"])
+def test_sssp_executable_gx_ngpus(graph, tmp_path_factory, fixture_graphs):
+    """bin/exe/sssp with GX_NGPUS=1 (gx_sssp_multi: the 1-D split with in-process RCCL
+    all-gathers of counts and pairs, BASELINE config 4's SSSP half): bit-exact against the
+    oracle and within the Graphalytics rule of the validation file."""
+    import os
+    from oracle import oracle as O
+    d, g = load_dir(tmp_path_factory, graph, fixture_graphs)
+    out = d / "out-sssp-multi"
+    env = dict(os.environ, GX_NGPUS="1")
+    res = subprocess.run(job_argv("sssp", d, out, g, d), capture_output=True, text=True, timeout=120, env=env)
+    assert res.returncode == 0, res.stderr
+    assert "GX_NGPUS" not in res.stderr
+    assert re.search(r"^SSSP duration: \d+(\.\d+)?s$", res.stdout, re.M), res.stdout
+    ids, vals = parse_output(out, "sssp")
+    np.testing.assert_array_equal(ids, g.mapping)
+    got = np.array([np.inf if v == "infinity" else float(v) for v in vals])
+    src = int(np.flatnonzero(g.mapping == np.uint64(g.param("sssp", "source-vertex")))[0])
+    assert np.array_equal(got, O.sssp(g.csr, src))
+    check_against_validation("SSSP", g.mapping, list(got), read_validation(FIXTURES / f"{graph}-SSSP"))

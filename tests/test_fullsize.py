@@ -158,3 +158,26 @@ def test_bfs_wcc_cdlp_syncit(syncit):
     ref = O.cdlp(csr, True, 10, nthreads=O.max_threads())
     for call in range(2):
         assert np.array_equal(A.LA_CDLP(G, 10), ref), f"cdlp call {call}"
+
+
+def _multi(fn, ctx_handle, csr, *args):
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    out = np.zeros(csr.n)
+    arr = (C.c_void_p * 1)(ctx_handle.value)
+    s = csr.as_c()
+    N.check(getattr(N.lib(), fn)(arr, 1, C.byref(s), *args, N.as_dp(out)), fn)
+    return out
+
+
+def test_multi_paths_at_full_size(syn75, syn85):
+    """The executables' GX_NGPUS paths (one device, size-1 RCCL clique) at the config sizes:
+    gx_pagerank_multi on SYN-7_5 (the device-built interleaved plan) and gx_sssp_multi on
+    SYN-8_5 (the exchange protocol, one host read per round)."""
+    csr, G = syn75
+    got = _multi("gx_pagerank_multi", G.ctx.handle, csr, 0, 0.85, 10)
+    np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, 10, nthreads=O.max_threads()), rtol=PR_RTOL, atol=0)
+    csr, G = syn85
+    src = _maxdeg(csr)
+    got = _multi("gx_sssp_multi", G.ctx.handle, csr, 0, src)
+    assert np.array_equal(got, O.sssp_par(csr, src, 0.0, nthreads=O.max_threads()))
