@@ -208,7 +208,10 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                  {"GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536", "GX_PR_LONG_NNZ": "1024"},
                                  {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192"},
                                  {"GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192", "GX_PR_SORTED_ROWS": "64",
-                                  "GX_PR_LANEPERM": "0"}])
+                                  "GX_PR_LANEPERM": "0"},
+                                 {"GX_PR_NARROW_MIN": "4096"}, {"GX_PR_NARROW_MIN": "1073741824"},
+                                 {"GX_PR_WIDE_COST": "64", "GX_PR_ROW_COST": "0", "GX_PR_UNIT_NNZ": "8192"},
+                                 {"GX_PR_ROW_COST": "1024", "GX_PR_BLOCK_NNZ": "65536"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
     """The default plan, non-temporal index loads and sparse narrow gathers (GX_PR_CP=1 / 5, the large-graph default), the plan's key sort in groups of two segments or with 64-bit keys, without the lane permutation, blocks cut into many units, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
     blocks (several workgroups per sorted block, combined through slabs by the last arriver)
@@ -291,7 +294,8 @@ def test_pagerank_mixed_escape_rounds(ctx, monkeypatch, laneperm):
                                  {"GX_SSSP_PULL": "2", "GX_SSSP_DSCALE": "200"},
                                  {"GX_SSSP_PULL_FRAC": "50", "GX_SSSP_DSCALE": "5"},
                                  {"GX_SSSP_FUSE": "0"}, {"GX_SSSP_FUSE": "300", "GX_SSSP_DSCALE": "0.5"},
-                                 {"GX_SSSP_FUSE_MAX": "3", "GX_SSSP_DSCALE": "1"}])
+                                 {"GX_SSSP_FUSE_MAX": "3", "GX_SSSP_DSCALE": "1"},
+                                 {"GX_SSSP_DELTA": "0.01"}, {"GX_SSSP_DELTA": "1000"}])
 def test_sssp_pull_heavy_phase(ctx, monkeypatch, env):
     """Heavy phases pushed, always pulled, and pulled only for big settled lists, over narrow
     and wide buckets, with buckets opened one at a time or fused (GX_SSSP_FUSE entries,
@@ -403,12 +407,14 @@ def test_cdlp_tier_boundaries(ctx, directed):
         np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=iters), O.cdlp(csr, directed, iters))
 
 
-@pytest.mark.parametrize("active", ["1", "0"])
-def test_cdlp_active_set(ctx, monkeypatch, active):
+@pytest.mark.parametrize("active,lag", [("1", "2"), ("0", "2"), ("1", "1")])
+def test_cdlp_active_set(ctx, monkeypatch, active, lag):
     """From the third iteration gx_cdlp recomputes only the neighbours of the last iteration's
     changes (GX_CDLP_ACTIVE=0: every vertex): labels equal the oracle's at every count, on
-    graphs whose labels settle and on ones that keep oscillating (directed and undirected)."""
+    graphs whose labels settle and on ones that keep oscillating (directed and undirected),
+    with the fixed-point exit read two iterations late (the default) or one (GX_CDLP_LAG=1)."""
     monkeypatch.setenv("GX_CDLP_ACTIVE", active)
+    monkeypatch.setenv("GX_CDLP_LAG", lag)
     for g in (_rmat(14, 16, 4), _rmat(12, 4, 8), _rmat(11, 8, 3, undirected=False), _G(_tier_graph(False), False),
               _G(_tier_graph(True), True)):
         for iters in (2, 3, 5, 12):
