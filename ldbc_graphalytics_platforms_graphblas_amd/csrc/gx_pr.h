@@ -147,6 +147,15 @@ struct PrPart {
                                  // gathers from column nt_col on (x larger than the L2s)
     uint32_t nt_col = 65536;
     uint32_t nsorted = 0, nlong_pad = 0;
+    // paced sweep (GX_PR_PACE, gx_pr_sorted.hip): x's columns cut into windows (window 0 below
+    // pace_h, then 2^pace_wshift columns each); per unit the round at which each window starts
+    // (narrow rounds, then wide rounds: units x 2 (nw + 1)); per XCD one progress word per CU
+    // slot.  The units of one XCD and generation keep within pace_d windows of each other, so
+    // the x lines one fetches into the XCD's L2 are still there for the others.
+    int pace = 0;
+    uint32_t pace_nw = 0, pace_h = 0, pace_wshift = 18, pace_d = 1, pace_polls = 64;
+    DBuf<int32_t> pace_rounds;
+    DBuf<uint32_t> pace_prog;
     // dangling-score sum fused into the kernel: blocks holding out-degree-0 rows publish a
     // partial, the last of them adds them up in slot order
     bool fused_dangling = false;

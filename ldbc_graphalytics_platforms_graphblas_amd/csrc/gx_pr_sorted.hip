@@ -87,6 +87,10 @@ struct SortedArgs {
     uint32_t nt_col;         // CP bit 2: narrow supergroups from this column on gathered non-temporally
     double *xd;              // x of the rows past `live` (store_x, gx_pr.h)
     int64_t live;
+    // paced sweep (PrPart::pace)
+    const int32_t *pace_rounds;
+    uint32_t *pace_prog;
+    uint32_t pace_nw, pace_d, pace_polls, pace_ncus;
 };
 
 // Returns the row's score if the row is dangling (out-degree 0), else 0.
@@ -237,7 +241,7 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // 8 and 9 (the others run it unchanged).
 template <int PROBE, int CP>   // CP bit 0: index loads non-temporal (bit 2: gather_narrow)
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
-                                             double *acc, int64_t step64) {
+                                             double *acc, int64_t step64, int32_t k0 = 0, int32_t k1 = 0x7fffffff) {
     const int tid = threadIdx.x;
     const int64_t z0 = b.nz_begin;
     const int32_t lo = (int32_t)(lo64 - z0), hi = (int32_t)(hi64 - z0), step = (int32_t)step64;
@@ -343,10 +347,12 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
     // the scheduler and the exits are not shared: a load hoisted above the issue that still
     // reads its buffer, or one exit block adding "tA or tB", makes the register allocator copy
     // a buffer at the loop latch, and a copy waits for the loads in flight.
-    const int32_t nr = (hi - lo + step - 1) / step;   // rounds of this unit
+    // rounds [k0, k1) of this unit (a paced sweep's window; all of them by default)
+    const int32_t nr = min((hi - lo + step - 1) / step, k1) - k0;
+    if (nr <= 0) return;
     Rd dA, dB;
     Gt tA, tB;
-    int32_t R = lo;
+    int32_t R = lo + k0 * step;
     load(dA, R);
     load(dB, R + step);
     issue(dA, R, tA);
@@ -401,11 +407,14 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
 // Same pipeline as gather_units: round i+1's gathers issue before round i's LDS adds, the
 // loads two rounds ahead, buffers A/B alternating.
 template <int CP, int PROBE = 0>
-__device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedUnit &u, double *acc) {
+__device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedUnit &u, double *acc, int32_t i0 = 0,
+                                              int32_t i1 = 0x7fffffff) {
     constexpr int W = kBS / kWave;   // supergroups per round
     const int32_t nrounds = (u.nsg + W - 1) / W;
     if (u.unit >= nrounds) return;
-    const int32_t nr = (nrounds - u.unit + u.nunits - 1) / u.nunits;
+    // rounds [i0, i1) of this unit (a paced sweep's window; all of them by default)
+    const int32_t nr = min((nrounds - u.unit + u.nunits - 1) / u.nunits, i1) - i0;
+    if (nr <= 0) return;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid >> 6;
@@ -421,7 +430,7 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
         uint32_t r[kU];
     };
     auto load = [&](Rd &d, int32_t i) {
-        const int32_t sg = (u.unit + i * u.nunits) * W + wave;
+        const int32_t sg = (u.unit + (i + i0) * u.nunits) * W + wave;
         const uint32_t g = sg < u.nsg ? sg0 + (uint32_t)sg : a.null_sg;
         const u32x4 *qa = reinterpret_cast<const u32x4 *>(a.npk + (size_t)g * kNSg) + lane;
         d.q = (CP & 1) ? __builtin_nontemporal_load(qa) : *qa;
@@ -507,13 +516,47 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
     }
 }
 
+// Paced sweep (PrPart::pace): the CU slot of this workgroup inside its XCD (SE, SH, CU ids of
+// HW_REG_HW_ID bits 8..15) and the XCD's progress words (HW_REG_XCC_ID).  Placement is read,
+// not assumed; it only steers speed (cdna_hip_programming.md §1: never correctness).
+__device__ __forceinline__ uint32_t *pace_slot(const SortedArgs &a) {
+    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;         // HW_REG_XCC_ID[3:0]
+    const uint32_t cu = (uint32_t)__builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4) & 255u;   // HW_REG_HW_ID[15:8]
+    return a.pace_prog + xcc * 256u + cu;
+}
+
+// Entering window `win` of generation `gen`: publish it, then wait (bounded: pace_polls polls)
+// until no unit of the same generation on this XCD is more than pace_d windows behind.  The
+// whole workgroup waits at the barriers; wave 0 polls the XCD's 256 slots with L1-bypassing
+// 16-B loads (L2-served; the slots are written with plain stores, which stay in L2).
+__device__ __forceinline__ void pace_wait(const SortedArgs &a, uint32_t *slot, uint32_t gen, uint32_t win) {
+    __syncthreads();
+    if (threadIdx.x < kWave) {
+        const uint32_t me = (gen << 16) | (win + 1);
+        if (threadIdx.x == 0) *reinterpret_cast<volatile uint32_t *>(slot) = me;
+        const gx_u32x4 *base = reinterpret_cast<const gx_u32x4 *>(a.pace_prog + (size_t)(slot - a.pace_prog) / 256 * 256);
+        for (uint32_t p = 0; p < a.pace_polls; p++) {
+            const gx_u32x4 q = __builtin_nontemporal_load(base + threadIdx.x);
+            const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+            uint32_t lo = 0xffffu;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if ((w4[j] >> 16) == gen && (w4[j] & 0xffffu)) lo = min(lo, w4[j] & 0xffffu);
+            for (int off = 32; off > 0; off >>= 1) lo = min(lo, (uint32_t)__shfl_xor((int)lo, off, kWave));
+            if (win + 1 <= lo + a.pace_d) break;
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
+    __syncthreads();
+}
+
 // One iteration's SpMV over split blocks.  Grid: [0, nlong_pad) LONG row segments (padded to a
 // multiple of 8), then the units (largest first; the blocks of rows without entries last).  A multi-unit block's units store their row sums write-through (sc1) to
 // their own slab, drain them (vmcnt(0)) and take a ticket; the last arriver adds the slabs in
 // unit order with sc1 loads and runs the epilogue (MI355X_MICROARCH.md "Valid forms": sc1 stores
 // drained before the counter add, sc1 loads by the workgroup whose add came last).
 // TIMES: debug build with per-workgroup timestamps (GX_PR_UNIT_TIMES).
-template <bool TIMES, int PROBE = 0, int CP = 0>
+template <bool TIMES, int PROBE = 0, int CP = 0, bool PACE = false>
 __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs a) {
     extern __shared__ double acc[];
     __shared__ double wred[kBS / kWave];
@@ -549,8 +592,25 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
     if (!empty) {
         for (int i = tid; i < nrows; i += kBS) acc[i] = 0.0;
         __syncthreads();
-        gather_narrow<CP, PROBE>(a, u, acc);
-        gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step);
+        if constexpr (PACE) {
+            // window by window: the narrow rounds, then the wide rounds starting in it
+            const uint32_t nw = a.pace_nw;
+            const int32_t *pr = a.pace_rounds + (size_t)(w - a.nlong_pad) * 2 * (nw + 1);
+            uint32_t *slot = pace_slot(a);
+            const uint32_t gen = (w - a.nlong_pad) / a.pace_ncus;
+            for (uint32_t win = 0; win < nw; win++) {
+                const int32_t n0 = pr[win], n1 = pr[win + 1], w0 = pr[nw + 1 + win], w1 = pr[nw + 2 + win];
+                if (n0 == n1 && w0 == w1) continue;
+                pace_wait(a, slot, gen, win);
+                if (n1 > n0) gather_narrow<CP, PROBE>(a, u, acc, n0, n1);
+                if (w1 > w0) gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step, w0, w1);
+            }
+            __syncthreads();
+            if (tid == 0) *reinterpret_cast<volatile uint32_t *>(slot) = 0u;   // this CU's sweep is over
+        } else {
+            gather_narrow<CP, PROBE>(a, u, acc);
+            gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step);
+        }
         __syncthreads();
     }
     if (TIMES && tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
@@ -878,6 +938,49 @@ __global__ __launch_bounds__(256) void k_narrow_emit(const RowBlock *__restrict_
             }
             put(c - at, spk[z0 + e] & ((1u << kRowBits) - 1), c);
         }
+    }
+}
+
+// Paced sweep plan: per unit, the first narrow round and the first wide round whose column is
+// in window w (window 0: columns below h; window w >= 1 from h + (w - 1) 2^wshift), w = 0..nw,
+// by binary searches over the unit's rounds (their first columns ascend).  One workgroup per unit.
+__global__ __launch_bounds__(64) void k_pace_rounds(const SortedUnit *__restrict__ units, uint32_t nunits,
+                                                    const uint32_t *__restrict__ nbase, const int32_t *__restrict__ sci,
+                                                    uint32_t nw, uint32_t h, uint32_t wshift, int32_t *__restrict__ out) {
+    const uint32_t ui = blockIdx.x;
+    if (ui >= nunits) return;
+    const SortedUnit u = units[ui];
+    int32_t *o = out + (size_t)ui * 2 * (nw + 1);
+    constexpr int W = kBS / kWave;
+    const int32_t nrounds = (u.nsg + W - 1) / W;
+    const int32_t nrn = u.unit >= nrounds ? 0 : (nrounds - u.unit + u.nunits - 1) / u.nunits;
+    const int32_t nrw = u.lo < u.hi ? (int32_t)((u.hi - u.lo + u.step - 1) / u.step) : 0;
+    const uint32_t sg0 = (uint32_t)(u.nbeg / kNSg);
+    for (uint32_t w = threadIdx.x; w <= nw; w += blockDim.x) {
+        int32_t rn = 0, rw = 0;
+        if (w == nw) {
+            rn = nrn;
+            rw = nrw;
+        } else if (w > 0) {
+            const uint64_t start = (uint64_t)h + ((uint64_t)(w - 1) << wshift);
+            int32_t L = 0, H = nrn;
+            while (L < H) {
+                const int32_t mid = (L + H) >> 1;
+                if ((uint64_t)nbase[sg0 + (uint32_t)((u.unit + mid * u.nunits) * W)] >= start) H = mid;
+                else L = mid + 1;
+            }
+            rn = L;
+            L = 0;
+            H = nrw;
+            while (L < H) {
+                const int32_t mid = (L + H) >> 1;
+                if ((uint64_t)(uint32_t)sci[u.lo + (int64_t)mid * u.step] >= start) H = mid;
+                else L = mid + 1;
+            }
+            rw = L;
+        }
+        o[w] = rn;
+        o[nw + 1 + w] = rw;
     }
 }
 
@@ -1297,6 +1400,27 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         GX_HIP_TRY(hipMemset(p->uticket.p, 0, p->uticket.n * 4));
     }
     p->unit_nnz = T;
+    // paced sweep (GX_PR_PACE=1; GX_PR_PACE_H first boundary column, GX_PR_PACE_W log2 window
+    // columns, GX_PR_PACE_D windows of lead, GX_PR_PACE_POLLS the bound on a wait)
+    p->pace = env_int("GX_PR_PACE", 0, 0, 1);
+    if (p->pace && p->nunits) {
+        const uint64_t ncols = p->nranks == 1 ? std::max<uint64_t>(p->n_global, 1) : p->chunk * (uint64_t)p->nranks;
+        p->pace_h = (uint32_t)env_int("GX_PR_PACE_H", 524288, 0, 1 << 30);
+        p->pace_wshift = (uint32_t)env_int("GX_PR_PACE_W", 18, 10, 30);
+        p->pace_d = (uint32_t)env_int("GX_PR_PACE_D", 1, 0, 1 << 14);
+        p->pace_polls = (uint32_t)env_int("GX_PR_PACE_POLLS", 64, 0, 1 << 20);
+        const uint64_t wcols = 1ull << p->pace_wshift;
+        p->pace_nw = 1 + (uint32_t)(ncols > p->pace_h ? (ncols - p->pace_h + wcols - 1) / wcols : 0);
+        if (p->pace_nw > 65000) p->pace_nw = 65000;
+        GX_TRY(p->pace_rounds.alloc((size_t)p->nunits * 2 * (p->pace_nw + 1)));
+        GX_TRY(p->pace_prog.alloc(8 * 256));
+        GX_HIP_TRY(hipMemsetAsync(p->pace_prog.p, 0, 8 * 256 * sizeof(uint32_t), p->ctx->stream));
+        hipLaunchKernelGGL(k_pace_rounds, dim3(p->nunits), dim3(64), 0, p->ctx->stream, p->units.p, p->nunits,
+                           p->nbase.p ? p->nbase.p : nullptr, p->sci.p, p->pace_nw, p->pace_h, p->pace_wshift,
+                           p->pace_rounds.p);
+        GX_TRY(check_launch("k_pace_rounds"));
+        GX_HIP_TRY(hipStreamSynchronize(p->ctx->stream));
+    }
     clk.mark("units");
     // fused dangling sum: every dangling row in a sorted block (none in a LONG block), one slot
     // per block holding dangling rows
@@ -1367,6 +1491,12 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.nbase = p->nbase.p;
     a.null_sg = p->null_sg;
     a.nt_col = p->nt_col;
+    a.pace_rounds = p->pace_rounds.p;
+    a.pace_prog = p->pace_prog.p;
+    a.pace_nw = p->pace_nw;
+    a.pace_d = p->pace_d;
+    a.pace_polls = p->pace_polls;
+    a.pace_ncus = (uint32_t)std::max(1, p->ctx->num_cus);
     const char *times_path = std::getenv("GX_PR_UNIT_TIMES");   // debug: not under graph capture
     const uint32_t nw = p->nlong_pad + p->nunits;
     if (times_path && nw) {
@@ -1398,7 +1528,11 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
 #endif
             // (narrow gathers three rounds deep ran the same: SYN-8_5 752-753 against 753-754
             // us, SYN-7_5 72.1-73.2 against 71.5-72.4; tools/r03_depth_ab.sh)
-            if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5>), dim3(nw), dim3(kBS), lds, s, a);
+            if (p->pace && p->nunits) {
+                if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5, true>), dim3(nw), dim3(kBS), lds, s, a);
+                else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1, true>), dim3(nw), dim3(kBS), lds, s, a);
+                else hipLaunchKernelGGL((k_pr_pull_units<false, 0, 0, true>), dim3(nw), dim3(kBS), lds, s, a);
+            } else if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5>), dim3(nw), dim3(kBS), lds, s, a);
             else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1>), dim3(nw), dim3(kBS), lds, s, a);
             else hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
         }

@@ -34,6 +34,19 @@ def cut(rp, B, R):
     return out
 
 
+def sweep_groups(rp, ci, blocks, gsize=32):
+    """Line fetches if the blocks ran in sweep groups of `gsize` (one XCD each, sweeping x in
+    lockstep, so a line is fetched once per group): blocks in size order, consecutive groups."""
+    sizes = [rp[b] - rp[a] for (a, b) in blocks]
+    order = np.argsort(sizes)[::-1]
+    total = 0
+    for g0 in range(0, len(order), gsize):
+        lines = np.unique(np.concatenate([np.unique(ci[rp[blocks[i][0]]:rp[blocks[i][1]]] >> 4)
+                                          for i in order[g0:g0 + gsize]]))
+        total += len(lines)
+    return total
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=23)
@@ -43,6 +56,7 @@ def main():
     ap.add_argument("--R", type=int, default=16320)
     ap.add_argument("--H", type=int, nargs="*", default=[65536, 524288])
     ap.add_argument("--tail-rows", type=int, nargs="*", default=[])
+    ap.add_argument("--groups", type=int, nargs="*", default=[], help="sweep-group sizes to model")
     args = ap.parse_args()
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
     t0 = time.time()
@@ -103,6 +117,10 @@ def main():
         print(f"  H={h}: hub entries {eh / 1e6:.1f} M lines {lh / 1e6:.2f} M ({eh / max(1, lh):.1f}/line); "
               f"tail entries {et / 1e6:.1f} M lines {lt / 1e6:.2f} M ({et / max(1, lt):.1f}/line); "
               f"x line bytes {(lh + lt) * 128 / 1e9:.2f} GB")
+    for gs in args.groups:
+        f = sweep_groups(rp, ci, blocks, gs)
+        print(f"  sweep groups of {gs} blocks in lockstep: {f / 1e6:.2f} M line fetches ({f * 128 / 1e9:.2f} GB)",
+              flush=True)
     # alternative: tail entries (columns >= H) regrouped by taller row ranges
     for R2 in args.tail_rows:
         for h in H:
