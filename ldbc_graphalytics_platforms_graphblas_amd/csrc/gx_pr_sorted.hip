@@ -237,8 +237,9 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // (L1 hits), 5 no gathers + conflict-free LDS adds (acc[tid]), 6 gathers + conflict-free LDS
 // adds, 7 no index loads (entries synthesised from the position, columns = the base),
 // 8 gathers of columns >= 512 Ki folded into the first 512 Ki (the sparse tail as local as the
-// hub lines), 9 every gather folded into the first 64 Ki columns.  gather_narrow takes 2, 4,
-// 8 and 9 (the others run it unchanged).
+// hub lines), 9 every gather folded into the first 64 Ki columns, 10 no entries at all (the
+// fixed costs: zeroing, epilogue, slabs), 11 as 3 (index loads and decode only).
+// gather_narrow takes all but 7 (which runs it unchanged).
 template <int PROBE, int CP>   // CP bit 0: index loads non-temporal (bit 2: gather_narrow)
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
                                              double *acc, int64_t step64, int32_t k0 = 0, int32_t k1 = 0x7fffffff) {
@@ -327,7 +328,7 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
         }
 #pragma unroll
         for (int i = 0; i < kU; i++) {
-            if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5) t.g[i] = (double)c[i];
+            if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11) t.g[i] = (double)c[i];
             else if constexpr (PROBE == 4) t.g[i] = a.x_in[c[i] & 4095];
             else if constexpr (PROBE == 8) t.g[i] = a.x_in[c[i] >= (1 << 19) ? (c[i] & ((1 << 19) - 1)) : c[i]];
             else if constexpr (PROBE == 9) t.g[i] = a.x_in[c[i] & 65535];
@@ -338,7 +339,7 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
     auto add = [&](const Gt &t) {
 #pragma unroll
         for (int i = 0; i < kU; i++) {
-            if constexpr (PROBE == 1 || PROBE == 3) rsum += t.g[i];
+            if constexpr (PROBE == 1 || PROBE == 3 || PROBE == 11) rsum += t.g[i];
             else if constexpr (PROBE == 5 || PROBE == 6) atomicAdd(&acc[tid], t.g[i]);
             else atomicAdd(&acc[t.r[i]], t.g[i]);
         }
@@ -381,7 +382,7 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
     } else {
         add(tA);
     }
-    if constexpr (PROBE == 1 || PROBE == 3) atomicAdd(&acc[tid], rsum);
+    if constexpr (PROBE == 1 || PROBE == 3 || PROBE == 11) atomicAdd(&acc[tid], rsum);
 }
 
 // Inclusive prefix sum over the 64 lanes by DPP moves (row_shr 1/2/4/8 inside each 16-lane
@@ -463,11 +464,11 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
             col[k] = bk + ((sk >> (8 * (k & 3))) & 255u);
             bk += (tk >> (8 * (k & 3))) & 255u;
         }
-        if constexpr (PROBE == 2 || PROBE == 4 || PROBE == 8 || PROBE == 9) {
+        if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11 || PROBE == 4 || PROBE == 8 || PROBE == 9) {
 #pragma unroll
             for (int k = 0; k < kU; k++) {
                 const uint32_t c = col[k];
-                if constexpr (PROBE == 2) t.g[k] = (double)c;
+                if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11) t.g[k] = (double)c;
                 else if constexpr (PROBE == 4) t.g[k] = a.x_in[c & 4095u];
                 else if constexpr (PROBE == 8) t.g[k] = a.x_in[c >= (1u << 19) ? (c & ((1u << 19) - 1)) : c];
                 else t.g[k] = a.x_in[c & 65535u];
@@ -481,9 +482,14 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
             for (int k = 0; k < kU; k++) t.g[k] = *reinterpret_cast<const double *>(xb + (col[k] << 3));
         }
     };
+    double rsum = 0.0;   // PROBE 1 / 3 / 11: register sum instead of the LDS adds
     auto add = [&](const Gt &t) {
 #pragma unroll
-        for (int k = 0; k < kU; k++) atomicAdd(&acc[t.r[k]], t.g[k]);
+        for (int k = 0; k < kU; k++) {
+            if constexpr (PROBE == 1 || PROBE == 3 || PROBE == 11) rsum += t.g[k];
+            else if constexpr (PROBE == 5 || PROBE == 6) atomicAdd(&acc[threadIdx.x], t.g[k]);
+            else atomicAdd(&acc[t.r[k]], t.g[k]);
+        }
     };
     Rd dA, dB;
     Gt tA, tB;
@@ -514,6 +520,7 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
     } else {
         add(tA);
     }
+    if constexpr (PROBE == 1 || PROBE == 3 || PROBE == 11) atomicAdd(&acc[threadIdx.x], rsum);
 }
 
 // Paced sweep (PrPart::pace): the CU slot of this workgroup inside its XCD (SE, SH, CU ids of
@@ -607,7 +614,7 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
             }
             __syncthreads();
             if (tid == 0) *reinterpret_cast<volatile uint32_t *>(slot) = 0u;   // this CU's sweep is over
-        } else {
+        } else if constexpr (PROBE != 10) {   // probe 10: no entries at all (the fixed costs)
             gather_narrow<CP, PROBE>(a, u, acc);
             gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step);
         }
@@ -1520,7 +1527,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
 #define GX_PROBE_CASE(k) case k: if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, k, 5>), dim3(nw), dim3(kBS), lds, s, a); \
                                  else hipLaunchKernelGGL((k_pr_pull_units<false, k>), dim3(nw), dim3(kBS), lds, s, a); break;
                 GX_PROBE_CASE(1) GX_PROBE_CASE(2) GX_PROBE_CASE(3) GX_PROBE_CASE(4) GX_PROBE_CASE(5) GX_PROBE_CASE(6) GX_PROBE_CASE(7)
-                GX_PROBE_CASE(8) GX_PROBE_CASE(9)
+                GX_PROBE_CASE(8) GX_PROBE_CASE(9) GX_PROBE_CASE(10) GX_PROBE_CASE(11)
 #undef GX_PROBE_CASE
                 default: hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
                 }
