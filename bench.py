@@ -80,7 +80,7 @@ KERNELS = {"bfs": ["bfs_topdown", "bfs_bottomup"], "wcc": ["wcc_sample", "wcc_ho
            "sssp": ["sssp_relax", "sssp_advance"],
            "cdlp": ["cdlp_tiny", "cdlp_small", "cdlp_light_s", "cdlp_light", "cdlp_mid2", "cdlp_mid4", "cdlp_mid",
                     "cdlp_heavy", "cdlp_first", "cdlp_mark", "cdlp_sparse"],
-           "lcc": ["lcc_orient", "lcc_triangles"]}
+           "lcc": ["lcc_orient", "lcc_triangles", "lcc_core"]}
 
 
 def usable_cores() -> int:

@@ -25,6 +25,7 @@
 // Oriented entries are packed as (vertex << 2) | popcount(flag), so n < 2^29.
 // Counts are exact integers, so the result is deterministic and equal to the oracle bit for
 // bit (one fp64 division per vertex).
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -43,6 +44,8 @@ constexpr int kWave2Max = 512;         // ... and <= 512 (1024-slot tables)
 constexpr int kBlockMax = 8192;        // workgroup tier: table sized to the tier's largest |O(u)|
 constexpr int kBlockSlots = 16384;     //   (dynamic LDS, at most 128 KiB)
 constexpr uint32_t kCntMask = (1u << 30) - 1;   // hash value: flag popcount << 30 | x count
+constexpr uint32_t kVMask = (1u << 29) - 1;     // in-orientation entry: core bit 31 | v << 2 | popcount
+constexpr uint32_t kCoreBit = 1u << 31;
 
 __device__ __forceinline__ bool ranks_above(int64_t du, int32_t u, int64_t dv, int32_t v) {
     return du > dv || (du == dv && u > v);
@@ -242,10 +245,13 @@ __device__ __forceinline__ unsigned long long probe_in_group(const int64_t *__re
     const int64_t i = ib + lane;
     const bool has = i < ie;
     const uint32_t ic = has ? icode[i] : 0u;
-    const int32_t v = (int32_t)(ic >> 2);
+    const int32_t v = (int32_t)((ic >> 2) & kVMask);
     const uint32_t p_vu = ic & 3u;
-    const int64_t vb = has ? orp[v] : 0;
-    const int32_t vl = has ? (int32_t)(orp[v + 1] - vb) : 0;
+    // a dense-core in-neighbour (core bit): its triangles {v, u, x} lie wholly in the core
+    // (u and x rank above v) and are counted by the core's MFMA pass (k_lcc_core_mfma)
+    const bool walk = has && !(ic & kCoreBit);
+    const int64_t vb = walk ? orp[v] : 0;
+    const int32_t vl = walk ? (int32_t)(orp[v + 1] - vb) : 0;
     int32_t incl = vl;
 #pragma unroll
     for (int off = 1; off < kWave; off <<= 1) {
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_wave(const int64_t *__restric
             probe_in_group(orp, ocode, icode, ib, ie, hkey, hval, slots - 1, vcnt, lane, &s_ws[wv]);
         wave_sync_lds();
         const uint32_t c = vcnt[lane];
-        if (c && ib + lane < ie) atomicAdd(&tc[icode[ib + lane] >> 2], (unsigned long long)c);
+        if (c && ib + lane < ie) atomicAdd(&tc[(icode[ib + lane] >> 2) & kVMask], (unsigned long long)c);
         for (uint32_t s = lane; s < slots; s += kWave) {
             const uint32_t cx = hval[s] & kCntMask;
             if (cx) atomicAdd(&tc[hkey[s]], (unsigned long long)cx);
@@ -371,7 +377,7 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_block(const int64_t *__restri
         if (ib < ie) tu = probe_in_group(orp, ocode, icode, ib, ie, hkey, hval, slots - 1, vcnt, lane, &s_ws[wv]);
         wave_sync_lds();
         const uint32_t c = vcnt[lane];
-        if (c && ib + lane < ie) atomicAdd(&tc[icode[ib + lane] >> 2], (unsigned long long)c);
+        if (c && ib + lane < ie) atomicAdd(&tc[(icode[ib + lane] >> 2) & kVMask], (unsigned long long)c);
         for (int off = 32; off > 0; off >>= 1) tu += __shfl_xor(tu, off, kWave);
         if (lane == 0) s_tu[wv] = tu;
         __syncthreads();
@@ -399,7 +405,8 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_merge_in(const int64_t *__res
     for (int64_t t = irp[u] + (int64_t)blockIdx.x * kLccBlock + threadIdx.x; t < irp[u + 1];
          t += (int64_t)gridDim.x * kLccBlock) {
         const uint32_t ic = icode[t];
-        const int32_t v = (int32_t)(ic >> 2);
+        if (ic & kCoreBit) continue;   // wholly in the dense core (k_lcc_core_mfma)
+        const int32_t v = (int32_t)((ic >> 2) & kVMask);
         const uint32_t p_vu = ic & 3u;
         int64_t i = orp[v], j = ub;
         const int64_t ie = orp[v + 1];
@@ -434,7 +441,7 @@ __global__ __launch_bounds__(kLccBlock) void k_lcc_work(const int64_t *__restric
     for (int64_t u = ((int64_t)blockIdx.x * kLccBlock + threadIdx.x) / kWave; u < n; u += nw) {
         uint64_t w = 0;
         for (int64_t k = irp[u] + lane; k < irp[u + 1]; k += kWave) {
-            const int32_t v = (int32_t)(icode[k] >> 2);
+            const int32_t v = (int32_t)((icode[k] >> 2) & kVMask);
             w += 1 + (uint64_t)(orp[v + 1] - orp[v]);
         }
         for (int off = 32; off > 0; off >>= 1) w += __shfl_xor(w, off, kWave);
@@ -449,6 +456,143 @@ __global__ void k_lcc_final(const int64_t *__restrict__ srp, const unsigned long
         const int64_t k = srp[v + 1] - srp[v];
         out[v] = k < 2 ? 0.0 : (double)tc[v] / ((double)k * (double)(k - 1));
     }
+}
+
+// ---- dense core on the matrix cores ----
+// The vertices of closure degree > dcut (the top of the orientation order, so every triangle
+// whose lowest-ranked vertex is in the core lies wholly in it) form a small, dense K x K block
+// of S: on SYN-cit the 4 K highest-degree vertices hold 15.5 % of the hash kernels' probe work
+// at 9 % density, the 8 K highest 34 % at 5 % (tools/dense_tiles.py).  Its
+// triangles are counted as a masked dense product: with W[j][k] the number of stored directions
+// between core vertices j and k (0, 1, 2) and B = (W > 0),
+//     t(i) = 1/2 sum_j B[i][j] (W B)[j][i],
+// each core triangle {i, j, k} adding w(j, k) at i, as the hash kernels do.  W B is an int8
+// GEMM on v_mfma_i32_32x32x32_i8 (exact int32 sums), the mask and the row sums fused into its
+// epilogue, 64 x 64 output tiles whose mask is empty skipped.  The hash kernels skip the
+// in-neighbours v in the core (core bit of the in-orientation entry), i.e. exactly the core's
+// triangles.
+constexpr int kCoreWG = 128;   // output tile of a workgroup (4 waves of 64 x 64)
+
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
+
+// closure degree and id of every vertex (a stable descending sort of the degrees follows)
+__global__ void k_core_degkeys(const int64_t *__restrict__ srp, int64_t n, uint32_t *__restrict__ deg,
+                               int32_t *__restrict__ ids) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        deg[v] = (uint32_t)(srp[v + 1] - srp[v]);
+        ids[v] = (int32_t)v;
+    }
+}
+
+// core index of the first K vertices of the degree-descending order (coreidx pre-filled -1)
+__global__ void k_core_place(const int32_t *__restrict__ sorted_ids, int32_t K, int32_t *__restrict__ coreidx,
+                             int32_t *__restrict__ corev) {
+    for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < K; i += gridDim.x * blockDim.x) {
+        const int32_t v = sorted_ids[i];
+        coreidx[v] = i;
+        corev[i] = v;
+    }
+}
+
+// W and B rows of the core (one wave per core vertex), and the 64 x 64 tiles holding entries
+__global__ __launch_bounds__(256) void k_core_fill(const int64_t *__restrict__ srp, const int32_t *__restrict__ sci,
+                                                   const uint8_t *__restrict__ sflag, const int32_t *__restrict__ coreidx,
+                                                   const int32_t *__restrict__ corev, int32_t K, int32_t Kp,
+                                                   int8_t *__restrict__ W, int8_t *__restrict__ B,
+                                                   uint8_t *__restrict__ tmask) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int32_t nt = Kp / 64;
+    for (int32_t i = (blockIdx.x * 256 + threadIdx.x) / kWave; i < K; i += gridDim.x * 256 / kWave) {
+        const int32_t v = corev[i];
+        for (int64_t e = srp[v] + lane; e < srp[v + 1]; e += kWave) {
+            const int32_t c = coreidx[sci[e]];
+            if (c < 0) continue;
+            W[(int64_t)i * Kp + c] = (int8_t)__popc((uint32_t)sflag[e]);
+            B[(int64_t)i * Kp + c] = 1;
+            tmask[(i / 64) * nt + c / 64] = 1;
+        }
+    }
+}
+
+// the core bit on every in-orientation entry whose source v is in the core
+__global__ void k_core_mark_in(uint32_t *__restrict__ icode, int64_t m, const int32_t *__restrict__ coreidx) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t ic = icode[k];
+        if (coreidx[(ic >> 2) & kVMask] >= 0) icode[k] = ic | kCoreBit;
+    }
+}
+
+// P = W B over 128 x 128 workgroup tiles, each wave 64 x 64 (2 x 2 MFMA tiles of 32 x 32, k
+// steps of 32), then t(i) += sum_j B[j][i] P[j][i] over the tile's rows j.  W and B are
+// symmetric, row-major Kp x Kp int8: the A operand (rows j) and the B operand (column i = row
+// i of B) are both 16 contiguous bytes per lane (lane l: row l & 31, k = 16 (l >> 5) + 0..15).
+// C/D: column lane & 31, row (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5).
+__global__ __launch_bounds__(256) void k_lcc_core_mfma(const int8_t *__restrict__ W, const int8_t *__restrict__ B,
+                                                       const uint8_t *__restrict__ tmask, int32_t Kp,
+                                                       unsigned long long *__restrict__ tcore) {
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int32_t nwg = Kp / kCoreWG;
+    const int32_t J0 = (int32_t)(blockIdx.x / nwg) * kCoreWG + (wv >> 1) * 64;
+    const int32_t I0 = (int32_t)(blockIdx.x % nwg) * kCoreWG + (wv & 1) * 64;
+    if (!tmask[(J0 / 64) * (Kp / 64) + I0 / 64]) return;   // B[j][i] = 0 over the tile: nothing to add
+    const int r = lane & 31, h = lane >> 5;
+    const int8_t *a0 = W + (int64_t)(J0 + r) * Kp + 16 * h, *a1 = a0 + (int64_t)32 * Kp;
+    const int8_t *b0 = B + (int64_t)(I0 + r) * Kp + 16 * h, *b1 = b0 + (int64_t)32 * Kp;
+    i32x16 acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) acc[m][n][q] = 0;
+    i32x4 fa0 = *reinterpret_cast<const i32x4 *>(a0), fa1 = *reinterpret_cast<const i32x4 *>(a1);
+    i32x4 fb0 = *reinterpret_cast<const i32x4 *>(b0), fb1 = *reinterpret_cast<const i32x4 *>(b1);
+    for (int32_t k = 32; k <= Kp; k += 32) {
+        i32x4 na0, na1, nb0, nb1;
+        if (k < Kp) {   // the next k step's fragments, in flight while this one multiplies
+            na0 = *reinterpret_cast<const i32x4 *>(a0 + k);
+            na1 = *reinterpret_cast<const i32x4 *>(a1 + k);
+            nb0 = *reinterpret_cast<const i32x4 *>(b0 + k);
+            nb1 = *reinterpret_cast<const i32x4 *>(b1 + k);
+        }
+        acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0, fb1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1, fb1, acc[1][1], 0, 0, 0);
+        if (k < Kp) {
+            fa0 = na0;
+            fa1 = na1;
+            fb0 = nb0;
+            fb1 = nb1;
+        }
+    }
+    // epilogue: lane's column i = I0 + 32 n + r; its rows j = J0 + 32 m + 8 g + 4 h + (0..3);
+    // the mask B[j][i] = B[i][j] (symmetric): four contiguous bytes of row i per (m, g)
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        const int32_t i = I0 + 32 * n + r;
+        const int8_t *brow = B + (int64_t)i * Kp;
+        int64_t s = 0;
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint32_t mk = *reinterpret_cast<const uint32_t *>(brow + J0 + 32 * m + 8 * g + 4 * h);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if ((mk >> (8 * q)) & 0xffu) s += acc[m][n][4 * g + q];
+            }
+        s += __shfl_xor(s, 32, kWave);
+        if (h == 0 && s) atomicAdd(&tcore[i], (unsigned long long)s);
+    }
+}
+
+// tc[corev[i]] += tcore[i] / 2 (each core pair (j, k) came in both orders)
+__global__ void k_core_final(const unsigned long long *__restrict__ tcore, const int32_t *__restrict__ corev, int32_t K,
+                             unsigned long long *__restrict__ tc) {
+    for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < K; i += gridDim.x * blockDim.x)
+        if (tcore[i]) atomicAdd(&tc[corev[i]], tcore[i] / 2);
 }
 
 // Degree-ordered orientation O of the closure S (CSR orp / ocode) and its transpose I
@@ -617,7 +761,77 @@ struct LccCache {
     LccItems L;
     DBuf<unsigned long long> tc;
     DBuf<double> out;
+    // dense core (GX_LCC_CORE = its largest size; 0: none)
+    int32_t K = 0, Kp = 0;
+    DBuf<int32_t> coreidx, corev;
+    DBuf<int8_t> W, B;
+    DBuf<uint8_t> tmask;
+    DBuf<unsigned long long> tcore;
 };
+
+// The dense core of gx_lcc (k_lcc_core_mfma): the vertices of closure degree above the
+// (kmax + 1)-th largest degree, at most kmax of them; their W / B rows and tile mask, and the
+// core bit on the in-orientation entries.  Built once with the cached orientation.
+int lcc_core_build(gx_graph *g, LccCache &C, int32_t kmax, hipStream_t s) {
+    const int64_t n = (int64_t)g->n;
+    const DevCSR &S = g->S;
+    if (kmax <= 0 || n <= kmax) return GX_SUCCESS;
+    int32_t K = 0;
+    {
+        DBuf<uint32_t> d0, d1;
+        DBuf<int32_t> i0, i1;
+        GX_TRY(d0.alloc(n));
+        GX_TRY(d1.alloc(n));
+        GX_TRY(i0.alloc(n));
+        GX_TRY(i1.alloc(n));
+        hipLaunchKernelGGL(k_core_degkeys, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, S.rp.p, n, d0.p, i0.p);
+        GX_TRY(check_launch("k_core_degkeys"));
+        GX_TRY(sort_pairs_desc_u32_i32(d0.p, d1.p, i0.p, i1.p, (size_t)n, s));
+        std::vector<uint32_t> top((size_t)kmax + 1);
+        GX_HIP_TRY(hipMemcpyAsync(top.data(), d1.p, top.size() * 4, hipMemcpyDeviceToHost, s));
+        GX_HIP_TRY(hipStreamSynchronize(s));
+        const uint32_t dcut = top[(size_t)kmax];
+        while (K < kmax && top[(size_t)K] > dcut) K++;   // every vertex of degree > dcut: upward closed
+        if (K < kCoreWG) return GX_SUCCESS;
+        C.K = K;
+        C.Kp = (K + kCoreWG - 1) / kCoreWG * kCoreWG;
+        GX_TRY(C.coreidx.alloc(n));
+        GX_TRY(C.corev.alloc(K));
+        GX_HIP_TRY(hipMemsetAsync(C.coreidx.p, 0xff, n * 4, s));
+        hipLaunchKernelGGL(k_core_place, dim3(grid_for(K, 256, 1024)), dim3(256), 0, s, i1.p, K, C.coreidx.p, C.corev.p);
+        GX_TRY(check_launch("k_core_place"));
+        GX_HIP_TRY(hipStreamSynchronize(s));   // the sort buffers are freed at the end of the block
+    }
+    const int64_t kp = C.Kp, nt = kp / 64;
+    GX_TRY(C.W.alloc(kp * kp, 16));
+    GX_TRY(C.B.alloc(kp * kp, 16));
+    GX_TRY(C.tmask.alloc(nt * nt));
+    GX_TRY(C.tcore.alloc(kp));
+    GX_HIP_TRY(hipMemsetAsync(C.W.p, 0, kp * kp, s));
+    GX_HIP_TRY(hipMemsetAsync(C.B.p, 0, kp * kp, s));
+    GX_HIP_TRY(hipMemsetAsync(C.tmask.p, 0, nt * nt, s));
+    hipLaunchKernelGGL(k_core_fill, dim3(grid_for((uint64_t)K * kWave, 256, 8192)), dim3(256), 0, s, S.rp.p, S.ci.p,
+                       S.flag.p, C.coreidx.p, C.corev.p, K, C.Kp, C.W.p, C.B.p, C.tmask.p);
+    GX_TRY(check_launch("k_core_fill"));
+    if (C.O.m)
+        hipLaunchKernelGGL(k_core_mark_in, dim3(grid_for(C.O.m, 256, 16384)), dim3(256), 0, s, C.O.icode.p, C.O.m,
+                           C.coreidx.p);
+    GX_TRY(check_launch("k_core_mark_in"));
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    return GX_SUCCESS;
+}
+
+int lcc_core_count(gx_graph *g, LccCache &C, unsigned long long *tc, hipStream_t s) {
+    if (!C.K) return GX_SUCCESS;
+    KTimer kt(g->ctx, "lcc_core", s);
+    GX_HIP_TRY(hipMemsetAsync(C.tcore.p, 0, (size_t)C.Kp * 8, s));
+    const int32_t nwg = C.Kp / kCoreWG;
+    hipLaunchKernelGGL(k_lcc_core_mfma, dim3((unsigned)nwg * nwg), dim3(256), 0, s, C.W.p, C.B.p, C.tmask.p, C.Kp,
+                       C.tcore.p);
+    GX_TRY(check_launch("k_lcc_core_mfma"));
+    hipLaunchKernelGGL(k_core_final, dim3(grid_for(C.K, 256, 1024)), dim3(256), 0, s, C.tcore.p, C.corev.p, C.K, tc);
+    return check_launch("k_core_final");
+}
 
 }  // namespace
 }  // namespace gx
@@ -639,6 +853,10 @@ extern "C" int gx_lcc(gx_graph *g, double *lcc) {
     if (!C) {
         auto fresh = std::make_shared<LccCache>();
         GX_TRY(lcc_orient(g, fresh->O, s));
+        // the dense core (GX_LCC_CORE = its largest size, 0 none), before the items are cut:
+        // its in-orientation entries carry the core bit the hash kernels skip
+        const char *ce = std::getenv("GX_LCC_CORE");
+        GX_TRY(lcc_core_build(g, *fresh, ce ? std::atoi(ce) : 0, s));
         GX_TRY(lcc_items(fresh->O, 0, n, fresh->L, s));
         GX_TRY(fresh->tc.alloc(n));
         GX_TRY(fresh->out.alloc(n));
@@ -647,6 +865,7 @@ extern "C" int gx_lcc(gx_graph *g, double *lcc) {
     }
     GX_HIP_TRY(hipMemsetAsync(C->tc.p, 0, n * 8, s));
     GX_TRY(lcc_count_items(g, C->O, C->L, C->tc.p, s));
+    GX_TRY(lcc_core_count(g, *C, C->tc.p, s));
     hipLaunchKernelGGL(k_lcc_final, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->S.rp.p, C->tc.p, n, C->out.p);
     GX_TRY(check_launch("k_lcc_final"));
     GX_TRY(device_end(ctx));
