@@ -152,6 +152,8 @@ struct PrPart {
     // (narrow rounds, then wide rounds: units x 2 (nw + 1)); per XCD one progress word per CU
     // slot.  The units of one XCD and generation keep within pace_d windows of each other, so
     // the x lines one fetches into the XCD's L2 are still there for the others.
+    bool rows_desc = false;      // row lengths non-increasing (an undirected hub-first plan): the
+                                 // block cut jumps by binary search
     int pace = 0;
     uint32_t pace_nw = 0, pace_h = 0, pace_wshift = 18, pace_d = 1, pace_polls = 64;
     DBuf<int32_t> pace_rounds;

@@ -1082,6 +1082,27 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     std::vector<std::pair<int64_t, int32_t>> longrows;
     int32_t nsegs = 0;
     int64_t r = 0;
+    if (p->rows_desc) {
+        // lengths non-increasing: the LONG rows are a prefix, and each block's end is the row
+        // limit or the last row pointer within B of its start, found by binary search (the
+        // row-by-row loop below took 3.5 ms for SYN-8_5's 8.4 M rows; this cut is the same)
+        while (r < rows && h_rp[r + 1] - h_rp[r] > LT) {
+            longrows.push_back({h_rp[r + 1] - h_rp[r], (int32_t)r});
+            r++;
+        }
+        while (r < rows) {
+            const int64_t start = r, lim = std::min<int64_t>(rows, start + R);
+            const int64_t limit = h_rp[start] + B;
+            int64_t lo = start + 1, hi = lim + 1;   // first e in (start, lim] with h_rp[e] > limit
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) / 2;
+                if (h_rp[mid] > limit) hi = mid;
+                else lo = mid + 1;
+            }
+            r = std::max<int64_t>(start + 1, lo - 1);
+            sortb.push_back({h_rp[start], h_rp[r], (int32_t)start, (int32_t)r, -1, 0});
+        }
+    }
     while (r < rows) {
         const int64_t len = h_rp[r + 1] - h_rp[r];
         if (len > LT) {
@@ -1151,6 +1172,13 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     std::vector<int64_t> h_nbeg(sortb.size(), 0);
     p->ncodes = 0;
     p->nnarrow = 0;
+    // device temporaries of the plan, released after the unit-size search (which runs on the
+    // host while the narrow codes and the lane permutation are built)
+    DBuf<int32_t> d_seg_row;
+    DBuf<SegDesc> d_segd;
+    DBuf<int64_t> srow;
+    DBuf<uint32_t> d_fill, d_noff, d_nsplit, d_ncode;
+    DBuf<int64_t> d_nbeg;
     if (nnz > 0) {
         // segments in row order: the sorted blocks and the LONG rows
         std::vector<std::pair<int32_t, int32_t>> order_;   // (first row, index: block i >= 0, LONG row -1 - j)
@@ -1175,8 +1203,6 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         while ((1ull << colbits) < ncols) colbits++;
         int segbits = 1;
         while ((1ull << segbits) < segd.size()) segbits++;
-        DBuf<int32_t> d_seg_row;
-        DBuf<SegDesc> d_segd;
         GX_TRY(d_seg_row.alloc(seg_row.size()));
         GX_TRY(d_segd.alloc(segd.size()));
         GX_HIP_TRY(hipMemcpyAsync(d_seg_row.p, seg_row.data(), seg_row.size() * 4, hipMemcpyHostToDevice, s));
@@ -1190,7 +1216,6 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         const KeySrc ks{p->rp, rows, p->src_rp, p->src_ci, p->src_order, p->src_perm, d_seg_row.p,
                         (int32_t)segd.size(), colbits, (int32_t)((1ll << gbits) - 1)};
         const int64_t nslabs = (int64_t)((nnz + kWave - 1) / kWave);
-        DBuf<int64_t> srow;
         GX_TRY(srow.alloc(nslabs + 1));
         GX_TRY(slab_rows(p->rp, rows, nslabs, srow.p, s));
         clk.mark("segments + slab rows");
@@ -1232,8 +1257,6 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         GX_TRY(check_launch("k_sorted_pack"));
         clk.mark("keys + sort + pack");
         // the narrow prefixes (GX_PR_NARROW=0: none) and their codes, before the lane permutation
-        DBuf<uint32_t> d_fill, d_noff, d_nsplit, d_ncode;
-        DBuf<int64_t> d_nbeg;
         if (!sortb.empty()) {
             const unsigned nsb = (unsigned)sortb.size();
             GX_TRY(d_fill.alloc(std::max<int64_t>(ngroups, 1)));
@@ -1275,7 +1298,6 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                                p->spk.p, p->sci.p);
             GX_TRY(check_launch("k_sorted_laneperm"));
         }
-        GX_HIP_TRY(hipStreamSynchronize(s));   // the segment tables are freed at return
     }
     p->ci = p->sci.p;   // the LONG rows read their (column-sorted) entries there
     clk.mark("laneperm");
@@ -1294,6 +1316,7 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         const int64_t En = std::min<int64_t>(E, 256 * (int64_t)h_nsplit[i]);
         return En + (E - En) * wide_cost4 / 4;
     };
+    if (sortb.empty()) GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries above
     if (!sortb.empty()) {
         if (std::getenv("GX_PR_UNIT_NNZ")) {
             T = env_int("GX_PR_UNIT_NNZ", 65536, 1024, 1 << 30);
@@ -1339,6 +1362,7 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
             if (env_int("GX_PR_VERBOSE", 0, 0, 1))
                 std::fprintf(stderr, "[gx_pr] unit size %lld: simulated launch %.1f us\n", (long long)T, best);
         }
+        GX_HIP_TRY(hipStreamSynchronize(s));   // narrow codes + lane permutation done: temporaries may go
         clk.mark("unit size");
         std::vector<SortedUnit> units;
         int64_t slab = 0;

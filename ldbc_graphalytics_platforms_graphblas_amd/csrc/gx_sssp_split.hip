@@ -122,13 +122,12 @@ __device__ __forceinline__ int64_t sbucket(unsigned long long bits, double inv_d
 __device__ __forceinline__ uint32_t nchunks(int64_t len) { return (uint32_t)max<int64_t>(1, (len + kSChunk - 1) / kSChunk); }
 
 // ---- tile reservations ----
-// A kernel that queues vertices works in tiles of kTile elements per workgroup: each element
+// A kernel that queues vertices works in tiles of kSB * kPer elements per workgroup: each element
 // takes its offsets inside the tile from LDS atomics, then one thread per queue reserves the
 // tile's range with one global atomic.  A shared counter then sees one atomic per queue and
 // tile instead of one per wave (same-address atomics serialise at ~11-20 ns each: the first
 // version of this file spent most of its time there).
 constexpr int kPer = 8;                    // elements per thread and tile
-constexpr int kTile = kSB * kPer;
 enum : int { kQFv = 0, kQFi, kQSv, kQSi, kQOvf, kQRing, kQCat = kQRing + kW };
 
 // elements per thread for `tot` elements over the grid: the full kPer only when the input
