@@ -571,43 +571,6 @@ void host_copy(void *dst, const void *src, size_t bytes) {
     }
 }
 
-// The degree sequence of rp sorted descending, as row pointers nrp (n + 1) and lengths nout
-// (n): what a stable descending sort of the rows by length yields, computed from a histogram
-// of the lengths without moving any row (gx_pagerank's hub-first plan of an undirected graph
-// needs only these on the host).  Threaded: per-thread histograms, then every length fills
-// its own contiguous range.
-void host_sorted_lengths(const int64_t *rp, uint64_t n, int64_t *nrp, int32_t *nout) {
-    int64_t maxd = 0;
-#pragma omp parallel for schedule(static) reduction(max : maxd)
-    for (int64_t v = 0; v < (int64_t)n; v++) maxd = std::max(maxd, rp[v + 1] - rp[v]);
-    const int nt = omp_get_max_threads();
-    std::vector<std::vector<int64_t>> hist(nt);
-#pragma omp parallel
-    {
-        std::vector<int64_t> &h = hist[omp_get_thread_num()];
-        h.assign((size_t)maxd + 1, 0);
-#pragma omp for schedule(static)
-        for (int64_t v = 0; v < (int64_t)n; v++) h[(size_t)(rp[v + 1] - rp[v])]++;
-    }
-    std::vector<int64_t> cnt((size_t)maxd + 1, 0), pos((size_t)maxd + 2, 0), base((size_t)maxd + 2, 0);
-    for (const auto &h : hist)
-        for (size_t d = 0; d < h.size(); d++) cnt[d] += h[d];
-    // descending: the longest rows first
-    for (int64_t d = maxd; d >= 0; d--) {
-        pos[(size_t)d] = pos[(size_t)d + 1] + (d < maxd ? cnt[(size_t)d + 1] : 0);
-        base[(size_t)d] = base[(size_t)d + 1] + (d < maxd ? cnt[(size_t)d + 1] * (d + 1) : 0);
-    }
-#pragma omp parallel for schedule(dynamic, 64)
-    for (int64_t d = 0; d <= maxd; d++) {
-        const int64_t c = cnt[(size_t)d], p0 = pos[(size_t)d], b0 = base[(size_t)d];
-        for (int64_t k = 0; k < c; k++) {
-            nout[p0 + k] = (int32_t)d;
-            nrp[p0 + k] = b0 + k * d;
-        }
-    }
-    nrp[n] = n ? rp[n] - rp[0] : 0;
-}
-
 int host_threads() { return omp_get_max_threads(); }
 
 void host_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }

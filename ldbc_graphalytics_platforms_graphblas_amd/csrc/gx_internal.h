@@ -38,8 +38,6 @@ void host_hub_order(const uint64_t *rp, uint64_t n, uint32_t *order);
 void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows, uint64_t nrows, const int32_t *colmap,
                     int64_t *out_rp, int32_t *out_ci);
 // CSR of A' (rows sorted)
-// descending length sequence of the rows of rp: row pointers nrp (n + 1) and lengths nout (n)
-void host_sorted_lengths(const int64_t *rp, uint64_t n, int64_t *nrp, int32_t *nout);
 // OpenMP threads of the calling host thread (gx_*_multi gives each device's thread a share)
 int host_threads();
 void host_set_threads(int n);

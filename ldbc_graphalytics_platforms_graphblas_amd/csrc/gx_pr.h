@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <vector>
 
+#include <algorithm>
+
 #include "gx_device.h"
 
 namespace gx {
@@ -179,15 +181,38 @@ struct PrPart {
     DBuf<int32_t> perm;        // old vertex id -> position in the hub-first order
 };
 
-// Read-only host array (a std::vector, or a buffer the plan filled without zeroing it).
+// A non-increasing sequence of n row lengths as its runs of equal values: run k covers
+// positions [pos[k], pos[k+1]) with length val[k], and base[k] entries come before it.  The row
+// pointers and lengths of an undirected graph's hub-first rows, known from the device's sorted
+// degrees without moving 12 n bytes to the host (pr_single_plan).
+struct LengthRuns {
+    std::vector<int64_t> pos, val, base;
+    uint64_t n = 0;
+    int64_t total = 0;
+    size_t run(uint64_t i) const {
+        return (size_t)(std::upper_bound(pos.begin(), pos.end(), (int64_t)i) - pos.begin()) - 1;
+    }
+    int64_t prefix(uint64_t i) const {
+        if (i >= n) return total;
+        const size_t k = run(i);
+        return base[k] + ((int64_t)i - pos[k]) * val[k];
+    }
+    int64_t length(uint64_t i) const { return val[run(i)]; }
+};
+
+// Read-only host array (a std::vector, or a buffer the plan filled without zeroing it), or the
+// row pointers (prefix) / lengths of a LengthRuns.  Elements are values, not references.
 template <typename T>
 struct HostView {
     const T *p = nullptr;
     size_t n = 0;
+    const LengthRuns *runs = nullptr;
+    bool prefix = false;
     HostView(const std::vector<T> &v) : p(v.data()), n(v.size()) {}
     HostView(const T *ptr, size_t count) : p(ptr), n(count) {}
+    HostView(const LengthRuns *r, bool pre) : n(pre ? r->n + 1 : r->n), runs(r), prefix(pre) {}
     size_t size() const { return n; }
-    const T &operator[](size_t i) const { return p[i]; }
+    T operator[](size_t i) const { return p ? p[i] : (T)(prefix ? runs->prefix(i) : runs->length(i)); }
 };
 
 // Build the row-block plan and dangling list from a local pull CSR (host row pointers

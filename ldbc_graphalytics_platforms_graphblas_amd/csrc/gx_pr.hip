@@ -531,6 +531,18 @@ __global__ void k_hub_apply(const int32_t *__restrict__ sorted_ids, int64_t n, c
     }
 }
 
+// Runs of equal values in the sorted (non-increasing) degrees: (position << 32 | degree) of
+// every run's first element, in any order; the count may pass `cap` (then nothing past it is
+// written and the caller falls back to the full arrays).
+__global__ void k_degree_runs(const uint32_t *__restrict__ sdeg, int64_t n, uint64_t *__restrict__ runs,
+                              uint32_t *__restrict__ count, uint32_t cap) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i > 0 && sdeg[i] == sdeg[i - 1]) continue;
+        const uint32_t k = atomicAdd(count, 1u);
+        if (k < cap) runs[k] = ((uint64_t)i << 32) | sdeg[i];
+    }
+}
+
 // Device `d` of `ndev` (gx_pagerank_multi's interleaved partition): its local row j is hub-first
 // position i = d + j ndev; the row's source vertex, out-degree and pull length (plen[rows] = 0
 // for the exclusive scan).
@@ -684,22 +696,13 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     GX_HIP_TRY(hipMemsetAsync(p->xb.p, 0, p->chunk * sizeof(double), s));
     GX_TRY(p->rank_out.alloc(n));
     GX_TRY(p->result.alloc(n));
-    // not value-initialised: zeroing 12 n bytes on one thread cost more than the transfer
-    std::unique_ptr<int64_t[]> nrp(new int64_t[n + 1]);
-    std::unique_ptr<int32_t[]> nout(new int32_t[n]);
     // An undirected graph pulls over A itself, so the hub-first rows' lengths are its degrees
-    // sorted descending: the host derives them from its own row pointers while the device sorts
-    // (host_sorted_lengths), instead of downloading 12 n bytes after the sort (SYN-8_5: 6.6 ms).
-    // A directed graph pulls over A' in out-degree order: its row lengths come from the device.
-    std::thread host_lengths;
-    if (!g->directed)
-        host_lengths = std::thread([&] { host_sorted_lengths(g->A.h_rp.data(), n, nrp.get(), nout.get()); });
-    struct Join {
-        std::thread &t;
-        ~Join() {
-            if (t.joinable()) t.join();
-        }
-    } join{host_lengths};
+    // sorted descending: the host gets them as runs of equal degrees (a few thousand pairs,
+    // k_degree_runs over the device's sorted keys) instead of 12 n bytes of row pointers and
+    // lengths (SYN-8_5: 6.6 ms of download).  A directed graph pulls over A' in out-degree order:
+    // its row lengths come from the device.
+    LengthRuns runs;
+    bool have_runs = false;
     {
         DBuf<uint32_t> d0, d1;
         DBuf<int32_t> i0, i1;
@@ -717,14 +720,47 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
                            p->perm.p, p->outdeg_own.p, plen.p);
         GX_TRY(check_launch("k_hub_apply"));
         GX_TRY(scan_exclusive_i64(plen.p, p->rp_own.p, n + 1, s));
+        if (!g->directed) {
+            constexpr uint32_t kRunCap = 1u << 20;
+            DBuf<uint64_t> rb;
+            DBuf<uint32_t> rc;
+            GX_TRY(rb.alloc(kRunCap));
+            GX_TRY(rc.alloc(1));
+            GX_HIP_TRY(hipMemsetAsync(rc.p, 0, 4, s));
+            hipLaunchKernelGGL(k_degree_runs, dim3(grid), dim3(256), 0, s, d1.p, (int64_t)n, rb.p, rc.p, kRunCap);
+            GX_TRY(check_launch("k_degree_runs"));
+            uint32_t nr = 0;
+            GX_HIP_TRY(hipMemcpyAsync(&nr, rc.p, 4, hipMemcpyDeviceToHost, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));
+            if (nr <= kRunCap) {
+                std::vector<uint64_t> h(nr);
+                if (nr) GX_HIP_TRY(hipMemcpy(h.data(), rb.p, (size_t)nr * 8, hipMemcpyDeviceToHost));
+                std::sort(h.begin(), h.end());   // by position
+                runs.n = n;
+                int64_t acc = 0;
+                for (size_t k = 0; k < h.size(); k++) {
+                    const int64_t pos = (int64_t)(h[k] >> 32), val = (int64_t)(uint32_t)h[k];
+                    if (k) acc += (pos - runs.pos.back()) * runs.val.back();
+                    runs.pos.push_back(pos);
+                    runs.val.push_back(val);
+                    runs.base.push_back(acc);
+                }
+                runs.total = (int64_t)P.nnz;
+                have_runs = true;
+            }
+        }
         GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries are freed at the end of the block
     }
     clk.mark("hub order + row pointers (device)");
-    if (g->directed) {
+    // not value-initialised: zeroing 12 n bytes on one thread cost more than the transfer
+    std::unique_ptr<int64_t[]> nrp;
+    std::unique_ptr<int32_t[]> nout;
+    if (!have_runs) {
+        nrp.reset(new int64_t[n + 1]);
+        nout.reset(new int32_t[n]);
         GX_TRY(download(ctx, nrp.get(), p->rp_own.p, n + 1, Xfer::Raw64));
         GX_TRY(download(ctx, nout.get(), p->outdeg_own.p, n, Xfer::Raw32));
     } else {
-        host_lengths.join();
         p->rows_desc = true;   // row lengths non-increasing: the LONG rows are a prefix
     }
     clk.mark("row pointers to the host");
@@ -732,8 +768,12 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     p->src_ci = P.ci.p;
     p->src_order = p->order.p;
     p->src_perm = p->perm.p;
-    GX_TRY(pr_plan(p.get(), HostView<int64_t>(nrp.get(), n + 1), p->rp_own.p, nullptr, p->outdeg_own.p,
-                   HostView<int32_t>(nout.get(), n)));
+    if (have_runs)
+        GX_TRY(pr_plan(p.get(), HostView<int64_t>(&runs, true), p->rp_own.p, nullptr, p->outdeg_own.p,
+                       HostView<int32_t>(&runs, false)));
+    else
+        GX_TRY(pr_plan(p.get(), HostView<int64_t>(nrp.get(), n + 1), p->rp_own.p, nullptr, p->outdeg_own.p,
+                       HostView<int32_t>(nout.get(), n)));
     GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors above die at return
     clk.mark("pr_plan");
     *out = p.release();
