@@ -86,6 +86,7 @@ struct SsspState {
     int32_t dsrc;                 // defer list the advance reads (mode 4)
     int32_t sphase;               // sub-phase number (dedup tag of the defer lists)
     double delta, sub_delta;      // bucket width; sub-phase width (0: no sub-phases)
+    uint32_t sub_min;             // an opened bucket takes sub-phases from this many entries on
     uint32_t ring_cnt[kRing];
 };
 
@@ -354,8 +355,10 @@ __global__ void k_sssp_plan(SsspState *st) {
             }
             st->cur = last;
             st->mode = 1;
-            // the opened bucket's first sub-phase
-            st->sublim = st->sub_delta > 0.0 ? dbits((double)b * st->delta + st->sub_delta) : ~0ull;
+            // the opened bucket's first sub-phase, for buckets large enough that re-relaxations
+            // cost more than the sub-phases' extra steps (small ones open whole)
+            st->sublim = st->sub_delta > 0.0 && tot >= st->sub_min ? dbits((double)b * st->delta + st->sub_delta)
+                                                                  : ~0ull;
             st->slot = s;
             st->nslots = (int32_t)(last - b + 1);
             st->consume = s;
@@ -867,7 +870,7 @@ __global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxe
 }
 
 __global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t fuse, int32_t fuse_max,
-                            double sub_delta) {
+                            double sub_delta, uint32_t sub_min) {
     SsspState *st = B.st;
     const uint32_t nch = chunks_of(B.lend[src] - B.rp[src]);
     for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x) B.q[0][j] = ((uint64_t)(uint32_t)src << 32) | j;
@@ -901,6 +904,7 @@ __global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t
         st->ovf_cnt[0] = st->ovf_cnt[1] = 0;
         st->delta = B.delta;
         st->sub_delta = sub_delta;
+        st->sub_min = sub_min;
         st->sublim = sub_delta > 0.0 ? dbits(sub_delta) : ~0ull;
         st->dmin = ~0ull;
         st->dfr_cnt[0] = st->dfr_cnt[1] = 0;
@@ -1210,13 +1214,20 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     if (const char *e = std::getenv("GX_SSSP_FUSE_MAX")) fuse_max = std::max(1, std::min(kRing, std::atoi(e)));
     // light sub-phases: GX_SSSP_SUB = S splits each bucket's light phase into sub-phases of
     // delta / S, so that its vertices are relaxed closer to distance order (S <= 1: none)
+    // delta / S; the source's bucket always, later buckets only when they open with at least
+    // GX_SSSP_SUB_MIN entries (default 1/64 of the non-isolated vertices)
     double sub_delta = 0.0;
+    uint32_t sub_min = 0;
     {
         const char *e = std::getenv("GX_SSSP_SUB");
         const double S = e ? std::atof(e) : 1.0;
         if (S > 1.0) sub_delta = delta / S;
+        const char *m = std::getenv("GX_SSSP_SUB_MIN");
+        sub_min = m ? (uint32_t)std::strtoul(m, nullptr, 10)
+                    : (uint32_t)std::max<int64_t>(1, lay.n_active / 64);
     }
-    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min, fuse, fuse_max, sub_delta);
+    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min, fuse, fuse_max, sub_delta,
+                       sub_min);
     GX_TRY(check_launch("k_sssp_seed"));
     const unsigned grid = (unsigned)std::max(1, ctx->num_cus) * 8;
     // a bound every correct run stays far below: each step settles a vertex or a bucket

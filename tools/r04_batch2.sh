@@ -12,7 +12,7 @@ GX_PLAN_TIMES=1 timeout -k 10 300 python bench.py --no-cpu-baseline --no-seconda
     > "$OUT/plan_times.json" 2> "$OUT/plan_times.err" || exit 1
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --steps 10 --warmup 2 > "$OUT/bench_pr.json" \
     2> "$OUT/bench_pr.err" || exit 1
-for k in 1 8; do
+for k in 1 8 16; do
   GX_SSSP_SUB=$k GX_SSSP_VERBOSE=1 timeout -k 10 300 python bench.py --algorithm sssp --no-cpu-baseline --steps 2 \
       --warmup 1 > "$OUT/sssp_v_$k.json" 2> "$OUT/sssp_v_$k.err" || exit 1
 done
