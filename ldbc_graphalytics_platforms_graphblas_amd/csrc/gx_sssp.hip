@@ -77,16 +77,6 @@ struct SsspState {
     int32_t pull;                 // heavy phase pulled by the unsettled vertices (k_sssp_pull)
     uint32_t pull_min;            // settled-list size from which the heavy phase is pulled
     unsigned long long smin;      // smallest distance on the settled list (pull bound)
-    // light sub-phases (GX_SSSP_SUB): near pushes at or past `sublim` are deferred; when the near
-    // queue drains, the limit moves to the smallest deferred distance + sub_delta
-    unsigned long long sublim;    // ~0: no limit
-    unsigned long long dmin;      // smallest distance on the defer list being appended
-    uint32_t dfr_cnt[2];
-    int32_t dsel;                 // defer list the relaxations append to
-    int32_t dsrc;                 // defer list the advance reads (mode 4)
-    int32_t sphase;               // sub-phase number (dedup tag of the defer lists)
-    double delta, sub_delta;      // bucket width; sub-phase width (0: no sub-phases)
-    uint32_t sub_min;             // an opened bucket takes sub-phases from this many entries on
     uint32_t ring_cnt[kRing];
 };
 
@@ -105,8 +95,6 @@ struct SsspBufs {
     int32_t *ring;                // kRing slots of ring_cap vertices
     int32_t *ovf[2];
     int32_t *settled;             // vertices of the current bucket (heavy edges pending)
-    int32_t *dfr[2];              // deferred light-phase vertices (sub-phases)
-    int32_t *dstamp;              // sub-phase a vertex was last deferred in
     uint64_t ring_cap;
     double delta, inv_delta;
     SsspState *st;
@@ -148,8 +136,8 @@ __device__ __forceinline__ void wave_min_to(unsigned long long m, unsigned long 
 // Mid-kernel flushes (a full stage) are per wave; the final one is per workgroup, so a launch
 // costs at most one atomic per queue per workgroup plus one per full stage.
 constexpr int kStage = 512;
-constexpr int kTagNear = kRing, kTagOvf = kRing + 1, kTagDefer = kRing + 2;   // tags 0..kRing-1: ring slots
-constexpr int kCats = 4 + kRing;   // near items, settled, overflow, defer, ring slots
+constexpr int kTagNear = kRing, kTagOvf = kRing + 1;   // tags 0..kRing-1 are ring slots
+constexpr int kCats = 3 + kRing;                       // near items, settled, overflow, ring slots
 
 struct Stage {
     int32_t v[kStage];
@@ -164,20 +152,9 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// where a launch's pushes go: the near queue it fills, the overflow and defer lists of the
-// current epoch / sub-phase, with their counters
-struct Queues {
-    uint64_t *near_out;
-    uint32_t *near_count;
-    int32_t *ovf;
-    uint32_t *ovf_count;
-    int32_t *dfr;
-    uint32_t *dfr_count;
-};
-
-__device__ __forceinline__ uint32_t *queue_counter(int cat, const SsspBufs &B, const Queues &Q) {
-    return cat == 0 ? Q.near_count : cat == 1 ? &B.st->settled_cnt : cat == 2 ? Q.ovf_count
-                                  : cat == 3 ? Q.dfr_count : &B.st->ring_cnt[cat - 4];
+__device__ __forceinline__ uint32_t *queue_counter(int cat, const SsspBufs &B, uint32_t *near_count,
+                                                   uint32_t *ovf_count) {
+    return cat == 0 ? near_count : cat == 1 ? &B.st->settled_cnt : cat == 2 ? ovf_count : &B.st->ring_cnt[cat - 3];
 }
 
 // pass 1: per-queue totals of the n staged pushes into sg.cnt
@@ -185,7 +162,7 @@ __device__ __forceinline__ void stage_count(Stage &sg, uint32_t n) {
     const int lane = threadIdx.x & (kWave - 1);
     if (lane < kCats) sg.cnt[lane] = 0;
     wave_lds_sync();
-    uint32_t items = 0, nset = 0, novf = 0, ndef = 0;
+    uint32_t items = 0, nset = 0, novf = 0;
     for (uint32_t base = 0; base < n; base += kWave) {
         const uint32_t i = base + lane;
         if (i < n) {
@@ -195,10 +172,8 @@ __device__ __forceinline__ void stage_count(Stage &sg, uint32_t n) {
                 nset += (tag >> 7) & 1u;
             } else if (q == (uint32_t)kTagOvf) {
                 novf++;
-            } else if (q == (uint32_t)kTagDefer) {
-                ndef++;
             } else {
-                atomicAdd(&sg.cnt[4 + q], 1u);
+                atomicAdd(&sg.cnt[3 + q], 1u);
             }
         }
     }
@@ -206,21 +181,20 @@ __device__ __forceinline__ void stage_count(Stage &sg, uint32_t n) {
         items += __shfl_xor(items, off, kWave);
         nset += __shfl_xor(nset, off, kWave);
         novf += __shfl_xor(novf, off, kWave);
-        ndef += __shfl_xor(ndef, off, kWave);
     }
     if (lane == 0) {
         sg.cnt[0] = items;
         sg.cnt[1] = nset;
         sg.cnt[2] = novf;
-        sg.cnt[3] = ndef;
     }
     wave_lds_sync();
 }
 
 // pass 2: write the staged pushes into the ranges starting at sg.base
-__device__ __forceinline__ void stage_write(Stage &sg, uint32_t n, const SsspBufs &B, const Queues &Q) {
+__device__ __forceinline__ void stage_write(Stage &sg, uint32_t n, const SsspBufs &B, uint64_t *near_out,
+                                            int32_t *ovf) {
     const int lane = threadIdx.x & (kWave - 1);
-    uint32_t r_items = sg.base[0], r_set = sg.base[1], r_ovf = sg.base[2], r_def = sg.base[3];
+    uint32_t r_items = sg.base[0], r_set = sg.base[1], r_ovf = sg.base[2];
     for (uint32_t base = 0; base < n; base += kWave) {
         const uint32_t i = base + lane;
         const bool valid = i < n;
@@ -236,7 +210,7 @@ __device__ __forceinline__ void stage_write(Stage &sg, uint32_t n, const SsspBuf
             if (lane >= off) x += y;
         }
         const uint32_t at = r_items + x - k;
-        for (uint32_t j = 0; j < k; j++) Q.near_out[at + j] = ((uint64_t)(uint32_t)v << 32) | j;
+        for (uint32_t j = 0; j < k; j++) near_out[at + j] = ((uint64_t)(uint32_t)v << 32) | j;
         r_items += __shfl(x, kWave - 1, kWave);
         const uint64_t below = (1ull << lane) - 1;
         const bool set = near && (tag & 0x80u);
@@ -245,34 +219,32 @@ __device__ __forceinline__ void stage_write(Stage &sg, uint32_t n, const SsspBuf
         r_set += (uint32_t)__popcll(ms);
         const bool to_ovf = valid && q == (uint32_t)kTagOvf;
         const uint64_t mo = __ballot(to_ovf);
-        if (to_ovf) Q.ovf[r_ovf + __popcll(mo & below)] = v;
+        if (to_ovf) ovf[r_ovf + __popcll(mo & below)] = v;
         r_ovf += (uint32_t)__popcll(mo);
-        const bool to_def = valid && q == (uint32_t)kTagDefer;
-        const uint64_t md = __ballot(to_def);
-        if (to_def) Q.dfr[r_def + __popcll(md & below)] = v;
-        r_def += (uint32_t)__popcll(md);
-        if (valid && q < (uint32_t)kRing) B.ring[(uint64_t)q * B.ring_cap + atomicAdd(&sg.base[4 + q], 1u)] = v;
+        if (valid && q < (uint32_t)kRing) B.ring[(uint64_t)q * B.ring_cap + atomicAdd(&sg.base[3 + q], 1u)] = v;
     }
     wave_lds_sync();
 }
 
 // full stage mid-kernel: reserve for this wave alone
-__device__ __forceinline__ void stage_flush(Stage &sg, uint32_t &n, const SsspBufs &B, const Queues &Q) {
+__device__ __forceinline__ void stage_flush(Stage &sg, uint32_t &n, const SsspBufs &B, uint64_t *near_out,
+                                            uint32_t *near_count, int32_t *ovf, uint32_t *ovf_count) {
     wave_lds_sync();
     stage_count(sg, n);
     const int lane = threadIdx.x & (kWave - 1);
     if (lane < kCats) {
         const uint32_t c = sg.cnt[lane];
-        sg.base[lane] = c ? atomicAdd(queue_counter(lane, B, Q), c) : 0u;
+        sg.base[lane] = c ? atomicAdd(queue_counter(lane, B, near_count, ovf_count), c) : 0u;
     }
     wave_lds_sync();
-    stage_write(sg, n, B, Q);
+    stage_write(sg, n, B, near_out, ovf);
     n = 0;
 }
 
 // end of the kernel: one reservation per queue for the whole workgroup.  Every thread of
 // the workgroup must call it.
-__device__ __forceinline__ void stage_final(Stage *stages, uint32_t &n, const SsspBufs &B, const Queues &Q) {
+__device__ __forceinline__ void stage_final(Stage *stages, uint32_t &n, const SsspBufs &B, uint64_t *near_out,
+                                            uint32_t *near_count, int32_t *ovf, uint32_t *ovf_count) {
     constexpr int kWaves = kSsspBlock / kWave;
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     Stage &sg = stages[wid];
@@ -287,12 +259,12 @@ __device__ __forceinline__ void stage_final(Stage *stages, uint32_t &n, const Ss
             stages[w].base[lane] = tot;
             tot += c;
         }
-        const uint32_t b = tot ? atomicAdd(queue_counter(lane, B, Q), tot) : 0u;
+        const uint32_t b = tot ? atomicAdd(queue_counter(lane, B, near_count, ovf_count), tot) : 0u;
 #pragma unroll
         for (int w = 0; w < kWaves; w++) stages[w].base[lane] += b;
     }
     __syncthreads();
-    if (n) stage_write(sg, n, B, Q);
+    if (n) stage_write(sg, n, B, near_out, ovf);
     n = 0;
 }
 
@@ -315,18 +287,6 @@ __global__ void k_sssp_plan(SsspState *st) {
     st->qcnt[qin ^ 1] = 0;
     st->mode = 0;
     if (st->qcnt[qin] > 0) return;
-    if (!st->heavy && st->dfr_cnt[st->dsel] > 0) {
-        // the next light sub-phase: the limit moves to the smallest deferred distance plus the
-        // sub-phase width, and the deferred vertices below it join the near queue (mode 4)
-        st->mode = 4;
-        st->dsrc = st->dsel;
-        st->dsel ^= 1;
-        st->dfr_cnt[st->dsel] = 0;
-        st->sphase++;
-        st->sublim = dbits(bitsd(st->dmin) + st->sub_delta);
-        st->dmin = ~0ull;
-        return;
-    }
     if (!st->heavy && st->settled_cnt > 0) {
         st->heavy = 1;
         st->mode = 3;
@@ -355,10 +315,6 @@ __global__ void k_sssp_plan(SsspState *st) {
             }
             st->cur = last;
             st->mode = 1;
-            // the opened bucket's first sub-phase, for buckets large enough that re-relaxations
-            // cost more than the sub-phases' extra steps (small ones open whole)
-            st->sublim = st->sub_delta > 0.0 && tot >= st->sub_min ? dbits((double)b * st->delta + st->sub_delta)
-                                                                  : ~0ull;
             st->slot = s;
             st->nslots = (int32_t)(last - b + 1);
             st->consume = s;
@@ -384,9 +340,7 @@ __global__ void k_sssp_plan(SsspState *st) {
 // Mode 1: turn the opened ring bucket into near items (and settled-list entries);
 // mode 2: split the overflow into the new ring window;
 // mode 3: emit heavy-phase items for the bucket's settled list and record the distance
-//         their edges are relaxed with;
-// mode 4: the deferred vertices below the new sub-phase limit become near items (and
-//         settled-list entries), the others are deferred again.
+//         their edges are relaxed with.
 // Ring / overflow entries whose edges were all relaxed at their current distance are dropped.
 __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     const SsspState *st = B.st;
@@ -406,9 +360,6 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     } else if (mode == 2) {
         list = B.ovf[st->split_src];
         count = st->ovf_cnt[st->split_src];
-    } else if (mode == 4) {
-        list = B.dfr[st->dsrc];
-        count = st->dfr_cnt[st->dsrc];
     } else {
         list = B.settled;
         count = st->settled_cnt;
@@ -418,10 +369,9 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     if (fn > 1 && (int)threadIdx.x < fn) fcnt[threadIdx.x] = st->ring_cnt[(fslot + threadIdx.x) % kRing];
     __syncthreads();
     const int64_t cur = st->cur, win_base = st->win_base, lim = win_base + kRing;
-    const int32_t epoch = st->epoch, sphase = st->sphase;
-    const unsigned long long sublim = st->sublim;
+    const int32_t epoch = st->epoch;
     const bool pull = mode == 3 && st->pull;
-    unsigned long long mymin = ~0ull, n_skip = 0, dmin = ~0ull;
+    unsigned long long mymin = ~0ull, n_skip = 0;
     const uint32_t stride = gridDim.x * kSsspBlock;
     const uint32_t nround = (count + stride - 1) / stride;
     // pushes are staged per wave in LDS and flushed in bulk, as in k_sssp_relax
@@ -429,11 +379,13 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     Stage &sg = stages[threadIdx.x / kWave];
     uint32_t staged = 0;
     const int lane = threadIdx.x & (kWave - 1);
-    const Queues Q{B.q[qin], &B.st->qcnt[qin], B.ovf[epoch & 1], &B.st->ovf_cnt[epoch & 1], B.dfr[st->dsel],
-                   &B.st->dfr_cnt[st->dsel]};
+    uint64_t *near_out = B.q[qin];
+    uint32_t *near_count = &B.st->qcnt[qin];
+    int32_t *ovf = B.ovf[epoch & 1];
+    uint32_t *ovf_count = &B.st->ovf_cnt[epoch & 1];
     for (uint32_t it = 0; it < nround; it++) {
         const uint32_t f = it * stride + blockIdx.x * kSsspBlock + threadIdx.x;
-        bool to_near = false, to_ring = false, to_ovf = false, to_set = false, to_def = false;
+        bool to_near = false, to_ring = false, to_ovf = false, to_set = false;
         int32_t v = 0;
         int slot = 0;
         uint32_t nch = 0;
@@ -447,18 +399,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
                 v = list[f];
             }
             const unsigned long long db = B.dist[v];
-            if (mode == 4) {
-                if (db < sublim) {
-                    if (claim(&B.near_stamp[v], r)) {
-                        to_near = true;
-                        nch = chunks_of(B.lend[v] - B.rp[v]);
-                        to_set = B.sstamp[v] != (int32_t)cur && atomicExch(&B.sstamp[v], (int32_t)cur) != (int32_t)cur;
-                    }
-                } else if (claim(&B.dstamp[v], sphase)) {
-                    to_def = true;
-                    dmin = min(dmin, db);
-                }
-            } else if (mode == 3) {
+            if (mode == 3) {
                 B.relaxed[v] = db;   // heavy edges now, light edges already relaxed at db
                 if (pull) {
                     mymin = min(mymin, db);
@@ -490,22 +431,21 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
                 }
             }
         }
-        const bool take = to_near | to_ring | to_ovf | to_def;
+        const bool take = to_near | to_ring | to_ovf;
         const uint64_t mask = __ballot(take);
         if (mask == 0) continue;
         if (take) {
             const uint32_t pos = staged + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
             sg.v[pos] = v;
             sg.tag[pos] = to_near ? ((uint32_t)kTagNear | (to_set ? 0x80u : 0u) | (nch << 8))
-                                  : to_def ? (uint32_t)kTagDefer : (to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot);
+                                  : (to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot);
         }
         staged += (uint32_t)__popcll(mask);
-        if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, Q);
+        if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
     }
-    stage_final(stages, staged, B, Q);
+    stage_final(stages, staged, B, near_out, near_count, ovf, ovf_count);
     if (mode == 2) wave_min_to(mymin, &B.st->ovf_minb);
     if (pull) wave_min_to(mymin, &B.st->smin);
-    if (mode == 4) wave_min_to(dmin, &B.st->dmin);
     wave_count(B.stats, 7, n_skip);
 }
 
@@ -528,8 +468,10 @@ __device__ __forceinline__ void sssp_pull(const SsspBufs &B, Stage *stages, unsi
     const int32_t epoch = st->epoch, cur32 = (int32_t)cur;
     const unsigned long long bound = dbits(bitsd(st->smin) + B.delta);
     const uint64_t n = B.ring_cap;
-    // a pull never pushes near items or deferred ones
-    const Queues Q{B.q[0], &B.st->qcnt[0], B.ovf[epoch & 1], &B.st->ovf_cnt[epoch & 1], B.dfr[0], &B.st->dfr_cnt[0]};
+    uint64_t *near_out = B.q[0];   // a pull never pushes near items
+    uint32_t *near_count = &B.st->qcnt[0];
+    int32_t *ovf = B.ovf[epoch & 1];
+    uint32_t *ovf_count = &B.st->ovf_cnt[epoch & 1];
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t wave = (blockIdx.x * kSsspBlock + threadIdx.x) / kWave;
     const uint64_t nwaves = gridDim.x * (kSsspBlock / kWave);
@@ -627,9 +569,9 @@ __device__ __forceinline__ void sssp_pull(const SsspBufs &B, Stage *stages, unsi
             sg.tag[pos] = to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot;
         }
         staged += (uint32_t)__popcll(mask);
-        if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, Q);
+        if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
     }
-    stage_final(stages, staged, B, Q);
+    stage_final(stages, staged, B, near_out, near_count, ovf, ovf_count);
     wave_min_to(mymin, &B.st->ovf_minb);
     if (B.stats) {
         wave_count(B.stats, 0, c_items);
@@ -665,20 +607,20 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
     }
     if (count == 0) return;
     const int64_t cur = st->cur, lim = st->win_base + kRing;
-    const int32_t epoch = st->epoch, rn = r + 1, cur32 = (int32_t)cur, sphase = st->sphase;
-    // light phase: near pushes at or past the sub-phase limit are deferred
-    const unsigned long long sublim = heavy ? ~0ull : st->sublim;
+    const int32_t epoch = st->epoch, rn = r + 1, cur32 = (int32_t)cur;
     const uint64_t *near_in = B.q[qin];
-    const Queues Q{B.q[qin ^ 1], &B.st->qcnt[qin ^ 1], B.ovf[epoch & 1], &B.st->ovf_cnt[epoch & 1], B.dfr[st->dsel],
-                   &B.st->dfr_cnt[st->dsel]};
+    uint64_t *near_out = B.q[qin ^ 1];
+    uint32_t *near_count = &B.st->qcnt[qin ^ 1];
+    int32_t *ovf = B.ovf[epoch & 1];
+    uint32_t *ovf_count = &B.st->ovf_cnt[epoch & 1];
     const __amdgpu_buffer_rsrc_t dist_r =
         __builtin_amdgcn_make_buffer_rsrc(B.dist, (short)0, (int)(B.ring_cap * 8u), 0x00020000);
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = (blockIdx.x * kSsspBlock + threadIdx.x) / kWave;
     const uint32_t nwaves = gridDim.x * (kSsspBlock / kWave);
     uint32_t staged = 0;
-    unsigned long long mymin = ~0ull, dmin = ~0ull, c_items = 0, c_edges = 0, c_try = 0, c_impr = 0, c_near = 0,
-                       c_ring = 0, c_ovf = 0;
+    unsigned long long mymin = ~0ull, c_items = 0, c_edges = 0, c_try = 0, c_impr = 0, c_near = 0, c_ring = 0,
+                       c_ovf = 0;
     // a wave takes up to 64 items, fewer when the queue is short, so that small rounds (a
     // hub's chunks) spread over all waves instead of serialising in a few
     const uint32_t ipw = min((uint32_t)kWave, max(1u, (count + nwaves - 1) / nwaves));
@@ -740,7 +682,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
             // Improvements, then their dedup claims, each step issued for all slots before any
             // result is used: the claims are memory-side round trips, and chaining them slot by
             // slot serialised up to 4 x 2 of them per lane.
-            int cls[kSlots];       // 0 nothing, 1 near, 2 ring slot, 3 overflow, 4 deferred
+            int cls[kSlots];       // 0 nothing, 1 near, 2 ring slot, 3 overflow
             int32_t tag[kSlots];
             int32_t *stp[kSlots];
             int slot[kSlots];
@@ -763,12 +705,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
                         c_impr++;
                         int64_t b = bucket_of(nd, B.inv_delta);
                         if (heavy && b <= cur) b = cur + 1;
-                        if (b <= cur && ndb >= sublim) {
-                            cls[q] = 4;
-                            stp[q] = B.dstamp + v[q];
-                            tag[q] = sphase;
-                            dmin = min(dmin, ndb);
-                        } else if (b <= cur) {
+                        if (b <= cur) {
                             cls[q] = 1;
                             stp[q] = B.near_stamp + v[q];
                             tag[q] = rn;
@@ -821,7 +758,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
 #pragma unroll
             for (int q = 0; q < kSlots; q++) {
                 const bool to_near = won[q] && cls[q] == 1, to_ring = won[q] && cls[q] == 2,
-                           to_ovf = won[q] && cls[q] == 3, to_def = won[q] && cls[q] == 4;
+                           to_ovf = won[q] && cls[q] == 3;
                 const uint32_t nch = to_near ? chunks_of(rhi[q] - rlo[q]) : 0u;
                 c_near += to_near;
                 c_ring += to_ring;
@@ -833,17 +770,15 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
                     const uint32_t pos = staged + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
                     sg.v[pos] = v[q];
                     sg.tag[pos] = to_near ? ((uint32_t)kTagNear | (to_set[q] ? 0x80u : 0u) | (nch << 8))
-                                          : to_def ? (uint32_t)kTagDefer
-                                                   : (to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot[q]);
+                                          : (to_ovf ? (uint32_t)kTagOvf : (uint32_t)slot[q]);
                 }
                 staged += (uint32_t)__popcll(mask);
-                if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, Q);
+                if (staged > (uint32_t)(kStage - kWave)) stage_flush(sg, staged, B, near_out, near_count, ovf, ovf_count);
             }
         }
     }
-    stage_final(stages, staged, B, Q);
+    stage_final(stages, staged, B, near_out, near_count, ovf, ovf_count);
     wave_min_to(mymin, &B.st->ovf_minb);
-    wave_min_to(dmin, &B.st->dmin);
     if (B.stats) {
         wave_count(B.stats, 0, c_items);
         wave_count(B.stats, 1, c_edges);
@@ -856,7 +791,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
 }
 
 __global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxed, int32_t *near_stamp,
-                            int32_t *bstamp, int32_t *ostamp, int32_t *sstamp, int32_t *dstamp, int64_t n) {
+                            int32_t *bstamp, int32_t *ostamp, int32_t *sstamp, int64_t n) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
          v += (int64_t)gridDim.x * blockDim.x) {
         dist[v] = 0x7FF0000000000000ull;   // +infinity
@@ -865,12 +800,10 @@ __global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxe
         bstamp[v] = -1;
         ostamp[v] = 0;
         sstamp[v] = -1;
-        dstamp[v] = 0;
     }
 }
 
-__global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t fuse, int32_t fuse_max,
-                            double sub_delta, uint32_t sub_min) {
+__global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t fuse, int32_t fuse_max) {
     SsspState *st = B.st;
     const uint32_t nch = chunks_of(B.lend[src] - B.rp[src]);
     for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x) B.q[0][j] = ((uint64_t)(uint32_t)src << 32) | j;
@@ -902,15 +835,6 @@ __global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t
         st->qcnt[0] = nch;
         st->qcnt[1] = 0;
         st->ovf_cnt[0] = st->ovf_cnt[1] = 0;
-        st->delta = B.delta;
-        st->sub_delta = sub_delta;
-        st->sub_min = sub_min;
-        st->sublim = sub_delta > 0.0 ? dbits(sub_delta) : ~0ull;
-        st->dmin = ~0ull;
-        st->dfr_cnt[0] = st->dfr_cnt[1] = 0;
-        st->dsel = 0;
-        st->dsrc = 0;
-        st->sphase = 1;
     }
 }
 
@@ -1038,7 +962,7 @@ int ensure_sssp_layout(gx_graph *g, double delta, hipStream_t s) {
 constexpr int kGraphSteps = 8;
 struct SsspWork {
     DBuf<unsigned long long> dist, relaxed;
-    DBuf<int32_t> nstamp, bstamp, ostamp, sstamp, ring, ovf0, ovf1, settled, dfr0, dfr1, dstamp;
+    DBuf<int32_t> nstamp, bstamp, ostamp, sstamp, ring, ovf0, ovf1, settled;
     DBuf<uint64_t> q0, q1;
     DBuf<SsspState> st;
     int32_t *h_done = nullptr;     // round, done of the state (pinned)
@@ -1065,9 +989,6 @@ struct SsspWork {
         GX_TRY(ring.alloc((uint64_t)n * kRing));
         GX_TRY(ovf0.alloc(n));
         GX_TRY(ovf1.alloc(n));
-        GX_TRY(dfr0.alloc(n));
-        GX_TRY(dfr1.alloc(n));
-        GX_TRY(dstamp.alloc(n));
         GX_TRY(q0.alloc(qcap));
         GX_TRY(q1.alloc(qcap));
         GX_TRY(st.alloc(1));
@@ -1187,10 +1108,10 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     auto &st = W.st;
     SsspBufs B{g->A.rp.p,   lay.lend.p,   lay.ci.p,      lay.w.p,    dist.p,       relaxed.p,  nstamp.p,
                bstamp.p,    ostamp.p,     sstamp.p,      {W.q0.p, W.q1.p}, W.ring.p, {W.ovf0.p, W.ovf1.p},
-               W.settled.p, {W.dfr0.p, W.dfr1.p}, W.dstamp.p, (uint64_t)n,  delta,  inv_delta,  st.p, stats.p};
+               W.settled.p, (uint64_t)n,  delta,         inv_delta,  st.p,         stats.p};
 
     hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nstamp.p,
-                       bstamp.p, ostamp.p, sstamp.p, W.dstamp.p, n);
+                       bstamp.p, ostamp.p, sstamp.p, n);
     GX_TRY(check_launch("k_sssp_init"));
     // heavy phases whose settled list holds at least 1/GX_SSSP_PULL_FRAC (default 8) of the
     // non-isolated vertices are pulled (undirected graphs; GX_SSSP_PULL=0 never, 2 always).
@@ -1212,22 +1133,7 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     int32_t fuse_max = kRing;
     if (const char *e = std::getenv("GX_SSSP_FUSE")) fuse = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GX_SSSP_FUSE_MAX")) fuse_max = std::max(1, std::min(kRing, std::atoi(e)));
-    // light sub-phases: GX_SSSP_SUB = S splits each bucket's light phase into sub-phases of
-    // delta / S, so that its vertices are relaxed closer to distance order (S <= 1: none)
-    // delta / S; the source's bucket always, later buckets only when they open with at least
-    // GX_SSSP_SUB_MIN entries (default 1/64 of the non-isolated vertices)
-    double sub_delta = 0.0;
-    uint32_t sub_min = 0;
-    {
-        const char *e = std::getenv("GX_SSSP_SUB");
-        const double S = e ? std::atof(e) : 1.0;
-        if (S > 1.0) sub_delta = delta / S;
-        const char *m = std::getenv("GX_SSSP_SUB_MIN");
-        sub_min = m ? (uint32_t)std::strtoul(m, nullptr, 10)
-                    : (uint32_t)std::max<int64_t>(1, lay.n_active / 64);
-    }
-    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min, fuse, fuse_max, sub_delta,
-                       sub_min);
+    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min, fuse, fuse_max);
     GX_TRY(check_launch("k_sssp_seed"));
     const unsigned grid = (unsigned)std::max(1, ctx->num_cus) * 8;
     // a bound every correct run stays far below: each step settles a vertex or a bucket

@@ -90,18 +90,6 @@ def test_sssp_syn85(syn85):
         sp.close()
 
 
-@pytest.mark.parametrize("sub", ["4", "16"])
-def test_sssp_syn85_subphases(syn85, monkeypatch, sub):
-    """gx_sssp with light sub-phases (GX_SSSP_SUB: each bucket's light phase in delta / S
-    slices, deferred vertices joining as the limit moves): the same distances bit for bit."""
-    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
-    csr, G = syn85
-    monkeypatch.setenv("GX_SSSP_SUB", sub)
-    src = _maxdeg(csr)
-    ref = O.sssp_par(csr, src, 0.0, nthreads=O.max_threads())
-    assert np.array_equal(A.LA_SSSP(G, src), ref)
-
-
 def test_pagerank_syn75(syn75):
     """Config 2 (pr.cpp:61): the default plan at full size, first and warm call."""
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
