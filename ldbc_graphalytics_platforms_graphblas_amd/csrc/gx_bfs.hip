@@ -362,6 +362,9 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const int64_t n = (int64_t)g->n;
+    int64_t src_rp[2] = {0, 0};   // the source's out-degree (the host row pointers are lazy)
+    GX_HIP_TRY(hipMemcpy(src_rp, g->A.rp.p + src, sizeof(src_rp), hipMemcpyDeviceToHost));
+    const int64_t src_deg = src_rp[1] - src_rp[0];
     DBuf<int32_t> level;
     DBuf<uint64_t> q0, q1;
     DBuf<uint32_t> qcount;
@@ -397,7 +400,7 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         DBuf<BfsState> st;
         GX_TRY(st.alloc(1));
         BfsState h{};
-        const int64_t dsrc = g->A.h_rp[src + 1] - g->A.h_rp[src];
+        const int64_t dsrc = src_deg;
         h.have_queue = 1;
         h.has_in = in != nullptr;
         h.n = (unsigned long long)n;
@@ -484,7 +487,7 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     uint32_t qsize = 0;
     GX_HIP_TRY(hipMemcpyAsync(&qsize, qcount.p, 4, hipMemcpyDeviceToHost, s));
     GX_HIP_TRY(hipStreamSynchronize(s));
-    unsigned long long mf = (unsigned long long)(g->A.h_rp[src + 1] - g->A.h_rp[src]);
+    unsigned long long mf = (unsigned long long)src_deg;
     unsigned long long mu = g->nnz;
     bool bottom_up = false;
     int32_t depth = 0;

@@ -1452,7 +1452,7 @@ int cdlp_relabel(gx_graph *g, CdlpCache &C, hipStream_t s) {
         order[pos] = (int32_t)v;
         perm[v] = (int32_t)pos;
     }
-    auto new_rp = [&](const std::vector<int64_t> &h, std::vector<int64_t> &out) {
+    auto new_rp = [&](const HostRowPtr &h, std::vector<int64_t> &out) {
         out.assign(n + 1, 0);
         for (int64_t i = 0; i < n; i++) out[i + 1] = out[i] + (h[order[i] + 1] - h[order[i]]);
     };
@@ -1487,6 +1487,7 @@ int cdlp_cache(gx_graph *g, int iters, bool relabel, CdlpCache **out, hipStream_
     if (!C) {
         auto fresh = std::make_shared<CdlpCache>();
         fresh->relabel = relabel;
+        GX_TRY(ensure_host_rp(g->ctx, g->A));
         fresh->G = cdlp_view(g);
         if (relabel) GX_TRY(cdlp_relabel(g, *fresh, s));
         GX_TRY(cdlp_plan(fresh->G, 0, n, fresh->P, s));
@@ -1669,6 +1670,7 @@ extern "C" int gx_cdlp_part_create(gx_graph *g, uint64_t v0, uint64_t v1, gx_cdl
     if (v0 > v1 || v1 > g->n) return fail(GX_INVALID_INDEX, "gx_cdlp_part_create: bad vertex range");
     GX_HIP_TRY(hipSetDevice(g->ctx->device));
     if (g->directed) GX_TRY(ensure_transpose(g));
+    GX_TRY(ensure_host_rp(g->ctx, g->A));
     auto p = std::make_unique<gx_cdlp_part>();
     p->g = g;
     GX_TRY(cdlp_plan(cdlp_view(g), (int64_t)v0, (int64_t)v1, p->plan, g->ctx->stream));

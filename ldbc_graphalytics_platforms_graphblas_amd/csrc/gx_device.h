@@ -75,13 +75,36 @@ struct DBuf {
     }
 };
 
+// std::allocator whose value-less construct leaves the element uninitialised: a host array
+// that is written in full next (row pointers filled by parallel copies or device downloads)
+// is not zero-filled, page by page, on one thread first (13 ms for SYN-8_5's 67 MB).
+template <typename T>
+struct NoInitAlloc : std::allocator<T> {
+    template <typename U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <typename U>
+    NoInitAlloc(const NoInitAlloc<U> &) {}
+    template <typename U>
+    void construct(U *p) noexcept {
+        ::new (static_cast<void *>(p)) U;
+    }
+    template <typename U, typename... Args>
+    void construct(U *p, Args &&...args) {
+        ::new (static_cast<void *>(p)) U(std::forward<Args>(args)...);
+    }
+};
+using HostRowPtr = std::vector<int64_t, NoInitAlloc<int64_t>>;
+
 struct DevCSR {
     uint64_t n = 0, nnz = 0;
     DBuf<int64_t> rp;         // n + 1
     DBuf<int32_t> ci;         // nnz (+16 B slack)
     DBuf<double> w;           // nnz or empty
     DBuf<uint8_t> flag;       // nnz or empty (closure only)
-    std::vector<int64_t> h_rp;  // host copy of the row pointers (row-block planning)
+    HostRowPtr h_rp;            // host copy of the row pointers (row-block planning)
     bool built = false;
 };
 
@@ -103,10 +126,11 @@ struct gx_ctx {
     std::string device_name;
     int num_cus = 0;
     // pinned staging for uploads and result hand-back (allocated by gx_init, outside the
-    // Graphalytics processing time); two buffers so host work overlaps the DMA
+    // Graphalytics processing time); several buffers so host work overlaps the DMA
     static constexpr size_t kStageBytes = 32u << 20;
-    void *staging[2] = {nullptr, nullptr};
-    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    static constexpr int kStageBufs = 4;
+    void *staging[kStageBufs] = {};
+    hipEvent_t stage_ev[kStageBufs] = {};
     // auxiliary streams for independent kernels of one step (fork/join by events), lazy
     hipStream_t aux[2] = {nullptr, nullptr};
     hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
@@ -114,6 +138,10 @@ struct gx_ctx {
 
 namespace gx {
 int ensure_aux_streams(gx_ctx *ctx);
+// The host copy of c's row pointers (c.h_rp), downloaded on first use: gx_graph_create keeps
+// none, so a path that never plans from them (PageRank on an undirected graph) never pays
+// for them.
+int ensure_host_rp(gx_ctx *ctx, DevCSR &c);
 // Device -> host copy of `count` elements through the context's pinned staging buffers, the
 // conversion of each chunk (parallel, on the host) overlapping the next chunk's DMA.
 enum class Xfer { Raw64, Raw32, Levels, Widen32 };   // 8 / 4 B as is; int32 level -> int64 (INF); int32 -> uint64

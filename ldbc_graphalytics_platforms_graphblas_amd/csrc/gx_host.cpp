@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cctype>
 #include <cinttypes>
+#include <emmintrin.h>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -549,13 +550,35 @@ extern "C" int gx_read_mtx(const char *path, gx_csr *out) {
 
 namespace gx {
 
-bool host_narrow(const uint64_t *in, uint64_t count, uint64_t limit, int32_t *out) {
+bool host_narrow(const uint64_t *in, uint64_t count, uint64_t limit, int32_t *out, bool nt) {
     int bad = 0;
+    if (!nt || (reinterpret_cast<uintptr_t>(out) & 15)) {
 #pragma omp parallel for schedule(static) reduction(| : bad)
-    for (int64_t k = 0; k < (int64_t)count; k++) {
-        const uint64_t c = in[k];
-        bad |= c >= limit;
-        out[k] = (int32_t)c;
+        for (int64_t k = 0; k < (int64_t)count; k++) {
+            const uint64_t c = in[k];
+            bad |= c >= limit;
+            out[k] = (int32_t)c;
+        }
+        return bad == 0;
+    }
+    // streaming stores: the staging buffer is read next by the DMA engine, not by this core,
+    // so its lines are not fetched for ownership first
+    const int64_t nq = (int64_t)(count / 4);
+#pragma omp parallel reduction(| : bad)
+    {
+#pragma omp for schedule(static)
+        for (int64_t q = 0; q < nq; q++) {
+            const uint64_t *p = in + 4 * q;
+            const uint64_t c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
+            bad |= (c0 >= limit) | (c1 >= limit) | (c2 >= limit) | (c3 >= limit);
+            _mm_stream_si128(reinterpret_cast<__m128i *>(out + 4 * q),
+                             _mm_set_epi32((int32_t)c3, (int32_t)c2, (int32_t)c1, (int32_t)c0));
+        }
+        _mm_sfence();
+    }
+    for (uint64_t k = (uint64_t)nq * 4; k < count; k++) {
+        bad |= in[k] >= limit;
+        out[k] = (int32_t)in[k];
     }
     return bad == 0;
 }

@@ -18,7 +18,7 @@ int fail(int code, const std::string &msg);
 // ---- multi-threaded host helpers (gx_host.cpp, OpenMP): the host side of uploads and
 // result hand-back, which sit inside the Graphalytics processing time ----
 // out[i] = (int32) in[i]; false if any in[i] >= limit.
-bool host_narrow(const uint64_t *in, uint64_t count, uint64_t limit, int32_t *out);
+bool host_narrow(const uint64_t *in, uint64_t count, uint64_t limit, int32_t *out, bool nt = false);
 // parallel memcpy
 void host_copy(void *dst, const void *src, size_t bytes);
 // rp[i] <= rp[i+1] for all i < n

@@ -165,6 +165,7 @@ extern "C" int gx_wcc_part_hook(gx_graph *g, uint64_t v0, uint64_t v1, int32_t *
     GX_TRY(check_range(g, v0, v1, "gx_wcc_part_hook"));
     GX_HIP_TRY(hipSetDevice(g->ctx->device));
     hipStream_t s = pick_stream(g, stream);
+    GX_TRY(ensure_host_rp(g->ctx, g->A));
     const int64_t e0 = g->A.h_rp[v0], e1 = g->A.h_rp[v1];
     if (e1 > e0)
         hipLaunchKernelGGL(k_wccp_hook, dim3(grid_for((uint64_t)((e1 - e0 + 15) / 16), kPartBlock, 1u << 30)),

@@ -208,7 +208,8 @@ struct HostView {
     size_t n = 0;
     const LengthRuns *runs = nullptr;
     bool prefix = false;
-    HostView(const std::vector<T> &v) : p(v.data()), n(v.size()) {}
+    template <typename Alloc>
+    HostView(const std::vector<T, Alloc> &v) : p(v.data()), n(v.size()) {}
     HostView(const T *ptr, size_t count) : p(ptr), n(count) {}
     HostView(const LengthRuns *r, bool pre) : n(pre ? r->n + 1 : r->n), runs(r), prefix(pre) {}
     size_t size() const { return n; }

@@ -600,6 +600,7 @@ static int pr_single_plan_adaptive(gx_graph *g, PrPart **out) {
     hipStream_t s = ctx->stream;
     DevCSR &P = g->directed ? g->AT : g->A;
     PlanClock clk("single", s);
+    GX_TRY(ensure_host_rp(ctx, g->A));
     std::vector<int32_t> h_outdeg(n), order, perm;
     for (uint64_t v = 0; v < n; v++) h_outdeg[v] = (int32_t)(g->A.h_rp[v + 1] - g->A.h_rp[v]);
     hub_order(h_outdeg, order, perm);

@@ -51,7 +51,7 @@ extern "C" int gx_init(int device, gx_ctx **out) {
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
-    for (int i = 0; i < 2 && e == hipSuccess; i++) {
+    for (int i = 0; i < gx_ctx::kStageBufs && e == hipSuccess; i++) {
         e = hipHostMalloc(&ctx->staging[i], gx_ctx::kStageBytes);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming);
     }
@@ -94,7 +94,7 @@ extern "C" int gx_free(gx_ctx *ctx) {
         if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
     }
     if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < gx_ctx::kStageBufs; i++) {
         if (ctx->stage_ev[i]) (void)hipEventDestroy(ctx->stage_ev[i]);
         if (ctx->staging[i]) (void)hipHostFree(ctx->staging[i]);
     }
@@ -192,6 +192,14 @@ int download(gx_ctx *ctx, void *dst, const void *src_dev, uint64_t count, Xfer k
     return GX_SUCCESS;
 }
 
+int ensure_host_rp(gx_ctx *ctx, DevCSR &c) {
+    if (c.h_rp.size() == c.n + 1) return GX_SUCCESS;
+    HostRowPtr h(c.n + 1);
+    GX_TRY(download(ctx, h.data(), c.rp.p, c.n + 1, Xfer::Raw64));
+    c.h_rp.swap(h);
+    return GX_SUCCESS;
+}
+
 int ensure_aux_streams(gx_ctx *ctx) {
     if (ctx->aux[0]) return GX_SUCCESS;
     for (int i = 0; i < 2; i++) {
@@ -263,18 +271,48 @@ int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool 
     hipStream_t s = ctx->stream;
     *bad = false;
     int c = 0;
+    static const bool times = [] {
+        const char *e = std::getenv("GX_PLAN_TIMES");
+        return e && std::atoi(e) != 0;
+    }();
+    auto env_int = [](const char *name, int def) {
+        const char *e = std::getenv(name);
+        return e ? std::atoi(e) : def;
+    };
+    const int nbuf = std::min(std::max(env_int("GX_UPLOAD_BUFS", 2), 2), gx_ctx::kStageBufs);
+    const int thr = env_int("GX_UPLOAD_THREADS", 0), saved_thr = host_threads();
+    if (thr > 0) host_set_threads(thr);
+    struct Restore {
+        int t;
+        bool on;
+        ~Restore() {
+            if (on) host_set_threads(t);
+        }
+    } restore{saved_thr, thr > 0};
+    using clk = std::chrono::steady_clock;
+    double t_wait = 0, t_fill = 0;
+    const auto t0 = clk::now();
     for (uint64_t off = 0; off < count; off += chunk, c++) {
-        const int b = c & 1;
+        const int b = c % nbuf;
         const uint64_t cnt = std::min<uint64_t>(chunk, count - off);
-        if (c >= 2) GX_HIP_TRY(hipEventSynchronize(ctx->stage_ev[b]));   // its previous copy is done
+        auto ta = clk::now();
+        if (c >= nbuf) GX_HIP_TRY(hipEventSynchronize(ctx->stage_ev[b]));   // its previous copy is done
+        auto tb = clk::now();
         if (!fill(off, cnt, ctx->staging[b])) {
             *bad = true;
             break;
         }
+        auto tc = clk::now();
+        t_wait += std::chrono::duration<double, std::milli>(tb - ta).count();
+        t_fill += std::chrono::duration<double, std::milli>(tc - tb).count();
         GX_HIP_TRY(hipMemcpyAsync(dst + off * elem, ctx->staging[b], cnt * elem, hipMemcpyHostToDevice, s));
         GX_HIP_TRY(hipEventRecord(ctx->stage_ev[b], s));
     }
     GX_HIP_TRY(hipStreamSynchronize(s));
+    if (times)
+        std::fprintf(stderr, "[upload] %llu x %zu B, %d buffers, %d threads: %8.2f ms (host fill %.2f ms, copy wait %.2f ms)\n",
+                     (unsigned long long)count, elem, nbuf, host_threads(),
+                     std::chrono::duration<double, std::milli>(clk::now() - t0).count(), t_fill, t_wait);
     return GX_SUCCESS;
 }
 
@@ -290,8 +328,10 @@ extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_gr
         return fail(GX_NOT_IMPLEMENTED, "gx_graph_create: n >= 2^31 needs 64-bit column indices");
     if (A->rowptr[0] != 0 || A->rowptr[A->n] != A->nnz)
         return fail(GX_INVALID_VALUE, "gx_graph_create: inconsistent row pointers");
+    PlanClock clk("graph_create", ctx->stream);
     if (!host_monotone(A->rowptr, A->n)) return fail(GX_INVALID_VALUE, "gx_graph_create: row pointers not monotone");
     GX_HIP_TRY(hipSetDevice(ctx->device));
+    clk.mark("checks");
     const uint64_t n = A->n, nnz = A->nnz;
     std::unique_ptr<gx_graph> g(new gx_graph());
     g->ctx = ctx;
@@ -301,22 +341,24 @@ extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_gr
     g->weighted = A->vals != nullptr;
     g->A.n = n;
     g->A.nnz = nnz;
-    g->A.h_rp.resize(n + 1);
-    host_copy(g->A.h_rp.data(), A->rowptr, (n + 1) * 8);
     GX_TRY(g->A.rp.alloc(n + 1));
     GX_TRY(g->A.ci.alloc(nnz, 16));
     if (g->weighted) GX_TRY(g->A.w.alloc(nnz));
+    clk.mark("device buffers");
     bool bad = false;
+    const char *nt_env = std::getenv("GX_UPLOAD_NT");
+    const bool nt = !nt_env || std::atoi(nt_env) != 0;   // streaming stores unless GX_UPLOAD_NT=0
     GX_TRY(upload(ctx, reinterpret_cast<char *>(g->A.rp.p), n + 1, 8,
                   [&](uint64_t off, uint64_t cnt, void *buf) {
-                      host_copy(buf, g->A.h_rp.data() + off, cnt * 8);
+                      host_copy(buf, reinterpret_cast<const int64_t *>(A->rowptr) + off, cnt * 8);
                       return true;
                   }, &bad));
     GX_TRY(upload(ctx, reinterpret_cast<char *>(g->A.ci.p), nnz, 4,
                   [&](uint64_t off, uint64_t cnt, void *buf) {
-                      return host_narrow(A->colidx + off, cnt, n, static_cast<int32_t *>(buf));
+                      return host_narrow(A->colidx + off, cnt, n, static_cast<int32_t *>(buf), nt);
                   }, &bad));
     if (bad) return fail(GX_INVALID_INDEX, "gx_graph_create: column out of range");
+    clk.mark("upload");
     if (g->weighted)
         GX_TRY(upload(ctx, reinterpret_cast<char *>(g->A.w.p), nnz, 8,
                       [&](uint64_t off, uint64_t cnt, void *buf) {
@@ -372,7 +414,8 @@ void free_copy(gx_graph *h) { (void)gx_graph_free(h); }
 int build_hub(gx_graph *g) {
     const int64_t n = (int64_t)g->n;
     hipStream_t s = g->ctx->stream;
-    const std::vector<int64_t> &h = g->A.h_rp;
+    GX_TRY(ensure_host_rp(g->ctx, g->A));
+    const HostRowPtr &h = g->A.h_rp;
     int64_t maxd = 0;
     for (int64_t v = 0; v < n; v++) maxd = std::max(maxd, h[v + 1] - h[v]);
     std::vector<int64_t> start((size_t)maxd + 2, 0);

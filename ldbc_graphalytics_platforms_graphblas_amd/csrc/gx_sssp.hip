@@ -907,6 +907,7 @@ int ensure_sssp_layout(gx_graph *g, double delta, hipStream_t s) {
     auto L = std::make_unique<SsspLayout>();
     L->delta = delta;
     L->n_active = n;
+    GX_TRY(ensure_host_rp(g->ctx, g->A));
     if ((int64_t)g->A.h_rp.size() == n + 1) {
         L->n_active = 0;
         for (int64_t v = 0; v < n; v++) L->n_active += g->A.h_rp[v + 1] != g->A.h_rp[v];

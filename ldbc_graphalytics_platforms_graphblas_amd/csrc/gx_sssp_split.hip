@@ -935,6 +935,7 @@ static int split_build(gx_sssp_split *p, gx_graph *g) {
     // vertices with edges (gx_sssp's rule; GX_SSSP_PULL = 0 never, 2 always); buckets are fused
     // while they hold at most n / 16 vertices (GX_SSSP_FUSE)
     int64_t nonisolated = n;
+    GX_TRY(ensure_host_rp(g->ctx, g->A));
     if ((int64_t)g->A.h_rp.size() == n + 1) {
         nonisolated = 0;
         for (int64_t v = 0; v < n; v++) nonisolated += g->A.h_rp[v + 1] != g->A.h_rp[v];
