@@ -79,7 +79,7 @@ DOMINANT = {"bfs": ["bfs_topdown"], "wcc": ["wcc_hook"], "sssp": ["sssp_relax"],
 KERNELS = {"bfs": ["bfs_topdown", "bfs_bottomup"], "wcc": ["wcc_sample", "wcc_hook", "wcc_compress"],
            "sssp": ["sssp_relax", "sssp_advance"],
            "cdlp": ["cdlp_tiny", "cdlp_small", "cdlp_light_s", "cdlp_light", "cdlp_mid2", "cdlp_mid4", "cdlp_mid",
-                    "cdlp_heavy", "cdlp_first", "cdlp_mark", "cdlp_sparse"],
+                    "cdlp_heavy", "cdlp_first", "cdlp_mark", "cdlp_keep", "cdlp_sparse"],
            "lcc": ["lcc_orient", "lcc_triangles", "lcc_core"]}
 
 

@@ -9,8 +9,8 @@
 // atomics that never lose an update (the reference's LDS insert is unlocked,
 // cdlp_kernel.cu:685-694), in-edges are included for directed graphs, and degree-0 vertices
 // are written (cdlp_kernel.cu:108-112, 1060-1063).
-//   deg <= 16        : one thread per vertex, labels and counts in registers.
-//   deg <= 64        : one wave per vertex, labels in registers, counts by 64 shuffles.
+//   deg <= 32        : one thread per vertex, labels in registers (vote, else a register sort).
+//   deg <= 64        : one wave per vertex, labels in registers, counts by ballots.
 //   deg <= kLdsHash/2: one wave per vertex, open-addressing hash table in that wave's LDS
 //   (kLightSlots slots for deg <= kLightSlots/2, kLdsHash slots above).
 //   deg <= 2048      : one 256-thread workgroup per vertex, 4K-slot LDS table (4 per CU).
@@ -62,9 +62,14 @@ struct CdlpArgs {
     // have nothing to do unless *dense
     int sparse;
     int cshards;   // *changed is cshards words kFlagStride apart (raise_flag_sharded)
+    // own-label check of a dense active iteration ran (k_cdlp_keep_*): k_cdlp_tiny recomputes
+    // every tiny vertex although the iteration is sparse (null: never)
+    const int *keep = nullptr;
 };
 
 __device__ __forceinline__ bool tier_idle(const CdlpArgs &a) { return a.sparse && *a.dense == 0; }
+
+__device__ __forceinline__ bool keep_on(const CdlpArgs &a) { return a.keep && *a.keep != 0; }
 
 // Uniform per launch: whether every vertex is recomputed.
 __device__ __forceinline__ bool all_active(const CdlpArgs &a) { return !a.act || *a.dense; }
@@ -216,14 +221,34 @@ __device__ __forceinline__ Vote wave_vote(Vote v) {
 }
 
 // Tiny vertices (deg <= kTiny, including isolated ones): one THREAD per vertex, labels in
-// registers (clamped loads, all in flight), mode by register compares -- 64 vertices per wave
-// instead of one (two thirds of the vertices of a power-law graph have degree <= 8).
-constexpr int kTiny = 16;
+// registers (all loads in flight), 64 vertices per wave instead of one (two thirds of the
+// vertices of a power-law graph have degree <= 8, 84 % of SYN-7_5's <= 32).  The strict-
+// majority vote first; else the labels are sorted in registers (a bitonic network, unrolled)
+// and the longest run wins, the first one (smallest label) among equal runs.
+constexpr int kTiny = 32;
+
+__device__ __forceinline__ void sort_regs(uint32_t (&L)[kTiny]) {
+#pragma unroll
+    for (int k = 2; k <= kTiny; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < kTiny; i++) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint32_t x = L[i], y = L[l];
+                    const bool up = (i & k) == 0;
+                    L[i] = up ? min(x, y) : max(x, y);
+                    L[l] = up ? max(x, y) : min(x, y);
+                }
+            }
+}
 
 __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
-    if (tier_idle(a)) return;
+    const bool kp = keep_on(a);
+    if (tier_idle(a) && !kp) return;
     bool any = false;
-    const bool all = all_active(a);
+    const bool all = all_active(a) || kp;
     for (int64_t v = a.v0 + (int64_t)blockIdx.x * kCdlpBlock + threadIdx.x; v < a.v1;
          v += (int64_t)gridDim.x * kCdlpBlock) {
         const int64_t ob = a.rpA[v], od = a.rpA[v + 1] - ob;
@@ -239,7 +264,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
         if (d > 0 && active(a, all, v)) {
             uint32_t L[kTiny];
 #pragma unroll
-            for (int k = 0; k < kTiny; k++) L[k] = (uint32_t)label_at(a, ob, od, ib, min((int64_t)k, d - 1));
+            for (int k = 0; k < kTiny; k++) L[k] = k < d ? (uint32_t)label_at(a, ob, od, ib, k) : kEmpty;
             Vote vt{kEmpty, 0u};
 #pragma unroll
             for (int k = 0; k < kTiny; k++) vt = vote_add(vt, L[k], k < d);
@@ -249,20 +274,20 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
             if (a.first) {
                 uint32_t mn = kEmpty;
 #pragma unroll
-                for (int k = 0; k < kTiny; k++) mn = k < d ? min(mn, L[k]) : mn;
+                for (int k = 0; k < kTiny; k++) mn = min(mn, L[k]);   // padding is kEmpty
                 best = (int32_t)mn;
             } else if (2 * (int64_t)nc > d) {
                 best = (int32_t)vt.c;   // strict majority
             } else {
-                uint32_t bc = 0, bl = kEmpty;
+                sort_regs(L);           // labels ascending, the padding last
+                uint32_t bc = 0, bl = kEmpty, run = 0, prev = kEmpty;
 #pragma unroll
-                for (int i = 0; i < kTiny; i++) {
-                    uint32_t c = 0;
-#pragma unroll
-                    for (int j = 0; j < kTiny; j++) c += (j < d && L[j] == L[i]) ? 1u : 0u;
-                    if (i < d && (c > bc || (c == bc && L[i] < bl))) {
-                        bc = c;
-                        bl = L[i];
+                for (int k = 0; k < kTiny; k++) {
+                    run = L[k] == prev ? run + 1u : 1u;
+                    prev = L[k];
+                    if (k < d && run > bc) {
+                        bc = run;
+                        bl = L[k];
                     }
                 }
                 best = (int32_t)bl;
@@ -1045,6 +1070,189 @@ __global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const 
     if (any) raise_flag_sharded(a.changed, a.cshards);
 }
 
+// ---- own-label check (dense active iterations) ----------------------------------------
+// From the third iteration on, a vertex whose own label is held by more than half of its
+// neighbours keeps it: that label is then the unique mode (SYN-7_5: every vertex of degree
+// > 16 but 17 % passes at the third iteration, all but 0.05 % of the entries at the fourth).
+// When an iteration's active set overflowed (*dense), one edge-parallel pass counts, per
+// vertex of degree > kTiny, the neighbours holding its label; the vertices that fail go to
+// the sparse iteration's activation lists (huge ones are stamped for their tier), tiny ones
+// are recomputed by k_cdlp_tiny, and the iteration turns sparse (*dense = 0).  This replaces
+// the tier kernels' pass over every vertex (~0.5 ms per dense iteration on SYN-7_5).
+//
+// Edge-parallel layout of a CSR (built once per graph): bit k of word s says that a
+// non-empty row starts at entry 64 s + k, sne[s] is the position in ne (the non-empty rows,
+// ascending) of the row that holds entry 64 s.  Lane k of a 64-entry slab then finds its row
+// as ne[sne[s] + popcount(bits up to k) - bit 0], without a search.
+__global__ __launch_bounds__(256) void k_keep_flags(const int64_t *__restrict__ rp, int64_t n, int64_t *flag) {
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += (int64_t)gridDim.x * 256)
+        flag[v] = rp[v + 1] > rp[v] ? 1 : 0;
+}
+
+// ne holds each row with its sign bit set when its degree (out + in) is at most kTiny: those
+// are k_cdlp_tiny's, the check skips their entries.
+__global__ __launch_bounds__(256) void k_keep_layout(const int64_t *__restrict__ rp, int64_t n,
+                                                     const int64_t *__restrict__ nepos, const int64_t *__restrict__ rpA,
+                                                     const int64_t *__restrict__ rpT, int32_t *ne,
+                                                     unsigned long long *bits, int32_t *sne) {
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += (int64_t)gridDim.x * 256) {
+        const int64_t b = rp[v], e = rp[v + 1];
+        if (e == b) continue;
+        const int32_t p = (int32_t)nepos[v];
+        ne[p] = cdlp_degree(rpA, rpT, v) > kTiny ? (int32_t)v : (int32_t)((uint32_t)v | 0x80000000u);
+        atomicOr(&bits[b >> 6], 1ull << (b & 63));
+        for (int64_t sl = (b + kWave - 1) / kWave; sl * kWave < e; sl++) sne[sl] = p;
+    }
+}
+
+// Counts, for every row of degree > kTiny (out + in degree), the entries of this CSR whose
+// label equals the row's own label, into kcnt.  A wave takes kKeepU consecutive 64-entry slabs
+// with every load of the chunk issued before the first compare (the chain is bits / sne ->
+// ne -> labels), and carries its last row's count across the slabs: one atomic per row and
+// chunk.  The first launch of an iteration (A's entries) also records whether the check runs
+// (*keep = *dense) and empties the activation lists.
+struct alignas(64) KeepW8 {
+    unsigned long long w[8];
+};
+struct alignas(32) KeepS8 {
+    int32_t s[8];
+};
+constexpr int64_t kKeepPad = 32;   // the layout's slabs rounded up to this (the largest chunk)
+
+template <int kKeepU>
+__global__ __launch_bounds__(256) void k_cdlp_keep_count(const int32_t *__restrict__ ci, int64_t nnz,
+                                                         const unsigned long long *__restrict__ bits,
+                                                         const int32_t *__restrict__ sne, const int32_t *__restrict__ ne,
+                                                         const int32_t *__restrict__ lab, uint32_t *kcnt,
+                                                         const int *dense, int *keep, unsigned int *lcounts, int head) {
+    const bool run = *dense != 0;
+    if (head && blockIdx.x == 0) {
+        if (threadIdx.x == 0) *keep = run ? 1 : 0;
+        if (run)
+            for (int i = threadIdx.x; i < 3 * kCdlpSubs; i += 256) lcounts[(int64_t)i * kCntStride] = 0u;
+    }
+    if (!run) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    // wave-uniform in the compiler's view too: the slab words and row positions are scalar loads
+    const int64_t gw = (int64_t)blockIdx.x * (256 / kWave) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
+    const int64_t nslabs = (nnz + kWave - 1) / kWave;
+    const int64_t nchunks = (nslabs + kKeepU - 1) / kKeepU;
+    const unsigned long long upto = lane == kWave - 1 ? ~0ull : (2ull << lane) - 1ull;
+    for (int64_t ch = gw; ch < nchunks; ch += nw) {
+        const int64_t sl0 = ch * kKeepU;
+        // every load unconditional (clamped indices): predicated loads would each wait in turn.
+        // The chunk's slab words and row positions are two wide scalar loads (the layout is
+        // padded to whole chunks, zero words past the last slab).
+        unsigned long long W[kKeepU];
+        int32_t R[kKeepU], Cl[kKeepU], S[kKeepU];
+#pragma unroll
+        for (int h = 0; h < kKeepU / 8; h++) {
+            const KeepW8 wb = *reinterpret_cast<const KeepW8 *>(bits + sl0 + 8 * h);
+            const KeepS8 sb = *reinterpret_cast<const KeepS8 *>(sne + sl0 + 8 * h);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                W[8 * h + i] = wb.w[i];
+                S[8 * h + i] = sb.s[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kKeepU; u++) Cl[u] = ci[min(sl0 * kWave + u * kWave + lane, nnz - 1)];
+#pragma unroll
+        for (int u = 0; u < kKeepU; u++) R[u] = ne[S[u] + __popcll(W[u] & upto) - (int)(W[u] & 1ull)];
+        uint32_t M = 0, V = 0;   // bit u: lane's entry of slab u is checked / holds the row's own label
+#pragma unroll
+        for (int u = 0; u < kKeepU; u++) {
+            const int32_t x = lab[Cl[u]], y = lab[R[u] & 0x7fffffff];
+            const bool valid = (sl0 + u) * kWave + lane < nnz && R[u] >= 0;
+            V |= valid ? 1u << u : 0u;
+            M |= valid && x == y ? 1u << u : 0u;
+        }
+        int32_t crow = -1;
+        uint32_t ccnt = 0;
+#pragma unroll
+        for (int u = 0; u < kKeepU; u++) {
+            const bool valid = (V >> u) & 1u;
+            const int seg = __popcll(W[u] & upto);
+            unsigned long long rem = __ballot(valid);
+            while (rem) {
+                const int lead = __ffsll((long long)rem) - 1;
+                const int sg = __builtin_amdgcn_readlane(seg, lead);
+                const int32_t r = __builtin_amdgcn_readlane(R[u], lead);
+                const bool in = valid && seg == sg;
+                const unsigned long long grp = __ballot(in);
+                const uint32_t c = (uint32_t)__popcll(__ballot(in && ((M >> u) & 1u)));
+                if (r == crow) {
+                    ccnt += c;
+                } else {
+                    if (ccnt && lane == 0) atomicAdd(&kcnt[crow], ccnt);
+                    crow = r;
+                    ccnt = c;
+                }
+                rem &= ~grp;
+            }
+        }
+        if (ccnt && lane == 0) atomicAdd(&kcnt[crow], ccnt);
+    }
+}
+
+// Per vertex of degree > kTiny: keep (2 count > degree) or recompute: onto the activation list
+// of its degree (the sparse kernels' lists, shard = wave index mod kCdlpSubs), or, huge, the
+// iteration's stamp for the huge tier (a kept huge vertex loses a stamp k_cdlp_mark gave it).
+// kcnt is left zero.  A full list sets *kover.
+__global__ __launch_bounds__(256) void k_cdlp_keep_apply(const int64_t *__restrict__ rpA, const int64_t *__restrict__ rpT,
+                                                         int64_t v0, int64_t v1, uint32_t *kcnt, int32_t *act,
+                                                         int32_t stamp, const int *keep, unsigned int *counts,
+                                                         int32_t *al, int64_t asub, int *kover) {
+    if (*keep == 0) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t gw = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave;
+    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
+    const int j = (int)(gw % kCdlpSubs);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int64_t b = v0 + gw * kWave; b < v1; b += nw * kWave) {
+        const int64_t v = b + lane;
+        int L = -1;
+        if (v < v1) {
+            const int64_t d = cdlp_degree(rpA, rpT, v);
+            if (d > kTiny) {
+                const uint32_t c = kcnt[v];
+                if (c) kcnt[v] = 0u;
+                const bool kept = 2 * (int64_t)c > d;
+                if (d > kMidMax) {
+                    if (!kept) act[v] = stamp;
+                    else if (act[v] == stamp) act[v] = stamp - 1;
+                } else if (!kept) {
+                    L = d <= kSparseWaveMax ? 0 : d <= kSparseG2Max ? 1 : 2;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const unsigned long long m = __ballot(L == q);
+            if (!m) continue;
+            unsigned int base = 0;
+            if (lane == 0) base = atomicAdd(&counts[((1 + q) * kCdlpSubs + j) * kCntStride], (unsigned int)__popcll(m));
+            base = __shfl(base, 0, kWave);
+            if (L == q) {
+                const unsigned int idx = base + (unsigned int)__popcll(m & below);
+                if (idx < (unsigned int)asub) al[((int64_t)q * kCdlpSubs + j) * asub + idx] = (int32_t)v;
+                else *kover = 1;
+            }
+        }
+    }
+}
+
+// The check's outcome: lists that fit make the iteration sparse; a full one leaves it dense
+// (every tier kernel recomputes every vertex, as without the check).
+__global__ void k_cdlp_keep_finish(int *dense, int *keep, int *kover) {
+    if (*keep) {
+        if (*kover) *keep = 0;
+        else *dense = 0;
+    }
+    *kover = 0;
+}
+
 // First iteration of an undirected graph whose rows are sorted by column: every label is still
 // its vertex id, so the result is the row's first column (the smallest neighbour), one load per
 // vertex instead of a pass over every label (~470 us of tier kernels on SYN-7_5).
@@ -1292,12 +1500,13 @@ struct SparseLists {
 
 int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
                    const int32_t *act = nullptr, int32_t stamp = 0, const int *dense = nullptr, bool first = false,
-                   const SparseLists *sl = nullptr, int cshards = 1) {
+                   const SparseLists *sl = nullptr, int cshards = 1, const int *keep = nullptr) {
     gx_ctx *ctx = g.ctx;
     const int64_t n = g.n;
     CdlpArgs a{g.rpA,  g.ciA,  g.rpT, g.ciT,  cur,        nxt,     n,        changed,
                P.v0,   P.v1,   act,   stamp,  dense,      first && !g.directed ? 1 : 0,
                sl ? 1 : 0,     cshards};
+    a.keep = keep;
     const bool tiers = !(sl && sl->only);   // sparse-only: the huge tier alone beside the sparse kernels
     if (sl) {
         // exit at once when *dense (the tier kernels below then recompute every vertex)
@@ -1317,6 +1526,11 @@ int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t 
                            sl->al + 2 * shards, sl->asub, cnt + 2 * kCdlpSubs * kCntStride, o ? P.d_mv4.p : nullptr,
                            (int64_t)P.n_mid4, o ? P.d_mv.p : nullptr, (int64_t)P.n_mid);
         GX_TRY(check_launch("k_cdlp_sparse_group"));
+        if (o && keep && P.v1 > P.v0) {   // the own-label check's tiny vertices (no tier kernels here)
+            hipLaunchKernelGGL(k_cdlp_tiny, dim3(grid_for((uint64_t)(P.v1 - P.v0), kCdlpBlock, 8192)),
+                               dim3(kCdlpBlock), 0, s, a);
+            GX_TRY(check_launch("k_cdlp_tiny"));
+        }
     }
     hipStream_t s1 = s, s2 = s;   // one stream: overlapped tier kernels slowed each other down
     if (tiers && P.n_mid2) {
@@ -1407,6 +1621,15 @@ struct CdlpCache {
     int64_t sub = 0, asub = 0;
     bool rows_sorted = false;   // A's rows sorted by column (k_rows_sorted)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    // the own-label check's edge-parallel layout of G's A (and A'), its counters and flags
+    // (keep, kover); built by the first call that needs it
+    struct KeepCsr {
+        DBuf<unsigned long long> bits;
+        DBuf<int32_t> sne, ne;
+    } kA, kT;
+    DBuf<uint32_t> kcnt;
+    DBuf<int> kflags;
+    bool keep_built = false;
     ~CdlpCache() {
         if (hflag) (void)hipHostFree(hflag);
         for (hipEvent_t e : ev)
@@ -1475,6 +1698,43 @@ int cdlp_relabel(gx_graph *g, CdlpCache &C, hipStream_t s) {
     return GX_SUCCESS;
 }
 
+// The own-label check's layout of one CSR (k_keep_layout).
+int keep_layout(const int64_t *rp, int64_t n, int64_t nnz, const int64_t *rpA, const int64_t *rpT, CdlpCache::KeepCsr &K,
+                hipStream_t s) {
+    const int64_t nslabs = (nnz + kWave - 1) / kWave;
+    const size_t padded = (size_t)((nslabs + kKeepPad - 1) / kKeepPad * kKeepPad + kKeepPad);
+    GX_TRY(K.bits.alloc(padded));
+    GX_TRY(K.sne.alloc(padded));
+    GX_TRY(K.ne.alloc((size_t)std::max<int64_t>(n, 1)));
+    GX_HIP_TRY(hipMemsetAsync(K.bits.p, 0, padded * 8, s));
+    GX_HIP_TRY(hipMemsetAsync(K.sne.p, 0, padded * 4, s));
+    GX_HIP_TRY(hipMemsetAsync(K.ne.p, 0, (size_t)std::max<int64_t>(n, 1) * 4, s));
+    if (n == 0 || nnz == 0) return GX_SUCCESS;
+    DBuf<int64_t> flag, pos;
+    GX_TRY(flag.alloc(n));
+    GX_TRY(pos.alloc(n));
+    hipLaunchKernelGGL(k_keep_flags, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, rp, n, flag.p);
+    GX_TRY(check_launch("k_keep_flags"));
+    GX_TRY(scan_exclusive_i64(flag.p, pos.p, (size_t)n, s));
+    hipLaunchKernelGGL(k_keep_layout, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, rp, n, pos.p, rpA, rpT, K.ne.p,
+                       K.bits.p, K.sne.p);
+    GX_TRY(check_launch("k_keep_layout"));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // flag / pos die at return
+    return GX_SUCCESS;
+}
+
+int keep_build(CdlpCache &C, hipStream_t s) {
+    const CdlpGraph &G = C.G;
+    GX_TRY(keep_layout(G.rpA, G.n, G.nnzA, G.rpA, G.rpT, C.kA, s));
+    if (G.directed) GX_TRY(keep_layout(G.rpT, G.n, G.nnzT, G.rpA, G.rpT, C.kT, s));
+    GX_TRY(C.kcnt.alloc((size_t)std::max<int64_t>(G.n, 1)));
+    GX_HIP_TRY(hipMemsetAsync(C.kcnt.p, 0, (size_t)std::max<int64_t>(G.n, 1) * 4, s));
+    GX_TRY(C.kflags.alloc(2));
+    GX_HIP_TRY(hipMemsetAsync(C.kflags.p, 0, 2 * sizeof(int), s));
+    C.keep_built = true;
+    return GX_SUCCESS;
+}
+
 // The staging plan: every entry's column, sorted within kStageBlock-entry blocks, and its
 // position in the block.
 int cdlp_cache(gx_graph *g, int iters, bool relabel, CdlpCache **out, hipStream_t s) {
@@ -1496,7 +1756,9 @@ int cdlp_cache(gx_graph *g, int iters, bool relabel, CdlpCache **out, hipStream_
         GX_TRY(fresh->act.alloc(n));
         fresh->sub = std::max<int64_t>(16, n / 32 / kCdlpSubs);   // entries per sub-list
         GX_TRY(fresh->clist.alloc((size_t)fresh->sub * kCdlpSubs));
-        fresh->asub = std::max<int64_t>(16, n / 16 / kCdlpSubs);   // active vertices per shard and list
+        // active vertices per shard and list (GX_CDLP_ASUB: a test's small capacity, so lists overflow)
+        fresh->asub = std::max<int64_t>(16, n / 8 / kCdlpSubs);
+        if (const char *e = std::getenv("GX_CDLP_ASUB")) fresh->asub = std::max<int64_t>(1, std::atoll(e));
         GX_TRY(fresh->al.alloc((size_t)fresh->asub * kCdlpSubs * (kCdlpLists - 1)));
         GX_TRY(fresh->dense.alloc(1));
         if (!g->directed && g->nnz > 0) {
@@ -1593,6 +1855,10 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
     const char *lg = std::getenv("GX_CDLP_LAG");
     const int lag = lg && std::atoi(lg) == 1 ? 1 : 2;
     const int64_t sub = C->sub;
+    // GX_CDLP_KEEP=0: a dense active iteration runs the tier kernels over every vertex instead
+    // of the own-label check
+    const bool keep = active && use_sparse && env_on("GX_CDLP_KEEP");
+    if (keep && !C->keep_built) GX_TRY(keep_build(*C, s));
     if (active) {
         hipLaunchKernelGGL(k_cdlp_fill_u32, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s,
                            reinterpret_cast<uint32_t *>(C->act.p), 0xffffffffu, n);   // stamp -1: never active
@@ -1604,22 +1870,50 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         int *changed = C->changed.p + (size_t)it * kFlagShards * kFlagStride;
         if (active && it >= 2) {
             // nxt still holds the input of iteration it-1, cur its output
-            KTimer kt(ctx, "cdlp_mark", s);
             unsigned int *cnt = C->ccount.p + (size_t)it * kCdlpLists * kCdlpSubs * kCntStride;
-            hipLaunchKernelGGL(k_cdlp_changed, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, nxt, cur, G.rpA, G.rpT,
-                               n, C->clist.p, sub, cnt, C->dense.p);
-            GX_TRY(check_launch("k_cdlp_changed"));
-            // 32 waves per shard of the change list (the grid must be a multiple of kCdlpSubs waves)
-            hipLaunchKernelGGL(k_cdlp_mark, dim3(8 * kCdlpSubs), dim3(kCdlpSubs), 0, s, G.rpA, G.ciA, G.rpT, G.ciT,
-                               C->clist.p, sub, cnt, C->act.p, (int32_t)it, C->dense.p, C->al.p, C->asub);
-            GX_TRY(check_launch("k_cdlp_mark"));
+            {
+                KTimer kt(ctx, "cdlp_mark", s);
+                hipLaunchKernelGGL(k_cdlp_changed, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, nxt, cur, G.rpA,
+                                   G.rpT, n, C->clist.p, sub, cnt, C->dense.p);
+                GX_TRY(check_launch("k_cdlp_changed"));
+                // 32 waves per shard of the change list (the grid must be a multiple of kCdlpSubs waves)
+                hipLaunchKernelGGL(k_cdlp_mark, dim3(8 * kCdlpSubs), dim3(kCdlpSubs), 0, s, G.rpA, G.ciA, G.rpT, G.ciT,
+                                   C->clist.p, sub, cnt, C->act.p, (int32_t)it, C->dense.p, C->al.p, C->asub);
+                GX_TRY(check_launch("k_cdlp_mark"));
+            }
             // sparse-only (no idle tier launches, ~60 us per iteration on SYN-7_5) when iteration
             // it-1-lag, the last whose flags the host has seen, did not overflow its lists: changes
             // shrink as labels settle.  A wrong guess costs the fallback lists' full pass.
             const bool only = sparse_only == 2 || (sparse_only == 1 && it >= 3 + lag && (hflag[it - 1 - lag] & 2) == 0);
+            // the own-label check where the iteration may be dense (in a sparse-only one its three
+            // idle launches cost more than the rare dense case's fallback pass)
+            int *kf = keep && (!only || sparse_only == 2) ? C->kflags.p : nullptr;
+            if (kf) {
+                KTimer kk(ctx, "cdlp_keep", s);
+                // counts of the own label among each vertex's neighbours (exit unless *dense)
+                // one wave per U slabs (the count kernel exits unless *dense); GX_CDLP_KEEP_U = 8 / 16 / 32
+                const char *ku = std::getenv("GX_CDLP_KEEP_U");
+                const int U = ku ? std::atoi(ku) : 16;
+                auto count = [&](const int32_t *ci, int64_t nnz_, const CdlpCache::KeepCsr &K, int head) {
+                    const unsigned grid = grid_for(
+                        (uint64_t)std::max<int64_t>(1, (nnz_ + (int64_t)kWave * U - 1) / ((int64_t)kWave * U)) * kWave, 256,
+                        16384);
+                    const auto kern = U == 8 ? k_cdlp_keep_count<8> : U == 32 ? k_cdlp_keep_count<32> : k_cdlp_keep_count<16>;
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, ci, nnz_, K.bits.p, K.sne.p, K.ne.p, cur,
+                                       C->kcnt.p, C->dense.p, kf, cnt + kCdlpSubs * kCntStride, head);
+                    return check_launch("k_cdlp_keep_count");
+                };
+                GX_TRY(count(G.ciA, G.nnzA, C->kA, 1));
+                if (G.directed) GX_TRY(count(G.ciT, G.nnzT, C->kT, 0));
+                hipLaunchKernelGGL(k_cdlp_keep_apply, dim3(8 * kCdlpSubs), dim3(256), 0, s, G.rpA, G.rpT, (int64_t)0, n,
+                                   C->kcnt.p, C->act.p, (int32_t)it, kf, cnt, C->al.p, C->asub, kf + 1);
+                GX_TRY(check_launch("k_cdlp_keep_apply"));
+                hipLaunchKernelGGL(k_cdlp_keep_finish, dim3(1), dim3(1), 0, s, C->dense.p, kf, kf + 1);
+                GX_TRY(check_launch("k_cdlp_keep_finish"));
+            }
             const SparseLists sl{C->al.p, C->asub, cnt, only};
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
-                                  use_sparse ? &sl : nullptr, kFlagShards));
+                                  use_sparse ? &sl : nullptr, kFlagShards, kf));
         } else if (it == 0 && C->rows_sorted && first_sorted) {
             // on the caller's graph and vertex order (whose rows the check found sorted)
             KTimer kt(ctx, "cdlp_first", s);

@@ -594,6 +594,14 @@ void host_copy(void *dst, const void *src, size_t bytes) {
     }
 }
 
+void host_prefault(void *p, size_t bytes) {
+    constexpr size_t kPage = 4096;
+    char *c = static_cast<char *>(p);
+    const int64_t np = (int64_t)((bytes + kPage - 1) / kPage);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < np; i++) *reinterpret_cast<volatile char *>(c + i * kPage) = 0;
+}
+
 int host_threads() { return omp_get_max_threads(); }
 
 void host_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }

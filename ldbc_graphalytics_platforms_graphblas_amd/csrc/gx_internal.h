@@ -37,10 +37,13 @@ void host_hub_order(const uint64_t *rp, uint64_t n, uint32_t *order);
 // the rows `rows[j]` of (rp, ci) as a local CSR (out_rp from 0) with columns renamed by colmap
 void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows, uint64_t nrows, const int32_t *colmap,
                     int64_t *out_rp, int32_t *out_ci);
-// CSR of A' (rows sorted)
+// Write one byte per 4 KiB page of a caller's output buffer (parallel) while the device
+// computes: its first-touch page faults are then off the result copy's critical path.
+void host_prefault(void *p, size_t bytes);
 // OpenMP threads of the calling host thread (gx_*_multi gives each device's thread a share)
 int host_threads();
 void host_set_threads(int n);
+// CSR of A' (rows sorted)
 void host_transpose(uint64_t n, const uint64_t *rp, const uint64_t *ci, uint64_t *trp, uint64_t *tci);
 
 }  // namespace gx

@@ -865,12 +865,14 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
     if (iters < 0) return fail(GX_INVALID_VALUE, "gx_pagerank: negative iteration count");
     const uint64_t n = g->n;
     if (n == 0) return GX_SUCCESS;
+    const auto t_entry = std::chrono::steady_clock::now();
     gx_ctx *ctx = g->ctx;
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     GX_TRY(device_begin(ctx));
     if (g->directed) GX_TRY(ensure_transpose(g));
     if (!g->pr) GX_TRY(pr_single_plan(g, &g->pr));
+    const auto t_plan = std::chrono::steady_clock::now();
     PrPart *p = g->pr;
     p->damping = damping;
     double *cur = p->xa.p, *nxt = p->xb.p;
@@ -879,17 +881,29 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
         GX_TRY(pr_step(p, cur, nxt, it == iters - 1 ? p->rank_out.p : nullptr, s));
         std::swap(cur, nxt);
     }
+    using clk = std::chrono::steady_clock;
+    static const bool times = std::getenv("GX_PLAN_TIMES") && std::atoi(std::getenv("GX_PLAN_TIMES")) != 0;
+    const auto t0 = clk::now();
+    auto ms = [&](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    clk::time_point t1 = t0;
     if (iters > 0) {
         hipLaunchKernelGGL(k_gather_perm, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, p->rank_out.p,
                            p->perm.p, (int64_t)n, p->result.p);
         GX_TRY(check_launch("k_gather_perm"));
+        host_prefault(rank, n * sizeof(double));
+        t1 = clk::now();
     }
     GX_TRY(device_end(ctx));
+    const auto t2 = clk::now();
     if (iters == 0) {
         for (uint64_t v = 0; v < n; v++) rank[v] = 1.0 / (double)n;
         return GX_SUCCESS;
     }
     GX_TRY(download(ctx, rank, p->result.p, n, Xfer::Raw64));
+    if (times)
+        std::fprintf(stderr, "[pagerank] plan %.2f ms, launches %.2f ms, prefault %.2f ms, device wait %.2f ms, "
+                     "result copy %.2f ms (device %.2f ms)\n", ms(t_entry, t_plan), ms(t_plan, t0), ms(t0, t1),
+                     ms(t1, t2), ms(t2, clk::now()), ctx->last_device_ms);
     return GX_SUCCESS;
 }
 
