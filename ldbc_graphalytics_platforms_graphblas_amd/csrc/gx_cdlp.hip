@@ -975,31 +975,36 @@ __global__ __launch_bounds__(256) void k_cdlp_sparse_wave(CdlpArgs a, const int3
     if (any) raise_flag_sharded(a.changed, a.cshards);
 }
 
-// Sparse iterations, active vertices of kSparseWaveMax < degree <= kMidMax: one workgroup each
-// with a kSlots-slot LDS table (the mid tier's method, without its pipelining).  Two shapes:
-// 256 threads / 4K slots (four workgroups per CU) up to kSparseG2Max, 1024 / 16K above.
+// Sparse iterations, active vertices of kSparseWaveMax < degree <= kMidMax: one workgroup each,
+// kMaxDeg / kBlock labels per thread in registers, the strict-majority vote, else a kSlots-slot
+// LDS table (the mid tier's method, without its pipelining).  Shapes: 256 threads / 4K slots
+// (four or more workgroups per CU) for both lists; a vertex above 2048 without a majority (its
+// 2d slots do not fit; none from SYN-7_5's fourth iteration on) is appended to `redo`, which
+// the 1024-thread / 16K-slot instance then recomputes (rin: that list, *rcount entries).
 // Fallback when *dense in a sparse-only iteration: every vertex of fl then fl2.
-template <int kBlock, int kSlots>
+template <int kBlock, int kSlots, int kMaxDeg>
 __global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const int32_t *__restrict__ gl,
                                                               int64_t asub, const unsigned int *gcount,
                                                               const int32_t *__restrict__ fl, int64_t fn,
-                                                              const int32_t *__restrict__ fl2, int64_t fn2) {
-    const bool full = *a.dense != 0;
+                                                              const int32_t *__restrict__ fl2, int64_t fn2,
+                                                              int32_t *redo, unsigned int *rcount,
+                                                              const int32_t *__restrict__ rin) {
+    const bool full = !rin && *a.dense != 0;
     if (full && !fl && !fl2) return;
     __shared__ uint32_t K[kSlots];
     __shared__ uint32_t C[kSlots];
     __shared__ unsigned long long red[kBlock / kWave];
     __shared__ uint32_t cnt[kBlock / kWave];
     __shared__ uint32_t bcast[1];
-    constexpr int R = kSlots / (2 * kBlock);
+    constexpr int R = kMaxDeg / kBlock;
     constexpr int NW = kBlock / kWave;
     const int tid = threadIdx.x;
     const int j = (int)(blockIdx.x % kCdlpSubs);   // the grid is a multiple of kCdlpSubs
-    const int32_t *src = full ? fl : gl + (int64_t)j * asub;
-    const int64_t c = full ? fn + fn2 : (int64_t)shard_count(gcount, j, asub);
-    const int64_t step = full ? gridDim.x : gridDim.x / kCdlpSubs;
+    const int32_t *src = rin ? rin : full ? fl : gl + (int64_t)j * asub;
+    const int64_t c = rin ? (int64_t)*rcount : full ? fn + fn2 : (int64_t)shard_count(gcount, j, asub);
+    const int64_t step = rin || full ? gridDim.x : gridDim.x / kCdlpSubs;
     bool any = false;
-    for (int64_t i = full ? blockIdx.x : blockIdx.x / kCdlpSubs; i < c; i += step) {
+    for (int64_t i = rin || full ? blockIdx.x : blockIdx.x / kCdlpSubs; i < c; i += step) {
         const int64_t v = full && i >= fn ? fl2[i - fn] : src[i];   // full: fn == 0 when fl is null
         const VMeta m = vmeta(a, v);
         const int64_t d = (int64_t)m.od + m.id;
@@ -1032,6 +1037,12 @@ __global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const 
 #pragma unroll
         for (int q = 0; q < NW; q++) nc += cnt[q];
         int32_t best = (int32_t)cand;
+        if (2 * (int64_t)nc <= d && 2 * d > kSlots) {
+            // no majority and no room for the table: the 16K-slot instance recomputes it
+            if (tid == 0) redo[atomicAdd(rcount, 1u)] = (int32_t)v;
+            __syncthreads();   // red / cnt / bcast are free for the next vertex
+            continue;
+        }
         if (2 * (int64_t)nc <= d) {
             int log2ts = 1;
             while ((1ll << log2ts) < 2 * d) log2ts++;
@@ -1496,6 +1507,8 @@ struct SparseLists {
     int64_t asub;
     const unsigned int *counts;   // the change list's counters, then the three lists'
     bool only;                    // sparse-only: no tier kernels but the huge ones
+    int32_t *redo;                // k_cdlp_sparse_group's vertices for the 16K-slot instance
+    unsigned int *rcount;         // this iteration's redo count (zero at its start)
 };
 
 int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
@@ -1518,14 +1531,19 @@ int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t 
         hipLaunchKernelGGL(k_cdlp_sparse_wave, dim3(8 * kCdlpSubs), dim3(256), 0, s, a, sl->al, sl->asub, cnt,
                            o ? P.d_wall.p : nullptr, (int64_t)P.n_wall);
         GX_TRY(check_launch("k_cdlp_sparse_wave"));
-        hipLaunchKernelGGL((k_cdlp_sparse_group<kMid2Block, kMid2Slots>), dim3(4 * kCdlpSubs), dim3(kMid2Block), 0, s,
-                           a, sl->al + shards, sl->asub, cnt + kCdlpSubs * kCntStride, o ? P.d_mv2.p : nullptr,
-                           (int64_t)P.n_mid2, nullptr, (int64_t)0);
+        hipLaunchKernelGGL((k_cdlp_sparse_group<kMid2Block, kMid2Slots, kMid2Max>), dim3(4 * kCdlpSubs),
+                           dim3(kMid2Block), 0, s, a, sl->al + shards, sl->asub, cnt + kCdlpSubs * kCntStride,
+                           o ? P.d_mv2.p : nullptr, (int64_t)P.n_mid2, nullptr, (int64_t)0, nullptr, nullptr, nullptr);
         GX_TRY(check_launch("k_cdlp_sparse_group2"));
-        hipLaunchKernelGGL((k_cdlp_sparse_group<kMidBlock, kMidSlots>), dim3(kCdlpSubs), dim3(kMidBlock), 0, s, a,
-                           sl->al + 2 * shards, sl->asub, cnt + 2 * kCdlpSubs * kCntStride, o ? P.d_mv4.p : nullptr,
-                           (int64_t)P.n_mid4, o ? P.d_mv.p : nullptr, (int64_t)P.n_mid);
+        hipLaunchKernelGGL((k_cdlp_sparse_group<kMid2Block, kMid2Slots, kMidMax>), dim3(8 * kCdlpSubs),
+                           dim3(kMid2Block), 0, s, a, sl->al + 2 * shards, sl->asub, cnt + 2 * kCdlpSubs * kCntStride,
+                           o ? P.d_mv4.p : nullptr, (int64_t)P.n_mid4, o ? P.d_mv.p : nullptr, (int64_t)P.n_mid,
+                           sl->redo, sl->rcount, nullptr);
         GX_TRY(check_launch("k_cdlp_sparse_group"));
+        hipLaunchKernelGGL((k_cdlp_sparse_group<kMidBlock, kMidSlots, kMidMax>), dim3(kCdlpSubs), dim3(kMidBlock), 0,
+                           s, a, nullptr, (int64_t)0, nullptr, nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr,
+                           sl->rcount, sl->redo);
+        GX_TRY(check_launch("k_cdlp_sparse_redo"));
         if (o && keep && P.v1 > P.v0) {   // the own-label check's tiny vertices (no tier kernels here)
             hipLaunchKernelGGL(k_cdlp_tiny, dim3(grid_for((uint64_t)(P.v1 - P.v0), kCdlpBlock, 8192)),
                                dim3(kCdlpBlock), 0, s, a);
@@ -1630,6 +1648,8 @@ struct CdlpCache {
     DBuf<uint32_t> kcnt;
     DBuf<int> kflags;
     bool keep_built = false;
+    DBuf<int32_t> redo;         // k_cdlp_sparse_group's vertices for the 16K-slot instance
+    DBuf<unsigned int> rcnt;    // one redo count per iteration
     ~CdlpCache() {
         if (hflag) (void)hipHostFree(hflag);
         for (hipEvent_t e : ev)
@@ -1761,6 +1781,7 @@ int cdlp_cache(gx_graph *g, int iters, bool relabel, CdlpCache **out, hipStream_
         if (const char *e = std::getenv("GX_CDLP_ASUB")) fresh->asub = std::max<int64_t>(1, std::atoll(e));
         GX_TRY(fresh->al.alloc((size_t)fresh->asub * kCdlpSubs * (kCdlpLists - 1)));
         GX_TRY(fresh->dense.alloc(1));
+        GX_TRY(fresh->redo.alloc(std::max<size_t>(1, fresh->P.n_mid4 + fresh->P.n_mid)));
         if (!g->directed && g->nnz > 0) {
             // the caller's rows sorted: the first iteration is each row's first column
             // (k_cdlp_first_sorted on the caller's graph, then moved to the relabelled order)
@@ -1791,6 +1812,7 @@ int cdlp_cache(gx_graph *g, int iters, bool relabel, CdlpCache **out, hipStream_
         const int cap = std::max(iters, 16);
         GX_TRY(C->changed.alloc((size_t)cap * kFlagShards * kFlagStride));
         GX_TRY(C->ccount.alloc((size_t)cap * kCdlpLists * kCdlpSubs * kCntStride));
+        GX_TRY(C->rcnt.alloc((size_t)cap));
         if (C->hflag) (void)hipHostFree(C->hflag);
         C->hflag = nullptr;
         GX_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&C->hflag), sizeof(int) * cap, hipHostMallocMapped));
@@ -1864,6 +1886,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                            reinterpret_cast<uint32_t *>(C->act.p), 0xffffffffu, n);   // stamp -1: never active
         GX_TRY(check_launch("k_cdlp_fill_u32"));
         GX_HIP_TRY(hipMemsetAsync(C->ccount.p, 0, sizeof(unsigned int) * kCdlpLists * kCdlpSubs * kCntStride * iters, s));
+        GX_HIP_TRY(hipMemsetAsync(C->rcnt.p, 0, sizeof(unsigned int) * iters, s));
     }
     int32_t *cur = C->la.p, *nxt = C->lb.p;
     for (int it = 0; it < iters; it++) {
@@ -1911,7 +1934,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                 hipLaunchKernelGGL(k_cdlp_keep_finish, dim3(1), dim3(1), 0, s, C->dense.p, kf, kf + 1);
                 GX_TRY(check_launch("k_cdlp_keep_finish"));
             }
-            const SparseLists sl{C->al.p, C->asub, cnt, only};
+            const SparseLists sl{C->al.p, C->asub, cnt, only, C->redo.p, C->rcnt.p + it};
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
                                   use_sparse ? &sl : nullptr, kFlagShards, kf));
         } else if (it == 0 && C->rows_sorted && first_sorted) {
