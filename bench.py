@@ -47,8 +47,8 @@ METRIC = "edges/sec (GTEPS) per algorithm at 1/2/4/8 GPUs; % HBM roofline"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=300)   # ~2.3 s of PageRank on SYN-8_5: the GPU is busy long enough to be seen
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--damping", type=float, default=0.85)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
