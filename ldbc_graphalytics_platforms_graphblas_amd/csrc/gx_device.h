@@ -241,7 +241,8 @@ int device_end(gx_ctx *ctx);
 // Radix sort of (u64 key, u32 value) pairs on bits [0, end_bit) of the key, into k_out / v_out.
 int sort_pairs_u64_u32(uint64_t *k_in, uint64_t *k_out, uint32_t *v_in, uint32_t *v_out, size_t m, int end_bit,
                        hipStream_t s);
-// Radix sorts / scan on the context's stream (rocPRIM), each synchronising before it returns.
+// Radix sorts / scan (rocPRIM) enqueued on stream s, not synchronised; their temporary storage
+// is one per device, ordered across streams by an event (gx_runtime.hip rocprim_tmp).
 int sort_keys_u64(uint64_t *k_in, uint64_t *k_out, size_t m, int end_bit, hipStream_t s);
 int sort_pairs_u32_u16(uint32_t *k_in, uint32_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
                        hipStream_t s);

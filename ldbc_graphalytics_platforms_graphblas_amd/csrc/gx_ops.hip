@@ -80,11 +80,19 @@ struct Monoid<kPlusPairI64> {
 
 // The multiplicative op on (matrix value a, vector value u(j)): mxv takes mult(a, u), vxm
 // mult(u, a) (the matrix operand second); SECOND picks the second operand, PAIR is 1.
+// fp64 -> uint64 the way GraphBLAS typecasts (GB_cast_to_uint64_t): NaN and values <= 0 give
+// 0, values >= 2^64 give UINT64_MAX, the rest truncate.
+__device__ __forceinline__ unsigned long long cast_u64(double x) {
+    if (!(x > 0.0)) return 0ull;   // NaN too
+    if (x >= 18446744073709551616.0) return ~0ull;
+    return (unsigned long long)x;
+}
+
 template <int SR, bool VXM>
 __device__ __forceinline__ typename Monoid<SR>::T term(double a, const void *u, int64_t j) {
     if constexpr (SR == kPlusSecondF64) return VXM ? a : static_cast<const double *>(u)[j];
     else if constexpr (SR == kMinSecondU64)
-        return VXM ? (unsigned long long)a : static_cast<const unsigned long long *>(u)[j];
+        return VXM ? cast_u64(a) : static_cast<const unsigned long long *>(u)[j];
     else if constexpr (SR == kMinPlusF64) {
         const double x = static_cast<const double *>(u)[j];
         return VXM ? x + a : a + x;

@@ -610,7 +610,33 @@ static int grow_slot(DBuf<char> *slots, size_t bytes, void **p) {
     return GX_SUCCESS;
 }
 
-static int rocprim_tmp(size_t bytes, void **p) { return grow_slot(g_tmp, bytes, p); }
+// The rocPRIM temporary storage is one grow-only buffer per device, shared by every stream
+// and context on it: a user on another stream than the last one first waits for the last
+// use (an event recorded after each sort / scan), so two queued users never overlap in it.
+struct TmpUse {
+    hipStream_t last = nullptr;
+    hipEvent_t done = nullptr;
+};
+static TmpUse *const g_tmp_use = new TmpUse[64];
+
+static int rocprim_tmp(size_t bytes, void **p, hipStream_t s) {
+    int dev = 0;
+    GX_HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(GX_NOT_IMPLEMENTED, "more than 64 devices");
+    TmpUse &u = g_tmp_use[dev];
+    if (!u.done) GX_HIP_TRY(hipEventCreateWithFlags(&u.done, hipEventDisableTiming));
+    if (u.last && u.last != s) GX_HIP_TRY(hipStreamWaitEvent(s, u.done, 0));
+    return grow_slot(g_tmp, bytes, p);
+}
+
+static int rocprim_tmp_release(hipStream_t s) {
+    int dev = 0;
+    GX_HIP_TRY(hipGetDevice(&dev));
+    TmpUse &u = g_tmp_use[dev];
+    GX_HIP_TRY(hipEventRecord(u.done, s));
+    u.last = s;
+    return GX_SUCCESS;
+}
 
 // Plan-time scratch of the current device (the PageRank plan's sort keys and values): grow-only
 // and kept, so a plan neither frees gigabytes (hipFree waits for the device) nor allocates
@@ -622,9 +648,9 @@ int sort_keys_u64(uint64_t *k_in, uint64_t *k_out, size_t m, int end_bit, hipStr
     size_t tmp_bytes = 0;
     GX_HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, k_in, k_out, m, 0, end_bit, s));
     void *tmp = nullptr;
-    GX_TRY(rocprim_tmp(tmp_bytes, &tmp));
+    GX_TRY(rocprim_tmp(tmp_bytes, &tmp, s));
     GX_HIP_TRY(rocprim::radix_sort_keys(tmp, tmp_bytes, k_in, k_out, m, 0, end_bit, s));
-    return GX_SUCCESS;
+    return rocprim_tmp_release(s);
 }
 
 template <typename K, typename V>
@@ -636,12 +662,12 @@ static int sort_pairs_kv(K *k_in, K *k_out, V *v_in, V *v_out, size_t m, int end
     else
         GX_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
     void *tmp = nullptr;
-    GX_TRY(rocprim_tmp(tmp_bytes, &tmp));
+    GX_TRY(rocprim_tmp(tmp_bytes, &tmp, s));
     if (desc)
         GX_HIP_TRY(rocprim::radix_sort_pairs_desc(tmp, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
     else
         GX_HIP_TRY(rocprim::radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, m, 0, end_bit, s));
-    return GX_SUCCESS;
+    return rocprim_tmp_release(s);
 }
 
 int sort_pairs_u32_u16(uint32_t *k_in, uint32_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m, int end_bit,
@@ -668,9 +694,9 @@ int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s)
     size_t tmp_bytes = 0;
     GX_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp_bytes, in, out, (int64_t)0, m, rocprim::plus<int64_t>(), s));
     void *tmp = nullptr;
-    GX_TRY(rocprim_tmp(tmp_bytes, &tmp));
+    GX_TRY(rocprim_tmp(tmp_bytes, &tmp, s));
     GX_HIP_TRY(rocprim::exclusive_scan(tmp, tmp_bytes, in, out, (int64_t)0, m, rocprim::plus<int64_t>(), s));
-    return GX_SUCCESS;
+    return rocprim_tmp_release(s);
 }
 
 int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,

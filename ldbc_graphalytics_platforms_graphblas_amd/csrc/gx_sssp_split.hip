@@ -76,6 +76,13 @@ struct SplitState {
     uint32_t nmode[6];            // rounds per mode (GX_SPLIT_VERBOSE)
     unsigned long long nitems[6]; // items / candidates per mode (rank-local)
     int8_t modelog[256];          // mode of rounds 1..256 (GX_SPLIT_VERBOSE)
+    // the settled list's capacity (sverts: vertices, sitems: items).  A vertex re-settled in
+    // its epoch is listed again, so an epoch could in principle list more than fit: the
+    // writes past them are dropped, the run stops (done) and err is set, which the host turns
+    // into an error instead of returning distances.
+    uint32_t sv_cap;
+    uint64_t si_cap;
+    int32_t err;
 };
 
 // Per-vertex records, one 16-B line each: the slice row (light entries [start, start + nl),
@@ -228,8 +235,13 @@ __device__ __forceinline__ void tile_write(const SplitBufs &B, const Tile &T, co
     if (P.take)
         for (uint32_t j = 0; j < P.nl; j++) B.fitems[list][T.base[kQFi] + P.offi + j] = ((uint64_t)(uint32_t)v << 32) | j;
     if (P.isv) {
-        B.sverts[T.base[kQSv] + P.offsv] = (int32_t)v;
-        for (uint32_t j = 0; j < P.nh; j++) B.sitems[T.base[kQSi] + P.offs + j] = ((uint64_t)(uint32_t)v << 32) | j;
+        const uint64_t iv = (uint64_t)T.base[kQSv] + P.offsv, is = (uint64_t)T.base[kQSi] + P.offs;
+        if (iv < B.st->sv_cap && is + P.nh <= B.st->si_cap) {
+            B.sverts[iv] = (int32_t)v;
+            for (uint32_t j = 0; j < P.nh; j++) B.sitems[is + j] = ((uint64_t)(uint32_t)v << 32) | j;
+        } else {
+            atomicOr(&B.st->err, 1);
+        }
     }
     if (P.q == kQOvf) B.ovf[B.st->oe][T.base[kQOvf] + P.offr] = (int32_t)v;
     else if (P.q >= kQRing) B.ring[(uint64_t)(P.q - kQRing) * (uint64_t)B.n + T.base[P.q] + P.offr] = (int32_t)v;
@@ -246,10 +258,13 @@ __global__ void k_split_start(SplitBufs B, int64_t src) {
     for (int64_t v = i; v < B.v1 - B.v0; v += (int64_t)gridDim.x * kSB) B.istamp[v] = 0;
 }
 
-__global__ void k_split_seed(SplitBufs B, int64_t src, uint32_t pull_min, uint32_t fuse) {
+__global__ void k_split_seed(SplitBufs B, int64_t src, uint32_t pull_min, uint32_t fuse, uint32_t sv_cap,
+                             uint64_t si_cap) {
     SplitState *st = B.st;
     if (threadIdx.x == 0) {
         memset(st, 0, sizeof(SplitState));
+        st->sv_cap = sv_cap;
+        st->si_cap = si_cap;
         st->epoch = 1;
         st->epoch_round = 1;
         st->ostamp_tag = 1;
@@ -282,6 +297,12 @@ __global__ void k_split_plan(SplitState *st) {
 }
 
 __device__ void k_split_plan_body(SplitState *st) {
+    if (st->err || st->sv > st->sv_cap || st->si > st->si_cap) {   // the settled list overflowed
+        st->err = 1;
+        st->done = 1;
+        st->mode = kNone;
+        return;
+    }
     if (st->consume >= 0) {
         for (int j = 0; j < st->consume_n; j++) st->ring_cnt[(st->consume + j) % kW] = 0;
         st->consume = -1;
@@ -817,6 +838,8 @@ struct gx_sssp_split {
     bool hub_checked = false;     // gx_sssp_split_run looked for the hub-first copy
     int rounds_hint = 0;          // rounds the last gx_sssp_split_run took
     int64_t n = 0, v0 = 0, v1 = 0, snnz = 0, onnz = 0;
+    uint32_t sv_cap = 0;          // settled-list capacities (SplitState::sv_cap / si_cap)
+    uint64_t si_cap = 0;
     double delta = 1.0;
     uint32_t pull_min = 0, fuse = 0;
     DBuf<VRec> vrec;
@@ -1000,6 +1023,8 @@ static int split_build(gx_sssp_split *p, gx_graph *g) {
     // state: item lists hold at most one item per vertex plus one per 256 slice entries
     const uint64_t icap = (uint64_t)n + (uint64_t)p->snnz / kSChunk + 64;
     const int64_t n1 = std::max<int64_t>(n, 1), own1 = std::max<int64_t>(own, 1);
+    p->sv_cap = (uint32_t)n1;
+    p->si_cap = icap;
     GX_TRY(p->dist.alloc(n1));
     GX_TRY(p->lrel.alloc(n1));
     for (DBuf<int32_t> *b : {&p->qstamp, &p->sverts, &p->ovf0, &p->ovf1}) GX_TRY(b->alloc(n1));
@@ -1042,7 +1067,8 @@ extern "C" int gx_sssp_split_start(gx_sssp_split *p, uint64_t src, void *stream)
     const SplitBufs B = p->bufs();
     hipLaunchKernelGGL(k_split_start, dim3(grid_for(std::max<int64_t>(p->n, 1), kSB, 8192)), dim3(kSB), 0, s, B,
                        (int64_t)src);
-    hipLaunchKernelGGL(k_split_seed, dim3(1), dim3(kSB), 0, s, B, (int64_t)src, p->pull_min, p->fuse);
+    hipLaunchKernelGGL(k_split_seed, dim3(1), dim3(kSB), 0, s, B, (int64_t)src, p->pull_min, p->fuse, p->sv_cap,
+                       p->si_cap);
     return check_launch("k_split_seed");
 }
 
@@ -1060,10 +1086,20 @@ extern "C" int gx_sssp_split_apply(gx_sssp_split *p, const uint64_t *pairs, cons
     return split_apply(p, pairs, counts, nranks, stride, split_stream(p, stream));
 }
 
+// Fails when the run stopped on a full settled list (SplitState::err) instead of finishing.
+static int split_check(gx_sssp_split *p, hipStream_t s) {
+    int32_t err = 0;
+    GX_HIP_TRY(hipMemcpyAsync(&err, &p->st.p->err, sizeof(err), hipMemcpyDeviceToHost, s));
+    GX_HIP_TRY(hipStreamSynchronize(s));
+    if (err) return fail(GX_OUT_OF_MEMORY, "gx_sssp_split: an epoch settled more vertices than the settled list holds");
+    return GX_SUCCESS;
+}
+
 extern "C" int gx_sssp_split_distances(gx_sssp_split *p, double *dist, void *stream) {
     if (!p || !dist) return fail(GX_NULL_POINTER, "gx_sssp_split_distances: null argument");
     GX_HIP_TRY(hipSetDevice(p->g->ctx->device));
     hipStream_t s = split_stream(p, stream);
+    GX_TRY(split_check(p, s));
     const void *res = nullptr;
     GX_TRY(remap_out(p->g, p->dist.p, 8, s, &res));   // hub-first copy -> the caller's order
     GX_HIP_TRY(hipMemcpyAsync(dist, res, (size_t)p->n * 8, hipMemcpyDeviceToDevice, s));
@@ -1120,6 +1156,7 @@ extern "C" int gx_sssp_split_run(gx_sssp_split *p, uint64_t src, double *dist_ho
         for (int i = 0; i < std::min(h.round, 256); i++) std::fprintf(stderr, " %d", (int)h.modelog[i]);
         std::fprintf(stderr, "\n");
     }
+    GX_TRY(split_check(p, s));
     const void *res = nullptr;
     GX_TRY(remap_out(p->g, p->dist.p, 8, s, &res));   // hub-first copy -> the caller's order
     GX_HIP_TRY(hipStreamSynchronize(s));

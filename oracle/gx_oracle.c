@@ -715,7 +715,8 @@ int orc_mxv(int64_t n, const int64_t *rp, const int64_t *ci, const double *wt, i
             switch (sr) {
                 case ORC_PLUS_SECOND_FP64: accd += vxm ? a : ud[j]; break;
                 case ORC_MIN_SECOND_UINT64: {
-                    const uint64_t v = vxm ? (uint64_t)a : uu[j];
+                    /* GraphBLAS's fp64 -> uint64 typecast (GB_cast_to_uint64_t): saturating */
+                    const uint64_t v = vxm ? (!(a > 0.0) ? 0 : a >= 18446744073709551616.0 ? UINT64_MAX : (uint64_t)a) : uu[j];
                     if (v < accu) accu = v;
                     break;
                 }

@@ -46,7 +46,7 @@ def numpy_mxv(csr, sr, u, up, vxm, t0):
         if sr == O.PLUS_SECOND_FP64:
             t[i] = sum((M[i, j] if vxm else u[j]) for j in js) if len(js) else 0.0
         elif sr == O.MIN_SECOND_UINT64:
-            t[i] = min((np.uint64(M[i, j]) if vxm else u[j]) for j in js) if len(js) else np.iinfo(np.uint64).max
+            t[i] = min((sat_u64(M[i, j]) if vxm else u[j]) for j in js) if len(js) else np.iinfo(np.uint64).max
         elif sr == O.ANY_PAIR_BOOL:
             t[i] = 1 if len(js) else 0
         elif sr == O.MIN_PLUS_FP64:
@@ -54,6 +54,26 @@ def numpy_mxv(csr, sr, u, up, vxm, t0):
         else:
             t[i] = len(js)
     return t, hit
+
+
+def sat_u64(x):
+    """GraphBLAS's fp64 -> uint64 typecast (GB_cast_to_uint64_t): NaN and x <= 0 -> 0, x >= 2^64 ->
+    UINT64_MAX, else truncation."""
+    if not x > 0.0:
+        return np.uint64(0)
+    if x >= 18446744073709551616.0:
+        return np.uint64(np.iinfo(np.uint64).max)
+    return np.uint64(int(x))
+
+
+def odd_weights(csr, seed=5):
+    """The same graph with weights GraphBLAS must saturate: negative, NaN, above 2^64, fractional."""
+    import copy
+    rng = np.random.default_rng(seed)
+    out = copy.copy(csr)
+    pool = np.array([-3.5, np.nan, 2.0 ** 70, 0.75, 7.9, 1e19, 0.0, 42.0])
+    out.vals = pool[rng.integers(0, len(pool), csr.nnz)]
+    return out
 
 
 def rand_u(sr, n, rng):
@@ -214,6 +234,37 @@ def gpu_ops(G):
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
     return (lambda sr, u, desc, w=None: A.mxv(G, sr, u, None, None, desc | (A.DESC_ACCUM if w is not None else 0), w),
             lambda sr, u, up, mask, desc, w=None, wp=None: A.vxm(G, sr, u, up, mask, desc, w, wp))
+
+
+def test_oracle_min_second_saturates():
+    """MIN_SECOND_UINT64 vxm takes the matrix value as uint64 the way GraphBLAS typecasts it
+    (a plain cast is undefined for negative, NaN and huge weights)."""
+    csr = odd_weights(rmat(6, 4, 11, undirected=False, weighted=True))
+    u = np.arange(csr.n, dtype=np.uint64)
+    for t0 in (False, True):
+        want, hit = numpy_mxv(csr, O.MIN_SECOND_UINT64, u, None, True, t0)
+        got, gp = O.mxv(csr, O.MIN_SECOND_UINT64, u, None, None, O.DESC_T0 if t0 else 0, None,
+                        np.zeros(csr.n, np.uint8), vxm=True)
+        np.testing.assert_array_equal(gp.astype(bool), hit)
+        np.testing.assert_array_equal(got[hit], want[hit])
+
+
+@pytest.mark.gpu
+def test_gpu_min_second_saturates(gpu_ctx):
+    """The device's MIN_SECOND_UINT64 vxm saturates fp64 -> uint64 like the oracle."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    csr = odd_weights(rmat(9, 8, 7, undirected=False, weighted=True))
+    G = A.Graph(gpu_ctx, csr, directed=True)
+    try:
+        u = np.arange(csr.n, dtype=np.uint64)
+        for desc in (0, A.DESC_T0):
+            p0 = np.zeros(csr.n, np.uint8)
+            got, gp = A.vxm(G, O.MIN_SECOND_UINT64, u, None, None, desc, None, p0)
+            want, wp = O.mxv(csr, O.MIN_SECOND_UINT64, u, None, None, desc, None, p0, vxm=True)
+            np.testing.assert_array_equal(gp, wp)
+            np.testing.assert_array_equal(got, want)
+    finally:
+        G.close()
 
 
 @pytest.mark.gpu
