@@ -691,32 +691,52 @@ struct KeySrc {
     int32_t segmask;            // segment bits kept in the key (its sort group's share)
 };
 
-// One wave per 64-entry slab of the plan's rows, lane = entry (coalesced key / row writes and
-// row-contiguous column reads; the row by the slab shuffle search, gx_device.h slab_row_of).
+// The segment of every local row (one workgroup per segment; rows of skipped empty blocks fall
+// in the segment before them and are never looked up: they hold no entry).
+__global__ __launch_bounds__(256) void k_row_seg(const int32_t *__restrict__ seg_row, int32_t nseg, int32_t *rowseg) {
+    for (int32_t sg = blockIdx.x; sg < nseg; sg += gridDim.x)
+        for (int32_t r = seg_row[sg] + threadIdx.x; r < seg_row[sg + 1]; r += 256) rowseg[r] = sg;
+}
+
+// One wave per kKeyU 64-entry slabs of the plan's rows, lane = entry (coalesced key / row writes
+// and row-contiguous column reads; the row by the slab shuffle search, gx_device.h
+// slab_row_of, the segment from rowseg).  The slabs' chains (row -> source row -> column ->
+// renamed column) are issued side by side: one slab at a time this kernel was a chain of
+// ~15 dependent loads per slab (a binary search of the segments among them), ~10 ms on SYN-8_5.
+constexpr int kKeyU = 4;
+
 template <typename K>
 __global__ __launch_bounds__(256) void k_sorted_keys(KeySrc k, int64_t nnz, const int64_t *__restrict__ srow,
-                                                     int64_t nslabs, K *__restrict__ keys, uint16_t *__restrict__ vals) {
+                                                     int64_t nslabs, const int32_t *__restrict__ rowseg,
+                                                     K *__restrict__ keys, uint16_t *__restrict__ vals) {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
-    for (int64_t sl = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; sl < nslabs; sl += nw) {
-        const int64_t e = sl * kWave + lane;
-        const bool valid = e < nnz;
-        const int64_t i = slab_row_of(k.rp, srow, k.rows, sl, valid ? e : nnz - 1, lane);
-        // the segment of the slab's first row (uniform search), then forward per lane
-        const int64_t r0 = srow[sl];
-        int lo = 0, hi = k.nseg;   // seg_row[lo] <= r0 < seg_row[lo + 1]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (k.seg_row[mid] <= r0) lo = mid;
-            else hi = mid;
+    const int64_t nch = (nslabs + kKeyU - 1) / kKeyU;
+    for (int64_t ch = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; ch < nch; ch += nw) {
+        int64_t e[kKeyU], i[kKeyU], rpi[kKeyU], sp[kKeyU];
+        int32_t sg[kKeyU], c0[kKeyU];
+#pragma unroll
+        for (int u = 0; u < kKeyU; u++) {
+            const int64_t sl = min(ch * kKeyU + u, nslabs - 1);
+            e[u] = (ch * kKeyU + u) * kWave + lane;
+            i[u] = slab_row_of(k.rp, srow, k.rows, sl, min(e[u], nnz - 1), lane);
         }
-        while (lo + 1 < k.nseg && k.seg_row[lo + 1] <= i) lo++;
-        if (valid) {
-            const int64_t v = k.order ? k.order[i] : i;
-            const int32_t c0 = k.sci[k.srp[v] + (e - k.rp[i])];
-            const uint32_t c = (uint32_t)(k.perm ? k.perm[c0] : c0);
-            keys[e] = ((K)(lo & k.segmask) << k.colbits) | (K)c;
-            vals[e] = (uint16_t)(i - k.seg_row[lo]);
+#pragma unroll
+        for (int u = 0; u < kKeyU; u++) {
+            sg[u] = rowseg[i[u]];
+            rpi[u] = k.rp[i[u]];
+            const int64_t v = k.order ? k.order[i[u]] : i[u];
+            sp[u] = k.srp[v];
+        }
+#pragma unroll
+        for (int u = 0; u < kKeyU; u++) c0[u] = k.sci[sp[u] + (min(e[u], nnz - 1) - rpi[u])];
+#pragma unroll
+        for (int u = 0; u < kKeyU; u++) {
+            const uint32_t c = (uint32_t)(k.perm ? k.perm[c0[u]] : c0[u]);
+            if (e[u] < nnz) {
+                keys[e[u]] = ((K)(sg[u] & k.segmask) << k.colbits) | (K)c;
+                vals[e[u]] = (uint16_t)(i[u] - k.seg_row[sg[u]]);
+            }
         }
     }
 }
@@ -731,29 +751,41 @@ struct SegDesc {
     int32_t pad;
 };
 
+// A workgroup per kPackChunk entries of one segment (host-built list: no search per entry); the
+// chunks start on the segment's 256-entry supergroups, so each of a thread's 16 entries lies in
+// one supergroup whose base / last keys every thread of the workgroup reads alike.
+constexpr int64_t kPackChunk = 4096;
+struct PackChunk {
+    int64_t z0;
+    int32_t seg;
+    int32_t pad;
+};
+
 template <typename K>
-__global__ __launch_bounds__(256) void k_sorted_pack(const SegDesc *__restrict__ segs, int32_t nseg, int64_t nnz,
-                                                     const K *__restrict__ keys, const uint16_t *__restrict__ vals,
-                                                     uint32_t colmask, int32_t *__restrict__ sci,
-                                                     uint32_t *__restrict__ spk, uint32_t *__restrict__ gbase) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x) {
-        int lo = 0, hi = nseg;   // the segment holding e: segs[lo].z0 <= e < segs[lo].z1
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (segs[mid].z0 <= e) lo = mid;
-            else hi = mid;
+__global__ __launch_bounds__(256) void k_sorted_pack(const SegDesc *__restrict__ segs, const PackChunk *__restrict__ chunks,
+                                                     int64_t nchunks, const K *__restrict__ keys,
+                                                     const uint16_t *__restrict__ vals, uint32_t colmask,
+                                                     int32_t *__restrict__ sci, uint32_t *__restrict__ spk,
+                                                     uint32_t *__restrict__ gbase) {
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const PackChunk pc = chunks[c];
+        const SegDesc sg = segs[pc.seg];
+        const int64_t z1 = min(pc.z0 + kPackChunk, sg.z1);
+#pragma unroll 4
+        for (int64_t g0 = pc.z0; g0 < z1; g0 += 256) {
+            const int64_t e = g0 + threadIdx.x;
+            const bool in = e < z1;
+            const uint32_t col = in ? (uint32_t)keys[e] & colmask : 0u;
+            if (in) sci[e] = (int32_t)col;
+            if (sg.gseg < 0 || !in) continue;
+            const int64_t q = (g0 - sg.z0) >> 8;
+            const uint32_t base = (uint32_t)keys[g0] & colmask;
+            const uint32_t lastc = (uint32_t)keys[min(g0 + 255, sg.z1 - 1)] & colmask;
+            const bool esc = lastc - base >= (1u << (32 - kRowBits));
+            const uint32_t row = vals[e];
+            spk[e] = esc ? row : ((col - base) << kRowBits) | row;
+            if (threadIdx.x == 0) gbase[sg.gseg + q] = esc ? (base | 0x80000000u) : base;
         }
-        const SegDesc sg = segs[lo];
-        const uint32_t col = (uint32_t)keys[e] & colmask;
-        sci[e] = (int32_t)col;
-        if (sg.gseg < 0) continue;
-        const int64_t t = e - sg.z0, q = t >> 8;
-        const uint32_t base = (uint32_t)keys[sg.z0 + (q << 8)] & colmask;
-        const uint32_t lastc = (uint32_t)keys[min(sg.z0 + (q << 8) + 255, sg.z1 - 1)] & colmask;
-        const bool esc = lastc - base >= (1u << (32 - kRowBits));
-        const uint32_t row = vals[e];
-        spk[e] = esc ? row : ((col - base) << kRowBits) | row;
-        if ((t & 255) == 0) gbase[sg.gseg + q] = esc ? (base | 0x80000000u) : base;
     }
 }
 
@@ -1177,6 +1209,8 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     DBuf<int32_t> d_seg_row;
     DBuf<SegDesc> d_segd;
     DBuf<int64_t> srow;
+    DBuf<int32_t> d_rowseg;
+    DBuf<PackChunk> d_pch;
     DBuf<uint32_t> d_fill, d_noff, d_nsplit, d_ncode;
     DBuf<int64_t> d_nbeg;
     if (nnz > 0) {
@@ -1218,9 +1252,20 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         const int64_t nslabs = (int64_t)((nnz + kWave - 1) / kWave);
         GX_TRY(srow.alloc(nslabs + 1));
         GX_TRY(slab_rows(p->rp, rows, nslabs, srow.p, s));
+        GX_TRY(d_rowseg.alloc(std::max<int64_t>(rows, 1)));
+        hipLaunchKernelGGL(k_row_seg, dim3((unsigned)std::min<size_t>(segd.size(), 65535)), dim3(256), 0, s, d_seg_row.p,
+                           (int32_t)segd.size(), d_rowseg.p);
+        GX_TRY(check_launch("k_row_seg"));
+        // the pack's chunks: kPackChunk entries of one segment each, from the segment's start
+        std::vector<PackChunk> pch;
+        for (size_t g = 0; g < segd.size(); g++)
+            for (int64_t z = segd[g].z0; z < segd[g].z1; z += kPackChunk) pch.push_back({z, (int32_t)g, 0});
+        GX_TRY(d_pch.alloc(std::max<size_t>(pch.size(), 1)));
+        if (!pch.empty())
+            GX_HIP_TRY(hipMemcpyAsync(d_pch.p, pch.data(), pch.size() * sizeof(PackChunk), hipMemcpyHostToDevice, s));
         clk.mark("segments + slab rows");
-        const unsigned kgrid = grid_for((uint64_t)nslabs * kWave, 256, 16384);
-        const unsigned pgrid = grid_for(nnz, 256, 1u << 20);
+        const unsigned kgrid = grid_for((uint64_t)((nslabs + kKeyU - 1) / kKeyU) * kWave, 256, 16384);
+        const unsigned pgrid = (unsigned)std::min<size_t>(std::max<size_t>(pch.size(), 1), 1u << 20);
         const uint32_t colmask = (uint32_t)((1ull << colbits) - 1);
         // keys and values in the kept plan scratch: [k0 | k1 | v0 | v1]
         const size_t kb = narrow ? 4 : 8, align = 256;
@@ -1232,8 +1277,8 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         clk.mark("key buffers");
         if (narrow) {
             uint32_t *k0 = reinterpret_cast<uint32_t *>(scr), *k1 = reinterpret_cast<uint32_t *>(scr + kbytes);
-            hipLaunchKernelGGL(k_sorted_keys<uint32_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs, k0,
-                               v0);
+            hipLaunchKernelGGL(k_sorted_keys<uint32_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs,
+                               d_rowseg.p, k0, v0);
             GX_TRY(check_launch("k_sorted_keys"));
             clk.mark("keys");
             const size_t G = (size_t)1 << gbits;
@@ -1243,16 +1288,16 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                 GX_TRY(sort_pairs_u32_u16(k0 + z0, k1 + z0, v0 + z0, v1 + z0, (size_t)(z1 - z0), gbits + colbits, s));
             }
             clk.mark("sort");
-            hipLaunchKernelGGL(k_sorted_pack<uint32_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
-                               (int64_t)nnz, k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
+            hipLaunchKernelGGL(k_sorted_pack<uint32_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, d_pch.p,
+                               (int64_t)pch.size(), k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
         } else {
             uint64_t *k0 = reinterpret_cast<uint64_t *>(scr), *k1 = reinterpret_cast<uint64_t *>(scr + kbytes);
-            hipLaunchKernelGGL(k_sorted_keys<uint64_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs, k0,
-                               v0);
+            hipLaunchKernelGGL(k_sorted_keys<uint64_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs,
+                               d_rowseg.p, k0, v0);
             GX_TRY(check_launch("k_sorted_keys"));
             GX_TRY(sort_pairs_u64_u16(k0, k1, v0, v1, (size_t)nnz, segbits + colbits, s));
-            hipLaunchKernelGGL(k_sorted_pack<uint64_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, (int32_t)segd.size(),
-                               (int64_t)nnz, k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
+            hipLaunchKernelGGL(k_sorted_pack<uint64_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, d_pch.p,
+                               (int64_t)pch.size(), k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
         }
         GX_TRY(check_launch("k_sorted_pack"));
         clk.mark("keys + sort + pack");
