@@ -713,29 +713,29 @@ __global__ __launch_bounds__(256) void k_sorted_keys(KeySrc k, int64_t nnz, cons
     const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
     const int64_t nch = (nslabs + kKeyU - 1) / kKeyU;
     for (int64_t ch = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; ch < nch; ch += nw) {
-        int64_t e[kKeyU], i[kKeyU], rpi[kKeyU], sp[kKeyU];
-        int32_t sg[kKeyU], c0[kKeyU];
+        int32_t i[kKeyU], sg[kKeyU], c0[kKeyU];
+        int64_t rpi[kKeyU], sp[kKeyU];
+        const int64_t e0 = ch * kKeyU * kWave + lane;   // lane's entry of slab u: e0 + u * kWave
 #pragma unroll
         for (int u = 0; u < kKeyU; u++) {
             const int64_t sl = min(ch * kKeyU + u, nslabs - 1);
-            e[u] = (ch * kKeyU + u) * kWave + lane;
-            i[u] = slab_row_of(k.rp, srow, k.rows, sl, min(e[u], nnz - 1), lane);
+            i[u] = (int32_t)slab_row_of(k.rp, srow, k.rows, sl, min(e0 + u * kWave, nnz - 1), lane);
         }
 #pragma unroll
         for (int u = 0; u < kKeyU; u++) {
             sg[u] = rowseg[i[u]];
             rpi[u] = k.rp[i[u]];
-            const int64_t v = k.order ? k.order[i[u]] : i[u];
-            sp[u] = k.srp[v];
+            sp[u] = k.srp[k.order ? k.order[i[u]] : i[u]];
         }
 #pragma unroll
-        for (int u = 0; u < kKeyU; u++) c0[u] = k.sci[sp[u] + (min(e[u], nnz - 1) - rpi[u])];
+        for (int u = 0; u < kKeyU; u++) c0[u] = k.sci[sp[u] + (min(e0 + u * kWave, nnz - 1) - rpi[u])];
 #pragma unroll
         for (int u = 0; u < kKeyU; u++) {
             const uint32_t c = (uint32_t)(k.perm ? k.perm[c0[u]] : c0[u]);
-            if (e[u] < nnz) {
-                keys[e[u]] = ((K)(sg[u] & k.segmask) << k.colbits) | (K)c;
-                vals[e[u]] = (uint16_t)(i[u] - k.seg_row[sg[u]]);
+            const int64_t e = e0 + u * kWave;
+            if (e < nnz) {
+                keys[e] = ((K)(sg[u] & k.segmask) << k.colbits) | (K)c;
+                vals[e] = (uint16_t)(i[u] - k.seg_row[sg[u]]);
             }
         }
     }
