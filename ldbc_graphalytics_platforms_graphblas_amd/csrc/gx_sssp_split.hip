@@ -76,10 +76,13 @@ struct SplitState {
     uint32_t nmode[6];            // rounds per mode (GX_SPLIT_VERBOSE)
     unsigned long long nitems[6]; // items / candidates per mode (rank-local)
     int8_t modelog[256];          // mode of rounds 1..256 (GX_SPLIT_VERBOSE)
-    // the settled list's capacity (sverts: vertices, sitems: items).  A vertex re-settled in
-    // its epoch is listed again, so an epoch could in principle list more than fit: the
-    // writes past them are dropped, the run stops (done) and err is set, which the host turns
-    // into an error instead of returning distances.
+    // The settled list is a ring (sverts: vertices, sitems: items; positions taken modulo the
+    // capacity): a vertex re-settled in its epoch is listed again, so an epoch may list more
+    // than n.  Only [sv_done, sv) is live when a round writes (a heavy round reads its batch
+    // in prep / relax, before its apply lists anything), and a vertex is listed at most once
+    // between two heavy phases, so n vertices and their items always fit.  Should
+    // a write ever land on live entries, it is dropped, the run stops and err is set, which
+    // the host turns into an error instead of returning distances.
     uint32_t sv_cap;
     uint64_t si_cap;
     int32_t err;
@@ -235,10 +238,11 @@ __device__ __forceinline__ void tile_write(const SplitBufs &B, const Tile &T, co
     if (P.take)
         for (uint32_t j = 0; j < P.nl; j++) B.fitems[list][T.base[kQFi] + P.offi + j] = ((uint64_t)(uint32_t)v << 32) | j;
     if (P.isv) {
+        const SplitState *st = B.st;
         const uint64_t iv = (uint64_t)T.base[kQSv] + P.offsv, is = (uint64_t)T.base[kQSi] + P.offs;
-        if (iv < B.st->sv_cap && is + P.nh <= B.st->si_cap) {
-            B.sverts[iv] = (int32_t)v;
-            for (uint32_t j = 0; j < P.nh; j++) B.sitems[is + j] = ((uint64_t)(uint32_t)v << 32) | j;
+        if (iv - st->sv_done < st->sv_cap && is + P.nh - st->si_done <= st->si_cap) {
+            B.sverts[iv % st->sv_cap] = (int32_t)v;
+            for (uint32_t j = 0; j < P.nh; j++) B.sitems[(is + j) % st->si_cap] = ((uint64_t)(uint32_t)v << 32) | j;
         } else {
             atomicOr(&B.st->err, 1);
         }
@@ -297,7 +301,7 @@ __global__ void k_split_plan(SplitState *st) {
 }
 
 __device__ void k_split_plan_body(SplitState *st) {
-    if (st->err || st->sv > st->sv_cap || st->si > st->si_cap) {   // the settled list overflowed
+    if (st->err || st->sv - st->sv_done > st->sv_cap || st->si - st->si_done > st->si_cap) {   // ring overrun
         st->err = 1;
         st->done = 1;
         st->mode = kNone;
@@ -444,7 +448,7 @@ __global__ __launch_bounds__(kSB) void k_split_prep(SplitBufs B) {
         const int32_t round = st->round;
         unsigned long long m = ~0ull;
         for (uint32_t i = st->sb0 + blockIdx.x * kSB + threadIdx.x; i < st->sb1; i += gridDim.x * kSB) {
-            const int32_t u = B.sverts[i];
+            const int32_t u = B.sverts[i % st->sv_cap];
             B.srec[u].hmark = round;
             if (mode == kPull) m = min(m, B.dist[u]);
         }
@@ -565,7 +569,7 @@ __global__ __launch_bounds__(kSB) void k_split_relax(SplitBufs B) {
             int64_t e0 = 0, len = 0;
             unsigned long long du = 0;
             if (lane < (int)G && gi < i1) {
-                const uint64_t x = items[gi];
+                const uint64_t x = items[heavy ? gi % st->si_cap : gi];
                 const int64_t u = (int64_t)(x >> 32), j = (int64_t)(x & 0xffffffffu);
                 const VRec vr = B.vrec[u];
                 const int64_t a = heavy ? vr.start + vr.nl : vr.start, b = a + (heavy ? vr.nh : vr.nl);
