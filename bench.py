@@ -499,17 +499,30 @@ def measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True):
     # torch.distributed all-gather per piece and iteration (pr_partition.PartitionedPageRank)
     driver = os.environ.get("GX_PR_DRIVER", "device")
     use_graph = os.environ.get("GX_PR_GRAPH", "1") != "0"
+    # GX_PR_EXCHANGE=p2p: the one-shot peer-to-peer exchange (IPC-mapped peer vectors, one
+    # write per peer) instead of RCCL's all-gather; off by default (not yet measured on a node
+    # with more than one GPU)
+    exchange = os.environ.get("GX_PR_EXCHANGE", "rccl")
     comm = dpr = None
     if driver == "device":
         ok = 1
         try:
-            if dist:
-                def share_id(uid: bytes) -> bytes:
-                    box = [uid]
-                    dist.broadcast_object_list(box, src=0)
-                    return box[0]
-                comm = Comm(ctx, world, rank, share_id)
-            dpr = DevicePageRank(steppers, comm, use_graph=use_graph)
+            if exchange == "p2p":
+                def share_all(h: bytes):
+                    if not dist:
+                        return [h]
+                    box = [None] * world
+                    dist.all_gather_object(box, h)
+                    return box
+                dpr = DevicePageRank(steppers, None, use_graph=use_graph, p2p=(world, rank, share_all))
+            else:
+                if dist:
+                    def share_id(uid: bytes) -> bytes:
+                        box = [uid]
+                        dist.broadcast_object_list(box, src=0)
+                        return box[0]
+                    comm = Comm(ctx, world, rank, share_id)
+                dpr = DevicePageRank(steppers, comm, use_graph=use_graph)
             dpr.run(args.iters, stream.cuda_stream)
             torch.cuda.synchronize(device)
         except Exception as e:   # noqa: BLE001 -- reported, then every rank takes the host driver
@@ -590,6 +603,8 @@ def measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True):
     out = dict(elapsed=elapsed, t_setup=t_setup, t_first=t_first, launches=launches, mean_launch_s=mean_launch_s,
                bytes_per_launch=bytes_per_launch, achieved=bytes_per_launch / mean_launch_s / 1e9,
                driver=driver, use_graph=use_graph, pieces=pieces, vranks=vranks, partition=partition,
+               exchange=("p2p" if exchange == "p2p" else "rccl" if comm is not None else "device copies")
+               if driver == "device" else "torch.distributed",
                events_in_timed=events_in_timed, exchanged=steppers[0].chunk * vranks / n, result=result)
     if dpr is not None:
         dpr.close()
@@ -745,6 +760,7 @@ def main():
                 else "one rank",
                 "exchanged_doubles_per_n": m["exchanged"],
                 "driver": m["driver"] + (", hipGraph" if m["driver"] == "device" and m["use_graph"] else ""),
+                "exchange": m["exchange"],
                 "roofline_events": "timed steps" if m["events_in_timed"] else "instrumented pass after the timed steps",
                 "device": dev_name,
                 "cus": cus,

@@ -264,6 +264,24 @@ int gx_pr_dist_run(gx_pr_dist *dist, int iters, int use_graph, void *stream);
 int gx_pr_dist_scores(gx_pr_dist *dist, int piece, double *scores);
 int gx_pr_dist_free(gx_pr_dist *dist);
 
+/* ---- one-shot peer-to-peer exchange (no RCCL) -----
+ * The same runner, but each exchange is direct: every rank writes its chunk into every
+ * peer's exchanged vector (IPC-mapped over xGMI, one write per peer and piece, all links at
+ * once) and raises an arrival flag there; the next SpMV waits for every rank's flag.
+ *   gx_pr_dist_create_p2p : rank `rank` of `nranks` processes (<= 64), pieces as for
+ *                           gx_pr_dist_create; writes GX_P2P_HANDLE_BYTES of IPC handles
+ *                           of this rank's buffers to `handle`.
+ *   gx_pr_dist_p2p_attach : `handles` = every rank's handle in rank order (an all-gather
+ *                           of `handle`; NULL allowed for one rank); collective in effect,
+ *                           required before gx_pr_dist_run.
+ * A wait that never sees a peer's flag gives up after GX_P2P_POLLS polls (default 2^22,
+ * seconds) and gx_pr_dist_scores then fails with GX_DEVICE_ERROR.
+ * ------------------------------------------------------------------------------- */
+#define GX_P2P_HANDLE_BYTES 192
+int gx_pr_dist_create_p2p(int nranks, int rank, gx_pr_part *const *pieces, int npieces, uint8_t *handle,
+                          gx_pr_dist **dist);
+int gx_pr_dist_p2p_attach(gx_pr_dist *dist, const uint8_t *handles);
+
 /* ---- one process, N GPUs (the executables' GX_NGPUS switch) ------------------------
  * gx_pagerank_multi: Graphalytics PageRank of the host CSR A on the ndev devices of `ctxs`
  * (one gx_ctx per distinct device).  The pull matrix (A' built on the host for a directed

@@ -87,6 +87,8 @@ SIGNATURES = [
     ("gx_pr_dist_run", C.c_int, [_P, C.c_int, C.c_int, _P]),
     ("gx_pr_dist_scores", C.c_int, [_P, C.c_int, _DP]),
     ("gx_pr_dist_free", C.c_int, [_P]),
+    ("gx_pr_dist_create_p2p", C.c_int, [C.c_int, C.c_int, C.POINTER(_P), C.c_int, C.c_char_p, C.POINTER(_P)]),
+    ("gx_pr_dist_p2p_attach", C.c_int, [_P, C.c_char_p]),
     ("gx_pagerank_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(gx_csr), C.c_int, C.c_double, C.c_int, _DP]),
     ("gx_sssp_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(gx_csr), C.c_int, C.c_uint64, _DP]),
     ("gx_pr_partition", C.c_int, [C.c_uint64, _U64P, C.c_int, C.POINTER(C.c_uint32), _U64P, _U64P]),

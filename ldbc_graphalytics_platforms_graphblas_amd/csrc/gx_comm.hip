@@ -94,6 +94,72 @@ int rccl_fail(const char *what, ncclResult_t e) {
         if (_r != ncclSuccess) return rccl_fail(what, _r); \
     } while (0)
 
+// ---- one-shot peer-to-peer exchange (gx_pr_dist_create_p2p) ----
+// Every rank writes its chunk straight into every peer's exchanged vector (IPC-mapped over
+// xGMI: one write per peer, all 7 links at once) instead of RCCL's ring, then raises an
+// arrival flag in the peer's flag array.  Tokens grow monotonically across runs (a device
+// run counter, so a replayed hipGraph raises new ones): token = run * kTok + step, step 0 =
+// the initial exchange, it + 1 = iteration it's.  Memory model (LLVM AMDGPU, gfx942/950):
+// the writer's data stores, a system-scope release, the flag store (system scope); the reader
+// polls with system-scope loads and ends with a system-scope acquire, and the SpMV that
+// reads x follows in stream order.  A wait gives up after `polls` polls (a dead or diverged
+// peer), sets the error word and exits, so no wave spins forever.
+constexpr uint64_t kTok = 1ull << 24;
+
+__global__ void k_p2p_begin(uint64_t *seq) {
+    if (threadIdx.x == 0) seq[0] += 1;
+}
+
+// chunk doubles of src into dst[q] + off for every rank q (blockIdx.y; chunk, off: multiples
+// of 2), then flag[q][slot] = this run's token for `step`, raised by the workgroup that takes
+// the last ticket (after every workgroup's system-scope release).  A few workgroups per peer:
+// one xGMI link is ~50 GB/s, and the puts run beside the next piece's SpMV.
+__global__ __launch_bounds__(256) void k_p2p_put(const double *__restrict__ src, uint64_t chunk,
+                                                 double *const *__restrict__ dst, uint64_t off,
+                                                 uint64_t *const *__restrict__ flags, uint64_t slot,
+                                                 const uint64_t *seq, uint64_t step, uint32_t *ticket) {
+    double2 *d = reinterpret_cast<double2 *>(dst[blockIdx.y] + off);
+    const double2 *s = reinterpret_cast<const double2 *>(src);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < chunk / 2; i += (uint64_t)gridDim.x * 256) d[i] = s[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the stores reach the peers first
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const uint32_t all = gridDim.x * gridDim.y;
+    if (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) != all - 1) return;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint64_t tok = seq[0] * kTok + step;
+    for (uint32_t q = 0; q < gridDim.y; q++) __hip_atomic_store(flags[q] + slot, tok, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// flag[q][slot] = this run's token for `step`, for every rank q < world
+__global__ void k_p2p_signal(uint64_t *const *__restrict__ flags, int world, uint64_t slot, const uint64_t *seq,
+                             uint64_t step) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    const int q = threadIdx.x;
+    if (q < world) __hip_atomic_store(flags[q] + slot, seq[0] * kTok + step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// one wave: until flags[0 .. count) all hold at least (run - prev) * kTok + step
+__global__ __launch_bounds__(64) void k_p2p_wait(const uint64_t *flags, int count, const uint64_t *seq, uint64_t step,
+                                                 uint64_t prev, uint64_t *err, uint32_t polls) {
+    const uint64_t target = (seq[0] - prev) * kTok + step;
+    // after a timeout the run's results are void: later waits of the run do not poll again
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    for (uint32_t it = 0;; it++) {
+        bool ok = true;
+        for (int i = threadIdx.x; i < count; i += 64)
+            ok = ok && __hip_atomic_load(flags + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= target;
+        if (__all(ok)) break;
+        if (it >= polls) {
+            if (threadIdx.x == 0) __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
+}
+
 }  // namespace
 }  // namespace gx
 
@@ -124,9 +190,21 @@ struct PrDist {
     int g_iters = -1;
     hipStream_t g_stream = nullptr;
     hipStream_t last_stream = nullptr;
+    // one-shot peer-to-peer exchange (gx_pr_dist_create_p2p): flags[p * world + q] = the last
+    // token rank q raised here for piece p, flags[np * world + q] = q's end of its last run
+    bool p2p = false, attached = false;
+    DBuf<uint64_t> flags, seq;            // seq[0]: runs started; seq[1]: a wait timed out
+    DBuf<double *> pxa, pxb;              // per rank: its xa / xb (ours for this rank)
+    DBuf<uint64_t *> pfl;                 // per rank: its flags
+    std::vector<void *> opened;           // the peers' IPC mappings
+    DBuf<uint32_t> tickets;               // per piece: k_p2p_put's workgroup tickets
+    uint32_t polls = 1u << 22;
+    uint32_t put_blocks = 32;             // workgroups per peer (GX_P2P_BLOCKS)
 
     ~PrDist() {
         (void)hipSetDevice(ctx->device);
+        (void)hipDeviceSynchronize();
+        for (void *q : opened) (void)hipIpcCloseMemHandle(q);
         if (gexec) (void)hipGraphExecDestroy(gexec);
         if (graph) (void)hipGraphDestroy(graph);
         for (hipEvent_t e : ev_piece) (void)hipEventDestroy(e);
@@ -136,9 +214,21 @@ struct PrDist {
 
     size_t span() const { return chunk * (size_t)world; }   // one piece's slab
 
-    // exchange piece p's local chunk into slab p of `x` (after what s has enqueued so far)
-    int gather(int p, double *x, hipStream_t s) {
+    int np() const { return (int)pieces.size(); }
+
+    // exchange piece p's local chunk into slab p of `x` (after what s has enqueued so far);
+    // `step` names the exchange for the peer-to-peer flags
+    int gather(int p, double *x, hipStream_t s, uint64_t step) {
         double *dst = x + (size_t)p * span();
+        if (p2p) {
+            GX_HIP_TRY(hipEventRecord(ev_piece[p], s));
+            GX_HIP_TRY(hipStreamWaitEvent(cs, ev_piece[p], 0));
+            const unsigned blocks = (unsigned)std::min<uint64_t>(put_blocks, (chunk / 2 + 255) / 256);
+            hipLaunchKernelGGL(k_p2p_put, dim3(std::max(blocks, 1u), world), dim3(256), 0, cs, xl[p]->p, chunk,
+                               x == xa.p ? pxa.p : pxb.p, (uint64_t)p * span() + (uint64_t)rank * chunk, pfl.p,
+                               (uint64_t)p * world + rank, seq.p, step, tickets.p + p);
+            return check_launch("k_p2p_put");
+        }
         if (!comm) {
             GX_HIP_TRY(hipMemcpyAsync(dst, xl[p]->p, chunk * sizeof(double), hipMemcpyDeviceToDevice, s));
             return GX_SUCCESS;
@@ -149,32 +239,53 @@ struct PrDist {
         return GX_SUCCESS;
     }
 
-    int join(hipStream_t s) {   // compute stream waits for every gather issued so far
-        if (!comm) return GX_SUCCESS;
+    // compute stream waits for every gather issued so far (peer-to-peer: and for every
+    // rank's chunks of exchange `step` to have arrived here)
+    int join(hipStream_t s, uint64_t step) {
+        if (!comm && !p2p) return GX_SUCCESS;
         GX_HIP_TRY(hipEventRecord(ev_comm, cs));
         GX_HIP_TRY(hipStreamWaitEvent(s, ev_comm, 0));
+        if (p2p) {
+            hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, s, flags.p, np() * world, seq.p, step, (uint64_t)0,
+                               seq.p + 1, polls);
+            GX_TRY(check_launch("k_p2p_wait"));
+        }
         return GX_SUCCESS;
     }
 
     int enqueue(int iters, hipStream_t s) {
         const int np = (int)pieces.size();
-        const bool swap_only = !comm && np == 1;   // one rank, one piece: no exchange at all
+        const bool swap_only = !comm && !p2p && np == 1;   // one rank, one piece: no exchange at all
         double *xr = xa.p, *xw = xb.p;
+        if (p2p) {
+            // a new run; its first exchange overwrites the peers' xa, so every peer must have
+            // finished reading it in the previous run (their end-of-run tokens)
+            hipLaunchKernelGGL(k_p2p_begin, dim3(1), dim3(64), 0, s, seq.p);
+            GX_TRY(check_launch("k_p2p_begin"));
+            hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, s, flags.p + (size_t)np * world, world, seq.p,
+                               (uint64_t)0, (uint64_t)1, seq.p + 1, polls);
+            GX_TRY(check_launch("k_p2p_wait"));
+        }
         for (int p = 0; p < np; p++) GX_TRY(pr_init(pieces[p], swap_only ? xr : xl[p]->p, s));
         if (!swap_only) {
-            for (int p = 0; p < np; p++) GX_TRY(gather(p, xr, s));
-            GX_TRY(join(s));
+            for (int p = 0; p < np; p++) GX_TRY(gather(p, xr, s, 0));
+            GX_TRY(join(s, 0));
         }
         for (int it = 0; it < iters; it++) {
             const bool last = it == iters - 1;
             for (int p = 0; p < np; p++) {
                 double *out = swap_only ? xw : xl[p]->p;
                 GX_TRY(pr_step(pieces[p], xr, out, last ? ro[p]->p : nullptr, s));
-                if (!last && !swap_only) GX_TRY(gather(p, xw, s));
+                if (!last && !swap_only) GX_TRY(gather(p, xw, s, (uint64_t)it + 1));
             }
             if (last) break;
-            if (!swap_only) GX_TRY(join(s));
+            if (!swap_only) GX_TRY(join(s, (uint64_t)it + 1));
             std::swap(xr, xw);
+        }
+        if (p2p) {   // this rank is done reading its vectors: the end-of-run token to every rank
+            hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, s, pfl.p, world, (uint64_t)np * world + rank, seq.p,
+                               (uint64_t)0);
+            GX_TRY(check_launch("k_p2p_signal"));
         }
         return GX_SUCCESS;
     }
@@ -252,9 +363,10 @@ extern "C" int gx_comm_free(gx_comm *comm) {
     return GX_SUCCESS;
 }
 
-extern "C" int gx_pr_dist_create(gx_comm *comm, gx_pr_part *const *parts, int npieces, gx_pr_dist **out) {
+namespace {
+
+int dist_create(gx_comm *comm, int world, int rank, bool p2p, gx_pr_part *const *parts, int npieces, gx_pr_dist **out) {
     if (!parts || !out || npieces < 1) return fail(GX_NULL_POINTER, "gx_pr_dist_create: null argument");
-    const int world = comm ? comm->nranks : 1, rank = comm ? comm->rank : 0;
     PrPart *p0 = reinterpret_cast<PrPart *>(parts[0]);
     if (!p0) return fail(GX_NULL_POINTER, "gx_pr_dist_create: null piece");
     if (comm && comm->ctx != p0->ctx) return fail(GX_INVALID_VALUE, "gx_pr_dist_create: comm and pieces on different contexts");
@@ -294,7 +406,22 @@ extern "C" int gx_pr_dist_create(gx_comm *comm, gx_pr_part *const *parts, int np
     hipError_t e = hipSuccess;
     if (rc == GX_SUCCESS) e = hipMemset(d.xa.p, 0, full * sizeof(double));
     if (rc == GX_SUCCESS && e == hipSuccess) e = hipMemset(d.xb.p, 0, full * sizeof(double));
-    if (rc == GX_SUCCESS && e == hipSuccess && comm) {
+    if (rc == GX_SUCCESS && e == hipSuccess && p2p) {
+        d.p2p = true;
+        const size_t nf = (size_t)(npieces + 1) * world;
+        rc = d.flags.alloc(nf);
+        if (rc == GX_SUCCESS) rc = d.seq.alloc(2);
+        if (rc == GX_SUCCESS) rc = d.pxa.alloc(world);
+        if (rc == GX_SUCCESS) rc = d.pxb.alloc(world);
+        if (rc == GX_SUCCESS) rc = d.pfl.alloc(world);
+        if (rc == GX_SUCCESS) rc = d.tickets.alloc(npieces);
+        if (rc == GX_SUCCESS) e = hipMemset(d.tickets.p, 0, npieces * sizeof(uint32_t));
+        if (rc == GX_SUCCESS && e == hipSuccess) e = hipMemset(d.flags.p, 0, nf * sizeof(uint64_t));
+        if (rc == GX_SUCCESS && e == hipSuccess) e = hipMemset(d.seq.p, 0, 2 * sizeof(uint64_t));
+        if (const char *pl = std::getenv("GX_P2P_POLLS")) d.polls = (uint32_t)std::strtoul(pl, nullptr, 10);
+        if (const char *pb = std::getenv("GX_P2P_BLOCKS")) d.put_blocks = std::max(1u, (uint32_t)std::strtoul(pb, nullptr, 10));
+    }
+    if (rc == GX_SUCCESS && e == hipSuccess && (comm || p2p)) {
         e = hipStreamCreateWithFlags(&d.cs, hipStreamNonBlocking);
         d.ev_piece.assign(npieces, nullptr);
         for (int p = 0; p < npieces && e == hipSuccess; p++)
@@ -311,10 +438,79 @@ extern "C" int gx_pr_dist_create(gx_comm *comm, gx_pr_part *const *parts, int np
     return GX_SUCCESS;
 }
 
+}  // namespace
+
+extern "C" int gx_pr_dist_create(gx_comm *comm, gx_pr_part *const *parts, int npieces, gx_pr_dist **out) {
+    return dist_create(comm, comm ? comm->nranks : 1, comm ? comm->rank : 0, false, parts, npieces, out);
+}
+
+// IPC handles of this rank: xa, xb, flags (hipIpcMemHandle_t each)
+extern "C" int gx_pr_dist_create_p2p(int nranks, int rank, gx_pr_part *const *parts, int npieces, uint8_t *handle,
+                                     gx_pr_dist **out) {
+    if (!handle || !out) return fail(GX_NULL_POINTER, "gx_pr_dist_create_p2p: null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks || nranks > 64)
+        return fail(GX_INVALID_VALUE, "gx_pr_dist_create_p2p: bad rank/nranks (at most 64 ranks)");
+    static_assert(3 * sizeof(hipIpcMemHandle_t) <= GX_P2P_HANDLE_BYTES, "handle bytes");
+    gx_pr_dist *h = nullptr;
+    GX_TRY(dist_create(nullptr, nranks, rank, true, parts, npieces, &h));
+    PrDist &d = h->d;
+    std::memset(handle, 0, GX_P2P_HANDLE_BYTES);
+    hipIpcMemHandle_t m[3];
+    void *bufs[3] = {d.xa.p, d.xb.p, d.flags.p};
+    for (int k = 0; k < 3; k++) {
+        const hipError_t e = hipIpcGetMemHandle(&m[k], bufs[k]);
+        if (e != hipSuccess) {
+            delete h;
+            return fail(GX_DEVICE_ERROR, std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e));
+        }
+        std::memcpy(handle + k * sizeof(hipIpcMemHandle_t), &m[k], sizeof(hipIpcMemHandle_t));
+    }
+    *out = h;
+    return GX_SUCCESS;
+}
+
+// handles: nranks * GX_P2P_HANDLE_BYTES in rank order (this rank's own entry is not opened)
+extern "C" int gx_pr_dist_p2p_attach(gx_pr_dist *h, const uint8_t *handles) {
+    if (!h) return fail(GX_NULL_POINTER, "gx_pr_dist_p2p_attach: null argument");
+    PrDist &d = h->d;
+    if (!d.p2p) return fail(GX_INVALID_OBJECT, "gx_pr_dist_p2p_attach: not a peer-to-peer runner");
+    if (d.attached) return fail(GX_INVALID_OBJECT, "gx_pr_dist_p2p_attach: already attached");
+    if (!handles && d.world > 1) return fail(GX_NULL_POINTER, "gx_pr_dist_p2p_attach: null handles");
+    GX_HIP_TRY(hipSetDevice(d.ctx->device));
+    std::vector<double *> a(d.world), b(d.world);
+    std::vector<uint64_t *> f(d.world);
+    for (int q = 0; q < d.world; q++) {
+        if (q == d.rank) {
+            a[q] = d.xa.p;
+            b[q] = d.xb.p;
+            f[q] = d.flags.p;
+            continue;
+        }
+        void *ptr[3] = {nullptr, nullptr, nullptr};
+        for (int k = 0; k < 3; k++) {
+            hipIpcMemHandle_t m;
+            std::memcpy(&m, handles + (size_t)q * GX_P2P_HANDLE_BYTES + k * sizeof(hipIpcMemHandle_t), sizeof(m));
+            const hipError_t e = hipIpcOpenMemHandle(&ptr[k], m, hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess)
+                return fail(GX_DEVICE_ERROR, "hipIpcOpenMemHandle (rank " + std::to_string(q) + "): " + hipGetErrorString(e));
+            d.opened.push_back(ptr[k]);
+        }
+        a[q] = static_cast<double *>(ptr[0]);
+        b[q] = static_cast<double *>(ptr[1]);
+        f[q] = static_cast<uint64_t *>(ptr[2]);
+    }
+    GX_HIP_TRY(hipMemcpy(d.pxa.p, a.data(), d.world * sizeof(double *), hipMemcpyHostToDevice));
+    GX_HIP_TRY(hipMemcpy(d.pxb.p, b.data(), d.world * sizeof(double *), hipMemcpyHostToDevice));
+    GX_HIP_TRY(hipMemcpy(d.pfl.p, f.data(), d.world * sizeof(uint64_t *), hipMemcpyHostToDevice));
+    d.attached = true;
+    return GX_SUCCESS;
+}
+
 extern "C" int gx_pr_dist_run(gx_pr_dist *h, int iters, int use_graph, void *stream) {
     if (!h) return fail(GX_NULL_POINTER, "gx_pr_dist_run: null argument");
     if (iters < 1) return fail(GX_INVALID_VALUE, "gx_pr_dist_run: iters must be >= 1");
     PrDist &d = h->d;
+    if (d.p2p && !d.attached) return fail(GX_INVALID_OBJECT, "gx_pr_dist_run: peer-to-peer runner not attached");
     GX_HIP_TRY(hipSetDevice(d.ctx->device));
     return d.run(iters, use_graph != 0, stream ? (hipStream_t)stream : d.ctx->stream);
 }
@@ -325,6 +521,11 @@ extern "C" int gx_pr_dist_scores(gx_pr_dist *h, int piece, double *scores) {
     if (piece < 0 || piece >= (int)d.pieces.size()) return fail(GX_INVALID_INDEX, "gx_pr_dist_scores: bad piece");
     GX_HIP_TRY(hipSetDevice(d.ctx->device));
     if (d.last_stream) GX_HIP_TRY(hipStreamSynchronize(d.last_stream));
+    if (d.p2p) {
+        uint64_t err = 0;
+        GX_HIP_TRY(hipMemcpy(&err, d.seq.p + 1, sizeof(err), hipMemcpyDeviceToHost));
+        if (err) return fail(GX_DEVICE_ERROR, "gx_pr_dist_scores: a peer-to-peer wait timed out (a peer stopped or diverged)");
+    }
     const uint64_t rows = d.pieces[piece]->rows;
     if (rows) GX_HIP_TRY(hipMemcpy(scores, d.ro[piece]->p, rows * sizeof(double), hipMemcpyDeviceToHost));
     return GX_SUCCESS;

@@ -315,16 +315,44 @@ class DevicePageRank:
     PartitionedPageRank, without a host round trip per iteration.
 
     `steppers` are the GpuStep pieces of this rank (piece p = virtual rank p*nranks+rank);
-    `comm` is a Comm, or None for one rank."""
+    `comm` is a Comm, or None for one rank.
 
-    def __init__(self, steppers: Sequence["GpuStep"], comm: Optional[Comm], use_graph: bool = True):
+    `p2p = (nranks, rank, share_all)` selects the one-shot peer-to-peer exchange instead
+    (gx_pr_dist_create_p2p; no RCCL, `comm` must be None): `share_all(bytes) -> list of
+    bytes` hands every rank's IPC handle to every rank in rank order (bench.py:
+    torch.distributed.all_gather_object); every rank constructs its runner together."""
+
+    def __init__(self, steppers: Sequence["GpuStep"], comm: Optional[Comm], use_graph: bool = True,
+                 p2p: Optional[tuple] = None):
         from . import _native as N
         self.N = N
         self.steps = list(steppers)
+        lib = N.lib()
         arr = (C.c_void_p * len(self.steps))(*[s.part.value for s in self.steps])
         self.handle = C.c_void_p()
-        N.check(N.lib().gx_pr_dist_create(comm.handle if comm is not None else None, arr, len(self.steps),
+        if p2p is None:
+            N.check(lib.gx_pr_dist_create(comm.handle if comm is not None else None, arr, len(self.steps),
                                           C.byref(self.handle)), "gx_pr_dist_create")
+        else:
+            if comm is not None:
+                raise ValueError("the peer-to-peer exchange takes no RCCL communicator")
+            nranks, rank, share_all = p2p
+            nb = 192   # GX_P2P_HANDLE_BYTES
+            mine = C.create_string_buffer(nb)
+            rc = lib.gx_pr_dist_create_p2p(nranks, rank, arr, len(self.steps), mine, C.byref(self.handle))
+            err = lib.gx_last_error().decode(errors="replace") if rc else ""
+            got = share_all(mine.raw if rc == 0 else b"")   # every rank takes part, also after a failure
+            if rc:
+                raise RuntimeError(f"gx_pr_dist_create_p2p: {err}")
+            if len(got) != nranks or any(len(g) != nb for g in got):
+                self.close()
+                raise RuntimeError("gx_pr_dist_create_p2p: a rank has no peer-to-peer handle")
+            allh = C.create_string_buffer(b"".join(got), nb * nranks)
+            rc = lib.gx_pr_dist_p2p_attach(self.handle, allh)
+            if rc:
+                msg = lib.gx_last_error().decode(errors="replace")
+                self.close()
+                raise RuntimeError(f"gx_pr_dist_p2p_attach: {msg}")
         self.use_graph = use_graph
 
     def run(self, iters: int, stream: int = 0) -> None:

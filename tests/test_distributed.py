@@ -277,6 +277,110 @@ def test_gpu_device_driven_pagerank(pieces, use_graph, with_comm):
     ctx.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("pieces", [1, 3])
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_gpu_p2p_exchange_one_rank(pieces, use_graph):
+    """gx_pr_dist_create_p2p with one rank: the put / flag / wait protocol writing into this
+    rank's own vector (pieces exchanged by the peer-to-peer kernels), replayed and re-captured."""
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import DevicePageRank, GpuStep
+    csr = rmat(13, 16, 11)
+    perm, hub, bounds = interleaved_relabel(csr, pieces)
+    ctx = Context(0)
+    lrs = [slice_rows(hub, bounds, p) for p in range(pieces)]
+    steps = [GpuStep(ctx, csr.n, pieces, lr, 0.85) for lr in lrs]
+    dpr = DevicePageRank(steps, None, use_graph=use_graph, p2p=(1, 0, lambda h: [h]))
+    stream = torch.cuda.Stream(torch.device("cuda", 0))
+    for iters in (6, 6, 4):
+        dpr.run(iters, stream.cuda_stream)
+        got = np.concatenate(dpr.scores([lr.rows for lr in lrs]))[perm]
+        np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, iters), rtol=1e-12)
+    dpr.close()
+    for s in steps:
+        s.close()
+    ctx.close()
+
+
+def _p2p_worker(rank, world, port, q, pieces):
+    """One rank of the peer-to-peer exchange; both ranks share GPU 0 (IPC between two
+    processes on one device), the handles travel over gloo."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+        from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import DevicePageRank, GpuStep
+        torch.cuda.set_device(0)
+        csr = rmat(12, 16, 7)
+        perm, hub, bounds = interleaved_relabel(csr, world * pieces)
+        lrs = [slice_rows(hub, bounds, p * world + rank) for p in range(pieces)]
+        ctx = Context(0)
+        steps = [GpuStep(ctx, csr.n, world * pieces, lr, 0.85) for lr in lrs]
+
+        def share_all(h):
+            box = [None] * world
+            dist.all_gather_object(box, h)
+            return box
+        dpr = DevicePageRank(steps, None, use_graph=True, p2p=(world, rank, share_all))
+        stream = torch.cuda.Stream(torch.device("cuda", 0))
+        results = []
+        for iters in (6, 6, 4):   # replayed, then re-captured
+            dpr.run(iters, stream.cuda_stream)
+            mine = [(lr.rank, a) for lr, a in zip(lrs, dpr.scores([lr.rows for lr in lrs]))]
+            parts = [None] * world
+            dist.all_gather_object(parts, mine)
+            if rank == 0:
+                ordered = sorted((v for part in parts for v in part), key=lambda t: t[0])
+                results.append((iters, np.concatenate([a for _, a in ordered])[perm]))
+        dist.barrier()   # no rank unmaps a vector a peer still writes
+        dpr.close()
+        for s in steps:
+            s.close()
+        ctx.close()
+        if rank == 0:
+            q.put(results)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pieces", [1, 2])
+def test_gpu_p2p_exchange_world2_one_device(pieces):
+    """Two processes, the peer-to-peer exchange between them (IPC-mapped vectors and flags on
+    one device), against the oracle over three runs."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_p2p_worker, args=(r, 2, port, q, pieces)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        results = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    csr = rmat(12, 16, 7)
+    for iters, got in results:
+        np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, iters), rtol=1e-12)
+
+
+def test_p2p_runner_rejects_bad_arguments():
+    """gx_pr_dist_create_p2p / _attach argument checks, before any device work."""
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    import ctypes as C
+    lib = N.lib()
+    h = C.c_void_p()
+    buf = C.create_string_buffer(192)
+    assert lib.gx_pr_dist_create_p2p(2, 2, None, 1, buf, C.byref(h)) != 0     # rank >= nranks
+    assert lib.gx_pr_dist_create_p2p(65, 0, None, 1, buf, C.byref(h)) != 0    # > 64 ranks
+    assert lib.gx_pr_dist_create_p2p(2, 0, None, 1, None, C.byref(h)) != 0    # no handle buffer
+    assert lib.gx_pr_dist_p2p_attach(None, buf) != 0
+
+
 def test_device_runner_rejects_mismatched_pieces():
     """Piece p must be virtual rank p * nranks + rank: checked before any device work."""
     from ldbc_graphalytics_platforms_graphblas_amd import _native as N
