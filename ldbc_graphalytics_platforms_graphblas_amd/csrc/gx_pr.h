@@ -157,6 +157,8 @@ struct PrPart {
     bool rows_desc = false;      // row lengths non-increasing (an undirected hub-first plan): the
                                  // block cut jumps by binary search
     int pace = 0;
+    int queue_on = -1;           // GX_PR_QUEUE: one resident workgroup per CU pulling work items (-1 auto)
+    DBuf<uint32_t> queue;        // its counters (k_pr_pull_units QUEUE)
     uint32_t pace_nw = 0, pace_h = 0, pace_wshift = 18, pace_d = 1, pace_polls = 64;
     DBuf<int32_t> pace_rounds;
     DBuf<uint32_t> pace_prog;

@@ -91,6 +91,8 @@ struct SortedArgs {
     const int32_t *pace_rounds;
     uint32_t *pace_prog;
     uint32_t pace_nw, pace_d, pace_polls, pace_ncus;
+    // work queue (GX_PR_QUEUE): [0] next work item, [1] workgroups done (reset by the last)
+    uint32_t *queue;
 };
 
 // Returns the row's score if the row is dangling (out-degree 0), else 0.
@@ -557,19 +559,15 @@ __device__ __forceinline__ void pace_wait(const SortedArgs &a, uint32_t *slot, u
     __syncthreads();
 }
 
-// One iteration's SpMV over split blocks.  Grid: [0, nlong_pad) LONG row segments (padded to a
-// multiple of 8), then the units (largest first; the blocks of rows without entries last).  A multi-unit block's units store their row sums write-through (sc1) to
+// One iteration's SpMV over split blocks.  Work items: [0, nlong_pad) LONG row segments (padded
+// to a multiple of 8), then the units (largest first; the blocks of rows without entries last).  A multi-unit block's units store their row sums write-through (sc1) to
 // their own slab, drain them (vmcnt(0)) and take a ticket; the last arriver adds the slabs in
 // unit order with sc1 loads and runs the epilogue (MI355X_MICROARCH.md "Valid forms": sc1 stores
 // drained before the counter add, sc1 loads by the workgroup whose add came last).
 // TIMES: debug build with per-workgroup timestamps (GX_PR_UNIT_TIMES).
-template <bool TIMES, int PROBE = 0, int CP = 0, bool PACE = false>
-__global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs a) {
-    extern __shared__ double acc[];
-    __shared__ double wred[kBS / kWave];
-    __shared__ int last;
-
-    const uint32_t w = blockIdx.x;
+template <bool TIMES, int PROBE, int CP, bool PACE>
+__device__ __forceinline__ void pull_item(const SortedArgs &a, const uint32_t w, double *acc, double *wred, int &last,
+                                          const double teleport) {
     const int tid = threadIdx.x;
     __shared__ uint64_t ts[2];   // TIMES: start, gather end (LDS, so no registers are held)
     if (TIMES && tid == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
@@ -581,9 +579,6 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
             a.utimes[4 * w + 3] = (uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);   // HW_REG_XCC_ID[3:0]
         }
     };
-    double dsum = 0.0;
-    for (int k = 0; k < a.nranks; k++) dsum += a.x_in[(int64_t)k * a.chunk + a.chunk - 1];
-    const double teleport = a.teleport0 + a.damping_over_n * dsum;
     if (a.zero_slot && w == 0 && tid == 0) a.x_out[a.chunk - 1] = 0.0;
     if (w < a.nlong_pad) {
         if (w < a.nlong) long_segment(a, a.blocks[w], wred, teleport);
@@ -668,6 +663,47 @@ __global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs
         if (slot >= 0) dangling_publish(a, slot, d, wred, &last);
     }
     stamp();
+}
+
+// The next work item for the whole workgroup.  Not inlined: inlined, the compiler turned the
+// thread-0 branch into the exit of an inner loop that the other lanes of wave 0 kept running
+// (barriers and all) while lane 0 waited to take the next item, and the launch never ended.
+__device__ __noinline__ uint32_t queue_fetch(uint32_t *q, uint32_t *slot) {
+    if (threadIdx.x == 0) *slot = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t w = *slot;
+    __syncthreads();   // every thread has read the slot before the next fetch rewrites it
+    return w;
+}
+
+// One workgroup per work item, or (QUEUE, GX_PR_QUEUE=1) one resident workgroup per CU taking
+// items from a device counter in the same order: the dispatcher deals workgroups to the XCDs
+// round-robin, so an item whose XCD has no free CU waits even while other XCDs idle; from a
+// queue every CU takes the next item the moment it is free.
+template <bool TIMES, int PROBE = 0, int CP = 0, bool PACE = false, bool QUEUE = false>
+__global__ __launch_bounds__(kBS, TIMES ? 1 : 4) void k_pr_pull_units(SortedArgs a) {
+    extern __shared__ double acc[];
+    __shared__ double wred[kBS / kWave];
+    __shared__ int last;
+    double dsum = 0.0;
+    for (int k = 0; k < a.nranks; k++) dsum += a.x_in[(int64_t)k * a.chunk + a.chunk - 1];
+    const double teleport = a.teleport0 + a.damping_over_n * dsum;
+    if constexpr (!QUEUE) {
+        pull_item<TIMES, PROBE, CP, PACE>(a, blockIdx.x, acc, wred, last, teleport);
+    } else {
+        __shared__ uint32_t item;
+        const uint32_t total = a.nlong_pad + a.nunits;
+        for (;;) {
+            const uint32_t w = queue_fetch(a.queue, &item);   // (its barriers: the last item's LDS is free)
+            if (w >= total) break;
+            pull_item<TIMES, PROBE, CP, PACE>(a, w, acc, wred, last, teleport);
+        }
+        if (threadIdx.x == 0 &&
+            __hip_atomic_fetch_add(&a.queue[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+            __hip_atomic_store(&a.queue[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.queue[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // The plan's one radix sort.  The rows are cut into segments, in row order: the sorted blocks
@@ -1476,6 +1512,11 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         GX_HIP_TRY(hipMemset(p->uticket.p, 0, p->uticket.n * 4));
     }
     p->unit_nnz = T;
+    // work queue: on (1), off (0), or (default) when the launch has at least two items per CU
+    // (SYN-8_5, 887 items: 755 -> 716 us per launch; SYN-7_5 ran 3 % slower from a queue)
+    p->queue_on = env_int("GX_PR_QUEUE", -1, -1, 1);
+    GX_TRY(p->queue.alloc(2));
+    GX_HIP_TRY(hipMemset(p->queue.p, 0, 2 * sizeof(uint32_t)));
     // paced sweep (GX_PR_PACE=1; GX_PR_PACE_H first boundary column, GX_PR_PACE_W log2 window
     // columns, GX_PR_PACE_D windows of lead, GX_PR_PACE_POLLS the bound on a wait)
     p->pace = env_int("GX_PR_PACE", 0, 0, 1);
@@ -1573,6 +1614,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.pace_d = p->pace_d;
     a.pace_polls = p->pace_polls;
     a.pace_ncus = (uint32_t)std::max(1, p->ctx->num_cus);
+    a.queue = p->queue.p;
     const char *times_path = std::getenv("GX_PR_UNIT_TIMES");   // debug: not under graph capture
     const uint32_t nw = p->nlong_pad + p->nunits;
     if (times_path && nw) {
@@ -1608,6 +1650,12 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                 if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5, true>), dim3(nw), dim3(kBS), lds, s, a);
                 else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1, true>), dim3(nw), dim3(kBS), lds, s, a);
                 else hipLaunchKernelGGL((k_pr_pull_units<false, 0, 0, true>), dim3(nw), dim3(kBS), lds, s, a);
+            } else if (p->queue_on == 1 || (p->queue_on == -1 && nw >= 2u * (unsigned)std::max(1, p->ctx->num_cus))) {
+                // one resident workgroup per CU (the LDS allows no second), never more than the items
+                const unsigned nq = std::min<unsigned>(nw, (unsigned)std::max(1, p->ctx->num_cus));
+                if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5, false, true>), dim3(nq), dim3(kBS), lds, s, a);
+                else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1, false, true>), dim3(nq), dim3(kBS), lds, s, a);
+                else hipLaunchKernelGGL((k_pr_pull_units<false, 0, 0, false, true>), dim3(nq), dim3(kBS), lds, s, a);
             } else if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5>), dim3(nw), dim3(kBS), lds, s, a);
             else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1>), dim3(nw), dim3(kBS), lds, s, a);
             else hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);

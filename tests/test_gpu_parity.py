@@ -212,6 +212,9 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                  {"GX_PR_NARROW_MIN": "4096"}, {"GX_PR_NARROW_MIN": "1073741824"},
                                  {"GX_PR_WIDE_COST": "64", "GX_PR_ROW_COST": "0", "GX_PR_UNIT_NNZ": "8192"},
                                  {"GX_PR_ROW_COST": "1024", "GX_PR_BLOCK_NNZ": "65536"},
+                                 {"GX_PR_QUEUE": "1"}, {"GX_PR_QUEUE": "0"},
+                                 {"GX_PR_QUEUE": "1", "GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192",
+                                  "GX_PR_LONG_NNZ": "1024", "GX_PR_CP": "5", "GX_PR_NT_COL": "1000"},
                                  {"GX_PR_PACE": "1", "GX_PR_PACE_H": "1024", "GX_PR_PACE_W": "10"},
                                  {"GX_PR_PACE": "1", "GX_PR_PACE_H": "0", "GX_PR_PACE_W": "11", "GX_PR_PACE_D": "0",
                                   "GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536"},
