@@ -1648,6 +1648,9 @@ struct CdlpCache {
     DBuf<uint32_t> kcnt;
     DBuf<int> kflags;
     bool keep_built = false;
+    // entries the check reads: with the hub-first copy (rows by total degree, descending) the
+    // rows of degree <= kTiny, which it skips, hold every entry from here on
+    int64_t keep_nnzA = 0, keep_nnzT = 0;
     DBuf<int32_t> redo;         // k_cdlp_sparse_group's vertices for the 16K-slot instance
     DBuf<unsigned int> rcnt;    // one redo count per iteration
     ~CdlpCache() {
@@ -1751,6 +1754,21 @@ int keep_build(CdlpCache &C, hipStream_t s) {
     GX_HIP_TRY(hipMemsetAsync(C.kcnt.p, 0, (size_t)std::max<int64_t>(G.n, 1) * 4, s));
     GX_TRY(C.kflags.alloc(2));
     GX_HIP_TRY(hipMemsetAsync(C.kflags.p, 0, 2 * sizeof(int), s));
+    C.keep_nnzA = G.nnzA;
+    C.keep_nnzT = G.directed ? G.nnzT : 0;
+    if (C.relabel && G.h_rpA && (!G.directed || G.h_rpT)) {
+        auto deg = [&](int64_t i) {
+            return (G.h_rpA[i + 1] - G.h_rpA[i]) + (G.directed ? G.h_rpT[i + 1] - G.h_rpT[i] : 0);
+        };
+        int64_t lo = 0, hi = G.n;   // the first position of degree <= kTiny (degrees non-increasing)
+        while (lo < hi) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if (deg(mid) > kTiny) lo = mid + 1;
+            else hi = mid;
+        }
+        C.keep_nnzA = G.h_rpA[lo];
+        if (G.directed) C.keep_nnzT = G.h_rpT[lo];
+    }
     C.keep_built = true;
     return GX_SUCCESS;
 }
@@ -1926,8 +1944,8 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                                        C->kcnt.p, C->dense.p, kf, cnt + kCdlpSubs * kCntStride, head);
                     return check_launch("k_cdlp_keep_count");
                 };
-                GX_TRY(count(G.ciA, G.nnzA, C->kA, 1));
-                if (G.directed) GX_TRY(count(G.ciT, G.nnzT, C->kT, 0));
+                GX_TRY(count(G.ciA, C->keep_nnzA, C->kA, 1));
+                if (G.directed) GX_TRY(count(G.ciT, C->keep_nnzT, C->kT, 0));
                 hipLaunchKernelGGL(k_cdlp_keep_apply, dim3(8 * kCdlpSubs), dim3(256), 0, s, G.rpA, G.rpT, (int64_t)0, n,
                                    C->kcnt.p, C->act.p, (int32_t)it, kf, cnt, C->al.p, C->asub, kf + 1);
                 GX_TRY(check_launch("k_cdlp_keep_apply"));
