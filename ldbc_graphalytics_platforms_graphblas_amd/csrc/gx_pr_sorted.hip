@@ -1112,8 +1112,8 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // Sorted blocks of up to block_nnz entries and sorted_rows rows, each cut into units of at
     // most T entries (interleaved rounds), one workgroup each, one workgroup per CU; rows longer
     // than block_nnz / 4 take the LONG path.  block_nnz = 1 Mi with 4 Ki rows, 4 Mi once nnz / CUs
-    // passes 384 Ki, 8 Mi with 16 Ki rows once it passes 2 Mi, at most 4x the power of two
-    // nearest nnz / CUs; T is a quarter block, or past 2 Mi entries per CU chosen by simulating
+    // passes 384 Ki, 32 Mi with 16 Ki rows once it passes 2 Mi, at most 4x (16x past 2 Mi) the
+    // power of two nearest nnz / CUs; T is a quarter block, or past 2 Mi entries per CU chosen by simulating
     // the launch (pr_unit_makespan).  GX_PR_BLOCK_NNZ, GX_PR_SORTED_ROWS, GX_PR_LONG_NNZ,
     // GX_PR_UNIT_NNZ override.  Measured (tools/pr_units_sweep.sh, us per launch): SYN-7_5 100;
     // graph500-22 267; SYN-8_5 1064-1070 (round 2, before X4).  Larger blocks cut the x line
@@ -1127,7 +1127,11 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // 32 units each ran 50 us per launch against 34 with 128 Ki blocks
     int64_t pow2 = 1 << 14;
     while (pow2 < (1 << 24) && (double)(2 * pow2) <= per_cu * 1.41421356) pow2 *= 2;
-    const int64_t bdef = std::min<int64_t>(huge ? 8 << 20 : per_cu > 384.0 * 1024 ? 4 << 20 : 1 << 20, 4 * pow2);
+    // huge graphs: 32 Mi-entry blocks since the work queue (SYN-8_5, us per launch: 8 Mi 714,
+    // 16 Mi 690, 32 Mi 685, 64 Mi 700, 128 Mi 702; profiles/r04_pr_block_sweep_queue.txt):
+    // fewer blocks re-read x, and the queue keeps the larger units balanced
+    const int64_t bdef = huge ? std::min<int64_t>(32 << 20, 16 * pow2)
+                              : std::min<int64_t>(per_cu > 384.0 * 1024 ? 4 << 20 : 1 << 20, 4 * pow2);
     const int64_t B = env_int("GX_PR_BLOCK_NNZ", (int)bdef, 1024, 1 << 30);
     p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)std::max<int64_t>(B / 4, kRound), 1024, 1 << 30);
     p->sorted_nnz = (int)B;
