@@ -280,9 +280,13 @@ def test_gpu_device_driven_pagerank(pieces, use_graph, with_comm):
 @pytest.mark.gpu
 @pytest.mark.parametrize("pieces", [1, 3])
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_gpu_p2p_exchange_one_rank(pieces, use_graph):
+@pytest.mark.parametrize("blocks", [None, "1"])
+def test_gpu_p2p_exchange_one_rank(pieces, use_graph, blocks, monkeypatch):
     """gx_pr_dist_create_p2p with one rank: the put / flag / wait protocol writing into this
-    rank's own vector (pieces exchanged by the peer-to-peer kernels), replayed and re-captured."""
+    rank's own vector (pieces exchanged by the peer-to-peer kernels), replayed and re-captured;
+    GX_P2P_BLOCKS=1: one put workgroup per peer (the copy loop and the last-ticket signal)."""
+    if blocks:
+        monkeypatch.setenv("GX_P2P_BLOCKS", blocks)
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
     from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import DevicePageRank, GpuStep
     csr = rmat(13, 16, 11)
