@@ -1632,8 +1632,12 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
         // One workgroup per CU also keeps fewer concurrent sweeps of x: SYN-7_5 ran 100-104 us per
         // launch against 109-125 with two (round 2, tools/pr_units_sweep.sh).
         const size_t lds = (size_t)(1 << kRowBits) * sizeof(double);
+        const bool use_queue = p->queue_on == 1 || (p->queue_on == -1 && nw >= 2u * (unsigned)std::max(1, p->ctx->num_cus));
+        const unsigned nq = std::min<unsigned>(nw, (unsigned)std::max(1, p->ctx->num_cus));
         if (a.utimes) {
-            hipLaunchKernelGGL((k_pr_pull_units<true>), dim3(nw), dim3(kBS), lds, s, a);
+            // (per-item stamps; the queued debug kernel runs without the cache policy)
+            if (use_queue) hipLaunchKernelGGL((k_pr_pull_units<true, 0, 0, false, true>), dim3(nq), dim3(kBS), lds, s, a);
+            else hipLaunchKernelGGL((k_pr_pull_units<true>), dim3(nw), dim3(kBS), lds, s, a);
         } else {
 #ifdef GX_PR_PROBES
             if (const char *pe = std::getenv("GX_PR_PROBE")) {
@@ -1654,9 +1658,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                 if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5, true>), dim3(nw), dim3(kBS), lds, s, a);
                 else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1, true>), dim3(nw), dim3(kBS), lds, s, a);
                 else hipLaunchKernelGGL((k_pr_pull_units<false, 0, 0, true>), dim3(nw), dim3(kBS), lds, s, a);
-            } else if (p->queue_on == 1 || (p->queue_on == -1 && nw >= 2u * (unsigned)std::max(1, p->ctx->num_cus))) {
+            } else if (use_queue) {
                 // one resident workgroup per CU (the LDS allows no second), never more than the items
-                const unsigned nq = std::min<unsigned>(nw, (unsigned)std::max(1, p->ctx->num_cus));
                 if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 5, false, true>), dim3(nq), dim3(kBS), lds, s, a);
                 else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1, false, true>), dim3(nq), dim3(kBS), lds, s, a);
                 else hipLaunchKernelGGL((k_pr_pull_units<false, 0, 0, false, true>), dim3(nq), dim3(kBS), lds, s, a);

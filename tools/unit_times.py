@@ -18,6 +18,10 @@ for path in sys.argv[1:]:
     dur = t1 - t0
     print(f"== {path}: {len(rows)} workgroups, span {us(t1.max() - base):.1f} us, "
           f"last start {us(t0.max() - base):.1f} us, median dur {us(np.median(dur)):.1f} us")
+    cus = 256
+    busy = [int((((t0 - base) <= t * 100) & ((t1 - base) > t * 100)).sum()) for t in range(0, int(us(t1.max() - base)), 10)]
+    print(f"   sum of item durations / {cus} CUs {us(dur.sum()) / cus:.1f} us (the balanced span); "
+          f"items in flight every 10 us: {busy}")
     u = kind == "unit"
     g = tg - t0
     rate = ents[u] / np.maximum(1, g[u])   # entries per 10 ns
