@@ -1076,12 +1076,14 @@ int env_int(const char *name, int dflt, int lo, int hi) {
 // picks the unit size on large graphs, so that the units of the large blocks land in as few
 // waves as the CUs allow.
 double pr_unit_makespan(const std::vector<int64_t> &ents, const std::vector<int64_t> &effs, const std::vector<int64_t> &rws,
-                        const std::vector<int64_t> &lsegs, int64_t t, int cus) {
+                        const std::vector<int64_t> &lsegs, int64_t t, int cus, bool by_cost) {
     constexpr double kRate = 2900.0, kRow = 0.002, kFixed = 1.5, kSlab = 0.0005;
     std::vector<double> cost;
     for (size_t i = 0; i < ents.size(); i++) {
         const int64_t E = ents[i];
-        const int64_t k = std::max<int64_t>(1, std::min((E + kRound - 1) / kRound, (E + t - 1) / t));
+        // units by cost, not entries: a block of mostly wide (sparse-tail) entries runs at about
+        // half the hub blocks' entry rate, so it is cut into more units (pr_unit_count)
+        const int64_t k = std::max<int64_t>(1, std::min((E + kRound - 1) / kRound, ((by_cost ? effs[i] : E) + t - 1) / t));
         const double c = (double)effs[i] / (double)k / kRate + kRow * (double)rws[i] + kFixed +
                          (k > 1 ? kSlab * (double)rws[i] * (double)k : 0.0);
         for (int64_t j = 0; j < k; j++) cost.push_back(c);
@@ -1401,6 +1403,8 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         const int64_t En = std::min<int64_t>(E, 256 * (int64_t)h_nsplit[i]);
         return En + (E - En) * wide_cost4 / 4;
     };
+    // huge graphs: units per block by weighted entries with GX_PR_UNIT_BY_COST=1 (default: by entries)
+    const bool unit_by_cost = huge && env_int("GX_PR_UNIT_BY_COST", 0, 0, 1) == 1;
     if (sortb.empty()) GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries above
     if (!sortb.empty()) {
         if (std::getenv("GX_PR_UNIT_NNZ")) {
@@ -1436,7 +1440,7 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
             for (int w = 0; w < nth; w++)
                 th.emplace_back([&, w]() {
                     for (size_t i = (size_t)w; i < cand.size(); i += (size_t)nth)
-                        span[i] = pr_unit_makespan(ents, effs, rws, lsegs, cand[i], (int)cus);
+                        span[i] = pr_unit_makespan(ents, effs, rws, lsegs, cand[i], (int)cus, unit_by_cost);
                 });
             for (auto &x : th) x.join();
             for (size_t i = 0; i < cand.size(); i++)
@@ -1456,7 +1460,10 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
             const RowBlock &b = sortb[i];
             const int64_t E = b.nz_end - b.nz_begin;
             const int64_t rounds = (E + kRound - 1) / kRound;
-            const int32_t k = (int32_t)std::max<int64_t>(1, std::min<int64_t>(rounds, (E + T - 1) / T));
+            // units per block: by weighted entries (eff_entries; = E unless the plan weights wide
+            // entries, GX_PR_WIDE_COST), as the simulation that picked T counts them
+            const int64_t Ek = unit_by_cost ? eff_entries((int64_t)i) : E;
+            const int32_t k = (int32_t)std::max<int64_t>(1, std::min<int64_t>(rounds, (Ek + T - 1) / T));
             const int64_t rows_b = b.row_end - b.row_begin;
             for (int32_t j = 0; j < k; j++) {
                 SortedUnit u;
