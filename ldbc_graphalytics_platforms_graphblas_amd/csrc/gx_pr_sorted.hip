@@ -22,9 +22,10 @@
 // scores agree with the row-order sum to ~1e-15 relative but are not bit-reproducible run to
 // run (the parity bar is 1e-12 relative, tests/test_gpu_parity.py).
 //
-// Each sorted block is cut into interleaved units (one workgroup each, LDS accumulators for
+// Each sorted block is cut into interleaved units (one work item each, LDS accumulators for
 // every row of the block); a multi-unit block's units combine through write-through slabs and
-// an arrival ticket.  Rows longer than `long_nnz` take the LONG path (a workgroup per
+// an arrival ticket.  Items run one workgroup each, or, on launches of >= 2 items per CU, from
+// a device work queue drained by one resident workgroup per CU (k_pr_pull_units QUEUE).  Rows longer than `long_nnz` take the LONG path (a workgroup per
 // 8192-entry segment, in row order); their workgroups come first.  A block without any entry
 // (isolated vertices: 29.5 % of SYN-7_5's rows) runs only the epilogue.  Its rows were also
 // tried as 64 Ki-row blocks at the end of the grid: a CU streams one such block's epilogue at
