@@ -1396,16 +1396,19 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     p->nunits = 0;
     // the cost of a block's entries in the unit order and the launch simulation: narrow ones 1,
     // wide (sparse-tail) ones GX_PR_WIDE_COST / 4 each, since their x lines are shared by fewer
-    // entries.  3 on large graphs (SYN-8_5 757-764 -> 755-756 us per launch, tools/r03_wc_ab.sh;
-    // the sparse tail units no longer finish last), 1 otherwise (SYN-7_5: no change)
-    const int64_t wide_cost4 = env_int("GX_PR_WIDE_COST", huge ? 12 : 4, 4, 64);
+    // entries.  On huge graphs 6, with the units cut by this cost (unit_by_cost below): SYN-8_5
+    // under the work queue 687 -> 630 us per launch (weight 4: 632, 8: 642; by entries with
+    // weight 6: 664; profiles/r04_pr_wide_cost_ab.txt).  Round 3, before the queue: 3 (757-764
+    // -> 755-756 us, tools/r03_wc_ab.sh).  1 otherwise (SYN-7_5: no change)
+    const int64_t wide_cost4 = env_int("GX_PR_WIDE_COST", huge ? 24 : 4, 4, 64);
     auto eff_entries = [&](int64_t i) -> int64_t {
         const int64_t E = sortb[i].nz_end - sortb[i].nz_begin;
         const int64_t En = std::min<int64_t>(E, 256 * (int64_t)h_nsplit[i]);
         return En + (E - En) * wide_cost4 / 4;
     };
-    // huge graphs: units per block by weighted entries with GX_PR_UNIT_BY_COST=1 (default: by entries)
-    const bool unit_by_cost = huge && env_int("GX_PR_UNIT_BY_COST", 0, 0, 1) == 1;
+    // huge graphs: units per block by weighted entries (GX_PR_UNIT_BY_COST=0: by entries), so a
+    // block of mostly wide entries, ~half the hub blocks' entry rate, is cut into more units
+    const bool unit_by_cost = huge && env_int("GX_PR_UNIT_BY_COST", 1, 0, 1) == 1;
     if (sortb.empty()) GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries above
     if (!sortb.empty()) {
         if (std::getenv("GX_PR_UNIT_NNZ")) {

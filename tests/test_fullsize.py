@@ -76,10 +76,11 @@ def test_pagerank_syn85(syn85):
     np.testing.assert_allclose(got, ref, rtol=PR_RTOL, atol=0)
 
 
-@pytest.mark.parametrize("env", [{"GX_PR_UNIT_BY_COST": "1"}, {"GX_PR_QUEUE": "0", "GX_PR_BLOCK_NNZ": "8388608"}])
+@pytest.mark.parametrize("env", [{"GX_PR_UNIT_BY_COST": "0", "GX_PR_WIDE_COST": "12"}, {"GX_PR_QUEUE": "0", "GX_PR_BLOCK_NNZ": "8388608"}])
 def test_pagerank_syn85_plan_knobs(syn85, monkeypatch, env):
     """The huge-graph plan knobs at full size on a fresh graph (the plan is cached per graph):
-    units cut by weighted entries, and the launch without the work queue on 8 Mi blocks."""
+    units cut by entries (the round-4 plan before the cost weighting), and the launch without
+    the work queue on 8 Mi blocks."""
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context, Graph, LA_PR
     for k, v in env.items():
         monkeypatch.setenv(k, v)
