@@ -284,9 +284,10 @@ int gx_pr_dist_p2p_attach(gx_pr_dist *dist, const uint8_t *handles);
 
 /* ---- one process, N GPUs (the executables' GX_NGPUS switch) ------------------------
  * gx_pagerank_multi: Graphalytics PageRank of the host CSR A on the ndev devices of `ctxs`
- * (one gx_ctx per distinct device).  The pull matrix (A' built on the host for a directed
- * graph) is 1-D row partitioned: the hub-first order is dealt round-robin over the devices
- * (gx_pr_partition), each device gets its rows with columns already in the exchange layout,
+ * (one gx_ctx per distinct device, or virtual devices: see gx_lcc_multi).  The pull matrix
+ * (A' built on each device for a directed graph) is 1-D row partitioned: the hub-first order is
+ * dealt round-robin over the devices (gx_pr_partition; each device derives it by the same
+ * device sort), each device gets its rows with columns already in the exchange layout,
  * and every iteration is one SpMV per device (k_pr_pull_units) plus one grouped in-process
  * RCCL all-gather (ncclCommInitAll over the devices, xGMI) of the live rows and dangling
  * slots.  rank[v] in A's vertex order.  Replaces LA_PR (pr.cpp:47-66) when bin/exe/pr runs with
@@ -307,6 +308,19 @@ int gx_pr_partition(uint64_t n, const uint64_t *rowptr, int nparts, uint32_t *or
  * by an in-process RCCL clique.  dist[v] in A's vertex order, +inf = unreached, bit-identical
  * to gx_sssp.  Replaces LA_SSSP (sssp.cpp:53-81) when it runs on several GPUs. */
 int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, uint64_t src, double *dist);
+/* gx_lcc_multi: LAGraph_lcc of the host CSR A on the ndev devices of `ctxs`, in one process
+ * (bin/exe/lcc with GX_NGPUS=N; BASELINE config 5, "LCC on cit-Patents, 1 -> 8 GPUs").  Every
+ * device holds A and its degree orientation and counts the triangles of a range of middle
+ * vertices balanced by probe work (gx_lcc_part_ranges); the n integer counters are summed onto
+ * the first device by one reduction (in-process RCCL ncclReduce).  lcc[v] in A's vertex order,
+ * bit-identical to gx_lcc.  Replaces LA_LCC (lcc.cpp:61-71) when it runs on several GPUs.
+ *
+ * Virtual devices: the three gx_*_multi calls also accept ndev >= 2 contexts that are ALL on
+ * one device (gx_init(d) called ndev times).  Each is then planned and run exactly as a
+ * separate GPU would be, and every collective becomes device-to-device copies (reduce: device
+ * adds) with the collective's ordering, so the N > 1 path runs, and is tested, on one GPU.
+ * Mixed layouts (some contexts sharing a device, some not) are GX_INVALID_VALUE. */
+int gx_lcc_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, double *lcc);
 
 /* ---------------------------------------------------------------------------------
  * Multi-GPU steps for the other algorithms.  The graph is replicated on

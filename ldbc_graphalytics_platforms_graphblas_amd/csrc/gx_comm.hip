@@ -50,6 +50,8 @@ struct Rccl {
     ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
                                hipStream_t) = nullptr;
     ncclResult_t (*comm_init_all)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
+                           hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
@@ -76,9 +78,10 @@ const Rccl &rccl() {
         r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
         r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
         r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+        r.reduce = reinterpret_cast<decltype(r.reduce)>(dlsym(h, "ncclReduce"));
         r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
         r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.error_string &&
-               r.comm_init_all && r.group_start && r.group_end;
+               r.comm_init_all && r.group_start && r.group_end && r.reduce;
         if (!r.ok) r.error = "librccl.so.1 lacks an expected entry point";
     });
     return r;
@@ -511,6 +514,9 @@ extern "C" int gx_pr_dist_run(gx_pr_dist *h, int iters, int use_graph, void *str
     if (iters < 1) return fail(GX_INVALID_VALUE, "gx_pr_dist_run: iters must be >= 1");
     PrDist &d = h->d;
     if (d.p2p && !d.attached) return fail(GX_INVALID_OBJECT, "gx_pr_dist_run: peer-to-peer runner not attached");
+    // a token is run * kTok + step with step <= iters: a longer run would raise tokens that
+    // satisfy the next run's waits early
+    if (d.p2p && (uint64_t)iters >= kTok - 1) return fail(GX_INVALID_VALUE, "gx_pr_dist_run: at most 2^24 - 2 iterations with the peer-to-peer exchange");
     GX_HIP_TRY(hipSetDevice(d.ctx->device));
     return d.run(iters, use_graph != 0, stream ? (hipStream_t)stream : d.ctx->stream);
 }
@@ -535,12 +541,141 @@ extern "C" int gx_pr_dist_scores(gx_pr_dist *h, int piece, double *scores) {
 
 namespace {
 
-// The in-process run of gx_pagerank_multi: one PrPart, stream and RCCL communicator per device
-// (ncclCommInitAll), every collective issued for all devices inside one group.
-struct MultiRun {
+// Adds src into dst (n words): the local reduction of Clique::reduce_sum_u64.
+__global__ __launch_bounds__(256) void k_add_u64(uint64_t *__restrict__ dst, const uint64_t *__restrict__ src, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) dst[i] += src[i];
+}
+
+bool one_device(gx_ctx *const *ctxs, int ndev) {
+    for (int d = 1; d < ndev; d++)
+        if (ctxs[d]->device != ctxs[0]->device) return false;
+    return true;
+}
+
+// The exchange among the ndev contexts of a one-process multi-device call (gx_*_multi).
+// Contexts on distinct devices form an in-process RCCL clique (ncclCommInitAll; xGMI between
+// MI355X GPUs), every collective issued for all devices inside one group.  Two or more
+// contexts that all sit on ONE device are virtual devices (bin/exe/* with GX_NGPUS=N and
+// GX_MULTI_SIM=1): the same call, partition and kernels per virtual device, with each
+// collective restated as device-to-device copies with its semantics -- every context's
+// stream waits for every sender before the copies, and for every receiver after them, so a
+// send buffer is never rewritten while a peer still reads it.  That runs the N > 1 code of
+// gx_pagerank_multi / gx_sssp_multi / gx_lcc_multi on a one-GPU box.
+// One context alone keeps a size-1 RCCL clique, so the RCCL path stays exercised there too.
+struct Clique {
     int ndev = 0;
     std::vector<gx_ctx *> ctx;
     std::vector<ncclComm_t> comm;
+    bool local = false;
+    std::vector<hipEvent_t> ev_in, ev_out;
+
+    ~Clique() {
+        for (int d = 0; d < ndev; d++) {
+            (void)hipSetDevice(ctx[d]->device);
+            (void)hipStreamSynchronize(ctx[d]->stream);
+        }
+        for (ncclComm_t c : comm)
+            if (c) (void)rccl().comm_destroy(c);
+        for (hipEvent_t e : ev_in) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_out) (void)hipEventDestroy(e);
+    }
+
+    int init(gx_ctx *const *ctxs, int n) {
+        ndev = n;
+        ctx.assign(ctxs, ctxs + n);
+        local = n > 1 && one_device(ctxs, n);
+        if (!local) {
+            std::vector<int> devs(n);
+            for (int d = 0; d < n; d++) devs[d] = ctxs[d]->device;
+            comm.assign(n, nullptr);
+            GX_NCCL_TRY("ncclCommInitAll", rccl().comm_init_all(comm.data(), n, devs.data()));
+            return GX_SUCCESS;
+        }
+        GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+        ev_in.assign(n, nullptr);
+        ev_out.assign(n, nullptr);
+        for (int d = 0; d < n; d++) {
+            GX_HIP_TRY(hipEventCreateWithFlags(&ev_in[d], hipEventDisableTiming));
+            GX_HIP_TRY(hipEventCreateWithFlags(&ev_out[d], hipEventDisableTiming));
+        }
+        return GX_SUCCESS;
+    }
+
+    hipStream_t st(int d) const { return ctx[d]->stream; }
+
+    // local mode: every stream waits for what every stream has enqueued so far
+    int fence_in() {
+        for (int e = 0; e < ndev; e++) GX_HIP_TRY(hipEventRecord(ev_in[e], st(e)));
+        for (int d = 0; d < ndev; d++)
+            for (int e = 0; e < ndev; e++)
+                if (e != d) GX_HIP_TRY(hipStreamWaitEvent(st(d), ev_in[e], 0));
+        return GX_SUCCESS;
+    }
+    int fence_out() {
+        for (int d = 0; d < ndev; d++) GX_HIP_TRY(hipEventRecord(ev_out[d], st(d)));
+        for (int e = 0; e < ndev; e++)
+            for (int d = 0; d < ndev; d++)
+                if (d != e) GX_HIP_TRY(hipStreamWaitEvent(st(e), ev_out[d], 0));
+        return GX_SUCCESS;
+    }
+
+    // recv(d)[e * bytes, (e + 1) * bytes) = send(e)[0, bytes) for every pair (ncclAllGather)
+    template <class S, class R>
+    int all_gather(S send, R recv, size_t bytes) {
+        if (local) {
+            GX_HIP_TRY(hipSetDevice(ctx[0]->device));
+            GX_TRY(fence_in());
+            for (int d = 0; d < ndev; d++)
+                for (int e = 0; e < ndev; e++)
+                    GX_HIP_TRY(hipMemcpyAsync(static_cast<char *>(recv(d)) + (size_t)e * bytes, send(e), bytes,
+                                              hipMemcpyDeviceToDevice, st(d)));
+            return fence_out();
+        }
+        const Rccl &r = rccl();
+        GX_NCCL_TRY("ncclGroupStart", r.group_start());
+        for (int d = 0; d < ndev; d++) {
+            const ncclResult_t e = r.all_gather(send(d), recv(d), bytes, ncclUint8, comm[d], st(d));
+            if (e != ncclSuccess) {
+                (void)r.group_end();
+                return rccl_fail("ncclAllGather", e);
+            }
+        }
+        GX_NCCL_TRY("ncclGroupEnd", r.group_end());
+        return GX_SUCCESS;
+    }
+
+    // buf(0)[i] = sum over d of buf(d)[i], i < count (ncclReduce, root 0, in place there); the
+    // other devices' buffers are left as they were in local mode, undefined under RCCL
+    template <class B>
+    int reduce_sum_u64(B buf, size_t count) {
+        if (local) {
+            GX_HIP_TRY(hipSetDevice(ctx[0]->device));
+            GX_TRY(fence_in());
+            for (int e = 1; e < ndev && count; e++) {
+                hipLaunchKernelGGL(k_add_u64, dim3(grid_for(count, 256, 8192)), dim3(256), 0, st(0), buf(0), buf(e),
+                                   (uint64_t)count);
+                GX_TRY(check_launch("k_add_u64"));
+            }
+            return fence_out();
+        }
+        const Rccl &r = rccl();
+        GX_NCCL_TRY("ncclGroupStart", r.group_start());
+        for (int d = 0; d < ndev; d++) {
+            const ncclResult_t e = r.reduce(buf(d), buf(d), count, ncclUint64, ncclSum, 0, comm[d], st(d));
+            if (e != ncclSuccess) {
+                (void)r.group_end();
+                return rccl_fail("ncclReduce", e);
+            }
+        }
+        GX_NCCL_TRY("ncclGroupEnd", r.group_end());
+        return GX_SUCCESS;
+    }
+};
+
+// The in-process run of gx_pagerank_multi: one PrPart and its vectors per device.
+struct MultiRun {
+    int ndev = 0;
+    std::vector<gx_ctx *> ctx;
     std::vector<PrPart *> part;
     std::vector<std::unique_ptr<DBuf<double>>> xr, xw, xl, ro;
     uint64_t chunk = 0;
@@ -550,8 +685,6 @@ struct MultiRun {
             (void)hipSetDevice(ctx[d]->device);
             (void)hipStreamSynchronize(ctx[d]->stream);
         }
-        for (ncclComm_t c : comm)
-            if (c) (void)rccl().comm_destroy(c);
         for (int d = 0; d < ndev; d++) {
             (void)hipSetDevice(ctx[d]->device);
             delete part[d];
@@ -561,31 +694,25 @@ struct MultiRun {
             ro[d].reset();
         }
     }
-
-    // every device's local chunk into every device's `dst` (the exchanged vector)
-    int gather(std::vector<std::unique_ptr<DBuf<double>>> &dst) {
-        const Rccl &r = rccl();
-        GX_NCCL_TRY("ncclGroupStart", r.group_start());
-        for (int d = 0; d < ndev; d++) {
-            const ncclResult_t e = r.all_gather(xl[d]->p, dst[d]->p, chunk, ncclFloat64, comm[d], ctx[d]->stream);
-            if (e != ncclSuccess) {
-                (void)r.group_end();
-                return rccl_fail("ncclAllGather", e);
-            }
-        }
-        GX_NCCL_TRY("ncclGroupEnd", r.group_end());
-        return GX_SUCCESS;
-    }
 };
 
 // Run fn(d) for every device on a host thread of its own (its device current, an equal share
 // of the host's OpenMP threads), so the devices' uploads and plans overlap; one device runs
-// inline.  The first failure's code and message come back on the calling thread.
+// inline.  Virtual devices (every context on one device) run one after the other on the
+// calling thread, each drained before the next: they share the device's grow-only sort and
+// plan scratch (gx_runtime.hip), which one host thread at a time may use.  The first
+// failure's code and message come back on the calling thread.
 template <class F>
 int per_device(gx_ctx *const *ctxs, int ndev, F fn) {
-    if (ndev == 1) {
-        GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
-        return fn(0);
+    if (ndev == 1 || one_device(ctxs, ndev)) {
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            const int rc = fn(d);
+            if (rc != GX_SUCCESS)
+                return ndev == 1 ? rc : fail(rc, "virtual device " + std::to_string(d) + ": " + gx_last_error());
+            GX_HIP_TRY(hipStreamSynchronize(ctxs[d]->stream));
+        }
+        return GX_SUCCESS;
     }
     std::vector<int> rc(ndev, GX_SUCCESS);
     std::vector<std::string> msg(ndev);
@@ -604,6 +731,8 @@ int per_device(gx_ctx *const *ctxs, int ndev, F fn) {
     return GX_SUCCESS;
 }
 
+// Contexts must be all on distinct devices (an RCCL clique) or all on one device (virtual
+// devices exchanging by copies); RCCL is required for the former and for one context.
 int check_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, const char *who) {
     if (!ctxs || !A || (A->nnz && !A->colidx) || !A->rowptr) return fail(GX_NULL_POINTER, std::string(who) + ": null argument");
     if (ndev < 1) return fail(GX_INVALID_VALUE, std::string(who) + ": ndev < 1");
@@ -611,8 +740,12 @@ int check_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, const char *who)
         if (!ctxs[d]) return fail(GX_NULL_POINTER, std::string(who) + ": null context");
     for (int d = 0; d < ndev; d++)
         for (int e = 0; e < d; e++)
+            if (ctxs[d] == ctxs[e]) return fail(GX_INVALID_VALUE, std::string(who) + ": a context passed twice");
+    if (ndev > 1 && one_device(ctxs, ndev)) return GX_SUCCESS;
+    for (int d = 0; d < ndev; d++)
+        for (int e = 0; e < d; e++)
             if (ctxs[d]->device == ctxs[e]->device)
-                return fail(GX_INVALID_VALUE, std::string(who) + ": one context per distinct device");
+                return fail(GX_INVALID_VALUE, std::string(who) + ": contexts must be on distinct devices, or all on one");
     const Rccl &r = rccl();
     if (!r.ok) return fail(GX_NOT_IMPLEMENTED, r.error);
     return GX_SUCCESS;
@@ -626,14 +759,6 @@ struct MultiGraphs {
         for (gx_graph *x : g) (void)gx_graph_free(x);
     }
 };
-
-int comm_init_all(gx_ctx *const *ctxs, int ndev, std::vector<ncclComm_t> &comm) {
-    std::vector<int> devs(ndev);
-    for (int d = 0; d < ndev; d++) devs[d] = ctxs[d]->device;
-    comm.assign(ndev, nullptr);
-    GX_NCCL_TRY("ncclCommInitAll", rccl().comm_init_all(comm.data(), ndev, devs.data()));
-    return GX_SUCCESS;
-}
 
 }  // namespace
 
@@ -652,7 +777,9 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     // interleaved hub-first partition (pr_partition.interleaved_relabel): hub-first position i
     // goes to device i % ndev as its local row i / ndev.  The vertices with out-edges come
     // first in that order, so device 0 holds the most live rows, ceil(nlive / ndev): the
-    // chunk every device exchanges (+ the zero padding slot and the dangling slot).
+    // chunk every device exchanges (+ the zero padding slot and the dangling slot).  The pull
+    // matrix of a directed graph is A', whose rows with out-edges in the PageRank sense are
+    // still A's rows with out-edges: liveness is A's out-degree either way.
     uint64_t nlive = 0;
     for (uint64_t v = 0; v < n; v++) nlive += A->rowptr[v + 1] != A->rowptr[v];
     MultiRun M;
@@ -688,13 +815,19 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         GX_HIP_TRY(hipMemsetAsync(M.xw[d]->p, 0, full * sizeof(double), s));
         return GX_SUCCESS;
     }));
-    GX_TRY(comm_init_all(ctxs, ndev, M.comm));
+    Clique C;
+    GX_TRY(C.init(ctxs, ndev));
+    const size_t cbytes = M.chunk * sizeof(double);
+    auto gather = [&](std::vector<std::unique_ptr<DBuf<double>>> &dst) {
+        return C.all_gather([&](int d) { return (const void *)M.xl[d]->p; }, [&](int d) { return (void *)dst[d]->p; },
+                            cbytes);
+    };
     // init, then per iteration: every device's SpMV, one grouped all-gather
     for (int d = 0; d < ndev; d++) {
         GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
         GX_TRY(pr_init(M.part[d], M.xl[d]->p, ctxs[d]->stream));
     }
-    GX_TRY(M.gather(M.xr));
+    GX_TRY(gather(M.xr));
     for (int it = 0; it < iters; it++) {
         const bool last = it == iters - 1;
         for (int d = 0; d < ndev; d++) {
@@ -702,7 +835,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
             GX_TRY(pr_step(M.part[d], M.xr[d]->p, M.xl[d]->p, last ? M.ro[d]->p : nullptr, ctxs[d]->stream));
         }
         if (last) break;
-        GX_TRY(M.gather(M.xw));
+        GX_TRY(gather(M.xw));
         std::swap(M.xr, M.xw);
     }
     // scores back in A's vertex order: device d's local row j is vertex order_d[j]
@@ -723,7 +856,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
 }
 
 // Multi-device SSSP in one process (bin/exe/sssp with GX_NGPUS; config 4's other half): the
-// 1-D split of gx_sssp_split on every device, the rounds exchanged by in-process RCCL.
+// 1-D split of gx_sssp_split on every device, the rounds exchanged by the clique.
 // Device d owns the targets [ranges[d], ranges[d+1]) (contiguous, ~nnz / ndev stored entries
 // each); per round: every device relaxes into its owned vertices, the 2-word counts
 // {pairs, done} are all-gathered and read by the host (the only host read of a round), then
@@ -753,14 +886,12 @@ extern "C" int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int
         DBuf<uint64_t> pairs, count, counts, all;
     };
     std::vector<Dev> D(ndev);
-    std::vector<ncclComm_t> comm;
     uint64_t *hc = nullptr;
     // released in this order on every exit: the splits and buffers on their devices, the
-    // communicators, the pinned words (the graphs go last, with G)
+    // pinned words (the clique is destroyed before, the graphs after, with G)
     struct Cleanup {
         gx_ctx *const *ctxs;
         std::vector<Dev> &D;
-        std::vector<ncclComm_t> &comm;
         uint64_t *&hc;
         ~Cleanup() {
             for (size_t d = 0; d < D.size(); d++) {
@@ -773,11 +904,9 @@ extern "C" int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int
                 D[d].counts.release();
                 D[d].all.release();
             }
-            for (ncclComm_t c : comm)
-                if (c) (void)rccl().comm_destroy(c);
             if (hc) (void)hipHostFree(hc);
         }
-    } cleanup{ctxs, D, comm, hc};
+    } cleanup{ctxs, D, hc};
     GX_TRY(per_device(ctxs, ndev, [&](int d) -> int {
         GX_TRY(gx_graph_create(ctxs[d], A, directed, &G.g[d]));
         GX_TRY(gx_sssp_split_create(G.g[d], ranges[d], ranges[d + 1], &D[d].sp));
@@ -787,29 +916,20 @@ extern "C" int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int
         GX_TRY(D[d].all.alloc(2 * maxown * (uint64_t)ndev));
         return GX_SUCCESS;
     }));
-    GX_TRY(comm_init_all(ctxs, ndev, comm));
+    Clique C;
+    GX_TRY(C.init(ctxs, ndev));
     GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
     GX_HIP_TRY(hipHostMalloc((void **)&hc, 2 * (size_t)ndev * sizeof(uint64_t), hipHostMallocDefault));
-    const Rccl &r = rccl();
-    auto gather = [&](auto send, auto recv, size_t words) -> int {
-        GX_NCCL_TRY("ncclGroupStart", r.group_start());
-        for (int d = 0; d < ndev; d++) {
-            const ncclResult_t e = r.all_gather(send(d), recv(d), words, ncclUint64, comm[d], ctxs[d]->stream);
-            if (e != ncclSuccess) {
-                (void)r.group_end();
-                return rccl_fail("ncclAllGather", e);
-            }
-        }
-        GX_NCCL_TRY("ncclGroupEnd", r.group_end());
-        return GX_SUCCESS;
-    };
-    for (int d = 0; d < ndev; d++) GX_TRY(gx_sssp_split_start(D[d].sp, src, ctxs[d]->stream));
+    for (int d = 0; d < ndev; d++) {
+        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+        GX_TRY(gx_sssp_split_start(D[d].sp, src, ctxs[d]->stream));
+    }
     for (uint64_t round = 0;; round++) {
         if (round > 4 * (n + 16)) return fail(GX_DEVICE_ERROR, "gx_sssp_multi: no fixed point");
         for (int d = 0; d < ndev; d++)
             GX_TRY(gx_sssp_split_relax(D[d].sp, D[d].pairs.p, D[d].count.p, ctxs[d]->stream));
-        GX_TRY(gather([&](int d) { return (const void *)D[d].count.p; }, [&](int d) { return (void *)D[d].counts.p; },
-                      2));
+        GX_TRY(C.all_gather([&](int d) { return (const void *)D[d].count.p; },
+                            [&](int d) { return (void *)D[d].counts.p; }, 2 * sizeof(uint64_t)));
         GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
         GX_HIP_TRY(hipMemcpyAsync(hc, D[0].counts.p, 2 * (size_t)ndev * sizeof(uint64_t), hipMemcpyDeviceToHost,
                                   ctxs[0]->stream));
@@ -821,11 +941,20 @@ extern "C" int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int
             m = std::max(m, hc[2 * d]);
         }
         if (ndone == ndev) break;
-        if (ndone) return fail(GX_DEVICE_ERROR, "gx_sssp_multi: devices disagree on termination");
+        if (ndone) {
+            // a device that stopped alone stopped on an error (a full settled list):
+            // report that cause rather than the disagreement it led to
+            for (int d = 0; d < ndev; d++)
+                if (hc[2 * d + 1]) {
+                    GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+                    GX_TRY(sssp_split_check(D[d].sp, ctxs[d]->stream));
+                }
+            return fail(GX_DEVICE_ERROR, "gx_sssp_multi: devices disagree on termination");
+        }
         if (m > maxown) return fail(GX_DEVICE_ERROR, "gx_sssp_multi: pair count beyond the owned range");
         if (m)
-            GX_TRY(gather([&](int d) { return (const void *)D[d].pairs.p; }, [&](int d) { return (void *)D[d].all.p; },
-                          2 * m));
+            GX_TRY(C.all_gather([&](int d) { return (const void *)D[d].pairs.p; },
+                                [&](int d) { return (void *)D[d].all.p; }, 2 * m * sizeof(uint64_t)));
         for (int d = 0; d < ndev; d++)
             GX_TRY(gx_sssp_split_apply(D[d].sp, m ? D[d].all.p : D[d].pairs.p, D[d].counts.p, ndev, m,
                                        ctxs[d]->stream));
@@ -837,6 +966,67 @@ extern "C" int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int
     GX_TRY(gx_sssp_split_distances(D[0].sp, out.p, ctxs[0]->stream));
     GX_HIP_TRY(hipStreamSynchronize(ctxs[0]->stream));
     GX_TRY(download(ctxs[0], dist, out.p, n, Xfer::Raw64));
+    return GX_SUCCESS;
+}
+
+// Multi-device LCC in one process (bin/exe/lcc with GX_NGPUS; BASELINE config 5, "LCC on
+// cit-Patents, 1 -> 8 GPUs"): A is replicated, every device builds the degree orientation
+// (gx_lcc_part_create) and counts the triangles whose middle vertex lies in its range of
+// orientation sources, the ranges balanced by the probe work sum |O(v)| over in-neighbours
+// (gx_lcc_part_ranges); the n triangle counters of all devices are summed onto device 0 by one
+// reduction, which divides by the closure degree there (gx_lcc_part_finish).  The counters are
+// integers, so the result is bit-identical to gx_lcc whatever the split.  Replaces LA_LCC
+// (lcc.cpp:61-71) when it runs on several GPUs.
+extern "C" int gx_lcc_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, double *lcc) {
+    GX_TRY(check_multi(ctxs, ndev, A, "gx_lcc_multi"));
+    if (!lcc) return fail(GX_NULL_POINTER, "gx_lcc_multi: null argument");
+    const uint64_t n = A->n;
+    if (n == 0) return GX_SUCCESS;
+    if (n >= (1ull << 29)) return fail(GX_NOT_IMPLEMENTED, "gx_lcc_multi: more than 2^29 vertices (packed oriented entries)");
+    MultiGraphs G;
+    G.g.assign(ndev, nullptr);
+    struct Dev {
+        gx_lcc_part *part = nullptr;
+        DBuf<uint64_t> tc;
+    };
+    std::vector<Dev> D(ndev);
+    struct Cleanup {
+        gx_ctx *const *ctxs;
+        std::vector<Dev> &D;
+        ~Cleanup() {
+            for (size_t d = 0; d < D.size(); d++) {
+                (void)hipSetDevice(ctxs[d]->device);
+                (void)hipStreamSynchronize(ctxs[d]->stream);
+                (void)gx_lcc_part_free(D[d].part);
+                D[d].part = nullptr;
+                D[d].tc.release();
+            }
+        }
+    } cleanup{ctxs, D};
+    GX_TRY(per_device(ctxs, ndev, [&](int d) -> int {
+        GX_TRY(gx_graph_create(ctxs[d], A, directed, &G.g[d]));
+        GX_TRY(gx_lcc_part_create(G.g[d], &D[d].part));
+        GX_TRY(D[d].tc.alloc(n));
+        return GX_SUCCESS;
+    }));
+    std::vector<uint64_t> ranges(ndev + 1);
+    GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+    GX_TRY(gx_lcc_part_ranges(D[0].part, ndev, ranges.data()));
+    GX_TRY(per_device(ctxs, ndev, [&](int d) -> int {
+        GX_HIP_TRY(hipMemsetAsync(D[d].tc.p, 0, n * sizeof(uint64_t), ctxs[d]->stream));
+        return gx_lcc_part_counts(D[d].part, ranges[d], ranges[d + 1], D[d].tc.p, ctxs[d]->stream);
+    }));
+    {
+        Clique C;
+        GX_TRY(C.init(ctxs, ndev));
+        GX_TRY(C.reduce_sum_u64([&](int d) { return D[d].tc.p; }, n));
+    }
+    GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+    DBuf<double> out;
+    GX_TRY(out.alloc(n));
+    GX_TRY(gx_lcc_part_finish(D[0].part, D[0].tc.p, out.p, ctxs[0]->stream));
+    GX_HIP_TRY(hipStreamSynchronize(ctxs[0]->stream));
+    GX_TRY(download(ctxs[0], lcc, out.p, n, Xfer::Raw64));
     return GX_SUCCESS;
 }
 

@@ -256,6 +256,10 @@ int plan_scratch(size_t bytes, void **p);
 int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,
                      int32_t *ci, hipStream_t s);
 
+// GX_OUT_OF_MEMORY when a split SSSP run stopped on a full settled list (gx_sssp_split.hip);
+// synchronises s.
+int sssp_split_check(gx_sssp_split *p, hipStream_t s);
+
 // Lazily build the transposed / closure CSR of a graph on the device.
 int ensure_transpose(gx_graph *g);
 int ensure_closure(gx_graph *g);

@@ -666,14 +666,17 @@ __device__ __forceinline__ void pull_item(const SortedArgs &a, const uint32_t w,
     stamp();
 }
 
-// The next work item for the whole workgroup.  Not inlined: inlined, the compiler turned the
-// thread-0 branch into the exit of an inner loop that the other lanes of wave 0 kept running
-// (barriers and all) while lane 0 waited to take the next item, and the launch never ended.
-__device__ __noinline__ uint32_t queue_fetch(uint32_t *q, uint32_t *slot) {
+// The next work item for the whole workgroup.  Thread 0 takes it from the counter; every
+// thread reads it back through readfirstlane, so the item is a scalar (SGPR) value and the
+// caller's `w >= total` loop exit is a uniform scalar branch by construction, whatever the
+// compiler inlines.  (Round 4 first read the slot as a per-lane VGPR value: inlined, the
+// compiler turned the thread-0 branch into the exit of an inner loop that the other lanes of
+// wave 0 kept running, barriers and all, and the launch never ended; a __noinline__ hid it.)
+__device__ __forceinline__ uint32_t queue_fetch(uint32_t *q, uint32_t *slot) {
     if (threadIdx.x == 0) *slot = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    const uint32_t w = *slot;
-    __syncthreads();   // every thread has read the slot before the next fetch rewrites it
+    const uint32_t w = __builtin_amdgcn_readfirstlane(*slot);
+    __syncthreads();   // every wave has read the slot before the next fetch rewrites it
     return w;
 }
 

@@ -51,8 +51,10 @@ extern "C" int gx_init(int device, gx_ctx **out) {
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+    // two staging buffers now; GX_UPLOAD_BUFS > 2 adds the others on first use (ADVICE r04:
+    // 64 MB of idle pinned memory per context otherwise)
     for (int i = 0; i < gx_ctx::kStageBufs && e == hipSuccess; i++) {
-        e = hipHostMalloc(&ctx->staging[i], gx_ctx::kStageBytes);
+        if (i < 2) e = hipHostMalloc(&ctx->staging[i], gx_ctx::kStageBytes);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming);
     }
     // warm the runtime's fill and copy paths (first use initialises them): outside the
@@ -280,6 +282,8 @@ int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool 
         return e ? std::atoi(e) : def;
     };
     const int nbuf = std::min(std::max(env_int("GX_UPLOAD_BUFS", 2), 2), gx_ctx::kStageBufs);
+    for (int b = 2; b < nbuf; b++)
+        if (!ctx->staging[b]) GX_HIP_TRY(hipHostMalloc(&ctx->staging[b], gx_ctx::kStageBytes));
     const int thr = env_int("GX_UPLOAD_THREADS", 0), saved_thr = host_threads();
     if (thr > 0) host_set_threads(thr);
     struct Restore {

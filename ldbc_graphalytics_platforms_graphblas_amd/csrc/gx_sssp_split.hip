@@ -1091,7 +1091,7 @@ extern "C" int gx_sssp_split_apply(gx_sssp_split *p, const uint64_t *pairs, cons
 }
 
 // Fails when the run stopped on a full settled list (SplitState::err) instead of finishing.
-static int split_check(gx_sssp_split *p, hipStream_t s) {
+int gx::sssp_split_check(gx_sssp_split *p, hipStream_t s) {
     int32_t err = 0;
     GX_HIP_TRY(hipMemcpyAsync(&err, &p->st.p->err, sizeof(err), hipMemcpyDeviceToHost, s));
     GX_HIP_TRY(hipStreamSynchronize(s));
@@ -1103,7 +1103,7 @@ extern "C" int gx_sssp_split_distances(gx_sssp_split *p, double *dist, void *str
     if (!p || !dist) return fail(GX_NULL_POINTER, "gx_sssp_split_distances: null argument");
     GX_HIP_TRY(hipSetDevice(p->g->ctx->device));
     hipStream_t s = split_stream(p, stream);
-    GX_TRY(split_check(p, s));
+    GX_TRY(sssp_split_check(p, s));
     const void *res = nullptr;
     GX_TRY(remap_out(p->g, p->dist.p, 8, s, &res));   // hub-first copy -> the caller's order
     GX_HIP_TRY(hipMemcpyAsync(dist, res, (size_t)p->n * 8, hipMemcpyDeviceToDevice, s));
@@ -1160,7 +1160,7 @@ extern "C" int gx_sssp_split_run(gx_sssp_split *p, uint64_t src, double *dist_ho
         for (int i = 0; i < std::min(h.round, 256); i++) std::fprintf(stderr, " %d", (int)h.modelog[i]);
         std::fprintf(stderr, "\n");
     }
-    GX_TRY(split_check(p, s));
+    GX_TRY(sssp_split_check(p, s));
     const void *res = nullptr;
     GX_TRY(remap_out(p->g, p->dist.p, 8, s, &res));   // hub-first copy -> the caller's order
     GX_HIP_TRY(hipStreamSynchronize(s));

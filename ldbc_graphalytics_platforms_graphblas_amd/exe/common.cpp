@@ -120,15 +120,20 @@ int Main(int argc, char **argv, Algorithm alg) {
         if (p.thread_num > 0) omp_set_num_threads((int)p.thread_num);
         int device = 0;
         if (const char *d = std::getenv("GX_DEVICE")) device = std::atoi(d);
-        // GX_NGPUS = N: PageRank and SSSP (BASELINE config 4) on devices [GX_DEVICE,
-        // GX_DEVICE + N) in this one process (gx_pagerank_multi / gx_sssp_multi: 1-D row
-        // partition, in-process RCCL all-gathers); execute-job.sh cannot pass new flags
-        // (execute-job.sh:68-151), so the backend comes from the environment.
+        // GX_NGPUS = N: PageRank, SSSP (BASELINE config 4) and LCC (config 5) on devices
+        // [GX_DEVICE, GX_DEVICE + N) in this one process (gx_pagerank_multi / gx_sssp_multi /
+        // gx_lcc_multi: 1-D partitions, in-process RCCL collectives); execute-job.sh cannot pass
+        // new flags (execute-job.sh:68-151), so the backend comes from the environment
+        // (SURVEY.md 8b).  GX_MULTI_SIM=1 puts the N contexts on device GX_DEVICE alone
+        // (virtual devices, collectives as device copies): the N > 1 path on a one-GPU box.
         // The other algorithms run on one GPU.
         int ngpus = 0;
         if (const char *g = std::getenv("GX_NGPUS")) ngpus = std::max(1, std::atoi(g));
-        if (ngpus && alg != Algorithm::PR && alg != Algorithm::SSSP)
-            std::cerr << "GX_NGPUS: only PageRank and SSSP run on several GPUs; this algorithm runs on device "
+        const char *sim_env = std::getenv("GX_MULTI_SIM");
+        const bool sim = sim_env && std::atoi(sim_env) != 0;
+        const bool multi_alg = alg == Algorithm::PR || alg == Algorithm::SSSP || alg == Algorithm::LCC;
+        if (ngpus && !multi_alg)
+            std::cerr << "GX_NGPUS: only PageRank, SSSP and LCC run on several GPUs; this algorithm runs on device "
                       << device << std::endl;
 
         CsrHolder A;
@@ -151,13 +156,15 @@ int Main(int argc, char **argv, Algorithm alg) {
 
         CtxHolder H;
         OK(gx_init(device, &H.ctx), "gx_init");
-        const bool multi = ngpus > 0 && (alg == Algorithm::PR || alg == Algorithm::SSSP);
+        const bool multi = ngpus > 0 && multi_alg;
         if (multi)
             for (int k = 1; k < ngpus; k++) {
                 gx_ctx *c = nullptr;
-                OK(gx_init(device + k, &c), "gx_init (GX_NGPUS)");
+                OK(gx_init(sim ? device : device + k, &c), "gx_init (GX_NGPUS)");
                 H.more.push_back(c);
             }
+        std::vector<gx_ctx *> ctxs{H.ctx};
+        ctxs.insert(ctxs.end(), H.more.begin(), H.more.end());
         // result arrays are not value-initialised: zero-filling SYN-8_5's 67 MB on one thread cost
         // ~10 ms inside the markers; libgx touches their pages in parallel while the device works
         std::unique_ptr<int64_t[]> level;
@@ -178,8 +185,6 @@ int Main(int argc, char **argv, Algorithm alg) {
             case Algorithm::PR:
                 vals.reset(new double[n]);
                 if (multi) {
-                    std::vector<gx_ctx *> ctxs{H.ctx};
-                    ctxs.insert(ctxs.end(), H.more.begin(), H.more.end());
                     OK(gx_pagerank_multi(ctxs.data(), ngpus, &A.csr, p.directed ? 1 : 0, p.damping_factor,
                                          p.max_iteration, vals.get()),
                        "gx_pagerank_multi");
@@ -190,8 +195,6 @@ int Main(int argc, char **argv, Algorithm alg) {
             case Algorithm::SSSP:
                 vals.reset(new double[n]);
                 if (multi) {
-                    std::vector<gx_ctx *> ctxs{H.ctx};
-                    ctxs.insert(ctxs.end(), H.more.begin(), H.more.end());
                     OK(gx_sssp_multi(ctxs.data(), ngpus, &A.csr, p.directed ? 1 : 0, src, vals.get()),
                        "gx_sssp_multi");
                 } else {
@@ -208,7 +211,10 @@ int Main(int argc, char **argv, Algorithm alg) {
                 break;
             case Algorithm::LCC:
                 vals.reset(new double[n]);
-                OK(gx_lcc(H.g, vals.get()), "gx_lcc");
+                if (multi)
+                    OK(gx_lcc_multi(ctxs.data(), ngpus, &A.csr, p.directed ? 1 : 0, vals.get()), "gx_lcc_multi");
+                else
+                    OK(gx_lcc(H.g, vals.get()), "gx_lcc");
                 break;
         }
         const auto t_end = GetCurrentMilliseconds();

@@ -479,3 +479,84 @@ def test_gx_sssp_multi_rejects_bad_arguments():
     assert N.lib().gx_sssp_multi(arr, 1, C.byref(s), 0, 0, N.as_dp(out)) != 0
     assert N.lib().gx_sssp_multi(None, 1, C.byref(s), 0, 0, N.as_dp(out)) != 0
     assert N.lib().gx_pagerank_multi(arr, 1, C.byref(s), 0, 0.85, 10, N.as_dp(out)) != 0
+
+
+def _multi_call(fn, ctxs, csr, *args):
+    """gx_<alg>_multi over the contexts `ctxs` (A.Context objects) -> result array."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    out = np.zeros(csr.n)
+    arr = (C.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+    s = csr.as_c()
+    N.check(getattr(N.lib(), fn)(arr, len(ctxs), C.byref(s), *args, N.as_dp(out)), fn)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [2, 3, 8])
+@pytest.mark.parametrize("undirected", [True, False])
+def test_multi_virtual_devices(k, undirected):
+    """The executables' N > 1 path on one GPU: k contexts on device 0 are k
+    virtual devices, each planned and run as its own GPU would be (pr_multi_plan's interleaved
+    rows and owner * chunk + local column map with the device transpose when directed; the SSSP
+    range cut; the LCC probe-work ranges), the collectives restated as device copies with their
+    ordering.  PageRank rtol 1e-12, SSSP and LCC bit-exact, against the oracle."""
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    ctxs = [Context(0) for _ in range(k)]
+    try:
+        for scale, ef in ((10, 8), (14, 16)):
+            csr = rmat(scale, ef, 5 + scale, undirected=undirected)
+            got = _multi_call("gx_pagerank_multi", ctxs, csr, int(not undirected), 0.85, 10)
+            np.testing.assert_allclose(got, O.pagerank(csr, not undirected, 0.85, 10), rtol=1e-12, atol=0)
+            assert np.array_equal(_multi_call("gx_lcc_multi", ctxs, csr, int(not undirected)),
+                                  O.lcc(csr, not undirected)), (k, scale)
+            wcsr = rmat(scale, ef, 7 + scale, undirected=undirected, weighted=True)
+            deg = np.diff(wcsr.rowptr.astype(np.int64))
+            for src in (int(np.argmax(deg)), int(np.flatnonzero(deg == 0)[0]) if (deg == 0).any() else 0):
+                got = _multi_call("gx_sssp_multi", ctxs, wcsr, int(not undirected), src)
+                assert np.array_equal(got, O.sssp(wcsr, src)), (k, scale, src)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.gpu
+def test_multi_virtual_devices_edge_cases():
+    """More virtual devices than rows with out-edges (some own nothing live), an edgeless graph,
+    and LCC on one device (a size-1 RCCL clique and its ncclReduce)."""
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import CSR
+    ctxs = [Context(0) for _ in range(8)]
+    try:
+        # a 5-vertex path 0-1-2 plus two isolated vertices, undirected and weighted
+        rp = np.array([0, 1, 3, 4, 4, 4], dtype=np.uint64)
+        ci = np.array([1, 0, 2, 1], dtype=np.uint64)
+        w = np.array([0.5, 0.5, 2.0, 2.0])
+        tiny = CSR(5, rp, ci, w)
+        got = _multi_call("gx_pagerank_multi", ctxs, tiny, 0, 0.85, 10)
+        np.testing.assert_allclose(got, O.pagerank(tiny, False, 0.85, 10), rtol=1e-12, atol=0)
+        assert np.array_equal(_multi_call("gx_sssp_multi", ctxs, tiny, 0, 2), O.sssp(tiny, 2))
+        assert np.array_equal(_multi_call("gx_lcc_multi", ctxs, tiny, 0), O.lcc(tiny, False))
+        empty = CSR(4, np.zeros(5, dtype=np.uint64), np.zeros(0, dtype=np.uint64), np.zeros(0))
+        np.testing.assert_allclose(_multi_call("gx_pagerank_multi", ctxs[:3], empty, 1, 0.85, 10),
+                                   O.pagerank(empty, True, 0.85, 10), rtol=1e-12, atol=0)
+        assert np.array_equal(_multi_call("gx_lcc_multi", ctxs[:3], empty, 1), np.zeros(4))
+        csr = rmat(12, 8, 31, undirected=False)
+        assert np.array_equal(_multi_call("gx_lcc_multi", ctxs[:1], csr, 1), O.lcc(csr, True))
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_multi_rejects_bad_contexts():
+    """gx_lcc_multi / gx_pagerank_multi refuse null contexts and ndev < 1 before any device
+    work (no GPU needed)."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    csr = rmat(6, 4, 1, undirected=True)
+    s = csr.as_c()
+    out = np.zeros(csr.n)
+    for fn, args in (("gx_lcc_multi", (0,)), ("gx_pagerank_multi", (0, 0.85, 10))):
+        arr = (C.c_void_p * 2)(None, None)
+        assert getattr(N.lib(), fn)(arr, 2, C.byref(s), *args, N.as_dp(out)) == -2   # GX_NULL_POINTER
+        assert getattr(N.lib(), fn)(arr, 0, C.byref(s), *args, N.as_dp(out)) == -3   # ndev < 1

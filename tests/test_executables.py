@@ -183,3 +183,38 @@ def test_sssp_executable_gx_ngpus(graph, tmp_path_factory, fixture_graphs):
     src = int(np.flatnonzero(g.mapping == np.uint64(g.param("sssp", "source-vertex")))[0])
     assert np.array_equal(got, O.sssp(g.csr, src))
     check_against_validation("SSSP", g.mapping, list(got), read_validation(FIXTURES / f"{graph}-SSSP"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,graph", [("pr", "example-directed"), ("pr", "test-pr-undirected"),
+                                       ("sssp", "example-undirected"), ("sssp", "test-sssp-directed"),
+                                       ("lcc", "example-directed"), ("lcc", "test-lcc-undirected"),
+                                       ("lcc", "example-undirected")])
+@pytest.mark.parametrize("ngpus", [1, 2, 3])
+def test_executable_gx_ngpus_virtual(alg, graph, ngpus, tmp_path_factory, fixture_graphs):
+    """bin/exe/{pr,sssp,lcc} with GX_NGPUS=N: N = 1 is a size-1 in-process RCCL clique, N > 1
+    runs N virtual devices on this box's one GPU (GX_MULTI_SIM=1), the same partition and
+    kernels an N-GPU node runs, with the collectives as device copies.  Against the oracle (PR
+    rtol 1e-12, SSSP and LCC bit-exact) and the Graphalytics rule of the validation file."""
+    import os
+    from oracle import oracle as O
+    d, g = load_dir(tmp_path_factory, graph, fixture_graphs)
+    out = d / f"out-{alg}-n{ngpus}"
+    env = dict(os.environ, GX_NGPUS=str(ngpus), GX_MULTI_SIM="1")
+    res = subprocess.run(job_argv(alg, d, out, g, d), capture_output=True, text=True, timeout=120, env=env)
+    assert res.returncode == 0, res.stderr
+    assert "GX_NGPUS" not in res.stderr
+    assert len(re.findall(r"Processing (starts|ends) at: \d+", res.stdout)) == 2
+    ids, vals = parse_output(out, alg)
+    np.testing.assert_array_equal(ids, g.mapping)
+    got = np.array([np.inf if v == "infinity" else float(v) for v in vals])
+    if alg == "pr":
+        want = O.pagerank(g.csr, g.directed, float(g.param("pr", "damping-factor")),
+                          int(g.param("pr", "num-iterations")))
+        np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
+    elif alg == "sssp":
+        src = int(np.flatnonzero(g.mapping == np.uint64(g.param("sssp", "source-vertex")))[0])
+        assert np.array_equal(got, O.sssp(g.csr, src))
+    else:
+        assert np.array_equal(got, O.lcc(g.csr, g.directed))
+    check_against_validation(alg.upper(), g.mapping, list(got), read_validation(FIXTURES / f"{graph}-{alg.upper()}"))

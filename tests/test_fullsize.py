@@ -201,3 +201,46 @@ def test_multi_paths_at_full_size(syn75, syn85):
     src = _maxdeg(csr)
     got = _multi("gx_sssp_multi", G.ctx.handle, csr, 0, src)
     assert np.array_equal(got, O.sssp_par(csr, src, 0.0, nthreads=O.max_threads()))
+
+
+def _multi_k(fn, k, csr, *args):
+    """gx_<alg>_multi on k virtual devices of this GPU (k contexts on device 0)."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    ctxs = [Context(0) for _ in range(k)]
+    try:
+        out = np.zeros(csr.n)
+        arr = (C.c_void_p * k)(*[c.handle.value for c in ctxs])
+        s = csr.as_c()
+        N.check(getattr(N.lib(), fn)(arr, k, C.byref(s), *args, N.as_dp(out)), fn)
+        return out
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_multi_virtual_devices_syn75_syncit(syn75, syncit):
+    """The N = 8 path of bin/exe/pr and bin/exe/lcc at config sizes, on 8 virtual devices of one
+    GPU: PageRank on SYN-7_5 (undirected) and on SYN-cit (directed: A'
+    on every device, the owner * chunk + local column map), LCC on SYN-cit (config 5's
+    stand-in; probe-work ranges, one reduction)."""
+    csr, _ = syn75
+    got = _multi_k("gx_pagerank_multi", 8, csr, 0, 0.85, 10)
+    np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, 10, nthreads=O.max_threads()), rtol=PR_RTOL, atol=0)
+    csr, _ = syncit
+    got = _multi_k("gx_pagerank_multi", 8, csr, 1, 0.85, 10)
+    np.testing.assert_allclose(got, O.pagerank(csr, True, 0.85, 10, nthreads=O.max_threads()), rtol=PR_RTOL, atol=0)
+    got = _multi_k("gx_lcc_multi", 8, csr, 1)
+    assert np.array_equal(got, O.lcc(csr, True, nthreads=O.max_threads()))
+
+
+def test_multi_virtual_devices_syn85(syn85):
+    """Config 4 (PageRank + SSSP on datagen-8_5-fb, 8 GPUs) through the executables' entry
+    points on 8 virtual devices: PageRank rtol 1e-12, SSSP bit-exact."""
+    csr, _ = syn85
+    src = _maxdeg(csr)
+    got = _multi_k("gx_sssp_multi", 8, csr, 0, src)
+    assert np.array_equal(got, O.sssp_par(csr, src, 0.0, nthreads=O.max_threads()))
+    got = _multi_k("gx_pagerank_multi", 8, csr, 0, 0.85, 10)
+    np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, 10, nthreads=O.max_threads()), rtol=PR_RTOL, atol=0)
