@@ -184,6 +184,7 @@ struct gx_graph {
     const int32_t *out_order = nullptr;
     gx::DBuf<uint64_t> remap_tmp;         // on a copy: n words of scratch for the remap
     int64_t live = 0;                     // on a copy: vertices of degree > 0 (a prefix of its ids)
+    bool rows_sorted = false;             // on a copy: every row sorted by (hub-first) column
     int sssp_calls = 0, wcc_calls = 0, hub_bfs_calls = 0;
 };
 
@@ -251,6 +252,10 @@ int sort_pairs_u64_u16(uint64_t *k_in, uint64_t *k_out, uint16_t *v_in, uint16_t
 // stable descending sort of (key, value) pairs, all 32 key bits
 int sort_pairs_desc_u32_i32(uint32_t *k_in, uint32_t *k_out, int32_t *v_in, int32_t *v_out, size_t m, hipStream_t s);
 int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s);
+// every row of (rp, ci_in) sorted by column into ci_out, weights (optional) alongside
+// (rocPRIM segmented radix sort on bits [0, end_bit)); n, nnz < 2^32
+int sort_rows_i32(const int64_t *rp, int64_t n, int64_t nnz, int32_t *ci_in, int32_t *ci_out, double *w_in,
+                  double *w_out, int end_bit, hipStream_t s);
 // grow-only device scratch of the current device, kept between calls (gx_runtime.hip)
 int plan_scratch(size_t bytes, void **p);
 int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, int64_t n, int64_t *rp,

@@ -666,14 +666,21 @@ __device__ __forceinline__ void pull_item(const SortedArgs &a, const uint32_t w,
     stamp();
 }
 
-// The next work item for the whole workgroup.  Thread 0 takes it from the counter; every
-// thread reads it back through readfirstlane, so the item is a scalar (SGPR) value and the
-// caller's `w >= total` loop exit is a uniform scalar branch by construction, whatever the
-// compiler inlines.  (Round 4 first read the slot as a per-lane VGPR value: inlined, the
-// compiler turned the thread-0 branch into the exit of an inner loop that the other lanes of
-// wave 0 kept running, barriers and all, and the launch never ended; a __noinline__ hid it.)
+// The next work item for the whole workgroup, with no divergent branch anywhere: wave 0 takes
+// it (a scalar branch: readfirstlane of the thread id) by an add in which lane 0 adds 1 and the
+// other lanes 0, so lane 0's return value is the item; readfirstlane makes it a scalar, which
+// wave 0 stores to LDS and every wave reads back through readfirstlane again.  The caller's
+// `w >= total` loop exit is therefore a uniform scalar branch.  Round 4's version took the item
+// under `threadIdx.x == 0`, a divergent branch: inlined, the compiler turned that branch into
+// the exit of an inner loop which the other lanes of wave 0 kept running, barriers and all,
+// while lane 0 waited to fetch, and the launch never ended (a __noinline__ hid it; reading the
+// slot through readfirstlane alone did not: the divergent branch was still there).
 __device__ __forceinline__ uint32_t queue_fetch(uint32_t *q, uint32_t *slot) {
-    if (threadIdx.x == 0) *slot = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < (uint32_t)kWave) {
+        const uint32_t v = __hip_atomic_fetch_add(q, (threadIdx.x & (kWave - 1)) == 0 ? 1u : 0u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        *slot = __builtin_amdgcn_readfirstlane(v);
+    }
     __syncthreads();
     const uint32_t w = __builtin_amdgcn_readfirstlane(*slot);
     __syncthreads();   // every wave has read the slot before the next fetch rewrites it

@@ -388,7 +388,7 @@ namespace gx {
 namespace {
 
 // Row i of the copy = row order[i] of the parent, columns renamed through perm (one wave per
-// row; row contents keep the parent's order).
+// row; row contents keep the parent's order until build_hub sorts them).
 __global__ __launch_bounds__(256) void k_hub_copy(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
                                                   const double *__restrict__ w, const int32_t *__restrict__ order,
                                                   const int32_t *__restrict__ perm, const int64_t *__restrict__ nrp,
@@ -456,6 +456,32 @@ int build_hub(gx_graph *g) {
                            g->A.ci.p, g->weighted ? g->A.w.p : nullptr, g->hub_order.p, g->hub_perm.p, c->A.rp.p, n,
                            c->A.ci.p, g->weighted ? c->A.w.p : nullptr);
         GX_TRY(check_launch("k_hub_copy"));
+        // rows sorted by their hub-first ids (GX_HUB_SORT=0 keeps the parent's entry order): a
+        // row's first entries are then its largest hubs.  Afforest's first sampling round alone
+        // (each vertex hooked to its first neighbour) then joins the giant component: on
+        // SYN-g500-22 2.40 M vertices under one root and 1 507 outside it, where the parent's
+        // order left 17 603 roots and a second round of 1.53 M hooks aimed at a few hot roots
+        // (115 K at the hottest; tools/wcc_round_model.py), which k_afforest_minhook served in
+        // series.  BFS bottom-up probes the hubs first for the same reason.
+        const char *se = std::getenv("GX_HUB_SORT");
+        if (!(se && std::atoi(se) == 0) && g->nnz) {
+            DBuf<int32_t> ci2;
+            DBuf<double> w2;
+            GX_TRY(ci2.alloc(g->nnz, 16));
+            if (g->weighted) GX_TRY(w2.alloc(g->nnz));
+            int bits = 1;
+            while ((1ll << bits) < n) bits++;
+            GX_TRY(sort_rows_i32(c->A.rp.p, n, (int64_t)g->nnz, c->A.ci.p, ci2.p, g->weighted ? c->A.w.p : nullptr,
+                                 g->weighted ? w2.p : nullptr, bits, s));
+            std::swap(c->A.ci.p, ci2.p);
+            std::swap(c->A.ci.n, ci2.n);
+            if (g->weighted) {
+                std::swap(c->A.w.p, w2.p);
+                std::swap(c->A.w.n, w2.n);
+            }
+            GX_HIP_TRY(hipStreamSynchronize(s));   // the unsorted buffers are freed at the end of the block
+            c->rows_sorted = true;
+        }
     }
     GX_HIP_TRY(hipStreamSynchronize(s));   // the host vectors die at return
     GX_TRY(c->remap_tmp.alloc(std::max<int64_t>(n, 1)));
@@ -691,6 +717,28 @@ int sort_pairs_u64_u32(uint64_t *k_in, uint64_t *k_out, uint32_t *v_in, uint32_t
 
 int sort_pairs_desc_u32_i32(uint32_t *k_in, uint32_t *k_out, int32_t *v_in, int32_t *v_out, size_t m, hipStream_t s) {
     return sort_pairs_kv(k_in, k_out, v_in, v_out, m, 32, true, s);
+}
+
+int sort_rows_i32(const int64_t *rp, int64_t n, int64_t nnz, int32_t *ci_in, int32_t *ci_out, double *w_in,
+                  double *w_out, int end_bit, hipStream_t s) {
+    if (!nnz || !n) return GX_SUCCESS;
+    if (nnz >= (1ll << 32) || n >= (1ll << 32)) return fail(GX_NOT_IMPLEMENTED, "sort_rows_i32: more than 2^32 entries");
+    size_t tmp_bytes = 0;
+    if (w_in)
+        GX_HIP_TRY(rocprim::segmented_radix_sort_pairs(nullptr, tmp_bytes, ci_in, ci_out, w_in, w_out, (unsigned)nnz,
+                                                       (unsigned)n, rp, rp + 1, 0, end_bit, s));
+    else
+        GX_HIP_TRY(rocprim::segmented_radix_sort_keys(nullptr, tmp_bytes, ci_in, ci_out, (unsigned)nnz, (unsigned)n, rp,
+                                                      rp + 1, 0, end_bit, s));
+    void *tmp = nullptr;
+    GX_TRY(rocprim_tmp(tmp_bytes, &tmp, s));
+    if (w_in)
+        GX_HIP_TRY(rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, ci_in, ci_out, w_in, w_out, (unsigned)nnz,
+                                                       (unsigned)n, rp, rp + 1, 0, end_bit, s));
+    else
+        GX_HIP_TRY(rocprim::segmented_radix_sort_keys(tmp, tmp_bytes, ci_in, ci_out, (unsigned)nnz, (unsigned)n, rp,
+                                                      rp + 1, 0, end_bit, s));
+    return rocprim_tmp_release(s);
 }
 
 int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s) {

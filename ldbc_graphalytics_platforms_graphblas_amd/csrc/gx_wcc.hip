@@ -231,10 +231,10 @@ __global__ void k_iota(int32_t *a, int64_t n) {
         a[v] = (int32_t)v;
 }
 
-// Afforest's two sampling rounds (each vertex with its first, then its second neighbour),
-// each followed by pointer jumping: round 0 by k_afforest_hook0/link0, round 1 by min-hook
-// passes before the CAS links (GX_WCC_HOOK0=0 / GX_WCC_MINHOOK=0: CAS links only).
-int afforest_sample(gx_graph *g, int32_t *parent, unsigned vgrid, hipStream_t s) {
+// Afforest's sampling rounds (each vertex with its first, then its second neighbour), each
+// followed by pointer jumping: round 0 by k_afforest_hook0/link0, round 1 by min-hook passes
+// before the CAS links (GX_WCC_HOOK0=0 / GX_WCC_MINHOOK=0: CAS links only).
+int afforest_sample(gx_graph *g, int32_t *parent, unsigned vgrid, int rounds, hipStream_t s) {
     gx_ctx *ctx = g->ctx;
     const int64_t n = (int64_t)g->n;
     // default on for undirected graphs only: on SYN-cit (directed, out-neighbours) the
@@ -242,7 +242,7 @@ int afforest_sample(gx_graph *g, int32_t *parent, unsigned vgrid, hipStream_t s)
     const bool und = !g->directed;
     const bool hook0 = std::getenv("GX_WCC_HOOK0") ? std::atoi(std::getenv("GX_WCC_HOOK0")) != 0 : und;
     const int minhook = std::getenv("GX_WCC_MINHOOK") ? std::atoi(std::getenv("GX_WCC_MINHOOK")) : (und ? 1 : 0);
-    for (int r = 0; r < 2; r++) {
+    for (int r = 0; r < rounds; r++) {
         for (int pass = 0; r > 0 && pass < minhook; pass++) {
             KTimer kt(ctx, "wcc_sample", s);
             hipLaunchKernelGGL(k_afforest_minhook, dim3(vgrid), dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, r,
@@ -332,8 +332,13 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
     const unsigned vgrid = grid_for(n, kWccBlock, 8192);
     if (!g->directed && nnz) {
         // ---- Afforest: sample two neighbours per vertex, find the giant component from
-        // 1024 sampled roots, then link only the remaining edges of the other vertices.
-        GX_TRY(afforest_sample(g, parent.p, vgrid, s));
+        // 1024 sampled roots, then link only the remaining edges of the other vertices.  On the
+        // hub-first copy with sorted rows one round suffices: every first neighbour is the
+        // vertex's largest hub, so that round already joins the giant component (build_hub,
+        // gx_runtime.hip); GX_WCC_ROUNDS overrides (1 or 2).
+        int rounds = g->rows_sorted ? 1 : 2;
+        if (const char *e = std::getenv("GX_WCC_ROUNDS")) rounds = std::max(1, std::min(2, std::atoi(e)));
+        GX_TRY(afforest_sample(g, parent.p, vgrid, rounds, s));
         // sample ids: a fixed hash sequence, uploaded once per graph size
         if (!g->wcc_ids.p || g->wcc_ids_n != n) {
             std::vector<int32_t> ids(kSamples);
@@ -354,7 +359,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         {
             KTimer kt(ctx, "wcc_hook", s);
             hipLaunchKernelGGL(k_afforest_finish, dim3(grid_for((uint64_t)n, kWccBlock, 8192)),
-                               dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, 2, giant_d, parent.p);
+                               dim3(kWccBlock), 0, s, g->A.rp.p, g->A.ci.p, n, rounds, giant_d, parent.p);
         }
         GX_TRY(check_launch("k_afforest_finish"));
         {
@@ -364,7 +369,7 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
         GX_TRY(check_launch("k_wcc_compress"));
     }
     if (g->directed && nnz) {
-        GX_TRY(afforest_sample(g, parent.p, vgrid, s));
+        GX_TRY(afforest_sample(g, parent.p, vgrid, 2, s));
         {
             KTimer kt(ctx, "wcc_hook", s);
             hipLaunchKernelGGL(k_wcc_link_edges,

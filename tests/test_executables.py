@@ -218,3 +218,44 @@ def test_executable_gx_ngpus_virtual(alg, graph, ngpus, tmp_path_factory, fixtur
     else:
         assert np.array_equal(got, O.lcc(g.csr, g.directed))
     check_against_validation(alg.upper(), g.mapping, list(got), read_validation(FIXTURES / f"{graph}-{alg.upper()}"))
+
+
+REF_EXECUTE_JOB = __import__("pathlib").Path("/root/reference/bin/sh/execute-job.sh")
+
+
+@pytest.mark.skipif(not REF_EXECUTE_JOB.exists(), reason="the reference checkout is not on this machine")
+@pytest.mark.parametrize("alg", ["bfs", "wcc", "pr", "cdlp", "lcc", "sssp"])
+def test_job_argv_matches_reference_execute_job(alg, tmp_path):
+    """job_argv() restates the COMMAND that execute-job.sh:68-139 builds; this pins it to the
+    script itself, run in place (not copied): a symlink to it under a temporary root makes its
+    rootdir (execute-job.sh:5) resolve there, where a stub bin/exe/<alg> records its argv.  The
+    script's quirks are covered: --num-threads becomes --threadnum, --job-id --jobid, and the
+    sssp lines without a trailing backslash (execute-job.sh:130, 135) still split into words."""
+    import os
+    (tmp_path / "bin" / "sh").mkdir(parents=True)
+    (tmp_path / "bin" / "exe").mkdir(parents=True)
+    os.symlink(REF_EXECUTE_JOB, tmp_path / "bin" / "sh" / "execute-job.sh")
+    log = tmp_path / "log"
+    log.mkdir()
+    stub = tmp_path / "bin" / "exe" / alg
+    stub.write_text('#!/bin/bash\nprintf "%s\\n" "$@" > "$(dirname "$0")/argv.txt"\n')
+    stub.chmod(0o755)
+    d, out = tmp_path / "graph", tmp_path / "out"
+
+    class G:   # the job's parameters, as Graphalytics passes them
+        directed = True
+
+        @staticmethod
+        def param(a, key):
+            return {"source-vertex": "6", "damping-factor": "0.85", "num-iterations": "10",
+                    "max-iterations": "10"}[key]
+
+    res = subprocess.run(["bash", str(tmp_path / "bin" / "sh" / "execute-job.sh"), "--job-id", "job-1",
+                          "--log-path", str(log), "--algorithm", alg, "--source-vertex", "6",
+                          "--max-iteration", "10", "--damping-factor", "0.85", "--input-dir", str(d),
+                          "--output-file", str(out), "--num-threads", "4", "--directed", "true"],
+                         capture_output=True, text=True, timeout=60)
+    assert res.returncode == 0, res.stderr
+    got = (tmp_path / "bin" / "exe" / "argv.txt").read_text().split("\n")[:-1]
+    want = job_argv(alg, d, out, G, log)
+    assert got == want[1:], (got, want)

@@ -534,16 +534,20 @@ def test_bfs_level_driver(ctx, monkeypatch, device):
         np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "BFS", source=s), O.bfs(csr, s))
 
 
-@pytest.mark.parametrize("hub", ["1", "2"])
-def test_hub_first_copy(ctx, monkeypatch, hub):
+@pytest.mark.parametrize("env", [{"GX_HUB": "1"}, {"GX_HUB": "2"}, {"GX_HUB": "2", "GX_HUB_SORT": "0"},
+                                 {"GX_HUB": "2", "GX_WCC_ROUNDS": "2"}])
+def test_hub_first_copy(ctx, monkeypatch, env):
     """BFS, WCC and SSSP on the hub-first relabelled copy of an undirected graph (built from
-    the second call on a graph, GX_HUB=1, or from the first, GX_HUB=2): results come back in
-    the caller's vertex order -- levels and distances gathered through the permutation, WCC
-    labels renamed to each component's smallest caller id -- on graphs with many components,
-    isolated vertices and unreachable ones, over three calls on one graph."""
+    the second call on a graph, GX_HUB=1, or from the first, GX_HUB=2; rows sorted by hub-first
+    id, or in the parent's order with GX_HUB_SORT=0; WCC with one sampling round on the sorted
+    copy, or two): results come back in the caller's vertex order -- levels and distances
+    gathered through the permutation, WCC labels renamed to each component's smallest caller
+    id -- on graphs with many components, isolated vertices and unreachable ones, over three
+    calls on one graph."""
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
-    monkeypatch.setenv("GX_HUB", hub)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     n = 30000
     perm = np.random.default_rng(11).permutation(n)
     keep = np.arange(n - 1) % 53 != 0
