@@ -1418,12 +1418,12 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     };
     // huge graphs: units per block by weighted entries (GX_PR_UNIT_BY_COST=0: by entries), so a
     // block of mostly wide entries, ~half the hub blocks' entry rate, is cut into more units
-    const bool unit_by_cost = huge && env_int("GX_PR_UNIT_BY_COST", 1, 0, 1) == 1;
+    const bool unit_by_cost = env_int("GX_PR_UNIT_BY_COST", huge ? 1 : 0, 0, 1) == 1;
     if (sortb.empty()) GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries above
     if (!sortb.empty()) {
         if (std::getenv("GX_PR_UNIT_NNZ")) {
             T = env_int("GX_PR_UNIT_NNZ", 65536, 1024, 1 << 30);
-        } else if (!huge) {
+        } else if (!huge && !env_int("GX_PR_UNIT_SIM", 0, 0, 1)) {
             // a quarter block: measured best on SYN-7_5 (256 Ki of 1 Mi: 100 us per launch;
             // 232 Ki: 130) and on its 1/8 partition (32 Ki of 128 Ki: 33.5 us; 24 Ki: 38.8;
             // 64 Ki: 47.7; tools/pr_piece_sweep.sh)
