@@ -265,6 +265,11 @@ int gx_pr_dist_scores(gx_pr_dist *dist, int piece, double *scores);
 int gx_pr_dist_free(gx_pr_dist *dist);
 
 /* ---- one-shot peer-to-peer exchange (no RCCL) -----
+ * EXPERIMENTAL: tested only with two processes sharing one GPU (IPC mappings on one device);
+ * the cross-device case (puts over xGMI into another GPU's coarse-grained memory, polled by the
+ * owner) has not run on a multi-GPU node yet -- tests/test_distributed.py::
+ * test_gpu_p2p_exchange_world2_two_devices is that check, skipped on a one-GPU box.  RCCL
+ * (gx_pr_dist_create) is the supported exchange. */
  * The same runner, but each exchange is direct: every rank writes its chunk into every
  * peer's exchanged vector (IPC-mapped over xGMI, one write per peer and piece, all links at
  * once) and raises an arrival flag there; the next SpMV waits for every rank's flag.
@@ -275,7 +280,10 @@ int gx_pr_dist_free(gx_pr_dist *dist);
  *                           of `handle`; NULL allowed for one rank); collective in effect,
  *                           required before gx_pr_dist_run.
  * A wait that never sees a peer's flag gives up after GX_P2P_POLLS polls (default 2^22,
- * seconds) and gx_pr_dist_scores then fails with GX_DEVICE_ERROR.
+ * seconds) and gx_pr_dist_scores then fails with GX_DEVICE_ERROR.  At most 2^24 - 2 iterations
+ * per run (tokens are run * 2^24 + step).  Before any rank calls gx_pr_dist_free, every rank must
+ * have stopped issuing runs and passed a barrier (e.g. MPI_Barrier after its last
+ * gx_pr_dist_scores): free unmaps this rank's vectors, which a peer's next run would write.
  * ------------------------------------------------------------------------------- */
 #define GX_P2P_HANDLE_BYTES 192
 int gx_pr_dist_create_p2p(int nranks, int rank, gx_pr_part *const *pieces, int npieces, uint8_t *handle,

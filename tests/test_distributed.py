@@ -306,19 +306,21 @@ def test_gpu_p2p_exchange_one_rank(pieces, use_graph, blocks, monkeypatch):
     ctx.close()
 
 
-def _p2p_worker(rank, world, port, q, pieces):
+def _p2p_worker(rank, world, port, q, pieces, own_device=False):
     """One rank of the peer-to-peer exchange; both ranks share GPU 0 (IPC between two
-    processes on one device), the handles travel over gloo."""
+    processes on one device), or rank r runs on GPU r (own_device: puts over xGMI into the
+    peer's memory); the handles travel over gloo."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
         from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import DevicePageRank, GpuStep
-        torch.cuda.set_device(0)
+        dev = rank if own_device else 0
+        torch.cuda.set_device(dev)
         csr = rmat(12, 16, 7)
         perm, hub, bounds = interleaved_relabel(csr, world * pieces)
         lrs = [slice_rows(hub, bounds, p * world + rank) for p in range(pieces)]
-        ctx = Context(0)
+        ctx = Context(dev)
         steps = [GpuStep(ctx, csr.n, world * pieces, lr, 0.85) for lr in lrs]
 
         def share_all(h):
@@ -326,7 +328,7 @@ def _p2p_worker(rank, world, port, q, pieces):
             dist.all_gather_object(box, h)
             return box
         dpr = DevicePageRank(steps, None, use_graph=True, p2p=(world, rank, share_all))
-        stream = torch.cuda.Stream(torch.device("cuda", 0))
+        stream = torch.cuda.Stream(torch.device("cuda", dev))
         results = []
         for iters in (6, 6, 4):   # replayed, then re-captured
             dpr.run(iters, stream.cuda_stream)
@@ -356,6 +358,33 @@ def test_gpu_p2p_exchange_world2_one_device(pieces):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_p2p_worker, args=(r, 2, port, q, pieces)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        results = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    csr = rmat(12, 16, 7)
+    for iters, got in results:
+        np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, iters), rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_p2p_exchange_world2_two_devices():
+    """The peer-to-peer exchange across devices: rank r on GPU r, the puts cross
+    xGMI into the peer's vectors and flags.  Skipped where fewer than two GPUs are visible."""
+    from ldbc_graphalytics_platforms_graphblas_amd import device_count
+    if device_count() < 2:
+        pytest.skip("needs two GPUs")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_p2p_worker, args=(r, 2, port, q, 1, True)) for r in range(2)]
     for p in procs:
         p.start()
     try:
