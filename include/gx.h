@@ -269,7 +269,7 @@ int gx_pr_dist_free(gx_pr_dist *dist);
  * the cross-device case (puts over xGMI into another GPU's coarse-grained memory, polled by the
  * owner) has not run on a multi-GPU node yet -- tests/test_distributed.py::
  * test_gpu_p2p_exchange_world2_two_devices is that check, skipped on a one-GPU box.  RCCL
- * (gx_pr_dist_create) is the supported exchange. */
+ * (gx_pr_dist_create) is the supported exchange.
  * The same runner, but each exchange is direct: every rank writes its chunk into every
  * peer's exchanged vector (IPC-mapped over xGMI, one write per peer and piece, all links at
  * once) and raises an arrival flag there; the next SpMV waits for every rank's flag.
