@@ -77,6 +77,8 @@ struct SsspState {
     int32_t pull;                 // heavy phase pulled by the unsettled vertices (k_sssp_pull)
     uint32_t pull_min;            // settled-list size from which the heavy phase is pulled
     unsigned long long smin;      // smallest distance on the settled list (pull bound)
+    int32_t bits_dirty;           // the settled bitmap holds a past pull's bits
+    int32_t clear_bits;           // this step's advance clears the bitmap (all workgroups)
     uint32_t ring_cnt[kRing];
 };
 
@@ -91,6 +93,8 @@ struct SsspBufs {
     int32_t *bstamp;              // bucket a vertex was last put into a ring slot for
     int32_t *ostamp;              // overflow epoch a vertex was last put on the overflow
     int32_t *sstamp;              // bucket a vertex was last put on the settled list for
+    uint32_t *sbits;              // pulled heavy phase: one bit per vertex on the settled list
+    uint32_t nbits;               // words of sbits
     uint64_t *q[2];               // near work items
     int32_t *ring;                // kRing slots of ring_cap vertices
     int32_t *ovf[2];
@@ -279,6 +283,7 @@ __global__ void k_sssp_plan(SsspState *st) {
         return;
     }
     const int32_t r = ++st->round;
+    st->clear_bits = 0;
     if (st->consume >= 0) {
         for (int j = 0; j < st->consume_n; j++) st->ring_cnt[(st->consume + j) % kRing] = 0;
         st->consume = -1;
@@ -286,13 +291,26 @@ __global__ void k_sssp_plan(SsspState *st) {
     const int qin = r & 1;
     st->qcnt[qin ^ 1] = 0;
     st->mode = 0;
-    if (st->qcnt[qin] > 0) return;
+    if (st->qcnt[qin] > 0) {
+        if (st->bits_dirty) {
+            st->clear_bits = 1;
+            st->bits_dirty = 0;
+        }
+        return;
+    }
     if (!st->heavy && st->settled_cnt > 0) {
         st->heavy = 1;
         st->mode = 3;
         st->pull = st->settled_cnt >= st->pull_min;
         st->smin = ~0ull;
+        if (st->pull) st->bits_dirty = 1;   // this step's advance sets the bits (cleared before, below)
         return;
+    }
+    // any later step's advance clears a pull's bits (never the advance that sets them: a pull
+    // is a mode-3 step, and the one after it is not)
+    if (st->bits_dirty) {
+        st->clear_bits = 1;
+        st->bits_dirty = 0;
     }
     st->heavy = 0;
     st->settled_cnt = 0;
@@ -344,6 +362,11 @@ __global__ void k_sssp_plan(SsspState *st) {
 // Ring / overflow entries whose edges were all relaxed at their current distance are dropped.
 __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     const SsspState *st = B.st;
+    if (st->clear_bits) {   // a past pull's settled bitmap, cleared by the whole grid
+        uint4 *w4 = reinterpret_cast<uint4 *>(B.sbits);
+        for (uint32_t i = blockIdx.x * kSsspBlock + threadIdx.x; i < B.nbits / 4; i += gridDim.x * kSsspBlock)
+            w4[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     const int mode = st->mode;
     if (mode == 0) return;
     const int32_t r = st->round;
@@ -403,6 +426,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
                 B.relaxed[v] = db;   // heavy edges now, light edges already relaxed at db
                 if (pull) {
                     mymin = min(mymin, db);
+                    atomicOr(&B.sbits[(uint32_t)v >> 5], 1u << (v & 31));
                 } else {
                     to_near = true;
                     nch = chunks_of(B.rp[v + 1] - B.lend[v]);
@@ -465,7 +489,7 @@ __device__ __forceinline__ void sssp_pull(const SsspBufs &B, Stage *stages, unsi
     constexpr int kSlots = 4;
     const SsspState *st = B.st;
     const int64_t cur = st->cur, lim = st->win_base + kRing;
-    const int32_t epoch = st->epoch, cur32 = (int32_t)cur;
+    const int32_t epoch = st->epoch;
     const unsigned long long bound = dbits(bitsd(st->smin) + B.delta);
     const uint64_t n = B.ring_cap;
     uint64_t *near_out = B.q[0];   // a pull never pushes near items
@@ -524,14 +548,17 @@ __device__ __forceinline__ void sssp_pull(const SsspBufs &B, Stage *stages, unsi
 #pragma unroll
             for (int q = 0; q < kSlots; q++) wk[q] = B.w[k[q]];
 #pragma unroll
-            for (int q = 0; q < kSlots; q++) ss[q] = B.sstamp[u[q]];
+            for (int q = 0; q < kSlots; q++) ss[q] = (int32_t)((B.sbits[(uint32_t)u[q] >> 5] >> (u[q] & 31)) & 1u);
+            // the settled sources' distances only: the 1 MB bitmap (SYN-8_5) stays in the XCD's L2
+            // where sstamp (32 MB) came from the Infinity Cache, and most in-edges of an
+            // unsettled vertex start at unsettled ones
 #pragma unroll
             for (int q = 0; q < kSlots; q++)
-                du[q] = __hip_atomic_load(&B.dist[u[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                du[q] = ss[q] ? __hip_atomic_load(&B.dist[u[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0ull;
 #pragma unroll
             for (int q = 0; q < kSlots; q++) {
                 c_edges += act[q];
-                if (act[q] && ss[q] == cur32) {
+                if (act[q] && ss[q]) {
                     c_try++;
                     const unsigned long long ndb = dbits(bitsd(du[q]) + wk[q]);
                     if (ndb < tdv[q]) atomicMin(&vmin[to[q]], ndb);
@@ -824,6 +851,8 @@ __global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t
         st->heavy = 0;
         st->pull = 0;
         st->pull_min = pull_min;
+        st->bits_dirty = 1;   // a past run may have left bits: the first advance clears them
+        st->clear_bits = 0;
         st->smin = ~0ull;
         st->slot = 0;
         st->nslots = 1;
@@ -961,9 +990,11 @@ int ensure_sssp_layout(gx_graph *g, double delta, hipStream_t s) {
 // arguments point into these buffers).  A run replays the graph, copying the done flag to
 // pinned memory after each replay while the next one is already queued.
 constexpr int kGraphSteps = 8;
+inline uint32_t nbit_words(int64_t n) { return (uint32_t)(((n + 31) / 32 + 3) / 4 * 4); }
 struct SsspWork {
     DBuf<unsigned long long> dist, relaxed;
     DBuf<int32_t> nstamp, bstamp, ostamp, sstamp, ring, ovf0, ovf1, settled;
+    DBuf<uint32_t> sbits;          // settled bitmap of a pulled heavy phase (padded to 4 words)
     DBuf<uint64_t> q0, q1;
     DBuf<SsspState> st;
     int32_t *h_done = nullptr;     // round, done of the state (pinned)
@@ -986,6 +1017,8 @@ struct SsspWork {
         GX_TRY(bstamp.alloc(n));
         GX_TRY(ostamp.alloc(n));
         GX_TRY(sstamp.alloc(n));
+        GX_TRY(sbits.alloc(nbit_words(n)));
+        GX_HIP_TRY(hipMemset(sbits.p, 0, nbit_words(n) * 4));
         GX_TRY(settled.alloc(n));
         GX_TRY(ring.alloc((uint64_t)n * kRing));
         GX_TRY(ovf0.alloc(n));
@@ -1108,7 +1141,8 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     auto &nstamp = W.nstamp, &bstamp = W.bstamp, &ostamp = W.ostamp, &sstamp = W.sstamp;
     auto &st = W.st;
     SsspBufs B{g->A.rp.p,   lay.lend.p,   lay.ci.p,      lay.w.p,    dist.p,       relaxed.p,  nstamp.p,
-               bstamp.p,    ostamp.p,     sstamp.p,      {W.q0.p, W.q1.p}, W.ring.p, {W.ovf0.p, W.ovf1.p},
+               bstamp.p,    ostamp.p,     sstamp.p,      W.sbits.p,  nbit_words(n), {W.q0.p, W.q1.p}, W.ring.p,
+               {W.ovf0.p, W.ovf1.p},
                W.settled.p, (uint64_t)n,  delta,         inv_delta,  st.p,         stats.p};
 
     hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nstamp.p,
