@@ -252,10 +252,6 @@ int sort_pairs_u64_u16(uint64_t *k_in, uint64_t *k_out, uint16_t *v_in, uint16_t
 // stable descending sort of (key, value) pairs, all 32 key bits
 int sort_pairs_desc_u32_i32(uint32_t *k_in, uint32_t *k_out, int32_t *v_in, int32_t *v_out, size_t m, hipStream_t s);
 int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s);
-// every segment [offsets[i] - offsets[0], offsets[i + 1] - offsets[0]) of the pairs sorted
-// by key bits [0, end_bit) (rocPRIM segmented radix sort; offsets on the device, nseg + 1)
-int sort_segments_u32_u16(uint32_t *k_in, uint32_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m,
-                          const int64_t *offsets, int64_t nseg, int end_bit, hipStream_t s);
 // every row of (rp, ci_in) sorted by column into ci_out, weights (optional) alongside
 // (rocPRIM segmented radix sort on bits [0, end_bit)); n, nnz < 2^32
 int sort_rows_i32(const int64_t *rp, int64_t n, int64_t nnz, int32_t *ci_in, int32_t *ci_out, double *w_in,

@@ -1299,12 +1299,9 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         // the key (SYN-8_5: 556 segments x 2^23 columns = 33 bits, two groups of 32-bit keys
         // instead of one sort of 64-bit keys)
         const bool narrow = colbits <= 31 && !env_int("GX_PR_WIDE_KEYS", 0, 0, 1);
-        // GX_PR_SEGSORT=1: column-only keys, one segmented sort of all segments (a segment is a
-        // contiguous entry range already: colbits key bits instead of colbits + segment bits)
-        const bool segsort = narrow && env_int("GX_PR_SEGSORT", 0, 0, 1);
-        const int gbits = segsort ? 0
-                          : narrow ? std::min({segbits, 32 - colbits, env_int("GX_PR_SORT_GROUP_BITS", 32, 1, 32)})
-                                   : segbits;
+        // (column-only keys and one rocPRIM segmented sort of the ~556 segments ran the plan's sort
+        // in 494 ms against 16 ms: it sorts a segment per workgroup; gpurun_out run m6, removed)
+        const int gbits = narrow ? std::min({segbits, 32 - colbits, env_int("GX_PR_SORT_GROUP_BITS", 32, 1, 32)}) : segbits;
         const KeySrc ks{p->rp, rows, p->src_rp, p->src_ci, p->src_order, p->src_perm, d_seg_row.p,
                         (int32_t)segd.size(), colbits, (int32_t)((1ll << gbits) - 1)};
         const int64_t nslabs = (int64_t)((nnz + kWave - 1) / kWave);
@@ -1339,25 +1336,11 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                                d_rowseg.p, k0, v0);
             GX_TRY(check_launch("k_sorted_keys"));
             clk.mark("keys");
-            if (segsort) {
-                // segments tile [segd[0].z0, segd.back().z1) in row order
-                std::vector<int64_t> offs(segd.size() + 1);
-                for (size_t g = 0; g < segd.size(); g++) offs[g] = segd[g].z0 - segd[0].z0;
-                offs[segd.size()] = segd.back().z1 - segd[0].z0;
-                DBuf<int64_t> d_offs;
-                GX_TRY(d_offs.alloc(offs.size()));
-                GX_HIP_TRY(hipMemcpyAsync(d_offs.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, s));
-                const int64_t z0 = segd[0].z0;
-                GX_TRY(sort_segments_u32_u16(k0 + z0, k1 + z0, v0 + z0, v1 + z0, (size_t)(offs.back()), d_offs.p,
-                                             (int64_t)segd.size(), colbits, s));
-                GX_HIP_TRY(hipStreamSynchronize(s));   // d_offs is freed at the end of the block
-            } else {
-                const size_t G = (size_t)1 << gbits;
-                for (size_t g0 = 0; g0 < segd.size(); g0 += G) {
-                    const size_t g1 = std::min(segd.size(), g0 + G) - 1;
-                    const int64_t z0 = segd[g0].z0, z1 = segd[g1].z1;
-                    GX_TRY(sort_pairs_u32_u16(k0 + z0, k1 + z0, v0 + z0, v1 + z0, (size_t)(z1 - z0), gbits + colbits, s));
-                }
+            const size_t G = (size_t)1 << gbits;
+            for (size_t g0 = 0; g0 < segd.size(); g0 += G) {
+                const size_t g1 = std::min(segd.size(), g0 + G) - 1;
+                const int64_t z0 = segd[g0].z0, z1 = segd[g1].z1;
+                GX_TRY(sort_pairs_u32_u16(k0 + z0, k1 + z0, v0 + z0, v1 + z0, (size_t)(z1 - z0), gbits + colbits, s));
             }
             clk.mark("sort");
             hipLaunchKernelGGL(k_sorted_pack<uint32_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, d_pch.p,

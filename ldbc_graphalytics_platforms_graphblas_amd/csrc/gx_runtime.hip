@@ -741,20 +741,6 @@ int sort_rows_i32(const int64_t *rp, int64_t n, int64_t nnz, int32_t *ci_in, int
     return rocprim_tmp_release(s);
 }
 
-int sort_segments_u32_u16(uint32_t *k_in, uint32_t *k_out, uint16_t *v_in, uint16_t *v_out, size_t m,
-                          const int64_t *offsets, int64_t nseg, int end_bit, hipStream_t s) {
-    if (!m || !nseg) return GX_SUCCESS;
-    if (m >= (1ull << 32)) return fail(GX_NOT_IMPLEMENTED, "sort_segments_u32_u16: more than 2^32 entries");
-    size_t tmp_bytes = 0;
-    GX_HIP_TRY(rocprim::segmented_radix_sort_pairs(nullptr, tmp_bytes, k_in, k_out, v_in, v_out, (unsigned)m, (unsigned)nseg,
-                                                   offsets, offsets + 1, 0, end_bit, s));
-    void *tmp = nullptr;
-    GX_TRY(rocprim_tmp(tmp_bytes, &tmp, s));
-    GX_HIP_TRY(rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (unsigned)m, (unsigned)nseg,
-                                                   offsets, offsets + 1, 0, end_bit, s));
-    return rocprim_tmp_release(s);
-}
-
 int scan_exclusive_i64(const int64_t *in, int64_t *out, size_t m, hipStream_t s) {
     if (!m) return GX_SUCCESS;
     size_t tmp_bytes = 0;

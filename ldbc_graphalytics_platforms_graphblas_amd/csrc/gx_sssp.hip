@@ -89,10 +89,10 @@ struct SsspBufs {
     const double *w;
     unsigned long long *dist;
     unsigned long long *relaxed;  // distance all edges of v were last relaxed with
-    int32_t *near_stamp;          // round a vertex was last queued as near
+    unsigned long long *nsw;      // (bucket a vertex was last put on the settled list for << 32) |
+                                  // round it was last queued as near: one word, one exchange
     int32_t *bstamp;              // bucket a vertex was last put into a ring slot for
     int32_t *ostamp;              // overflow epoch a vertex was last put on the overflow
-    int32_t *sstamp;              // bucket a vertex was last put on the settled list for
     uint32_t *sbits;              // pulled heavy phase: one bit per vertex on the settled list
     uint32_t nbits;               // words of sbits
     uint64_t *q[2];               // near work items
@@ -105,9 +105,8 @@ struct SsspBufs {
     unsigned long long *stats;    // GX_SSSP_VERBOSE work counters, else null
 };
 
-// First push of v under `tag`: a plain load filters repeats, the exchange settles races.
-__device__ __forceinline__ bool claim(int32_t *stamp, int32_t tag) {
-    return __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag && atomicExch(stamp, tag) != tag;
+__device__ __forceinline__ unsigned long long nsw_pack(int64_t bucket, int32_t round) {
+    return ((unsigned long long)(uint32_t)bucket << 32) | (uint32_t)round;
 }
 
 constexpr int kStatLanes = 256;
@@ -410,13 +409,14 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
         const uint32_t f = it * stride + blockIdx.x * kSsspBlock + threadIdx.x;
         bool to_near = false, to_ring = false, to_ovf = false, to_set = false;
         int32_t v = 0;
-        int slot = 0;
+        int slot = 0, fj = 0;
         uint32_t nch = 0;
         if (f < count) {
             if (fn > 1) {   // entry f of the fused slots' concatenation
                 uint32_t g = f;
                 int j = 0;
                 while (g >= fcnt[j]) g -= fcnt[j++];
+                fj = j;
                 v = B.ring[(uint64_t)((fslot + j) % kRing) * B.ring_cap + g];
             } else {
                 v = list[f];
@@ -436,9 +436,12 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
             } else if (mode == 1) {
                 // entries are unique within a slot (plain stores); a vertex can sit in two
                 // fused slots, so there the near stamp is claimed
-                if (fn == 1 || claim(&B.near_stamp[v], r)) {
-                    if (fn == 1) B.near_stamp[v] = r;
-                    B.sstamp[v] = (int32_t)cur;
+                // a vertex pushed to several buckets of a fused group has one live entry, in the
+                // slot of the bucket its bstamp names (later pushes only lower it): the others are
+                // skipped without the exchange a claim would cost (3.4 M of them when SYN-8_5's
+                // window opens whole)
+                if (fn == 1 || B.bstamp[v] == (int32_t)(cur - (fn - 1) + fj)) {
+                    B.nsw[v] = nsw_pack(cur, r);
                     to_near = to_set = true;
                     nch = chunks_of(B.lend[v] - B.rp[v]);
                 }
@@ -479,7 +482,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
 // pushing its heavy edges scans far more edges than can improve anything: nearly all of them
 // lead to vertices settled already.  Pulling skips every vertex whose distance is at most
 // fl(smin + delta), the smallest value a heavy relaxation from this bucket can produce, and
-// relaxes the heavy edges of the rest whose source is on the settled list (sstamp == cur),
+// relaxes the heavy edges of the rest whose source is on the settled list (its bit in sbits),
 // with the push's operands (dist[u] + w) and the push's strict-min test, so the distances
 // are bit-identical.  Lanes take 64 consecutive vertices and walk their concatenated heavy
 // edges as k_sssp_relax walks items; a vertex's candidates meet in an LDS min (its whole row
@@ -550,7 +553,7 @@ __device__ __forceinline__ void sssp_pull(const SsspBufs &B, Stage *stages, unsi
 #pragma unroll
             for (int q = 0; q < kSlots; q++) ss[q] = (int32_t)((B.sbits[(uint32_t)u[q] >> 5] >> (u[q] & 31)) & 1u);
             // the settled sources' distances only: the 1 MB bitmap (SYN-8_5) stays in the XCD's L2
-            // where sstamp (32 MB) came from the Infinity Cache, and most in-edges of an
+            // where a per-vertex stamp (32 MB) came from the Infinity Cache, and most in-edges of an
             // unsettled vertex start at unsettled ones
 #pragma unroll
             for (int q = 0; q < kSlots; q++)
@@ -575,13 +578,19 @@ __device__ __forceinline__ void sssp_pull(const SsspBufs &B, Stage *stages, unsi
             c_impr++;
             int64_t b = bucket_of(bitsd(m), B.inv_delta);
             if (b <= cur) b = cur + 1;
+            // v0 is this lane's alone in a pull (its candidates met in LDS), so no other lane
+            // pushes it in this launch: a plain test and store instead of a claim's exchange
             if (b < lim) {
-                if (claim(&B.bstamp[v0], (int32_t)b)) {
+                if (B.bstamp[v0] != (int32_t)b) {
+                    B.bstamp[v0] = (int32_t)b;
                     to_ring = true;
                     slot = (int)(b % kRing);
                 }
             } else {
-                if (claim(&B.ostamp[v0], epoch)) to_ovf = true;
+                if (B.ostamp[v0] != epoch) {
+                    B.ostamp[v0] = epoch;
+                    to_ovf = true;
+                }
                 mymin = min(mymin, (unsigned long long)b);
             }
         }
@@ -634,7 +643,7 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
     }
     if (count == 0) return;
     const int64_t cur = st->cur, lim = st->win_base + kRing;
-    const int32_t epoch = st->epoch, rn = r + 1, cur32 = (int32_t)cur;
+    const int32_t epoch = st->epoch, rn = r + 1;
     const uint64_t *near_in = B.q[qin];
     uint64_t *near_out = B.q[qin ^ 1];
     uint32_t *near_count = &B.st->qcnt[qin ^ 1];
@@ -711,13 +720,13 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
             // slot serialised up to 4 x 2 of them per lane.
             int cls[kSlots];       // 0 nothing, 1 near, 2 ring slot, 3 overflow
             int32_t tag[kSlots];
-            int32_t *stp[kSlots];
+            int32_t *stp[kSlots];  // ring slot / overflow stamp; near pushes claim nsw instead
             int slot[kSlots];
 #pragma unroll
             for (int q = 0; q < kSlots; q++) {
                 cls[q] = 0;
                 tag[q] = 0;
-                stp[q] = B.near_stamp;
+                stp[q] = B.bstamp;
                 slot[q] = 0;
                 c_edges += act[q];
                 if (act[q]) {
@@ -734,7 +743,6 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
                         if (heavy && b <= cur) b = cur + 1;
                         if (b <= cur) {
                             cls[q] = 1;
-                            stp[q] = B.near_stamp + v[q];
                             tag[q] = rn;
                         } else if (b < lim) {
                             cls[q] = 2;
@@ -750,37 +758,39 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
                     }
                 }
             }
-            // claim = a plain load that filters repeats, then the exchange that settles races
+            // claim = a plain load that filters repeats, then the exchange that settles races.  A
+            // near push claims its round and its bucket's settled-list entry in one 64-bit word
+            // (nsw): one exchange where two stamps took two
             int32_t seen[kSlots];
+            unsigned long long nseen[kSlots];
+            const unsigned long long ntag = nsw_pack(cur, rn);
 #pragma unroll
-            for (int q = 0; q < kSlots; q++)
-                seen[q] = cls[q] ? __hip_atomic_load(stp[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag[q];
+            for (int q = 0; q < kSlots; q++) {
+                nseen[q] = cls[q] == 1 ? __hip_atomic_load(&B.nsw[v[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ntag;
+                seen[q] = cls[q] > 1 ? __hip_atomic_load(stp[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag[q];
+            }
+            bool won[kSlots], to_set[kSlots];
 #pragma unroll
-            for (int q = 0; q < kSlots; q++)
-                if (seen[q] != tag[q]) seen[q] = atomicExch(stp[q], tag[q]);
-            bool won[kSlots];
+            for (int q = 0; q < kSlots; q++) {
+                to_set[q] = false;
+                if (cls[q] == 1) {
+                    if ((uint32_t)nseen[q] != (uint32_t)rn) nseen[q] = atomicExch(&B.nsw[v[q]], ntag);
+                    else nseen[q] = ntag;   // pushed this round already
+                } else if (seen[q] != tag[q]) {
+                    seen[q] = atomicExch(stp[q], tag[q]);
+                }
+            }
             int64_t rlo[kSlots], rhi[kSlots];
 #pragma unroll
             for (int q = 0; q < kSlots; q++) {
-                won[q] = cls[q] != 0 && seen[q] != tag[q];
+                won[q] = cls[q] == 1 ? (uint32_t)nseen[q] != (uint32_t)rn : cls[q] != 0 && seen[q] != tag[q];
+                // near pushes also join the settled list, once per bucket
+                to_set[q] = cls[q] == 1 && won[q] && (uint32_t)(nseen[q] >> 32) != (uint32_t)cur;
                 rlo[q] = rhi[q] = 0;
                 if (won[q] && cls[q] == 1) {
                     rlo[q] = B.rp[v[q]];
                     rhi[q] = B.lend[v[q]];
                 }
-            }
-            // near pushes also join the settled list, once per bucket
-            int32_t sset[kSlots];
-#pragma unroll
-            for (int q = 0; q < kSlots; q++)
-                sset[q] = (won[q] && cls[q] == 1)
-                              ? __hip_atomic_load(&B.sstamp[v[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : cur32;
-            bool to_set[kSlots];
-#pragma unroll
-            for (int q = 0; q < kSlots; q++) {
-                to_set[q] = false;
-                if (sset[q] != cur32) to_set[q] = atomicExch(&B.sstamp[v[q]], cur32) != cur32;
             }
 #pragma unroll
             for (int q = 0; q < kSlots; q++) {
@@ -817,16 +827,15 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
     }
 }
 
-__global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxed, int32_t *near_stamp,
-                            int32_t *bstamp, int32_t *ostamp, int32_t *sstamp, int64_t n) {
+__global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxed, unsigned long long *nsw,
+                            int32_t *bstamp, int32_t *ostamp, int64_t n) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
          v += (int64_t)gridDim.x * blockDim.x) {
         dist[v] = 0x7FF0000000000000ull;   // +infinity
         relaxed[v] = ~0ull;                // never equal to a distance
-        near_stamp[v] = -1;
+        nsw[v] = ~0ull;                    // round -1, bucket -1
         bstamp[v] = -1;
         ostamp[v] = 0;
-        sstamp[v] = -1;
     }
 }
 
@@ -837,8 +846,7 @@ __global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t
     if (threadIdx.x < kRing) st->ring_cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         B.dist[src] = 0ull;
-        B.near_stamp[src] = 0;
-        B.sstamp[src] = 0;
+        B.nsw[src] = nsw_pack(0, 0);
         B.settled[0] = src;
         st->settled_cnt = 1;
         st->cur = 0;
@@ -993,7 +1001,8 @@ constexpr int kGraphSteps = 8;
 inline uint32_t nbit_words(int64_t n) { return (uint32_t)(((n + 31) / 32 + 3) / 4 * 4); }
 struct SsspWork {
     DBuf<unsigned long long> dist, relaxed;
-    DBuf<int32_t> nstamp, bstamp, ostamp, sstamp, ring, ovf0, ovf1, settled;
+    DBuf<unsigned long long> nsw;
+    DBuf<int32_t> bstamp, ostamp, ring, ovf0, ovf1, settled;
     DBuf<uint32_t> sbits;          // settled bitmap of a pulled heavy phase (padded to 4 words)
     DBuf<uint64_t> q0, q1;
     DBuf<SsspState> st;
@@ -1013,10 +1022,9 @@ struct SsspWork {
     int alloc(int64_t n, uint64_t qcap) {
         GX_TRY(dist.alloc(n));
         GX_TRY(relaxed.alloc(n));
-        GX_TRY(nstamp.alloc(n));
+        GX_TRY(nsw.alloc(n));
         GX_TRY(bstamp.alloc(n));
         GX_TRY(ostamp.alloc(n));
-        GX_TRY(sstamp.alloc(n));
         GX_TRY(sbits.alloc(nbit_words(n)));
         GX_HIP_TRY(hipMemset(sbits.p, 0, nbit_words(n) * 4));
         GX_TRY(settled.alloc(n));
@@ -1138,15 +1146,16 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     }
     SsspWork &W = *static_cast<SsspWork *>(lay.work.get());
     auto &dist = W.dist, &relaxed = W.relaxed;
-    auto &nstamp = W.nstamp, &bstamp = W.bstamp, &ostamp = W.ostamp, &sstamp = W.sstamp;
+    auto &nsw = W.nsw;
+    auto &bstamp = W.bstamp, &ostamp = W.ostamp;
     auto &st = W.st;
-    SsspBufs B{g->A.rp.p,   lay.lend.p,   lay.ci.p,      lay.w.p,    dist.p,       relaxed.p,  nstamp.p,
-               bstamp.p,    ostamp.p,     sstamp.p,      W.sbits.p,  nbit_words(n), {W.q0.p, W.q1.p}, W.ring.p,
+    SsspBufs B{g->A.rp.p,   lay.lend.p,   lay.ci.p,      lay.w.p,    dist.p,       relaxed.p,  nsw.p,
+               bstamp.p,    ostamp.p,     W.sbits.p,     nbit_words(n), {W.q0.p, W.q1.p}, W.ring.p,
                {W.ovf0.p, W.ovf1.p},
                W.settled.p, (uint64_t)n,  delta,         inv_delta,  st.p,         stats.p};
 
-    hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nstamp.p,
-                       bstamp.p, ostamp.p, sstamp.p, n);
+    hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nsw.p,
+                       bstamp.p, ostamp.p, n);
     GX_TRY(check_launch("k_sssp_init"));
     // heavy phases whose settled list holds at least 1/GX_SSSP_PULL_FRAC (default 8) of the
     // non-isolated vertices are pulled (undirected graphs; GX_SSSP_PULL=0 never, 2 always).
