@@ -124,6 +124,13 @@ int gx_bfs(gx_graph *g, uint64_t src, int64_t *level);
  * LAGraph_Cached_AT (pr.cpp:58-61).  Graphalytics PR with dangling redistribution,
  * exactly `iters` iterations, fp64. */
 int gx_pagerank(gx_graph *g, double damping, int iters, double *rank);
+/* The whole of bin/exe/pr's processing (pr.cpp:77-79: LAGraph_New .. LAGr_PageRankGX between the
+ * markers) in one call: upload of the host CSR A, plan, iterations.  For an undirected graph the
+ * columns cross the host link chunk by chunk on a host thread while the device builds the plan
+ * from the row pointers and takes each chunk as it lands, and the weights (unused by PageRank) are
+ * not uploaded.  Same result as gx_graph_create + gx_pagerank + gx_graph_free (which directed
+ * graphs and GX_PR_FUSED=0 run); a column >= n fails with GX_INVALID_INDEX. */
+int gx_pagerank_csr(gx_ctx *ctx, const gx_csr *A, int directed, double damping, int iters, double *rank);
 
 /* Diagonal fill + LAGraph_Cached_EMin + LAGr_SingleSourceShortestPath(Delta = 2.5)
  * (sssp.cpp:53-81).  dist[v] fp64, +INFINITY when unreachable (printed `infinity`,

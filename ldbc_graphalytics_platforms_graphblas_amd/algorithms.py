@@ -111,6 +111,16 @@ def LA_PR(G: Graph, damping_factor: float, iteration_num: int) -> np.ndarray:
     return out
 
 
+def LA_PR_csr(ctx: Context, csr: CSR, directed: bool, damping_factor: float, iteration_num: int) -> np.ndarray:
+    """pr.cpp:77-79 as bin/exe/pr runs it: upload + plan + iterations in one call
+    (gx_pagerank_csr: the column upload overlapped with the plan)."""
+    out = np.empty(csr.n, dtype=np.float64)
+    s = csr.as_c()
+    N.check(N.lib().gx_pagerank_csr(ctx.handle, C.byref(s), int(directed), float(damping_factor), int(iteration_num),
+                                     N.as_dp(out)), "gx_pagerank_csr")
+    return out
+
+
 def LA_SSSP(G: Graph, source_vertex: int) -> np.ndarray:
     """sssp.cpp:53-81: fp64 distances, +inf for unreachable vertices."""
     out = np.empty(G.n, dtype=np.float64)

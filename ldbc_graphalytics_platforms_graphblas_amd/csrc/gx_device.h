@@ -13,8 +13,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <map>
+#include <thread>
 #include <memory>
 #include <string>
 #include <vector>
@@ -158,6 +160,28 @@ struct SsspLayout {
 };
 }  // namespace gx
 
+namespace gx {
+// An asynchronous column upload (gx_pagerank_csr, the executable's PageRank): a host thread
+// narrows and copies A's columns chunk by chunk on a stream of its own; chunk c's copy is done
+// once ev[c] fires, and `ready` counts the chunks whose copies (and events) are enqueued.  A
+// consumer waits for `ready` on the host, then for ev[c] on its own stream, so its kernels on
+// chunk c run while the later chunks are still crossing the host link.
+struct UploadJob {
+    hipStream_t us = nullptr;
+    std::vector<hipEvent_t> ev;
+    std::vector<int64_t> end;          // entry index just past chunk c
+    std::atomic<int> ready{0};
+    std::atomic<int> failed{0};
+    int rc = 0;
+    std::string msg;
+    std::thread th;
+    int device = 0;
+    ~UploadJob();
+    int wait_chunk(int c);             // host: chunk c's copy is enqueued (GX_SUCCESS), or the job failed
+    int join();                        // thread and stream finished; the job's error, if any
+};
+}  // namespace gx
+
 struct gx_graph {
     gx_ctx *ctx = nullptr;
     uint64_t n = 0, nnz = 0;
@@ -185,6 +209,7 @@ struct gx_graph {
     gx::DBuf<uint64_t> remap_tmp;         // on a copy: n words of scratch for the remap
     int64_t live = 0;                     // on a copy: vertices of degree > 0 (a prefix of its ids)
     bool rows_sorted = false;             // on a copy: every row sorted by (hub-first) column
+    std::shared_ptr<gx::UploadJob> job;   // columns still arriving (gx_pagerank_csr), else null
     int sssp_calls = 0, wcc_calls = 0, hub_bfs_calls = 0;
 };
 
@@ -264,6 +289,10 @@ int sort_keys_to_csr(DBuf<uint64_t> &keys, DBuf<uint64_t> &scratch, size_t m, in
 // GX_OUT_OF_MEMORY when a split SSSP run stopped on a full settled list (gx_sssp_split.hip);
 // synchronises s.
 int sssp_split_check(gx_sssp_split *p, hipStream_t s);
+
+// gx_pagerank_csr's graph: row pointers uploaded, the columns arriving through g->job (no
+// weights); every other use of g must g->job->join() first.
+int graph_create_async(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **out);
 
 // Lazily build the transposed / closure CSR of a graph on the device.
 int ensure_transpose(gx_graph *g);

@@ -177,6 +177,8 @@ struct PrPart {
     const int32_t *src_ci = nullptr;
     const int32_t *src_order = nullptr;
     const int32_t *src_perm = nullptr;
+    UploadJob *job = nullptr;  // the source columns still arriving (gx_pagerank_csr): the plan's key
+                               // pass scatters each chunk from the source order once it has landed
     DBuf<int32_t> order;       // hub-first position -> old vertex id (gx_pagerank)
     // single-GPU driver buffers (gx_pagerank): vertices relabelled hub-first
     DBuf<double> xa, xb, rank_out, result;

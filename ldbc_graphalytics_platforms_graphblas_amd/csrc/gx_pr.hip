@@ -769,6 +769,9 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     p->src_ci = P.ci.p;
     p->src_order = p->order.p;
     p->src_perm = p->perm.p;
+    // the columns still arriving (gx_pagerank_csr; undirected: the pull matrix is A itself): the
+    // plan's key pass takes them chunk by chunk as they land (pr_plan_sorted)
+    p->job = g->directed ? nullptr : g->job.get();
     if (have_runs)
         GX_TRY(pr_plan(p.get(), HostView<int64_t>(&runs, true), p->rp_own.p, nullptr, p->outdeg_own.p,
                        HostView<int32_t>(&runs, false)));
@@ -776,6 +779,7 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
         GX_TRY(pr_plan(p.get(), HostView<int64_t>(nrp.get(), n + 1), p->rp_own.p, nullptr, p->outdeg_own.p,
                        HostView<int32_t>(nout.get(), n)));
     GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors above die at return
+    p->job = nullptr;
     clk.mark("pr_plan");
     *out = p.release();
     return GX_SUCCESS;
@@ -870,8 +874,23 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
     GX_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     GX_TRY(device_begin(ctx));
+    // columns still arriving (gx_pagerank_csr): only the sorted single plan consumes them as they
+    // land; every other path waits for all of them
+    const char *ke = std::getenv("GX_PR_KERNEL");
+    if (g->job && (g->directed || g->pr || (ke && std::strcmp(ke, "adaptive") == 0))) {
+        GX_TRY(g->job->join());
+        g->job.reset();
+    }
     if (g->directed) GX_TRY(ensure_transpose(g));
-    if (!g->pr) GX_TRY(pr_single_plan(g, &g->pr));
+    if (!g->pr) {
+        const int rc = pr_single_plan(g, &g->pr);
+        if (g->job) {   // the plan has taken every chunk (or stopped early): the upload is over
+            const int jrc = g->job->join();
+            g->job.reset();
+            if (rc == GX_SUCCESS && jrc != GX_SUCCESS) return jrc;
+        }
+        if (rc != GX_SUCCESS) return rc;
+    }
     const auto t_plan = std::chrono::steady_clock::now();
     PrPart *p = g->pr;
     p->damping = damping;
@@ -905,6 +924,28 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
                      "result copy %.2f ms (device %.2f ms)\n", ms(t_entry, t_plan), ms(t_plan, t0), ms(t0, t1),
                      ms(t1, t2), ms(t2, clk::now()), ctx->last_device_ms);
     return GX_SUCCESS;
+}
+
+// The executable's PageRank (bin/exe/pr: pr.cpp:77-79 brackets LAGraph_New .. LAGr_PageRankGX
+// between its markers): upload + plan + iterations in one call.  For an undirected graph the
+// columns are uploaded by a host thread chunk by chunk while the plan builds the hub-first order
+// from the row pointers and then takes each chunk as it lands (graph_create_async,
+// pr_plan_sorted's source-side key pass), and the weights, which PageRank never reads, are not
+// uploaded at all.  Directed graphs (the plan needs A' whole) and GX_PR_FUSED=0 take
+// gx_graph_create + gx_pagerank.
+extern "C" int gx_pagerank_csr(gx_ctx *ctx, const gx_csr *A, int directed, double damping, int iters, double *rank) {
+    if (!ctx || !A || !rank) return fail(GX_NULL_POINTER, "gx_pagerank_csr: null argument");
+    if (iters < 0) return fail(GX_INVALID_VALUE, "gx_pagerank_csr: negative iteration count");
+    const char *fe = std::getenv("GX_PR_FUSED");
+    const bool fused = !directed && !(fe && std::atoi(fe) == 0);
+    gx_graph *g = nullptr;
+    if (fused) GX_TRY(graph_create_async(ctx, A, directed, &g));
+    else GX_TRY(gx_graph_create(ctx, A, directed, &g));
+    const int rc = gx_pagerank(g, damping, iters, rank);
+    std::string msg = rc != GX_SUCCESS ? gx_last_error() : "";
+    const int frc = gx_graph_free(g);   // joins an upload the call left running (an early error)
+    if (rc != GX_SUCCESS) return fail(rc, msg);
+    return frc;
 }
 
 // ---------------------------------------------------------------- row partition API

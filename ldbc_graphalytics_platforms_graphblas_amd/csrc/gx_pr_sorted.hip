@@ -34,6 +34,7 @@
 #include <functional>
 #include <queue>
 #include <thread>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -788,6 +789,35 @@ __global__ __launch_bounds__(256) void k_sorted_keys(KeySrc k, int64_t nnz, cons
     }
 }
 
+// The key pass from the source side (PrPart::job): the source entries [e0, e1) of one uploaded
+// chunk, one wave per 64-entry slab of the SOURCE CSR, lane = entry.  Source row u is local row
+// perm[u] (the single plan's hub-first relabelling: order and perm are inverse), so entry e of
+// row u lands at local position rp[perm[u]] + (e - srp[u]), the position the gather pass
+// (k_sorted_keys) gives it: the sort that follows sees the same keys in the same places.  Each
+// chunk runs as soon as its copy has landed, under the copies of the later chunks.
+template <typename K>
+__global__ __launch_bounds__(256) void k_scatter_keys(KeySrc k, int64_t n_src, const int64_t *__restrict__ ssrow,
+                                                      int64_t sl0, int64_t sl1, int64_t nnz,
+                                                      const int32_t *__restrict__ rowseg, K *__restrict__ keys,
+                                                      uint16_t *__restrict__ vals) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
+    const int64_t nslabs_src = (nnz + kWave - 1) / kWave;
+    for (int64_t sl = sl0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; sl < sl1; sl += nw) {
+        const int64_t e = sl * kWave + lane;
+        const int64_t ee = min(e, nnz - 1);
+        const int64_t u = slab_row_of(k.srp, ssrow, n_src, min(sl, nslabs_src - 1), ee, lane);
+        const int32_t i = k.perm[u];
+        const int32_t sg = rowseg[i];
+        const int64_t dst = k.rp[i] + (ee - k.srp[u]);
+        const uint32_t c = (uint32_t)k.perm[k.sci[ee]];
+        if (e < nnz) {
+            keys[dst] = ((K)(sg & k.segmask) << k.colbits) | (K)c;
+            vals[dst] = (uint16_t)(i - k.seg_row[sg]);
+        }
+    }
+}
+
 // sci / spk / gbase from the sorted (key, row) pairs: every entry's column into sci (the LONG
 // path and the escape supergroups read it), and for the sorted blocks (segments with gseg >= 0)
 // the packed entries and the base column of each 256-entry supergroup, aligned to the block's
@@ -1330,11 +1360,36 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         GX_TRY(plan_scratch(2 * kbytes + 2 * vbytes, reinterpret_cast<void **>(&scr)));
         uint16_t *v0 = reinterpret_cast<uint16_t *>(scr + 2 * kbytes), *v1 = reinterpret_cast<uint16_t *>(scr + 2 * kbytes + vbytes);
         clk.mark("key buffers");
+        // the key pass: over the local rows (gather), or chunk by chunk from the source side while
+        // the source columns are still being uploaded (PrPart::job, gx_pagerank_csr)
+        auto key_pass = [&](auto *kk) -> int {
+            using K = std::remove_pointer_t<decltype(kk)>;
+            if (!p->job) {
+                hipLaunchKernelGGL(k_sorted_keys<K>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs,
+                                   d_rowseg.p, kk, v0);
+                return check_launch("k_sorted_keys");
+            }
+            const int64_t n_src = (int64_t)p->n_global;
+            DBuf<int64_t> ssrow;
+            GX_TRY(ssrow.alloc(nslabs + 1));
+            GX_TRY(slab_rows(p->src_rp, n_src, nslabs, ssrow.p, s));
+            UploadJob *job = p->job;
+            for (size_t c = 0; c < job->ev.size(); c++) {
+                GX_TRY(job->wait_chunk((int)c));
+                GX_HIP_TRY(hipStreamWaitEvent(s, job->ev[c], 0));
+                const int64_t e0 = c ? job->end[c - 1] : 0, e1 = job->end[c];
+                const int64_t sl0 = e0 / kWave, sl1 = (e1 + kWave - 1) / kWave;   // chunks are 64-aligned
+                hipLaunchKernelGGL(k_scatter_keys<K>, dim3(grid_for((uint64_t)(sl1 - sl0) * kWave, 256, 4096)), dim3(256),
+                                   0, s, ks, n_src, ssrow.p, sl0, sl1, (int64_t)nnz, d_rowseg.p, kk, v0);
+                GX_TRY(check_launch("k_scatter_keys"));
+            }
+            GX_TRY(job->join());
+            GX_HIP_TRY(hipStreamSynchronize(s));   // ssrow is freed on return
+            return GX_SUCCESS;
+        };
         if (narrow) {
             uint32_t *k0 = reinterpret_cast<uint32_t *>(scr), *k1 = reinterpret_cast<uint32_t *>(scr + kbytes);
-            hipLaunchKernelGGL(k_sorted_keys<uint32_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs,
-                               d_rowseg.p, k0, v0);
-            GX_TRY(check_launch("k_sorted_keys"));
+            GX_TRY(key_pass(k0));
             clk.mark("keys");
             const size_t G = (size_t)1 << gbits;
             for (size_t g0 = 0; g0 < segd.size(); g0 += G) {
@@ -1347,9 +1402,7 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                                (int64_t)pch.size(), k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);
         } else {
             uint64_t *k0 = reinterpret_cast<uint64_t *>(scr), *k1 = reinterpret_cast<uint64_t *>(scr + kbytes);
-            hipLaunchKernelGGL(k_sorted_keys<uint64_t>, dim3(kgrid), dim3(256), 0, s, ks, (int64_t)nnz, srow.p, nslabs,
-                               d_rowseg.p, k0, v0);
-            GX_TRY(check_launch("k_sorted_keys"));
+            GX_TRY(key_pass(k0));
             GX_TRY(sort_pairs_u64_u16(k0, k1, v0, v1, (size_t)nnz, segbits + colbits, s));
             hipLaunchKernelGGL(k_sorted_pack<uint64_t>, dim3(pgrid), dim3(256), 0, s, d_segd.p, d_pch.p,
                                (int64_t)pch.size(), k1, v1, colmask, p->sci.p, p->spk.p, p->gbase.p);

@@ -267,10 +267,16 @@ namespace {
 // single-threaded conversion pass plus a pageable copy, which dominated the Graphalytics
 // processing time of the small-iteration algorithms.
 // fill(first, count, staging) writes `count` elements of `elem` bytes; false = bad input.
-template <class Fill>
-int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool *bad) {
+// On stream `us` (null: the context's); after(c) runs once chunk c's copy is enqueued; `sync`
+// waits for the last copy.
+struct NoAfter {
+    int operator()(int) const { return GX_SUCCESS; }
+};
+template <class Fill, class After = NoAfter>
+int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool *bad, hipStream_t us = nullptr,
+           After after = After(), bool sync = true) {
     const uint64_t chunk = gx_ctx::kStageBytes / elem;
-    hipStream_t s = ctx->stream;
+    hipStream_t s = us ? us : ctx->stream;
     *bad = false;
     int c = 0;
     static const bool times = [] {
@@ -311,8 +317,9 @@ int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool 
         t_fill += std::chrono::duration<double, std::milli>(tc - tb).count();
         GX_HIP_TRY(hipMemcpyAsync(dst + off * elem, ctx->staging[b], cnt * elem, hipMemcpyHostToDevice, s));
         GX_HIP_TRY(hipEventRecord(ctx->stage_ev[b], s));
+        GX_TRY(after(c));
     }
-    GX_HIP_TRY(hipStreamSynchronize(s));
+    if (sync) GX_HIP_TRY(hipStreamSynchronize(s));
     if (times)
         std::fprintf(stderr, "[upload] %llu x %zu B, %d buffers, %d threads: %8.2f ms (host fill %.2f ms, copy wait %.2f ms)\n",
                      (unsigned long long)count, elem, nbuf, host_threads(),
@@ -321,6 +328,105 @@ int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool 
 }
 
 }  // namespace
+}  // namespace gx
+
+namespace gx {
+
+UploadJob::~UploadJob() {
+    if (th.joinable()) th.join();
+    (void)hipSetDevice(device);
+    if (us) (void)hipStreamSynchronize(us);
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    if (us) (void)hipStreamDestroy(us);
+}
+
+int UploadJob::wait_chunk(int c) {
+    while (ready.load(std::memory_order_acquire) <= c) {
+        if (failed.load(std::memory_order_acquire)) return join();
+        std::this_thread::yield();
+    }
+    return GX_SUCCESS;
+}
+
+int UploadJob::join() {
+    if (th.joinable()) th.join();
+    if (us) GX_HIP_TRY(hipStreamSynchronize(us));
+    if (rc != GX_SUCCESS) return fail(rc, msg);
+    return GX_SUCCESS;
+}
+
+// The graph of gx_pagerank_csr: row pointers uploaded (and the context's stream drained), the
+// columns on their way (g->job); no weights (PageRank does not read them).
+int graph_create_async(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **out) {
+    *out = nullptr;
+    if (!A->rowptr || (A->nnz && !A->colidx)) return fail(GX_NULL_POINTER, "gx_pagerank_csr: null CSR arrays");
+    if (A->n >= (1ull << 31) - 64) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_csr: n >= 2^31 needs 64-bit column indices");
+    if (A->rowptr[0] != 0 || A->rowptr[A->n] != A->nnz)
+        return fail(GX_INVALID_VALUE, "gx_pagerank_csr: inconsistent row pointers");
+    if (!host_monotone(A->rowptr, A->n)) return fail(GX_INVALID_VALUE, "gx_pagerank_csr: row pointers not monotone");
+    GX_HIP_TRY(hipSetDevice(ctx->device));
+    const uint64_t n = A->n, nnz = A->nnz;
+    std::unique_ptr<gx_graph> g(new gx_graph());
+    g->ctx = ctx;
+    g->n = n;
+    g->nnz = nnz;
+    g->directed = directed != 0;
+    g->weighted = false;
+    g->A.n = n;
+    g->A.nnz = nnz;
+    GX_TRY(g->A.rp.alloc(n + 1));
+    GX_TRY(g->A.ci.alloc(nnz, 16));
+    bool bad = false;
+    GX_TRY(upload(ctx, reinterpret_cast<char *>(g->A.rp.p), n + 1, 8,
+                  [&](uint64_t off, uint64_t cnt, void *buf) {
+                      host_copy(buf, reinterpret_cast<const int64_t *>(A->rowptr) + off, cnt * 8);
+                      return true;
+                  }, &bad));
+    auto job = std::make_shared<UploadJob>();
+    job->device = ctx->device;
+    GX_HIP_TRY(hipStreamCreateWithFlags(&job->us, hipStreamNonBlocking));
+    const uint64_t chunk = gx_ctx::kStageBytes / 4;
+    for (uint64_t off = 0; off < nnz; off += chunk) {
+        hipEvent_t e = nullptr;
+        GX_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        job->ev.push_back(e);
+        job->end.push_back((int64_t)std::min(nnz, off + chunk));
+    }
+    const char *nt_env = std::getenv("GX_UPLOAD_NT");
+    const bool nt = !nt_env || std::atoi(nt_env) != 0;
+    UploadJob *j = job.get();
+    int32_t *dst = g->A.ci.p;
+    const uint64_t *cols = A->colidx;
+    const int nthreads = host_threads();
+    j->th = std::thread([ctx, j, dst, cols, n, nnz, nt, nthreads] {
+        host_set_threads(nthreads);
+        bool bad2 = false;
+        int rc = hipSetDevice(ctx->device) == hipSuccess ? GX_SUCCESS : fail(GX_DEVICE_ERROR, "hipSetDevice");
+        if (rc == GX_SUCCESS)
+            rc = upload(ctx, reinterpret_cast<char *>(dst), nnz, 4,
+                        [&](uint64_t off, uint64_t cnt, void *buf) {
+                            return host_narrow(cols + off, cnt, n, static_cast<int32_t *>(buf), nt);
+                        },
+                        &bad2, j->us,
+                        [&](int c) -> int {
+                            GX_HIP_TRY(hipEventRecord(j->ev[c], j->us));
+                            j->ready.store(c + 1, std::memory_order_release);
+                            return GX_SUCCESS;
+                        },
+                        false);
+        if (rc == GX_SUCCESS && bad2) rc = fail(GX_INVALID_INDEX, "gx_pagerank_csr: column out of range");
+        if (rc != GX_SUCCESS) {
+            j->rc = rc;
+            j->msg = gx_last_error();
+            j->failed.store(1, std::memory_order_release);
+        }
+    });
+    g->A.built = true;
+    g->job = job;
+    *out = g.release();
+    return GX_SUCCESS;
+}
+
 }  // namespace gx
 
 extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **out) {
@@ -376,6 +482,7 @@ extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_gr
 
 extern "C" int gx_graph_free(gx_graph *g) {
     if (!g) return GX_SUCCESS;
+    if (g->job) (void)g->job->join();
     (void)hipSetDevice(g->ctx->device);
     (void)hipStreamSynchronize(g->ctx->stream);
     delete g->pr;

@@ -596,3 +596,36 @@ def test_lcc_dense_core(ctx, monkeypatch, kmax):
         graphs.append(_G(csr_from_edges(n, src[keep], dst[keep], None, symmetric=not directed), directed))
     for g in graphs:
         np.testing.assert_array_equal(gpu_run(ctx, g, "LCC"), O.lcc(g.csr, g.directed))
+
+
+@pytest.mark.parametrize("env", [{}, {"GX_PR_FUSED": "0"}, {"GX_PLAN_TIMES": "1"}])
+def test_pagerank_csr_fused(ctx, monkeypatch, env):
+    """gx_pagerank_csr (bin/exe/pr's one call): the columns uploaded by a host thread while the
+    plan takes each 8 Mi-entry chunk as it lands, from the source side.  Against the oracle at
+    1e-12 on undirected graphs of one and of several chunks (scale 19: 16.6 M entries, 2 chunks),
+    a weighted one (weights not uploaded), a directed one (unfused path), an edgeless one."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import CSR
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    graphs = [(_rmat(12, 8, 5).csr, False), (_rmat(19, 16, 6).csr, False), (_rmat(13, 8, 7, weighted=True).csr, False),
+              (_rmat(12, 8, 8, undirected=False).csr, True),
+              (CSR(5, np.zeros(6, dtype=np.uint64), np.zeros(0, dtype=np.uint64), None), False)]
+    for csr, directed in graphs:
+        got = A.LA_PR_csr(ctx, csr, directed, 0.85, 10)
+        np.testing.assert_allclose(got, O.pagerank(csr, directed, 0.85, 10), rtol=PR_RTOL, atol=0)
+
+
+def test_pagerank_csr_rejects_bad_columns(ctx):
+    """A column >= n fails with GX_INVALID_INDEX (found by the upload thread, reported by the
+    call), with one chunk and with the bad entry in the second chunk, and the context stays
+    usable."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    for csr in (_rmat(12, 8, 5).csr, _rmat(19, 16, 6).csr):
+        bad = type(csr)(csr.n, csr.rowptr.copy(), csr.colidx.copy(), None)
+        bad.colidx[-3] = csr.n + 7
+        with pytest.raises(N.GxError):
+            A.LA_PR_csr(ctx, bad, False, 0.85, 10)
+        got = A.LA_PR_csr(ctx, csr, False, 0.85, 10)
+        np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, 10), rtol=PR_RTOL, atol=0)
