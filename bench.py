@@ -626,9 +626,11 @@ def exe_path_pr(csr, args, ctx):
     (gx_graph_create, whose upload rate is reported, then the first gx_pagerank, which plans) and
     a warm call of the API."""
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
     t0 = time.perf_counter()
-    r = A.LA_PR_csr(ctx, csr, False, args.damping, args.iters)
+    r, g = A.LA_PR_csr(ctx, csr, False, args.damping, args.iters, keep=True)
     t_fused = time.perf_counter() - t0
+    N.lib().gx_graph_free(g)   # after the end marker, as bin/exe/pr does
     t0 = time.perf_counter()
     G = A.Graph(ctx, csr, False)
     t_up = time.perf_counter() - t0

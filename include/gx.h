@@ -129,8 +129,11 @@ int gx_pagerank(gx_graph *g, double damping, int iters, double *rank);
  * columns cross the host link chunk by chunk on a host thread while the device builds the plan
  * from the row pointers and takes each chunk as it lands, and the weights (unused by PageRank) are
  * not uploaded.  Same result as gx_graph_create + gx_pagerank + gx_graph_free (which directed
- * graphs and GX_PR_FUSED=0 run); a column >= n fails with GX_INVALID_INDEX. */
-int gx_pagerank_csr(gx_ctx *ctx, const gx_csr *A, int directed, double damping, int iters, double *rank);
+ * graphs and GX_PR_FUSED=0 run); a column >= n fails with GX_INVALID_INDEX.  keep != NULL: the
+ * device graph (with its cached plan; its weights are absent) is handed to the caller, who
+ * frees it with gx_graph_free (bin/exe/pr does so after its end marker); NULL: freed here. */
+int gx_pagerank_csr(gx_ctx *ctx, const gx_csr *A, int directed, double damping, int iters, double *rank,
+                    gx_graph **keep);
 
 /* Diagonal fill + LAGraph_Cached_EMin + LAGr_SingleSourceShortestPath(Delta = 2.5)
  * (sssp.cpp:53-81).  dist[v] fp64, +INFINITY when unreachable (printed `infinity`,

@@ -111,14 +111,18 @@ def LA_PR(G: Graph, damping_factor: float, iteration_num: int) -> np.ndarray:
     return out
 
 
-def LA_PR_csr(ctx: Context, csr: CSR, directed: bool, damping_factor: float, iteration_num: int) -> np.ndarray:
+def LA_PR_csr(ctx: Context, csr: CSR, directed: bool, damping_factor: float, iteration_num: int,
+              keep: bool = False):
     """pr.cpp:77-79 as bin/exe/pr runs it: upload + plan + iterations in one call
-    (gx_pagerank_csr: the column upload overlapped with the plan)."""
+    (gx_pagerank_csr: the column upload overlapped with the plan).  keep=True returns
+    (scores, the device graph's handle) -- free it with gx_graph_free -- as bin/exe/pr keeps the
+    graph until after its end marker."""
     out = np.empty(csr.n, dtype=np.float64)
     s = csr.as_c()
+    g = C.c_void_p()
     N.check(N.lib().gx_pagerank_csr(ctx.handle, C.byref(s), int(directed), float(damping_factor), int(iteration_num),
-                                     N.as_dp(out)), "gx_pagerank_csr")
-    return out
+                                     N.as_dp(out), C.byref(g) if keep else None), "gx_pagerank_csr")
+    return (out, g) if keep else out
 
 
 def LA_SSSP(G: Graph, source_vertex: int) -> np.ndarray:

@@ -933,19 +933,27 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
 // pr_plan_sorted's source-side key pass), and the weights, which PageRank never reads, are not
 // uploaded at all.  Directed graphs (the plan needs A' whole) and GX_PR_FUSED=0 take
 // gx_graph_create + gx_pagerank.
-extern "C" int gx_pagerank_csr(gx_ctx *ctx, const gx_csr *A, int directed, double damping, int iters, double *rank) {
+extern "C" int gx_pagerank_csr(gx_ctx *ctx, const gx_csr *A, int directed, double damping, int iters, double *rank,
+                               gx_graph **keep) {
     if (!ctx || !A || !rank) return fail(GX_NULL_POINTER, "gx_pagerank_csr: null argument");
     if (iters < 0) return fail(GX_INVALID_VALUE, "gx_pagerank_csr: negative iteration count");
+    if (keep) *keep = nullptr;
     const char *fe = std::getenv("GX_PR_FUSED");
     const bool fused = !directed && !(fe && std::atoi(fe) == 0);
     gx_graph *g = nullptr;
     if (fused) GX_TRY(graph_create_async(ctx, A, directed, &g));
     else GX_TRY(gx_graph_create(ctx, A, directed, &g));
     const int rc = gx_pagerank(g, damping, iters, rank);
-    std::string msg = rc != GX_SUCCESS ? gx_last_error() : "";
-    const int frc = gx_graph_free(g);   // joins an upload the call left running (an early error)
-    if (rc != GX_SUCCESS) return fail(rc, msg);
-    return frc;
+    if (rc != GX_SUCCESS) {
+        const std::string msg = gx_last_error();
+        (void)gx_graph_free(g);   // joins an upload the call left running (an early error)
+        return fail(rc, msg);
+    }
+    // the graph and its plan (gigabytes of device memory) are the caller's to free, outside the
+    // processing time if it likes (bin/exe/pr frees after its end marker, as before)
+    if (keep) *keep = g;
+    else return gx_graph_free(g);
+    return GX_SUCCESS;
 }
 
 // ---------------------------------------------------------------- row partition API

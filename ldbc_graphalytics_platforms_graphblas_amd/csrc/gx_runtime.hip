@@ -397,7 +397,9 @@ int graph_create_async(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **ou
     UploadJob *j = job.get();
     int32_t *dst = g->A.ci.p;
     const uint64_t *cols = A->colidx;
-    const int nthreads = host_threads();
+    // one host thread fewer than the caller's: the calling thread plans meanwhile (with all of
+    // them narrowing, the plan's host steps ran 10x slower)
+    const int nthreads = std::max(1, host_threads() - 1);
     j->th = std::thread([ctx, j, dst, cols, n, nnz, nt, nthreads] {
         host_set_threads(nthreads);
         bool bad2 = false;

@@ -193,7 +193,7 @@ int Main(int argc, char **argv, Algorithm alg) {
                        "gx_pagerank_multi");
                 } else {
                     OK(gx_pagerank_csr(H.ctx, &A.csr, p.directed ? 1 : 0, p.damping_factor, p.max_iteration,
-                                       vals.get()),
+                                       vals.get(), &H.g),   // freed after the end marker
                        "gx_pagerank_csr");
                 }
                 break;
