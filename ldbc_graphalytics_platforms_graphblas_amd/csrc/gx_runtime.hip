@@ -397,9 +397,11 @@ int graph_create_async(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **ou
     UploadJob *j = job.get();
     int32_t *dst = g->A.ci.p;
     const uint64_t *cols = A->colidx;
-    // one host thread fewer than the caller's: the calling thread plans meanwhile (with all of
-    // them narrowing, the plan's host steps ran 10x slower)
-    const int nthreads = std::max(1, host_threads() - 1);
+    // half the caller's host threads (GX_UPLOAD_THREADS overrides): the calling thread plans
+    // meanwhile, and the host link, not the narrowing, bounds the upload (SYN-8_5: 28 ms of fill
+    // with 15 threads in 48 ms of copies); with every thread narrowing, the plan's host steps and
+    // small copies ran 10x slower
+    const int nthreads = std::max(1, host_threads() / 2);
     j->th = std::thread([ctx, j, dst, cols, n, nnz, nt, nthreads] {
         host_set_threads(nthreads);
         bool bad2 = false;
