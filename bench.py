@@ -486,6 +486,11 @@ def measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True):
     if partition == "ranges":
         perm, hub = hub_relabel(csr)
         bounds = partition_rows(hub.rowptr, vranks)
+    elif partition == "blocks":
+        # GX_PR_PARTITION=blocks: the whole-graph plan's blocks dealt whole (block_relabel); each
+        # rank's plan then cuts its rows as the whole graph's (GX_PR_HUGE=1 semantics)
+        from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import block_relabel
+        perm, hub, bounds = block_relabel(csr, vranks)
     else:
         perm, hub, bounds = interleaved_relabel(csr, vranks)
     lrs = [slice_rows(hub, bounds, p * world + rank) for p in range(pieces)]

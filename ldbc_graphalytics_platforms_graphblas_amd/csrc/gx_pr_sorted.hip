@@ -1162,7 +1162,9 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // graph500-22 267; SYN-8_5 1064-1070 (round 2, before X4).  Larger blocks cut the x line
     // requests (tools/pr_line_model.py) but give the last arriver more slabs per row.
     const double per_cu = std::max(1.0, (double)nnz / (double)cus);
-    const bool huge = per_cu > (double)(2 << 20);
+    // GX_PR_HUGE=1: the huge-graph plan whatever the size (a rank of a block partition,
+    // pr_partition.block_relabel, cuts its rows as the whole graph's plan does)
+    const bool huge = per_cu > (double)(2 << 20) || env_int("GX_PR_HUGE", 0, 0, 1) == 1;
     const int rmax = kMaxBlockRows;   // rows per block (LDS accumulators: 16 Ki rows = 128 KiB, the top 64 junk)
     p->sorted_rows = env_int("GX_PR_SORTED_ROWS", huge ? rmax : 4096, 64, rmax);
     // ... and at most 4x the power of two nearest nnz / CUs, so that a small partition (one rank

@@ -82,6 +82,49 @@ def interleaved_relabel(csr: CSR, nparts: int):
     return perm, out, bounds
 
 
+def block_relabel(csr: CSR, nparts: int, rows_per_block: int = 16320, block_nnz: int = 32 << 20):
+    """The single-GPU plan's sorted blocks dealt whole over `nparts` parts: the hub-first order
+    cut greedily into blocks of at most `rows_per_block` rows and `block_nnz` entries (as
+    pr_plan_sorted cuts a huge graph, gx_pr_sorted.hip), the blocks assigned largest first to the
+    part with the fewest entries (LPT), and each part's blocks kept in hub-first order as one
+    contiguous id range.  Unlike interleaved_relabel, whose parts hold every nparts-th hub-first
+    row (so a part's 16 Ki-row block spans nparts x as many hub positions and shares each x line
+    with nparts x fewer entries), every part's blocks are the whole-graph plan's own: the same
+    entries per gathered x line, 1/nparts of the blocks.  Rows without out-edges come last in
+    each part (the hub-first tail's blocks are the last ones of every part that gets them), so
+    live_rows holds.  Returns (perm, relabelled CSR, bounds) as interleaved_relabel."""
+    n = csr.n
+    deg = np.diff(csr.rowptr.astype(np.int64))
+    hub = np.argsort(-deg, kind="stable")
+    hdeg = deg[hub]
+    pre = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(hdeg, out=pre[1:])
+    starts = []
+    r = 0
+    while r < n:
+        lim = min(n, r + rows_per_block)
+        # the last row end within block_nnz of the block's start (at least one row)
+        e = int(np.searchsorted(pre, pre[r] + block_nnz, side="right")) - 1
+        e = max(r + 1, min(e, lim))
+        starts.append(r)
+        r = e
+    starts.append(n)
+    nb = len(starts) - 1
+    sizes = np.array([pre[starts[i + 1]] - pre[starts[i]] for i in range(nb)], dtype=np.int64)
+    load = np.zeros(nparts, dtype=np.int64)
+    owner = np.zeros(nb, dtype=np.int64)
+    for b in np.argsort(-sizes, kind="stable"):
+        p = int(np.argmin(load))
+        owner[b] = p
+        load[p] += sizes[b] + (starts[b + 1] - starts[b])   # entries + a row term (epilogue)
+    parts = [[hub[starts[b]:starts[b + 1]] for b in range(nb) if owner[b] == p] for p in range(nparts)]
+    deal = [np.concatenate(x) if x else np.zeros(0, dtype=np.int64) for x in parts]
+    bounds = np.zeros(nparts + 1, dtype=np.uint64)
+    bounds[1:] = np.cumsum([len(d) for d in deal])
+    perm, out = relabel(csr, np.concatenate(deal) if n else hub)
+    return perm, out, bounds
+
+
 def partition_rows(rowptr: np.ndarray, nranks: int) -> np.ndarray:
     """Row boundaries [0 = b0 <= b1 <= ... <= b_nranks = n] with ~nnz/nranks entries each."""
     rp = np.asarray(rowptr, dtype=np.int64)

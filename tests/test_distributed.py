@@ -18,7 +18,8 @@ import torch.multiprocessing as mp
 from conftest import ROOT  # noqa: F401  (sys.path)
 from ldbc_graphalytics_platforms_graphblas_amd.graphio import rmat
 from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import (PartitionedPageRank, hub_relabel,
-                                                                    interleaved_relabel, live_rows, local_pieces,
+                                                                    block_relabel, interleaved_relabel, live_rows,
+                                                                    local_pieces,
                                                                     local_rows, partition_rows, slice_rows)
 from oracle import oracle as O
 
@@ -79,8 +80,9 @@ def _worker(rank, world, port, q, pieces=1, layout="ranges"):
     try:
         csr = rmat(11, 8, 5)
         perm, hub = hub_relabel(csr)
-        if layout == "interleave":   # bench.py's default layout
-            perm, hub, bounds = interleaved_relabel(csr, world * pieces)
+        if layout in ("interleave", "blocks"):   # bench.py's default layout, or whole plan blocks
+            perm, hub, bounds = (interleaved_relabel(csr, world * pieces) if layout == "interleave"
+                                 else block_relabel(csr, world * pieces, rows_per_block=96, block_nnz=2048))
             lrs = [slice_rows(hub, bounds, p * world + rank) for p in range(pieces)]
             pr = PartitionedPageRank([CpuStep(csr.n, world * pieces, lr, 0.85) for lr in lrs], world,
                                      [lr.rows for lr in lrs], "cpu", all_gather=_gloo_gather_async)
@@ -143,6 +145,29 @@ def test_interleaved_relabel_balances_rows_and_entries():
     assert 8 * (ranges.max() + 1) > 3 * csr.n
 
 
+def test_block_relabel_deals_whole_blocks():
+    """block_relabel: every part's rows are whole blocks of the hub-first order (at most
+    rows_per_block rows and block_nnz entries each, a longer row alone), entries balanced within
+    the largest block, rows without out-edges last in every part, the relabelling isomorphic."""
+    for undirected, k in ((True, 2), (True, 8), (False, 3)):
+        csr = rmat(12, 8, 17, undirected=undirected)
+        deg = np.diff(csr.rowptr.astype(np.int64))
+        perm, g, b = block_relabel(csr, k, rows_per_block=200, block_nnz=4096)
+        b = b.astype(np.int64)
+        assert b[0] == 0 and b[-1] == csr.n and (np.diff(b) >= 0).all()
+        ent = np.array([int(g.rowptr[b[i + 1]]) - int(g.rowptr[b[i]]) for i in range(k)])
+        assert ent.sum() == csr.nnz
+        # the largest block bounds the imbalance (LPT over entries + rows)
+        gdeg = np.diff(g.rowptr.astype(np.int64))
+        assert ent.max() - ent.min() <= max(4096, int(gdeg.max())) + 200
+        assert live_rows(g, b) is not None
+        # isomorphic: row perm[v] of g is row v of csr with renamed columns
+        for v in (0, 1, int(np.argmax(deg)), csr.n - 1):
+            a = np.sort(perm[csr.colidx[csr.rowptr[v]:csr.rowptr[v + 1]].astype(np.int64)])
+            r = perm[v]
+            assert np.array_equal(np.sort(g.colidx[g.rowptr[r]:g.rowptr[r + 1]].astype(np.int64)), a)
+
+
 def test_live_rows_prefix_and_exchange_size():
     """Hub-first layouts keep every part's rows without out-edges last, so only the leading
     live rows are exchanged: the padded exchange is ~(vertices with out-edges) doubles."""
@@ -187,7 +212,8 @@ def test_hub_relabel_is_isomorphic():
     np.testing.assert_allclose(a, b, rtol=1e-12)
 
 
-@pytest.mark.parametrize("pieces,layout", [(1, "ranges"), (2, "ranges"), (1, "interleave"), (2, "interleave")])
+@pytest.mark.parametrize("pieces,layout", [(1, "ranges"), (2, "ranges"), (1, "interleave"), (2, "interleave"),
+                                           (1, "blocks"), (2, "blocks")])
 def test_gloo_world2_matches_oracle(pieces, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -241,6 +267,30 @@ def test_gpu_partition_api_simulated_ranks(nranks, live):
         s.close()
     ctx.close()
     np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, iters), rtol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pieces", [2, 8])
+def test_gpu_block_partition_pieces(pieces, monkeypatch):
+    """The block partition (bench.py GX_PR_PARTITION=blocks): the whole-graph plan's blocks
+    dealt whole over `pieces` virtual ranks, each planned as a huge graph (GX_PR_HUGE=1), run by
+    the device-driven runner with device copies; against the oracle."""
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import DevicePageRank, GpuStep
+    monkeypatch.setenv("GX_PR_HUGE", "1")
+    csr = rmat(14, 16, 12)
+    perm, hub, bounds = block_relabel(csr, pieces, rows_per_block=1024, block_nnz=65536)
+    ctx = Context(0)
+    lrs = [slice_rows(hub, bounds, p) for p in range(pieces)]
+    steps = [GpuStep(ctx, csr.n, pieces, lr, 0.85) for lr in lrs]
+    dpr = DevicePageRank(steps, None, use_graph=True)
+    dpr.run(10, 0)
+    got = np.concatenate(dpr.scores([lr.rows for lr in lrs]))[perm]
+    dpr.close()
+    for s in steps:
+        s.close()
+    ctx.close()
+    np.testing.assert_allclose(got, O.pagerank(csr, False, 0.85, 10), rtol=1e-12)
 
 
 @pytest.mark.gpu
