@@ -491,6 +491,8 @@ def measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True):
         # rank's plan then cuts its rows as the whole graph's (GX_PR_HUGE=1 semantics)
         from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import block_relabel
         perm, hub, bounds = block_relabel(csr, vranks)
+        if vranks > 1:
+            os.environ.setdefault("GX_PR_HUGE", "1")
     else:
         perm, hub, bounds = interleaved_relabel(csr, vranks)
     lrs = [slice_rows(hub, bounds, p * world + rank) for p in range(pieces)]

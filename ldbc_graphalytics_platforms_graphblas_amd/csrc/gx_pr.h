@@ -77,6 +77,14 @@ struct SortedUnit {
     int32_t r0, r1;     //   supergroup seg
 };
 
+// A row stripe of a multi-unit block, combined by k_pr_combine after the units' launch
+// (PrPart::comb_kernel): rows [s0, s1) of the block whose rows start at local row r0 and whose
+// k slabs of nrows doubles begin at uslab[slab]; dslot its dangling partial's slot or -1.
+struct CombStripe {
+    int64_t slab;
+    int32_t r0, nrows, s0, s1, k, dslot;
+};
+
 // x of local row `row`: rows [0, live) sit in the exchanged chunk, the rest (out-degree 0, so
 // no rank ever gathers them) in the rank-private xd, so that only the gathered prefix of each
 // rank's rows travels in the all-gather (gx_pr_part_create_live).
@@ -141,6 +149,11 @@ struct PrPart {
     uint32_t nunits = 0;
     DBuf<double> uslab;          // partial row sums of the multi-unit blocks
     DBuf<uint32_t> uticket;      // per multi-unit block: arrivals of the current iteration
+    // GX_PR_COMBINE=1: the multi-unit blocks' slabs are added up and their epilogue run by a
+    // second kernel over row stripes (k_pr_combine), not by each block's last arriving unit
+    bool comb_kernel = false;
+    DBuf<CombStripe> cstripes;
+    uint32_t ncstripes = 0;
     DBuf<uint64_t> utimes;       // debug (GX_PR_UNIT_TIMES): per-workgroup timestamps
     int utimes_launch = 0;
     int long_nnz = 65536;        // longer rows take the LONG segment path

@@ -46,6 +46,7 @@ namespace {
 
 constexpr int kRowBits = 14;     // packed entry: (column - group base) << kRowBits | row in block
 constexpr int kBS = 1024;        // threads of a k_pr_pull_units workgroup (16 waves, one per CU)
+constexpr int kCombRows = (1 << kRowBits) / kBS;   // rows per thread in a slab combine (16)
 constexpr int kU = 8;            // entries per lane and round (two 16-B index loads)
 constexpr int kRound = kBS * kU; // entries of one round of a workgroup
 constexpr int kNSg = 512;        // codes of a narrow supergroup: one wave's 16-B load per lane
@@ -95,6 +96,9 @@ struct SortedArgs {
     uint32_t pace_nw, pace_d, pace_polls, pace_ncus;
     // work queue (GX_PR_QUEUE): [0] next work item, [1] workgroups done (reset by the last)
     uint32_t *queue;
+    // combine kernel (PrPart::comb_kernel): the units of multi-unit blocks only store their slabs
+    int comb;
+    const CombStripe *cstripes;
 };
 
 // Returns the row's score if the row is dangling (out-degree 0), else 0.
@@ -139,6 +143,7 @@ __device__ __forceinline__ double epilogue_rows(const SortedArgs &a, int64_t r0,
 // block publishes its partial in its slot (agent scope) and takes a ticket; the last of the
 // ndblocks participants adds the partials up with the whole workgroup (thread t takes slots
 // t, t + kBS, ...; fixed tree, so the order is fixed) into the chunk's last x slot.
+template <int BS = kBS>
 __device__ __forceinline__ void dangling_publish(const SortedArgs &a, int32_t slot, double d, double *wred, int *last) {
     const int tid = threadIdx.x;
     d = wave_sum(d);
@@ -148,7 +153,7 @@ __device__ __forceinline__ void dangling_publish(const SortedArgs &a, int32_t sl
     if (tid == 0) {
         double tot = 0.0;
 #pragma unroll
-        for (int w = 0; w < kBS / kWave; w++) tot += wred[w];
+        for (int w = 0; w < BS / kWave; w++) tot += wred[w];
         __hip_atomic_store(&a.dpart[slot], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -159,7 +164,7 @@ __device__ __forceinline__ void dangling_publish(const SortedArgs &a, int32_t sl
     if (!*last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     double v = 0.0;
-    for (uint32_t j = tid; j < a.ndblocks; j += kBS) v += __hip_atomic_load(&a.dpart[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t j = tid; j < a.ndblocks; j += BS) v += __hip_atomic_load(&a.dpart[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     v = wave_sum(v);
     __syncthreads();
     if ((tid & (kWave - 1)) == 0) wred[tid / kWave] = v;
@@ -167,7 +172,7 @@ __device__ __forceinline__ void dangling_publish(const SortedArgs &a, int32_t sl
     if (tid == 0) {
         double all = 0.0;
 #pragma unroll
-        for (int w = 0; w < kBS / kWave; w++) all += wred[w];
+        for (int w = 0; w < BS / kWave; w++) all += wred[w];
         __hip_atomic_store(a.dticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         a.x_out[a.chunk - 1] = all;
     }
@@ -618,6 +623,13 @@ __device__ __forceinline__ void pull_item(const SortedArgs &a, const uint32_t w,
         __syncthreads();
     }
     if (TIMES && tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
+    if (u.nunits > 1 && a.comb) {
+        // the combine kernel adds the slabs after this launch (the launch boundary orders them)
+        double *mine = a.uslab + u.slab + (int64_t)u.unit * nrows;
+        for (int i = tid; i < nrows; i += kBS) mine[i] = acc[i];
+        stamp();
+        return;
+    }
     if (u.nunits > 1) {
         double *mine = a.uslab + u.slab + (int64_t)u.unit * nrows;
         for (int i = tid; i < nrows; i += kBS)
@@ -639,18 +651,55 @@ __device__ __forceinline__ void pull_item(const SortedArgs &a, const uint32_t w,
             return;
         }
         // after tid 0's acquire (this CU's L1 invalidated) and the barrier, plain loads see the
-        // other units' slabs; four rows per thread at a time keep 4 x nunits loads in flight
+        // other units' slabs.  All kCombRows rows of a thread at once (a block's 16 Ki rows in
+        // one pass), so a slab costs one round trip: the slabs live beyond this XCD's L2, and
+        // four rows at a time made the combine of 5 slabs ~30 us of a 1/8 piece's 80
+        // (tools/unit_times.py).  The adds keep unit order.
         const double *slabs = a.uslab + u.slab;
-        for (int i0 = tid; i0 < nrows; i0 += 4 * kBS) {
-            double s[4] = {0.0, 0.0, 0.0, 0.0};
+        if (2 * nrows <= kBS) {
+            // few rows (the longest rows' blocks, split into up to 256 units): S threads per
+            // row, thread g summing slabs g, g + S, ... 16 loads at a time, then the S partials
+            // added in group order through LDS above the block's rows -- a row-per-thread loop
+            // would take one round trip per slab (256 on a 1/8 piece's first block)
+            int S = 2;
+            while (4 * S * nrows <= 2 * kBS && S < u.nunits) S *= 2;
+            double *part = acc + (1 << (kRowBits - 1));
+            const int r = tid % nrows, g = tid / nrows;
+            if (g < S) {
+                double s = 0.0;
+                for (int j0 = g; j0 < u.nunits; j0 += kCombRows * S) {
+                    double v[kCombRows];
+#pragma unroll
+                    for (int q = 0; q < kCombRows; q++) {
+                        const int j = j0 + q * S;
+                        v[q] = j < u.nunits ? slabs[(int64_t)j * nrows + r] : 0.0;
+                    }
+#pragma unroll
+                    for (int q = 0; q < kCombRows; q++) s += v[q];
+                }
+                part[g * nrows + r] = s;
+            }
+            __syncthreads();
+            if (tid < nrows) {
+                double s = 0.0;
+                for (int q = 0; q < S; q++) s += part[q * nrows + tid];
+                acc[tid] = s;
+            }
+        } else
+        for (int i0 = tid; i0 < nrows; i0 += kCombRows * kBS) {
+            double s[kCombRows];
+#pragma unroll
+            for (int q = 0; q < kCombRows; q++) s[q] = 0.0;
             for (int j = 0; j < u.nunits; j++) {
                 const double *sl = slabs + (int64_t)j * nrows;
+                double v[kCombRows];
 #pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (i0 + q * kBS < nrows) s[q] += sl[i0 + q * kBS];
+                for (int q = 0; q < kCombRows; q++) v[q] = i0 + q * kBS < nrows ? sl[i0 + q * kBS] : 0.0;
+#pragma unroll
+                for (int q = 0; q < kCombRows; q++) s[q] += v[q];
             }
 #pragma unroll
-            for (int q = 0; q < 4; q++)
+            for (int q = 0; q < kCombRows; q++)
                 if (i0 + q * kBS < nrows) acc[i0 + q * kBS] = s[q];
         }
         // each thread reads back only the acc entries it wrote: no barrier needed
@@ -665,6 +714,52 @@ __device__ __forceinline__ void pull_item(const SortedArgs &a, const uint32_t w,
         if (slot >= 0) dangling_publish(a, slot, d, wred, &last);
     }
     stamp();
+}
+
+// The slabs of the multi-unit blocks (GX_PR_COMBINE=1), one workgroup per row stripe of at
+// most kCombBS rows: S threads per row (S = 1 for full stripes, up to kCombBS / rows for the
+// few-row blocks of the longest rows), thread g adding slabs g, g + S, ... in order, 16 loads in
+// flight, then the S partials in group order; the row's epilogue; the stripe's dangling partial.
+// Spread over the chip instead of one last-arriving workgroup per block, whose k round trips to
+// the slabs (a 1/8 piece's 33 Mi-entry block: 75 units of 9 Ki rows) outlasted the launch.
+constexpr int kCombBS = 256;
+__global__ __launch_bounds__(kCombBS) void k_pr_combine(SortedArgs a) {
+    __shared__ double part[kCombBS];
+    __shared__ double wred[kCombBS / kWave];
+    __shared__ int last;
+    double dsum = 0.0;
+    for (int k = 0; k < a.nranks; k++) dsum += a.x_in[(int64_t)k * a.chunk + a.chunk - 1];
+    const double teleport = a.teleport0 + a.damping_over_n * dsum;
+    const CombStripe c = a.cstripes[blockIdx.x];
+    const int rows = c.s1 - c.s0;
+    int S = 1;
+    while (2 * S * rows <= kCombBS && S < c.k) S *= 2;
+    const int tid = threadIdx.x, r = tid % rows, g = tid / rows;
+    double s = 0.0;
+    if (g < S) {
+        const double *sl = a.uslab + c.slab + c.s0 + r;
+        for (int j0 = g; j0 < c.k; j0 += 16 * S) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int j = j0 + q * S;
+                v[q] = j < c.k ? sl[(int64_t)j * c.nrows] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q++) s += v[q];
+        }
+    }
+    if (S > 1) {
+        if (g < S) part[g * rows + r] = s;
+        __syncthreads();
+        if (tid < rows) {
+            s = 0.0;
+            for (int q = 0; q < S; q++) s += part[q * rows + tid];
+        }
+    }
+    double d = 0.0;
+    if (tid < rows) d = sorted_epilogue(a, (int64_t)c.r0 + c.s0 + tid, s, teleport);
+    if (c.dslot >= 0) dangling_publish<kCombBS>(a, c.dslot, d, wred, &last);
 }
 
 // The next work item for the whole workgroup, with no divergent branch anywhere: wave 0 takes
@@ -1116,15 +1211,33 @@ int env_int(const char *name, int dflt, int lo, int hi) {
 // (zeroing, epilogue, slab store), ~1.5 us fixed, and the last arriver's slab reads.  It
 // picks the unit size on large graphs, so that the units of the large blocks land in as few
 // waves as the CUs allow.
+struct UnitCost {
+    // entries per us, us per row, us fixed, us per row and slab (GX_PR_SIM_RATE, GX_PR_SIM_ROW_PS,
+    // GX_PR_SIM_SLAB_PS override: entries / us and ps)
+    double rate = 2900.0, row = 0.002, fixed = 1.5, slab = 0.0005;
+    // model 1 (GX_PR_SIM_MODEL=1): a multi-unit block's units each store their slab (slab per
+    // row), and only the last arriver pays the combine, one round trip (rt us, GX_PR_SIM_RT_NS)
+    // per 16 Ki slab entries
+    int model = 0;
+    double rt = 2.0;
+};
+
 double pr_unit_makespan(const std::vector<int64_t> &ents, const std::vector<int64_t> &effs, const std::vector<int64_t> &rws,
-                        const std::vector<int64_t> &lsegs, int64_t t, int cus, bool by_cost) {
-    constexpr double kRate = 2900.0, kRow = 0.002, kFixed = 1.5, kSlab = 0.0005;
+                        const std::vector<int64_t> &lsegs, int64_t t, int cus, bool by_cost, const UnitCost &uc) {
+    const double kRate = uc.rate, kRow = uc.row, kFixed = uc.fixed, kSlab = uc.slab;
     std::vector<double> cost;
     for (size_t i = 0; i < ents.size(); i++) {
         const int64_t E = ents[i];
         // units by cost, not entries: a block of mostly wide (sparse-tail) entries runs at about
         // half the hub blocks' entry rate, so it is cut into more units (pr_unit_count)
         const int64_t k = std::max<int64_t>(1, std::min((E + kRound - 1) / kRound, ((by_cost ? effs[i] : E) + t - 1) / t));
+        if (uc.model == 1) {
+            const double c = (double)effs[i] / (double)k / kRate + kRow * (double)rws[i] + kFixed +
+                             (k > 1 ? kSlab * (double)rws[i] : 0.0);
+            for (int64_t j = 0; j + 1 < k; j++) cost.push_back(c);
+            cost.push_back(c + (k > 1 ? uc.rt * std::ceil((double)k * (double)rws[i] / (double)(1 << kRowBits)) : 0.0));
+            continue;
+        }
         const double c = (double)effs[i] / (double)k / kRate + kRow * (double)rws[i] + kFixed +
                          (k > 1 ? kSlab * (double)rws[i] * (double)k : 0.0);
         for (int64_t j = 0; j < k; j++) cost.push_back(c);
@@ -1165,6 +1278,10 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // GX_PR_HUGE=1: the huge-graph plan whatever the size (a rank of a block partition,
     // pr_partition.block_relabel, cuts its rows as the whole graph's plan does)
     const bool huge = per_cu > (double)(2 << 20) || env_int("GX_PR_HUGE", 0, 0, 1) == 1;
+    // a rank of a block partition (pr_partition.block_relabel: the whole graph's 32 Mi-entry
+    // blocks dealt whole; bench.py sets GX_PR_HUGE=1 for it): the whole graph's block cut, and
+    // the unit cost model fitted to its pieces (below)
+    const bool piece = huge && p->nranks > 1;
     const int rmax = kMaxBlockRows;   // rows per block (LDS accumulators: 16 Ki rows = 128 KiB, the top 64 junk)
     p->sorted_rows = env_int("GX_PR_SORTED_ROWS", huge ? rmax : 4096, 64, rmax);
     // ... and at most 4x the power of two nearest nnz / CUs, so that a small partition (one rank
@@ -1175,7 +1292,8 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // huge graphs: 32 Mi-entry blocks since the work queue (SYN-8_5, us per launch: 8 Mi 714,
     // 16 Mi 690, 32 Mi 685, 64 Mi 700, 128 Mi 702; profiles/r04_pr_block_sweep_queue.txt):
     // fewer blocks re-read x, and the queue keeps the larger units balanced
-    const int64_t bdef = huge ? std::min<int64_t>(32 << 20, 16 * pow2)
+    const int64_t bdef = piece ? (int64_t)(32 << 20)
+                       : huge ? std::min<int64_t>(32 << 20, 16 * pow2)
                               : std::min<int64_t>(per_cu > 384.0 * 1024 ? 4 << 20 : 1 << 20, 4 * pow2);
     const int64_t B = env_int("GX_PR_BLOCK_NNZ", (int)bdef, 1024, 1 << 30);
     p->long_nnz = env_int("GX_PR_LONG_NNZ", (int)std::max<int64_t>(B / 4, kRound), 1024, 1 << 30);
@@ -1467,15 +1585,30 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // under the work queue 687 -> 630 us per launch (weight 4: 632, 8: 642; by entries with
     // weight 6: 664; profiles/r04_pr_wide_cost_ab.txt).  Round 3, before the queue: 3 (757-764
     // -> 755-756 us, tools/r03_wc_ab.sh).  1 otherwise (SYN-7_5: no change)
-    const int64_t wide_cost4 = env_int("GX_PR_WIDE_COST", huge ? 24 : 4, 4, 64);
+    const int64_t wide_cost4 = env_int("GX_PR_WIDE_COST", piece ? 11 : huge ? 24 : 4, 4, 64);
+    // GX_PR_COST_CODES=1: the narrow part priced by its codes, fillers included, not by its
+    // entries -- a mid-density block's column steps need up to one filler per entry, and its
+    // units ran at ~2.3 K entries/us against ~4.7 K for the hub blocks (1/8 piece, unit stamps)
+    // GX_PR_FILL_COST: a filler's cost in quarters of a narrow entry's.  Fitted to the unit
+    // stamps of the 8 pieces of SYN-8_5 (2 330 units, rms 8.6 us on 74): 8.3 us + 177 ps per
+    // narrow entry, 2.0x that per filler, 2.7x per wide entry (the piece defaults, GX_PR_SIM_*
+    // below); the whole graph's units fit 1.3x per filler and 7.4x per wide entry
+    const bool cost_codes = env_int("GX_PR_COST_CODES", piece ? 1 : 0, 0, 1) == 1;
+    const int64_t fill_cost4 = env_int("GX_PR_FILL_COST", piece ? 8 : 4, 0, 64);
     auto eff_entries = [&](int64_t i) -> int64_t {
         const int64_t E = sortb[i].nz_end - sortb[i].nz_begin;
         const int64_t En = std::min<int64_t>(E, 256 * (int64_t)h_nsplit[i]);
-        return En + (E - En) * wide_cost4 / 4;
+        const int64_t fill = cost_codes ? std::max<int64_t>(0, (int64_t)h_ncode[i] - En) : 0;
+        return En + fill * fill_cost4 / 4 + (E - En) * wide_cost4 / 4;
     };
     // huge graphs: units per block by weighted entries (GX_PR_UNIT_BY_COST=0: by entries), so a
     // block of mostly wide entries, ~half the hub blocks' entry rate, is cut into more units
     const bool unit_by_cost = env_int("GX_PR_UNIT_BY_COST", huge ? 1 : 0, 0, 1) == 1;
+    // GX_PR_COMBINE=1: the multi-unit blocks combined by k_pr_combine (stripes), not by their
+    // last arriving unit
+    p->comb_kernel = env_int("GX_PR_COMBINE", piece ? 1 : 0, 0, 1) == 1;
+    std::vector<CombStripe> stripes;
+    std::vector<char> multi(longb.size() + sortb.size(), 0);
     if (sortb.empty()) GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries above
     if (!sortb.empty()) {
         if (std::getenv("GX_PR_UNIT_NNZ")) {
@@ -1505,13 +1638,28 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                  t = t < 64 * kRound ? t + kRound : (t + t / 25 + kRound - 1) / kRound * kRound)
                 cand.push_back(t);
             std::vector<double> span(cand.size());
+            UnitCost uc;
+            if (piece) {   // the fit above; the combine kernel leaves the units only their slab stores
+                uc.rate = 5650.0;
+                uc.row = 0.0;
+                uc.fixed = 8.3;
+                uc.slab = 0.0002;
+                uc.model = 1;
+                uc.rt = p->comb_kernel ? 0.0 : 2.0;
+            }
+            uc.rate = (double)env_int("GX_PR_SIM_RATE", (int)uc.rate, 100, 1 << 20);
+            uc.row = 1e-6 * (double)env_int("GX_PR_SIM_ROW_PS", (int)(uc.row * 1e6), 0, 1 << 20);
+            uc.slab = 1e-6 * (double)env_int("GX_PR_SIM_SLAB_PS", (int)(uc.slab * 1e6), 0, 1 << 20);
+            uc.model = env_int("GX_PR_SIM_MODEL", uc.model, 0, 1);
+            uc.rt = 1e-3 * (double)env_int("GX_PR_SIM_RT_NS", (int)(uc.rt * 1e3), 0, 1 << 20);
+            uc.fixed = 1e-3 * (double)env_int("GX_PR_SIM_FIXED_NS", (int)(uc.fixed * 1e3), 0, 1 << 20);
             const int nth = (int)std::max<size_t>(1, std::min<size_t>({8, cand.size(),
                                                                        (size_t)std::max(1u, std::thread::hardware_concurrency())}));
             std::vector<std::thread> th;
             for (int w = 0; w < nth; w++)
                 th.emplace_back([&, w]() {
                     for (size_t i = (size_t)w; i < cand.size(); i += (size_t)nth)
-                        span[i] = pr_unit_makespan(ents, effs, rws, lsegs, cand[i], (int)cus, unit_by_cost);
+                        span[i] = pr_unit_makespan(ents, effs, rws, lsegs, cand[i], (int)cus, unit_by_cost, uc);
                 });
             for (auto &x : th) x.join();
             for (size_t i = 0; i < cand.size(); i++)
@@ -1519,8 +1667,23 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                     best = span[i];
                     T = cand[i];
                 }
-            if (env_int("GX_PR_VERBOSE", 0, 0, 1))
+            if (env_int("GX_PR_VERBOSE", 0, 0, 3))
                 std::fprintf(stderr, "[gx_pr] unit size %lld: simulated launch %.1f us\n", (long long)T, best);
+            if (env_int("GX_PR_VERBOSE", 0, 0, 3) >= 2) {
+                // the blocks whose units cost most at the chosen size
+                std::vector<std::pair<double, size_t>> top;
+                for (size_t i = 0; i < ents.size(); i++) {
+                    const int64_t k = std::max<int64_t>(1, std::min((ents[i] + kRound - 1) / kRound, ((unit_by_cost ? effs[i] : ents[i]) + T - 1) / T));
+                    top.push_back({pr_unit_makespan({ents[i]}, {effs[i]}, {rws[i]}, {}, T, 1 << 14, unit_by_cost, uc), i});
+                    (void)k;
+                }
+                std::sort(top.begin(), top.end(), std::greater<>());
+                for (size_t q = 0; q < std::min<size_t>(8, top.size()); q++) {
+                    const size_t i = top[q].second;
+                    std::fprintf(stderr, "[gx_pr]   block %zu: entries %lld eff %lld rows %lld -> longest unit %.1f us\n", i,
+                                 (long long)ents[i], (long long)effs[i], (long long)rws[i], top[q].first);
+                }
+            }
         }
         GX_HIP_TRY(hipStreamSynchronize(s));   // narrow codes + lane permutation done: temporaries may go
         clk.mark("unit size");
@@ -1555,7 +1718,16 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
                 u.nunits = k;
                 units.push_back(u);
             }
+            if (env_int("GX_PR_VERBOSE", 0, 0, 3) == 3)
+                std::fprintf(stderr, "[gx_pr blk] %zu E %lld En %lld codes %u eff %lld k %d rows %lld\n", i, (long long)E,
+                             (long long)std::min<int64_t>(E, 256 * (int64_t)h_nsplit[i]), h_ncode[i],
+                             (long long)eff_entries((int64_t)i), k, (long long)rows_b);
             if (k > 1) {
+                if (p->comb_kernel)
+                    for (int64_t s0 = 0; s0 < rows_b; s0 += kCombBS)
+                        stripes.push_back({slab, b.row_begin, (int32_t)rows_b, (int32_t)s0,
+                                           (int32_t)std::min<int64_t>(rows_b, s0 + kCombBS), k, -1});
+                multi[longb.size() + i] = 1;
                 slab += (int64_t)k * rows_b;
                 parts++;
             }
@@ -1580,7 +1752,7 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         // 8 i + q -- cut the fabric reads of SYN-8_5 by 9 % and still ran slower: 955 against
         // 925 us per launch, SYN-7_5 100 against 84; round 3)
         p->nunits = (uint32_t)units.size();
-        if (env_int("GX_PR_VERBOSE", 0, 0, 1))
+        if (env_int("GX_PR_VERBOSE", 0, 0, 3))
             std::fprintf(stderr, "[gx_pr] plan: rows %lld nnz %llu unit_nnz %lld block_nnz %d "
                          "long_nnz %d: %zu sorted blocks, %u LONG blocks (%u rows), %u units, %d multi-unit blocks, "
                          "slab %lld doubles; narrow %llu entries in %llu codes\n",
@@ -1628,14 +1800,19 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
         bool long_dangling = false;
         for (const RowBlock &b : longb) long_dangling |= h_outdeg[b.row_begin] == 0;
         uint32_t nd = 0;
-        for (size_t i = longb.size(); i < all.size(); i++) {
-            bool any = false;
+        auto dangling_in = [&](int64_t r0, int64_t r1) {
             if (p->d_range)   // the dangling rows are [d0, d0 + nd)
-                any = p->nd > 0 && all[i].row_begin < p->d0 + (int64_t)p->nd && all[i].row_end > p->d0;
-            else
-                for (int32_t r2 = all[i].row_begin; r2 < all[i].row_end && !any; r2++) any = h_outdeg[r2] == 0;
-            if (any) slot[i] = (int32_t)nd++;
+                return p->nd > 0 && r0 < p->d0 + (int64_t)p->nd && r1 > p->d0;
+            for (int64_t r2 = r0; r2 < r1; r2++)
+                if (h_outdeg[r2] == 0) return true;
+            return false;
+        };
+        for (size_t i = longb.size(); i < all.size(); i++) {
+            if (p->comb_kernel && multi[i]) continue;   // its stripes publish instead
+            if (dangling_in(all[i].row_begin, all[i].row_end)) slot[i] = (int32_t)nd++;
         }
+        for (CombStripe &c : stripes)
+            if (dangling_in((int64_t)c.r0 + c.s0, (int64_t)c.r0 + c.s1)) c.dslot = (int32_t)nd++;
         p->fused_dangling = p->nd > 0 && nd > 0 && !long_dangling;
         p->ndblocks = nd;
         if (p->fused_dangling) {
@@ -1645,6 +1822,11 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
             if (!all.empty()) GX_HIP_TRY(hipMemcpy(p->dslot.p, slot.data(), all.size() * 4, hipMemcpyHostToDevice));
             GX_HIP_TRY(hipMemset(p->fdticket.p, 0, 4));
         }
+    }
+    p->ncstripes = (uint32_t)stripes.size();
+    if (!stripes.empty()) {
+        GX_TRY(p->cstripes.alloc(stripes.size()));
+        GX_HIP_TRY(hipMemcpy(p->cstripes.p, stripes.data(), stripes.size() * sizeof(CombStripe), hipMemcpyHostToDevice));
     }
     clk.mark("dangling slots");
     return GX_SUCCESS;
@@ -1683,6 +1865,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
     a.nunits = p->nunits;
     a.uslab = p->uslab.p;
     a.uticket = p->uticket.p;
+    a.comb = p->ncstripes > 0 ? 1 : 0;
+    a.cstripes = p->cstripes.p;
     a.xd = p->xd.p;
     a.live = (int64_t)p->live;
     a.utimes = nullptr;
@@ -1745,6 +1929,8 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
             else if (p->cache_policy == 1) hipLaunchKernelGGL((k_pr_pull_units<false, 0, 1>), dim3(nw), dim3(kBS), lds, s, a);
             else hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
         }
+        // (inside the iteration's timer: the SpMV is both launches)
+        if (p->ncstripes) hipLaunchKernelGGL(k_pr_combine, dim3(p->ncstripes), dim3(kCombBS), 0, s, a);
         if (a.utimes && ++p->utimes_launch == env_int("GX_PR_UNIT_TIMES_LAUNCH", 5, 1, 1 << 30)) {
             std::vector<uint64_t> t(4 * (size_t)nw);
             std::vector<SortedUnit> us(p->nunits);
@@ -1753,7 +1939,11 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
             GX_HIP_TRY(hipMemcpy(t.data(), p->utimes.p, t.size() * 8, hipMemcpyDeviceToHost));
             if (p->nunits) GX_HIP_TRY(hipMemcpy(us.data(), p->units.p, us.size() * sizeof(SortedUnit), hipMemcpyDeviceToHost));
             if (p->nblocks) GX_HIP_TRY(hipMemcpy(bs.data(), p->blocks.p, bs.size() * sizeof(RowBlock), hipMemcpyDeviceToHost));
-            if (FILE *f = std::fopen(times_path, "w")) {
+            // a "%d" in the path numbers the plans that reach the launch (every piece its file)
+            static std::atomic<int> ndump{0};
+            char path[512];
+            std::snprintf(path, sizeof path, times_path, ndump.fetch_add(1));
+            if (FILE *f = std::fopen(path, "w")) {
                 std::fprintf(f, "wg kind blk unit nunits entries rows t0 tgather t1 xcc\n");
                 for (size_t w = 0; w < nw; w++) {
                     if (w >= p->nlong_blocks && w < p->nlong_pad) continue;

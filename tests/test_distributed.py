@@ -271,13 +271,15 @@ def test_gpu_partition_api_simulated_ranks(nranks, live):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pieces", [2, 8])
-def test_gpu_block_partition_pieces(pieces, monkeypatch):
+@pytest.mark.parametrize("combine", ["0", "1"])
+def test_gpu_block_partition_pieces(pieces, combine, monkeypatch):
     """The block partition (bench.py GX_PR_PARTITION=blocks): the whole-graph plan's blocks
     dealt whole over `pieces` virtual ranks, each planned as a huge graph (GX_PR_HUGE=1), run by
     the device-driven runner with device copies; against the oracle."""
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
     from ldbc_graphalytics_platforms_graphblas_amd.pr_partition import DevicePageRank, GpuStep
     monkeypatch.setenv("GX_PR_HUGE", "1")
+    monkeypatch.setenv("GX_PR_COMBINE", combine)
     csr = rmat(14, 16, 12)
     perm, hub, bounds = block_relabel(csr, pieces, rows_per_block=1024, block_nnz=65536)
     ctx = Context(0)

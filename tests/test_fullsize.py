@@ -76,7 +76,8 @@ def test_pagerank_syn85(syn85):
     np.testing.assert_allclose(got, ref, rtol=PR_RTOL, atol=0)
 
 
-@pytest.mark.parametrize("env", [{"GX_PR_UNIT_BY_COST": "0", "GX_PR_WIDE_COST": "12"}, {"GX_PR_QUEUE": "0", "GX_PR_BLOCK_NNZ": "8388608"}])
+@pytest.mark.parametrize("env", [{"GX_PR_UNIT_BY_COST": "0", "GX_PR_WIDE_COST": "12"}, {"GX_PR_QUEUE": "0", "GX_PR_BLOCK_NNZ": "8388608"},
+                                 {"GX_PR_COMBINE": "1", "GX_PR_UNIT_NNZ": "524288"}])
 def test_pagerank_syn85_plan_knobs(syn85, monkeypatch, env):
     """The huge-graph plan knobs at full size on a fresh graph (the plan is cached per graph):
     units cut by entries (the round-4 plan before the cost weighting), and the launch without

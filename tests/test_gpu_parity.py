@@ -213,6 +213,11 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                  {"GX_PR_WIDE_COST": "64", "GX_PR_ROW_COST": "0", "GX_PR_UNIT_NNZ": "8192"},
                                  {"GX_PR_ROW_COST": "1024", "GX_PR_BLOCK_NNZ": "65536"},
                                  {"GX_PR_QUEUE": "1"}, {"GX_PR_QUEUE": "0"},
+                                 {"GX_PR_COMBINE": "1", "GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "65536"},
+                                 {"GX_PR_COMBINE": "1", "GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192",
+                                  "GX_PR_SORTED_ROWS": "64"},
+                                 {"GX_PR_COMBINE": "1", "GX_PR_QUEUE": "1", "GX_PR_UNIT_NNZ": "1024",
+                                  "GX_PR_BLOCK_NNZ": "65536", "GX_PR_LONG_NNZ": "1024"},
                                  {"GX_PR_QUEUE": "1", "GX_PR_UNIT_NNZ": "1024", "GX_PR_BLOCK_NNZ": "8192",
                                   "GX_PR_LONG_NNZ": "1024", "GX_PR_CP": "5", "GX_PR_NT_COL": "1000"},
                                  {"GX_PR_PACE": "1", "GX_PR_PACE_H": "1024", "GX_PR_PACE_W": "10"},
@@ -222,7 +227,8 @@ def test_pagerank_long_row_segments(ctx, monkeypatch, laneperm):
                                   "GX_PR_NT_COL": "1000", "GX_PR_UNIT_NNZ": "8192", "GX_PR_BLOCK_NNZ": "524288"}])
 def test_pagerank_plan_variants(ctx, monkeypatch, env):
     """The default plan, non-temporal index loads and sparse narrow gathers (GX_PR_CP=1 / 5, the large-graph default), the plan's key sort in groups of two segments or with 64-bit keys, without the lane permutation, blocks cut into many units, tiny blocks, 16 Ki- / 2 Ki- / 64-row blocks, split
-    blocks (several workgroups per sorted block, combined through slabs by the last arriver)
+    blocks (several workgroups per sorted block, combined through slabs by the last arriver, or
+    by the stripes of the combine kernel, GX_PR_COMBINE=1)
     and the CSR-Adaptive kernel all give the oracle's scores (directed and undirected)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
