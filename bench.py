@@ -482,7 +482,11 @@ def measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True):
     # the per-piece launch against 1/8 of the whole-graph launch is the per-rank efficiency)
     pieces = max(1, int(os.environ.get("GX_PR_PIECES", "1")))
     vranks = world * pieces
-    partition = os.environ.get("GX_PR_PARTITION", "interleave")
+    # default: a huge graph (more than 2 Mi entries per CU: config 4's SYN-8_5) is dealt by
+    # the single-GPU plan's blocks (block_relabel; 1/8 pieces 139-150 us per SpMV against 208
+    # interleaved), a smaller one interleaved
+    huge = nnz / max(1, torch.cuda.get_device_properties(device).multi_processor_count) > (2 << 20)
+    partition = os.environ.get("GX_PR_PARTITION", "blocks" if huge and vranks > 1 else "interleave")
     if partition == "ranges":
         perm, hub = hub_relabel(csr)
         bounds = partition_rows(hub.rowptr, vranks)

@@ -780,11 +780,23 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     // chunk every device exchanges (+ the zero padding slot and the dangling slot).  The pull
     // matrix of a directed graph is A', whose rows with out-edges in the PageRank sense are
     // still A's rows with out-edges: liveness is A's out-degree either way.
+    // A huge graph (more than 2 Mi entries per CU, the single-GPU plan's huge-graph cut) is
+    // split by blocks instead (pr_multi_blocks; pr_partition.block_relabel): every device's
+    // blocks are the single-GPU plan's own, so its gathers share x lines as the whole graph's
+    // do (1/8 pieces of SYN-8_5: 140 us per SpMV against 208 interleaved).
+    // GX_PR_MULTI_PARTITION=blocks / interleave overrides.
     uint64_t nlive = 0;
     for (uint64_t v = 0; v < n; v++) nlive += A->rowptr[v + 1] != A->rowptr[v];
     MultiRun M;
     M.ndev = ndev;
     M.chunk = ((nlive + ndev - 1) / ndev + 2 + 31) / 32 * 32;
+    bool by_blocks = ndev > 1 && (double)A->rowptr[n] / (double)std::max(1, ctxs[0]->num_cus) > (double)(2 << 20);
+    if (const char *e = std::getenv("GX_PR_MULTI_PARTITION")) by_blocks = std::strcmp(e, "blocks") == 0;
+    MultiBlocks mb;
+    if (by_blocks) {
+        GX_TRY(pr_multi_blocks(A, directed, ndev, &mb));
+        M.chunk = mb.chunk;
+    }
     if (M.chunk * (uint64_t)ndev >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
     M.ctx.assign(ctxs, ctxs + ndev);
     M.part.assign(ndev, nullptr);
@@ -802,7 +814,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     GX_TRY(per_device(ctxs, ndev, [&](int d) -> int {
         GX_TRY(gx_graph_create(ctxs[d], A, directed, &G.g[d]));
         if (directed) GX_TRY(ensure_transpose(G.g[d]));
-        GX_TRY(pr_multi_plan(G.g[d], ndev, d, M.chunk, damping, &M.part[d]));
+        GX_TRY(pr_multi_plan(G.g[d], ndev, d, M.chunk, damping, by_blocks ? &mb : nullptr, &M.part[d]));
         rows[d] = M.part[d]->rows;
         const size_t full = M.chunk * (size_t)ndev;
         hipStream_t s = ctxs[d]->stream;

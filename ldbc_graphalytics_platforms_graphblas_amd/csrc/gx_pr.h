@@ -152,6 +152,7 @@ struct PrPart {
     // GX_PR_COMBINE=1: the multi-unit blocks' slabs are added up and their epilogue run by a
     // second kernel over row stripes (k_pr_combine), not by each block's last arriving unit
     bool comb_kernel = false;
+    bool force_huge = false;     // the huge-graph plan whatever the size (a block partition's rank)
     DBuf<CombStripe> cstripes;
     uint32_t ncstripes = 0;
     DBuf<uint64_t> utimes;       // debug (GX_PR_UNIT_TIMES): per-workgroup timestamps
@@ -248,9 +249,26 @@ int pr_init(PrPart *p, double *x_local, hipStream_t s);
 // gx_pagerank's single-rank plan of a graph: its pull matrix (A' when directed, which must be
 // built) relabelled hub-first, column-sorted blocks, x buffers and the hub-first perm.
 int pr_single_plan(gx_graph *g, PrPart **out);
+// Rows of a huge graph's sorted block (gx_pr_sorted.hip kMaxBlockRows) and its entries.
+constexpr int kPlanBlockRows = 16320;
+constexpr int64_t kPlanBlockNnz = 32 << 20;
+
+// gx_pagerank_multi's block partition (pr_partition.block_relabel restated): the hub-first
+// order cut into the single-GPU plan's blocks, dealt whole to the devices largest first (LPT);
+// per device its hub-first positions in order, per hub-first position its exchange slot
+// (owner * chunk + local row).
+struct MultiBlocks {
+    std::vector<std::vector<int32_t>> pos;
+    std::vector<int32_t> slot;
+    uint64_t chunk = 0;
+};
+int pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *out);
+
 // gx_pagerank_multi's plan of device d of ndev from its copy of the graph (A' built when
-// directed): hub-first positions d, d + ndev, ... as rows, columns in the exchange layout.
-int pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double damping, PrPart **out);
+// directed): hub-first positions d, d + ndev, ... as rows (or mb's blocks), columns in the
+// exchange layout.
+int pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double damping, const MultiBlocks *mb,
+                  PrPart **out);
 // A rank's plan from its local pull rows (h_rp from 0) with columns already in the exchange
 // layout (ci), the out-degree of each row's vertex, and its live prefix (gx_pr_part_create_live).
 int pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint64_t chunk, uint64_t live,

@@ -571,6 +571,30 @@ __global__ void k_multi_colmap(const int32_t *__restrict__ perm, int64_t n, int 
     }
 }
 
+// Rows of device d's block partition: hub-first positions pos[j] (MultiBlocks).
+__global__ void k_block_pick(const int32_t *__restrict__ order, const int32_t *__restrict__ nout,
+                             const int64_t *__restrict__ plen, const int32_t *__restrict__ pos, int64_t rows,
+                             int32_t *__restrict__ my_order, int32_t *__restrict__ my_out,
+                             int64_t *__restrict__ my_plen) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= rows; j += (int64_t)gridDim.x * blockDim.x) {
+        if (j == rows) {
+            my_plen[rows] = 0;
+            continue;
+        }
+        const int64_t i = pos[j];
+        my_order[j] = order[i];
+        my_out[j] = nout[i];
+        my_plen[j] = plen[i];
+    }
+}
+
+// vertex -> its exchange slot through its hub-first position (MultiBlocks::slot)
+__global__ void k_block_colmap(const int32_t *__restrict__ perm, int64_t n, const int32_t *__restrict__ slot,
+                               int32_t *__restrict__ colmap) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        colmap[v] = slot[perm[v]];
+}
+
 // Hub-first order: vertices by out-degree descending, ties by id (stable counting sort).
 // The pull SpMV gathers x(u) once per out-edge of u, so this packs the most gathered
 // entries of x into its first few MiB, which stay resident in each XCD's 4 MiB L2.
@@ -785,19 +809,96 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     return GX_SUCCESS;
 }
 
+// The block partition of gx_pagerank_multi (MultiBlocks), on the host from A: the hub-first
+// order (hub_order, as the devices' radix sort orders it), the pull rows' lengths in it (A's
+// out-degrees; A''s rows, the in-degrees, when directed), the greedy cut of pr_plan_sorted's
+// huge-graph blocks (kPlanBlockRows rows, kPlanBlockNnz entries; GX_PR_MULTI_BLOCK_ROWS /
+// _NNZ shrink them for tests), then largest block first to the device with the least entries +
+// rows.  A device's positions stay in hub-first order, so its rows without out-edges come last
+// (the live prefix).  The devices' own sorts must agree with each other, not with this order:
+// a position names whichever vertex a device's order puts there, and every device's plan and
+// column map read the same (device) order.
+int gx::pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *out) {
+    const uint64_t n = A->n;
+    std::vector<int32_t> outdeg(n), order, perm;
+    for (uint64_t v = 0; v < n; v++) outdeg[v] = (int32_t)(A->rowptr[v + 1] - A->rowptr[v]);
+    hub_order(outdeg, order, perm);
+    std::vector<int64_t> len(n);
+    if (directed) {
+        std::vector<int64_t> indeg(n, 0);
+        for (uint64_t e = 0; e < A->rowptr[n]; e++) indeg[A->colidx[e]]++;
+        for (uint64_t h = 0; h < n; h++) len[h] = indeg[order[h]];
+    } else {
+        for (uint64_t h = 0; h < n; h++) len[h] = outdeg[order[h]];
+    }
+    auto env = [](const char *name, int64_t dflt, int64_t lo, int64_t hi) {
+        const char *e = std::getenv(name);
+        const int64_t v = e ? std::atoll(e) : dflt;
+        return v >= lo && v <= hi ? v : dflt;
+    };
+    const int64_t R = env("GX_PR_MULTI_BLOCK_ROWS", kPlanBlockRows, 1, kPlanBlockRows);
+    const int64_t B = env("GX_PR_MULTI_BLOCK_NNZ", kPlanBlockNnz, 1, (int64_t)1 << 30);
+    std::vector<int64_t> starts;
+    for (uint64_t r = 0; r < n;) {
+        starts.push_back((int64_t)r);
+        uint64_t e = r;
+        int64_t ent = 0;
+        // at least one row; then rows while both caps hold
+        do ent += len[e++];
+        while (e < n && (int64_t)(e - r) < R && ent + len[e] <= B);
+        r = e;
+    }
+    starts.push_back((int64_t)n);
+    const size_t nb = starts.size() - 1;
+    std::vector<int64_t> size(nb);
+    for (size_t b = 0; b < nb; b++) {
+        int64_t s = 0;
+        for (int64_t h = starts[b]; h < starts[b + 1]; h++) s += len[h];
+        size[b] = s;
+    }
+    std::vector<size_t> byb(nb);
+    for (size_t b = 0; b < nb; b++) byb[b] = b;
+    std::stable_sort(byb.begin(), byb.end(), [&](size_t x, size_t y) { return size[x] > size[y]; });
+    std::vector<int64_t> load(ndev, 0);
+    std::vector<int> owner(nb, 0);
+    for (size_t b : byb) {
+        const int d = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        owner[b] = d;
+        load[d] += size[b] + (starts[b + 1] - starts[b]);
+    }
+    out->pos.assign(ndev, {});
+    for (size_t b = 0; b < nb; b++)
+        for (int64_t h = starts[b]; h < starts[b + 1]; h++) out->pos[owner[b]].push_back((int32_t)h);
+    uint64_t live = 0;
+    for (int d = 0; d < ndev; d++) {
+        uint64_t l = 0;
+        for (int32_t h : out->pos[d]) l += outdeg[order[h]] > 0;
+        live = std::max(live, l);
+    }
+    out->chunk = (live + 2 + 31) / 32 * 32;
+    if (out->chunk * (uint64_t)ndev >= (1ull << 31))
+        return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
+    out->slot.assign(n, 0);
+    for (int d = 0; d < ndev; d++)
+        for (size_t j = 0; j < out->pos[d].size(); j++)
+            out->slot[out->pos[d][j]] = (int32_t)((uint64_t)d * out->chunk + j);
+    return GX_SUCCESS;
+}
+
 // gx_pagerank_multi's plan of device `d` of `ndev`, all on that device from its copy of the
 // graph: the hub-first order (the same radix sort on every device, so every device derives
 // the same partition), the device's rows (hub-first positions d, d + ndev, ...) as the sorted
 // plan's source rows, and the column map into the exchange layout as its column renaming.
 // Replaces the host transpose / row picking / column remapping of round 3.
-int gx::pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double damping, PrPart **out) {
+int gx::pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double damping, const MultiBlocks *mb,
+                      PrPart **out) {
     const uint64_t n = g->n;
     gx_ctx *ctx = g->ctx;
     hipStream_t s = ctx->stream;
     DevCSR &P = g->directed ? g->AT : g->A;
     PlanClock clk("multi", s);
     GX_TRY(ensure_outdeg(g));
-    const uint64_t rows = n > (uint64_t)d ? (n - (uint64_t)d + ndev - 1) / ndev : 0;
+    const uint64_t rows = mb ? mb->pos[d].size() : n > (uint64_t)d ? (n - (uint64_t)d + ndev - 1) / ndev : 0;
     std::unique_ptr<PrPart> p(new PrPart());
     p->ctx = ctx;
     p->n_global = n;
@@ -805,6 +906,7 @@ int gx::pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double dampi
     p->rank = d;
     p->chunk = chunk;
     p->damping = damping;
+    p->force_huge = mb != nullptr;   // the whole graph's block cut (pr_plan_sorted `piece`)
     GX_TRY(p->order.alloc(std::max<uint64_t>(rows, 1)));
     GX_TRY(p->perm.alloc(n));   // the column map
     GX_TRY(p->rp_own.alloc(rows + 1));
@@ -829,13 +931,29 @@ int gx::pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double dampi
         hipLaunchKernelGGL(k_hub_apply, dim3(grid), dim3(256), 0, s, i1.p, (int64_t)n, g->outdeg.p, P.rp.p, ord.p,
                            i0.p, nout.p, plen.p);
         GX_TRY(check_launch("k_hub_apply"));
-        hipLaunchKernelGGL(k_multi_pick, dim3(grid_for(rows + 1, 256, 8192)), dim3(256), 0, s, ord.p, nout.p, plen.p,
-                           ndev, d, (int64_t)rows, p->order.p, p->outdeg_own.p, myplen.p);
-        GX_TRY(check_launch("k_multi_pick"));
-        hipLaunchKernelGGL(k_multi_colmap, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, i0.p, (int64_t)n, ndev,
-                           (int64_t)chunk, p->perm.p);
-        GX_TRY(check_launch("k_multi_colmap"));
-        GX_TRY(scan_exclusive_i64(myplen.p, p->rp_own.p, rows + 1, s));
+        if (mb) {
+            DBuf<int32_t> pos, slot;
+            GX_TRY(pos.alloc(std::max<uint64_t>(rows, 1)));
+            GX_TRY(slot.alloc(n));
+            if (rows) GX_HIP_TRY(hipMemcpy(pos.p, mb->pos[d].data(), rows * 4, hipMemcpyHostToDevice));
+            GX_HIP_TRY(hipMemcpy(slot.p, mb->slot.data(), n * 4, hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(k_block_pick, dim3(grid_for(rows + 1, 256, 8192)), dim3(256), 0, s, ord.p, nout.p, plen.p,
+                               pos.p, (int64_t)rows, p->order.p, p->outdeg_own.p, myplen.p);
+            GX_TRY(check_launch("k_block_pick"));
+            hipLaunchKernelGGL(k_block_colmap, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, i0.p, (int64_t)n, slot.p,
+                               p->perm.p);
+            GX_TRY(check_launch("k_block_colmap"));
+            GX_TRY(scan_exclusive_i64(myplen.p, p->rp_own.p, rows + 1, s));
+            GX_HIP_TRY(hipStreamSynchronize(s));   // pos / slot die here
+        } else {
+            hipLaunchKernelGGL(k_multi_pick, dim3(grid_for(rows + 1, 256, 8192)), dim3(256), 0, s, ord.p, nout.p, plen.p,
+                               ndev, d, (int64_t)rows, p->order.p, p->outdeg_own.p, myplen.p);
+            GX_TRY(check_launch("k_multi_pick"));
+            hipLaunchKernelGGL(k_multi_colmap, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, i0.p, (int64_t)n, ndev,
+                               (int64_t)chunk, p->perm.p);
+            GX_TRY(check_launch("k_multi_colmap"));
+        }
+        if (!mb) GX_TRY(scan_exclusive_i64(myplen.p, p->rp_own.p, rows + 1, s));
         GX_HIP_TRY(hipStreamSynchronize(s));   // the temporaries are freed at the end of the block
     }
     clk.mark("hub order + partition rows (device)");

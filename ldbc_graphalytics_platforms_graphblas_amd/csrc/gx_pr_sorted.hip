@@ -52,6 +52,7 @@ constexpr int kRound = kBS * kU; // entries of one round of a workgroup
 constexpr int kNSg = 512;        // codes of a narrow supergroup: one wave's 16-B load per lane
 constexpr int kJunkRow = (1 << kRowBits) - kWave;   // accumulators [16320, 16384) absorb fillers
 constexpr int kMaxBlockRows = kJunkRow;             // rows of a sorted block
+static_assert(kMaxBlockRows == kPlanBlockRows, "gx_pr.h block rows");
 
 struct SortedArgs {
     const RowBlock *blocks;
@@ -1277,7 +1278,7 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     const double per_cu = std::max(1.0, (double)nnz / (double)cus);
     // GX_PR_HUGE=1: the huge-graph plan whatever the size (a rank of a block partition,
     // pr_partition.block_relabel, cuts its rows as the whole graph's plan does)
-    const bool huge = per_cu > (double)(2 << 20) || env_int("GX_PR_HUGE", 0, 0, 1) == 1;
+    const bool huge = per_cu > (double)(2 << 20) || env_int("GX_PR_HUGE", 0, 0, 1) == 1 || p->force_huge;
     // a rank of a block partition (pr_partition.block_relabel: the whole graph's 32 Mi-entry
     // blocks dealt whole; bench.py sets GX_PR_HUGE=1 for it): the whole graph's block cut, and
     // the unit cost model fitted to its pieces (below)
@@ -1292,7 +1293,7 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // huge graphs: 32 Mi-entry blocks since the work queue (SYN-8_5, us per launch: 8 Mi 714,
     // 16 Mi 690, 32 Mi 685, 64 Mi 700, 128 Mi 702; profiles/r04_pr_block_sweep_queue.txt):
     // fewer blocks re-read x, and the queue keeps the larger units balanced
-    const int64_t bdef = piece ? (int64_t)(32 << 20)
+    const int64_t bdef = piece ? kPlanBlockNnz
                        : huge ? std::min<int64_t>(32 << 20, 16 * pow2)
                               : std::min<int64_t>(per_cu > 384.0 * 1024 ? 4 << 20 : 1 << 20, 4 * pow2);
     const int64_t B = env_int("GX_PR_BLOCK_NNZ", (int)bdef, 1024, 1 << 30);
@@ -1592,9 +1593,10 @@ int pr_plan_sorted(PrPart *p, HostView<int64_t> h_rp, HostView<int32_t> h_outdeg
     // GX_PR_FILL_COST: a filler's cost in quarters of a narrow entry's.  Fitted to the unit
     // stamps of the 8 pieces of SYN-8_5 (2 330 units, rms 8.6 us on 74): 8.3 us + 177 ps per
     // narrow entry, 2.0x that per filler, 2.7x per wide entry (the piece defaults, GX_PR_SIM_*
-    // below); the whole graph's units fit 1.3x per filler and 7.4x per wide entry
+    // below); the whole graph's units fit 1.3x per filler and 7.4x per wide entry.  Fillers
+    // priced as entries ran faster than at the fitted 2x (139 against 150 us per piece launch)
     const bool cost_codes = env_int("GX_PR_COST_CODES", piece ? 1 : 0, 0, 1) == 1;
-    const int64_t fill_cost4 = env_int("GX_PR_FILL_COST", piece ? 8 : 4, 0, 64);
+    const int64_t fill_cost4 = env_int("GX_PR_FILL_COST", 4, 0, 64);
     auto eff_entries = [&](int64_t i) -> int64_t {
         const int64_t E = sortb[i].nz_end - sortb[i].nz_begin;
         const int64_t En = std::min<int64_t>(E, 256 * (int64_t)h_nsplit[i]);

@@ -602,6 +602,30 @@ def test_multi_virtual_devices(k, undirected):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [2, 3, 8])
+@pytest.mark.parametrize("undirected", [True, False])
+@pytest.mark.parametrize("rows,nnz", [(64, 2048), (16320, 1 << 30), (1, 1 << 30)])
+def test_multi_virtual_devices_blocks(k, undirected, rows, nnz, monkeypatch):
+    """gx_pagerank_multi's block partition (pr_multi_blocks, the huge-graph default): the
+    hub-first order cut into blocks of at most `rows` rows and `nnz` entries -- small blocks,
+    one block holding the whole graph (every other device owns nothing), one row per block --
+    dealt largest first; each device planned with the whole graph's cut.  rtol 1e-12."""
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    monkeypatch.setenv("GX_PR_MULTI_PARTITION", "blocks")
+    monkeypatch.setenv("GX_PR_MULTI_BLOCK_ROWS", str(rows))
+    monkeypatch.setenv("GX_PR_MULTI_BLOCK_NNZ", str(nnz))
+    ctxs = [Context(0) for _ in range(k)]
+    try:
+        for scale, ef in ((10, 8), (13, 16)):
+            csr = rmat(scale, ef, 3 + scale, undirected=undirected)
+            got = _multi_call("gx_pagerank_multi", ctxs, csr, int(not undirected), 0.85, 10)
+            np.testing.assert_allclose(got, O.pagerank(csr, not undirected, 0.85, 10), rtol=1e-12, atol=0)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.gpu
 def test_multi_virtual_devices_edge_cases():
     """More virtual devices than rows with out-edges (some own nothing live), an edgeless graph,
     and LCC on one device (a size-1 RCCL clique and its ncclReduce)."""

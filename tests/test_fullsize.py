@@ -238,7 +238,8 @@ def test_multi_virtual_devices_syn75_syncit(syn75, syncit):
 
 def test_multi_virtual_devices_syn85(syn85):
     """Config 4 (PageRank + SSSP on datagen-8_5-fb, 8 GPUs) through the executables' entry
-    points on 8 virtual devices: PageRank rtol 1e-12, SSSP bit-exact."""
+    points on 8 virtual devices: PageRank rtol 1e-12 (a huge graph: the block partition,
+    pr_multi_blocks), SSSP bit-exact."""
     csr, _ = syn85
     src = _maxdeg(csr)
     got = _multi_k("gx_sssp_multi", 8, csr, 0, src)
