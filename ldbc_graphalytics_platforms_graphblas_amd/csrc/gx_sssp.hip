@@ -103,6 +103,7 @@ struct SsspBufs {
     double delta, inv_delta;
     SsspState *st;
     unsigned long long *stats;    // GX_SSSP_VERBOSE work counters, else null
+    uint32_t dense_div;           // an opening of more than n / dense_div entries scans the stamps (0: never)
 };
 
 __device__ __forceinline__ unsigned long long nsw_pack(int64_t bucket, int32_t round) {
@@ -386,7 +387,16 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
         list = B.settled;
         count = st->settled_cnt;
     }
-    if ((uint64_t)blockIdx.x * kSsspBlock >= count) return;   // no entry for this workgroup
+    // dense opening: when the opened slots hold more than n / 16 entries (SYN-8_5's window
+    // after its first pulled heavy phase: 3.4 M ring entries for 157 K live vertices, 419 us of
+    // random reads), scan every vertex's bucket stamp instead -- a vertex is live in the opened
+    // buckets exactly when its stamp names one of them (a push always stamps the bucket it
+    // enters, every later push only lowers it, and opened buckets never receive pushes), so the
+    // sequential 4 n bytes of stamps replace the entries' three random reads each
+    const uint32_t dense_div = B.dense_div;
+    const bool dense = mode == 1 && dense_div > 0 && (uint64_t)count * dense_div > B.ring_cap;
+    const uint32_t dom = dense ? (uint32_t)B.ring_cap : count;
+    if ((uint64_t)blockIdx.x * kSsspBlock >= dom) return;   // no entry for this workgroup
     __shared__ uint32_t fcnt[kRing];                            // fused slots' entry counts (mode 1)
     if (fn > 1 && (int)threadIdx.x < fn) fcnt[threadIdx.x] = st->ring_cnt[(fslot + threadIdx.x) % kRing];
     __syncthreads();
@@ -395,7 +405,8 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
     const bool pull = mode == 3 && st->pull;
     unsigned long long mymin = ~0ull, n_skip = 0;
     const uint32_t stride = gridDim.x * kSsspBlock;
-    const uint32_t nround = (count + stride - 1) / stride;
+    const uint32_t nround = (dom + stride - 1) / stride;
+    const int32_t lo32 = (int32_t)(cur - (fn - 1));   // the first opened bucket (stamps are 32-bit)
     // pushes are staged per wave in LDS and flushed in bulk, as in k_sssp_relax
     __shared__ Stage stages[kSsspBlock / kWave];
     Stage &sg = stages[threadIdx.x / kWave];
@@ -411,7 +422,21 @@ __global__ __launch_bounds__(kSsspBlock) void k_sssp_advance(SsspBufs B) {
         int32_t v = 0;
         int slot = 0, fj = 0;
         uint32_t nch = 0;
-        if (f < count) {
+        if (dense) {
+            if (f < dom) {
+                v = (int32_t)f;
+                const uint32_t k = (uint32_t)B.bstamp[v] - (uint32_t)lo32;
+                if (k < (uint32_t)fn) {
+                    if (B.dist[v] == B.relaxed[v]) {
+                        n_skip++;
+                    } else {
+                        B.nsw[v] = nsw_pack(cur, r);
+                        to_near = to_set = true;
+                        nch = chunks_of(B.lend[v] - B.rp[v]);
+                    }
+                }
+            }
+        } else if (f < count) {
             if (fn > 1) {   // entry f of the fused slots' concatenation
                 uint32_t g = f;
                 int j = 0;
@@ -1152,7 +1177,8 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     SsspBufs B{g->A.rp.p,   lay.lend.p,   lay.ci.p,      lay.w.p,    dist.p,       relaxed.p,  nsw.p,
                bstamp.p,    ostamp.p,     W.sbits.p,     nbit_words(n), {W.q0.p, W.q1.p}, W.ring.p,
                {W.ovf0.p, W.ovf1.p},
-               W.settled.p, (uint64_t)n,  delta,         inv_delta,  st.p,         stats.p};
+               W.settled.p, (uint64_t)n,  delta,         inv_delta,  st.p,         stats.p, 16u};
+    if (const char *e = std::getenv("GX_SSSP_DENSE")) B.dense_div = (uint32_t)std::strtoul(e, nullptr, 10);
 
     hipLaunchKernelGGL(k_sssp_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, dist.p, relaxed.p, nsw.p,
                        bstamp.p, ostamp.p, n);

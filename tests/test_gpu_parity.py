@@ -309,7 +309,10 @@ def test_pagerank_mixed_escape_rounds(ctx, monkeypatch, laneperm):
                                  {"GX_SSSP_PULL_FRAC": "50", "GX_SSSP_DSCALE": "5"},
                                  {"GX_SSSP_FUSE": "0"}, {"GX_SSSP_FUSE": "300", "GX_SSSP_DSCALE": "0.5"},
                                  {"GX_SSSP_FUSE_MAX": "3", "GX_SSSP_DSCALE": "1"},
-                                 {"GX_SSSP_DELTA": "0.01"}, {"GX_SSSP_DELTA": "1000"}])
+                                 {"GX_SSSP_DELTA": "0.01"}, {"GX_SSSP_DELTA": "1000"},
+                                 {"GX_SSSP_DENSE": "0"}, {"GX_SSSP_DENSE": "1000000"},
+                                 {"GX_SSSP_DENSE": "1000000", "GX_SSSP_FUSE": "0", "GX_SSSP_DSCALE": "0.5"},
+                                 {"GX_SSSP_DENSE": "1000000", "GX_SSSP_DELTA": "0.01"}])
 def test_sssp_pull_heavy_phase(ctx, monkeypatch, env):
     """Heavy phases pushed, always pulled, and pulled only for big settled lists, over narrow
     and wide buckets, with buckets opened one at a time or fused (GX_SSSP_FUSE entries,
