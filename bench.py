@@ -387,8 +387,14 @@ def run_algorithm_distributed(args):
     ctx = A.Context(local_rank)
     dev_name, cus = ctx.info()
     G = A.Graph(ctx, csr, directed)
-    rng = D.vertex_ranges(csr.rowptr, world)
-    ranks = [D.LocalRank(D.GpuBackend(G), int(rng[rank]), int(rng[rank + 1]), device, rank)]
+    # GX_SIM_RANKS=k at N = 1: k ranks on this GPU (LocalComm), for the exchange volumes of a
+    # k-GPU run (the times are one GPU's)
+    sim = int(os.environ.get("GX_SIM_RANKS", "0")) if world == 1 and not dist else 0
+    rng = D.vertex_ranges(csr.rowptr, sim or world)
+    if sim:
+        ranks = [D.LocalRank(D.GpuBackend(G), int(rng[k]), int(rng[k + 1]), device, k) for k in range(sim)]
+    else:
+        ranks = [D.LocalRank(D.GpuBackend(G), int(rng[rank]), int(rng[rank + 1]), device, rank)]
     comm = D.TorchComm() if dist else D.LocalComm()
 
     def call():
@@ -411,11 +417,13 @@ def run_algorithm_distributed(args):
     for _ in range(max(1, args.warmup)):
         out = call()
     barrier()
+    D.reset_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = call()
     barrier()
     elapsed = time.perf_counter() - t0
+    xstats = {k: v / args.steps for k, v in D.STATS.items()}   # per call
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -446,8 +454,11 @@ def run_algorithm_distributed(args):
             "data": f"synthetic (seeded R-MAT stand-in for {P['stands_for']}; no network for the real dataset)",
             "config": {"workload": f"{alg.upper()} {gname} (partitioned)", "algorithm": alg, "graph": gname,
                        "n": n, "nnz": nnz, "directed": directed, "source": src,
-                       "parallelism": f"replicated graph, {world} vertex ranges, RCCL exchange per round",
+                       "parallelism": (f"replicated graph, {sim} vertex ranges simulated on one GPU" if sim else
+                                       f"replicated graph, {world} vertex ranges, RCCL exchange per round"),
                        "device": dev_name, "cus": cus},
+            # per call and rank: frontier-sized words vs the dense collectives (distributed._exchange)
+            "exchange": {"mode": D.EXCHANGE, **xstats},
             "roofline": None, "cpu_baseline": None, "parity_vs_oracle": parity,
             "note": "wall time per call incl. per-round host syncs; the single-GPU path is bench.py --algorithm X",
         }

@@ -381,6 +381,18 @@ int gx_bfs_part_expand(gx_graph *g, uint64_t v0, uint64_t v1, const int64_t *lev
 int gx_bfs_part_commit(gx_graph *g, const uint8_t *next, int64_t *level, int64_t cur, uint64_t *count,
                        void *stream);
 
+/* Sparse exchange of a step's updates (BFS / WCC / CDLP at N > 1, distributed.py): the
+ * entries v in [v0, v1) of a whose value differs from b[v] (b null: from 0) are appended to
+ * words as (v << 32 | value) -- one 64-bit word each, *count (device int64, zeroed here) of
+ * them, in no particular order; elem_bytes 1 (uint8) or 4 (int32).  After an all-gather of
+ * the counts and of the first max-count words of every rank, gx_part_apply writes every
+ * rank's words (rank k's counts[k] words at words + k stride) into arr: op 0 set, 1 min, 2 max
+ * (min / max for 4-byte elements).  No gx_graph: runs on the current device, on `stream`. */
+int gx_part_changes(const void *a, const void *b, uint64_t v0, uint64_t v1, int elem_bytes, uint64_t *words,
+                    int64_t *count, void *stream);
+int gx_part_apply(const uint64_t *words, const int64_t *counts, int nranks, uint64_t stride, void *arr,
+                  int elem_bytes, int op, void *stream);
+
 int gx_wcc_part_init(gx_graph *g, int32_t *parent, void *stream);
 int gx_wcc_part_hook(gx_graph *g, uint64_t v0, uint64_t v1, int32_t *parent, int *changed, void *stream);
 int gx_wcc_part_compress(gx_graph *g, int32_t *parent, void *stream);

@@ -109,6 +109,77 @@ __global__ __launch_bounds__(kPartBlock) void k_wccp_compress(int32_t *parent, i
         parent[v] = find_root_p(parent, (int32_t)v);
 }
 
+// Sparse exchange (gx_part_changes / gx_part_apply): a tile of kChTile entries per workgroup
+// pass, 16 per thread, one counter atomic per tile (a queue atomic per wave serialised at
+// ~11 ns each).  A change leaves as one 64-bit word (v << 32 | value).
+constexpr int kChPer = 16;
+constexpr int kChTile = kPartBlock * kChPer;
+
+template <typename T>
+__global__ __launch_bounds__(kPartBlock) void k_part_changes(const T *__restrict__ a, const T *__restrict__ b,
+                                                             int64_t v0, int64_t v1, uint64_t *__restrict__ out,
+                                                             unsigned long long *count) {
+    __shared__ uint32_t wsum[kPartBlock / kWave];
+    __shared__ unsigned long long base;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+    for (int64_t t0 = v0 + (int64_t)blockIdx.x * kChTile; t0 < v1; t0 += (int64_t)gridDim.x * kChTile) {
+        uint32_t flags = 0, c = 0;
+#pragma unroll
+        for (int j = 0; j < kChPer; j++) {
+            const int64_t v = t0 + tid + (int64_t)j * kPartBlock;
+            if (v < v1 && a[v] != (b ? b[v] : (T)0)) {
+                flags |= 1u << j;
+                c++;
+            }
+        }
+        uint32_t incl = c;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, kWave);
+            if (lane >= off) incl += y;
+        }
+        if (lane == kWave - 1) wsum[wid] = incl;
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kPartBlock / kWave; w++) {
+            before += w < wid ? wsum[w] : 0u;
+            total += wsum[w];
+        }
+        if (tid == 0) base = total ? atomicAdd(count, (unsigned long long)total) : 0ull;
+        __syncthreads();
+        uint64_t at = base + before + incl - c;
+        for (int j = 0; j < kChPer; j++)
+            if (flags & (1u << j)) {
+                const int64_t v = t0 + tid + (int64_t)j * kPartBlock;
+                out[at++] = ((uint64_t)v << 32) | (uint32_t)a[v];
+            }
+        __syncthreads();   // wsum / base reused by the next tile
+    }
+}
+
+// op 0 set, 1 min, 2 max (int32 only for 1 / 2); rank k's count[k] words at words + k * stride
+template <typename T>
+__global__ __launch_bounds__(kPartBlock) void k_part_apply(const uint64_t *__restrict__ words,
+                                                           const int64_t *__restrict__ counts, int nranks,
+                                                           int64_t stride, T *arr, int op) {
+    const int64_t total = (int64_t)nranks * stride;
+    for (int64_t i = (int64_t)blockIdx.x * kPartBlock + threadIdx.x; i < total; i += (int64_t)gridDim.x * kPartBlock) {
+        const int64_t k = i / stride, j = i - k * stride;
+        if (j >= counts[k]) continue;
+        const uint64_t w = words[i];
+        const int64_t v = (int64_t)(w >> 32);
+        const T val = (T)(uint32_t)w;
+        if constexpr (sizeof(T) == 4) {
+            if (op == 1) atomicMin((int32_t *)&arr[v], (int32_t)val);
+            else if (op == 2) atomicMax((int32_t *)&arr[v], (int32_t)val);
+            else arr[v] = val;
+        } else {
+            arr[v] = val;
+        }
+    }
+}
+
 // NULL is the null (default) stream -- torch's default stream -- not the context's stream.
 hipStream_t pick_stream(gx_graph *, void *stream) { return (hipStream_t)stream; }
 
@@ -185,3 +256,42 @@ extern "C" int gx_wcc_part_compress(gx_graph *g, int32_t *parent, void *stream) 
 }
 
 GX_MODULE_WARMER(part)
+
+// Sparse exchange of a partitioned step's updates (distributed.py: BFS's discoveries, WCC's
+// hooked roots, CDLP's new labels at N > 1, when they are fewer than a dense collective moves).
+extern "C" int gx_part_changes(const void *a, const void *b, uint64_t v0, uint64_t v1, int elem_bytes,
+                               uint64_t *words, int64_t *count, void *stream) {
+    if (!a || !words || !count) return fail(GX_NULL_POINTER, "gx_part_changes: null argument");
+    if (v0 > v1 || v1 >= (1ull << 31)) return fail(GX_INVALID_INDEX, "gx_part_changes: bad vertex range");
+    if (elem_bytes != 1 && elem_bytes != 4) return fail(GX_INVALID_VALUE, "gx_part_changes: elements of 1 or 4 bytes");
+    hipStream_t s = (hipStream_t)stream;
+    GX_HIP_TRY(hipMemsetAsync(count, 0, sizeof(int64_t), s));
+    if (v1 == v0) return GX_SUCCESS;
+    const dim3 grid(grid_for((v1 - v0 + kChPer - 1) / kChPer, kPartBlock, 4096));
+    if (elem_bytes == 1)
+        hipLaunchKernelGGL(k_part_changes<uint8_t>, grid, dim3(kPartBlock), 0, s, (const uint8_t *)a,
+                           (const uint8_t *)b, (int64_t)v0, (int64_t)v1, words, (unsigned long long *)count);
+    else
+        hipLaunchKernelGGL(k_part_changes<int32_t>, grid, dim3(kPartBlock), 0, s, (const int32_t *)a,
+                           (const int32_t *)b, (int64_t)v0, (int64_t)v1, words, (unsigned long long *)count);
+    return check_launch("k_part_changes");
+}
+
+extern "C" int gx_part_apply(const uint64_t *words, const int64_t *counts, int nranks, uint64_t stride, void *arr,
+                             int elem_bytes, int op, void *stream) {
+    if (!words || !counts || !arr) return fail(GX_NULL_POINTER, "gx_part_apply: null argument");
+    if (nranks < 1) return fail(GX_INVALID_VALUE, "gx_part_apply: nranks < 1");
+    if (elem_bytes != 1 && elem_bytes != 4) return fail(GX_INVALID_VALUE, "gx_part_apply: elements of 1 or 4 bytes");
+    if (op < 0 || op > 2 || (elem_bytes == 1 && op != 0))
+        return fail(GX_INVALID_VALUE, "gx_part_apply: op 0 (set), or 1 / 2 (min / max) on 4-byte elements");
+    if (stride == 0) return GX_SUCCESS;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(grid_for((uint64_t)nranks * stride, kPartBlock, 8192));
+    if (elem_bytes == 1)
+        hipLaunchKernelGGL(k_part_apply<uint8_t>, grid, dim3(kPartBlock), 0, s, words, counts, nranks, (int64_t)stride,
+                           (uint8_t *)arr, op);
+    else
+        hipLaunchKernelGGL(k_part_apply<int32_t>, grid, dim3(kPartBlock), 0, s, words, counts, nranks, (int64_t)stride,
+                           (int32_t *)arr, op);
+    return check_launch("k_part_apply");
+}

@@ -12,11 +12,17 @@ The drivers below run a list of *local ranks* in lock step against a `Comm`:
 A backend supplies the per-rank device steps; GpuBackend binds the gx_*_part_* entry
 points of libgx (include/gx.h).  Every state array is full length on every rank:
 
-    BFS  : expand owned frontier rows -> next (uint8)   all-reduce MAX, commit levels
-    WCC  : hook owned rows' edges     -> parent (int32) all-reduce MIN, compress
+    BFS  : expand owned frontier rows -> next (uint8)   the discoveries as words, or
+                                                          all-reduce MAX; commit levels
+    WCC  : hook owned rows' edges     -> parent (int32) the changed entries as words (MIN),
+                                                          or all-reduce MIN; compress
     SSSP : 1-D split (gx_sssp_split): relax the edges into owned vertices -> the improved
            owned vertices as (vertex, fp64 bits) pairs, all-gathered (sparse, per round)
-    CDLP : new labels of owned rows   -> all-gather of the owned slices
+    CDLP : new labels of owned rows   -> the changed labels as words, or all-gather of
+                                         the owned slices
+
+The words exchange (_exchange, gx_part_changes / gx_part_apply) moves 8 bytes per changed
+entry after a count all-gather, and falls back to the dense collective when that is more.
     LCC  : triangle counts of owned orientation sources -> all-reduce SUM, finish
 
 Results are the single-GPU results (BFS levels, canonical WCC labels, the SSSP fixed point,
@@ -25,6 +31,7 @@ the CDLP labels, exact LCC counts).  The reference has no distributed path.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import List, Sequence
 
@@ -120,6 +127,14 @@ class GpuBackend:
     def bfs_commit(self, nxt, level, cur, count):
         self.N.check(self.lib.gx_bfs_part_commit(self.g, self._p(nxt), self._p(level), cur, self._p(count),
                                                  self._s()), "gx_bfs_part_commit")
+
+    def changes(self, a, b, v0, v1, elem, words, count):
+        self.N.check(self.lib.gx_part_changes(self._p(a), self._p(b) if b is not None else None, v0, v1, elem,
+                                              self._p(words), self._p(count), self._s()), "gx_part_changes")
+
+    def apply(self, words, counts, nranks, stride, arr, elem, op):
+        self.N.check(self.lib.gx_part_apply(self._p(words), self._p(counts), nranks, stride, self._p(arr), elem, op,
+                                            self._s()), "gx_part_apply")
 
     def wcc_init(self, parent):
         self.N.check(self.lib.gx_wcc_part_init(self.g, self._p(parent), self._s()), "gx_wcc_part_init")
@@ -234,9 +249,59 @@ def _zeros(rank: LocalRank, n: int, dtype):
     return torch.zeros(n, dtype=dtype, device=rank.device)
 
 
+OP_SET, OP_MIN, OP_MAX = 0, 1, 2
+# _exchange: "auto" (the smaller of words and dense), "sparse", "dense" (GX_EXCHANGE)
+EXCHANGE = os.environ.get("GX_EXCHANGE", "auto")
+# bytes each rank sent per exchange kind since the last reset (bench.py reports them)
+STATS = {"rounds": 0, "word_rounds": 0, "word_bytes": 0, "dense_bytes": 0, "dense_only_bytes": 0}
+
+
+def reset_stats():
+    for k in STATS:
+        STATS[k] = 0
+
+
+def _exchange(ranks: List[LocalRank], comm, arrs, olds, spans, elem: int, op: int, dense_bytes: int, dense,
+              dsts=None) -> int:
+    """Frontier-sized exchange: every rank's entries of arrs[k] over spans[k] = (v0, v1) that
+    differ from olds[k] (None: from 0) leave as (v << 32 | value) words (gx_part_changes); the
+    counts are all-gathered (the one host read), then the first max-count words of every rank,
+    which every rank applies with `op` (gx_part_apply) to dsts[k] (default arrs[k]).  When
+    those words would outweigh the dense collective (`dense_bytes` per rank, e.g. 2 n for an
+    all-reduce of n bytes), `dense()` runs instead (EXCHANGE = "sparse" / "dense" forces one).
+    Returns the number of changes over all ranks (0: nothing changed anywhere)."""
+    import torch
+    nranks = getattr(comm, "world_size", None) or len(ranks)
+    # room for any rank's count: the all-gather sends the first max-count words of every rank
+    words = [_zeros(r, max(1, a.numel()), torch.int64) for r, a in zip(ranks, arrs)]
+    cnt = [_zeros(r, 1, torch.int64) for r in ranks]
+    for r, a, b, (v0, v1), w, c in zip(ranks, arrs, olds, spans, words, cnt):
+        r.backend.changes(a, b, v0, v1, elem, w, c)
+    counts = [_zeros(r, nranks, torch.int64) for r in ranks]
+    comm.all_gather(counts, cnt)
+    cw = counts[0].cpu().numpy()   # identical on every rank
+    m, tot = int(cw.max()), int(cw.sum())
+    STATS["rounds"] += 1
+    STATS["dense_only_bytes"] += dense_bytes   # what the dense collective alone would move
+    if m == 0:
+        return 0
+    if EXCHANGE == "dense" or (EXCHANGE != "sparse" and 8 * m * nranks > dense_bytes):
+        STATS["dense_bytes"] += dense_bytes
+        dense()
+        return tot
+    STATS["word_rounds"] += 1
+    STATS["word_bytes"] += 8 * m * nranks
+    gathered = [_zeros(r, m * nranks, torch.int64) for r in ranks]
+    comm.all_gather(gathered, [w[:m] for w in words])
+    for r, g, cs, a in zip(ranks, gathered, counts, dsts if dsts is not None else arrs):
+        r.backend.apply(g, cs, nranks, m, a, elem, op)
+    return tot
+
+
 def bfs(ranks: List[LocalRank], comm, n: int, src: int):
     """Level-synchronous top-down BFS; returns rank 0's level tensor (int64, INT64_MAX =
-    unreached)."""
+    unreached).  A level's discoveries travel as vertex words while they are fewer than the
+    dense all-reduce MAX of the n-byte `next` moves (_exchange)."""
     import torch
     level = [_zeros(r, n, torch.int64) for r in ranks]
     for r, lv in zip(ranks, level):
@@ -246,7 +311,8 @@ def bfs(ranks: List[LocalRank], comm, n: int, src: int):
         nxt = [_zeros(r, n, torch.uint8) for r in ranks]
         for r, lv, nx in zip(ranks, level, nxt):
             r.backend.bfs_expand(r.v0, r.v1, lv, cur, nx)
-        comm.all_reduce(nxt, "max")
+        _exchange(ranks, comm, nxt, [None] * len(ranks), [(0, n)] * len(ranks), 1, OP_SET, 2 * n,
+                  lambda: comm.all_reduce(nxt, "max"))
         count = [_zeros(r, 1, torch.int64) for r in ranks]
         for r, lv, nx, c in zip(ranks, level, nxt, count):
             r.backend.bfs_commit(nx, lv, cur, c)
@@ -258,21 +324,24 @@ def bfs(ranks: List[LocalRank], comm, n: int, src: int):
 
 def wcc(ranks: List[LocalRank], comm, n: int):
     """Min-root hooking over owned rows + MIN exchange of the forest; returns parent (int32):
-    the smallest vertex id of each component."""
+    the smallest vertex id of each component.  Every rank starts a round with the same forest,
+    so only the entries its hooks changed travel (_exchange, applied with MIN); a round in which
+    no rank changed anything is the fixed point (no separate flag collective)."""
     import torch
     parent = [_zeros(r, n, torch.int32) for r in ranks]
     for r, p in zip(ranks, parent):
         r.backend.wcc_init(p)
     while True:
+        prev = [p.clone() for p in parent]
         changed = [_zeros(r, 1, torch.int32) for r in ranks]
         for r, p, c in zip(ranks, parent, changed):
             r.backend.wcc_hook(r.v0, r.v1, p, c)
-        comm.all_reduce(parent, "min")
+        tot = _exchange(ranks, comm, parent, prev, [(0, n)] * len(ranks), 4, OP_MIN, 8 * n,
+                        lambda: comm.all_reduce(parent, "min"))
+        if tot == 0:
+            break
         for r, p in zip(ranks, parent):
             r.backend.wcc_compress(p)
-        comm.all_reduce(changed, "max")
-        if int(changed[0].item()) == 0:
-            break
     return parent[0]
 
 
@@ -337,15 +406,21 @@ def cdlp(ranks: List[LocalRank], comm, n: int, iters: int, ranges: np.ndarray):
             changed = [_zeros(r, 1, torch.int32) for r in ranks]
             for p, lb, nx, c in zip(parts, labels, nxt, changed):
                 p.step(lb, nx, c)
-            send = [_zeros(r, chunk, torch.int32) for r in ranks]
-            for r, nx, sd in zip(ranks, nxt, send):
-                sd[:r.v1 - r.v0].copy_(nx[r.v0:r.v1])
-            gathered = [_zeros(r, chunk * nranks, torch.int32) for r in ranks]
-            comm.all_gather(gathered, send)
-            for g, lb in zip(gathered, labels):
-                lb.copy_(torch.cat([g[k * chunk:k * chunk + sizes[k]] for k in range(nranks)]))
-            comm.all_reduce(changed, "max")
-            if int(changed[0].item()) == 0:   # fixed point (LAGraph_cdlp.c:328-332)
+
+            def dense():
+                send = [_zeros(r, chunk, torch.int32) for r in ranks]
+                for r, nx, sd in zip(ranks, nxt, send):
+                    sd[:r.v1 - r.v0].copy_(nx[r.v0:r.v1])
+                gathered = [_zeros(r, chunk * nranks, torch.int32) for r in ranks]
+                comm.all_gather(gathered, send)
+                for g, lb in zip(gathered, labels):
+                    lb.copy_(torch.cat([g[k * chunk:k * chunk + sizes[k]] for k in range(nranks)]))
+
+            # the owned labels that changed, set into every rank's labels (_exchange); the
+            # all-gather of the owned slices when more than half of them changed
+            tot = _exchange(ranks, comm, nxt, labels, [(r.v0, r.v1) for r in ranks], 4, OP_SET, 4 * n, dense,
+                            dsts=labels)
+            if tot == 0:   # fixed point (LAGraph_cdlp.c:328-332)
                 break
         return labels[0]
     finally:

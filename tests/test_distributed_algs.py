@@ -58,6 +58,28 @@ class NumpyBackend:
         lv[m] = cur + 1
         count.numpy()[0] += int(m.sum())
 
+    # sparse exchange (gx_part_changes / gx_part_apply)
+    def changes(self, a, b, v0, v1, elem, words, count):
+        av = a.numpy()[v0:v1].astype(np.int64)
+        bv = b.numpy()[v0:v1].astype(np.int64) if b is not None else np.zeros_like(av)
+        idx = np.flatnonzero(av != bv)
+        w = words.numpy()
+        w[:len(idx)] = ((idx + v0).astype(np.int64) << 32) | (av[idx] & 0xFFFFFFFF)
+        count.numpy()[0] = len(idx)
+
+    def apply(self, words, counts, nranks, stride, arr, elem, op):
+        w, cs, a = words.numpy(), counts.numpy(), arr.numpy()
+        for k in range(nranks):
+            x = w[k * stride:k * stride + int(cs[k])]
+            v = (x >> 32).astype(np.int64)
+            val = (x & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(a.dtype)
+            if op == 0:
+                a[v] = val
+            elif op == 1:
+                np.minimum.at(a, v, val)
+            else:
+                np.maximum.at(a, v, val)
+
     # WCC
     def wcc_init(self, parent):
         parent.numpy()[:] = np.arange(self.n, dtype=np.int32)
@@ -324,8 +346,11 @@ def test_gloo_world2_all_algorithms():
         _check(res, csr, directed)
 
 
-def test_local_comm_numpy_three_ranks():
-    """The lock-step drivers with LocalComm (what the single-GPU simulation uses)."""
+@pytest.mark.parametrize("exchange", ["auto", "sparse", "dense"])
+def test_local_comm_numpy_three_ranks(exchange, monkeypatch):
+    """The lock-step drivers with LocalComm (what the single-GPU simulation uses), with the
+    frontier-sized word exchange chosen by size, always, or never (distributed._exchange)."""
+    monkeypatch.setattr(D, "EXCHANGE", exchange)
     for csr, directed in _graphs():
         rng = D.vertex_ranges(csr.rowptr, 3)
         be = NumpyBackend(csr, directed)
@@ -335,7 +360,9 @@ def test_local_comm_numpy_three_ranks():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nranks", [1, 2, 3])
-def test_gpu_partitioned_simulated_ranks(nranks):
+@pytest.mark.parametrize("exchange", ["auto", "sparse", "dense"])
+def test_gpu_partitioned_simulated_ranks(nranks, exchange, monkeypatch):
+    monkeypatch.setattr(D, "EXCHANGE", exchange)
     from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context, Graph
     ctx = Context(0)
     dev = torch.device("cuda", 0)
