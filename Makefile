@@ -67,4 +67,5 @@ $(PROBE_DIR)/gx_pr_sorted.hip.o: $(CSRC)/gx_pr_sorted.hip $(wildcard $(CSRC)/*.h
 	mkdir -p $(PROBE_DIR)
 	$(HIPCC) $(HIPFLAGS) -DGX_PR_PROBES -c $< -o $@
 tools/probe/libgx.so: $(filter-out $(BUILD)/gx_pr_sorted.hip.o,$(HIP_OBJS)) $(PROBE_DIR)/gx_pr_sorted.hip.o $(HOST_OBJS)
+	@mkdir -p tools/probe
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -ldl -Wl,-soname,libgx.so

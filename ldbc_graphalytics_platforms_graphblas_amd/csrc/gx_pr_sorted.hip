@@ -249,7 +249,9 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // 8 gathers of columns >= 512 Ki folded into the first 512 Ki (the sparse tail as local as the
 // hub lines), 9 every gather folded into the first 64 Ki columns, 10 no entries at all (the
 // fixed costs: zeroing, epilogue, slabs), 11 as 3 (index loads and decode only).
-// gather_narrow takes all but 7 (which runs it unchanged).
+// gather_narrow takes all but 7 (which runs it unchanged); 12 (gather_narrow only) reads the
+// narrow entries' x from LDS (the accumulators at column mod 16 Ki): the launch if x came from
+// LDS instead of the texture path.
 template <int PROBE, int CP>   // CP bit 0: index loads non-temporal (bit 2: gather_narrow)
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
                                              double *acc, int64_t step64, int32_t k0 = 0, int32_t k1 = 0x7fffffff) {
@@ -474,11 +476,13 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
             col[k] = bk + ((sk >> (8 * (k & 3))) & 255u);
             bk += (tk >> (8 * (k & 3))) & 255u;
         }
-        if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11 || PROBE == 4 || PROBE == 8 || PROBE == 9) {
+        if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11 || PROBE == 4 || PROBE == 8 || PROBE == 9 ||
+                      PROBE == 12) {
 #pragma unroll
             for (int k = 0; k < kU; k++) {
                 const uint32_t c = col[k];
                 if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11) t.g[k] = (double)c;
+                else if constexpr (PROBE == 12) t.g[k] = acc[c & ((1u << kRowBits) - 1)];   // x from LDS
                 else if constexpr (PROBE == 4) t.g[k] = a.x_in[c & 4095u];
                 else if constexpr (PROBE == 8) t.g[k] = a.x_in[c >= (1u << 19) ? (c & ((1u << 19) - 1)) : c];
                 else t.g[k] = a.x_in[c & 65535u];
@@ -1910,7 +1914,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
 #define GX_PROBE_CASE(k) case k: if (p->cache_policy == 5) hipLaunchKernelGGL((k_pr_pull_units<false, k, 5>), dim3(nw), dim3(kBS), lds, s, a); \
                                  else hipLaunchKernelGGL((k_pr_pull_units<false, k>), dim3(nw), dim3(kBS), lds, s, a); break;
                 GX_PROBE_CASE(1) GX_PROBE_CASE(2) GX_PROBE_CASE(3) GX_PROBE_CASE(4) GX_PROBE_CASE(5) GX_PROBE_CASE(6) GX_PROBE_CASE(7)
-                GX_PROBE_CASE(8) GX_PROBE_CASE(9) GX_PROBE_CASE(10) GX_PROBE_CASE(11)
+                GX_PROBE_CASE(8) GX_PROBE_CASE(9) GX_PROBE_CASE(10) GX_PROBE_CASE(11) GX_PROBE_CASE(12)
 #undef GX_PROBE_CASE
                 default: hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
                 }

@@ -8,7 +8,7 @@ OUT=${1:-gpurun_out/pr_probe}
 G=${2:-SYN-7_5}
 mkdir -p "$OUT"
 for k in ${3:-0 1 2 3 4 5 6 7 0}; do
-  GX_LIB=tools/probe/libgx.so GX_PR_PROBE=$k timeout -k 10 300 python bench.py --graph "$G" --no-cpu-baseline \
+  GX_LIB=${PROBE_LIB:-tools/probe/libgx.so} GX_PR_PROBE=$k timeout -k 10 300 python bench.py --graph "$G" --no-cpu-baseline \
       --no-secondary --steps 10 --warmup 2 > "$OUT/probe_${G}_$k.json" 2> "$OUT/probe_${G}_$k.err" || exit 1
   python3 -c "
 import json; d=json.loads(open('$OUT/probe_${G}_$k.json').read().strip().splitlines()[-1]); r=d['roofline']
