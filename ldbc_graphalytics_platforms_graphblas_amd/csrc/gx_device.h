@@ -43,6 +43,11 @@ constexpr int kWave = 64;
 
 struct PrPart;
 
+// While set (this thread), device frees are deferred into the list: a hipFree waits for the
+// whole device, so a plan's temporaries freed while the columns upload on another stream
+// (gx_pagerank_csr) waited for the queued copies -- SYN-8_5's fused plan spent 21 ms there.
+inline thread_local std::vector<void *> *g_deferred_frees = nullptr;
+
 // RAII device allocation (hipMalloc / hipFree); size in elements of T.
 template <typename T>
 struct DBuf {
@@ -53,7 +58,10 @@ struct DBuf {
     DBuf &operator=(const DBuf &) = delete;
     ~DBuf() { release(); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            if (g_deferred_frees) g_deferred_frees->push_back(p);
+            else (void)hipFree(p);
+        }
         p = nullptr;
         n = 0;
     }
@@ -133,6 +141,9 @@ struct gx_ctx {
     static constexpr int kStageBufs = 4;
     void *staging[kStageBufs] = {};
     hipEvent_t stage_ev[kStageBufs] = {};
+    // the column upload's stream of gx_pagerank_csr (made by gx_init: creating a stream took
+    // 10-30 ms inside the processing time)
+    hipStream_t upload_stream = nullptr;
     // auxiliary streams for independent kernels of one step (fork/join by events), lazy
     hipStream_t aux[2] = {nullptr, nullptr};
     hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
@@ -167,7 +178,7 @@ namespace gx {
 // consumer waits for `ready` on the host, then for ev[c] on its own stream, so its kernels on
 // chunk c run while the later chunks are still crossing the host link.
 struct UploadJob {
-    hipStream_t us = nullptr;
+    hipStream_t us = nullptr;          // the context's upload stream (borrowed)
     std::vector<hipEvent_t> ev;
     std::vector<int64_t> end;          // entry index just past chunk c
     std::atomic<int> ready{0};
@@ -176,6 +187,7 @@ struct UploadJob {
     std::string msg;
     std::thread th;
     int device = 0;
+    DBuf<uint32_t> packed;             // 24-bit columns before k_unpack24 (freed with the job)
     ~UploadJob();
     int wait_chunk(int c);             // host: chunk c's copy is enqueued (GX_SUCCESS), or the job failed
     int join();                        // thread and stream finished; the job's error, if any

@@ -19,6 +19,8 @@
 #include <cctype>
 #include <cinttypes>
 #include <emmintrin.h>
+#include <smmintrin.h>
+#include <tmmintrin.h>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -579,6 +581,104 @@ bool host_narrow(const uint64_t *in, uint64_t count, uint64_t limit, int32_t *ou
     for (uint64_t k = (uint64_t)nq * 4; k < count; k++) {
         bad |= in[k] >= limit;
         out[k] = (int32_t)in[k];
+    }
+    return bad == 0;
+}
+
+// Columns < limit <= 2^24 as packed 24-bit little-endian values: entry k in bytes [3k, 3k+3)
+// of out, 16 entries = 12 words = three streaming 16-B stores (the upload's host->device bytes
+// fall by a quarter; k_unpack24 widens them on the device).  out holds ceil(3 count / 4) words.
+// SSE4.1 / SSSE3 body (EPYC hosts; checked at run time): per 4 entries the low dwords by two
+// shuffles, the unsigned max for the range check, a byte shuffle to 12 bytes, and four 12-byte
+// groups merged into three 16-byte streaming stores.
+__attribute__((target("sse4.1,ssse3"))) static bool pack24_simd(const uint64_t *in, int64_t ng, uint64_t limit,
+                                                                uint32_t *out) {
+    const __m128i sq = _mm_setr_epi8(0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14, -1, -1, -1, -1);
+    int bad = 0;
+#pragma omp parallel reduction(| : bad)
+    {
+        __m128i mx = _mm_setzero_si128(), hi = _mm_setzero_si128();
+#pragma omp for schedule(static)
+        for (int64_t q = 0; q < ng; q++) {
+            const __m128i *p = reinterpret_cast<const __m128i *>(in + 16 * q);
+            __m128i g[4];
+            for (int k = 0; k < 4; k++) {
+                const __m128i a = _mm_loadu_si128(p + 2 * k), b = _mm_loadu_si128(p + 2 * k + 1);
+                // dwords: a0lo a0hi a1lo a1hi | b0lo b0hi b1lo b1hi
+                const __m128i lo = _mm_unpacklo_epi64(_mm_shuffle_epi32(a, 0x08), _mm_shuffle_epi32(b, 0x08));
+                const __m128i h = _mm_unpacklo_epi64(_mm_shuffle_epi32(a, 0x0d), _mm_shuffle_epi32(b, 0x0d));
+                mx = _mm_max_epu32(mx, lo);
+                hi = _mm_or_si128(hi, h);
+                g[k] = _mm_shuffle_epi8(lo, sq);
+            }
+            __m128i *o = reinterpret_cast<__m128i *>(out + 12 * q);
+            _mm_stream_si128(o, _mm_or_si128(g[0], _mm_slli_si128(g[1], 12)));
+            _mm_stream_si128(o + 1, _mm_or_si128(_mm_srli_si128(g[1], 4), _mm_slli_si128(g[2], 8)));
+            _mm_stream_si128(o + 2, _mm_or_si128(_mm_srli_si128(g[2], 8), _mm_slli_si128(g[3], 4)));
+        }
+        _mm_sfence();
+        alignas(16) uint32_t m[4], h[4];
+        _mm_store_si128(reinterpret_cast<__m128i *>(m), mx);
+        _mm_store_si128(reinterpret_cast<__m128i *>(h), hi);
+        for (int k = 0; k < 4; k++) bad |= (h[k] != 0) | ((uint64_t)m[k] >= limit);
+    }
+    return bad == 0;
+}
+
+bool host_pack24(const uint64_t *in, uint64_t count, uint64_t limit, uint32_t *out) {
+    int bad = 0;
+    const int64_t ng = (int64_t)(count / 16);
+    const bool aligned = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    static const bool simd = __builtin_cpu_supports("sse4.1") && __builtin_cpu_supports("ssse3");
+    if (aligned && simd && ng > 0) {
+        bad |= !pack24_simd(in, ng, limit, out);
+        unsigned char *b = reinterpret_cast<unsigned char *>(out);
+        for (uint64_t k = (uint64_t)ng * 16; k < count; k++) {
+            bad |= in[k] >= limit;
+            const uint32_t c = (uint32_t)in[k];
+            b[3 * k] = (unsigned char)c;
+            b[3 * k + 1] = (unsigned char)(c >> 8);
+            b[3 * k + 2] = (unsigned char)(c >> 16);
+        }
+        return bad == 0;
+    }
+#pragma omp parallel reduction(| : bad)
+    {
+#pragma omp for schedule(static)
+        for (int64_t q = 0; q < ng; q++) {
+            const uint64_t *p = in + 16 * q;
+            uint32_t c[16];
+            uint64_t any = 0;
+            for (int j = 0; j < 16; j++) {
+                any |= p[j] >= limit;
+                c[j] = (uint32_t)p[j];
+            }
+            bad |= (int)any;
+            uint32_t w[12];
+            for (int g = 0; g < 4; g++) {
+                const uint32_t c0 = c[4 * g], c1 = c[4 * g + 1], c2 = c[4 * g + 2], c3 = c[4 * g + 3];
+                w[3 * g] = (c0 & 0xffffffu) | (c1 << 24);
+                w[3 * g + 1] = ((c1 >> 8) & 0xffffu) | (c2 << 16);
+                w[3 * g + 2] = ((c2 >> 16) & 0xffu) | (c3 << 8);
+            }
+            uint32_t *o = out + 12 * q;
+            if (aligned) {
+                _mm_stream_si128(reinterpret_cast<__m128i *>(o), _mm_loadu_si128(reinterpret_cast<const __m128i *>(w)));
+                _mm_stream_si128(reinterpret_cast<__m128i *>(o + 4), _mm_loadu_si128(reinterpret_cast<const __m128i *>(w + 4)));
+                _mm_stream_si128(reinterpret_cast<__m128i *>(o + 8), _mm_loadu_si128(reinterpret_cast<const __m128i *>(w + 8)));
+            } else {
+                std::memcpy(o, w, sizeof w);
+            }
+        }
+        _mm_sfence();
+    }
+    unsigned char *b = reinterpret_cast<unsigned char *>(out);
+    for (uint64_t k = (uint64_t)ng * 16; k < count; k++) {
+        bad |= in[k] >= limit;
+        const uint32_t c = (uint32_t)in[k];
+        b[3 * k] = (unsigned char)c;
+        b[3 * k + 1] = (unsigned char)(c >> 8);
+        b[3 * k + 2] = (unsigned char)(c >> 16);
     }
     return bad == 0;
 }

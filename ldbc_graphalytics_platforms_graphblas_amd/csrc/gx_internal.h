@@ -19,6 +19,7 @@ int fail(int code, const std::string &msg);
 // result hand-back, which sit inside the Graphalytics processing time ----
 // out[i] = (int32) in[i]; false if any in[i] >= limit.
 bool host_narrow(const uint64_t *in, uint64_t count, uint64_t limit, int32_t *out, bool nt = false);
+bool host_pack24(const uint64_t *in, uint64_t count, uint64_t limit, uint32_t *out);
 // parallel memcpy
 void host_copy(void *dst, const void *src, size_t bytes);
 // rp[i] <= rp[i+1] for all i < n

@@ -14,22 +14,25 @@ namespace gx {
 
 // GX_PLAN_TIMES=1: the host-side phase times of a plan build on stderr (the stream is
 // synchronised at every mark, so device phases are attributed too).  Diagnostics only.
+// GX_PLAN_TIMES=2: host time only, no stream synchronisation (the phases' host-side cost,
+// without perturbing a call whose upload overlaps its plan).
 struct PlanClock {
-    bool on = false;
+    bool on = false, sync = true;
     hipStream_t s = nullptr;
     const char *what = "";
     std::chrono::steady_clock::time_point t;
     PlanClock(const char *w, hipStream_t st) : s(st), what(w) {
         const char *e = std::getenv("GX_PLAN_TIMES");
         on = e && std::atoi(e) != 0;
+        sync = !(e && std::atoi(e) == 2);
         if (on) {
-            (void)hipStreamSynchronize(s);
+            if (sync) (void)hipStreamSynchronize(s);
             t = std::chrono::steady_clock::now();
         }
     }
     void mark(const char *phase) {
         if (!on) return;
-        (void)hipStreamSynchronize(s);
+        if (sync) (void)hipStreamSynchronize(s);
         const auto now = std::chrono::steady_clock::now();
         std::fprintf(stderr, "[plan %s] %-28s %8.2f ms\n", what, phase,
                      std::chrono::duration<double, std::milli>(now - t).count());

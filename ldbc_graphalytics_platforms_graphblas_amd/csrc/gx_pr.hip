@@ -1001,10 +1001,22 @@ extern "C" int gx_pagerank(gx_graph *g, double damping, int iters, double *rank)
     }
     if (g->directed) GX_TRY(ensure_transpose(g));
     if (!g->pr) {
+        // the plan's temporaries are freed once the upload is over (g_deferred_frees)
+        std::vector<void *> deferred;
+        // the upload thread narrows with half the host threads: the plan's host loops take the
+        // other half (all of them on top of the upload's ran some fused calls 115 ms, not 88)
+        const int saved_threads = host_threads();
+        if (g->job) {
+            g_deferred_frees = &deferred;
+            host_set_threads(std::max(1, saved_threads - std::max(1, saved_threads / 2)));
+        }
         const int rc = pr_single_plan(g, &g->pr);
+        g_deferred_frees = nullptr;
+        host_set_threads(saved_threads);
         if (g->job) {   // the plan has taken every chunk (or stopped early): the upload is over
             const int jrc = g->job->join();
             g->job.reset();
+            for (void *q : deferred) (void)hipFree(q);
             if (rc == GX_SUCCESS && jrc != GX_SUCCESS) return jrc;
         }
         if (rc != GX_SUCCESS) return rc;
@@ -1059,9 +1071,12 @@ extern "C" int gx_pagerank_csr(gx_ctx *ctx, const gx_csr *A, int directed, doubl
     const char *fe = std::getenv("GX_PR_FUSED");
     const bool fused = !directed && !(fe && std::atoi(fe) == 0);
     gx_graph *g = nullptr;
+    PlanClock clk("pagerank_csr", ctx->stream);
     if (fused) GX_TRY(graph_create_async(ctx, A, directed, &g));
     else GX_TRY(gx_graph_create(ctx, A, directed, &g));
+    clk.mark("graph (columns on their way)");
     const int rc = gx_pagerank(g, damping, iters, rank);
+    clk.mark("gx_pagerank");
     if (rc != GX_SUCCESS) {
         const std::string msg = gx_last_error();
         (void)gx_graph_free(g);   // joins an upload the call left running (an early error)

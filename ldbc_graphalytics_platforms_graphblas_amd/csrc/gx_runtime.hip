@@ -49,6 +49,7 @@ extern "C" int gx_init(int device, gx_ctx **out) {
                                     : std::string(prop.gcnArchName);
     ctx->num_cus = prop.multiProcessorCount;
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
     // two staging buffers now; GX_UPLOAD_BUFS > 2 adds the others on first use (ADVICE r04:
@@ -91,6 +92,10 @@ extern "C" int gx_free(gx_ctx *ctx) {
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->upload_stream) {
+        (void)hipStreamSynchronize(ctx->upload_stream);
+        (void)hipStreamDestroy(ctx->upload_stream);
+    }
     for (int i = 0; i < 2; i++) {
         if (ctx->aux[i]) (void)hipStreamDestroy(ctx->aux[i]);
         if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
@@ -272,10 +277,14 @@ namespace {
 struct NoAfter {
     int operator()(int) const { return GX_SUCCESS; }
 };
+// Entries per staging chunk: a multiple of `align` (16 for the packed 24-bit columns, whose
+// chunks must start on a 48-byte boundary).
+uint64_t stage_chunk(size_t elem, uint64_t align = 1) { return gx_ctx::kStageBytes / elem / align * align; }
+
 template <class Fill, class After = NoAfter>
 int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool *bad, hipStream_t us = nullptr,
-           After after = After(), bool sync = true) {
-    const uint64_t chunk = gx_ctx::kStageBytes / elem;
+           After after = After(), bool sync = true, uint64_t align = 1) {
+    const uint64_t chunk = stage_chunk(elem, align);
     hipStream_t s = us ? us : ctx->stream;
     *bad = false;
     int c = 0;
@@ -315,7 +324,8 @@ int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool 
         auto tc = clk::now();
         t_wait += std::chrono::duration<double, std::milli>(tb - ta).count();
         t_fill += std::chrono::duration<double, std::milli>(tc - tb).count();
-        GX_HIP_TRY(hipMemcpyAsync(dst + off * elem, ctx->staging[b], cnt * elem, hipMemcpyHostToDevice, s));
+        // (whole 4-byte words: a packed chunk's last entries may end inside one)
+        GX_HIP_TRY(hipMemcpyAsync(dst + off * elem, ctx->staging[b], (cnt * elem + 3) / 4 * 4, hipMemcpyHostToDevice, s));
         GX_HIP_TRY(hipEventRecord(ctx->stage_ev[b], s));
         GX_TRY(after(c));
     }
@@ -331,13 +341,70 @@ int upload(gx_ctx *ctx, char *dst, uint64_t count, size_t elem, Fill fill, bool 
 }  // namespace gx
 
 namespace gx {
+namespace {
+
+// Packed 24-bit columns (host_pack24) -> int32, entries [e0, e1): a thread per 4 entries, three
+// aligned words in (e0 is a multiple of 16), four out.
+__global__ __launch_bounds__(256) void k_unpack24(const uint32_t *__restrict__ words, int64_t e0, int64_t e1,
+                                                  int32_t *__restrict__ out) {
+    const int64_t ng = (e1 - e0 + 3) / 4;
+    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (int64_t)gridDim.x * 256) {
+        const int64_t e = e0 + 4 * g;
+        const uint32_t *w = words + 3 * (e / 4);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+        const int32_t c0 = (int32_t)(w0 & 0xffffffu), c1 = (int32_t)((w0 >> 24) | ((w1 & 0xffffu) << 8)),
+                      c2 = (int32_t)((w1 >> 16) | ((w2 & 0xffu) << 16)), c3 = (int32_t)(w2 >> 8);
+        if (e + 3 < e1) {
+            *reinterpret_cast<int4 *>(out + e) = make_int4(c0, c1, c2, c3);
+        } else {
+            out[e] = c0;
+            if (e + 1 < e1) out[e + 1] = c1;
+            if (e + 2 < e1) out[e + 2] = c2;
+        }
+    }
+}
+
+// GX_UPLOAD_PACK=0 keeps 4-byte columns; else columns of a graph with fewer than 2^24 vertices
+// travel as 3 bytes (a quarter fewer bytes over the host link, which bounds the upload: SYN-8_5
+// 2.51 GB at ~52 GB/s)
+bool pack_columns(uint64_t n) {
+    const char *e = std::getenv("GX_UPLOAD_PACK");
+    return n <= (1ull << 24) && !(e && std::atoi(e) == 0);
+}
+
+// The columns into dst (int32 on the device) on stream s: packed (pack_columns) through
+// `packed` (>= ceil(3 nnz / 4) + 4 words) and widened chunk by chunk, or narrowed on the host.
+// after(c) runs once chunk c is on the device as int32 (in stream order).
+template <class After>
+int upload_columns(gx_ctx *ctx, const uint64_t *cols, uint64_t nnz, uint64_t n, int32_t *dst, uint32_t *packed,
+                   bool nt, bool *bad, hipStream_t s, After after, bool sync) {
+    if (!packed)
+        return upload(ctx, reinterpret_cast<char *>(dst), nnz, 4,
+                      [&](uint64_t off, uint64_t cnt, void *buf) {
+                          return host_narrow(cols + off, cnt, n, static_cast<int32_t *>(buf), nt);
+                      }, bad, s, after, sync);
+    const uint64_t chunk = stage_chunk(3, 16);
+    return upload(ctx, reinterpret_cast<char *>(packed), nnz, 3,
+                  [&](uint64_t off, uint64_t cnt, void *buf) {
+                      return host_pack24(cols + off, cnt, n, static_cast<uint32_t *>(buf));
+                  }, bad, s,
+                  [&](int c) -> int {
+                      const uint64_t e0 = (uint64_t)c * chunk, e1 = std::min(nnz, e0 + chunk);
+                      hipLaunchKernelGGL(k_unpack24, dim3(grid_for((e1 - e0 + 3) / 4, 256, 8192)), dim3(256), 0, s,
+                                         packed, (int64_t)e0, (int64_t)e1, dst);
+                      GX_TRY(check_launch("k_unpack24"));
+                      return after(c);
+                  }, sync, 16);
+}
+
+}  // namespace
 
 UploadJob::~UploadJob() {
     if (th.joinable()) th.join();
     (void)hipSetDevice(device);
     if (us) (void)hipStreamSynchronize(us);
-    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-    if (us) (void)hipStreamDestroy(us);
+    for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
 }
 
 int UploadJob::wait_chunk(int c) {
@@ -365,6 +432,7 @@ int graph_create_async(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **ou
         return fail(GX_INVALID_VALUE, "gx_pagerank_csr: inconsistent row pointers");
     if (!host_monotone(A->rowptr, A->n)) return fail(GX_INVALID_VALUE, "gx_pagerank_csr: row pointers not monotone");
     GX_HIP_TRY(hipSetDevice(ctx->device));
+    PlanClock clk("graph_create_async", ctx->stream);
     const uint64_t n = A->n, nnz = A->nnz;
     std::unique_ptr<gx_graph> g(new gx_graph());
     g->ctx = ctx;
@@ -382,14 +450,16 @@ int graph_create_async(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **ou
                       host_copy(buf, reinterpret_cast<const int64_t *>(A->rowptr) + off, cnt * 8);
                       return true;
                   }, &bad));
+    clk.mark("buffers + row pointers");
     auto job = std::make_shared<UploadJob>();
     job->device = ctx->device;
-    GX_HIP_TRY(hipStreamCreateWithFlags(&job->us, hipStreamNonBlocking));
-    const uint64_t chunk = gx_ctx::kStageBytes / 4;
+    job->us = ctx->upload_stream;
+    // the packed buffer and the chunk events are made by the upload thread (creating ~75 events
+    // and a 1.9 GB buffer here cost the calling thread ~12 ms before its plan could start)
+    const bool pack = pack_columns(n);
+    const uint64_t chunk = pack ? stage_chunk(3, 16) : stage_chunk(4);
     for (uint64_t off = 0; off < nnz; off += chunk) {
-        hipEvent_t e = nullptr;
-        GX_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        job->ev.push_back(e);
+        job->ev.push_back(nullptr);
         job->end.push_back((int64_t)std::min(nnz, off + chunk));
     }
     const char *nt_env = std::getenv("GX_UPLOAD_NT");
@@ -402,22 +472,20 @@ int graph_create_async(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **ou
     // with 15 threads in 48 ms of copies); with every thread narrowing, the plan's host steps and
     // small copies ran 10x slower
     const int nthreads = std::max(1, host_threads() / 2);
-    j->th = std::thread([ctx, j, dst, cols, n, nnz, nt, nthreads] {
+    j->th = std::thread([ctx, j, dst, cols, n, nnz, nt, nthreads, pack] {
         host_set_threads(nthreads);
         bool bad2 = false;
         int rc = hipSetDevice(ctx->device) == hipSuccess ? GX_SUCCESS : fail(GX_DEVICE_ERROR, "hipSetDevice");
+        if (rc == GX_SUCCESS && pack) rc = j->packed.alloc((3 * nnz + 3) / 4 + 4);
         if (rc == GX_SUCCESS)
-            rc = upload(ctx, reinterpret_cast<char *>(dst), nnz, 4,
-                        [&](uint64_t off, uint64_t cnt, void *buf) {
-                            return host_narrow(cols + off, cnt, n, static_cast<int32_t *>(buf), nt);
-                        },
-                        &bad2, j->us,
-                        [&](int c) -> int {
-                            GX_HIP_TRY(hipEventRecord(j->ev[c], j->us));
-                            j->ready.store(c + 1, std::memory_order_release);
-                            return GX_SUCCESS;
-                        },
-                        false);
+            rc = upload_columns(ctx, cols, nnz, n, dst, pack ? j->packed.p : nullptr, nt, &bad2, j->us,
+                                [&](int c) -> int {
+                                    GX_HIP_TRY(hipEventCreateWithFlags(&j->ev[c], hipEventDisableTiming));
+                                    GX_HIP_TRY(hipEventRecord(j->ev[c], j->us));
+                                    j->ready.store(c + 1, std::memory_order_release);
+                                    return GX_SUCCESS;
+                                },
+                                false);
         if (rc == GX_SUCCESS && bad2) rc = fail(GX_INVALID_INDEX, "gx_pagerank_csr: column out of range");
         if (rc != GX_SUCCESS) {
             j->rc = rc;
@@ -467,10 +535,11 @@ extern "C" int gx_graph_create(gx_ctx *ctx, const gx_csr *A, int directed, gx_gr
                       host_copy(buf, reinterpret_cast<const int64_t *>(A->rowptr) + off, cnt * 8);
                       return true;
                   }, &bad));
-    GX_TRY(upload(ctx, reinterpret_cast<char *>(g->A.ci.p), nnz, 4,
-                  [&](uint64_t off, uint64_t cnt, void *buf) {
-                      return host_narrow(A->colidx + off, cnt, n, static_cast<int32_t *>(buf), nt);
-                  }, &bad));
+    {
+        DBuf<uint32_t> packed;
+        if (pack_columns(n)) GX_TRY(packed.alloc((3 * nnz + 3) / 4 + 4));
+        GX_TRY(upload_columns(ctx, A->colidx, nnz, n, g->A.ci.p, packed.p, nt, &bad, ctx->stream, NoAfter(), true));
+    }
     if (bad) return fail(GX_INVALID_INDEX, "gx_graph_create: column out of range");
     clk.mark("upload");
     if (g->weighted)

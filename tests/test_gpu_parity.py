@@ -607,7 +607,7 @@ def test_lcc_dense_core(ctx, monkeypatch, kmax):
         np.testing.assert_array_equal(gpu_run(ctx, g, "LCC"), O.lcc(g.csr, g.directed))
 
 
-@pytest.mark.parametrize("env", [{}, {"GX_PR_FUSED": "0"}, {"GX_PLAN_TIMES": "1"}])
+@pytest.mark.parametrize("env", [{}, {"GX_PR_FUSED": "0"}, {"GX_PLAN_TIMES": "1"}, {"GX_UPLOAD_PACK": "0"}])
 def test_pagerank_csr_fused(ctx, monkeypatch, env):
     """gx_pagerank_csr (bin/exe/pr's one call): the columns uploaded by a host thread while the
     plan takes each 8 Mi-entry chunk as it lands, from the source side.  Against the oracle at
@@ -623,6 +623,43 @@ def test_pagerank_csr_fused(ctx, monkeypatch, env):
     for csr, directed in graphs:
         got = A.LA_PR_csr(ctx, csr, directed, 0.85, 10)
         np.testing.assert_allclose(got, O.pagerank(csr, directed, 0.85, 10), rtol=PR_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("pack", ["1", "0"])
+def test_upload_packed_columns(ctx, monkeypatch, pack):
+    """Columns travel as packed 24-bit values (host_pack24, widened by k_unpack24) when the graph
+    has fewer than 2^24 vertices, else (or GX_UPLOAD_PACK=0) as 4 bytes: edge counts around the
+    16-entry packing groups and the 4-entry widening groups, columns at the 24-bit limit's
+    edges, and a graph of several staging chunks (11 M entries a chunk), through gx_graph_create
+    (BFS, SSSP, PR) and gx_pagerank_csr."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import CSR, csr_from_edges
+    monkeypatch.setenv("GX_UPLOAD_PACK", pack)
+    rng = np.random.default_rng(5)
+    for m in (1, 3, 4, 5, 15, 16, 17, 31, 33, 47, 49):
+        n = 300
+        src = rng.integers(0, n, m)
+        dst = rng.integers(0, n, m)
+        dst[0] = n - 1
+        csr = csr_from_edges(n, src, dst, rng.random(m) + 0.5, symmetric=False)
+        g = _G(csr, True)
+        s = int(src[0])
+        np.testing.assert_array_equal(gpu_run(ctx, g, "BFS", source=s), O.bfs(csr, s))
+        np.testing.assert_array_equal(gpu_run(ctx, g, "SSSP", source=s), O.sssp(csr, s))
+        np.testing.assert_allclose(gpu_run(ctx, g, "PR", damping=0.85, iters=5), O.pagerank(csr, True, 0.85, 5),
+                                   rtol=PR_RTOL, atol=0)
+    # columns up to 2^24 - 1: every byte of the packed value in use
+    n = (1 << 24) - 1
+    rp = np.array([0] + [2] * 2 + [4] * (n - 2), dtype=np.uint64)
+    ci = np.array([n - 1, 1 << 16, 0, (1 << 23) + 5], dtype=np.uint64)
+    big = CSR(n, rp, ci, None)
+    np.testing.assert_array_equal(gpu_run(ctx, _G(big, True), "BFS", source=0), O.bfs(big, 0))
+    np.testing.assert_allclose(gpu_run(ctx, _G(big, True), "PR", damping=0.85, iters=3), O.pagerank(big, True, 0.85, 3),
+                               rtol=PR_RTOL, atol=0)
+    csr = _rmat(21, 16, 9).csr   # ~ 60 M entries: several chunks
+    np.testing.assert_allclose(A.LA_PR_csr(ctx, csr, False, 0.85, 5), O.pagerank(csr, False, 0.85, 5,
+                                                                                   nthreads=O.max_threads()),
+                               rtol=PR_RTOL, atol=0)
 
 
 def test_pagerank_csr_rejects_bad_columns(ctx):
