@@ -251,7 +251,8 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // fixed costs: zeroing, epilogue, slabs), 11 as 3 (index loads and decode only).
 // gather_narrow takes all but 7 (which runs it unchanged); 12 (gather_narrow only) reads the
 // narrow entries' x from LDS (the accumulators at column mod 16 Ki): the launch if x came from
-// LDS instead of the texture path.
+// LDS instead of the texture path; 13 (gather_narrow only) two 16-B loads per lane per 8
+// entries (the instruction count of a layout loading each lane's column span once).
 template <int PROBE, int CP>   // CP bit 0: index loads non-temporal (bit 2: gather_narrow)
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
                                              double *acc, int64_t step64, int32_t k0 = 0, int32_t k1 = 0x7fffffff) {
@@ -476,7 +477,17 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
             col[k] = bk + ((sk >> (8 * (k & 3))) & 255u);
             bk += (tk >> (8 * (k & 3))) & 255u;
         }
-        if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11 || PROBE == 4 || PROBE == 8 || PROBE == 9 ||
+        if constexpr (PROBE == 13) {
+            // two 16-B loads per lane instead of eight 8-B gathers: the instruction count of a
+            // layout whose lane loads its entries' column span once
+            typedef double d2 __attribute__((ext_vector_type(2)));
+            const d2 *x2 = reinterpret_cast<const d2 *>(a.x_in);
+            const uint32_t p0 = col[0] >> 1;
+            const d2 A = x2[p0], B = x2[p0 + 1];
+#pragma unroll
+            for (int k = 0; k < kU; k++) t.g[k] = (k & 3) == 0 ? A.x : (k & 3) == 1 ? A.y : (k & 3) == 2 ? B.x : B.y;
+            (void)b0;
+        } else if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11 || PROBE == 4 || PROBE == 8 || PROBE == 9 ||
                       PROBE == 12) {
 #pragma unroll
             for (int k = 0; k < kU; k++) {
@@ -1915,6 +1926,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                                  else hipLaunchKernelGGL((k_pr_pull_units<false, k>), dim3(nw), dim3(kBS), lds, s, a); break;
                 GX_PROBE_CASE(1) GX_PROBE_CASE(2) GX_PROBE_CASE(3) GX_PROBE_CASE(4) GX_PROBE_CASE(5) GX_PROBE_CASE(6) GX_PROBE_CASE(7)
                 GX_PROBE_CASE(8) GX_PROBE_CASE(9) GX_PROBE_CASE(10) GX_PROBE_CASE(11) GX_PROBE_CASE(12)
+                GX_PROBE_CASE(13)
 #undef GX_PROBE_CASE
                 default: hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
                 }
