@@ -47,7 +47,9 @@ METRIC = "edges/sec (GTEPS) per algorithm at 1/2/4/8 GPUs; % HBM roofline"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)   # ~2.3 s of PageRank on SYN-8_5: the GPU is busy long enough to be seen
+    # ~9.5 s of PageRank on SYN-8_5: a timed region the driver's GPU-busy sampling can see (300
+    # steps, 1.9 s, was seen 0 % busy in all 10 samples of a 47 s run)
+    ap.add_argument("--steps", type=int, default=1500)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--damping", type=float, default=0.85)
