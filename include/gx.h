@@ -392,6 +392,11 @@ int gx_part_changes(const void *a, const void *b, uint64_t v0, uint64_t v1, int 
                     int64_t *count, void *stream);
 int gx_part_apply(const uint64_t *words, const int64_t *counts, int nranks, uint64_t stride, void *arr,
                   int elem_bytes, int op, void *stream);
+/* BFS's dense exchange as bits: next (n bytes, 16-B aligned) -> bits (ceil(n / 32) words); after
+ * an all-gather of every rank's words (rank r at gathered + r ceil(n / 32)), next[v] = 1 where
+ * any rank's bit v is set (1 / N the bytes of an all-reduce MAX of next at N ranks over 8). */
+int gx_part_pack_bits(const uint8_t *next, uint64_t n, uint32_t *bits, void *stream);
+int gx_part_or_bits(const uint32_t *gathered, int nranks, uint64_t n, uint8_t *next, void *stream);
 
 int gx_wcc_part_init(gx_graph *g, int32_t *parent, void *stream);
 int gx_wcc_part_hook(gx_graph *g, uint64_t v0, uint64_t v1, int32_t *parent, int *changed, void *stream);

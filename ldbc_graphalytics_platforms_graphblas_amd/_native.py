@@ -103,6 +103,8 @@ SIGNATURES = [
     ("gx_wcc_part_compress", C.c_int, [_P, _P, _P]),
     ("gx_part_changes", C.c_int, [_P, _P, C.c_uint64, C.c_uint64, C.c_int, _P, _P, _P]),
     ("gx_part_apply", C.c_int, [_P, _P, C.c_int, C.c_uint64, _P, C.c_int, C.c_int, _P]),
+    ("gx_part_pack_bits", C.c_int, [_P, C.c_uint64, _P, _P]),
+    ("gx_part_or_bits", C.c_int, [_P, C.c_int, C.c_uint64, _P, _P]),
     ("gx_sssp_split_create", C.c_int, [_P, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
     ("gx_sssp_split_delta", C.c_int, [_P, _DP]),
     ("gx_sssp_split_start", C.c_int, [_P, C.c_uint64, _P]),

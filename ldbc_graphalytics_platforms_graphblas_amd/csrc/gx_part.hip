@@ -180,6 +180,37 @@ __global__ __launch_bounds__(kPartBlock) void k_part_apply(const uint64_t *__res
     }
 }
 
+// BFS's dense exchange as bits: next (one byte per vertex) -> one bit per vertex, and the
+// ranks' gathered bitmaps OR-ed back into next.  A thread per 32-bit word.
+__global__ __launch_bounds__(kPartBlock) void k_part_pack_bits(const uint8_t *__restrict__ next, int64_t n,
+                                                               uint32_t *__restrict__ bits) {
+    const int64_t nw = (n + 31) / 32;
+    for (int64_t w = (int64_t)blockIdx.x * kPartBlock + threadIdx.x; w < nw; w += (int64_t)gridDim.x * kPartBlock) {
+        uint32_t b = 0;
+        const int64_t v0 = w * 32;
+        if (v0 + 32 <= n) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(next + v0);   // next is 16-B aligned (tensor)
+            const uint4 a = q[0], c = q[1];
+            const uint32_t x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int j = 0; j < 32; j++) b |= (uint32_t)(((x[j >> 2] >> (8 * (j & 3))) & 0xffu) != 0) << j;
+        } else {
+            for (int64_t v = v0; v < n; v++) b |= (uint32_t)(next[v] != 0) << (v - v0);
+        }
+        bits[w] = b;
+    }
+}
+
+__global__ __launch_bounds__(kPartBlock) void k_part_or_bits(const uint32_t *__restrict__ gathered, int nranks,
+                                                             int64_t n, uint8_t *__restrict__ next) {
+    const int64_t nw = (n + 31) / 32;
+    for (int64_t v = (int64_t)blockIdx.x * kPartBlock + threadIdx.x; v < n; v += (int64_t)gridDim.x * kPartBlock) {
+        uint32_t any = 0;
+        for (int r = 0; r < nranks; r++) any |= gathered[(int64_t)r * nw + v / 32] >> (v & 31);
+        next[v] = (uint8_t)(any & 1u);
+    }
+}
+
 // NULL is the null (default) stream -- torch's default stream -- not the context's stream.
 hipStream_t pick_stream(gx_graph *, void *stream) { return (hipStream_t)stream; }
 
@@ -294,4 +325,22 @@ extern "C" int gx_part_apply(const uint64_t *words, const int64_t *counts, int n
         hipLaunchKernelGGL(k_part_apply<int32_t>, grid, dim3(kPartBlock), 0, s, words, counts, nranks, (int64_t)stride,
                            (int32_t *)arr, op);
     return check_launch("k_part_apply");
+}
+
+extern "C" int gx_part_pack_bits(const uint8_t *next, uint64_t n, uint32_t *bits, void *stream) {
+    if (!next || !bits) return fail(GX_NULL_POINTER, "gx_part_pack_bits: null argument");
+    if ((reinterpret_cast<uintptr_t>(next) & 15) != 0) return fail(GX_INVALID_VALUE, "gx_part_pack_bits: next not 16-B aligned");
+    if (n == 0) return GX_SUCCESS;
+    hipLaunchKernelGGL(k_part_pack_bits, dim3(grid_for((n + 31) / 32, kPartBlock, 8192)), dim3(kPartBlock), 0,
+                       (hipStream_t)stream, next, (int64_t)n, bits);
+    return check_launch("k_part_pack_bits");
+}
+
+extern "C" int gx_part_or_bits(const uint32_t *gathered, int nranks, uint64_t n, uint8_t *next, void *stream) {
+    if (!gathered || !next) return fail(GX_NULL_POINTER, "gx_part_or_bits: null argument");
+    if (nranks < 1) return fail(GX_INVALID_VALUE, "gx_part_or_bits: nranks < 1");
+    if (n == 0) return GX_SUCCESS;
+    hipLaunchKernelGGL(k_part_or_bits, dim3(grid_for(n, kPartBlock, 8192)), dim3(kPartBlock), 0, (hipStream_t)stream,
+                       gathered, nranks, (int64_t)n, next);
+    return check_launch("k_part_or_bits");
 }

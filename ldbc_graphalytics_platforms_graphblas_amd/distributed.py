@@ -136,6 +136,13 @@ class GpuBackend:
         self.N.check(self.lib.gx_part_apply(self._p(words), self._p(counts), nranks, stride, self._p(arr), elem, op,
                                             self._s()), "gx_part_apply")
 
+    def pack_bits(self, nxt, bits):
+        self.N.check(self.lib.gx_part_pack_bits(self._p(nxt), nxt.numel(), self._p(bits), self._s()), "gx_part_pack_bits")
+
+    def or_bits(self, gathered, nranks, nxt):
+        self.N.check(self.lib.gx_part_or_bits(self._p(gathered), nranks, nxt.numel(), self._p(nxt), self._s()),
+                     "gx_part_or_bits")
+
     def wcc_init(self, parent):
         self.N.check(self.lib.gx_wcc_part_init(self.g, self._p(parent), self._s()), "gx_wcc_part_init")
 
@@ -306,13 +313,17 @@ def bfs(ranks: List[LocalRank], comm, n: int, src: int):
     level = [_zeros(r, n, torch.int64) for r in ranks]
     for r, lv in zip(ranks, level):
         r.backend.bfs_init(src, lv)
+    nranks = getattr(comm, "world_size", None) or len(ranks)
+    # dense form: the bitmaps all-gathered (n / 8 bytes from each rank), or, from 16 ranks on,
+    # the all-reduce MAX of next (~2 n bytes)
+    dense_bytes = min(2 * n, nranks * ((n + 31) // 32) * 4)
     cur = 0
     while True:
         nxt = [_zeros(r, n, torch.uint8) for r in ranks]
         for r, lv, nx in zip(ranks, level, nxt):
             r.backend.bfs_expand(r.v0, r.v1, lv, cur, nx)
-        _exchange(ranks, comm, nxt, [None] * len(ranks), [(0, n)] * len(ranks), 1, OP_SET, 2 * n,
-                  lambda: comm.all_reduce(nxt, "max"))
+        _exchange(ranks, comm, nxt, [None] * len(ranks), [(0, n)] * len(ranks), 1, OP_SET, dense_bytes,
+                  lambda: _bfs_dense(ranks, comm, nxt, n))
         count = [_zeros(r, 1, torch.int64) for r in ranks]
         for r, lv, nx, c in zip(ranks, level, nxt, count):
             r.backend.bfs_commit(nx, lv, cur, c)
@@ -320,6 +331,24 @@ def bfs(ranks: List[LocalRank], comm, n: int, src: int):
             break
         cur += 1
     return level[0]
+
+
+def _bfs_dense(ranks: List[LocalRank], comm, nxt, n: int) -> None:
+    """A level's discoveries exchanged densely: bit-packed and all-gathered (gx_part_pack_bits /
+    gx_part_or_bits) while that is smaller than the all-reduce MAX of the n-byte `next`."""
+    import torch
+    nranks = getattr(comm, "world_size", None) or len(ranks)
+    nw = (n + 31) // 32
+    if nranks * nw * 4 >= 2 * n:
+        comm.all_reduce(nxt, "max")
+        return
+    bits = [_zeros(r, nw, torch.int32) for r in ranks]
+    for r, nx, b in zip(ranks, nxt, bits):
+        r.backend.pack_bits(nx, b)
+    gathered = [_zeros(r, nw * nranks, torch.int32) for r in ranks]
+    comm.all_gather(gathered, bits)
+    for r, g, nx in zip(ranks, gathered, nxt):
+        r.backend.or_bits(g, nranks, nx)
 
 
 def wcc(ranks: List[LocalRank], comm, n: int):

@@ -80,6 +80,19 @@ class NumpyBackend:
             else:
                 np.maximum.at(a, v, val)
 
+    def pack_bits(self, nxt, bits):
+        nx = nxt.numpy() != 0
+        pad = np.zeros(bits.numel() * 32, dtype=bool)
+        pad[:len(nx)] = nx
+        bits.numpy()[:] = np.packbits(pad.reshape(-1, 32)[:, ::-1], axis=1, bitorder="big").view(">u4").astype(np.uint32).view(np.int32).ravel()
+
+    def or_bits(self, gathered, nranks, nxt):
+        n = nxt.numel()
+        w = gathered.numpy().view(np.uint32).reshape(nranks, -1)
+        anyb = np.bitwise_or.reduce(w, axis=0)
+        v = np.arange(n)
+        nxt.numpy()[:] = ((anyb[v // 32] >> (v % 32)) & 1).astype(np.uint8)
+
     # WCC
     def wcc_init(self, parent):
         parent.numpy()[:] = np.arange(self.n, dtype=np.int32)
