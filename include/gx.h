@@ -339,6 +339,12 @@ int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, 
  * adds) with the collective's ordering, so the N > 1 path runs, and is tested, on one GPU.
  * Mixed layouts (some contexts sharing a device, some not) are GX_INVALID_VALUE. */
 int gx_lcc_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, double *lcc);
+/* gx_multi_prepare: creates the collective clique of the ndev contexts (ncclCommInitAll, or the
+ * copy events of virtual devices) that the gx_*_multi calls on the same context list reuse, so
+ * a caller pays it ahead of its timed region, as it pays gx_init.  Optional: the first
+ * gx_*_multi call on a list creates it otherwise.  The clique lives until gx_free of any of
+ * its contexts.  Same argument rules as gx_lcc_multi. */
+int gx_multi_prepare(gx_ctx *const *ctxs, int ndev);
 
 /* ---------------------------------------------------------------------------------
  * Multi-GPU steps for the other algorithms.  The graph is replicated on

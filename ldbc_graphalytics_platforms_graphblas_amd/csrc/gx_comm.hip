@@ -672,6 +672,36 @@ struct Clique {
     }
 };
 
+// The cliques of gx_*_multi, one per context list, kept until one of its contexts is freed
+// (forget_cliques from gx_free): ncclCommInitAll took ~0.5 s of every call.  gx_multi_prepare
+// makes one ahead of the caller's timed region, as gx_init does for a context.
+struct CliqueCache {
+    std::mutex mu;
+    std::vector<std::pair<std::vector<gx_ctx *>, std::shared_ptr<Clique>>> list;
+};
+// never destroyed: an exit-time destructor would tear down communicators after the HIP runtime
+CliqueCache &cliques() {
+    static CliqueCache *c = new CliqueCache;
+    return *c;
+}
+
+int get_clique(gx_ctx *const *ctxs, int n, std::shared_ptr<Clique> *out) {
+    CliqueCache &cc = cliques();
+    std::lock_guard<std::mutex> lk(cc.mu);
+    const std::vector<gx_ctx *> key(ctxs, ctxs + n);
+    for (auto &e : cc.list)
+        if (e.first == key) {
+            *out = e.second;
+            return GX_SUCCESS;
+        }
+    auto c = std::make_shared<Clique>();
+    GX_TRY(c->init(ctxs, n));
+    cc.list.push_back({key, c});
+    *out = c;
+    return GX_SUCCESS;
+}
+
+
 // The in-process run of gx_pagerank_multi: one PrPart and its vectors per device.
 struct MultiRun {
     int ndev = 0;
@@ -733,8 +763,13 @@ int per_device(gx_ctx *const *ctxs, int ndev, F fn) {
 
 // Contexts must be all on distinct devices (an RCCL clique) or all on one device (virtual
 // devices exchanging by copies); RCCL is required for the former and for one context.
+int check_ctxs(gx_ctx *const *ctxs, int ndev, const char *who);
 int check_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, const char *who) {
     if (!ctxs || !A || (A->nnz && !A->colidx) || !A->rowptr) return fail(GX_NULL_POINTER, std::string(who) + ": null argument");
+    return check_ctxs(ctxs, ndev, who);
+}
+int check_ctxs(gx_ctx *const *ctxs, int ndev, const char *who) {
+    if (!ctxs) return fail(GX_NULL_POINTER, std::string(who) + ": null argument");
     if (ndev < 1) return fail(GX_INVALID_VALUE, std::string(who) + ": ndev < 1");
     for (int d = 0; d < ndev; d++)
         if (!ctxs[d]) return fail(GX_NULL_POINTER, std::string(who) + ": null context");
@@ -761,6 +796,29 @@ struct MultiGraphs {
 };
 
 }  // namespace
+
+void gx::forget_cliques(gx_ctx *ctx) {
+    std::vector<std::shared_ptr<Clique>> drop;  // destroyed outside the lock
+    CliqueCache &cc = cliques();
+    {
+        std::lock_guard<std::mutex> lk(cc.mu);
+        for (size_t i = 0; i < cc.list.size();) {
+            auto &k = cc.list[i].first;
+            if (std::find(k.begin(), k.end(), ctx) != k.end()) {
+                drop.push_back(std::move(cc.list[i].second));
+                cc.list.erase(cc.list.begin() + i);
+            } else {
+                i++;
+            }
+        }
+    }
+}
+
+extern "C" int gx_multi_prepare(gx_ctx *const *ctxs, int ndev) {
+    GX_TRY(check_ctxs(ctxs, ndev, "gx_multi_prepare"));
+    std::shared_ptr<Clique> clique;
+    return get_clique(ctxs, ndev, &clique);
+}
 
 extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, double damping,
                                  int iters, double *rank) {
@@ -827,8 +885,9 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         GX_HIP_TRY(hipMemsetAsync(M.xw[d]->p, 0, full * sizeof(double), s));
         return GX_SUCCESS;
     }));
-    Clique C;
-    GX_TRY(C.init(ctxs, ndev));
+    std::shared_ptr<Clique> clique;
+    GX_TRY(get_clique(ctxs, ndev, &clique));
+    Clique &C = *clique;
     const size_t cbytes = M.chunk * sizeof(double);
     auto gather = [&](std::vector<std::unique_ptr<DBuf<double>>> &dst) {
         return C.all_gather([&](int d) { return (const void *)M.xl[d]->p; }, [&](int d) { return (void *)dst[d]->p; },
@@ -928,8 +987,9 @@ extern "C" int gx_sssp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int
         GX_TRY(D[d].all.alloc(2 * maxown * (uint64_t)ndev));
         return GX_SUCCESS;
     }));
-    Clique C;
-    GX_TRY(C.init(ctxs, ndev));
+    std::shared_ptr<Clique> clique;
+    GX_TRY(get_clique(ctxs, ndev, &clique));
+    Clique &C = *clique;
     GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
     GX_HIP_TRY(hipHostMalloc((void **)&hc, 2 * (size_t)ndev * sizeof(uint64_t), hipHostMallocDefault));
     for (int d = 0; d < ndev; d++) {
@@ -1029,8 +1089,9 @@ extern "C" int gx_lcc_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int 
         return gx_lcc_part_counts(D[d].part, ranges[d], ranges[d + 1], D[d].tc.p, ctxs[d]->stream);
     }));
     {
-        Clique C;
-        GX_TRY(C.init(ctxs, ndev));
+        std::shared_ptr<Clique> clique;
+        GX_TRY(get_clique(ctxs, ndev, &clique));
+        Clique &C = *clique;
         GX_TRY(C.reduce_sum_u64([&](int d) { return D[d].tc.p; }, n));
     }
     GX_HIP_TRY(hipSetDevice(ctxs[0]->device));

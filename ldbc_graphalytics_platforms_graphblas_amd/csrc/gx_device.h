@@ -48,6 +48,9 @@ struct PrPart;
 // (gx_pagerank_csr) waited for the queued copies -- SYN-8_5's fused plan spent 21 ms there.
 inline thread_local std::vector<void *> *g_deferred_frees = nullptr;
 
+// Drops the cached gx_*_multi cliques that include ctx (gx_comm.hip); gx_free calls it first.
+void forget_cliques(gx_ctx *ctx);
+
 // RAII device allocation (hipMalloc / hipFree); size in elements of T.
 template <typename T>
 struct DBuf {

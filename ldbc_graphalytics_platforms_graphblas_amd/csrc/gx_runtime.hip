@@ -83,6 +83,7 @@ extern "C" int gx_init(int device, gx_ctx **out) {
 
 extern "C" int gx_free(gx_ctx *ctx) {
     if (!ctx) return GX_SUCCESS;
+    forget_cliques(ctx);
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (auto &p : ctx->pending) {

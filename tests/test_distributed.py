@@ -665,3 +665,39 @@ def test_multi_rejects_bad_contexts():
         arr = (C.c_void_p * 2)(None, None)
         assert getattr(N.lib(), fn)(arr, 2, C.byref(s), *args, N.as_dp(out)) == -2   # GX_NULL_POINTER
         assert getattr(N.lib(), fn)(arr, 0, C.byref(s), *args, N.as_dp(out)) == -3   # ndev < 1
+    arr = (C.c_void_p * 2)(None, None)
+    assert N.lib().gx_multi_prepare(arr, 2) == -2
+    assert N.lib().gx_multi_prepare(arr, 0) == -3
+    assert N.lib().gx_multi_prepare(None, 1) == -2
+
+
+@pytest.mark.gpu
+def test_multi_clique_cache():
+    """gx_multi_prepare makes the clique the gx_*_multi calls on the same context list reuse; a
+    call on another list (a subset) makes its own; gx_free of a member drops every clique holding
+    it, and the survivors still run (results bit-exact / rtol 1e-12 every time)."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    ctxs = [Context(0) for _ in range(4)]
+    try:
+        arr = (C.c_void_p * 4)(*[c.handle.value for c in ctxs])
+        N.check(N.lib().gx_multi_prepare(arr, 4), "gx_multi_prepare")
+        N.check(N.lib().gx_multi_prepare(arr, 4), "gx_multi_prepare")
+        csr = rmat(11, 8, 41, undirected=False)
+        want_pr = O.pagerank(csr, True, 0.85, 10)
+        want_lcc = O.lcc(csr, True)
+        for sub in (ctxs, ctxs, ctxs[:2], ctxs[:1]):
+            np.testing.assert_allclose(_multi_call("gx_pagerank_multi", sub, csr, 1, 0.85, 10), want_pr,
+                                       rtol=1e-12, atol=0)
+            assert np.array_equal(_multi_call("gx_lcc_multi", sub, csr, 1), want_lcc)
+        ctxs[3].close()
+        ctxs = ctxs[:3]
+        np.testing.assert_allclose(_multi_call("gx_pagerank_multi", ctxs, csr, 1, 0.85, 10), want_pr,
+                                   rtol=1e-12, atol=0)
+        ctxs[0].close()
+        ctxs = ctxs[1:]
+        assert np.array_equal(_multi_call("gx_lcc_multi", ctxs, csr, 1), want_lcc)
+    finally:
+        for c in ctxs:
+            c.close()
