@@ -252,7 +252,10 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // gather_narrow takes all but 7 (which runs it unchanged); 12 (gather_narrow only) reads the
 // narrow entries' x from LDS (the accumulators at column mod 16 Ki): the launch if x came from
 // LDS instead of the texture path; 13 (gather_narrow only) two 16-B loads per lane per 8
-// entries (the instruction count of a layout loading each lane's column span once).
+// entries (the instruction count of a layout loading each lane's column span once); 14
+// (gather_narrow only) only the first entry of each column run gathers, the rest read 0; 15 as 14
+// with the run's value handed on by ds_bpermute (correct results); 16 = the product kernel
+// under the probes' launch (no queue), the baseline for 12-15.
 template <int PROBE, int CP>   // CP bit 0: index loads non-temporal (bit 2: gather_narrow)
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
                                              double *acc, int64_t step64, int32_t k0 = 0, int32_t k1 = 0x7fffffff) {
@@ -442,6 +445,7 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
     struct Gt {
         double g[kU];
         uint32_t r[kU];
+        uint64_t m[kU];   // PROBE 15: the leader mask of instruction k
     };
     auto load = [&](Rd &d, int32_t i) {
         const int32_t sg = (u.unit + (i + i0) * u.nunits) * W + wave;
@@ -477,7 +481,24 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
             col[k] = bk + ((sk >> (8 * (k & 3))) & 255u);
             bk += (tk >> (8 * (k & 3))) & 255u;
         }
-        if constexpr (PROBE == 13) {
+        if constexpr (PROBE == 14 || PROBE == 15) {
+            // only the first entry of each column run gathers (a zero step repeats the previous
+            // sorted entry's column, lane 0 always loads): 14 leaves the others at 0, 15 hands the
+            // leader's value to them by ds_bpermute in the add stage (correct results)
+            const bool ntl = (CP & 4) && b0 >= a.nt_col;
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                const uint32_t st = ((k < 4 ? pk[0] : pk[1]) >> (8 * (k & 3))) & 255u;
+                const bool lead = st != 0u || lane == 0;
+                if constexpr (PROBE == 15) t.m[k] = __builtin_amdgcn_ballot_w64(lead);
+                double v = 0.0;
+                if (lead) {
+                    const double *xp = reinterpret_cast<const double *>(xb + (col[k] << 3));
+                    v = ntl ? __builtin_nontemporal_load(xp) : *xp;
+                }
+                t.g[k] = v;
+            }
+        } else if constexpr (PROBE == 13) {
             // two 16-B loads per lane instead of eight 8-B gathers: the instruction count of a
             // layout whose lane loads its entries' column span once
             typedef double d2 __attribute__((ext_vector_type(2)));
@@ -508,10 +529,17 @@ __device__ __forceinline__ void gather_narrow(const SortedArgs &a, const SortedU
         }
     };
     double rsum = 0.0;   // PROBE 1 / 3 / 11: register sum instead of the LDS adds
+    const uint64_t lane_le = (2ull << lane) - 1;   // PROBE 15: lanes 0..lane
     auto add = [&](const Gt &t) {
 #pragma unroll
         for (int k = 0; k < kU; k++) {
-            if constexpr (PROBE == 1 || PROBE == 3 || PROBE == 11) rsum += t.g[k];
+            if constexpr (PROBE == 15) {
+                const int src = 63 - __builtin_clzll(t.m[k] & lane_le);   // bit 0 is always set
+                const uint64_t b = __builtin_bit_cast(uint64_t, t.g[k]);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)b);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)(b >> 32));
+                atomicAdd(&acc[t.r[k]], __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo));
+            } else if constexpr (PROBE == 1 || PROBE == 3 || PROBE == 11) rsum += t.g[k];
             else if constexpr (PROBE == 5 || PROBE == 6) atomicAdd(&acc[threadIdx.x], t.g[k]);
             else atomicAdd(&acc[t.r[k]], t.g[k]);
         }
@@ -1926,7 +1954,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                                  else hipLaunchKernelGGL((k_pr_pull_units<false, k>), dim3(nw), dim3(kBS), lds, s, a); break;
                 GX_PROBE_CASE(1) GX_PROBE_CASE(2) GX_PROBE_CASE(3) GX_PROBE_CASE(4) GX_PROBE_CASE(5) GX_PROBE_CASE(6) GX_PROBE_CASE(7)
                 GX_PROBE_CASE(8) GX_PROBE_CASE(9) GX_PROBE_CASE(10) GX_PROBE_CASE(11) GX_PROBE_CASE(12)
-                GX_PROBE_CASE(13)
+                GX_PROBE_CASE(13) GX_PROBE_CASE(14) GX_PROBE_CASE(15) GX_PROBE_CASE(16)
 #undef GX_PROBE_CASE
                 default: hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
                 }
