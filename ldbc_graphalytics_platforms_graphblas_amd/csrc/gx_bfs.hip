@@ -130,25 +130,36 @@ __device__ __forceinline__ void bfs_bottomup(const int64_t *__restrict__ rpi,
                                                             const int64_t *__restrict__ rpo,
                                                             const uint64_t *__restrict__ fb, int64_t n,
                                                             int32_t *level, int32_t depth,
-                                                            unsigned long long *counters /* found, edges */) {
+                                                            unsigned long long *counters /* found, edges */,
+                                                            uint64_t *fbn = nullptr) {
     __shared__ unsigned long long red[2][kBfsBlock / kWave];
     unsigned long long edges = 0, found = 0;
-    for (int64_t v = (int64_t)blockIdx.x * kBfsBlock + threadIdx.x; v < n; v += (int64_t)gridDim.x * kBfsBlock) {
-        if (level[v] >= 0) continue;
-        const int64_t b = rpi[v], e = rpi[v + 1];
+    // uniform trip count: a wave covers 64 aligned consecutive vertices per round, so with fbn
+    // its ballot of the vertices found is the next level's frontier word (no bitmap pass)
+    const int64_t stride = (int64_t)gridDim.x * kBfsBlock;
+    const int64_t nround = (n + stride - 1) / stride;
+    for (int64_t r = 0; r < nround; r++) {
+        const int64_t v = r * stride + (int64_t)blockIdx.x * kBfsBlock + threadIdx.x;
         bool take = false;
-        for (int64_t k = b; k < e && !take; k += 4) {
-            const int32_t u0 = cii[k];
-            const int32_t u1 = cii[min(k + 1, e - 1)];
-            const int32_t u2 = cii[min(k + 2, e - 1)];
-            const int32_t u3 = cii[min(k + 3, e - 1)];
-            // all four probes issue (no short-circuit), then one test
-            take = (in_frontier(fb, u0) | in_frontier(fb, u1) | in_frontier(fb, u2) | in_frontier(fb, u3)) != 0;
+        if (v < n && level[v] < 0) {
+            const int64_t b = rpi[v], e = rpi[v + 1];
+            for (int64_t k = b; k < e && !take; k += 4) {
+                const int32_t u0 = cii[k];
+                const int32_t u1 = cii[min(k + 1, e - 1)];
+                const int32_t u2 = cii[min(k + 2, e - 1)];
+                const int32_t u3 = cii[min(k + 3, e - 1)];
+                // all four probes issue (no short-circuit), then one test
+                take = (in_frontier(fb, u0) | in_frontier(fb, u1) | in_frontier(fb, u2) | in_frontier(fb, u3)) != 0;
+            }
+            if (take) {
+                level[v] = depth + 1;
+                edges += (unsigned long long)(rpo[v + 1] - rpo[v]);
+                found++;
+            }
         }
-        if (take) {
-            level[v] = depth + 1;
-            edges += (unsigned long long)(rpo[v + 1] - rpo[v]);
-            found++;
+        if (fbn) {
+            const uint64_t m = __ballot(take);
+            if ((threadIdx.x & (kWave - 1)) == 0 && v < n) fbn[v >> 6] = m;
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -252,7 +263,9 @@ struct BfsState {
     int32_t need_queue;    // this top-down level first rebuilds q[qi] from `level`
     int32_t bottom_up;
     int32_t has_in;
-    int32_t pad;
+    int32_t fbi;           // bottom-up reads frontier bitmap fb[fbi] and writes the next into fb[fbi ^ 1]
+    int32_t fb_ready;      // fb[fbi] already holds this level's frontier (the last level was bottom-up)
+    int32_t nextbits;      // bottom-up writes the next bitmap (GX_BFS_NEXTBITS, default on)
     unsigned long long mf, mu, fsize, n;
     uint32_t qcnt[2];
     unsigned long long nedges;
@@ -270,7 +283,12 @@ __global__ void k_bfs_plan(BfsState *st) {
             next_size = st->bucnt[0];
             next_edges = st->bucnt[1];
             st->have_queue = 0;
+            if (st->nextbits) {
+                st->fbi ^= 1;
+                st->fb_ready = 1;
+            }
         } else {
+            st->fb_ready = 0;
             st->qi ^= 1;
             next_size = st->qcnt[st->qi];
             next_edges = st->nedges;
@@ -306,18 +324,20 @@ __global__ void k_bfs_plan(BfsState *st) {
 }
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_bitmap_dev(const int32_t *__restrict__ level, int64_t n,
-                                                              const BfsState *st, uint64_t *fb) {
-    if (st->mode != 2) return;
-    bfs_bitmap(level, n, st->depth, fb);
+                                                              const BfsState *st, uint64_t *fb0, uint64_t *fb1) {
+    if (st->mode != 2 || st->fb_ready) return;
+    bfs_bitmap(level, n, st->depth, st->fbi ? fb1 : fb0);
 }
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup_dev(const int64_t *__restrict__ rpi,
                                                                 const int32_t *__restrict__ cii,
                                                                 const int64_t *__restrict__ rpo,
-                                                                const uint64_t *__restrict__ fb, int64_t n,
+                                                                uint64_t *fb0, uint64_t *fb1, int64_t n,
                                                                 int32_t *level, BfsState *st) {
     if (st->mode != 2) return;
-    bfs_bottomup(rpi, cii, rpo, fb, n, level, st->depth, st->bucnt);
+    const int i = st->fbi;
+    bfs_bottomup(rpi, cii, rpo, i ? fb1 : fb0, n, level, st->depth, st->bucnt,
+                 st->nextbits ? (i ? fb0 : fb1) : nullptr);
 }
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue_dev(const int64_t *__restrict__ rp,
@@ -371,7 +391,8 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
     DBuf<unsigned long long> nedges;
     DBuf<uint64_t> fbits;
     DBuf<unsigned long long> bucnt;
-    GX_TRY(fbits.alloc((n + 63) / 64));
+    GX_TRY(fbits.alloc(2 * ((n + 63) / 64)));   // two bitmaps: the device-driven path alternates them
+    uint64_t *const fb1 = fbits.p + (n + 63) / 64;
     GX_TRY(bucnt.alloc(2));
     const uint64_t qcap = (uint64_t)n + g->nnz / kChunk + 64;   // sum over vertices of ceil(deg / kChunk)
     GX_TRY(level.alloc(n));
@@ -407,6 +428,8 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         h.mf = (unsigned long long)dsrc;
         h.mu = g->nnz;
         h.fsize = (unsigned long long)((dsrc + kChunk - 1) / kChunk);
+        const char *nb = std::getenv("GX_BFS_NEXTBITS");
+        h.nextbits = !nb || std::atoi(nb) != 0;
         GX_HIP_TRY(hipMemcpyAsync(st.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, &st.p->qcnt[0],
                            (int32_t)src);
@@ -417,7 +440,13 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         std::unique_ptr<int32_t, void (*)(int32_t *)> done_guard(h_done, [](int32_t *p) { (void)hipHostFree(p); });
         GX_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         std::unique_ptr<ihipEvent_t, void (*)(hipEvent_t)> ev_guard(ev, [](hipEvent_t e) { (void)hipEventDestroy(e); });
-        const unsigned vgrid = grid_for(n, kBfsBlock, 8192);
+        // grids of the kernels that run idle on the levels of the other direction: an idle
+        // 8192-workgroup launch cost 2.6-3.0 us, a 2048 one 0.9 (r04_bfs_kernel_stats.csv);
+        // every kernel is a grid-stride loop (GX_BFS_GRID overrides)
+        const char *ge = std::getenv("GX_BFS_GRID");
+        const unsigned gcap = ge ? (unsigned)std::max(1, std::atoi(ge)) : 2048u;
+        const unsigned vgrid = grid_for(n, kBfsBlock, gcap);
+        const unsigned tgrid = std::min(8192u, gcap);
         const unsigned qgrid = (unsigned)std::min<int64_t>((n + kQTile - 1) / kQTile, 2048);
         auto enqueue = [&](int k) -> int {
             for (int i = 0; i < k; i++) {
@@ -425,15 +454,15 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
                 if (in) {
                     KTimer kt(ctx, "bfs_bottomup", s);
                     hipLaunchKernelGGL(k_bfs_bitmap_dev, dim3(vgrid), dim3(kBfsBlock), 0, s, level.p, n, st.p,
-                                       fbits.p);
+                                       fbits.p, fb1);
                     hipLaunchKernelGGL(k_bfs_bottomup_dev, dim3(bu_grid), dim3(kBfsBlock), 0, s, in->rp.p, in->ci.p,
-                                       g->A.rp.p, fbits.p, n, level.p, st.p);
+                                       g->A.rp.p, fbits.p, fb1, n, level.p, st.p);
                 }
                 KTimer kt(ctx, "bfs_topdown", s);
                 if (in)
                     hipLaunchKernelGGL(k_bfs_level_queue_dev, dim3(qgrid), dim3(kBfsBlock), 0, s, g->A.rp.p, level.p,
                                        n, st.p, q0.p, q1.p);
-                hipLaunchKernelGGL(k_bfs_topdown_dev, dim3(8192), dim3(kBfsBlock), 0, s, g->A.rp.p, g->A.ci.p,
+                hipLaunchKernelGGL(k_bfs_topdown_dev, dim3(tgrid), dim3(kBfsBlock), 0, s, g->A.rp.p, g->A.ci.p,
                                    level.p, st.p, q0.p, q1.p);
             }
             return check_launch("k_bfs_topdown_dev");

@@ -526,13 +526,20 @@ def test_wcc_sampling_modes(ctx, monkeypatch, env):
     np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "WCC"), O.wcc(csr))
 
 
-@pytest.mark.parametrize("device", ["1", "0"])
-def test_bfs_level_driver(ctx, monkeypatch, device):
+@pytest.mark.parametrize("device,nextbits,grid", [("1", "1", None), ("1", "0", None), ("1", "1", "3"),
+                                                  ("1", "0", "8192"), ("0", "1", None)])
+def test_bfs_level_driver(ctx, monkeypatch, device, nextbits, grid):
     """BFS levels planned on the device (GX_BFS_DEVICE=1, batches of levels, done flag read a
     batch late) or by the host: the oracle's levels on power-law graphs (top-down and
-    bottom-up levels), a 3 000-level chain (many batches) and an isolated source."""
+    bottom-up levels), a 3 000-level chain (many batches) and an isolated source.  On the device
+    path a bottom-up level writes the next level's frontier bitmap (GX_BFS_NEXTBITS=1) or a
+    bitmap pass rebuilds it from the levels; GX_BFS_GRID caps the grid-stride kernels' grids
+    (3 workgroups: many rounds per wave)."""
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
     monkeypatch.setenv("GX_BFS_DEVICE", device)
+    monkeypatch.setenv("GX_BFS_NEXTBITS", nextbits)
+    if grid:
+        monkeypatch.setenv("GX_BFS_GRID", grid)
     for g in (_rmat(14, 16, 4), _rmat(12, 8, 3, undirected=False)):
         s = _src(g)
         np.testing.assert_array_equal(gpu_run(ctx, g, "BFS", source=s), O.bfs(g.csr, s))
