@@ -196,8 +196,14 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__res
 // kQTile consecutive vertices: count the tile's items, one atomicAdd for its base, write.
 constexpr int64_t kQTile = 4096;
 
+// With fb (the frontier bitmap a bottom-up level left) the frontier test reads n/8 bytes of
+// bitmap words (one line per wave) instead of the n int32 levels, twice.
 __device__ __forceinline__ void bfs_level_queue(const int64_t *__restrict__ rp, const int32_t *__restrict__ level,
-                                                int64_t n, int32_t depth, uint64_t *queue, uint32_t *qcount) {
+                                                int64_t n, int32_t depth, uint64_t *queue, uint32_t *qcount,
+                                                const uint64_t *__restrict__ fb = nullptr) {
+    auto at_depth = [&](int64_t v) -> bool {
+        return fb ? ((fb[v >> 6] >> (v & 63)) & 1ull) != 0 : level[v] == depth;
+    };
     __shared__ uint32_t wsum[kBfsBlock / kWave];
     __shared__ uint32_t tile_base;
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -205,7 +211,7 @@ __device__ __forceinline__ void bfs_level_queue(const int64_t *__restrict__ rp, 
         const int64_t t1 = min(t0 + kQTile, n);
         uint32_t mine = 0;
         for (int64_t v = t0 + threadIdx.x; v < t1; v += kBfsBlock)
-            if (level[v] == depth) mine += chunks_of(rp[v + 1] - rp[v]);
+            if (at_depth(v)) mine += chunks_of(rp[v + 1] - rp[v]);
         for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off, kWave);
         if (lane == 0) wsum[w] = mine;
         __syncthreads();
@@ -219,7 +225,7 @@ __device__ __forceinline__ void bfs_level_queue(const int64_t *__restrict__ rp, 
         uint32_t base = tile_base;
         for (int64_t v0 = t0; v0 < t1; v0 += kBfsBlock) {
             const int64_t v = v0 + threadIdx.x;
-            const uint32_t k = (v < t1 && level[v] == depth) ? chunks_of(rp[v + 1] - rp[v]) : 0u;
+            const uint32_t k = (v < t1 && at_depth(v)) ? chunks_of(rp[v + 1] - rp[v]) : 0u;
             uint32_t x = k;   // inclusive scan over the workgroup: waves, then wave totals
 #pragma unroll
             for (int off = 1; off < kWave; off <<= 1) {
@@ -266,6 +272,8 @@ struct BfsState {
     int32_t fbi;           // bottom-up reads frontier bitmap fb[fbi] and writes the next into fb[fbi ^ 1]
     int32_t fb_ready;      // fb[fbi] already holds this level's frontier (the last level was bottom-up)
     int32_t nextbits;      // bottom-up writes the next bitmap (GX_BFS_NEXTBITS, default on)
+    int32_t qbits;         // a top-down queue rebuild reads that bitmap (GX_BFS_QBITS, default on)
+    int32_t pad2;
     unsigned long long mf, mu, fsize, n;
     uint32_t qcnt[2];
     unsigned long long nedges;
@@ -342,10 +350,12 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup_dev(const int64_t *_
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue_dev(const int64_t *__restrict__ rp,
                                                                    const int32_t *__restrict__ level, int64_t n,
-                                                                   BfsState *st, uint64_t *q0, uint64_t *q1) {
+                                                                   BfsState *st, uint64_t *q0, uint64_t *q1,
+                                                                   const uint64_t *fb0, const uint64_t *fb1) {
     if (st->mode != 1 || !st->need_queue) return;
     const int qi = st->qi;
-    bfs_level_queue(rp, level, n, st->depth, qi ? q1 : q0, &st->qcnt[qi]);
+    bfs_level_queue(rp, level, n, st->depth, qi ? q1 : q0, &st->qcnt[qi],
+                    st->fb_ready && st->qbits ? (st->fbi ? fb1 : fb0) : nullptr);
 }
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown_dev(const int64_t *__restrict__ rp,
@@ -430,6 +440,8 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         h.fsize = (unsigned long long)((dsrc + kChunk - 1) / kChunk);
         const char *nb = std::getenv("GX_BFS_NEXTBITS");
         h.nextbits = !nb || std::atoi(nb) != 0;
+        const char *qb = std::getenv("GX_BFS_QBITS");
+        h.qbits = !qb || std::atoi(qb) != 0;
         GX_HIP_TRY(hipMemcpyAsync(st.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, &st.p->qcnt[0],
                            (int32_t)src);
@@ -461,7 +473,7 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
                 KTimer kt(ctx, "bfs_topdown", s);
                 if (in)
                     hipLaunchKernelGGL(k_bfs_level_queue_dev, dim3(qgrid), dim3(kBfsBlock), 0, s, g->A.rp.p, level.p,
-                                       n, st.p, q0.p, q1.p);
+                                       n, st.p, q0.p, q1.p, fbits.p, fb1);
                 hipLaunchKernelGGL(k_bfs_topdown_dev, dim3(tgrid), dim3(kBfsBlock), 0, s, g->A.rp.p, g->A.ci.p,
                                    level.p, st.p, q0.p, q1.p);
             }

@@ -584,12 +584,22 @@ __global__ __launch_bounds__(256) void k_hub_copy(const int64_t *__restrict__ rp
     }
 }
 
-// out[order[x]] = in[x]: the copy's results in the caller's order.  A scatter, not a gather
-// through perm: the reads stream and the random accesses are stores, which nothing waits for.
+// out[order[x]] = in[x]: the copy's results in the caller's order as a scatter (GX_REMAP=scatter).
+// Measured slower than the gather below (BFS on SYN-g500-22 0.346-0.354 against 0.313-0.331 ms
+// per run, SSSP on SYN-8_5 6.04-6.06 against 5.98-5.99; profiles/r05_remap_ab.txt): its random
+// 4- or 8-byte stores write partial lines.
 template <typename T>
 __global__ void k_scatter_by(const T *__restrict__ in, const int32_t *__restrict__ order, int64_t n, T *__restrict__ out) {
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x)
         out[order[x]] = in[x];
+}
+
+// out[x] = in[perm[x]]: the remap as a gather (the default): coalesced stores of whole lines,
+// random reads served by the Infinity Cache.
+template <typename T>
+__global__ void k_gather_by(const T *__restrict__ in, const int32_t *__restrict__ perm, int64_t n, T *__restrict__ out) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x)
+        out[x] = in[perm[x]];
 }
 
 void free_copy(gx_graph *h) { (void)gx_graph_free(h); }
@@ -697,6 +707,18 @@ int remap_out(gx_graph *g, const void *buf, int elem, hipStream_t s, const void 
     const int64_t n = (int64_t)g->n;
     void *tmp = g->remap_tmp.p;   // n words, allocated with the copy
     const unsigned grid = grid_for((uint64_t)n, 256, 8192);
+    const char *re = std::getenv("GX_REMAP");
+    if (!(re && std::strcmp(re, "scatter") == 0)) {
+        if (elem == 8)
+            hipLaunchKernelGGL(k_gather_by<uint64_t>, dim3(grid), dim3(256), 0, s, static_cast<const uint64_t *>(buf),
+                               g->out_perm, n, static_cast<uint64_t *>(tmp));
+        else
+            hipLaunchKernelGGL(k_gather_by<uint32_t>, dim3(grid), dim3(256), 0, s, static_cast<const uint32_t *>(buf),
+                               g->out_perm, n, static_cast<uint32_t *>(tmp));
+        GX_TRY(check_launch("k_gather_by"));
+        *res = tmp;
+        return GX_SUCCESS;
+    }
     if (elem == 8)
         hipLaunchKernelGGL(k_scatter_by<uint64_t>, dim3(grid), dim3(256), 0, s, static_cast<const uint64_t *>(buf),
                            g->out_order, n, static_cast<uint64_t *>(tmp));

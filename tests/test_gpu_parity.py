@@ -526,18 +526,21 @@ def test_wcc_sampling_modes(ctx, monkeypatch, env):
     np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "WCC"), O.wcc(csr))
 
 
-@pytest.mark.parametrize("device,nextbits,grid", [("1", "1", None), ("1", "0", None), ("1", "1", "3"),
-                                                  ("1", "0", "8192"), ("0", "1", None)])
-def test_bfs_level_driver(ctx, monkeypatch, device, nextbits, grid):
+@pytest.mark.parametrize("device,nextbits,grid,qbits", [("1", "1", None, "1"), ("1", "1", None, "0"),
+                                                        ("1", "0", None, "1"), ("1", "1", "3", "1"),
+                                                        ("1", "0", "8192", "1"), ("0", "1", None, "1")])
+def test_bfs_level_driver(ctx, monkeypatch, device, nextbits, grid, qbits):
     """BFS levels planned on the device (GX_BFS_DEVICE=1, batches of levels, done flag read a
     batch late) or by the host: the oracle's levels on power-law graphs (top-down and
     bottom-up levels), a 3 000-level chain (many batches) and an isolated source.  On the device
     path a bottom-up level writes the next level's frontier bitmap (GX_BFS_NEXTBITS=1) or a
-    bitmap pass rebuilds it from the levels; GX_BFS_GRID caps the grid-stride kernels' grids
-    (3 workgroups: many rounds per wave)."""
+    bitmap pass rebuilds it from the levels, and a top-down level after it builds its queue from
+    that bitmap (GX_BFS_QBITS=1) or from the levels; GX_BFS_GRID caps the grid-stride kernels'
+    grids (3 workgroups: many rounds per wave)."""
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
     monkeypatch.setenv("GX_BFS_DEVICE", device)
     monkeypatch.setenv("GX_BFS_NEXTBITS", nextbits)
+    monkeypatch.setenv("GX_BFS_QBITS", qbits)
     if grid:
         monkeypatch.setenv("GX_BFS_GRID", grid)
     for g in (_rmat(14, 16, 4), _rmat(12, 8, 3, undirected=False)):
@@ -551,13 +554,13 @@ def test_bfs_level_driver(ctx, monkeypatch, device, nextbits, grid):
 
 
 @pytest.mark.parametrize("env", [{"GX_HUB": "1"}, {"GX_HUB": "2"}, {"GX_HUB": "2", "GX_HUB_SORT": "0"},
-                                 {"GX_HUB": "2", "GX_WCC_ROUNDS": "2"}])
+                                 {"GX_HUB": "2", "GX_WCC_ROUNDS": "2"}, {"GX_HUB": "2", "GX_REMAP": "scatter"}])
 def test_hub_first_copy(ctx, monkeypatch, env):
     """BFS, WCC and SSSP on the hub-first relabelled copy of an undirected graph (built from
     the second call on a graph, GX_HUB=1, or from the first, GX_HUB=2; rows sorted by hub-first
     id, or in the parent's order with GX_HUB_SORT=0; WCC with one sampling round on the sorted
     copy, or two): results come back in the caller's vertex order -- levels and distances
-    gathered through the permutation, WCC labels renamed to each component's smallest caller
+    gathered through the permutation (or scattered through its inverse, GX_REMAP=scatter), WCC labels renamed to each component's smallest caller
     id -- on graphs with many components, isolated vertices and unreachable ones, over three
     calls on one graph."""
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A

@@ -6,7 +6,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 for r in 1 2; do
  for v in new old; do
   for G in SYN-g500-22 SYN-cit; do
-   if [ $v = old ]; then E="GX_BFS_NEXTBITS=0 GX_BFS_GRID=8192"; else E=""; fi
+   if [ $v = old ]; then E="${OLD_ENV:-GX_BFS_NEXTBITS=0 GX_BFS_GRID=8192}"; else E=""; fi
    env $E timeout -k 10 200 python bench.py --algorithm bfs --graph $G --no-cpu-baseline --steps 200 --warmup 5 > $O/b_${v}_${G}_$r.json 2> $O/b_${v}_${G}_$r.err || exit 1
    python3 -c "import json;d=json.loads(open('$O/b_${v}_${G}_$r.json').read().strip().splitlines()[-1]);print('$v $G $r', d['ms_per_step'], d['roofline']['frac'])" | tee -a $O/summary.txt
   done
