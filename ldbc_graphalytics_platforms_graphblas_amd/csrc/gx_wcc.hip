@@ -18,6 +18,7 @@
 // of the component: comp[v] is canonical and equals the oracle's union-find labels exactly.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "gx_device.h"
 
@@ -198,20 +199,35 @@ __global__ __launch_bounds__(kWccBlock) void k_wcc_link_edges(const int64_t *__r
 }
 
 // Afforest's giant component: the most frequent root among kSamples sampled vertices (ties:
-// the smallest root), chosen by one workgroup (each thread counts its sample's root among
-// all of them in LDS), so the host does not wait for the samples between the passes.
+// the smallest root), chosen by one workgroup, so the host does not wait for the samples
+// between the passes.  The roots are counted in an LDS hash table (linear probing, CAS-claimed
+// keys, atomic counts).  Each thread scanning all samples (O(kSamples^2) LDS reads on one CU)
+// took 20 us of a 169 us WCC run.  Any root would be correct (the finish links every edge of
+// the vertices outside it); the most frequent one skips the most.
 constexpr int kSamples = 1024;
+constexpr int kGiantSlots = 2 * kSamples;
 
 __global__ __launch_bounds__(kSamples) void k_pick_giant(const int32_t *parent, const int32_t *__restrict__ ids,
                                                          int32_t *giant) {
-    __shared__ int32_t roots[kSamples];
+    __shared__ int32_t keys[kGiantSlots];
+    __shared__ uint32_t cnts[kGiantSlots];
     __shared__ unsigned long long best[kSamples / kWave];
     const int t = threadIdx.x;
+    for (int i = t; i < kGiantSlots; i += kSamples) {
+        keys[i] = -1;
+        cnts[i] = 0;
+    }
     const int32_t r = find_root(parent, ids[t]);
-    roots[t] = r;
     __syncthreads();
-    uint32_t c = 0;
-    for (int j = 0; j < kSamples; j++) c += roots[j] == r;
+    uint32_t h = ((uint32_t)r * 2654435761u) >> 21;   // 11 bits: kGiantSlots
+    for (;;) {
+        const int32_t k = atomicCAS(&keys[h], -1, r);
+        if (k == -1 || k == r) break;
+        h = (h + 1) & (kGiantSlots - 1);
+    }
+    atomicAdd(&cnts[h], 1u);
+    __syncthreads();
+    const uint32_t c = cnts[h];
     unsigned long long key = ((unsigned long long)c << 32) | (uint32_t)(0x7fffffff - r);
     for (int off = kWave / 2; off > 0; off >>= 1) {
         const unsigned long long o = __shfl_xor(key, off, kWave);
@@ -291,12 +307,27 @@ __global__ __launch_bounds__(kWccBlock) void k_wcc_min_orig(const int32_t *__res
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < kWccBlock / kWave; w++) lm = min(lm, wmin[w]);
-        if (giant >= 0 && lm != 0x7fffffff) atomicMin(&minorig[giant], lm);
+        // one atomic per workgroup on one word serialised (2 048 of them, 26 us per run on
+        // SYN-g500-22): only a workgroup whose minimum beats the word's current value sends one
+        if (giant >= 0 && lm != 0x7fffffff &&
+            lm < __hip_atomic_load(&minorig[giant], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(&minorig[giant], lm);
     }
 }
 
-// out[order[x]] = the label of x's component; vertices past `live` have no edges and are
-// their own component.  Scattered through order (streaming reads, random stores).
+// out[v] = the label of v's component, gathered through perm (x = perm[v], the hub-first
+// position of caller vertex v); vertices past `live` have no edges and are their own component.
+// Coalesced stores: the scatter below took 30 us per run on SYN-g500-22 (r05_wcc_kernel_stats.csv).
+__global__ void k_wcc_label_gather(const int32_t *__restrict__ parent, const int32_t *__restrict__ perm,
+                                   const int32_t *__restrict__ minorig, int64_t n, int64_t live,
+                                   int32_t *__restrict__ out) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t x = perm[v];
+        out[v] = x < live ? minorig[parent[x]] : (int32_t)v;
+    }
+}
+
+// The same as a scatter through order (GX_REMAP=scatter): streaming reads, random stores.
 __global__ void k_wcc_label_orig(const int32_t *__restrict__ parent, const int32_t *__restrict__ order,
                                  const int32_t *__restrict__ minorig, int64_t n, int64_t live,
                                  int32_t *__restrict__ out) {
@@ -393,8 +424,13 @@ extern "C" int gx_wcc(gx_graph *g, uint64_t *comp) {
             hipLaunchKernelGGL(k_wcc_min_orig, dim3(grid_for((uint64_t)live, kWccBlock, 2048)), dim3(kWccBlock), 0,
                                s, parent.p, g->out_order, live, giant_d, minorig);
         }
-        hipLaunchKernelGGL(k_wcc_label_orig, dim3(vgrid), dim3(256), 0, s, parent.p, g->out_order, minorig, n, live,
-                           lab);
+        const char *re = std::getenv("GX_REMAP");
+        if (re && std::strcmp(re, "scatter") == 0)
+            hipLaunchKernelGGL(k_wcc_label_orig, dim3(vgrid), dim3(256), 0, s, parent.p, g->out_order, minorig, n,
+                               live, lab);
+        else
+            hipLaunchKernelGGL(k_wcc_label_gather, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, parent.p,
+                               g->out_perm, minorig, n, live, lab);
         GX_TRY(check_launch("k_wcc_label_orig"));
         res = lab;
     }
