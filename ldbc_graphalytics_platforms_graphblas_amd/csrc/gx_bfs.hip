@@ -274,6 +274,7 @@ struct BfsState {
     int32_t nextbits;      // bottom-up writes the next bitmap (GX_BFS_NEXTBITS, default on)
     int32_t qbits;         // a top-down queue rebuild reads that bitmap (GX_BFS_QBITS, default on)
     int32_t pad2;
+    unsigned long long alpha, beta;   // Beamer's switch thresholds (GX_BFS_ALPHA / GX_BFS_BETA)
     unsigned long long mf, mu, fsize, n;
     uint32_t qcnt[2];
     unsigned long long nedges;
@@ -316,8 +317,8 @@ __global__ void k_bfs_plan(BfsState *st) {
     // Beamer: TD -> BU when the frontier's edges exceed the unexplored ones / 14; BU -> TD when
     // the frontier shrinks below n / 24
     if (st->has_in) {
-        if (!st->bottom_up && st->mf > st->mu / 14) st->bottom_up = 1;
-        else if (st->bottom_up && (long long)st->fsize < (long long)(st->n / 24)) st->bottom_up = 0;
+        if (!st->bottom_up && st->mf > st->mu / st->alpha) st->bottom_up = 1;
+        else if (st->bottom_up && (long long)st->fsize < (long long)(st->n / st->beta)) st->bottom_up = 0;
     }
     if (st->bottom_up) {
         st->mode = 2;
@@ -442,6 +443,9 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         h.nextbits = !nb || std::atoi(nb) != 0;
         const char *qb = std::getenv("GX_BFS_QBITS");
         h.qbits = !qb || std::atoi(qb) != 0;
+        const char *ae = std::getenv("GX_BFS_ALPHA"), *be = std::getenv("GX_BFS_BETA");
+        h.alpha = (unsigned long long)std::max(1, ae ? std::atoi(ae) : 14);
+        h.beta = (unsigned long long)std::max(1, be ? std::atoi(be) : 24);
         GX_HIP_TRY(hipMemcpyAsync(st.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, &st.p->qcnt[0],
                            (int32_t)src);

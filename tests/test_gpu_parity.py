@@ -553,6 +553,18 @@ def test_bfs_level_driver(ctx, monkeypatch, device, nextbits, grid, qbits):
         np.testing.assert_array_equal(gpu_run(ctx, _G(csr, False), "BFS", source=s), O.bfs(csr, s))
 
 
+@pytest.mark.parametrize("alpha,beta", [("1", "1000"), ("1000", "1"), ("24", "48")])
+def test_bfs_direction_thresholds(ctx, monkeypatch, alpha, beta):
+    """Beamer's switch thresholds (GX_BFS_ALPHA / GX_BFS_BETA): bottom-up from the first level
+    and kept to the end, top-down almost throughout, and a mid setting; levels bit-exact."""
+    monkeypatch.setenv("GX_BFS_ALPHA", alpha)
+    monkeypatch.setenv("GX_BFS_BETA", beta)
+    for g in (_rmat(14, 16, 4), _rmat(12, 8, 3, undirected=False)):
+        s = _src(g)
+        for _ in range(2):   # the second call runs on the hub-first copy / with the transpose
+            np.testing.assert_array_equal(gpu_run(ctx, g, "BFS", source=s), O.bfs(g.csr, s))
+
+
 @pytest.mark.parametrize("env", [{"GX_HUB": "1"}, {"GX_HUB": "2"}, {"GX_HUB": "2", "GX_HUB_SORT": "0"},
                                  {"GX_HUB": "2", "GX_WCC_ROUNDS": "2"}, {"GX_HUB": "2", "GX_REMAP": "scatter"}])
 def test_hub_first_copy(ctx, monkeypatch, env):
