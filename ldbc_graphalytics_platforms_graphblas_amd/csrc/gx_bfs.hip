@@ -445,7 +445,9 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         h.qbits = !qb || std::atoi(qb) != 0;
         const char *ae = std::getenv("GX_BFS_ALPHA"), *be = std::getenv("GX_BFS_BETA");
         h.alpha = (unsigned long long)std::max(1, ae ? std::atoi(ae) : 14);
-        h.beta = (unsigned long long)std::max(1, be ? std::atoi(be) : 24);
+        // beta 48 on undirected graphs (SYN-7_5 0.203-0.209 -> 0.186-0.192 ms, SYN-g500-22 ~1 %),
+        // 24 on directed ones (SYN-cit 2-6 % slower at 48): profiles/r05_bfs_beta_ab.txt
+        h.beta = (unsigned long long)std::max(1, be ? std::atoi(be) : (g->directed ? 24 : 48));
         GX_HIP_TRY(hipMemcpyAsync(st.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(256), 0, s, g->A.rp.p, level.p, q0.p, &st.p->qcnt[0],
                            (int32_t)src);
