@@ -1140,10 +1140,11 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         }
         g->mean_w = mean;
     }
-    // measured on the SYN stand-ins with bucket fusion: 3 for undirected graphs,
-    // whose big early buckets are pulled (round 3, tools/r03_pieces2.sh: SYN-8_5 6.4-6.7 ->
-    // 6.0-6.1 ms against 4, SYN-g500-22 3.7-3.8 -> 3.5), 0.5 for directed ones
-    double delta = 0.0, scale = g->directed ? 0.5 : 3.0;
+    // measured on the SYN stand-ins with bucket fusion: 2 for undirected graphs,
+    // whose big early buckets are pulled (round 5 re-sweep after the dense opening,
+    // profiles/r05_sssp_dscale_sweep.txt: against 3, SYN-8_5 5.88 -> 5.61 ms, SYN-g500-22
+    // 3.56 -> 3.01, SYN-7_5 1.91 -> 1.80; round 3 had chosen 3 over 4), 0.5 for directed ones
+    double delta = 0.0, scale = g->directed ? 0.5 : 2.0;
     if (const char *e = std::getenv("GX_SSSP_DELTA")) delta = std::atof(e);
     if (const char *e = std::getenv("GX_SSSP_DSCALE")) scale = std::atof(e);
     if (!(delta > 0.0)) {
