@@ -781,6 +781,9 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
     std::unique_ptr<int64_t[]> nrp;
     std::unique_ptr<int32_t[]> nout;
     if (!have_runs) {
+        // download() stages through the context's pinned buffers and events, which the column
+        // upload of gx_pagerank_csr (g->job) is using on its own thread: let it finish first
+        if (g->job) GX_TRY(g->job->join());
         nrp.reset(new int64_t[n + 1]);
         nout.reset(new int32_t[n]);
         GX_TRY(download(ctx, nrp.get(), p->rp_own.p, n + 1, Xfer::Raw64));

@@ -278,8 +278,11 @@ namespace {
 struct NoAfter {
     int operator()(int) const { return GX_SUCCESS; }
 };
-// Entries per staging chunk: a multiple of `align` (16 for the packed 24-bit columns, whose
-// chunks must start on a 48-byte boundary).
+// Entries per staging chunk: a multiple of `align`.  The packed 24-bit columns use kPackAlign =
+// 64: a chunk must start on a 48-byte boundary (16 entries) for k_unpack24, and on a whole
+// 64-entry slab for the source-side key pass of gx_pagerank_csr (k_scatter_keys covers slabs
+// [e0/64, ceil(e1/64)), so a boundary inside a slab would read the next chunk before it lands).
+constexpr uint64_t kPackAlign = 64;
 uint64_t stage_chunk(size_t elem, uint64_t align = 1) { return gx_ctx::kStageBytes / elem / align * align; }
 
 template <class Fill, class After = NoAfter>
@@ -384,7 +387,7 @@ int upload_columns(gx_ctx *ctx, const uint64_t *cols, uint64_t nnz, uint64_t n, 
                       [&](uint64_t off, uint64_t cnt, void *buf) {
                           return host_narrow(cols + off, cnt, n, static_cast<int32_t *>(buf), nt);
                       }, bad, s, after, sync);
-    const uint64_t chunk = stage_chunk(3, 16);
+    const uint64_t chunk = stage_chunk(3, kPackAlign);
     return upload(ctx, reinterpret_cast<char *>(packed), nnz, 3,
                   [&](uint64_t off, uint64_t cnt, void *buf) {
                       return host_pack24(cols + off, cnt, n, static_cast<uint32_t *>(buf));
@@ -395,7 +398,7 @@ int upload_columns(gx_ctx *ctx, const uint64_t *cols, uint64_t nnz, uint64_t n, 
                                          packed, (int64_t)e0, (int64_t)e1, dst);
                       GX_TRY(check_launch("k_unpack24"));
                       return after(c);
-                  }, sync, 16);
+                  }, sync, kPackAlign);
 }
 
 }  // namespace
@@ -458,11 +461,15 @@ int graph_create_async(gx_ctx *ctx, const gx_csr *A, int directed, gx_graph **ou
     // the packed buffer and the chunk events are made by the upload thread (creating ~75 events
     // and a 1.9 GB buffer here cost the calling thread ~12 ms before its plan could start)
     const bool pack = pack_columns(n);
-    const uint64_t chunk = pack ? stage_chunk(3, 16) : stage_chunk(4);
+    const uint64_t chunk = pack ? stage_chunk(3, kPackAlign) : stage_chunk(4, kPackAlign);
     for (uint64_t off = 0; off < nnz; off += chunk) {
         job->ev.push_back(nullptr);
         job->end.push_back((int64_t)std::min(nnz, off + chunk));
     }
+    // the key pass reads whole 64-entry slabs up to each chunk end: every end but the last must
+    // be slab-aligned
+    for (size_t c = 0; c + 1 < job->end.size(); c++)
+        if (job->end[c] % 64) return fail(GX_PANIC, "graph_create_async: upload chunk not 64-entry aligned");
     const char *nt_env = std::getenv("GX_UPLOAD_NT");
     const bool nt = !nt_env || std::atoi(nt_env) != 0;
     UploadJob *j = job.get();

@@ -268,23 +268,47 @@ def reset_stats():
         STATS[k] = 0
 
 
+class _Bufs:
+    """Per-call scratch of the round loops: one set of exchange buffers per rank,
+    allocated on first use and reused by every round of a bfs / wcc / cdlp call, so a round
+    costs no allocation beyond a gathered-words buffer that grows by doubling."""
+
+    def __init__(self):
+        self.d = {}
+
+    def get(self, key, rank: LocalRank, n: int, dtype, zero: bool = True):
+        import torch
+        t = self.d.get(key)
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = torch.zeros(max(n, 2 * t.numel() if t is not None else n), dtype=dtype, device=rank.device)
+            self.d[key] = t
+        elif zero:
+            t[:n].zero_()
+        return t[:n]
+
+
 def _exchange(ranks: List[LocalRank], comm, arrs, olds, spans, elem: int, op: int, dense_bytes: int, dense,
-              dsts=None) -> int:
+              dsts=None, bufs: "_Bufs" = None) -> int:
     """Frontier-sized exchange: every rank's entries of arrs[k] over spans[k] = (v0, v1) that
     differ from olds[k] (None: from 0) leave as (v << 32 | value) words (gx_part_changes); the
     counts are all-gathered (the one host read), then the first max-count words of every rank,
     which every rank applies with `op` (gx_part_apply) to dsts[k] (default arrs[k]).  When
     those words would outweigh the dense collective (`dense_bytes` per rank, e.g. 2 n for an
     all-reduce of n bytes), `dense()` runs instead (EXCHANGE = "sparse" / "dense" forces one).
-    Returns the number of changes over all ranks (0: nothing changed anywhere)."""
+    Returns the number of changes over all ranks (0: nothing changed anywhere).  `bufs` (one
+    per algorithm call) keeps the word, count and gathered buffers across rounds."""
     import torch
     nranks = getattr(comm, "world_size", None) or len(ranks)
+    if bufs is None:
+        bufs = _Bufs()
     # room for any rank's count: the all-gather sends the first max-count words of every rank
-    words = [_zeros(r, max(1, a.numel()), torch.int64) for r, a in zip(ranks, arrs)]
-    cnt = [_zeros(r, 1, torch.int64) for r in ranks]
+    # (written by gx_part_changes before they are read: no zeroing)
+    words = [bufs.get(("w", k), r, max(1, a.numel()), torch.int64, zero=False)
+             for k, (r, a) in enumerate(zip(ranks, arrs))]
+    cnt = [bufs.get(("c", k), r, 1, torch.int64) for k, r in enumerate(ranks)]
     for r, a, b, (v0, v1), w, c in zip(ranks, arrs, olds, spans, words, cnt):
         r.backend.changes(a, b, v0, v1, elem, w, c)
-    counts = [_zeros(r, nranks, torch.int64) for r in ranks]
+    counts = [bufs.get(("n", k), r, nranks, torch.int64) for k, r in enumerate(ranks)]
     comm.all_gather(counts, cnt)
     cw = counts[0].cpu().numpy()   # identical on every rank
     m, tot = int(cw.max()), int(cw.sum())
@@ -298,7 +322,7 @@ def _exchange(ranks: List[LocalRank], comm, arrs, olds, spans, elem: int, op: in
         return tot
     STATS["word_rounds"] += 1
     STATS["word_bytes"] += 8 * m * nranks
-    gathered = [_zeros(r, m * nranks, torch.int64) for r in ranks]
+    gathered = [bufs.get(("g", k), r, m * nranks, torch.int64, zero=False) for k, r in enumerate(ranks)]
     comm.all_gather(gathered, [w[:m] for w in words])
     for r, g, cs, a in zip(ranks, gathered, counts, dsts if dsts is not None else arrs):
         r.backend.apply(g, cs, nranks, m, a, elem, op)
@@ -318,13 +342,14 @@ def bfs(ranks: List[LocalRank], comm, n: int, src: int):
     # the all-reduce MAX of next (~2 n bytes)
     dense_bytes = min(2 * n, nranks * ((n + 31) // 32) * 4)
     cur = 0
+    bufs = _Bufs()
     while True:
-        nxt = [_zeros(r, n, torch.uint8) for r in ranks]
+        nxt = [bufs.get(("next", k), r, n, torch.uint8) for k, r in enumerate(ranks)]
         for r, lv, nx in zip(ranks, level, nxt):
             r.backend.bfs_expand(r.v0, r.v1, lv, cur, nx)
         _exchange(ranks, comm, nxt, [None] * len(ranks), [(0, n)] * len(ranks), 1, OP_SET, dense_bytes,
-                  lambda: _bfs_dense(ranks, comm, nxt, n))
-        count = [_zeros(r, 1, torch.int64) for r in ranks]
+                  lambda: _bfs_dense(ranks, comm, nxt, n, bufs), bufs=bufs)
+        count = [bufs.get(("count", k), r, 1, torch.int64) for k, r in enumerate(ranks)]
         for r, lv, nx, c in zip(ranks, level, nxt, count):
             r.backend.bfs_commit(nx, lv, cur, c)
         if int(count[0].item()) == 0:   # identical on every rank (same inputs)
@@ -333,7 +358,7 @@ def bfs(ranks: List[LocalRank], comm, n: int, src: int):
     return level[0]
 
 
-def _bfs_dense(ranks: List[LocalRank], comm, nxt, n: int) -> None:
+def _bfs_dense(ranks: List[LocalRank], comm, nxt, n: int, bufs: "_Bufs" = None) -> None:
     """A level's discoveries exchanged densely: bit-packed and all-gathered (gx_part_pack_bits /
     gx_part_or_bits) while that is smaller than the all-reduce MAX of the n-byte `next`."""
     import torch
@@ -342,10 +367,12 @@ def _bfs_dense(ranks: List[LocalRank], comm, nxt, n: int) -> None:
     if nranks * nw * 4 >= 2 * n:
         comm.all_reduce(nxt, "max")
         return
-    bits = [_zeros(r, nw, torch.int32) for r in ranks]
+    if bufs is None:
+        bufs = _Bufs()
+    bits = [bufs.get(("bits", k), r, nw, torch.int32, zero=False) for k, r in enumerate(ranks)]
     for r, nx, b in zip(ranks, nxt, bits):
         r.backend.pack_bits(nx, b)
-    gathered = [_zeros(r, nw * nranks, torch.int32) for r in ranks]
+    gathered = [bufs.get(("bitsg", k), r, nw * nranks, torch.int32, zero=False) for k, r in enumerate(ranks)]
     comm.all_gather(gathered, bits)
     for r, g, nx in zip(ranks, gathered, nxt):
         r.backend.or_bits(g, nranks, nx)
@@ -360,13 +387,15 @@ def wcc(ranks: List[LocalRank], comm, n: int):
     parent = [_zeros(r, n, torch.int32) for r in ranks]
     for r, p in zip(ranks, parent):
         r.backend.wcc_init(p)
+    bufs = _Bufs()
     while True:
-        prev = [p.clone() for p in parent]
-        changed = [_zeros(r, 1, torch.int32) for r in ranks]
+        prev = [bufs.get(("prev", k), r, n, torch.int32, zero=False).copy_(p)
+                for k, (r, p) in enumerate(zip(ranks, parent))]
+        changed = [bufs.get(("changed", k), r, 1, torch.int32) for k, r in enumerate(ranks)]
         for r, p, c in zip(ranks, parent, changed):
             r.backend.wcc_hook(r.v0, r.v1, p, c)
         tot = _exchange(ranks, comm, parent, prev, [(0, n)] * len(ranks), 4, OP_MIN, 8 * n,
-                        lambda: comm.all_reduce(parent, "min"))
+                        lambda: comm.all_reduce(parent, "min"), bufs=bufs)
         if tot == 0:
             break
         for r, p in zip(ranks, parent):
@@ -431,16 +460,18 @@ def cdlp(ranks: List[LocalRank], comm, n: int, iters: int, ranges: np.ndarray):
         nxt = [_zeros(r, n, torch.int32) for r in ranks]
         for p, lb in zip(parts, labels):
             p.init(lb)
+        bufs = _Bufs()
         for _ in range(iters):
-            changed = [_zeros(r, 1, torch.int32) for r in ranks]
+            changed = [bufs.get(("changed", k), r, 1, torch.int32) for k, r in enumerate(ranks)]
             for p, lb, nx, c in zip(parts, labels, nxt, changed):
                 p.step(lb, nx, c)
 
             def dense():
-                send = [_zeros(r, chunk, torch.int32) for r in ranks]
+                send = [bufs.get(("send", k), r, chunk, torch.int32) for k, r in enumerate(ranks)]
                 for r, nx, sd in zip(ranks, nxt, send):
                     sd[:r.v1 - r.v0].copy_(nx[r.v0:r.v1])
-                gathered = [_zeros(r, chunk * nranks, torch.int32) for r in ranks]
+                gathered = [bufs.get(("sendg", k), r, chunk * nranks, torch.int32, zero=False)
+                            for k, r in enumerate(ranks)]
                 comm.all_gather(gathered, send)
                 for g, lb in zip(gathered, labels):
                     lb.copy_(torch.cat([g[k * chunk:k * chunk + sizes[k]] for k in range(nranks)]))
@@ -448,7 +479,7 @@ def cdlp(ranks: List[LocalRank], comm, n: int, iters: int, ranges: np.ndarray):
             # the owned labels that changed, set into every rank's labels (_exchange); the
             # all-gather of the owned slices when more than half of them changed
             tot = _exchange(ranks, comm, nxt, labels, [(r.v0, r.v1) for r in ranks], 4, OP_SET, 4 * n, dense,
-                            dsts=labels)
+                            dsts=labels, bufs=bufs)
             if tot == 0:   # fixed point (LAGraph_cdlp.c:328-332)
                 break
         return labels[0]

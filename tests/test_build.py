@@ -43,3 +43,43 @@ def test_pagerank_kernel_does_not_spill():
     for k in prod:
         assert ks[k].get("VGPRs Spill", 0) == 0 and ks[k].get("ScratchSize", 0) == 0, (k, ks[k])
         assert ks[k].get("VGPRs", 0) <= 128, (k, ks[k])
+
+
+def device_asm(src):
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{ROOT}/include",
+           f"-I{ROOT}/ldbc_graphalytics_platforms_graphblas_amd/csrc", "--offload-device-only", "-S", str(src),
+           "-o", "-"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stderr[-2000:]
+    return res.stdout
+
+
+def test_queue_fetch_exit_is_uniform():
+    """the work-queue kernel's loop exit after queue_fetch must be a scalar
+    branch on SCC, set by a scalar compare of the readfirstlane'd item, and neither barrier that
+    publishes the item may sit inside an exec-masked region.  The two hangs of rounds 4-5
+    (gpurun_out/m1/variants.log) were exactly a divergent exit here, so this guards the emitted
+    ISA on the CPU instead of on a GPU box."""
+    import shutil
+    import sys
+    if not shutil.which(HIPCC):
+        pytest.skip("hipcc not available")
+    sys.path.insert(0, str(ROOT / "tools"))
+    import isa_exec_check as X
+    asm = device_asm(ROOT / "ldbc_graphalytics_platforms_graphblas_amd" / "csrc" / "gx_pr_sorted.hip")
+    syms = sorted(set(re.findall(r"^(_Z\w+k_pr_pull_unitsILb0ELi0ELi\d+ELb0ELb1E\w*):", asm, re.M)))
+    assert syms, "no QUEUE=true instantiation of k_pr_pull_units in the device assembly"
+    for sym in syms:
+        ins, labels = X.parse(X.kernel_body(asm, sym))
+        r = X.queue_fetch_region(ins, labels)
+        assert r is not None, sym
+        exit_op = ins[r["exit"]].split()[0]
+        assert exit_op in ("s_cbranch_scc0", "s_cbranch_scc1"), (sym, ins[r["exit"]])
+        assert r["cond"] is not None and ins[r["cond"]].startswith("s_cmp"), (sym, r["cond"] and ins[r["cond"]])
+        # the compared item is a scalar read back from LDS through readfirstlane
+        between = ins[r["barriers"][-1]:r["cond"]]
+        assert any(t.startswith("v_readfirstlane_b32") for t in between), (sym, between)
+        depth = X.exec_depth(ins, r["header"], r["exit"] + 1)
+        for b in r["barriers"][:2]:
+            assert depth[b - r["header"]] == 0, (sym, b, ins[r["header"]:b + 1])
+        assert depth[r["exit"] - r["header"]] == 0, (sym, "exit branch inside a masked region")
