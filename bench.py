@@ -485,15 +485,17 @@ def measure_pr(csr, args, ctx, device, stream, world, rank, dist, collect=True):
         PartitionedPageRank, hub_relabel, interleaved_relabel, partition_rows, slice_rows
     n, nnz = csr.n, csr.nnz
     # GX_PR_PIECES = P > 1: each rank owns P virtual ranks p * N + rank whose all-gathers overlap
-    # the next piece's SpMV (default 1: at N = 1 a 1/16 piece ran its SpMV at 0.48x the rate of
-    # a 1/8 one -- tools/pr_dist_n1.sh -- more than the overlap wins back).  Layout: the hub-first
+    # the next piece's SpMV.  Default 2 at N > 1 (round 6: the scheme bin/exe/pr's
+    # gx_pagerank_multi runs, so a scaling line measures the executables' path; only the last
+    # piece's exchange is exposed), 1 at N = 1, where there is nothing to hide (a 1/16 piece ran
+    # its SpMV at 0.48x the rate of a 1/8 one -- tools/pr_dist_n1.sh).  Layout: the hub-first
     # order (what gx_pagerank does internally) dealt round-robin over the N * pieces virtual
     # ranks, so each owns n / (N * pieces) rows AND ~nnz / (N * pieces) entries and the
     # exchanged vector is ~n long (interleaved_relabel); GX_PR_PARTITION=ranges keeps the
     # round-1 contiguous hub-first ranges balanced by entries.
     # (at N = 1, GX_PR_PIECES = 8 runs the 8 rank shares of config 4 on one GPU back to back:
     # the per-piece launch against 1/8 of the whole-graph launch is the per-rank efficiency)
-    pieces = max(1, int(os.environ.get("GX_PR_PIECES", "1")))
+    pieces = max(1, int(os.environ.get("GX_PR_PIECES", "2" if world > 1 else "1")))
     vranks = world * pieces
     # default: a huge graph (more than 2 Mi entries per CU: config 4's SYN-8_5) is dealt by
     # the single-GPU plan's blocks (block_relabel; 1/8 pieces 139-150 us per SpMV against 208

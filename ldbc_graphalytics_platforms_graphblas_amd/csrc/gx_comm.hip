@@ -563,27 +563,54 @@ bool one_device(gx_ctx *const *ctxs, int ndev) {
 // gx_pagerank_multi / gx_sssp_multi / gx_lcc_multi on a one-GPU box.
 // One context alone keeps a size-1 RCCL clique, so the RCCL path stays exercised there too.
 struct Clique {
+    static constexpr int kMaxPieces = 8;   // gx_pagerank_multi's pieces per device (events below)
     int ndev = 0;
     std::vector<gx_ctx *> ctx;
     std::vector<ncclComm_t> comm;
     bool local = false;
     std::vector<hipEvent_t> ev_in, ev_out;
+    // per device: a comm stream (the pieces' exchanges overlap the next piece's SpMV on the
+    // compute stream), an event per piece (its SpMV done) and one for the iteration's
+    // exchanges (made here, by gx_multi_prepare, outside the processing time: creating a stream
+    // cost 10-30 ms inside a call)
+    std::vector<hipStream_t> cs;
+    std::vector<hipEvent_t> ev_piece, ev_comm;
 
     ~Clique() {
         for (int d = 0; d < ndev; d++) {
             (void)hipSetDevice(ctx[d]->device);
             (void)hipStreamSynchronize(ctx[d]->stream);
+            if (d < (int)cs.size() && cs[d]) (void)hipStreamSynchronize(cs[d]);
         }
         for (ncclComm_t c : comm)
             if (c) (void)rccl().comm_destroy(c);
         for (hipEvent_t e : ev_in) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_out) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_piece)
+            if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_comm)
+            if (e) (void)hipEventDestroy(e);
+        for (int d = 0; d < (int)cs.size(); d++)
+            if (cs[d]) {
+                (void)hipSetDevice(ctx[d]->device);
+                (void)hipStreamDestroy(cs[d]);
+            }
     }
 
     int init(gx_ctx *const *ctxs, int n) {
         ndev = n;
         ctx.assign(ctxs, ctxs + n);
         local = n > 1 && one_device(ctxs, n);
+        cs.assign(n, nullptr);
+        ev_comm.assign(n, nullptr);
+        ev_piece.assign((size_t)n * kMaxPieces, nullptr);
+        for (int d = 0; d < n; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_HIP_TRY(hipStreamCreateWithFlags(&cs[d], hipStreamNonBlocking));
+            GX_HIP_TRY(hipEventCreateWithFlags(&ev_comm[d], hipEventDisableTiming));
+            for (int p = 0; p < kMaxPieces; p++)
+                GX_HIP_TRY(hipEventCreateWithFlags(&ev_piece[(size_t)d * kMaxPieces + p], hipEventDisableTiming));
+        }
         if (!local) {
             std::vector<int> devs(n);
             for (int d = 0; d < n; d++) devs[d] = ctxs[d]->device;
@@ -603,38 +630,53 @@ struct Clique {
 
     hipStream_t st(int d) const { return ctx[d]->stream; }
 
-    // local mode: every stream waits for what every stream has enqueued so far
-    int fence_in() {
-        for (int e = 0; e < ndev; e++) GX_HIP_TRY(hipEventRecord(ev_in[e], st(e)));
+    // local mode: every stream of `sel` waits for what every such stream has enqueued so far
+    template <class Sel>
+    int fence_in(Sel sel) {
+        for (int e = 0; e < ndev; e++) GX_HIP_TRY(hipEventRecord(ev_in[e], sel(e)));
         for (int d = 0; d < ndev; d++)
             for (int e = 0; e < ndev; e++)
-                if (e != d) GX_HIP_TRY(hipStreamWaitEvent(st(d), ev_in[e], 0));
+                if (e != d) GX_HIP_TRY(hipStreamWaitEvent(sel(d), ev_in[e], 0));
         return GX_SUCCESS;
     }
-    int fence_out() {
-        for (int d = 0; d < ndev; d++) GX_HIP_TRY(hipEventRecord(ev_out[d], st(d)));
+    template <class Sel>
+    int fence_out(Sel sel) {
+        for (int d = 0; d < ndev; d++) GX_HIP_TRY(hipEventRecord(ev_out[d], sel(d)));
         for (int e = 0; e < ndev; e++)
             for (int d = 0; d < ndev; d++)
-                if (d != e) GX_HIP_TRY(hipStreamWaitEvent(st(e), ev_out[d], 0));
+                if (d != e) GX_HIP_TRY(hipStreamWaitEvent(sel(e), ev_out[d], 0));
         return GX_SUCCESS;
     }
+    int fence_in() {
+        return fence_in([&](int d) { return st(d); });
+    }
+    int fence_out() {
+        return fence_out([&](int d) { return st(d); });
+    }
 
-    // recv(d)[e * bytes, (e + 1) * bytes) = send(e)[0, bytes) for every pair (ncclAllGather)
+    // recv(d)[e * bytes, (e + 1) * bytes) = send(e)[0, bytes) for every pair (ncclAllGather),
+    // on the compute streams
     template <class S, class R>
     int all_gather(S send, R recv, size_t bytes) {
+        return all_gather_on(send, recv, bytes, [&](int d) { return st(d); });
+    }
+
+    // the same on the streams sel(d) (the comm streams for gx_pagerank_multi's pieces)
+    template <class S, class R, class Sel>
+    int all_gather_on(S send, R recv, size_t bytes, Sel sel) {
         if (local) {
             GX_HIP_TRY(hipSetDevice(ctx[0]->device));
-            GX_TRY(fence_in());
+            GX_TRY(fence_in(sel));
             for (int d = 0; d < ndev; d++)
                 for (int e = 0; e < ndev; e++)
                     GX_HIP_TRY(hipMemcpyAsync(static_cast<char *>(recv(d)) + (size_t)e * bytes, send(e), bytes,
-                                              hipMemcpyDeviceToDevice, st(d)));
-            return fence_out();
+                                              hipMemcpyDeviceToDevice, sel(d)));
+            return fence_out(sel);
         }
         const Rccl &r = rccl();
         GX_NCCL_TRY("ncclGroupStart", r.group_start());
         for (int d = 0; d < ndev; d++) {
-            const ncclResult_t e = r.all_gather(send(d), recv(d), bytes, ncclUint8, comm[d], st(d));
+            const ncclResult_t e = r.all_gather(send(d), recv(d), bytes, ncclUint8, comm[d], sel(d));
             if (e != ncclSuccess) {
                 (void)r.group_end();
                 return rccl_fail("ncclAllGather", e);
@@ -702,9 +744,10 @@ int get_clique(gx_ctx *const *ctxs, int n, std::shared_ptr<Clique> *out) {
 }
 
 
-// The in-process run of gx_pagerank_multi: one PrPart and its vectors per device.
+// The in-process run of gx_pagerank_multi: per device its full vectors (xr, xw) and, per piece
+// (index d * npieces + p), a PrPart, its local chunk and its scores.
 struct MultiRun {
-    int ndev = 0;
+    int ndev = 0, npieces = 1;
     std::vector<gx_ctx *> ctx;
     std::vector<PrPart *> part;
     std::vector<std::unique_ptr<DBuf<double>>> xr, xw, xl, ro;
@@ -717,11 +760,14 @@ struct MultiRun {
         }
         for (int d = 0; d < ndev; d++) {
             (void)hipSetDevice(ctx[d]->device);
-            delete part[d];
-            xr[d].reset();
-            xw[d].reset();
-            xl[d].reset();
-            ro[d].reset();
+            for (int p = 0; p < npieces; p++) {
+                const size_t k = (size_t)d * npieces + p;
+                if (k < part.size()) delete part[k];
+                if (k < xl.size()) xl[k].reset();
+                if (k < ro.size()) ro[k].reset();
+            }
+            if (d < (int)xr.size()) xr[d].reset();
+            if (d < (int)xw.size()) xw[d].reset();
         }
     }
 };
@@ -832,96 +878,205 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         return GX_SUCCESS;
     }
     if (n >= (1ull << 31) - 64) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: n >= 2^31");
+    // Pieces (round 6): every device's rows are cut into P pieces, each its
+    // own plan and launch.  Piece p of every device runs, then its chunks are all-gathered on
+    // the comm streams while piece p + 1 runs on the compute streams, so only the last piece's
+    // exchange is exposed (1/P of it) instead of all of it.  Piece p of device d is virtual rank
+    // p * ndev + d of V = ndev * P ranges: x's slab p (ndev chunks) is what piece p's all-gather
+    // fills, the layout PrDist uses across processes.  GX_PR_MULTI_PIECES (1..8; default 2 for
+    // several devices, 1 for one: at N = 1 there is no exchange to hide).
+    int P = ndev > 1 ? 2 : 1;
+    if (const char *e = std::getenv("GX_PR_MULTI_PIECES")) P = std::atoi(e);
+    P = std::max(1, std::min(P, Clique::kMaxPieces));
+    // one device, one piece: no exchange at all, so the single-GPU call itself (upload
+    // overlapped with the plan, 24-bit columns: 77 ms on SYN-8_5 where this path's upload and
+    // separate plan took 149)
+    if (ndev == 1 && P == 1) return gx_pagerank_csr(ctxs[0], A, directed, damping, iters, rank, nullptr);
+    const int V = ndev * P;
     // interleaved hub-first partition (pr_partition.interleaved_relabel): hub-first position i
-    // goes to device i % ndev as its local row i / ndev.  The vertices with out-edges come
-    // first in that order, so device 0 holds the most live rows, ceil(nlive / ndev): the
-    // chunk every device exchanges (+ the zero padding slot and the dangling slot).  The pull
-    // matrix of a directed graph is A', whose rows with out-edges in the PageRank sense are
-    // still A's rows with out-edges: liveness is A's out-degree either way.
+    // goes to virtual rank i % V as its local row i / V.  The vertices with out-edges come first
+    // in that order, so virtual rank 0 holds the most live rows, ceil(nlive / V): the chunk every
+    // rank exchanges (+ the zero padding slot and the dangling slot).  The pull matrix of a
+    // directed graph is A', whose rows with out-edges in the PageRank sense are still A's rows
+    // with out-edges: liveness is A's out-degree either way.
     // A huge graph (more than 2 Mi entries per CU, the single-GPU plan's huge-graph cut) is
-    // split by blocks instead (pr_multi_blocks; pr_partition.block_relabel): every device's
-    // blocks are the single-GPU plan's own, so its gathers share x lines as the whole graph's
-    // do (1/8 pieces of SYN-8_5: 140 us per SpMV against 208 interleaved).
+    // split by blocks instead (pr_multi_blocks; pr_partition.block_relabel): every virtual
+    // rank's blocks are the single-GPU plan's own, so its gathers share x lines as the whole
+    // graph's do (1/8 pieces of SYN-8_5: 140 us per SpMV against 208 interleaved).
     // GX_PR_MULTI_PARTITION=blocks / interleave overrides.
     uint64_t nlive = 0;
     for (uint64_t v = 0; v < n; v++) nlive += A->rowptr[v + 1] != A->rowptr[v];
     MultiRun M;
     M.ndev = ndev;
-    M.chunk = ((nlive + ndev - 1) / ndev + 2 + 31) / 32 * 32;
-    bool by_blocks = ndev > 1 && (double)A->rowptr[n] / (double)std::max(1, ctxs[0]->num_cus) > (double)(2 << 20);
+    M.npieces = P;
+    M.chunk = ((nlive + V - 1) / V + 2 + 31) / 32 * 32;
+    bool by_blocks = V > 1 && (double)A->rowptr[n] / (double)std::max(1, ctxs[0]->num_cus) > (double)(2 << 20);
     if (const char *e = std::getenv("GX_PR_MULTI_PARTITION")) by_blocks = std::strcmp(e, "blocks") == 0;
+    // Partitioned upload (round 6; GX_PR_MULTI_UPLOAD=rows, the default for
+    // undirected graphs, whose pull rows are A's own): the host deals the hub-first order once
+    // and every virtual rank's rows leave the 64-bit input once, already in the exchange
+    // layout (host_pick_rows_checked), for that rank's device only -- the plan of bench.py's N > 1
+    // path (gx_pr_part_create).  "whole" (and every directed graph, whose pull rows are A''s)
+    // uploads A to every device and plans there (pr_multi_plan).
+    bool by_rows = !directed;
+    if (const char *e = std::getenv("GX_PR_MULTI_UPLOAD")) by_rows = by_rows && std::strcmp(e, "whole") != 0;
+    if (by_rows) {
+        if (A->rowptr[0] != 0 || A->rowptr[n] != A->nnz || !host_monotone(A->rowptr, n))
+            return fail(GX_INVALID_VALUE, "gx_pagerank_multi: inconsistent row pointers");
+    }
     MultiBlocks mb;
     if (by_blocks) {
-        GX_TRY(pr_multi_blocks(A, directed, ndev, &mb));
+        GX_TRY(pr_multi_blocks(A, directed, V, &mb));
         M.chunk = mb.chunk;
+    } else if (by_rows) {
+        GX_TRY(pr_multi_interleave(A, V, &mb));
+        if (mb.chunk != M.chunk) return fail(GX_PANIC, "gx_pagerank_multi: interleaved chunk mismatch");
     }
-    if (M.chunk * (uint64_t)ndev >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
+    if (M.chunk * (uint64_t)V >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
     M.ctx.assign(ctxs, ctxs + ndev);
-    M.part.assign(ndev, nullptr);
+    M.part.assign((size_t)V, nullptr);
     for (int d = 0; d < ndev; d++) {
         M.xr.emplace_back(new DBuf<double>());
         M.xw.emplace_back(new DBuf<double>());
+    }
+    for (int k = 0; k < V; k++) {
         M.xl.emplace_back(new DBuf<double>());
         M.ro.emplace_back(new DBuf<double>());
     }
+    auto piece = [&](int d, int p) { return (size_t)d * P + p; };
     MultiGraphs G;
     G.g.assign(ndev, nullptr);
-    std::vector<uint64_t> rows(ndev);
+    std::vector<uint64_t> rows((size_t)V);
+    // by_rows: the vertex of each local row of each piece (the scores' scatter), and the column
+    // map vertex -> exchange slot
+    std::vector<std::vector<int32_t>> vrows(by_rows ? (size_t)V : 0);
+    std::vector<int32_t> colmap;
+    std::vector<uint64_t> picked((size_t)V, 0);
+    if (by_rows) {
+        colmap.resize(n);
+        for (uint64_t v = 0; v < n; v++) colmap[v] = mb.slot[mb.perm[v]];
+    }
     // per device, on the device: upload A, A' if directed (LAGraph_Cached_AT, pr.cpp:60), the
-    // hub-first order and this device's plan (pr_multi_plan), the exchange buffers
+    // hub-first order and each piece's plan (pr_multi_plan), the exchange buffers; or (by_rows)
+    // each piece's own rows, picked on the host, and its plan
     GX_TRY(per_device(ctxs, ndev, [&](int d) -> int {
-        GX_TRY(gx_graph_create(ctxs[d], A, directed, &G.g[d]));
-        if (directed) GX_TRY(ensure_transpose(G.g[d]));
-        GX_TRY(pr_multi_plan(G.g[d], ndev, d, M.chunk, damping, by_blocks ? &mb : nullptr, &M.part[d]));
-        rows[d] = M.part[d]->rows;
-        const size_t full = M.chunk * (size_t)ndev;
+        if (!by_rows) {
+            GX_TRY(gx_graph_create(ctxs[d], A, directed, &G.g[d]));
+            if (directed) GX_TRY(ensure_transpose(G.g[d]));
+        }
         hipStream_t s = ctxs[d]->stream;
+        for (int p = 0; p < P; p++) {
+            const size_t k = piece(d, p);
+            const int vr = p * ndev + d;
+            if (by_rows) {
+                std::vector<int32_t> &vs = vrows[k];
+                const std::vector<int32_t> &pos = mb.pos[vr];
+                vs.resize(pos.size());
+                for (size_t j = 0; j < pos.size(); j++) vs[j] = mb.order[pos[j]];
+                std::vector<int64_t> h_rp(vs.size() + 1);
+                uint64_t cnt = 0;
+                for (int32_t v : vs) cnt += A->rowptr[v + 1] - A->rowptr[v];
+                std::vector<int32_t> ci(cnt), od(vs.size());
+                if (!host_pick_rows_checked(A->rowptr, A->colidx, vs.data(), vs.size(), colmap.data(), n, h_rp.data(),
+                                            ci.data()))
+                    return fail(GX_INVALID_INDEX, "gx_pagerank_multi: column out of range");
+                uint64_t live = 0;
+                for (size_t j = 0; j < vs.size(); j++) {
+                    od[j] = (int32_t)(h_rp[j + 1] - h_rp[j]);
+                    live += od[j] > 0;
+                }
+                picked[k] = cnt;
+                GX_TRY(pr_part_build(ctxs[d], n, V, vr, M.chunk, live, h_rp, ci, od, damping, &M.part[k], by_blocks));
+            } else {
+                GX_TRY(pr_multi_plan(G.g[d], V, vr, M.chunk, damping, by_blocks ? &mb : nullptr, &M.part[k]));
+            }
+            rows[k] = M.part[k]->rows;
+            GX_TRY(M.xl[k]->alloc(M.chunk));
+            GX_TRY(M.ro[k]->alloc(std::max<uint64_t>(rows[k], 1)));
+            GX_HIP_TRY(hipMemsetAsync(M.xl[k]->p, 0, M.chunk * sizeof(double), s));
+        }
+        const size_t full = M.chunk * (size_t)V;
         GX_TRY(M.xr[d]->alloc(full));
         GX_TRY(M.xw[d]->alloc(full));
-        GX_TRY(M.xl[d]->alloc(M.chunk));
-        GX_TRY(M.ro[d]->alloc(std::max<uint64_t>(rows[d], 1)));
-        GX_HIP_TRY(hipMemsetAsync(M.xl[d]->p, 0, M.chunk * sizeof(double), s));
         GX_HIP_TRY(hipMemsetAsync(M.xr[d]->p, 0, full * sizeof(double), s));
         GX_HIP_TRY(hipMemsetAsync(M.xw[d]->p, 0, full * sizeof(double), s));
         return GX_SUCCESS;
     }));
+    if (by_rows && std::getenv("GX_PLAN_TIMES")) {
+        uint64_t tot = 0;
+        for (uint64_t c : picked) tot += c;
+        std::fprintf(stderr, "[multi] partitioned upload: %llu of %llu input columns read (%.3fx), %d devices x %d pieces\n",
+                     (unsigned long long)tot, (unsigned long long)A->nnz, A->nnz ? (double)tot / (double)A->nnz : 0.0,
+                     ndev, P);
+    }
     std::shared_ptr<Clique> clique;
     GX_TRY(get_clique(ctxs, ndev, &clique));
     Clique &C = *clique;
-    const size_t cbytes = M.chunk * sizeof(double);
-    auto gather = [&](std::vector<std::unique_ptr<DBuf<double>>> &dst) {
-        return C.all_gather([&](int d) { return (const void *)M.xl[d]->p; }, [&](int d) { return (void *)dst[d]->p; },
-                            cbytes);
-    };
-    // init, then per iteration: every device's SpMV, one grouped all-gather
-    for (int d = 0; d < ndev; d++) {
-        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
-        GX_TRY(pr_init(M.part[d], M.xl[d]->p, ctxs[d]->stream));
-    }
-    GX_TRY(gather(M.xr));
-    for (int it = 0; it < iters; it++) {
-        const bool last = it == iters - 1;
+    const size_t cbytes = M.chunk * sizeof(double), span = M.chunk * (size_t)ndev;
+    // piece p's chunks into slab p of every device's dst, on the compute streams (init) or,
+    // after each device's piece-p SpMV, on the comm streams
+    auto gather = [&](int p, std::vector<std::unique_ptr<DBuf<double>>> &dst, bool on_comm) -> int {
+        auto send = [&](int d) { return (const void *)M.xl[piece(d, p)]->p; };
+        auto recv = [&](int d) { return (void *)(dst[d]->p + (size_t)p * span); };
+        if (!on_comm) return C.all_gather(send, recv, cbytes);
         for (int d = 0; d < ndev; d++) {
             GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
-            GX_TRY(pr_step(M.part[d], M.xr[d]->p, M.xl[d]->p, last ? M.ro[d]->p : nullptr, ctxs[d]->stream));
+            hipEvent_t ev = C.ev_piece[(size_t)d * Clique::kMaxPieces + p];
+            GX_HIP_TRY(hipEventRecord(ev, C.st(d)));
+            GX_HIP_TRY(hipStreamWaitEvent(C.cs[d], ev, 0));
         }
-        if (last) break;
-        GX_TRY(gather(M.xw));
-        std::swap(M.xr, M.xw);
-    }
-    // scores back in A's vertex order: device d's local row j is vertex order_d[j]
+        return C.all_gather_on(send, recv, cbytes, [&](int d) { return C.cs[d]; });
+    };
+    // the compute streams wait for every exchange issued on the comm streams
+    auto join = [&]() -> int {
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_HIP_TRY(hipEventRecord(C.ev_comm[d], C.cs[d]));
+            GX_HIP_TRY(hipStreamWaitEvent(C.st(d), C.ev_comm[d], 0));
+        }
+        return GX_SUCCESS;
+    };
     for (int d = 0; d < ndev; d++) {
         GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
-        std::vector<double> buf(rows[d]);
-        std::vector<int32_t> who(rows[d]);
-        if (rows[d]) {
-            GX_HIP_TRY(hipMemcpyAsync(buf.data(), M.ro[d]->p, rows[d] * sizeof(double), hipMemcpyDeviceToHost,
-                                      ctxs[d]->stream));
-            GX_HIP_TRY(hipMemcpyAsync(who.data(), M.part[d]->order.p, rows[d] * sizeof(int32_t),
-                                      hipMemcpyDeviceToHost, ctxs[d]->stream));
+        for (int p = 0; p < P; p++) GX_TRY(pr_init(M.part[piece(d, p)], M.xl[piece(d, p)]->p, ctxs[d]->stream));
+    }
+    for (int p = 0; p < P; p++) GX_TRY(gather(p, M.xr, false));
+    for (int it = 0; it < iters; it++) {
+        const bool last = it == iters - 1;
+        for (int p = 0; p < P; p++) {
+            for (int d = 0; d < ndev; d++) {
+                GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+                const size_t k = piece(d, p);
+                GX_TRY(pr_step(M.part[k], M.xr[d]->p, M.xl[k]->p, last ? M.ro[k]->p : nullptr, ctxs[d]->stream));
+            }
+            if (!last) GX_TRY(gather(p, M.xw, true));
+        }
+        if (last) break;
+        GX_TRY(join());
+        std::swap(M.xr, M.xw);
+    }
+    // scores back in A's vertex order: piece k's local row j is vertex order_k[j]
+    for (int d = 0; d < ndev; d++) {
+        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+        std::vector<std::vector<double>> buf(P);
+        std::vector<std::vector<int32_t>> who(P);
+        for (int p = 0; p < P; p++) {
+            const size_t k = piece(d, p);
+            buf[p].resize(rows[k]);
+            who[p].resize(rows[k]);
+            if (rows[k]) {
+                GX_HIP_TRY(hipMemcpyAsync(buf[p].data(), M.ro[k]->p, rows[k] * sizeof(double), hipMemcpyDeviceToHost,
+                                          ctxs[d]->stream));
+                if (by_rows)
+                    std::copy(vrows[k].begin(), vrows[k].end(), who[p].begin());
+                else
+                    GX_HIP_TRY(hipMemcpyAsync(who[p].data(), M.part[k]->order.p, rows[k] * sizeof(int32_t),
+                                              hipMemcpyDeviceToHost, ctxs[d]->stream));
+            }
         }
         GX_HIP_TRY(hipStreamSynchronize(ctxs[d]->stream));
-        for (uint64_t j = 0; j < rows[d]; j++) rank[who[j]] = buf[j];
+        for (int p = 0; p < P; p++)
+            for (uint64_t j = 0; j < buf[p].size(); j++) rank[who[p][j]] = buf[p][j];
     }
     return GX_SUCCESS;
 }

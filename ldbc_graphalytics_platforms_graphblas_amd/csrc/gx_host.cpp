@@ -765,6 +765,28 @@ void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows
     }
 }
 
+bool host_pick_rows_checked(const uint64_t *rp, const uint64_t *ci, const int32_t *rows, uint64_t nrows,
+                            const int32_t *colmap, uint64_t limit, int64_t *out_rp, int32_t *out_ci) {
+    out_rp[0] = 0;
+    for (uint64_t j = 0; j < nrows; j++) out_rp[j + 1] = out_rp[j] + (int64_t)(rp[rows[j] + 1] - rp[rows[j]]);
+    int bad = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(| : bad)
+    for (int64_t j = 0; j < (int64_t)nrows; j++) {
+        const uint64_t b = rp[rows[j]], e = rp[rows[j] + 1];
+        int32_t *o = out_ci + out_rp[j];
+        for (uint64_t k = b; k < e; k++) {
+            const uint64_t c = ci[k];
+            if (c >= limit) {
+                bad = 1;
+                o[k - b] = 0;
+            } else {
+                o[k - b] = colmap[c];
+            }
+        }
+    }
+    return !bad;
+}
+
 void host_transpose(uint64_t n, const uint64_t *rp, const uint64_t *ci, uint64_t *trp, uint64_t *tci) {
     const uint64_t nnz = rp[n];
     std::fill(trp, trp + n + 1, 0);

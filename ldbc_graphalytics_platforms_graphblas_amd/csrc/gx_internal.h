@@ -38,6 +38,10 @@ void host_hub_order(const uint64_t *rp, uint64_t n, uint32_t *order);
 // the rows `rows[j]` of (rp, ci) as a local CSR (out_rp from 0) with columns renamed by colmap
 void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows, uint64_t nrows, const int32_t *colmap,
                     int64_t *out_rp, int32_t *out_ci);
+// the same for a multi-device PageRank rank's rows (vertex ids), with every column checked
+// against `limit` (false: a column >= limit, written as 0)
+bool host_pick_rows_checked(const uint64_t *rp, const uint64_t *ci, const int32_t *rows, uint64_t nrows,
+                            const int32_t *colmap, uint64_t limit, int64_t *out_rp, int32_t *out_ci);
 // Write one byte per 4 KiB page of a caller's output buffer (parallel) while the device
 // computes: its first-touch page faults are then off the result copy's critical path.
 void host_prefault(void *p, size_t bytes);

@@ -264,8 +264,12 @@ struct MultiBlocks {
     std::vector<std::vector<int32_t>> pos;
     std::vector<int32_t> slot;
     uint64_t chunk = 0;
+    std::vector<int32_t> order, perm;   // the host hub-first order: position -> vertex, vertex -> position
 };
 int pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *out);
+// The interleaved partition in the same form: hub-first position h to rank h % ndev as its
+// local row h / ndev (pr_partition.interleaved_relabel).
+int pr_multi_interleave(const gx_csr *A, int ndev, MultiBlocks *out);
 
 // gx_pagerank_multi's plan of device d of ndev from its copy of the graph (A' built when
 // directed): hub-first positions d, d + ndev, ... as rows (or mb's blocks), columns in the
@@ -274,9 +278,10 @@ int pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double damping, 
                   PrPart **out);
 // A rank's plan from its local pull rows (h_rp from 0) with columns already in the exchange
 // layout (ci), the out-degree of each row's vertex, and its live prefix (gx_pr_part_create_live).
+// force_huge: plan with the whole graph's block cut (a rank of a block partition).
 int pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint64_t chunk, uint64_t live,
                   const std::vector<int64_t> &h_rp, const std::vector<int32_t> &ci, const std::vector<int32_t> &h_outdeg,
-                  double damping, PrPart **out);
+                  double damping, PrPart **out, bool force_huge = false);
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 
 }  // namespace gx

@@ -823,8 +823,9 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
 // column map read the same (device) order.
 int gx::pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *out) {
     const uint64_t n = A->n;
-    std::vector<int32_t> outdeg(n), order, perm;
+    std::vector<int32_t> outdeg(n);
     for (uint64_t v = 0; v < n; v++) outdeg[v] = (int32_t)(A->rowptr[v + 1] - A->rowptr[v]);
+    std::vector<int32_t> &order = out->order, &perm = out->perm;
     hub_order(outdeg, order, perm);
     std::vector<int64_t> len(n);
     if (directed) {
@@ -910,6 +911,27 @@ int gx::pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *ou
     for (int d = 0; d < ndev; d++)
         for (size_t j = 0; j < out->pos[d].size(); j++)
             out->slot[out->pos[d][j]] = (int32_t)((uint64_t)d * out->chunk + j);
+    return GX_SUCCESS;
+}
+
+int gx::pr_multi_interleave(const gx_csr *A, int ndev, MultiBlocks *out) {
+    const uint64_t n = A->n;
+    std::vector<int32_t> outdeg(n);
+    uint64_t nlive = 0;
+    for (uint64_t v = 0; v < n; v++) {
+        outdeg[v] = (int32_t)(A->rowptr[v + 1] - A->rowptr[v]);
+        nlive += outdeg[v] > 0;
+    }
+    hub_order(outdeg, out->order, out->perm);
+    out->chunk = ((nlive + ndev - 1) / ndev + 2 + 31) / 32 * 32;
+    if (out->chunk * (uint64_t)ndev >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
+    out->pos.assign(ndev, {});
+    out->slot.assign(n, 0);
+    for (uint64_t h = 0; h < n; h++) {
+        const int d = (int)(h % (uint64_t)ndev);
+        out->slot[h] = (int32_t)((uint64_t)d * out->chunk + out->pos[d].size());
+        out->pos[d].push_back((int32_t)h);
+    }
     return GX_SUCCESS;
 }
 
@@ -1173,7 +1195,7 @@ extern "C" int gx_pr_part_create_live(gx_ctx *ctx, uint64_t n_global, int nranks
 
 int gx::pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint64_t chunk, uint64_t live,
                       const std::vector<int64_t> &h_rp, const std::vector<int32_t> &ci,
-                      const std::vector<int32_t> &h_outdeg, double damping, PrPart **out) {
+                      const std::vector<int32_t> &h_outdeg, double damping, PrPart **out, bool force_huge) {
     const uint64_t rows = h_rp.size() - 1, nnz = (uint64_t)h_rp[rows];
     auto *p = new PrPart();
     p->ctx = ctx;
@@ -1183,6 +1205,7 @@ int gx::pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint
     p->chunk = chunk;
     p->live = live;
     p->damping = damping;
+    p->force_huge = force_huge;
     int rc = p->rp_own.alloc(rows + 1);
     if (rc == GX_SUCCESS) rc = p->ci_own.alloc(nnz, 16);
     if (rc == GX_SUCCESS) rc = p->outdeg_own.alloc(std::max<uint64_t>(rows, 1));

@@ -626,6 +626,33 @@ def test_multi_virtual_devices_blocks(k, undirected, rows, nnz, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2, 3])
+@pytest.mark.parametrize("pieces", [1, 3, 8])
+@pytest.mark.parametrize("layout", ["interleave", "blocks"])
+def test_multi_virtual_devices_pieces(k, pieces, layout, monkeypatch):
+    """gx_pagerank_multi's pipelined pieces (round 6): each device's rows
+    cut into `pieces` plans, piece p of device d being virtual rank p * k + d; piece p's chunks
+    all-gathered on the comm streams while piece p + 1 runs.  One piece (no overlap), more
+    pieces than some devices have live rows (8 pieces of a 2^10-vertex graph over 3 devices),
+    both partitions, directed and undirected; rtol 1e-12 against the oracle."""
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    monkeypatch.setenv("GX_PR_MULTI_PIECES", str(pieces))
+    monkeypatch.setenv("GX_PR_MULTI_PARTITION", layout)
+    monkeypatch.setenv("GX_PR_MULTI_BLOCK_ROWS", "64")
+    monkeypatch.setenv("GX_PR_MULTI_BLOCK_NNZ", "4096")
+    ctxs = [Context(0) for _ in range(k)]
+    try:
+        for undirected in (True, False):
+            for scale, ef in ((10, 8), (13, 16)):
+                csr = rmat(scale, ef, 11 + scale, undirected=undirected)
+                got = _multi_call("gx_pagerank_multi", ctxs, csr, int(not undirected), 0.85, 10)
+                np.testing.assert_allclose(got, O.pagerank(csr, not undirected, 0.85, 10), rtol=1e-12, atol=0)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.gpu
 def test_multi_virtual_devices_edge_cases():
     """More virtual devices than rows with out-edges (some own nothing live), an edgeless graph,
     and LCC on one device (a size-1 RCCL clique and its ncclReduce)."""
