@@ -893,6 +893,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     // separate plan took 149)
     if (ndev == 1 && P == 1) return gx_pagerank_csr(ctxs[0], A, directed, damping, iters, rank, nullptr);
     const int V = ndev * P;
+    PlanClock clk("multi_call", ctxs[0]->stream);
     // interleaved hub-first partition (pr_partition.interleaved_relabel): hub-first position i
     // goes to virtual rank i % V as its local row i / V.  The vertices with out-edges come first
     // in that order, so virtual rank 0 holds the most live rows, ceil(nlive / V): the chunk every
@@ -904,8 +905,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     // rank's blocks are the single-GPU plan's own, so its gathers share x lines as the whole
     // graph's do (1/8 pieces of SYN-8_5: 140 us per SpMV against 208 interleaved).
     // GX_PR_MULTI_PARTITION=blocks / interleave overrides.
-    uint64_t nlive = 0;
-    for (uint64_t v = 0; v < n; v++) nlive += A->rowptr[v + 1] != A->rowptr[v];
+    const uint64_t nlive = host_count_live(A->rowptr, n);
     MultiRun M;
     M.ndev = ndev;
     M.npieces = P;
@@ -913,13 +913,15 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     bool by_blocks = V > 1 && (double)A->rowptr[n] / (double)std::max(1, ctxs[0]->num_cus) > (double)(2 << 20);
     if (const char *e = std::getenv("GX_PR_MULTI_PARTITION")) by_blocks = std::strcmp(e, "blocks") == 0;
     // Partitioned upload (round 6; GX_PR_MULTI_UPLOAD=rows, the default for
-    // undirected graphs, whose pull rows are A's own): the host deals the hub-first order once
-    // and every virtual rank's rows leave the 64-bit input once, already in the exchange
-    // layout (host_pick_rows_checked), for that rank's device only -- the plan of bench.py's N > 1
-    // path (gx_pr_part_create).  "whole" (and every directed graph, whose pull rows are A''s)
-    // uploads A to every device and plans there (pr_multi_plan).
+    // undirected graphs, whose pull rows are A's own): the host deals the hub-first order once,
+    // and every virtual rank's rows leave the 64-bit input once, for that rank's device only,
+    // picked straight into the staging buffers (pr_part_build_rows); the plan's key pass renames
+    // the columns into the exchange layout through a device column map.  "whole" (and every
+    // directed graph, whose pull rows are A''s) uploads A to every device and plans there
+    // (pr_multi_plan).
     bool by_rows = !directed;
     if (const char *e = std::getenv("GX_PR_MULTI_UPLOAD")) by_rows = by_rows && std::strcmp(e, "whole") != 0;
+    if (const char *e = std::getenv("GX_PR_KERNEL")) by_rows = by_rows && std::strcmp(e, "adaptive") != 0;   // reads raw columns
     if (by_rows) {
         if (A->rowptr[0] != 0 || A->rowptr[n] != A->nnz || !host_monotone(A->rowptr, n))
             return fail(GX_INVALID_VALUE, "gx_pagerank_multi: inconsistent row pointers");
@@ -951,11 +953,13 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
     // map vertex -> exchange slot
     std::vector<std::vector<int32_t>> vrows(by_rows ? (size_t)V : 0);
     std::vector<int32_t> colmap;
-    std::vector<uint64_t> picked((size_t)V, 0);
+    std::vector<uint64_t> picked((size_t)V, 0);   // input columns each piece read
+    std::vector<std::unique_ptr<DBuf<int32_t>>> cmap(by_rows ? ndev : 0);
     if (by_rows) {
         colmap.resize(n);
-        for (uint64_t v = 0; v < n; v++) colmap[v] = mb.slot[mb.perm[v]];
+        host_compose(mb.slot.data(), mb.perm.data(), n, colmap.data());
     }
+    clk.mark("partition (host)");
     // per device, on the device: upload A, A' if directed (LAGraph_Cached_AT, pr.cpp:60), the
     // hub-first order and each piece's plan (pr_multi_plan), the exchange buffers; or (by_rows)
     // each piece's own rows, picked on the host, and its plan
@@ -963,6 +967,16 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         if (!by_rows) {
             GX_TRY(gx_graph_create(ctxs[d], A, directed, &G.g[d]));
             if (directed) GX_TRY(ensure_transpose(G.g[d]));
+        } else {
+            // the column map, once per device (the pieces' key passes rename through it)
+            cmap[d].reset(new DBuf<int32_t>());
+            GX_TRY(cmap[d]->alloc(n));
+            bool bad = false;
+            GX_TRY(upload_staged(ctxs[d], cmap[d]->p, n, 4,
+                                 [&](uint64_t off, uint64_t cnt, void *buf) {
+                                     host_copy(buf, colmap.data() + off, cnt * 4);
+                                     return true;
+                                 }, &bad));
         }
         hipStream_t s = ctxs[d]->stream;
         for (int p = 0; p < P; p++) {
@@ -973,20 +987,8 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
                 const std::vector<int32_t> &pos = mb.pos[vr];
                 vs.resize(pos.size());
                 for (size_t j = 0; j < pos.size(); j++) vs[j] = mb.order[pos[j]];
-                std::vector<int64_t> h_rp(vs.size() + 1);
-                uint64_t cnt = 0;
-                for (int32_t v : vs) cnt += A->rowptr[v + 1] - A->rowptr[v];
-                std::vector<int32_t> ci(cnt), od(vs.size());
-                if (!host_pick_rows_checked(A->rowptr, A->colidx, vs.data(), vs.size(), colmap.data(), n, h_rp.data(),
-                                            ci.data()))
-                    return fail(GX_INVALID_INDEX, "gx_pagerank_multi: column out of range");
-                uint64_t live = 0;
-                for (size_t j = 0; j < vs.size(); j++) {
-                    od[j] = (int32_t)(h_rp[j + 1] - h_rp[j]);
-                    live += od[j] > 0;
-                }
-                picked[k] = cnt;
-                GX_TRY(pr_part_build(ctxs[d], n, V, vr, M.chunk, live, h_rp, ci, od, damping, &M.part[k], by_blocks));
+                for (int32_t v : vs) picked[k] += A->rowptr[v + 1] - A->rowptr[v];
+                GX_TRY(pr_part_build_rows(ctxs[d], A, V, vr, M.chunk, vs, cmap[d]->p, damping, by_blocks, &M.part[k]));
             } else {
                 GX_TRY(pr_multi_plan(G.g[d], V, vr, M.chunk, damping, by_blocks ? &mb : nullptr, &M.part[k]));
             }
@@ -1002,6 +1004,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         GX_HIP_TRY(hipMemsetAsync(M.xw[d]->p, 0, full * sizeof(double), s));
         return GX_SUCCESS;
     }));
+    clk.mark("devices: upload + plans");
     if (by_rows && std::getenv("GX_PLAN_TIMES")) {
         uint64_t tot = 0;
         for (uint64_t c : picked) tot += c;
@@ -1055,6 +1058,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         GX_TRY(join());
         std::swap(M.xr, M.xw);
     }
+    clk.mark("iterations");
     // scores back in A's vertex order: piece k's local row j is vertex order_k[j]
     for (int d = 0; d < ndev; d++) {
         GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
@@ -1078,6 +1082,7 @@ extern "C" int gx_pagerank_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A,
         for (int p = 0; p < P; p++)
             for (uint64_t j = 0; j < buf[p].size(); j++) rank[who[p][j]] = buf[p][j];
     }
+    clk.mark("scores");
     return GX_SUCCESS;
 }
 

@@ -15,6 +15,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <thread>
 #include <memory>
@@ -162,6 +163,10 @@ int ensure_host_rp(gx_ctx *ctx, DevCSR &c);
 // conversion of each chunk (parallel, on the host) overlapping the next chunk's DMA.
 enum class Xfer { Raw64, Raw32, Levels, Widen32 };   // 8 / 4 B as is; int32 level -> int64 (INF); int32 -> uint64
 int download(gx_ctx *ctx, void *dst, const void *src_dev, uint64_t count, Xfer kind);
+// Host -> device of `count` elements of `elem` bytes through the pinned staging buffers:
+// fill(off, cnt, buf) writes elements [off, off + cnt) into buf (false: bad input, *bad set).
+int upload_staged(gx_ctx *ctx, void *dst, uint64_t count, size_t elem,
+                  const std::function<bool(uint64_t, uint64_t, void *)> &fill, bool *bad);
 // SSSP edge layout: every row of A split into its light (w < delta) edges, then its heavy
 // ones; built once per graph and delta by gx_sssp.
 struct SsspLayout {

@@ -765,23 +765,87 @@ void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows
     }
 }
 
-bool host_pick_rows_checked(const uint64_t *rp, const uint64_t *ci, const int32_t *rows, uint64_t nrows,
-                            const int32_t *colmap, uint64_t limit, int64_t *out_rp, int32_t *out_ci) {
-    out_rp[0] = 0;
-    for (uint64_t j = 0; j < nrows; j++) out_rp[j + 1] = out_rp[j] + (int64_t)(rp[rows[j] + 1] - rp[rows[j]]);
+void host_hub_order_par(const uint64_t *rp, uint64_t n, int32_t *order, int32_t *perm, int64_t *hdeg) {
+    // stable counting sort by descending degree, in parallel: degrees below kD by a histogram per
+    // thread (threads own contiguous vertex ranges, so equal degrees keep id order), the few
+    // hubs at or above it sorted on their own and put first
+    constexpr uint64_t kD = 1u << 16;
+    const int T = std::max(1, omp_get_max_threads());
+    std::vector<uint64_t> cnt((size_t)T * kD, 0);
+    std::vector<std::vector<uint32_t>> big(T);
+#pragma omp parallel num_threads(T)
+    {
+        const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+        const uint64_t v0 = n * t / nt, v1 = n * (t + 1) / nt;
+        uint64_t *c = cnt.data() + (size_t)t * kD;
+        for (uint64_t v = v0; v < v1; v++) {
+            const uint64_t d = rp[v + 1] - rp[v];
+            if (d >= kD) big[t].push_back((uint32_t)v);
+            else c[kD - 1 - d]++;   // bucket 0 = degree kD - 1 (descending order)
+        }
+    }
+    std::vector<uint32_t> hubs;
+    for (auto &b : big) hubs.insert(hubs.end(), b.begin(), b.end());
+    std::stable_sort(hubs.begin(), hubs.end(),
+                     [&](uint32_t a, uint32_t b) { return rp[a + 1] - rp[a] > rp[b + 1] - rp[b]; });
+    // exclusive offsets, bucket-major then thread
+    std::vector<uint64_t> off((size_t)T * kD);
+    uint64_t acc = hubs.size();
+    for (uint64_t b = 0; b < kD; b++)
+        for (int t = 0; t < T; t++) {
+            off[(size_t)t * kD + b] = acc;
+            acc += cnt[(size_t)t * kD + b];
+        }
+    for (size_t h = 0; h < hubs.size(); h++) {
+        order[h] = (int32_t)hubs[h];
+        perm[hubs[h]] = (int32_t)h;
+        hdeg[h] = (int64_t)(rp[hubs[h] + 1] - rp[hubs[h]]);
+    }
+#pragma omp parallel num_threads(T)
+    {
+        const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+        const uint64_t v0 = n * t / nt, v1 = n * (t + 1) / nt;
+        uint64_t *o = off.data() + (size_t)t * kD;
+        for (uint64_t v = v0; v < v1; v++) {
+            const uint64_t d = rp[v + 1] - rp[v];
+            if (d >= kD) continue;
+            const uint64_t pos = o[kD - 1 - d]++;
+            order[pos] = (int32_t)v;
+            perm[v] = (int32_t)pos;
+            hdeg[pos] = (int64_t)d;
+        }
+    }
+}
+
+void host_compose(const int32_t *a, const int32_t *idx, uint64_t n, int32_t *out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t v = 0; v < (int64_t)n; v++) out[v] = a[idx[v]];
+}
+
+uint64_t host_count_live(const uint64_t *rp, uint64_t n) {
+    uint64_t c = 0;
+#pragma omp parallel for schedule(static) reduction(+ : c)
+    for (int64_t v = 0; v < (int64_t)n; v++) c += rp[v + 1] != rp[v];
+    return c;
+}
+
+bool host_pick_span(const uint64_t *rp, const uint64_t *ci, const int32_t *rows, const int64_t *lrp, uint64_t nrows,
+                    uint64_t e0, uint64_t e1, uint64_t limit, int32_t *out) {
+    if (e1 <= e0) return true;
+    // the local rows overlapping [e0, e1): j0 = last row starting at or before e0
+    const int64_t j0 = (int64_t)(std::upper_bound(lrp, lrp + nrows + 1, (int64_t)e0) - lrp) - 1;
+    const int64_t j1 = (int64_t)(std::lower_bound(lrp, lrp + nrows + 1, (int64_t)e1) - lrp);
     int bad = 0;
-#pragma omp parallel for schedule(dynamic, 256) reduction(| : bad)
-    for (int64_t j = 0; j < (int64_t)nrows; j++) {
-        const uint64_t b = rp[rows[j]], e = rp[rows[j] + 1];
-        int32_t *o = out_ci + out_rp[j];
-        for (uint64_t k = b; k < e; k++) {
-            const uint64_t c = ci[k];
-            if (c >= limit) {
-                bad = 1;
-                o[k - b] = 0;
-            } else {
-                o[k - b] = colmap[c];
-            }
+#pragma omp parallel for schedule(dynamic, 64) reduction(| : bad)
+    for (int64_t j = std::max<int64_t>(j0, 0); j < std::min<int64_t>(j1, (int64_t)nrows); j++) {
+        const int64_t lb = std::max<int64_t>(lrp[j], (int64_t)e0), le = std::min<int64_t>(lrp[j + 1], (int64_t)e1);
+        if (lb >= le) continue;
+        const uint64_t *src = ci + rp[rows[j]] + (uint64_t)(lb - lrp[j]);
+        int32_t *o = out + (lb - (int64_t)e0);
+        for (int64_t k = 0; k < le - lb; k++) {
+            const uint64_t c = src[k];
+            bad |= c >= limit;
+            o[k] = (int32_t)(c < limit ? c : 0);
         }
     }
     return !bad;

@@ -38,10 +38,17 @@ void host_hub_order(const uint64_t *rp, uint64_t n, uint32_t *order);
 // the rows `rows[j]` of (rp, ci) as a local CSR (out_rp from 0) with columns renamed by colmap
 void host_pick_rows(const uint64_t *rp, const uint64_t *ci, const uint32_t *rows, uint64_t nrows, const int32_t *colmap,
                     int64_t *out_rp, int32_t *out_ci);
-// the same for a multi-device PageRank rank's rows (vertex ids), with every column checked
-// against `limit` (false: a column >= limit, written as 0)
-bool host_pick_rows_checked(const uint64_t *rp, const uint64_t *ci, const int32_t *rows, uint64_t nrows,
-                            const int32_t *colmap, uint64_t limit, int64_t *out_rp, int32_t *out_ci);
+// hub-first order in parallel (the same order as host_hub_order): order[h] = vertex, perm[v] =
+// position, hdeg[h] = degree of the vertex at position h
+void host_hub_order_par(const uint64_t *rp, uint64_t n, int32_t *order, int32_t *perm, int64_t *hdeg);
+// out[v] = a[idx[v]] (parallel)
+void host_compose(const int32_t *a, const int32_t *idx, uint64_t n, int32_t *out);
+// rows with at least one entry
+uint64_t host_count_live(const uint64_t *rp, uint64_t n);
+// entries [e0, e1) of the local CSR made of the rows `rows[j]` of (rp, ci) (local row
+// pointers lrp, from 0), narrowed to int32 into out[0, e1 - e0); false: a column >= limit
+bool host_pick_span(const uint64_t *rp, const uint64_t *ci, const int32_t *rows, const int64_t *lrp, uint64_t nrows,
+                    uint64_t e0, uint64_t e1, uint64_t limit, int32_t *out);
 // Write one byte per 4 KiB page of a caller's output buffer (parallel) while the device
 // computes: its first-touch page faults are then off the result copy's critical path.
 void host_prefault(void *p, size_t bytes);

@@ -282,6 +282,13 @@ int pr_multi_plan(gx_graph *g, int ndev, int d, uint64_t chunk, double damping, 
 int pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint64_t chunk, uint64_t live,
                   const std::vector<int64_t> &h_rp, const std::vector<int32_t> &ci, const std::vector<int32_t> &h_outdeg,
                   double damping, PrPart **out, bool force_huge = false);
+// gx_pagerank_multi's partitioned upload: a rank's rows `rows` (vertex ids of A, an undirected
+// graph's pull rows) picked from the host CSR A straight into the staging buffers (original
+// column ids, narrowed and checked), renamed to the exchange layout by the plan's key pass
+// through colmap (device, n entries: vertex -> owner * chunk + local row).
+int pr_part_build_rows(gx_ctx *ctx, const gx_csr *A, int nranks, int rank, uint64_t chunk,
+                       const std::vector<int32_t> &rows, const int32_t *colmap, double damping, bool force_huge,
+                       PrPart **out);
 int pr_step(PrPart *p, const double *x_full, double *x_local, double *rank_out, hipStream_t s);
 
 }  // namespace gx

@@ -823,18 +823,30 @@ int gx::pr_single_plan(gx_graph *g, PrPart **out) {
 // column map read the same (device) order.
 int gx::pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *out) {
     const uint64_t n = A->n;
-    std::vector<int32_t> outdeg(n);
-    for (uint64_t v = 0; v < n; v++) outdeg[v] = (int32_t)(A->rowptr[v + 1] - A->rowptr[v]);
+    // hub-first order, its degrees, all on the host's threads (the serial counting sort and its
+    // random re-reads of the degrees were ~350 ms of SYN-8_5's partition)
     std::vector<int32_t> &order = out->order, &perm = out->perm;
-    hub_order(outdeg, order, perm);
-    std::vector<int64_t> len(n);
-    if (directed) {
+    order.resize(n);
+    perm.resize(n);
+    std::vector<int64_t> hdeg(n);   // out-degree of the vertex at each hub-first position
+    const bool tm = std::getenv("GX_PLAN_TIMES") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (!tm) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[plan multi_blocks] %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    };
+    host_hub_order_par(A->rowptr, n, order.data(), perm.data(), hdeg.data());
+    mark("hub order (host)");
+    std::vector<int64_t> indeg_h;
+    if (directed) {   // the pull rows are A''s: their lengths are the in-degrees
         std::vector<int64_t> indeg(n, 0);
         for (uint64_t e = 0; e < A->rowptr[n]; e++) indeg[A->colidx[e]]++;
-        for (uint64_t h = 0; h < n; h++) len[h] = indeg[order[h]];
-    } else {
-        for (uint64_t h = 0; h < n; h++) len[h] = outdeg[order[h]];
+        indeg_h.resize(n);
+        for (uint64_t h = 0; h < n; h++) indeg_h[h] = indeg[order[h]];
     }
+    const std::vector<int64_t> &len = directed ? indeg_h : hdeg;
     auto env = [](const char *name, int64_t dflt, int64_t lo, int64_t hi) {
         const char *e = std::getenv(name);
         const int64_t v = e ? std::atoll(e) : dflt;
@@ -853,6 +865,7 @@ int gx::pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *ou
         r = e;
     }
     starts.push_back((int64_t)n);
+    mark("block cut");
     const size_t nb = starts.size() - 1;
     // work = entries + rows (the epilogue); live = rows with out-edges (the exchanged chunk)
     std::vector<int64_t> work(nb), blive(nb);
@@ -860,7 +873,7 @@ int gx::pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *ou
         int64_t s = 0, l = 0;
         for (int64_t h = starts[b]; h < starts[b + 1]; h++) {
             s += len[h];
-            l += outdeg[order[h]] > 0;
+            l += hdeg[h] > 0;
         }
         work[b] = s + (starts[b + 1] - starts[b]);
         blive[b] = l;
@@ -895,34 +908,37 @@ int gx::pr_multi_blocks(const gx_csr *A, int directed, int ndev, MultiBlocks *ou
         load[d] += (double)work[b];
         lv[d] += blive[b];
     }
+    mark("work + deal");
     out->pos.assign(ndev, {});
+    std::vector<uint64_t> npos(ndev, 0), lvd(ndev, 0);
+    for (size_t b = 0; b < nb; b++) {
+        npos[owner[b]] += (uint64_t)(starts[b + 1] - starts[b]);
+        lvd[owner[b]] += (uint64_t)blive[b];
+    }
+    for (int d = 0; d < ndev; d++) out->pos[d].reserve(npos[d]);
     for (size_t b = 0; b < nb; b++)
         for (int64_t h = starts[b]; h < starts[b + 1]; h++) out->pos[owner[b]].push_back((int32_t)h);
     uint64_t live = 0;
-    for (int d = 0; d < ndev; d++) {
-        uint64_t l = 0;
-        for (int32_t h : out->pos[d]) l += outdeg[order[h]] > 0;
-        live = std::max(live, l);
-    }
+    for (int d = 0; d < ndev; d++) live = std::max(live, lvd[d]);
     out->chunk = (live + 2 + 31) / 32 * 32;
     if (out->chunk * (uint64_t)ndev >= (1ull << 31))
         return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
+    mark("positions");
     out->slot.assign(n, 0);
     for (int d = 0; d < ndev; d++)
         for (size_t j = 0; j < out->pos[d].size(); j++)
             out->slot[out->pos[d][j]] = (int32_t)((uint64_t)d * out->chunk + j);
+    mark("slots");
     return GX_SUCCESS;
 }
 
 int gx::pr_multi_interleave(const gx_csr *A, int ndev, MultiBlocks *out) {
     const uint64_t n = A->n;
-    std::vector<int32_t> outdeg(n);
-    uint64_t nlive = 0;
-    for (uint64_t v = 0; v < n; v++) {
-        outdeg[v] = (int32_t)(A->rowptr[v + 1] - A->rowptr[v]);
-        nlive += outdeg[v] > 0;
-    }
-    hub_order(outdeg, out->order, out->perm);
+    const uint64_t nlive = host_count_live(A->rowptr, n);
+    out->order.resize(n);
+    out->perm.resize(n);
+    std::vector<int64_t> hdeg(n);
+    host_hub_order_par(A->rowptr, n, out->order.data(), out->perm.data(), hdeg.data());
     out->chunk = ((nlive + ndev - 1) / ndev + 2 + 31) / 32 * 32;
     if (out->chunk * (uint64_t)ndev >= (1ull << 31)) return fail(GX_NOT_IMPLEMENTED, "gx_pagerank_multi: exchange too large");
     out->pos.assign(ndev, {});
@@ -1225,6 +1241,61 @@ int gx::pr_part_build(gx_ctx *ctx, uint64_t n_global, int nranks, int rank, uint
         return rc;
     }
     *out = p;
+    return GX_SUCCESS;
+}
+
+int gx::pr_part_build_rows(gx_ctx *ctx, const gx_csr *A, int nranks, int rank, uint64_t chunk,
+                           const std::vector<int32_t> &rows, const int32_t *colmap, double damping, bool force_huge,
+                           PrPart **out) {
+    const uint64_t nr = rows.size();
+    std::vector<int64_t> h_rp(nr + 1);
+    std::vector<int32_t> h_outdeg(nr);
+    h_rp[0] = 0;
+    uint64_t live = 0;
+    for (uint64_t j = 0; j < nr; j++) {
+        const int64_t len = (int64_t)(A->rowptr[rows[j] + 1] - A->rowptr[rows[j]]);
+        h_rp[j + 1] = h_rp[j] + len;
+        h_outdeg[j] = (int32_t)len;   // undirected: the pull row is the vertex's out-edge list
+        live += len > 0;
+    }
+    const uint64_t nnz = (uint64_t)h_rp[nr];
+    std::unique_ptr<PrPart> p(new PrPart());
+    p->ctx = ctx;
+    p->n_global = A->n;
+    p->nranks = nranks;
+    p->rank = rank;
+    p->chunk = chunk;
+    p->live = live;
+    p->damping = damping;
+    p->force_huge = force_huge;
+    GX_TRY(p->rp_own.alloc(nr + 1));
+    GX_TRY(p->ci_own.alloc(nnz, 16));
+    GX_TRY(p->outdeg_own.alloc(std::max<uint64_t>(nr, 1)));
+    bool bad = false;
+    GX_TRY(upload_staged(ctx, p->rp_own.p, nr + 1, 8,
+                         [&](uint64_t off, uint64_t cnt, void *buf) {
+                             host_copy(buf, h_rp.data() + off, cnt * 8);
+                             return true;
+                         }, &bad));
+    if (nr)
+        GX_TRY(upload_staged(ctx, p->outdeg_own.p, nr, 4,
+                             [&](uint64_t off, uint64_t cnt, void *buf) {
+                                 host_copy(buf, h_outdeg.data() + off, cnt * 4);
+                                 return true;
+                             }, &bad));
+    GX_TRY(upload_staged(ctx, p->ci_own.p, nnz, 4,
+                         [&](uint64_t off, uint64_t cnt, void *buf) {
+                             return host_pick_span(A->rowptr, A->colidx, rows.data(), h_rp.data(), nr, off, off + cnt,
+                                                   A->n, static_cast<int32_t *>(buf));
+                         }, &bad));
+    if (bad) return fail(GX_INVALID_INDEX, "gx_pagerank_multi: column out of range");
+    p->src_rp = p->rp_own.p;
+    p->src_ci = p->ci_own.p;
+    p->src_perm = colmap;
+    GX_TRY(pr_plan(p.get(), HostView<int64_t>(h_rp), p->rp_own.p, p->ci_own.p, p->outdeg_own.p,
+                   HostView<int32_t>(h_outdeg)));
+    GX_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    *out = p.release();
     return GX_SUCCESS;
 }
 

@@ -403,6 +403,11 @@ int upload_columns(gx_ctx *ctx, const uint64_t *cols, uint64_t nnz, uint64_t n, 
 
 }  // namespace
 
+int upload_staged(gx_ctx *ctx, void *dst, uint64_t count, size_t elem,
+                  const std::function<bool(uint64_t, uint64_t, void *)> &fill, bool *bad) {
+    return upload(ctx, static_cast<char *>(dst), count, elem, fill, bad);
+}
+
 UploadJob::~UploadJob() {
     if (th.joinable()) th.join();
     (void)hipSetDevice(device);
