@@ -255,7 +255,9 @@ __device__ __forceinline__ void long_segment(const SortedArgs &a, const RowBlock
 // entries (the instruction count of a layout loading each lane's column span once); 14
 // (gather_narrow only) only the first entry of each column run gathers, the rest read 0; 15 as 14
 // with the run's value handed on by ds_bpermute (correct results); 16 = the product kernel
-// under the probes' launch (no queue), the baseline for 12-15.
+// under the probes' launch (no queue), the baseline for 12-15; 17 the wide entries (gather_units:
+// 4-byte packed entries and escapes) load and decode but do not gather (narrow unchanged), 18 no
+// wide entries at all (gather_units skipped): the wide tail's share of the launch (round 6).
 template <int PROBE, int CP>   // CP bit 0: index loads non-temporal (bit 2: gather_narrow)
 __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock &b, int64_t lo64, int64_t hi64,
                                              double *acc, int64_t step64, int32_t k0 = 0, int32_t k1 = 0x7fffffff) {
@@ -344,7 +346,7 @@ __device__ __forceinline__ void gather_units(const SortedArgs &a, const RowBlock
         }
 #pragma unroll
         for (int i = 0; i < kU; i++) {
-            if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11) t.g[i] = (double)c[i];
+            if constexpr (PROBE == 2 || PROBE == 3 || PROBE == 5 || PROBE == 11 || PROBE == 17) t.g[i] = (double)c[i];
             else if constexpr (PROBE == 4) t.g[i] = a.x_in[c[i] & 4095];
             else if constexpr (PROBE == 8) t.g[i] = a.x_in[c[i] >= (1 << 19) ? (c[i] & ((1 << 19) - 1)) : c[i]];
             else if constexpr (PROBE == 9) t.g[i] = a.x_in[c[i] & 65535];
@@ -662,7 +664,7 @@ __device__ __forceinline__ void pull_item(const SortedArgs &a, const uint32_t w,
             if (tid == 0) *reinterpret_cast<volatile uint32_t *>(slot) = 0u;   // this CU's sweep is over
         } else if constexpr (PROBE != 10) {   // probe 10: no entries at all (the fixed costs)
             gather_narrow<CP, PROBE>(a, u, acc);
-            gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step);
+            if constexpr (PROBE != 18) gather_units<PROBE, CP>(a, b, u.lo, u.hi, acc, u.step);
         }
         __syncthreads();
     }
@@ -1954,7 +1956,7 @@ int pr_step_sorted(PrPart *p, const double *x_full, double *x_local, double *ran
                                  else hipLaunchKernelGGL((k_pr_pull_units<false, k>), dim3(nw), dim3(kBS), lds, s, a); break;
                 GX_PROBE_CASE(1) GX_PROBE_CASE(2) GX_PROBE_CASE(3) GX_PROBE_CASE(4) GX_PROBE_CASE(5) GX_PROBE_CASE(6) GX_PROBE_CASE(7)
                 GX_PROBE_CASE(8) GX_PROBE_CASE(9) GX_PROBE_CASE(10) GX_PROBE_CASE(11) GX_PROBE_CASE(12)
-                GX_PROBE_CASE(13) GX_PROBE_CASE(14) GX_PROBE_CASE(15) GX_PROBE_CASE(16)
+                GX_PROBE_CASE(13) GX_PROBE_CASE(14) GX_PROBE_CASE(15) GX_PROBE_CASE(16) GX_PROBE_CASE(17) GX_PROBE_CASE(18)
 #undef GX_PROBE_CASE
                 default: hipLaunchKernelGGL((k_pr_pull_units<false>), dim3(nw), dim3(kBS), lds, s, a);
                 }
