@@ -345,6 +345,19 @@ int gx_lcc_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, d
  * gx_*_multi call on a list creates it otherwise.  The clique lives until gx_free of any of
  * its contexts.  Same argument rules as gx_lcc_multi. */
 int gx_multi_prepare(gx_ctx *const *ctxs, int ndev);
+/* gx_bfs_multi / gx_wcc_multi / gx_cdlp_multi: BFS levels (int64, INT64_MAX = unreached), WCC
+ * labels (the smallest vertex id of each component) and CDLP labels (vertex ids) of the host
+ * CSR A on the ndev devices of `ctxs`, in one process (bin/exe/{bfs,wcc,cdlp} with GX_NGPUS=N).
+ * The graph is replicated (gx_graph_create on every device); device d owns a contiguous vertex
+ * range of ~nnz / ndev entries and runs the gx_*_part_* steps below on it; per round only what
+ * the step changed crosses the clique (gx_part_changes words, counts read by the host), or the
+ * dense form when smaller (BFS: bitmaps OR-ed; CDLP: the owned label slices).  Results equal
+ * gx_bfs / gx_wcc / gx_cdlp bit for bit.  Replace LA_BFS (bfs.cpp:70-83), WeaklyConnectedComponents
+ * (wcc.cpp:39-66) and LA_CDLP (cdlp.cpp:54-81) when they run on several GPUs.  Same context
+ * rules (distinct devices or virtual devices) as gx_lcc_multi. */
+int gx_bfs_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, uint64_t src, int64_t *level);
+int gx_wcc_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, uint64_t *comp);
+int gx_cdlp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, int iters, uint64_t *labels);
 
 /* ---------------------------------------------------------------------------------
  * Multi-GPU steps for the other algorithms.  The graph is replicated on

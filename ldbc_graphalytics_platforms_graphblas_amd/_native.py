@@ -92,6 +92,11 @@ SIGNATURES = [
     ("gx_pagerank_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(gx_csr), C.c_int, C.c_double, C.c_int, _DP]),
     ("gx_sssp_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(gx_csr), C.c_int, C.c_uint64, _DP]),
     ("gx_lcc_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(gx_csr), C.c_int, _DP]),
+    ("gx_bfs_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(gx_csr), C.c_int, C.c_uint64,
+                               C.POINTER(C.c_int64)]),
+    ("gx_wcc_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(gx_csr), C.c_int, C.POINTER(C.c_uint64)]),
+    ("gx_cdlp_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(gx_csr), C.c_int, C.c_int,
+                                C.POINTER(C.c_uint64)]),
     ("gx_multi_prepare", C.c_int, [C.POINTER(_P), C.c_int]),
     ("gx_pagerank_csr", C.c_int, [_P, C.POINTER(gx_csr), C.c_int, C.c_double, C.c_int, _DP, C.POINTER(_P)]),
     ("gx_pr_partition", C.c_int, [C.c_uint64, _U64P, C.c_int, C.POINTER(C.c_uint32), _U64P, _U64P]),

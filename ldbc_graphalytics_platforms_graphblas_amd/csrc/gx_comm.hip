@@ -1263,6 +1263,359 @@ extern "C" int gx_lcc_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int 
     return GX_SUCCESS;
 }
 
+// ---- BFS / WCC / CDLP on several devices in one process (round 6) ----
+// bin/exe/{bfs,wcc,cdlp} with GX_NGPUS: the graph replicated on every device, device d owning
+// the vertex range [ranges[d], ranges[d+1]) (~nnz / ndev stored entries each), the rounds of
+// distributed.py (the torch.distributed driver) restated over the in-process clique: every
+// device runs its step on its own range, then only what the step changed travels as
+// (v << 32 | value) words (gx_part_changes: the counts all-gathered and read by the host, the
+// first max-count words of every device all-gathered, gx_part_apply on every device), or the
+// dense form when the words would outweigh it.  Every device starts a round with the same
+// state, so every device takes the same decisions; results are device 0's copy.
+namespace {
+
+std::vector<uint64_t> entry_ranges(const gx_csr *A, int ndev) {
+    const uint64_t n = A->n, nnz = A->nnz;
+    std::vector<uint64_t> ranges(ndev + 1, 0);
+    for (int k = 1; k < ndev; k++) {   // pr_partition.partition_rows: ~nnz / ndev entries each
+        const uint64_t target = nnz / ndev * k + nnz % ndev * k / ndev;
+        const uint64_t r = (uint64_t)(std::lower_bound(A->rowptr, A->rowptr + n + 1, target) - A->rowptr);
+        ranges[k] = std::min(std::max(r, ranges[k - 1]), n);
+    }
+    ranges[ndev] = n;
+    return ranges;
+}
+
+// Per-device buffers of the word exchange; `cap` words per device (any step changes at most n
+// entries), the gathered words grown on demand.
+struct WordExchange {
+    struct Dev {
+        DBuf<uint64_t> words, gathered;
+        DBuf<int64_t> count, counts;
+        uint64_t gcap = 0;
+    };
+    std::vector<Dev> D;
+    int64_t *hc = nullptr;   // pinned: the all-gathered counts (device 0's copy)
+    int ndev = 0;
+    gx_ctx *const *ctxs = nullptr;
+    uint64_t rounds = 0, word_rounds = 0, word_bytes = 0, dense_bytes = 0;
+
+    ~WordExchange() {
+        for (int d = 0; d < ndev; d++) {
+            (void)hipSetDevice(ctxs[d]->device);
+            (void)hipStreamSynchronize(ctxs[d]->stream);
+            D[d].words.release();
+            D[d].gathered.release();
+            D[d].count.release();
+            D[d].counts.release();
+        }
+        if (hc) (void)hipHostFree(hc);
+    }
+    int init(gx_ctx *const *c, int nd, uint64_t cap) {
+        ctxs = c;
+        ndev = nd;
+        D = std::vector<Dev>(nd);
+        for (int d = 0; d < nd; d++) {
+            GX_HIP_TRY(hipSetDevice(c[d]->device));
+            GX_TRY(D[d].words.alloc(std::max<uint64_t>(cap, 1)));
+            GX_TRY(D[d].count.alloc(1));
+            GX_TRY(D[d].counts.alloc(nd));
+        }
+        GX_HIP_TRY(hipSetDevice(c[0]->device));
+        GX_HIP_TRY(hipHostMalloc((void **)&hc, (size_t)nd * sizeof(int64_t), hipHostMallocDefault));
+        return GX_SUCCESS;
+    }
+    // arr(d)'s entries in span(d) that differ from old(d) (null: from 0) -> every device's dst(d)
+    // with op; dense() instead when 8 max-count ndev bytes exceed dense_bytes (GX_EXCHANGE =
+    // sparse / dense forces one).  *total = changes over all devices (0: none anywhere).
+    template <class Arr, class Old, class Span, class Dst, class Dense>
+    int run(Clique &C, Arr arr, Old old, Span span, int elem, int op, uint64_t dense_bytes, Dense dense, Dst dst,
+            uint64_t *total) {
+        rounds++;
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            const auto sp = span(d);
+            GX_TRY(gx_part_changes(arr(d), old(d), sp.first, sp.second, elem, D[d].words.p, D[d].count.p,
+                                   ctxs[d]->stream));
+        }
+        GX_TRY(C.all_gather([&](int d) { return (const void *)D[d].count.p; },
+                            [&](int d) { return (void *)D[d].counts.p; }, sizeof(int64_t)));
+        GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+        GX_HIP_TRY(hipMemcpyAsync(hc, D[0].counts.p, (size_t)ndev * sizeof(int64_t), hipMemcpyDeviceToHost,
+                                  ctxs[0]->stream));
+        GX_HIP_TRY(hipStreamSynchronize(ctxs[0]->stream));
+        uint64_t m = 0, tot = 0;
+        for (int d = 0; d < ndev; d++) {
+            m = std::max<uint64_t>(m, (uint64_t)hc[d]);
+            tot += (uint64_t)hc[d];
+        }
+        *total = tot;
+        if (m == 0) return GX_SUCCESS;
+        const char *ex = std::getenv("GX_EXCHANGE");
+        const bool force_dense = ex && std::strcmp(ex, "dense") == 0, force_sparse = ex && std::strcmp(ex, "sparse") == 0;
+        if (force_dense || (!force_sparse && 8 * m * (uint64_t)ndev > dense_bytes)) {
+            dense_bytes_add(dense_bytes);
+            return dense();
+        }
+        word_rounds++;
+        word_bytes += 8 * m * (uint64_t)ndev;
+        for (int d = 0; d < ndev; d++) {
+            if (D[d].gcap < m * (uint64_t)ndev) {
+                GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+                GX_HIP_TRY(hipStreamSynchronize(ctxs[d]->stream));   // the old buffer may still be read
+                D[d].gathered.release();
+                D[d].gcap = std::max<uint64_t>(m * (uint64_t)ndev, 2 * D[d].gcap);
+                GX_TRY(D[d].gathered.alloc(D[d].gcap));
+            }
+        }
+        GX_TRY(C.all_gather([&](int d) { return (const void *)D[d].words.p; },
+                            [&](int d) { return (void *)D[d].gathered.p; }, m * sizeof(uint64_t)));
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_TRY(gx_part_apply(D[d].gathered.p, D[d].counts.p, ndev, m, dst(d), elem, op, ctxs[d]->stream));
+        }
+        return GX_SUCCESS;
+    }
+    void dense_bytes_add(uint64_t b) { dense_bytes += b; }
+    void report(const char *who) const {
+        if (std::getenv("GX_PLAN_TIMES"))
+            std::fprintf(stderr, "[%s] %llu rounds, %llu as words (%.1f MB), dense %.1f MB per device\n", who,
+                         (unsigned long long)rounds, (unsigned long long)word_rounds, word_bytes / 1e6 / ndev,
+                         dense_bytes / 1e6);
+    }
+};
+
+// A replicated per-device array of n elements (device buffers, freed on their devices).
+template <class T>
+struct PerDev {
+    std::vector<DBuf<T>> b;
+    gx_ctx *const *ctxs = nullptr;
+    int ndev = 0;
+    ~PerDev() {
+        for (int d = 0; d < ndev; d++) {
+            (void)hipSetDevice(ctxs[d]->device);
+            (void)hipStreamSynchronize(ctxs[d]->stream);
+            b[d].release();
+        }
+    }
+    int alloc(gx_ctx *const *c, int nd, uint64_t n) {
+        ctxs = c;
+        ndev = nd;
+        b = std::vector<DBuf<T>>(nd);
+        for (int d = 0; d < nd; d++) {
+            GX_HIP_TRY(hipSetDevice(c[d]->device));
+            GX_TRY(b[d].alloc(std::max<uint64_t>(n, 1)));
+        }
+        return GX_SUCCESS;
+    }
+    T *operator[](int d) { return b[d].p; }
+};
+
+int upload_replicas(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, MultiGraphs &G) {
+    G.g.assign(ndev, nullptr);
+    return per_device(ctxs, ndev, [&](int d) -> int { return gx_graph_create(ctxs[d], A, directed, &G.g[d]); });
+}
+
+}  // namespace
+
+extern "C" int gx_bfs_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, uint64_t src,
+                            int64_t *level) {
+    GX_TRY(check_multi(ctxs, ndev, A, "gx_bfs_multi"));
+    if (!level) return fail(GX_NULL_POINTER, "gx_bfs_multi: null argument");
+    const uint64_t n = A->n;
+    if (src >= n) return fail(GX_INVALID_INDEX, "gx_bfs_multi: source out of range");
+    const std::vector<uint64_t> ranges = entry_ranges(A, ndev);
+    MultiGraphs G;
+    GX_TRY(upload_replicas(ctxs, ndev, A, directed, G));
+    std::shared_ptr<Clique> clique;
+    GX_TRY(get_clique(ctxs, ndev, &clique));
+    Clique &C = *clique;
+    const uint64_t nw = (n + 31) / 32;
+    PerDev<int64_t> lv, cnt;
+    PerDev<uint8_t> nxt;
+    PerDev<uint32_t> bits, gbits;
+    GX_TRY(lv.alloc(ctxs, ndev, n));
+    GX_TRY(cnt.alloc(ctxs, ndev, 1));
+    GX_TRY(nxt.alloc(ctxs, ndev, (n + 15) / 16 * 16));   // 16-B multiple (gx_part_pack_bits)
+    GX_TRY(bits.alloc(ctxs, ndev, nw));
+    GX_TRY(gbits.alloc(ctxs, ndev, nw * (uint64_t)ndev));
+    WordExchange X;
+    GX_TRY(X.init(ctxs, ndev, n));
+    for (int d = 0; d < ndev; d++) {
+        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+        GX_TRY(gx_bfs_part_init(G.g[d], src, lv[d], ctxs[d]->stream));
+    }
+    // dense form: every device's bitmap all-gathered and OR-ed (ndev n / 8 bytes < 2 n below 16)
+    const uint64_t dense_bytes = (uint64_t)ndev * nw * 4;
+    auto dense = [&]() -> int {
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_TRY(gx_part_pack_bits(nxt[d], n, bits[d], ctxs[d]->stream));
+        }
+        GX_TRY(C.all_gather([&](int d) { return (const void *)bits[d]; }, [&](int d) { return (void *)gbits[d]; },
+                            nw * sizeof(uint32_t)));
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_TRY(gx_part_or_bits(gbits[d], ndev, n, nxt[d], ctxs[d]->stream));
+        }
+        return GX_SUCCESS;
+    };
+    int64_t hcount = 0;
+    for (int64_t cur = 0;; cur++) {
+        if ((uint64_t)cur > n + 1) return fail(GX_DEVICE_ERROR, "gx_bfs_multi: no fixed point");
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_HIP_TRY(hipMemsetAsync(nxt[d], 0, n, ctxs[d]->stream));
+            GX_TRY(gx_bfs_part_expand(G.g[d], ranges[d], ranges[d + 1], lv[d], cur, nxt[d], ctxs[d]->stream));
+        }
+        uint64_t tot = 0;
+        GX_TRY(X.run(C, [&](int d) { return (const void *)nxt[d]; }, [&](int) { return (const void *)nullptr; },
+                     [&](int) { return std::make_pair((uint64_t)0, n); }, 1, 0, dense_bytes, dense,
+                     [&](int d) { return (void *)nxt[d]; }, &tot));
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_TRY(gx_bfs_part_commit(G.g[d], nxt[d], lv[d], cur, reinterpret_cast<uint64_t *>(cnt[d]),
+                                      ctxs[d]->stream));
+        }
+        GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+        GX_HIP_TRY(hipMemcpyAsync(&hcount, cnt[0], sizeof(int64_t), hipMemcpyDeviceToHost, ctxs[0]->stream));
+        GX_HIP_TRY(hipStreamSynchronize(ctxs[0]->stream));
+        if (hcount == 0) break;   // identical on every device (same inputs)
+    }
+    X.report("bfs_multi");
+    GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+    return download(ctxs[0], level, lv[0], n, Xfer::Raw64);
+}
+
+extern "C" int gx_wcc_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, uint64_t *comp) {
+    GX_TRY(check_multi(ctxs, ndev, A, "gx_wcc_multi"));
+    if (!comp) return fail(GX_NULL_POINTER, "gx_wcc_multi: null argument");
+    const uint64_t n = A->n;
+    if (n == 0) return GX_SUCCESS;
+    const std::vector<uint64_t> ranges = entry_ranges(A, ndev);
+    MultiGraphs G;
+    GX_TRY(upload_replicas(ctxs, ndev, A, directed, G));
+    std::shared_ptr<Clique> clique;
+    GX_TRY(get_clique(ctxs, ndev, &clique));
+    Clique &C = *clique;
+    PerDev<int32_t> par, prev;
+    PerDev<int> chg;
+    GX_TRY(par.alloc(ctxs, ndev, n));
+    GX_TRY(prev.alloc(ctxs, ndev, n));
+    GX_TRY(chg.alloc(ctxs, ndev, 1));
+    WordExchange X;
+    GX_TRY(X.init(ctxs, ndev, n));
+    for (int d = 0; d < ndev; d++) {
+        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+        GX_TRY(gx_wcc_part_init(G.g[d], par[d], ctxs[d]->stream));
+    }
+    // the changed parents always travel as words (applied with MIN): the dense form of the
+    // torch driver is an all-reduce MIN, which the words bound from above anyway
+    auto no_dense = [&]() -> int { return fail(GX_PANIC, "gx_wcc_multi: dense exchange"); };
+    for (uint64_t round = 0;; round++) {
+        if (round > n + 1) return fail(GX_DEVICE_ERROR, "gx_wcc_multi: no fixed point");
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_HIP_TRY(hipMemcpyAsync(prev[d], par[d], n * 4, hipMemcpyDeviceToDevice, ctxs[d]->stream));
+            GX_HIP_TRY(hipMemsetAsync(chg[d], 0, sizeof(int), ctxs[d]->stream));
+            GX_TRY(gx_wcc_part_hook(G.g[d], ranges[d], ranges[d + 1], par[d], chg[d], ctxs[d]->stream));
+        }
+        uint64_t tot = 0;
+        GX_TRY(X.run(C, [&](int d) { return (const void *)par[d]; }, [&](int d) { return (const void *)prev[d]; },
+                     [&](int) { return std::make_pair((uint64_t)0, n); }, 4, 1, ~0ull, no_dense,
+                     [&](int d) { return (void *)par[d]; }, &tot));
+        if (tot == 0) break;   // a round in which no device changed anything: the fixed point
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_TRY(gx_wcc_part_compress(G.g[d], par[d], ctxs[d]->stream));
+        }
+    }
+    X.report("wcc_multi");
+    GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+    return download(ctxs[0], comp, par[0], n, Xfer::Widen32);
+}
+
+extern "C" int gx_cdlp_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int directed, int iters,
+                             uint64_t *labels) {
+    GX_TRY(check_multi(ctxs, ndev, A, "gx_cdlp_multi"));
+    if (!labels) return fail(GX_NULL_POINTER, "gx_cdlp_multi: null argument");
+    if (iters < 0) return fail(GX_INVALID_VALUE, "gx_cdlp_multi: negative iteration count");
+    const uint64_t n = A->n;
+    if (n == 0) return GX_SUCCESS;
+    const std::vector<uint64_t> ranges = entry_ranges(A, ndev);
+    uint64_t chunk = 1;
+    for (int d = 0; d < ndev; d++) chunk = std::max(chunk, ranges[d + 1] - ranges[d]);
+    MultiGraphs G;
+    GX_TRY(upload_replicas(ctxs, ndev, A, directed, G));
+    std::shared_ptr<Clique> clique;
+    GX_TRY(get_clique(ctxs, ndev, &clique));
+    Clique &C = *clique;
+    PerDev<int32_t> lab, nxt, send, gath;
+    PerDev<int> chg;
+    GX_TRY(lab.alloc(ctxs, ndev, n));
+    GX_TRY(nxt.alloc(ctxs, ndev, n));
+    GX_TRY(send.alloc(ctxs, ndev, chunk));
+    GX_TRY(gath.alloc(ctxs, ndev, chunk * (uint64_t)ndev));
+    GX_TRY(chg.alloc(ctxs, ndev, 1));
+    std::vector<gx_cdlp_part *> part(ndev, nullptr);
+    struct Parts {
+        gx_ctx *const *ctxs;
+        std::vector<gx_cdlp_part *> &p;
+        ~Parts() {
+            for (size_t d = 0; d < p.size(); d++) {
+                (void)hipSetDevice(ctxs[d]->device);
+                (void)gx_cdlp_part_free(p[d]);
+            }
+        }
+    } parts_cleanup{ctxs, part};
+    WordExchange X;
+    GX_TRY(X.init(ctxs, ndev, n));
+    for (int d = 0; d < ndev; d++) {
+        GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+        GX_TRY(gx_cdlp_part_create(G.g[d], ranges[d], ranges[d + 1], &part[d]));
+        GX_TRY(gx_cdlp_part_init(part[d], lab[d], ctxs[d]->stream));
+    }
+    // dense form: the owned slices all-gathered (padded to the largest range) into every labels
+    auto dense = [&]() -> int {
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            const uint64_t own = ranges[d + 1] - ranges[d];
+            if (own)
+                GX_HIP_TRY(hipMemcpyAsync(send[d], nxt[d] + ranges[d], own * 4, hipMemcpyDeviceToDevice,
+                                          ctxs[d]->stream));
+        }
+        GX_TRY(C.all_gather([&](int d) { return (const void *)send[d]; }, [&](int d) { return (void *)gath[d]; },
+                            chunk * 4));
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            for (int e = 0; e < ndev; e++) {
+                const uint64_t own = ranges[e + 1] - ranges[e];
+                if (own)
+                    GX_HIP_TRY(hipMemcpyAsync(lab[d] + ranges[e], gath[d] + (uint64_t)e * chunk, own * 4,
+                                              hipMemcpyDeviceToDevice, ctxs[d]->stream));
+            }
+        }
+        return GX_SUCCESS;
+    };
+    for (int it = 0; it < iters; it++) {
+        for (int d = 0; d < ndev; d++) {
+            GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_HIP_TRY(hipMemsetAsync(chg[d], 0, sizeof(int), ctxs[d]->stream));
+            GX_TRY(gx_cdlp_part_step(part[d], lab[d], nxt[d], chg[d], ctxs[d]->stream));
+        }
+        uint64_t tot = 0;
+        // the owned labels that changed, set into every device's labels; the owned slices
+        // all-gathered when that is smaller
+        GX_TRY(X.run(C, [&](int d) { return (const void *)nxt[d]; }, [&](int d) { return (const void *)lab[d]; },
+                     [&](int d) { return std::make_pair(ranges[d], ranges[d + 1]); }, 4, 0, 4 * n, dense,
+                     [&](int d) { return (void *)lab[d]; }, &tot));
+        if (tot == 0) break;   // fixed point (LAGraph_cdlp.c:328-332)
+    }
+    X.report("cdlp_multi");
+    GX_HIP_TRY(hipSetDevice(ctxs[0]->device));
+    return download(ctxs[0], labels, lab[0], n, Xfer::Widen32);
+}
+
 extern "C" int gx_pr_dist_free(gx_pr_dist *h) {
     if (!h) return GX_SUCCESS;
     (void)hipSetDevice(h->d.ctx->device);

@@ -120,21 +120,19 @@ int Main(int argc, char **argv, Algorithm alg) {
         if (p.thread_num > 0) omp_set_num_threads((int)p.thread_num);
         int device = 0;
         if (const char *d = std::getenv("GX_DEVICE")) device = std::atoi(d);
-        // GX_NGPUS = N: PageRank, SSSP (BASELINE config 4) and LCC (config 5) on devices
-        // [GX_DEVICE, GX_DEVICE + N) in this one process (gx_pagerank_multi / gx_sssp_multi /
-        // gx_lcc_multi: 1-D partitions, in-process RCCL collectives); execute-job.sh cannot pass
-        // new flags (execute-job.sh:68-151), so the backend comes from the environment
-        // (SURVEY.md 8b).  GX_MULTI_SIM=1 puts the N contexts on device GX_DEVICE alone
-        // (virtual devices, collectives as device copies): the N > 1 path on a one-GPU box.
-        // The other algorithms run on one GPU.
+        // GX_NGPUS = N: every algorithm on devices [GX_DEVICE, GX_DEVICE + N) in this one process
+        // (gx_pagerank_multi / gx_sssp_multi / gx_lcc_multi: PageRank, SSSP (BASELINE config 4)
+        // and LCC (config 5) on 1-D partitions; gx_bfs_multi / gx_wcc_multi / gx_cdlp_multi on a
+        // replicated graph with vertex ranges and change-sized exchanges; in-process RCCL
+        // collectives); execute-job.sh cannot pass new flags (execute-job.sh:68-151), so the
+        // backend comes from the environment.  GX_MULTI_SIM=1 puts the N contexts
+        // on device GX_DEVICE alone (virtual devices, collectives as device copies): the N > 1
+        // path on a one-GPU box.
         int ngpus = 0;
         if (const char *g = std::getenv("GX_NGPUS")) ngpus = std::max(1, std::atoi(g));
         const char *sim_env = std::getenv("GX_MULTI_SIM");
         const bool sim = sim_env && std::atoi(sim_env) != 0;
-        const bool multi_alg = alg == Algorithm::PR || alg == Algorithm::SSSP || alg == Algorithm::LCC;
-        if (ngpus && !multi_alg)
-            std::cerr << "GX_NGPUS: only PageRank, SSSP and LCC run on several GPUs; this algorithm runs on device "
-                      << device << std::endl;
+        const bool multi_alg = true;
 
         CsrHolder A;
         ReadMatrix(p, &A.csr);
@@ -185,7 +183,10 @@ int Main(int argc, char **argv, Algorithm alg) {
         switch (alg) {
             case Algorithm::BFS:
                 level.reset(new int64_t[n]);
-                OK(gx_bfs(H.g, src, level.get()), "gx_bfs");
+                if (multi)
+                    OK(gx_bfs_multi(ctxs.data(), ngpus, &A.csr, p.directed ? 1 : 0, src, level.get()), "gx_bfs_multi");
+                else
+                    OK(gx_bfs(H.g, src, level.get()), "gx_bfs");
                 break;
             case Algorithm::PR:
                 vals.reset(new double[n]);
@@ -210,11 +211,18 @@ int Main(int argc, char **argv, Algorithm alg) {
                 break;
             case Algorithm::WCC:
                 labels.reset(new uint64_t[n]);
-                OK(gx_wcc(H.g, labels.get()), "gx_wcc");
+                if (multi)
+                    OK(gx_wcc_multi(ctxs.data(), ngpus, &A.csr, p.directed ? 1 : 0, labels.get()), "gx_wcc_multi");
+                else
+                    OK(gx_wcc(H.g, labels.get()), "gx_wcc");
                 break;
             case Algorithm::CDLP:
                 labels.reset(new uint64_t[n]);
-                OK(gx_cdlp(H.g, p.max_iteration, labels.get()), "gx_cdlp");
+                if (multi)
+                    OK(gx_cdlp_multi(ctxs.data(), ngpus, &A.csr, p.directed ? 1 : 0, p.max_iteration, labels.get()),
+                       "gx_cdlp_multi");
+                else
+                    OK(gx_cdlp(H.g, p.max_iteration, labels.get()), "gx_cdlp");
                 break;
             case Algorithm::LCC:
                 vals.reset(new double[n]);

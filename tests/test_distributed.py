@@ -652,6 +652,46 @@ def test_multi_virtual_devices_pieces(k, pieces, layout, monkeypatch):
             c.close()
 
 
+def _multi_out(fn, ctxs, csr, dtype, *args):
+    """gx_<alg>_multi with an integer result array of csr.n elements."""
+    import ctypes as C
+    from ldbc_graphalytics_platforms_graphblas_amd import _native as N
+    out = np.zeros(csr.n, dtype=dtype)
+    arr = (C.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+    s = csr.as_c()
+    ptr = out.ctypes.data_as(C.POINTER(C.c_int64 if dtype == np.int64 else C.c_uint64))
+    N.check(getattr(N.lib(), fn)(arr, len(ctxs), C.byref(s), *args, ptr), fn)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2, 3])
+@pytest.mark.parametrize("exchange", ["auto", "sparse", "dense"])
+def test_multi_virtual_devices_bfs_wcc_cdlp(k, exchange, monkeypatch):
+    """bin/exe/{bfs,wcc,cdlp}'s GX_NGPUS path (round 6): gx_bfs_multi /
+    gx_wcc_multi / gx_cdlp_multi on k virtual devices, the graph replicated, vertex ranges by
+    entries, per round the changed entries as words (or the dense form: BFS bitmaps, CDLP owned
+    slices), directed and undirected, against the oracle bit for bit."""
+    from ldbc_graphalytics_platforms_graphblas_amd.algorithms import Context
+    monkeypatch.setenv("GX_EXCHANGE", exchange)
+    ctxs = [Context(0) for _ in range(k)]
+    try:
+        for undirected in (True, False):
+            for scale, ef in ((10, 8), (13, 16)):
+                csr = rmat(scale, ef, 21 + scale, undirected=undirected)
+                deg = np.diff(csr.rowptr.astype(np.int64))
+                for src in (int(np.argmax(deg)), int(np.flatnonzero(deg == 0)[0]) if (deg == 0).any() else 1):
+                    got = _multi_out("gx_bfs_multi", ctxs, csr, np.int64, int(not undirected), src)
+                    assert np.array_equal(got, O.bfs(csr, src)), (k, scale, src)
+                got = _multi_out("gx_wcc_multi", ctxs, csr, np.uint64, int(not undirected))
+                assert np.array_equal(got.astype(np.int64), O.wcc(csr).astype(np.int64)), (k, scale)
+                got = _multi_out("gx_cdlp_multi", ctxs, csr, np.uint64, int(not undirected), 10)
+                assert np.array_equal(got.astype(np.int64), O.cdlp(csr, not undirected, 10).astype(np.int64)), (k, scale)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 @pytest.mark.gpu
 def test_multi_virtual_devices_edge_cases():
     """More virtual devices than rows with out-edges (some own nothing live), an edgeless graph,

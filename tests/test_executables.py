@@ -189,13 +189,17 @@ def test_sssp_executable_gx_ngpus(graph, tmp_path_factory, fixture_graphs):
 @pytest.mark.parametrize("alg,graph", [("pr", "example-directed"), ("pr", "test-pr-undirected"),
                                        ("sssp", "example-undirected"), ("sssp", "test-sssp-directed"),
                                        ("lcc", "example-directed"), ("lcc", "test-lcc-undirected"),
-                                       ("lcc", "example-undirected")])
+                                       ("lcc", "example-undirected"), ("bfs", "example-directed"),
+                                       ("bfs", "test-bfs-undirected"), ("wcc", "example-undirected"),
+                                       ("wcc", "test-wcc-directed"), ("cdlp", "example-directed"),
+                                       ("cdlp", "test-cdlp-undirected")])
 @pytest.mark.parametrize("ngpus", [1, 2, 3])
 def test_executable_gx_ngpus_virtual(alg, graph, ngpus, tmp_path_factory, fixture_graphs):
-    """bin/exe/{pr,sssp,lcc} with GX_NGPUS=N: N = 1 is a size-1 in-process RCCL clique, N > 1
-    runs N virtual devices on this box's one GPU (GX_MULTI_SIM=1), the same partition and
-    kernels an N-GPU node runs, with the collectives as device copies.  Against the oracle (PR
-    rtol 1e-12, SSSP and LCC bit-exact) and the Graphalytics rule of the validation file."""
+    """bin/exe/* with GX_NGPUS=N: N = 1 is a size-1 in-process RCCL clique (PageRank: the
+    single-GPU call), N > 1 runs N virtual devices on this box's one GPU (GX_MULTI_SIM=1), the
+    same partition and kernels an N-GPU node runs, with the collectives as device copies.
+    Against the oracle (PR rtol 1e-12, the others bit-exact) and the Graphalytics rule of the
+    validation file."""
     import os
     from oracle import oracle as O
     d, g = load_dir(tmp_path_factory, graph, fixture_graphs)
@@ -207,6 +211,16 @@ def test_executable_gx_ngpus_virtual(alg, graph, ngpus, tmp_path_factory, fixtur
     assert len(re.findall(r"Processing (starts|ends) at: \d+", res.stdout)) == 2
     ids, vals = parse_output(out, alg)
     np.testing.assert_array_equal(ids, g.mapping)
+    if alg in ("bfs", "wcc", "cdlp"):
+        expected = read_validation(FIXTURES / f"{graph}-{alg.upper()}")
+        if alg == "bfs":
+            check_against_validation("BFS", g.mapping, [int(v) for v in vals], expected)
+        else:
+            index = {int(m): i for i, m in enumerate(g.mapping)}
+            labels = np.array([index[int(v)] for v in vals], dtype=np.uint64)
+            check_against_validation(alg.upper(), g.mapping, labels, expected)
+        assert [int(v) for v in vals] == [int(expected[int(m)]) for m in g.mapping]   # bit-exact
+        return
     got = np.array([np.inf if v == "infinity" else float(v) for v in vals])
     if alg == "pr":
         want = O.pagerank(g.csr, g.directed, float(g.param("pr", "damping-factor")),
