@@ -1327,7 +1327,7 @@ struct WordExchange {
     }
     // arr(d)'s entries in span(d) that differ from old(d) (null: from 0) -> every device's dst(d)
     // with op; dense() instead when 8 max-count ndev bytes exceed dense_bytes (GX_EXCHANGE =
-    // sparse / dense forces one).  *total = changes over all devices (0: none anywhere).
+    // sparse / dense forces one; dense_bytes ~0: no dense form).  *total = changes over all devices (0: none anywhere).
     template <class Arr, class Old, class Span, class Dst, class Dense>
     int run(Clique &C, Arr arr, Old old, Span span, int elem, int op, uint64_t dense_bytes, Dense dense, Dst dst,
             uint64_t *total) {
@@ -1353,7 +1353,8 @@ struct WordExchange {
         if (m == 0) return GX_SUCCESS;
         const char *ex = std::getenv("GX_EXCHANGE");
         const bool force_dense = ex && std::strcmp(ex, "dense") == 0, force_sparse = ex && std::strcmp(ex, "sparse") == 0;
-        if (force_dense || (!force_sparse && 8 * m * (uint64_t)ndev > dense_bytes)) {
+        // (dense_bytes ~0: the caller has no dense form, words always)
+        if (dense_bytes != ~0ull && (force_dense || (!force_sparse && 8 * m * (uint64_t)ndev > dense_bytes))) {
             dense_bytes_add(dense_bytes);
             return dense();
         }
@@ -1474,6 +1475,7 @@ extern "C" int gx_bfs_multi(gx_ctx *const *ctxs, int ndev, const gx_csr *A, int 
                      [&](int d) { return (void *)nxt[d]; }, &tot));
         for (int d = 0; d < ndev; d++) {
             GX_HIP_TRY(hipSetDevice(ctxs[d]->device));
+            GX_HIP_TRY(hipMemsetAsync(cnt[d], 0, sizeof(int64_t), ctxs[d]->stream));   // commit adds to it
             GX_TRY(gx_bfs_part_commit(G.g[d], nxt[d], lv[d], cur, reinterpret_cast<uint64_t *>(cnt[d]),
                                       ctxs[d]->stream));
         }
