@@ -80,8 +80,6 @@ struct SsspState {
     int32_t bits_dirty;           // the settled bitmap holds a past pull's bits
     int32_t clear_bits;           // this step's advance clears the bitmap (all workgroups)
     uint32_t ring_cnt[kRing];
-    uint32_t ticket;              // k_sssp_relax's arrivals (the last one runs the next step's plan)
-    int32_t fold_plan;            // the plan runs at the end of k_sssp_relax, not as its own launch
 };
 
 struct SsspBufs {
@@ -279,7 +277,7 @@ __device__ __forceinline__ void stage_final(Stage *stages, uint32_t &n, const Ss
 //   light phase drained      -> heavy phase: relax the heavy edges of the bucket's vertices
 //   heavy phase drained      -> open the next non-empty ring bucket, else split the overflow,
 //                               else done
-__device__ void sssp_plan(SsspState *st) {
+__global__ void k_sssp_plan(SsspState *st) {
     if (st->done) {
         st->mode = 0;
         return;
@@ -355,26 +353,6 @@ __device__ void sssp_plan(SsspState *st) {
         return;
     }
     st->done = 1;
-}
-
-__global__ void k_sssp_plan(SsspState *st) { sssp_plan(st); }
-
-// The workgroup that arrives last at the end of a launch (every workgroup must call it, with
-// every thread): each thread's memory operations are released at agent scope before the
-// arrival, and the last arriver acquires, so it sees every other workgroup's atomics on the
-// state.  It also resets the ticket for the next launch.
-__device__ __forceinline__ bool last_arrival(uint32_t *ticket) {
-    __shared__ int last;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t all = gridDim.x * gridDim.y * gridDim.z;
-        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == all - 1;
-        if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    return last;
 }
 
 // Mode 1: turn the opened ring bucket into near items (and settled-list entries);
@@ -674,7 +652,7 @@ __device__ __forceinline__ void sssp_pull(const SsspBufs &B, Stage *stages, unsi
 // walks the concatenated edge range 64 x kSlots edges at a time, every lane finding the item
 // that owns its edge by a 6-step binary search over the scanned counts.  All lanes stay busy
 // whatever the degrees, and each lane keeps kSlots independent gather chains in flight.
-__device__ __forceinline__ void sssp_relax_body(const SsspBufs &B) {
+__global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
     constexpr int kSlots = 4;
     const SsspState *st = B.st;
     const int32_t r = st->round;
@@ -874,15 +852,6 @@ __device__ __forceinline__ void sssp_relax_body(const SsspBufs &B) {
     }
 }
 
-// The relaxation step, then (fold_plan, round 6) the next step's plan by the last workgroup to
-// finish: one launch per step fewer (the one-thread k_sssp_plan cost ~4.6 us x 54.5 steps per
-// SYN-8_5 run, r04_pmc_algorithms.json).  Every early exit of the body is workgroup-uniform,
-// so every workgroup arrives.
-__global__ __launch_bounds__(kSsspBlock) void k_sssp_relax(SsspBufs B) {
-    sssp_relax_body(B);
-    if (B.st->fold_plan && last_arrival(&B.st->ticket) && threadIdx.x == 0) sssp_plan(B.st);
-}
-
 __global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxed, unsigned long long *nsw,
                             int32_t *bstamp, int32_t *ostamp, int64_t n) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
@@ -895,8 +864,7 @@ __global__ void k_sssp_init(unsigned long long *dist, unsigned long long *relaxe
     }
 }
 
-__global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t fuse, int32_t fuse_max,
-                            int32_t fold_plan) {
+__global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t fuse, int32_t fuse_max) {
     SsspState *st = B.st;
     const uint32_t nch = chunks_of(B.lend[src] - B.rp[src]);
     for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x) B.q[0][j] = ((uint64_t)(uint32_t)src << 32) | j;
@@ -925,8 +893,6 @@ __global__ void k_sssp_seed(SsspBufs B, int32_t src, uint32_t pull_min, uint32_t
         st->consume_n = 0;
         st->fuse = fuse;
         st->fuse_max = fuse_max;
-        st->ticket = 0;
-        st->fold_plan = fold_plan;
         st->split_src = 0;
         st->qcnt[0] = nch;
         st->qcnt[1] = 0;
@@ -1053,7 +1019,7 @@ int ensure_sssp_layout(gx_graph *g, double delta, hipStream_t s) {
 }
 
 // Work buffers of gx_sssp, kept with the graph's light/heavy layout so repeated runs reuse
-// them, and the captured graph of kGraphSteps advance -> relax(+plan) steps (its kernel
+// them, and the captured graph of kGraphSteps plan -> advance -> relax steps (its kernel
 // arguments point into these buffers).  A run replays the graph, copying the done flag to
 // pinned memory after each replay while the next one is already queued.
 constexpr int kGraphSteps = 8;
@@ -1072,7 +1038,6 @@ struct SsspWork {
     hipGraphExec_t gexec = nullptr;
     hipStream_t g_stream = nullptr;
     unsigned g_grid = 0;
-    bool g_fold = false;
     ~SsspWork() {
         if (gexec) (void)hipGraphExecDestroy(gexec);
         if (graph) (void)hipGraphDestroy(graph);
@@ -1098,23 +1063,22 @@ struct SsspWork {
         GX_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         return GX_SUCCESS;
     }
-    // a step: advance -> relax, the relax's last workgroup planning the next step (the run's
-    // first plan is launched after the seed)
     int enqueue_steps(const SsspBufs &B, unsigned grid, int k, hipStream_t s) {
         for (int i = 0; i < k; i++) {
+            hipLaunchKernelGGL(k_sssp_plan, dim3(1), dim3(1), 0, s, B.st);
             hipLaunchKernelGGL(k_sssp_advance, dim3(grid), dim3(kSsspBlock), 0, s, B);
             hipLaunchKernelGGL(k_sssp_relax, dim3(grid), dim3(kSsspBlock), 0, s, B);
         }
         return check_launch("k_sssp_relax");
     }
-    int capture(const SsspBufs &B, unsigned grid, hipStream_t s, bool fold) {
-        if (gexec && g_stream == s && g_grid == grid && g_fold == fold) return GX_SUCCESS;
+    int capture(const SsspBufs &B, unsigned grid, hipStream_t s) {
+        if (gexec && g_stream == s && g_grid == grid) return GX_SUCCESS;
         if (gexec) (void)hipGraphExecDestroy(gexec);
         if (graph) (void)hipGraphDestroy(graph);
         gexec = nullptr;
         graph = nullptr;
         GX_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        const int rc = fold ? enqueue_steps(B, grid, kGraphSteps, s) : enqueue_unfolded(B, grid, kGraphSteps, s);
+        const int rc = enqueue_steps(B, grid, kGraphSteps, s);
         hipGraph_t gr = nullptr;
         const hipError_t e = hipStreamEndCapture(s, &gr);
         if (rc != GX_SUCCESS) {
@@ -1126,17 +1090,7 @@ struct SsspWork {
         GX_HIP_TRY(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
         g_stream = s;
         g_grid = grid;
-        g_fold = fold;
         return GX_SUCCESS;
-    }
-    // plan -> advance -> relax (GX_SSSP_FOLD=0)
-    int enqueue_unfolded(const SsspBufs &B, unsigned grid, int k, hipStream_t s) {
-        for (int i = 0; i < k; i++) {
-            hipLaunchKernelGGL(k_sssp_plan, dim3(1), dim3(1), 0, s, B.st);
-            hipLaunchKernelGGL(k_sssp_advance, dim3(grid), dim3(kSsspBlock), 0, s, B);
-            hipLaunchKernelGGL(k_sssp_relax, dim3(grid), dim3(kSsspBlock), 0, s, B);
-        }
-        return check_launch("k_sssp_relax");
     }
 };
 
@@ -1250,24 +1204,16 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
     int32_t fuse_max = kRing;
     if (const char *e = std::getenv("GX_SSSP_FUSE")) fuse = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char *e = std::getenv("GX_SSSP_FUSE_MAX")) fuse_max = std::max(1, std::min(kRing, std::atoi(e)));
-    // GX_SSSP_VERBOSE=2: one step per batch, a line per step (bucket, phase, items, work, time)
-    const bool per_step = verbose && std::atoi(std::getenv("GX_SSSP_VERBOSE")) >= 2;
-    // the plan folded into the relax kernel (GX_SSSP_FOLD=0: its own one-thread launch per step;
-    // the per-step trace keeps it separate to read the state between plan and advance)
-    const char *fe = std::getenv("GX_SSSP_FOLD");
-    const bool fold = !per_step && !(fe && std::atoi(fe) == 0);
-    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min, fuse, fuse_max, (int32_t)fold);
+    hipLaunchKernelGGL(k_sssp_seed, dim3(1), dim3(256), 0, s, B, (int32_t)src, pull_min, fuse, fuse_max);
     GX_TRY(check_launch("k_sssp_seed"));
-    if (fold) {
-        hipLaunchKernelGGL(k_sssp_plan, dim3(1), dim3(1), 0, s, st.p);   // the first step's plan
-        GX_TRY(check_launch("k_sssp_plan"));
-    }
     const unsigned grid = (unsigned)std::max(1, ctx->num_cus) * 8;
     // a bound every correct run stays far below: each step settles a vertex or a bucket
     const uint64_t max_steps = 8ull * (uint64_t)n + 4ull * (uint64_t)g->nnz + 1000000ull;
     uint64_t steps = 0;
     int batch = 4;
     int32_t done = 0;
+    // GX_SSSP_VERBOSE=2: one step per batch, a line per step (bucket, phase, items, work, time)
+    const bool per_step = verbose && std::atoi(std::getenv("GX_SSSP_VERBOSE")) >= 2;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     unsigned long long prev[8] = {};
     if (per_step) {
@@ -1282,7 +1228,7 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
         // The first batch is as many replays as the last run on this layout needed; when that
         // was enough, the remap to the caller's order (hub-first copy) is queued behind it
         // instead of an idle replay, and runs while the host reads the flag.
-        GX_TRY(W.capture(B, grid, s, fold));
+        GX_TRY(W.capture(B, grid, s));
         // capped, so that one long run (a deep chain) cannot queue many idle replays for the next
         const int hint = std::min(W.replays_hint, 12);
         auto read_state = [&]() -> int {
@@ -1338,7 +1284,7 @@ extern "C" int gx_sssp(gx_graph *g, uint64_t src, double *dist_out) {
             continue;
         }
         for (int i = 0; i < batch; i++) {
-            if (!fold) hipLaunchKernelGGL(k_sssp_plan, dim3(1), dim3(1), 0, s, st.p);
+            hipLaunchKernelGGL(k_sssp_plan, dim3(1), dim3(1), 0, s, st.p);
             {
                 KTimer kt(ctx, "sssp_advance", s);
                 hipLaunchKernelGGL(k_sssp_advance, dim3(grid), dim3(kSsspBlock), 0, s, B);
