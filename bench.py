@@ -60,6 +60,10 @@ def parse():
                     help="pr = the headline (SYN-8_5, BASELINE configs[3]'s graph); the others measure configs 3-5 "
                          "on 1 GPU")
     ap.add_argument("--graph", default=None, choices=sorted(PRESETS), help="synthetic stand-in (SURVEY.md 8d)")
+    ap.add_argument("--pmc-traffic", choices=["run", "committed"], default="run",
+                    help="PR roofline.traffic: measured in this run by two rocprofv3 --pmc child passes "
+                         "(FETCH_SIZE, WRITE_SIZE) of a one-step bench, or read from profiles/pmc_pr_pull.json")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--partitioned", action="store_true",
                     help="run --algorithm through the multi-GPU (vertex-range) path even at N=1")
     return ap.parse_args()
@@ -359,6 +363,53 @@ def pmc_alg_kernels(alg: str, workload: str):
     if not a:
         return None
     return {"source": name, **{k: round(v.get("us_per_run", 0.0), 2) for k, v in a.get("per_run_kernels", {}).items()}}
+
+
+def measure_pr_traffic(gname: str, timeout_s: int = 180):
+    """HBM bytes per k_pr_pull_units launch measured now: two child runs of a
+    one-step bench on the same graph under rocprofv3, one counter set each (MI355X_MICROARCH.md:
+    separate --pmc passes, FETCH_SIZE doubled on gfx950, WRITE_SIZE as is; KB per dispatch, the
+    mean over the pass's dispatches).  A child is a new process started by this one (never an
+    exec), in its own session, killed with its group at the time limit.  Returns (bytes or
+    None, note)."""
+    import csv
+    import glob
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, "rocprofv3 not found"
+    kb = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="gx_pmc_", dir="/tmp")
+        cmd = [exe, "--pmc", ctr, "--kernel-include-regex", "k_pr_pull_units", "--output-format", "csv", "-d", d,
+               "-o", "pmc", "--", sys.executable, str(ROOT / "bench.py"), "--graph", gname, "--steps", "1",
+               "--warmup", "0", "--no-cpu-baseline", "--no-secondary", "--pmc-child"]
+        env = dict(os.environ, TMPDIR="/tmp")
+        try:
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env, cwd=str(ROOT),
+                                 start_new_session=True)
+            try:
+                rc = p.wait(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return None, f"the {ctr} pass exceeded {timeout_s} s"
+            if rc != 0:
+                return None, f"the {ctr} pass failed (exit {rc})"
+            v = [float(r["Counter_Value"]) for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+                 for r in csv.DictReader(open(f)) if r.get("Counter_Name") == ctr]
+            if not v:
+                return None, f"the {ctr} pass recorded no dispatch"
+            kb[ctr] = (sum(v) / len(v), len(v))
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    fetch, write = kb["FETCH_SIZE"][0], kb["WRITE_SIZE"][0]
+    return (2 * fetch + write) * 1024, (f"measured in this run: rocprofv3 --pmc FETCH_SIZE ({kb['FETCH_SIZE'][1]} "
+                                        f"dispatches, x2 for gfx950) and WRITE_SIZE ({kb['WRITE_SIZE'][1]}) child passes "
+                                        f"of a one-step bench on {gname}")
 
 
 def pmc_traffic(workload: str):
@@ -735,15 +786,24 @@ def main():
     edges_total = nnz * args.iters * args.steps
     value = edges_total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
-    traffic = pmc_traffic(workload) if world == 1 else None
-    copy_gbs = stream_copy_gbs(device) if rank == 0 else None
+    traffic, traffic_src = None, None
+    if world == 1 and not args.pmc_child:
+        if args.pmc_traffic == "run":
+            traffic, traffic_src = measure_pr_traffic(gname)
+            if traffic is None:   # e.g. no profiler access: the committed pass, labelled as such
+                why = traffic_src
+                traffic = pmc_traffic(workload)
+                traffic_src = f"profiles/pmc_pr_pull.json (committed; the in-run passes: {why})"
+        else:
+            traffic, traffic_src = pmc_traffic(workload), "profiles/pmc_pr_pull.json (committed)"
+    copy_gbs = stream_copy_gbs(device) if rank == 0 and not args.pmc_child else None
 
     exe = None
     secondary = None
     cpu = None
     parity = None
     ref = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.pmc_child:
         exe, exe_r = exe_path_pr(csr, args, ctx)
         if not args.no_cpu_baseline:
             from oracle import oracle as O
@@ -780,7 +840,7 @@ def main():
                          # bin/exe/pr's processing time on this graph too
                          "processing": exe_path_pr(csr2, args, ctx)[0]}
 
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and not args.pmc_child:
         # the last timed step's scores (gathered from every rank at N > 1) against the fp64 oracle
         from oracle import oracle as O
         if ref is None:
@@ -827,6 +887,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "traffic_over_algorithmic": traffic / m["bytes_per_launch"] if traffic else None,
                 "bytes_per_launch": m["bytes_per_launch"],
                 "mean_launch_us": m["mean_launch_s"] * 1e6,
                 "launches": m["launches"],
