@@ -462,21 +462,29 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
 
 // Huge vertices (deg > kMidMax): the label multiset is cut into kHugeChunk-label chunks; a
 // 1024-thread workgroup histograms one chunk in a 64 KiB LDS table, then adds each distinct
-// label once into the vertex's global table (device-scope CAS + atomicAdd), so global
-// atomics scale with distinct labels per chunk, not with the degree.
+// label once into the vertex's global table, so global atomics scale with distinct labels per
+// chunk, not with the degree.  A global slot is one 64-bit word, (epoch << 58) | (count << 31) |
+// label, claimed and counted by one CAS: a slot whose epoch is not this iteration's is empty, so
+// the tables are never cleared (but once every kHugeEpochs iterations) and never scanned.  Every
+// successful CAS knows the label's count so far; a label's last update carries its final count,
+// so the maximum of (count << 32) | ~label over the updates is the vertex's winner.  Each
+// workgroup folds its updates into one 64-bit atomicMax on the vertex's key.
 constexpr int kHugeBlock = 1024;
 constexpr int kHugeChunk = 4096;
 constexpr int kHugeSlots = 2 * kHugeChunk;
+constexpr int kHugeEpochs = 63;                   // epochs 1..63 in the top 6 bits; 0: never used
+constexpr int64_t kHugeMaxDeg = (1ll << 27) - 1;  // the count field (bits 31..57)
 
 __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, const int32_t *__restrict__ hv,
                                                                  const int64_t *__restrict__ hoff,
                                                                  const int32_t *__restrict__ hlog2,
                                                                  const int32_t *__restrict__ cvert,
                                                                  const int64_t *__restrict__ cbeg,
-                                                                 uint32_t *gkeys, uint32_t *gcnts,
+                                                                 unsigned long long *gtab, uint32_t epoch,
                                                                  unsigned long long *vkey) {
     __shared__ uint32_t K[kHugeSlots];
     __shared__ uint32_t C[kHugeSlots];
+    __shared__ unsigned long long red[kHugeBlock / kWave];
     constexpr int kLog2 = 13;   // log2(kHugeSlots)
     const int tid = threadIdx.x;
     const int32_t hi = cvert[blockIdx.x];
@@ -515,57 +523,37 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
     __syncthreads();
     const int log2ts = hlog2[hi];
     const int64_t ts = 1ll << log2ts;
-    uint32_t *GK = gkeys + hoff[hi];
-    uint32_t *GC = gcnts + hoff[hi];
+    unsigned long long *GT = gtab + hoff[hi];
+    const unsigned long long ep = (unsigned long long)epoch << 58;
+    unsigned long long key = 0;
     for (int s = tid; s < kHugeSlots; s += kHugeBlock) {
         const uint32_t c = C[s];
         if (!c) continue;
         const uint32_t l = K[s];
         int64_t h = hash_slot(l, log2ts);
+        unsigned long long old = GT[h];   // a stale copy only costs a failed CAS
         for (;;) {
-            const uint32_t prev = atomicCAS(&GK[h], kEmpty, l);
-            if (prev == kEmpty || prev == l) {
-                atomicAdd(&GC[h], c);
+            const bool live = (old & (63ull << 58)) == ep;
+            if (live && (uint32_t)(old & 0x7fffffffu) != l) {   // another label's slot: probe on
+                h = (h + 1) & (ts - 1);
+                old = GT[h];
+                continue;
+            }
+            const unsigned long long nw = live ? old + ((unsigned long long)c << 31)
+                                               : ep | ((unsigned long long)c << 31) | (unsigned long long)l;
+            const unsigned long long prev = atomicCAS(&GT[h], old, nw);
+            if (prev == old) {
+                const unsigned long long kk = pack((uint32_t)((nw >> 31) & kHugeMaxDeg), l);
+                key = kk > key ? kk : key;
                 break;
             }
-            h = (h + 1) & (ts - 1);
-        }
-    }
-}
-
-// Reduce of the huge vertices' global tables, one workgroup per kHugeSeg-slot segment: the
-// segment's best (count << 32 | ~label) goes to the vertex's key by a 64-bit atomicMax, and
-// every slot read is reset, so the tables are clean for the next iteration without a memset.
-constexpr int64_t kHugeSeg = 16384;
-
-__global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_reduce(CdlpArgs a, const int32_t *__restrict__ hv,
-                                                                 const int32_t *__restrict__ sv,
-                                                                 const int64_t *__restrict__ sbeg,
-                                                                 const int64_t *__restrict__ hoff,
-                                                                 const int32_t *__restrict__ hlog2, uint32_t *gkeys,
-                                                                 uint32_t *gcnts, unsigned long long *vkey) {
-    __shared__ unsigned long long red[kHugeBlock / kWave];
-    const int32_t hi = sv[blockIdx.x];
-    // first iteration: the key is final already; inactive vertex: its tables were not touched
-    if (a.first || !active(a, all_active(a), hv[hi])) return;
-    const int64_t ts = 1ll << hlog2[hi];
-    const int64_t s0 = sbeg[blockIdx.x], s1 = min(s0 + kHugeSeg, ts);
-    uint32_t *GK = gkeys + hoff[hi];
-    uint32_t *GC = gcnts + hoff[hi];
-    unsigned long long key = 0;
-    for (int64_t s = s0 + threadIdx.x; s < s1; s += kHugeBlock) {
-        const uint32_t c = GC[s];
-        if (c) {
-            const unsigned long long kk = pack(c, GK[s]);
-            key = kk > key ? kk : key;
-            GC[s] = 0;
-            GK[s] = kEmpty;
+            old = prev;
         }
     }
     key = wave_max_u64(key);
-    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = key;
+    if ((tid & (kWave - 1)) == 0) red[tid / kWave] = key;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         unsigned long long m = red[0];
         for (int w = 1; w < kHugeBlock / kWave; w++) m = red[w] > m ? red[w] : m;
         if (m) atomicMax(&vkey[hi], m);
@@ -1371,11 +1359,9 @@ struct CdlpPlan {
     DBuf<int32_t> d_wall;               // every vertex of degree <= kSparseWaveMax (sparse fallback)
     size_t n_wall = 0;
     DBuf<int64_t> d_hoff, d_cbeg;
-    DBuf<uint32_t> gk, gc;
+    DBuf<unsigned long long> gtab;      // huge vertices' global tables (k_cdlp_huge_insert's words)
+    uint32_t epoch = 0;                 // the last iteration's table epoch (1..kHugeEpochs)
     DBuf<unsigned long long> vkey;      // per huge vertex best key (zero between iterations)
-    DBuf<int32_t> d_segv;               // huge-table segments: vertex index, first slot
-    DBuf<int64_t> d_segb;
-    size_t n_seg = 0;
 };
 
 // Switches read at every call (tests flip them within one process); unset means `dflt`.
@@ -1407,6 +1393,7 @@ int cdlp_plan(const CdlpGraph &g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream
         } else if (d <= kMidMax) {
             mv.push_back((int32_t)v);
         } else {
+            if (d > kHugeMaxDeg) return fail(GX_INVALID_VALUE, "gx_cdlp: a vertex degree exceeds 2^27 - 1");
             int l2 = 1;
             while ((1ll << l2) < 2 * d) l2++;
             for (int64_t c = 0; c < d; c += kHugeChunk) {
@@ -1442,27 +1429,11 @@ int cdlp_plan(const CdlpGraph &g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream
         GX_TRY(P.d_hv.alloc(hv.size()));
         GX_TRY(P.d_hl.alloc(hl.size()));
         GX_TRY(P.d_hoff.alloc(hoff.size()));
-        GX_TRY(P.gk.alloc(total));
-        GX_TRY(P.gc.alloc(total));
+        GX_TRY(P.gtab.alloc(total));
         GX_TRY(P.vkey.alloc(hv.size()));
         GX_HIP_TRY(hipMemsetAsync(P.vkey.p, 0, hv.size() * 8, s));
-        // the tables start clean; k_cdlp_huge_reduce resets every slot it consumes
-        hipLaunchKernelGGL(k_cdlp_fill_u32, dim3(grid_for(total, 256, 8192)), dim3(256), 0, s, P.gk.p, kEmpty, total);
-        GX_TRY(check_launch("k_cdlp_fill_u32"));
-        GX_HIP_TRY(hipMemsetAsync(P.gc.p, 0, (size_t)total * 4, s));
-        std::vector<int32_t> segv;
-        std::vector<int64_t> segb;
-        for (size_t i = 0; i < hv.size(); i++)
-            for (int64_t b = 0; b < (1ll << hl[i]); b += kHugeSeg) {
-                segv.push_back((int32_t)i);
-                segb.push_back(b);
-            }
-        P.n_seg = segv.size();
-        GX_TRY(P.d_segv.alloc(segv.size()));
-        GX_TRY(P.d_segb.alloc(segb.size()));
-        GX_HIP_TRY(hipMemcpyAsync(P.d_segv.p, segv.data(), segv.size() * 4, hipMemcpyHostToDevice, s));
-        GX_HIP_TRY(hipMemcpyAsync(P.d_segb.p, segb.data(), segb.size() * 8, hipMemcpyHostToDevice, s));
-        GX_HIP_TRY(hipStreamSynchronize(s));
+        GX_HIP_TRY(hipMemsetAsync(P.gtab.p, 0, (size_t)total * 8, s));   // epoch 0: every slot empty
+        P.epoch = 0;
         GX_TRY(P.d_cvert.alloc(cvert.size()));
         GX_TRY(P.d_cbeg.alloc(cbeg.size()));
         GX_HIP_TRY(hipMemcpyAsync(P.d_hv.p, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, s));
@@ -1560,12 +1531,17 @@ int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t 
     }
     if (P.n_huge) {
         KTimer kt(ctx, "cdlp_heavy", s1);
+        uint32_t ep = P.epoch;
+        if (!a.first) {   // a new epoch empties every table slot; past the last one, a real clear
+            if (++ep > (uint32_t)kHugeEpochs) {
+                GX_HIP_TRY(hipMemsetAsync(P.gtab.p, 0, (size_t)P.total * 8, s1));
+                ep = 1;
+            }
+            P.epoch = ep;
+        }
         hipLaunchKernelGGL(k_cdlp_huge_insert, dim3((unsigned)P.n_chunks), dim3(kHugeBlock), 0, s1, a, P.d_hv.p,
-                           P.d_hoff.p, P.d_hl.p, P.d_cvert.p, P.d_cbeg.p, P.gk.p, P.gc.p, P.vkey.p);
+                           P.d_hoff.p, P.d_hl.p, P.d_cvert.p, P.d_cbeg.p, P.gtab.p, ep, P.vkey.p);
         GX_TRY(check_launch("k_cdlp_huge_insert"));
-        hipLaunchKernelGGL(k_cdlp_huge_reduce, dim3((unsigned)P.n_seg), dim3(kHugeBlock), 0, s1, a, P.d_hv.p,
-                           P.d_segv.p, P.d_segb.p, P.d_hoff.p, P.d_hl.p, P.gk.p, P.gc.p, P.vkey.p);
-        GX_TRY(check_launch("k_cdlp_huge_reduce"));
         hipLaunchKernelGGL(k_cdlp_huge_final, dim3(grid_for(P.n_huge, 64, 1024)), dim3(64), 0, s1, a, P.d_hv.p,
                            (int32_t)P.n_huge, P.vkey.p);
         GX_TRY(check_launch("k_cdlp_huge_final"));

@@ -472,6 +472,23 @@ def test_cdlp_row_order_and_sparse(ctx, monkeypatch, first_sorted, sparse, only)
         np.testing.assert_array_equal(gpu_run(ctx, _G(t, True), "CDLP", iters=iters), O.cdlp(t, True, iters))
 
 
+@pytest.mark.parametrize("directed", [False, True])
+def test_cdlp_huge_table_epochs(ctx, directed):
+    """The huge tier's global tables are emptied by a new epoch per iteration, and cleared for
+    real once the 63 epochs are used up: many calls on one graph (the tables live in its cache)
+    run through the wrap, every result equal to the oracle's."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    t = _tier_graph(directed)
+    G = A.Graph(ctx, t, directed)
+    try:
+        want = {k: O.cdlp(t, directed, k) for k in (2, 3, 4, 5)}
+        for call in range(40):
+            k = 2 + call % 4
+            np.testing.assert_array_equal(A.LA_CDLP(G, k), want[k])
+    finally:
+        G.close()
+
+
 @pytest.mark.parametrize("keep,only,asub", [("1", "1", None), ("1", "2", None), ("1", "0", None), ("0", "1", None),
                                             ("1", "1", "2"), ("1", "2", "2")])
 @pytest.mark.parametrize("relabel", ["1", "0"])
