@@ -884,20 +884,23 @@ __global__ __launch_bounds__(256) void k_cdlp_mark(const int64_t *__restrict__ r
 // tier's method: strict-majority vote, else a 2d-slot LDS hash table).  When *dense and the
 // iteration has no tier kernels (a sparse-only iteration, fl != null), every vertex of the
 // fallback list fl is recomputed instead.
-__global__ __launch_bounds__(256) void k_cdlp_sparse_wave(CdlpArgs a, const int32_t *__restrict__ wl, int64_t asub,
-                                                          const unsigned int *wcount, const int32_t *__restrict__ fl,
-                                                          int64_t fn) {
+// The role bodies take their block index and block count (bid, nblk) and their LDS (lds) as
+// arguments, so k_cdlp_sparse_fused can run several roles in one launch.
+constexpr int kSparseWaveSlots = 2 * kSparseWaveMax;
+constexpr size_t kSparseWaveLds = (size_t)2 * (256 / kWave) * kSparseWaveSlots * sizeof(uint32_t);
+
+__device__ __forceinline__ void sparse_wave_role(const CdlpArgs &a, const int32_t *__restrict__ wl, int64_t asub,
+                                                 const unsigned int *wcount, const int32_t *__restrict__ fl,
+                                                 int64_t fn, int64_t bid, int64_t nblk, uint32_t *lds) {
     const bool full = *a.dense != 0;
     if (full && !fl) return;
-    constexpr int kSlots = 2 * kSparseWaveMax;
+    constexpr int kSlots = kSparseWaveSlots;
     constexpr int R = kSparseWaveMax / kWave;
-    __shared__ uint32_t keys[256 / kWave][kSlots];
-    __shared__ uint32_t cnts[256 / kWave][kSlots];
     const int lane = threadIdx.x & (kWave - 1);
-    uint32_t *K = keys[threadIdx.x / kWave];
-    uint32_t *C = cnts[threadIdx.x / kWave];
-    const int64_t gw = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave;
-    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);   // a multiple of kCdlpSubs
+    uint32_t *K = lds + (threadIdx.x / kWave) * kSlots;
+    uint32_t *C = lds + (256 / kWave) * kSlots + (threadIdx.x / kWave) * kSlots;
+    const int64_t gw = (bid * 256 + threadIdx.x) / kWave;
+    const int64_t nw = nblk * (256 / kWave);   // a multiple of kCdlpSubs
     const int j = (int)(gw % kCdlpSubs);
     const int32_t *src = full ? fl : wl + (int64_t)j * asub;
     const int64_t c = full ? fn : (int64_t)shard_count(wcount, j, asub);
@@ -963,6 +966,7 @@ __global__ __launch_bounds__(256) void k_cdlp_sparse_wave(CdlpArgs a, const int3
     if (any) raise_flag_sharded(a.changed, a.cshards);
 }
 
+
 // Sparse iterations, active vertices of kSparseWaveMax < degree <= kMidMax: one workgroup each,
 // kMaxDeg / kBlock labels per thread in registers, the strict-majority vote, else a kSlots-slot
 // LDS table (the mid tier's method, without its pipelining).  Shapes: 256 threads / 4K slots
@@ -970,29 +974,34 @@ __global__ __launch_bounds__(256) void k_cdlp_sparse_wave(CdlpArgs a, const int3
 // 2d slots do not fit; none from SYN-7_5's fourth iteration on) is appended to `redo`, which
 // the 1024-thread / 16K-slot instance then recomputes (rin: that list, *rcount entries).
 // Fallback when *dense in a sparse-only iteration: every vertex of fl then fl2.
+template <int kBlock, int kSlots>
+constexpr size_t sparse_group_lds() {
+    return (size_t)2 * kSlots * sizeof(uint32_t) + (kBlock / kWave) * (sizeof(unsigned long long) + sizeof(uint32_t)) +
+           sizeof(uint32_t);
+}
+
 template <int kBlock, int kSlots, int kMaxDeg>
-__global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const int32_t *__restrict__ gl,
-                                                              int64_t asub, const unsigned int *gcount,
-                                                              const int32_t *__restrict__ fl, int64_t fn,
-                                                              const int32_t *__restrict__ fl2, int64_t fn2,
-                                                              int32_t *redo, unsigned int *rcount,
-                                                              const int32_t *__restrict__ rin) {
+__device__ __forceinline__ void sparse_group_role(const CdlpArgs &a, const int32_t *__restrict__ gl, int64_t asub,
+                                                  const unsigned int *gcount, const int32_t *__restrict__ fl,
+                                                  int64_t fn, const int32_t *__restrict__ fl2, int64_t fn2,
+                                                  int32_t *redo, unsigned int *rcount, const int32_t *__restrict__ rin,
+                                                  int64_t bid, int64_t nblk, uint32_t *lds) {
     const bool full = !rin && *a.dense != 0;
     if (full && !fl && !fl2) return;
-    __shared__ uint32_t K[kSlots];
-    __shared__ uint32_t C[kSlots];
-    __shared__ unsigned long long red[kBlock / kWave];
-    __shared__ uint32_t cnt[kBlock / kWave];
-    __shared__ uint32_t bcast[1];
+    uint32_t *K = lds;
+    uint32_t *C = lds + kSlots;
+    unsigned long long *red = reinterpret_cast<unsigned long long *>(lds + 2 * kSlots);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(red + kBlock / kWave);
+    uint32_t *bcast = cnt + kBlock / kWave;
     constexpr int R = kMaxDeg / kBlock;
     constexpr int NW = kBlock / kWave;
     const int tid = threadIdx.x;
-    const int j = (int)(blockIdx.x % kCdlpSubs);   // the grid is a multiple of kCdlpSubs
+    const int j = (int)(bid % kCdlpSubs);   // the block count is a multiple of kCdlpSubs
     const int32_t *src = rin ? rin : full ? fl : gl + (int64_t)j * asub;
     const int64_t c = rin ? (int64_t)*rcount : full ? fn + fn2 : (int64_t)shard_count(gcount, j, asub);
-    const int64_t step = rin || full ? gridDim.x : gridDim.x / kCdlpSubs;
+    const int64_t step = rin || full ? nblk : nblk / kCdlpSubs;
     bool any = false;
-    for (int64_t i = rin || full ? blockIdx.x : blockIdx.x / kCdlpSubs; i < c; i += step) {
+    for (int64_t i = rin || full ? bid : bid / kCdlpSubs; i < c; i += step) {
         const int64_t v = full && i >= fn ? fl2[i - fn] : src[i];   // full: fn == 0 when fl is null
         const VMeta m = vmeta(a, v);
         const int64_t d = (int64_t)m.od + m.id;
@@ -1067,6 +1076,55 @@ __global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const 
         __syncthreads();   // red / cnt / bcast / the table are free for the next vertex
     }
     if (any) raise_flag_sharded(a.changed, a.cshards);
+}
+
+template <int kBlock, int kSlots, int kMaxDeg>
+__global__ __launch_bounds__(kBlock) void k_cdlp_sparse_group(CdlpArgs a, const int32_t *__restrict__ gl,
+                                                              int64_t asub, const unsigned int *gcount,
+                                                              const int32_t *__restrict__ fl, int64_t fn,
+                                                              const int32_t *__restrict__ fl2, int64_t fn2,
+                                                              int32_t *redo, unsigned int *rcount,
+                                                              const int32_t *__restrict__ rin) {
+    __shared__ uint32_t lds[(sparse_group_lds<kBlock, kSlots>() + 3) / 4];
+    sparse_group_role<kBlock, kSlots, kMaxDeg>(a, gl, asub, gcount, fl, fn, fl2, fn2, redo, rcount, rin, blockIdx.x,
+                                               gridDim.x, lds);
+}
+
+// The three sparse roles of an iteration in one launch (GX_CDLP_SPARSE_FUSED, the default):
+// blocks [0, 8S) recompute the wave list, [8S, 12S) the 2048-degree list, [12S, 20S) the
+// 8192-degree list (S = kCdlpSubs), each as its own kernel would.  The roles are independent
+// (they read `cur` and write disjoint vertices), and in a sparse iteration each is a short
+// chain of dependent loads, so one launch overlaps them instead of running them in turn.
+// Block b of a launch plays block boff + b, so three launches of one role range each are the
+// unfused form (an inlined role in two kernels crashes this compiler's call-graph update).
+struct SparseFusedArgs {
+    const int32_t *al;
+    int64_t asub;
+    const unsigned int *cnt;   // the three lists' counters (kCdlpSubs * kCntStride apart)
+    const int32_t *fw, *fg2, *fg4, *fg;   // fallback lists (sparse-only iterations) or null
+    int64_t nfw, nfg2, nfg4, nfg;
+    int32_t *redo;
+    unsigned int *rcount;
+};
+
+__global__ __launch_bounds__(256) void k_cdlp_sparse_fused(CdlpArgs a, SparseFusedArgs f, int boff) {
+    constexpr size_t kLds = kSparseWaveLds > sparse_group_lds<kMid2Block, kMid2Slots>()
+                                ? kSparseWaveLds
+                                : sparse_group_lds<kMid2Block, kMid2Slots>();
+    __shared__ uint32_t lds[(kLds + 3) / 4];
+    const int64_t S = kCdlpSubs, shards = S * f.asub;
+    const int64_t b = (int64_t)blockIdx.x + boff;
+    if (b < 8 * S) {
+        sparse_wave_role(a, f.al, f.asub, f.cnt, f.fw, f.nfw, b, 8 * S, lds);
+    } else if (b < 12 * S) {
+        sparse_group_role<kMid2Block, kMid2Slots, kMid2Max>(a, f.al + shards, f.asub, f.cnt + S * kCntStride, f.fg2,
+                                                            f.nfg2, nullptr, 0, nullptr, nullptr, nullptr, b - 8 * S,
+                                                            4 * S, lds);
+    } else {
+        sparse_group_role<kMid2Block, kMid2Slots, kMidMax>(a, f.al + 2 * shards, f.asub, f.cnt + 2 * S * kCntStride,
+                                                           f.fg4, f.nfg4, f.fg, f.nfg, f.redo, f.rcount, nullptr,
+                                                           b - 12 * S, 8 * S, lds);
+    }
 }
 
 // ---- own-label check (dense active iterations) ----------------------------------------
@@ -1495,22 +1553,34 @@ int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t 
     if (sl) {
         // exit at once when *dense (the tier kernels below then recompute every vertex)
         KTimer kt(ctx, "cdlp_sparse", s);
-        const int64_t shards = (int64_t)kCdlpSubs * sl->asub;
         const unsigned int *cnt = sl->counts + kCdlpSubs * kCntStride;
         // a sparse-only iteration's fallback lists (nothing else recomputes these vertices)
         const bool o = sl->only;
-        hipLaunchKernelGGL(k_cdlp_sparse_wave, dim3(8 * kCdlpSubs), dim3(256), 0, s, a, sl->al, sl->asub, cnt,
-                           o ? P.d_wall.p : nullptr, (int64_t)P.n_wall);
-        GX_TRY(check_launch("k_cdlp_sparse_wave"));
-        hipLaunchKernelGGL((k_cdlp_sparse_group<kMid2Block, kMid2Slots, kMid2Max>), dim3(4 * kCdlpSubs),
-                           dim3(kMid2Block), 0, s, a, sl->al + shards, sl->asub, cnt + kCdlpSubs * kCntStride,
-                           o ? P.d_mv2.p : nullptr, (int64_t)P.n_mid2, nullptr, (int64_t)0, nullptr, nullptr, nullptr);
-        GX_TRY(check_launch("k_cdlp_sparse_group2"));
-        hipLaunchKernelGGL((k_cdlp_sparse_group<kMid2Block, kMid2Slots, kMidMax>), dim3(8 * kCdlpSubs),
-                           dim3(kMid2Block), 0, s, a, sl->al + 2 * shards, sl->asub, cnt + 2 * kCdlpSubs * kCntStride,
-                           o ? P.d_mv4.p : nullptr, (int64_t)P.n_mid4, o ? P.d_mv.p : nullptr, (int64_t)P.n_mid,
-                           sl->redo, sl->rcount, nullptr);
-        GX_TRY(check_launch("k_cdlp_sparse_group"));
+        // GX_CDLP_SPARSE_FUSED=0: the three roles as three launches
+        const SparseFusedArgs f{sl->al,
+                                sl->asub,
+                                cnt,
+                                o ? P.d_wall.p : nullptr,
+                                o ? P.d_mv2.p : nullptr,
+                                o ? P.d_mv4.p : nullptr,
+                                o ? P.d_mv.p : nullptr,
+                                (int64_t)P.n_wall,
+                                (int64_t)P.n_mid2,
+                                (int64_t)P.n_mid4,
+                                (int64_t)P.n_mid,
+                                sl->redo,
+                                sl->rcount};
+        if (env_on("GX_CDLP_SPARSE_FUSED")) {
+            hipLaunchKernelGGL(k_cdlp_sparse_fused, dim3(20 * kCdlpSubs), dim3(256), 0, s, a, f, 0);
+            GX_TRY(check_launch("k_cdlp_sparse_fused"));
+        } else {
+            const int ranges[4] = {0, 8 * kCdlpSubs, 12 * kCdlpSubs, 20 * kCdlpSubs};
+            for (int q = 0; q < 3; q++) {
+                hipLaunchKernelGGL(k_cdlp_sparse_fused, dim3(ranges[q + 1] - ranges[q]), dim3(256), 0, s, a, f,
+                                   ranges[q]);
+                GX_TRY(check_launch("k_cdlp_sparse_fused"));
+            }
+        }
         hipLaunchKernelGGL((k_cdlp_sparse_group<kMidBlock, kMidSlots, kMidMax>), dim3(kCdlpSubs), dim3(kMidBlock), 0,
                            s, a, nullptr, (int64_t)0, nullptr, nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr,
                            sl->rcount, sl->redo);
