@@ -1253,6 +1253,106 @@ __global__ __launch_bounds__(256) void k_cdlp_keep_count(const int32_t *__restri
     }
 }
 
+// Column-sorted form of the count (the default where built; GX_CDLP_KEEP_SORTED=0: the slabs
+// above).  The slab pass is bound by the texture units' line rate: rocprofv3 on SYN-7_5 shows
+// TA busy 92 % of the launch for ~59 M L2 requests, one per label gather (its 64 lanes read 64
+// different lines).  Here the entries of the rows the check reads are cut into blocks of at
+// most kKeepBlock entries and a row span of at most kKeepRows rows, and each block's entries
+// are sorted by column (built once per graph): a block's label gathers walk the label array in
+// order, so a wave's lanes share lines (hub columns repeat many times per block).  Each entry
+// keeps its column (4 B) and its row within the block (2 B); the rows' own labels and counts
+// live in LDS, and one global atomic per (block, row) adds the count.
+constexpr int64_t kKeepBlockMax = 1 << 20;   // GX_CDLP_KEEP_BLOCK (build time): 1024 .. 1 Mi
+constexpr int kKeepRows = 1024;
+
+// One wave per included row: the row's entries as (block << 32 | column) keys with the row's
+// place in its block as the value (kpos: where the row's keys start; a row of kKeepBlock or
+// more entries spans whole blocks of its own, from rblk).
+__global__ __launch_bounds__(256) void k_keep_sorted_keys(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                          const int32_t *__restrict__ rows, const int64_t *__restrict__ kpos,
+                                                          const int32_t *__restrict__ rblk,
+                                                          const int32_t *__restrict__ brow0, int64_t nrows,
+                                                          int64_t kKeepBlock, uint64_t *keys, uint16_t *vals) {
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave; i < nrows;
+         i += (int64_t)gridDim.x * (256 / kWave)) {
+        const int64_t r = rows[i], b0 = rp[r], d = rp[r + 1] - b0;
+        for (int64_t k = lane; k < d; k += kWave) {
+            const int64_t b = d >= kKeepBlock ? rblk[i] + k / kKeepBlock : rblk[i];
+            keys[kpos[i] + k] = ((uint64_t)b << 32) | (uint32_t)ci[b0 + k];
+            vals[kpos[i] + k] = (uint16_t)(r - brow0[b]);
+        }
+    }
+}
+
+__global__ void k_keep_sorted_cols(const uint64_t *__restrict__ keys, int64_t m, int32_t *cols) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        cols[i] = (int32_t)(uint32_t)keys[i];
+}
+
+__global__ __launch_bounds__(256) void k_cdlp_keep_sorted(const int64_t *__restrict__ bstart,
+                                                          const int32_t *__restrict__ brow0, int64_t nb,
+                                                          const int32_t *__restrict__ scol,
+                                                          const uint16_t *__restrict__ srow,
+                                                          const int32_t *__restrict__ lab, int64_t n, uint32_t *kcnt,
+                                                          const int *dense, int *keep, unsigned int *lcounts, int head) {
+    const bool run = *dense != 0;
+    if (head && blockIdx.x == 0) {
+        if (threadIdx.x == 0) *keep = run ? 1 : 0;
+        if (run)
+            for (int i = threadIdx.x; i < 3 * kCdlpSubs; i += 256) lcounts[(int64_t)i * kCntStride] = 0u;
+    }
+    if (!run) return;
+    __shared__ int32_t own[kKeepRows];
+    __shared__ uint32_t cnt[kKeepRows];
+    const int tid = threadIdx.x;
+    for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const int64_t r0 = brow0[b], e0 = bstart[b], e1 = bstart[b + 1];
+        const int span = (int)min((int64_t)kKeepRows, n - r0);
+        for (int i = tid; i < span; i += 256) {
+            own[i] = lab[r0 + i];
+            cnt[i] = 0u;
+        }
+        __syncthreads();
+        // rounds of U entries per thread, software-pipelined: a round's label gathers are issued,
+        // then the next round's columns and rows, then the compares wait for the gathers only
+        constexpr int U = 8;
+        int32_t c[U];
+        uint32_t lr[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t k = min(e0 + tid + (int64_t)u * 256, e1 - 1);
+            c[u] = scol[k];
+            lr[u] = srow[k];
+        }
+        for (int64_t e = e0 + tid; e < e1; e += 256 * U) {
+            int32_t x[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) x[u] = lab[c[u]];
+            int32_t cn[U];
+            uint32_t ln[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t k = min(e + (int64_t)(U + u) * 256, e1 - 1);
+                cn[u] = scol[k];
+                ln[u] = srow[k];
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (e + (int64_t)u * 256 < e1 && x[u] == own[lr[u]]) atomicAdd(&cnt[lr[u]], 1u);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                c[u] = cn[u];
+                lr[u] = ln[u];
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < span; i += 256)
+            if (cnt[i]) atomicAdd(&kcnt[r0 + i], cnt[i]);
+        __syncthreads();   // own / cnt are free for the next block
+    }
+}
+
 // Per vertex of degree > kTiny: keep (2 count > degree) or recompute: onto the activation list
 // of its degree (the sparse kernels' lists, shard = wave index mod kCdlpSubs), or, huge, the
 // iteration's stamp for the huge tier (a kept huge vertex loses a stamp k_cdlp_mark gave it).
@@ -1690,7 +1790,14 @@ struct CdlpCache {
     struct KeepCsr {
         DBuf<unsigned long long> bits;
         DBuf<int32_t> sne, ne;
+        // column-sorted blocks (k_cdlp_keep_sorted): block b's entries are scol / srow
+        // [bstart[b], bstart[b + 1]), its rows start at brow0[b]
+        DBuf<int64_t> bstart;
+        DBuf<int32_t> brow0, scol;
+        DBuf<uint16_t> srow;
+        int64_t nb = 0;
     } kA, kT;
+    bool keep_sorted = false;   // kA / kT hold column-sorted blocks
     DBuf<uint32_t> kcnt;
     DBuf<int> kflags;
     bool keep_built = false;
@@ -1792,8 +1899,95 @@ int keep_layout(const int64_t *rp, int64_t n, int64_t nnz, const int64_t *rpA, c
     return GX_SUCCESS;
 }
 
+// The column-sorted blocks of one CSR (host row pointers h_rp, device rp / ci): the rows of
+// total degree > kTiny in order, cut greedily into blocks of <= kKeepBlock entries whose rows
+// span <= kKeepRows positions (a row of kKeepBlock or more entries takes whole blocks of its own).
+int keep_sorted_build(const CdlpGraph &G, const int64_t *h_rp, const int64_t *rp, const int32_t *ci,
+                      CdlpCache::KeepCsr &K, hipStream_t s) {
+    const char *kb = std::getenv("GX_CDLP_KEEP_BLOCK");
+    const int64_t kKeepBlock = kb ? std::min<int64_t>(kKeepBlockMax, std::max<int64_t>(1024, std::atoll(kb))) : 65536;
+    std::vector<int32_t> rows, rblk, brow0;
+    std::vector<int64_t> kpos, bsize;
+    int64_t m = 0, cur_e = 0;
+    bool open = false;
+    for (int64_t v = 0; v < G.n; v++) {
+        const int64_t dt = (G.h_rpA[v + 1] - G.h_rpA[v]) + (G.directed ? G.h_rpT[v + 1] - G.h_rpT[v] : 0);
+        const int64_t d = h_rp[v + 1] - h_rp[v];
+        if (dt <= kTiny || d == 0) continue;
+        if (d >= kKeepBlock) {
+            rows.push_back((int32_t)v);
+            kpos.push_back(m);
+            rblk.push_back((int32_t)brow0.size());
+            for (int64_t k = 0; k < d; k += kKeepBlock) {
+                brow0.push_back((int32_t)v);
+                bsize.push_back(std::min(kKeepBlock, d - k));
+            }
+            m += d;
+            open = false;
+            continue;
+        }
+        if (!open || cur_e + d > kKeepBlock || v - brow0.back() >= kKeepRows) {
+            brow0.push_back((int32_t)v);
+            bsize.push_back(0);
+            cur_e = 0;
+            open = true;
+        }
+        rows.push_back((int32_t)v);
+        kpos.push_back(m);
+        rblk.push_back((int32_t)brow0.size() - 1);
+        bsize.back() += d;
+        cur_e += d;
+        m += d;
+    }
+    K.nb = (int64_t)brow0.size();
+    if (m == 0 || K.nb >= (1ll << 31)) {
+        K.nb = 0;
+        return GX_SUCCESS;
+    }
+    std::vector<int64_t> bstart(brow0.size() + 1, 0);
+    for (size_t b = 0; b < bsize.size(); b++) bstart[b + 1] = bstart[b] + bsize[b];
+
+    DBuf<int32_t> d_rows, d_rblk;
+    DBuf<int64_t> d_kpos;
+    DBuf<uint64_t> keys, keys2;
+    DBuf<uint16_t> vals;
+    GX_TRY(d_rows.alloc(rows.size()));
+    GX_TRY(d_rblk.alloc(rblk.size()));
+    GX_TRY(d_kpos.alloc(kpos.size()));
+    GX_TRY(K.brow0.alloc(brow0.size()));
+    GX_TRY(K.bstart.alloc(bstart.size()));
+    GX_HIP_TRY(hipMemcpyAsync(d_rows.p, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, s));
+    GX_HIP_TRY(hipMemcpyAsync(d_rblk.p, rblk.data(), rblk.size() * 4, hipMemcpyHostToDevice, s));
+    GX_HIP_TRY(hipMemcpyAsync(d_kpos.p, kpos.data(), kpos.size() * 8, hipMemcpyHostToDevice, s));
+    GX_HIP_TRY(hipMemcpyAsync(K.brow0.p, brow0.data(), brow0.size() * 4, hipMemcpyHostToDevice, s));
+    GX_HIP_TRY(hipMemcpyAsync(K.bstart.p, bstart.data(), bstart.size() * 8, hipMemcpyHostToDevice, s));
+    GX_TRY(keys.alloc((size_t)m));
+    GX_TRY(keys2.alloc((size_t)m));
+    GX_TRY(vals.alloc((size_t)m));
+    GX_TRY(K.srow.alloc((size_t)m));
+    hipLaunchKernelGGL(k_keep_sorted_keys, dim3(grid_for((uint64_t)rows.size() * kWave, 256, 16384)), dim3(256), 0, s,
+                       rp, ci, d_rows.p, d_kpos.p, d_rblk.p, K.brow0.p, (int64_t)rows.size(), kKeepBlock, keys.p,
+                       vals.p);
+    GX_TRY(check_launch("k_keep_sorted_keys"));
+    int end_bit = 32;
+    while ((1ll << (end_bit - 32)) < K.nb) end_bit++;
+    GX_TRY(sort_pairs_u64_u16(keys.p, keys2.p, vals.p, K.srow.p, (size_t)m, end_bit, s));
+    keys.release();
+    vals.release();
+    GX_TRY(K.scol.alloc((size_t)m));
+    hipLaunchKernelGGL(k_keep_sorted_cols, dim3(grid_for((uint64_t)m, 256, 8192)), dim3(256), 0, s, keys2.p, m, K.scol.p);
+    GX_TRY(check_launch("k_keep_sorted_cols"));
+    GX_HIP_TRY(hipStreamSynchronize(s));   // host vectors and the key buffers die at return
+    return GX_SUCCESS;
+}
+
 int keep_build(CdlpCache &C, hipStream_t s) {
     const CdlpGraph &G = C.G;
+    if (G.h_rpA && (!G.directed || G.h_rpT) && env_on("GX_CDLP_KEEP_SORTED")) {
+        GX_TRY(keep_sorted_build(G, G.h_rpA, G.rpA, G.ciA, C.kA, s));
+        if (G.directed) GX_TRY(keep_sorted_build(G, G.h_rpT, G.rpT, G.ciT, C.kT, s));
+        C.keep_sorted = true;
+    }
     GX_TRY(keep_layout(G.rpA, G.n, G.nnzA, G.rpA, G.rpT, C.kA, s));
     if (G.directed) GX_TRY(keep_layout(G.rpT, G.n, G.nnzT, G.rpA, G.rpT, C.kT, s));
     GX_TRY(C.kcnt.alloc((size_t)std::max<int64_t>(G.n, 1)));
@@ -1990,8 +2184,20 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                                        C->kcnt.p, C->dense.p, kf, cnt + kCdlpSubs * kCntStride, head);
                     return check_launch("k_cdlp_keep_count");
                 };
-                GX_TRY(count(G.ciA, C->keep_nnzA, C->kA, 1));
-                if (G.directed) GX_TRY(count(G.ciT, C->keep_nnzT, C->kT, 0));
+                auto sorted = [&](const CdlpCache::KeepCsr &K, int head) {
+                    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(K.nb, 65536));
+                    hipLaunchKernelGGL(k_cdlp_keep_sorted, dim3(grid), dim3(256), 0, s, K.bstart.p, K.brow0.p, K.nb,
+                                       K.scol.p, K.srow.p, cur, n, C->kcnt.p, C->dense.p, kf,
+                                       cnt + kCdlpSubs * kCntStride, head);
+                    return check_launch("k_cdlp_keep_sorted");
+                };
+                if (C->keep_sorted && env_on("GX_CDLP_KEEP_SORTED")) {
+                    GX_TRY(sorted(C->kA, 1));
+                    if (G.directed) GX_TRY(sorted(C->kT, 0));
+                } else {
+                    GX_TRY(count(G.ciA, C->keep_nnzA, C->kA, 1));
+                    if (G.directed) GX_TRY(count(G.ciT, C->keep_nnzT, C->kT, 0));
+                }
                 hipLaunchKernelGGL(k_cdlp_keep_apply, dim3(8 * kCdlpSubs), dim3(256), 0, s, G.rpA, G.rpT, (int64_t)0, n,
                                    C->kcnt.p, C->act.p, (int32_t)it, kf, cnt, C->al.p, C->asub, kf + 1);
                 GX_TRY(check_launch("k_cdlp_keep_apply"));

@@ -492,20 +492,23 @@ def test_cdlp_huge_table_epochs(ctx, directed):
 @pytest.mark.parametrize("keep,only,asub", [("1", "1", None), ("1", "2", None), ("1", "0", None), ("0", "1", None),
                                             ("1", "1", "2"), ("1", "2", "2")])
 @pytest.mark.parametrize("relabel", ["1", "0"])
-def test_cdlp_own_label_check(ctx, monkeypatch, keep, only, asub, relabel):
+@pytest.mark.parametrize("sorted_", ["1", "0"])
+def test_cdlp_own_label_check(ctx, monkeypatch, keep, only, asub, relabel, sorted_):
     """Dense active iterations take the own-label check (GX_CDLP_KEEP, the default): vertices
     whose label more than half of their neighbours hold keep it, the rest go to the sparse
     kernels' lists and k_cdlp_tiny; with tiny lists (GX_CDLP_ASUB=2) they overflow and the
     iteration stays dense (every tier kernel).  Sparse-only iterations (GX_CDLP_SPARSE_ONLY=2)
     run the check without tier kernels.  Same labels as the oracle, directed and undirected,
-    on the caller's order and the relabelled copy."""
+    on the caller's order and the relabelled copy; the count on column-sorted blocks
+    (GX_CDLP_KEEP_SORTED, the default) or on 64-entry slabs."""
     monkeypatch.setenv("GX_CDLP_KEEP", keep)
+    monkeypatch.setenv("GX_CDLP_KEEP_SORTED", sorted_)
     monkeypatch.setenv("GX_CDLP_SPARSE_ONLY", only)
     monkeypatch.setenv("GX_CDLP_RELABEL", relabel)
     if asub:
         monkeypatch.setenv("GX_CDLP_ASUB", asub)
-    for g in (_rmat(14, 16, 4), _rmat(12, 4, 8), _rmat(11, 8, 3, undirected=False), _G(_tier_graph(False), False),
-              _G(_tier_graph(True), True)):
+    for g in (_rmat(14, 16, 4), _rmat(12, 4, 8), _rmat(11, 8, 3, undirected=False), _rmat(13, 48, 5),
+              _rmat(12, 24, 6, undirected=False), _G(_tier_graph(False), False), _G(_tier_graph(True), True)):
         for iters in (3, 4, 7):
             np.testing.assert_array_equal(gpu_run(ctx, g, "CDLP", iters=iters), O.cdlp(g.csr, g.directed, iters))
 
