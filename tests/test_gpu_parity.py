@@ -500,7 +500,7 @@ def test_cdlp_own_label_check(ctx, monkeypatch, keep, only, asub, relabel, sorte
     iteration stays dense (every tier kernel).  Sparse-only iterations (GX_CDLP_SPARSE_ONLY=2)
     run the check without tier kernels.  Same labels as the oracle, directed and undirected,
     on the caller's order and the relabelled copy; the count on column-sorted blocks
-    (GX_CDLP_KEEP_SORTED, the default) or on 64-entry slabs."""
+    (GX_CDLP_KEEP_SORTED, the default on the relabelled copy) or on 64-entry slabs."""
     monkeypatch.setenv("GX_CDLP_KEEP", keep)
     monkeypatch.setenv("GX_CDLP_KEEP_SORTED", sorted_)
     monkeypatch.setenv("GX_CDLP_SPARSE_ONLY", only)
