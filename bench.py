@@ -80,9 +80,12 @@ DEFAULT_GRAPH = {"pr": "SYN-8_5", "cdlp": "SYN-7_5", "bfs": "SYN-g500-22", "wcc"
                  "sssp": "SYN-8_5", "lcc": "SYN-cit"}
 # the dominant kernel of each algorithm: the KTimer names summed (CDLP's light tier runs as
 # two launches, the 256-slot instance "cdlp_light_s" and the 1024-slot "cdlp_light")
-DOMINANT = {"bfs": ["bfs_topdown"], "wcc": ["wcc_hook"], "sssp": ["sssp_relax"],
+DOMINANT = {"bfs": ["bfs_expand"], "wcc": ["wcc_hook"], "sssp": ["sssp_relax"],
             "cdlp": ["cdlp_light", "cdlp_light_s"], "lcc": ["lcc_triangles"]}
-KERNELS = {"bfs": ["bfs_topdown", "bfs_bottomup"], "wcc": ["wcc_sample", "wcc_hook", "wcc_compress"],
+# BFS: a level's frontier phase (bitmap / queue rebuild) and expansion (bottom-up / top-down);
+# GX_BFS_FUSED=0 brackets them as "bfs_bottomup" (bitmap + bottom-up) and "bfs_topdown"
+KERNELS = {"bfs": ["bfs_frontier", "bfs_expand", "bfs_topdown", "bfs_bottomup"],
+           "wcc": ["wcc_sample", "wcc_hook", "wcc_compress"],
            "sssp": ["sssp_relax", "sssp_advance"],
            "cdlp": ["cdlp_tiny", "cdlp_small", "cdlp_light_s", "cdlp_light", "cdlp_mid2", "cdlp_mid4", "cdlp_mid",
                     "cdlp_heavy", "cdlp_first", "cdlp_mark", "cdlp_keep", "cdlp_sparse"],

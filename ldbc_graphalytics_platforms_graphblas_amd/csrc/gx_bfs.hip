@@ -55,10 +55,11 @@ __device__ __forceinline__ void bfs_topdown(const int64_t *__restrict__ rp,
                                                            uint32_t qsize, int32_t *level,
                                                            int32_t depth, uint64_t *qout,
                                                            uint32_t *qcount,
-                                                           unsigned long long *next_edges) {
+                                                           unsigned long long *next_edges, uint32_t bid,
+                                                           uint32_t nblk) {
     const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = (blockIdx.x * kBfsBlock + threadIdx.x) / kWave;
-    const uint32_t nwaves = gridDim.x * (kBfsBlock / kWave);
+    const uint32_t wave = (bid * kBfsBlock + threadIdx.x) / kWave;
+    const uint32_t nwaves = nblk * (kBfsBlock / kWave);
     unsigned long long edges = 0;
     for (uint32_t f = wave; f < qsize; f += nwaves) {
         const uint64_t item = qin[f];
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown(const int64_t *__rest
                                                            const uint64_t *__restrict__ qin, uint32_t qsize,
                                                            int32_t *level, int32_t depth, uint64_t *qout,
                                                            uint32_t *qcount, unsigned long long *next_edges) {
-    bfs_topdown(rp, ci, qin, qsize, level, depth, qout, qcount, next_edges);
+    bfs_topdown(rp, ci, qin, qsize, level, depth, qout, qcount, next_edges, blockIdx.x, gridDim.x);
 }
 
 // bottom-up: one thread per vertex; in-edges in (rpi, cii)
@@ -101,11 +102,11 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown(const int64_t *__rest
 // wave (ballot over 64 consecutive vertices); n/8 bytes, so it stays resident in every XCD's
 // L2 while the bottom-up probes hit it at random (the int32 level array does not).
 __device__ __forceinline__ void bfs_bitmap(const int32_t *__restrict__ level, int64_t n, int32_t depth,
-                                           uint64_t *fb) {
-    const int64_t stride = (int64_t)gridDim.x * kBfsBlock;
+                                           uint64_t *fb, uint32_t bid, uint32_t nblk) {
+    const int64_t stride = (int64_t)nblk * kBfsBlock;
     const int64_t nround = (n + stride - 1) / stride;
     for (int64_t r = 0; r < nround; r++) {
-        const int64_t v = r * stride + (int64_t)blockIdx.x * kBfsBlock + threadIdx.x;
+        const int64_t v = r * stride + (int64_t)bid * kBfsBlock + threadIdx.x;
         const uint64_t m = __ballot(v < n && level[v] == depth);
         if ((threadIdx.x & (kWave - 1)) == 0 && v < n) fb[v >> 6] = m;
     }
@@ -113,7 +114,7 @@ __device__ __forceinline__ void bfs_bitmap(const int32_t *__restrict__ level, in
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_bitmap(const int32_t *__restrict__ level, int64_t n,
                                                           int32_t depth, uint64_t *fb) {
-    bfs_bitmap(level, n, depth, fb);
+    bfs_bitmap(level, n, depth, fb, blockIdx.x, gridDim.x);
 }
 
 __device__ __forceinline__ uint32_t in_frontier(const uint64_t *__restrict__ fb, int32_t u) {
@@ -131,15 +132,15 @@ __device__ __forceinline__ void bfs_bottomup(const int64_t *__restrict__ rpi,
                                                             const uint64_t *__restrict__ fb, int64_t n,
                                                             int32_t *level, int32_t depth,
                                                             unsigned long long *counters /* found, edges */,
-                                                            uint64_t *fbn = nullptr) {
+                                                            uint64_t *fbn, uint32_t bid, uint32_t nblk) {
     __shared__ unsigned long long red[2][kBfsBlock / kWave];
     unsigned long long edges = 0, found = 0;
     // uniform trip count: a wave covers 64 aligned consecutive vertices per round, so with fbn
     // its ballot of the vertices found is the next level's frontier word (no bitmap pass)
-    const int64_t stride = (int64_t)gridDim.x * kBfsBlock;
+    const int64_t stride = (int64_t)nblk * kBfsBlock;
     const int64_t nround = (n + stride - 1) / stride;
     for (int64_t r = 0; r < nround; r++) {
-        const int64_t v = r * stride + (int64_t)blockIdx.x * kBfsBlock + threadIdx.x;
+        const int64_t v = r * stride + (int64_t)bid * kBfsBlock + threadIdx.x;
         bool take = false;
         if (v < n && level[v] < 0) {
             const int64_t b = rpi[v], e = rpi[v + 1];
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup(const int64_t *__res
                                                             const uint64_t *__restrict__ fb, int64_t n,
                                                             int32_t *level, int32_t depth,
                                                             unsigned long long *counters) {
-    bfs_bottomup(rpi, cii, rpo, fb, n, level, depth, counters);
+    bfs_bottomup(rpi, cii, rpo, fb, n, level, depth, counters, nullptr, blockIdx.x, gridDim.x);
 }
 
 // Top-down queue of the vertices at `depth` (after bottom-up steps), built per tile of
@@ -200,14 +201,14 @@ constexpr int64_t kQTile = 4096;
 // bitmap words (one line per wave) instead of the n int32 levels, twice.
 __device__ __forceinline__ void bfs_level_queue(const int64_t *__restrict__ rp, const int32_t *__restrict__ level,
                                                 int64_t n, int32_t depth, uint64_t *queue, uint32_t *qcount,
-                                                const uint64_t *__restrict__ fb = nullptr) {
+                                                const uint64_t *__restrict__ fb, uint32_t bid, uint32_t nblk) {
     auto at_depth = [&](int64_t v) -> bool {
         return fb ? ((fb[v >> 6] >> (v & 63)) & 1ull) != 0 : level[v] == depth;
     };
     __shared__ uint32_t wsum[kBfsBlock / kWave];
     __shared__ uint32_t tile_base;
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    for (int64_t t0 = (int64_t)blockIdx.x * kQTile; t0 < n; t0 += (int64_t)gridDim.x * kQTile) {
+    for (int64_t t0 = (int64_t)bid * kQTile; t0 < n; t0 += (int64_t)nblk * kQTile) {
         const int64_t t1 = min(t0 + kQTile, n);
         uint32_t mine = 0;
         for (int64_t v = t0 + threadIdx.x; v < t1; v += kBfsBlock)
@@ -250,7 +251,7 @@ __device__ __forceinline__ void bfs_level_queue(const int64_t *__restrict__ rp, 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue(const int64_t *__restrict__ rp,
                                                                const int32_t *__restrict__ level, int64_t n,
                                                                int32_t depth, uint64_t *queue, uint32_t *qcount) {
-    bfs_level_queue(rp, level, n, depth, queue, qcount);
+    bfs_level_queue(rp, level, n, depth, queue, qcount, nullptr, blockIdx.x, gridDim.x);
 }
 
 // ---- device-driven levels ----------------------------------------------------------------
@@ -335,7 +336,7 @@ __global__ void k_bfs_plan(BfsState *st) {
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_bitmap_dev(const int32_t *__restrict__ level, int64_t n,
                                                               const BfsState *st, uint64_t *fb0, uint64_t *fb1) {
     if (st->mode != 2 || st->fb_ready) return;
-    bfs_bitmap(level, n, st->depth, st->fbi ? fb1 : fb0);
+    bfs_bitmap(level, n, st->depth, st->fbi ? fb1 : fb0, blockIdx.x, gridDim.x);
 }
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup_dev(const int64_t *__restrict__ rpi,
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_bottomup_dev(const int64_t *_
     if (st->mode != 2) return;
     const int i = st->fbi;
     bfs_bottomup(rpi, cii, rpo, i ? fb1 : fb0, n, level, st->depth, st->bucnt,
-                 st->nextbits ? (i ? fb0 : fb1) : nullptr);
+                 st->nextbits ? (i ? fb0 : fb1) : nullptr, blockIdx.x, gridDim.x);
 }
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue_dev(const int64_t *__restrict__ rp,
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_level_queue_dev(const int64_t
     if (st->mode != 1 || !st->need_queue) return;
     const int qi = st->qi;
     bfs_level_queue(rp, level, n, st->depth, qi ? q1 : q0, &st->qcnt[qi],
-                    st->fb_ready && st->qbits ? (st->fbi ? fb1 : fb0) : nullptr);
+                    st->fb_ready && st->qbits ? (st->fbi ? fb1 : fb0) : nullptr, blockIdx.x, gridDim.x);
 }
 
 __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown_dev(const int64_t *__restrict__ rp,
@@ -365,7 +366,50 @@ __global__ __launch_bounds__(kBfsBlock) void k_bfs_topdown_dev(const int64_t *__
     if (st->mode != 1) return;
     const int qi = st->qi;
     bfs_topdown(rp, ci, qi ? q1 : q0, st->qcnt[qi], level, st->depth, qi ? q0 : q1, &st->qcnt[qi ^ 1],
-                &st->nedges);
+                &st->nedges, blockIdx.x, gridDim.x);
+}
+
+// A level in two launches instead of four (GX_BFS_FUSED, the default): the frontier phase
+// (bottom-up: the bitmap unless the last level left it; top-down: the queue rebuild when
+// needed) and the expansion (bottom-up or top-down), each branching on the plan's mode, so
+// the direction not taken costs no idle launch.  Blocks past a phase's own grid exit, and the
+// phase runs on exactly the grid its separate kernel had.
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_frontier_dev(const int64_t *__restrict__ rp,
+                                                                const int32_t *__restrict__ level, int64_t n,
+                                                                BfsState *st, uint64_t *fb0, uint64_t *fb1,
+                                                                uint64_t *q0, uint64_t *q1, uint32_t vgrid,
+                                                                uint32_t qgrid) {
+    const int mode = st->mode;
+    if (mode == 2) {
+        if (st->fb_ready || blockIdx.x >= vgrid) return;
+        bfs_bitmap(level, n, st->depth, st->fbi ? fb1 : fb0, blockIdx.x, vgrid);
+    } else if (mode == 1) {
+        if (!st->need_queue || blockIdx.x >= qgrid) return;
+        const int qi = st->qi;
+        bfs_level_queue(rp, level, n, st->depth, qi ? q1 : q0, &st->qcnt[qi],
+                        st->fb_ready && st->qbits ? (st->fbi ? fb1 : fb0) : nullptr, blockIdx.x, qgrid);
+    }
+}
+
+__global__ __launch_bounds__(kBfsBlock) void k_bfs_expand_dev(const int64_t *__restrict__ rpi,
+                                                              const int32_t *__restrict__ cii,
+                                                              const int64_t *__restrict__ rp,
+                                                              const int32_t *__restrict__ ci, int32_t *level,
+                                                              int64_t n, BfsState *st, uint64_t *fb0, uint64_t *fb1,
+                                                              uint64_t *q0, uint64_t *q1, uint32_t bu_grid,
+                                                              uint32_t tgrid) {
+    const int mode = st->mode;
+    if (mode == 2) {
+        if (blockIdx.x >= bu_grid) return;
+        const int i = st->fbi;
+        bfs_bottomup(rpi, cii, rp, i ? fb1 : fb0, n, level, st->depth, st->bucnt,
+                     st->nextbits ? (i ? fb0 : fb1) : nullptr, blockIdx.x, bu_grid);
+    } else if (mode == 1) {
+        if (blockIdx.x >= tgrid) return;
+        const int qi = st->qi;
+        bfs_topdown(rp, ci, qi ? q1 : q0, st->qcnt[qi], level, st->depth, qi ? q0 : q1, &st->qcnt[qi ^ 1],
+                    &st->nedges, blockIdx.x, tgrid);
+    }
 }
 
 __global__ void k_bfs_seed(const int64_t *__restrict__ rp, int32_t *level, uint64_t *queue, uint32_t *qcount,
@@ -466,9 +510,23 @@ extern "C" int gx_bfs(gx_graph *g, uint64_t src, int64_t *level_out) {
         const unsigned vgrid = grid_for(n, kBfsBlock, gcap);
         const unsigned tgrid = std::min(8192u, gcap);
         const unsigned qgrid = (unsigned)std::min<int64_t>((n + kQTile - 1) / kQTile, 2048);
+        const char *fe = std::getenv("GX_BFS_FUSED");
+        const bool fused = !fe || std::atoi(fe) != 0;
         auto enqueue = [&](int k) -> int {
             for (int i = 0; i < k; i++) {
                 hipLaunchKernelGGL(k_bfs_plan, dim3(1), dim3(1), 0, s, st.p);
+                if (fused) {
+                    if (in) {
+                        KTimer kt(ctx, "bfs_frontier", s);
+                        hipLaunchKernelGGL(k_bfs_frontier_dev, dim3(std::max(vgrid, qgrid)), dim3(kBfsBlock), 0, s,
+                                           g->A.rp.p, level.p, n, st.p, fbits.p, fb1, q0.p, q1.p, vgrid, qgrid);
+                    }
+                    KTimer kt(ctx, "bfs_expand", s);
+                    hipLaunchKernelGGL(k_bfs_expand_dev, dim3(std::max(in ? bu_grid : 0u, tgrid)), dim3(kBfsBlock), 0,
+                                       s, in ? in->rp.p : nullptr, in ? in->ci.p : nullptr, g->A.rp.p, g->A.ci.p,
+                                       level.p, n, st.p, fbits.p, fb1, q0.p, q1.p, in ? bu_grid : 0u, tgrid);
+                    continue;
+                }
                 if (in) {
                     KTimer kt(ctx, "bfs_bottomup", s);
                     hipLaunchKernelGGL(k_bfs_bitmap_dev, dim3(vgrid), dim3(kBfsBlock), 0, s, level.p, n, st.p,

@@ -549,16 +549,19 @@ def test_wcc_sampling_modes(ctx, monkeypatch, env):
 @pytest.mark.parametrize("device,nextbits,grid,qbits", [("1", "1", None, "1"), ("1", "1", None, "0"),
                                                         ("1", "0", None, "1"), ("1", "1", "3", "1"),
                                                         ("1", "0", "8192", "1"), ("0", "1", None, "1")])
-def test_bfs_level_driver(ctx, monkeypatch, device, nextbits, grid, qbits):
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_bfs_level_driver(ctx, monkeypatch, device, nextbits, grid, qbits, fused):
     """BFS levels planned on the device (GX_BFS_DEVICE=1, batches of levels, done flag read a
     batch late) or by the host: the oracle's levels on power-law graphs (top-down and
     bottom-up levels), a 3 000-level chain (many batches) and an isolated source.  On the device
     path a bottom-up level writes the next level's frontier bitmap (GX_BFS_NEXTBITS=1) or a
     bitmap pass rebuilds it from the levels, and a top-down level after it builds its queue from
     that bitmap (GX_BFS_QBITS=1) or from the levels; GX_BFS_GRID caps the grid-stride kernels'
-    grids (3 workgroups: many rounds per wave)."""
+    grids (3 workgroups: many rounds per wave).  A level runs as two launches branching on the
+    plan's direction (GX_BFS_FUSED=1, the default) or as the four direction kernels."""
     from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
     monkeypatch.setenv("GX_BFS_DEVICE", device)
+    monkeypatch.setenv("GX_BFS_FUSED", fused)
     monkeypatch.setenv("GX_BFS_NEXTBITS", nextbits)
     monkeypatch.setenv("GX_BFS_QBITS", qbits)
     if grid:
@@ -566,6 +569,16 @@ def test_bfs_level_driver(ctx, monkeypatch, device, nextbits, grid, qbits):
     for g in (_rmat(14, 16, 4), _rmat(12, 8, 3, undirected=False)):
         s = _src(g)
         np.testing.assert_array_equal(gpu_run(ctx, g, "BFS", source=s), O.bfs(g.csr, s))
+    # a directed graph with its transpose (bottom-up levels): two calls on one graph
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    gd = _rmat(12, 8, 3, undirected=False)
+    G = A.Graph(ctx, gd.csr, True)
+    try:
+        s = _src(gd)
+        for _ in range(3):
+            np.testing.assert_array_equal(A.LA_BFS(G, s), O.bfs(gd.csr, s))
+    finally:
+        G.close()
     n = 3000
     perm = np.random.default_rng(2).permutation(n)
     csr = csr_from_edges(n + 1, perm[:-1], perm[1:], None, symmetric=True)   # vertex n isolated
