@@ -1116,15 +1116,23 @@ __global__ __launch_bounds__(256) void k_cdlp_sparse_fused(CdlpArgs a, SparseFus
     const int64_t b = (int64_t)blockIdx.x + boff;
     if (b < 8 * S) {
         sparse_wave_role(a, f.al, f.asub, f.cnt, f.fw, f.nfw, b, 8 * S, lds);
-    } else if (b < 12 * S) {
+    } else {
         sparse_group_role<kMid2Block, kMid2Slots, kMid2Max>(a, f.al + shards, f.asub, f.cnt + S * kCntStride, f.fg2,
                                                             f.nfg2, nullptr, 0, nullptr, nullptr, nullptr, b - 8 * S,
                                                             4 * S, lds);
-    } else {
-        sparse_group_role<kMid2Block, kMid2Slots, kMidMax>(a, f.al + 2 * shards, f.asub, f.cnt + 2 * S * kCntStride,
-                                                           f.fg4, f.nfg4, f.fg, f.nfg, f.redo, f.rcount, nullptr,
-                                                           b - 12 * S, 8 * S, lds);
     }
+}
+
+// The 8192-degree list on 512-thread workgroups, 16 labels per thread in registers: as a third
+// role of k_cdlp_sparse_fused (256 threads, 32 labels each) it set the fused kernel's registers
+// to 175 VGPRs, two workgroups per CU for every role.
+constexpr int kSparseBigBlock = 512;
+__global__ __launch_bounds__(kSparseBigBlock) void k_cdlp_sparse_big(CdlpArgs a, SparseFusedArgs f) {
+    __shared__ uint32_t lds[(sparse_group_lds<kSparseBigBlock, kMid2Slots>() + 3) / 4];
+    const int64_t S = kCdlpSubs, shards = S * f.asub;
+    sparse_group_role<kSparseBigBlock, kMid2Slots, kMidMax>(a, f.al + 2 * shards, f.asub, f.cnt + 2 * S * kCntStride,
+                                                            f.fg4, f.nfg4, f.fg, f.nfg, f.redo, f.rcount, nullptr,
+                                                            blockIdx.x, gridDim.x, lds);
 }
 
 // ---- own-label check (dense active iterations) ----------------------------------------
@@ -1671,16 +1679,18 @@ int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t 
                                 sl->redo,
                                 sl->rcount};
         if (env_on("GX_CDLP_SPARSE_FUSED")) {
-            hipLaunchKernelGGL(k_cdlp_sparse_fused, dim3(20 * kCdlpSubs), dim3(256), 0, s, a, f, 0);
+            hipLaunchKernelGGL(k_cdlp_sparse_fused, dim3(12 * kCdlpSubs), dim3(256), 0, s, a, f, 0);
             GX_TRY(check_launch("k_cdlp_sparse_fused"));
         } else {
-            const int ranges[4] = {0, 8 * kCdlpSubs, 12 * kCdlpSubs, 20 * kCdlpSubs};
-            for (int q = 0; q < 3; q++) {
+            const int ranges[3] = {0, 8 * kCdlpSubs, 12 * kCdlpSubs};
+            for (int q = 0; q < 2; q++) {
                 hipLaunchKernelGGL(k_cdlp_sparse_fused, dim3(ranges[q + 1] - ranges[q]), dim3(256), 0, s, a, f,
                                    ranges[q]);
                 GX_TRY(check_launch("k_cdlp_sparse_fused"));
             }
         }
+        hipLaunchKernelGGL(k_cdlp_sparse_big, dim3(8 * kCdlpSubs), dim3(kSparseBigBlock), 0, s, a, f);
+        GX_TRY(check_launch("k_cdlp_sparse_big"));
         hipLaunchKernelGGL((k_cdlp_sparse_group<kMidBlock, kMidSlots, kMidMax>), dim3(kCdlpSubs), dim3(kMidBlock), 0,
                            s, a, nullptr, (int64_t)0, nullptr, nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr,
                            sl->rcount, sl->redo);
