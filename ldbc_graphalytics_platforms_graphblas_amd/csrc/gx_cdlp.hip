@@ -65,6 +65,12 @@ struct CdlpArgs {
     // own-label check of a dense active iteration ran (k_cdlp_keep_*): k_cdlp_tiny recomputes
     // every tiny vertex although the iteration is sparse (null: never)
     const int *keep = nullptr;
+    // huge vertices' majority bound (relabelled graphs, active iterations; null: off): hlb[hi] a
+    // lower bound on the count of the vertex's label among the last iteration's input labels,
+    // hchg[hi] its neighbour entries whose label changed since (counted by k_cdlp_mark)
+    int32_t *hlb = nullptr;
+    int32_t *hchg = nullptr;
+    const int *hvalid = nullptr;   // k_cdlp_mark counted every change (the change list was complete)
 };
 
 __device__ __forceinline__ bool tier_idle(const CdlpArgs &a) { return a.sparse && *a.dense == 0; }
@@ -496,6 +502,12 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
         ib = a.rpT[v];
         id = a.rpT[v + 1] - ib;
     }
+    // Majority bound (active iterations whose change list was complete, so k_cdlp_mark counted
+    // every changed entry): the label held a count of at least hlb among the last input; each
+    // changed neighbour entry lowers that by at most one.  Still a strict majority: it is the
+    // unique mode, the vertex keeps it, and k_cdlp_huge_final carries the bound on.  Every chunk
+    // of the vertex decides alike.
+    if (a.hlb && a.sparse && *a.hvalid && 2 * ((int64_t)a.hlb[hi] - a.hchg[hi]) > od + id) return;
     const int64_t k0 = cbeg[blockIdx.x], k1 = min(k0 + kHugeChunk, od + id);
     for (int s = tid; s < kHugeSlots; s += kHugeBlock) {
         K[s] = kEmpty;
@@ -564,8 +576,13 @@ __global__ void k_cdlp_huge_final(CdlpArgs a, const int32_t *__restrict__ hv, in
                                   unsigned long long *vkey) {
     for (int32_t hi = blockIdx.x * blockDim.x + threadIdx.x; hi < nhuge; hi += gridDim.x * blockDim.x) {
         const int64_t v = hv[hi];
-        const int32_t best = active(a, all_active(a), v) ? (int32_t)(kEmpty - (uint32_t)(vkey[hi] & 0xffffffffu))
-                                                         : a.lab[v];
+        // recomputed (a key), or inactive / kept by the majority bound (its label stays)
+        const unsigned long long k = vkey[hi];
+        const int32_t best = k ? (int32_t)(kEmpty - (uint32_t)(k & 0xffffffffu)) : a.lab[v];
+        if (a.hlb) {
+            a.hlb[hi] = k ? (int32_t)(k >> 32) : a.hlb[hi] - a.hchg[hi];
+            a.hchg[hi] = 0;
+        }
         vkey[hi] = 0;   // clean for the next iteration
         a.nxt[v] = best;
         if (best != a.lab[v]) raise_flag_sharded(a.changed, a.cshards);
@@ -833,12 +850,14 @@ __global__ __launch_bounds__(256) void k_cdlp_mark(const int64_t *__restrict__ r
                                                    const int64_t *__restrict__ rpT, const int32_t *__restrict__ ciT,
                                                    const uint64_t *__restrict__ list, int64_t sub,
                                                    unsigned int *counts, int32_t *act, int32_t stamp, int *dense,
-                                                   int32_t *al, int64_t asub) {
+                                                   int32_t *al, int64_t asub, int32_t *hchg, int32_t nhuge,
+                                                   int *hvalid) {
     __shared__ int over;
     if (threadIdx.x == 0) over = 0;
     __syncthreads();
     if (counts[threadIdx.x * kCntStride] > (unsigned int)sub) over = 1;   // kCdlpSubs == blockDim.x
     __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0 && hvalid) *hvalid = over ? 0 : 1;
     if (over) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *dense = 1;
         return;
@@ -860,6 +879,8 @@ __global__ __launch_bounds__(256) void k_cdlp_mark(const int64_t *__restrict__ r
             int64_t w = -1;
             if (k < k1) w = k < od ? ciA[ob + k] : ciT[ib + (k - od)];
             const bool fresh = w >= 0 && atomicExch(&act[w], stamp) != stamp;
+            // a huge vertex (the relabelled graph's first nhuge) counts every changed entry
+            if (hchg && w >= 0 && w < nhuge) atomicAdd(&hchg[w], 1);
             const int64_t dw = fresh ? cdlp_degree(rpA, rpT, w) : 0;
             // activation list 1 + L: L = 0 (wave), 1 (256-thread group), 2 (1024-thread group)
             const int L = !fresh || dw > kMidMax ? -1 : dw <= kSparseWaveMax ? 0 : dw <= kSparseG2Max ? 1 : 2;
@@ -1368,7 +1389,8 @@ __global__ __launch_bounds__(256) void k_cdlp_keep_sorted(const int64_t *__restr
 __global__ __launch_bounds__(256) void k_cdlp_keep_apply(const int64_t *__restrict__ rpA, const int64_t *__restrict__ rpT,
                                                          int64_t v0, int64_t v1, uint32_t *kcnt, int32_t *act,
                                                          int32_t stamp, const int *keep, unsigned int *counts,
-                                                         int32_t *al, int64_t asub, int *kover) {
+                                                         int32_t *al, int64_t asub, int *kover, int32_t *hlb,
+                                                         const int32_t *hchg, int32_t nhuge) {
     if (*keep == 0) return;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t gw = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave;
@@ -1387,6 +1409,8 @@ __global__ __launch_bounds__(256) void k_cdlp_keep_apply(const int64_t *__restri
                 if (d > kMidMax) {
                     if (!kept) act[v] = stamp;
                     else if (act[v] == stamp) act[v] = stamp - 1;
+                    // a kept huge vertex's bound is its exact count (k_cdlp_huge_final subtracts hchg)
+                    if (kept && hlb && v < nhuge) hlb[v] = (int32_t)c + hchg[v];
                 } else if (!kept) {
                     L = d <= kSparseWaveMax ? 0 : d <= kSparseG2Max ? 1 : 2;
                 }
@@ -1528,6 +1552,11 @@ struct CdlpPlan {
     DBuf<unsigned long long> gtab;      // huge vertices' global tables (k_cdlp_huge_insert's words)
     uint32_t epoch = 0;                 // the last iteration's table epoch (1..kHugeEpochs)
     DBuf<unsigned long long> vkey;      // per huge vertex best key (zero between iterations)
+    // the huge vertices' majority bound (gx_cdlp on the relabelled graph): hlb / hchg per huge
+    // vertex, the change list's completeness flag; huge_prefix: the huge vertices are [0, n_huge)
+    DBuf<int32_t> hlb, hchg;
+    DBuf<int> hvalid;
+    bool huge_prefix = false;
 };
 
 // Switches read at every call (tests flip them within one process); unset means `dflt`.
@@ -1596,6 +1625,14 @@ int cdlp_plan(const CdlpGraph &g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream
         GX_TRY(P.d_hl.alloc(hl.size()));
         GX_TRY(P.d_hoff.alloc(hoff.size()));
         GX_TRY(P.gtab.alloc(total));
+        GX_TRY(P.hlb.alloc(hv.size()));
+        GX_TRY(P.hchg.alloc(hv.size()));
+        GX_TRY(P.hvalid.alloc(1));
+        GX_HIP_TRY(hipMemsetAsync(P.hlb.p, 0, hv.size() * 4, s));
+        GX_HIP_TRY(hipMemsetAsync(P.hchg.p, 0, hv.size() * 4, s));
+        GX_HIP_TRY(hipMemsetAsync(P.hvalid.p, 0, sizeof(int), s));
+        P.huge_prefix = true;
+        for (size_t i = 0; i < hv.size(); i++) P.huge_prefix = P.huge_prefix && hv[i] == (int32_t)i;
         GX_TRY(P.vkey.alloc(hv.size()));
         GX_HIP_TRY(hipMemsetAsync(P.vkey.p, 0, hv.size() * 8, s));
         GX_HIP_TRY(hipMemsetAsync(P.gtab.p, 0, (size_t)total * 8, s));   // epoch 0: every slot empty
@@ -1650,13 +1687,19 @@ struct SparseLists {
 
 int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
                    const int32_t *act = nullptr, int32_t stamp = 0, const int *dense = nullptr, bool first = false,
-                   const SparseLists *sl = nullptr, int cshards = 1, const int *keep = nullptr) {
+                   const SparseLists *sl = nullptr, int cshards = 1, const int *keep = nullptr,
+                   bool hbound = false) {
     gx_ctx *ctx = g.ctx;
     const int64_t n = g.n;
     CdlpArgs a{g.rpA,  g.ciA,  g.rpT, g.ciT,  cur,        nxt,     n,        changed,
                P.v0,   P.v1,   act,   stamp,  dense,      first && !g.directed ? 1 : 0,
                sl ? 1 : 0,     cshards};
     a.keep = keep;
+    if (hbound) {
+        a.hlb = P.hlb.p;
+        a.hchg = P.hchg.p;
+        a.hvalid = P.hvalid.p;
+    }
     const bool tiers = !(sl && sl->only);   // sparse-only: the huge tier alone beside the sparse kernels
     if (sl) {
         // exit at once when *dense (the tier kernels below then recompute every vertex)
@@ -2158,6 +2201,9 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         GX_HIP_TRY(hipMemsetAsync(C->ccount.p, 0, sizeof(unsigned int) * kCdlpLists * kCdlpSubs * kCntStride * iters, s));
         GX_HIP_TRY(hipMemsetAsync(C->rcnt.p, 0, sizeof(unsigned int) * iters, s));
     }
+    // the huge vertices' majority bound (GX_CDLP_HUGE_BOUND=0: off): the relabelled graph, whose
+    // huge vertices are [0, n_huge), so k_cdlp_mark can count their changed entries by id
+    const bool hbound = relabel && P.n_huge && P.huge_prefix && env_on("GX_CDLP_HUGE_BOUND");
     int32_t *cur = C->la.p, *nxt = C->lb.p;
     for (int it = 0; it < iters; it++) {
         int *changed = C->changed.p + (size_t)it * kFlagShards * kFlagStride;
@@ -2171,7 +2217,8 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                 GX_TRY(check_launch("k_cdlp_changed"));
                 // 32 waves per shard of the change list (the grid must be a multiple of kCdlpSubs waves)
                 hipLaunchKernelGGL(k_cdlp_mark, dim3(8 * kCdlpSubs), dim3(kCdlpSubs), 0, s, G.rpA, G.ciA, G.rpT, G.ciT,
-                                   C->clist.p, sub, cnt, C->act.p, (int32_t)it, C->dense.p, C->al.p, C->asub);
+                                   C->clist.p, sub, cnt, C->act.p, (int32_t)it, C->dense.p, C->al.p, C->asub,
+                                   hbound ? P.hchg.p : nullptr, (int32_t)P.n_huge, hbound ? P.hvalid.p : nullptr);
                 GX_TRY(check_launch("k_cdlp_mark"));
             }
             // sparse-only (no idle tier launches, ~60 us per iteration on SYN-7_5) when iteration
@@ -2211,14 +2258,15 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                     if (G.directed) GX_TRY(count(G.ciT, C->keep_nnzT, C->kT, 0));
                 }
                 hipLaunchKernelGGL(k_cdlp_keep_apply, dim3(8 * kCdlpSubs), dim3(256), 0, s, G.rpA, G.rpT, (int64_t)0, n,
-                                   C->kcnt.p, C->act.p, (int32_t)it, kf, cnt, C->al.p, C->asub, kf + 1);
+                                   C->kcnt.p, C->act.p, (int32_t)it, kf, cnt, C->al.p, C->asub, kf + 1,
+                                   hbound ? P.hlb.p : nullptr, hbound ? P.hchg.p : nullptr, (int32_t)P.n_huge);
                 GX_TRY(check_launch("k_cdlp_keep_apply"));
                 hipLaunchKernelGGL(k_cdlp_keep_finish, dim3(1), dim3(1), 0, s, C->dense.p, kf, kf + 1);
                 GX_TRY(check_launch("k_cdlp_keep_finish"));
             }
             const SparseLists sl{C->al.p, C->asub, cnt, only, C->redo.p, C->rcnt.p + it};
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
-                                  use_sparse ? &sl : nullptr, kFlagShards, kf));
+                                  use_sparse ? &sl : nullptr, kFlagShards, kf, hbound));
         } else if (it == 0 && C->rows_sorted && first_sorted) {
             // on the caller's graph and vertex order (whose rows the check found sorted)
             KTimer kt(ctx, "cdlp_first", s);
@@ -2236,7 +2284,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             // (`first`) assumes no row repeats a column; k_rows_sorted found the caller's rows
             // strictly ascending, i.e. duplicate-free (else the counting path runs).
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0 && C->rows_sorted, nullptr,
-                                  kFlagShards));
+                                  kFlagShards, nullptr, hbound));
         }
         hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(kWave), 0, s, changed, kFlagShards,
                            active && it >= 2 ? C->dense.p : nullptr, dflag + it);
