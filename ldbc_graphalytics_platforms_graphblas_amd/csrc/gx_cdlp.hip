@@ -65,13 +65,27 @@ struct CdlpArgs {
     // own-label check of a dense active iteration ran (k_cdlp_keep_*): k_cdlp_tiny recomputes
     // every tiny vertex although the iteration is sparse (null: never)
     const int *keep = nullptr;
-    // huge vertices' majority bound (relabelled graphs, active iterations; null: off): hlb[hi] a
-    // lower bound on the count of the vertex's label among the last iteration's input labels,
-    // hchg[hi] its neighbour entries whose label changed since (counted by k_cdlp_mark)
-    int32_t *hlb = nullptr;
-    int32_t *hchg = nullptr;
+    // recount bound (gx_cdlp; null: off): the count of v's label among its neighbour entries is
+    // at least vlb[v] - vchg[v] -- vlb the count when v's label was last computed, vchg the
+    // changed neighbour entries k_cdlp_mark has counted since
+    int32_t *vlb = nullptr;
+    int32_t *vchg = nullptr;
     const int *hvalid = nullptr;   // k_cdlp_mark counted every change (the change list was complete)
 };
+
+// v's label was computed with at least c occurrences in this iteration's input.
+__device__ __forceinline__ void bound_set(const CdlpArgs &a, int64_t v, uint32_t c) {
+    if (a.vlb) {
+        a.vlb[v] = (int32_t)c;
+        a.vchg[v] = 0;
+    }
+}
+
+// An active iteration whose change list was complete: v's label still holds a strict majority
+// (each changed entry lowers its count by at most one), so it is the unique mode and v keeps it.
+__device__ __forceinline__ bool bound_keeps(const CdlpArgs &a, int64_t v, int64_t d) {
+    return a.vlb && a.sparse && *a.hvalid && 2 * ((int64_t)a.vlb[v] - a.vchg[v]) > d;
+}
 
 __device__ __forceinline__ bool tier_idle(const CdlpArgs &a) { return a.sparse && *a.dense == 0; }
 
@@ -277,6 +291,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
             uint32_t nc = 0;
 #pragma unroll
             for (int k = 0; k < kTiny; k++) nc += (k < d && L[k] == vt.c) ? 1u : 0u;
+            uint32_t cnt = 0;   // the winner's count (the recount bound)
             if (a.first) {
                 uint32_t mn = kEmpty;
 #pragma unroll
@@ -284,6 +299,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
                 best = (int32_t)mn;
             } else if (2 * (int64_t)nc > d) {
                 best = (int32_t)vt.c;   // strict majority
+                cnt = nc;
             } else {
                 sort_regs(L);           // labels ascending, the padding last
                 uint32_t bc = 0, bl = kEmpty, run = 0, prev = kEmpty;
@@ -297,7 +313,9 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_tiny(CdlpArgs a) {
                     }
                 }
                 best = (int32_t)bl;
+                cnt = bc;
             }
+            bound_set(a, v, cnt);
         }
         a.nxt[v] = best;
         any |= best != old;
@@ -324,12 +342,15 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
         const uint32_t my = lane < d ? (uint32_t)label_at(a, ob, od, ib, lane) : kEmpty;
         const uint32_t cand = __shfl(wave_vote(Vote{my, lane < d ? 1u : 0u}).c, 0, kWave);
         int32_t best;
+        uint32_t cnt = 0;   // the winner's count (the recount bound)
+        const uint32_t ncand = (uint32_t)__popcll(__ballot(lane < d && my == cand));
         if (d == 0) {
             best = old;   // inactive (or isolated)
         } else if (a.first) {
             best = (int32_t)wave_min_u32(my);
-        } else if (2 * (int64_t)__popcll(__ballot(lane < d && my == cand)) > d) {
+        } else if (2 * (int64_t)ncand > d) {
             best = (int32_t)cand;   // strict majority
+            cnt = ncand;
         } else {
             // one round per distinct label: the first remaining lane's label, its lanes by one
             // ballot (lane reads, no LDS; the d shuffles this replaces were ds_bpermute each)
@@ -346,10 +367,12 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_small(CdlpArgs a, const int
                 rem &= ~eq;
             }
             best = (int32_t)bl;
+            cnt = bc;
         }
         if (lane == 0) {
             a.nxt[v] = best;
             any |= best != old;
+            if (d > 0) bound_set(a, v, cnt);
         }
     }
     if (any) raise_flag_sharded(a.changed, a.cshards);
@@ -446,9 +469,10 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
         }
 #pragma unroll
         for (int r = 0; r < R; r++) L[r] = cn[r] >= 0 ? (uint32_t)lsrc(a)[cn[r]] : kEmpty;   // link 4
-        const int32_t best = d == 0 ? old
-                             : maj ? (int32_t)cand
-                                   : (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+        const unsigned long long wk = maj ? 0ull : wave_max_u64(key);
+        const int32_t best = d == 0 ? old : maj ? (int32_t)cand : (int32_t)(kEmpty - (uint32_t)(wk & 0xffffffffu));
+        // the winner's count (the recount bound; 0 for the first iteration's minimum)
+        const uint32_t cnt = a.first ? 0u : maj ? (uint32_t)nc : (uint32_t)(wk >> 32);
         if (!maj) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -457,6 +481,7 @@ __global__ __launch_bounds__(kCdlpBlock) void k_cdlp_light(CdlpArgs a, const int
         if (lane == 0) {
             a.nxt[v] = best;
             any |= best != old;
+            if (d > 0) bound_set(a, v, cnt);
         }
         if (!more) break;
         i = inext;
@@ -502,12 +527,9 @@ __global__ __launch_bounds__(kHugeBlock) void k_cdlp_huge_insert(CdlpArgs a, con
         ib = a.rpT[v];
         id = a.rpT[v + 1] - ib;
     }
-    // Majority bound (active iterations whose change list was complete, so k_cdlp_mark counted
-    // every changed entry): the label held a count of at least hlb among the last input; each
-    // changed neighbour entry lowers that by at most one.  Still a strict majority: it is the
-    // unique mode, the vertex keeps it, and k_cdlp_huge_final carries the bound on.  Every chunk
-    // of the vertex decides alike.
-    if (a.hlb && a.sparse && *a.hvalid && 2 * ((int64_t)a.hlb[hi] - a.hchg[hi]) > od + id) return;
+    // the recount bound: a vertex whose label provably keeps a strict majority skips the
+    // recount (every chunk of the vertex decides alike)
+    if (bound_keeps(a, v, od + id)) return;
     const int64_t k0 = cbeg[blockIdx.x], k1 = min(k0 + kHugeChunk, od + id);
     for (int s = tid; s < kHugeSlots; s += kHugeBlock) {
         K[s] = kEmpty;
@@ -579,10 +601,7 @@ __global__ void k_cdlp_huge_final(CdlpArgs a, const int32_t *__restrict__ hv, in
         // recomputed (a key), or inactive / kept by the majority bound (its label stays)
         const unsigned long long k = vkey[hi];
         const int32_t best = k ? (int32_t)(kEmpty - (uint32_t)(k & 0xffffffffu)) : a.lab[v];
-        if (a.hlb) {
-            a.hlb[hi] = k ? (int32_t)(k >> 32) : a.hlb[hi] - a.hchg[hi];
-            a.hchg[hi] = 0;
-        }
+        if (k) bound_set(a, v, a.first ? 0u : (uint32_t)(k >> 32));
         vkey[hi] = 0;   // clean for the next iteration
         a.nxt[v] = best;
         if (best != a.lab[v]) raise_flag_sharded(a.changed, a.cshards);
@@ -649,6 +668,7 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
         // branches are the same in every thread; an inactive vertex (d == 0) skips it all.
         uint32_t cand = kEmpty;
         bool maj = true;
+        uint32_t ccount = 0;   // the candidate's count (the recount bound; 0 in the first iteration)
         if (d > 0 && a.first) {
             uint32_t mn = kEmpty;
 #pragma unroll
@@ -682,6 +702,7 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
 #pragma unroll
             for (int j = 0; j < kMidBlock / kWave; j++) nc += cnt[j];
             maj = 2 * (int64_t)nc > d;
+            ccount = nc;
         }
         int log2ts = 1;
         while ((1ll << log2ts) < 2 * d) log2ts++;
@@ -727,6 +748,7 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
                 const int32_t best = d == 0 ? a.lab[v] : (int32_t)cand;
                 a.nxt[v] = best;
                 any |= best != a.lab[v];
+                if (d > 0) bound_set(a, v, ccount);
             }
         } else {
             key = wave_max_u64(key);
@@ -738,6 +760,7 @@ __global__ __launch_bounds__(kMidBlock) void k_cdlp_mid(CdlpArgs a, const int32_
                 const int32_t best = (int32_t)(kEmpty - (uint32_t)(mx & 0xffffffffu));
                 a.nxt[v] = best;
                 any |= best != a.lab[v];
+                bound_set(a, v, (uint32_t)(mx >> 32));
             }
         }
         if (d > 0) __syncthreads();   // red / cnt / bcast and the table are free for the next vertex
@@ -850,8 +873,7 @@ __global__ __launch_bounds__(256) void k_cdlp_mark(const int64_t *__restrict__ r
                                                    const int64_t *__restrict__ rpT, const int32_t *__restrict__ ciT,
                                                    const uint64_t *__restrict__ list, int64_t sub,
                                                    unsigned int *counts, int32_t *act, int32_t stamp, int *dense,
-                                                   int32_t *al, int64_t asub, int32_t *hchg, int32_t nhuge,
-                                                   int *hvalid) {
+                                                   int32_t *al, int64_t asub, int32_t *vchg, int *hvalid) {
     __shared__ int over;
     if (threadIdx.x == 0) over = 0;
     __syncthreads();
@@ -879,8 +901,8 @@ __global__ __launch_bounds__(256) void k_cdlp_mark(const int64_t *__restrict__ r
             int64_t w = -1;
             if (k < k1) w = k < od ? ciA[ob + k] : ciT[ib + (k - od)];
             const bool fresh = w >= 0 && atomicExch(&act[w], stamp) != stamp;
-            // a huge vertex (the relabelled graph's first nhuge) counts every changed entry
-            if (hchg && w >= 0 && w < nhuge) atomicAdd(&hchg[w], 1);
+            // the recount bound: every changed neighbour entry of w
+            if (vchg && w >= 0) atomicAdd(&vchg[w], 1);
             const int64_t dw = fresh ? cdlp_degree(rpA, rpT, w) : 0;
             // activation list 1 + L: L = 0 (wave), 1 (256-thread group), 2 (1024-thread group)
             const int L = !fresh || dw > kMidMax ? -1 : dw <= kSparseWaveMax ? 0 : dw <= kSparseG2Max ? 1 : 2;
@@ -931,6 +953,7 @@ __device__ __forceinline__ void sparse_wave_role(const CdlpArgs &a, const int32_
         const int64_t v = src[i];
         const VMeta m = vmeta(a, v);
         const int64_t d = (int64_t)m.od + m.id;
+        if (bound_keeps(a, v, d)) continue;   // its label provably stays (nxt already holds it)
         uint32_t L[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -947,8 +970,10 @@ __device__ __forceinline__ void sparse_wave_role(const CdlpArgs &a, const int32_
         for (int r = 0; r < R; r++)
             if ((int64_t)r * kWave < d) nc += __popcll(__ballot((int64_t)r * kWave + lane < d && L[r] == cand));
         int32_t best = old;
+        uint32_t cnt = 0;   // the winner's count (the recount bound)
         if (d > 0 && 2 * nc > d) {
             best = (int32_t)cand;
+            cnt = (uint32_t)nc;
         } else if (d > 0) {
             int log2ts = 1;
             while ((1ll << log2ts) < 2 * d) log2ts++;
@@ -974,7 +999,9 @@ __device__ __forceinline__ void sparse_wave_role(const CdlpArgs &a, const int32_
                     key = kk > key ? kk : key;
                 }
             }
-            best = (int32_t)(kEmpty - (uint32_t)(wave_max_u64(key) & 0xffffffffu));
+            const unsigned long long wk = wave_max_u64(key);
+            best = (int32_t)(kEmpty - (uint32_t)(wk & 0xffffffffu));
+            cnt = (uint32_t)(wk >> 32);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -982,6 +1009,7 @@ __device__ __forceinline__ void sparse_wave_role(const CdlpArgs &a, const int32_
         if (lane == 0) {
             a.nxt[v] = best;
             any |= best != old;
+            if (d > 0) bound_set(a, v, cnt);
         }
     }
     if (any) raise_flag_sharded(a.changed, a.cshards);
@@ -1026,6 +1054,7 @@ __device__ __forceinline__ void sparse_group_role(const CdlpArgs &a, const int32
         const int64_t v = full && i >= fn ? fl2[i - fn] : src[i];   // full: fn == 0 when fl is null
         const VMeta m = vmeta(a, v);
         const int64_t d = (int64_t)m.od + m.id;
+        if (bound_keeps(a, v, d)) continue;   // uniform in the workgroup; nxt already holds the label
         uint32_t L[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -1055,6 +1084,7 @@ __device__ __forceinline__ void sparse_group_role(const CdlpArgs &a, const int32
 #pragma unroll
         for (int q = 0; q < NW; q++) nc += cnt[q];
         int32_t best = (int32_t)cand;
+        uint32_t wcount = nc;   // the winner's count (the recount bound)
         if (2 * (int64_t)nc <= d && 2 * d > kSlots) {
             // no majority and no room for the table: the 16K-slot instance recomputes it
             if (tid == 0) redo[atomicAdd(rcount, 1u)] = (int32_t)v;
@@ -1088,11 +1118,13 @@ __device__ __forceinline__ void sparse_group_role(const CdlpArgs &a, const int32
             unsigned long long mx = red[0];
             for (int q = 1; q < NW; q++) mx = red[q] > mx ? red[q] : mx;
             best = (int32_t)(kEmpty - (uint32_t)(mx & 0xffffffffu));
+            wcount = (uint32_t)(mx >> 32);
         }
         if (tid == 0) {
             const int32_t old = a.lab[v];
             a.nxt[v] = best;
             any |= best != old;
+            if (d > 0) bound_set(a, v, wcount);
         }
         __syncthreads();   // red / cnt / bcast / the table are free for the next vertex
     }
@@ -1389,8 +1421,8 @@ __global__ __launch_bounds__(256) void k_cdlp_keep_sorted(const int64_t *__restr
 __global__ __launch_bounds__(256) void k_cdlp_keep_apply(const int64_t *__restrict__ rpA, const int64_t *__restrict__ rpT,
                                                          int64_t v0, int64_t v1, uint32_t *kcnt, int32_t *act,
                                                          int32_t stamp, const int *keep, unsigned int *counts,
-                                                         int32_t *al, int64_t asub, int *kover, int32_t *hlb,
-                                                         const int32_t *hchg, int32_t nhuge) {
+                                                         int32_t *al, int64_t asub, int *kover, int32_t *vlb,
+                                                         int32_t *vchg) {
     if (*keep == 0) return;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t gw = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kWave;
@@ -1406,11 +1438,14 @@ __global__ __launch_bounds__(256) void k_cdlp_keep_apply(const int64_t *__restri
                 const uint32_t c = kcnt[v];
                 if (c) kcnt[v] = 0u;
                 const bool kept = 2 * (int64_t)c > d;
+                if (kept && vlb) {   // the recount bound: the own label's exact count
+                    vlb[v] = (int32_t)c;
+                    vchg[v] = 0;
+                }
                 if (d > kMidMax) {
                     if (!kept) act[v] = stamp;
                     else if (act[v] == stamp) act[v] = stamp - 1;
-                    // a kept huge vertex's bound is its exact count (k_cdlp_huge_final subtracts hchg)
-                    if (kept && hlb && v < nhuge) hlb[v] = (int32_t)c + hchg[v];
+
                 } else if (!kept) {
                     L = d <= kSparseWaveMax ? 0 : d <= kSparseG2Max ? 1 : 2;
                 }
@@ -1552,11 +1587,12 @@ struct CdlpPlan {
     DBuf<unsigned long long> gtab;      // huge vertices' global tables (k_cdlp_huge_insert's words)
     uint32_t epoch = 0;                 // the last iteration's table epoch (1..kHugeEpochs)
     DBuf<unsigned long long> vkey;      // per huge vertex best key (zero between iterations)
-    // the huge vertices' majority bound (gx_cdlp on the relabelled graph): hlb / hchg per huge
-    // vertex, the change list's completeness flag; huge_prefix: the huge vertices are [0, n_huge)
-    DBuf<int32_t> hlb, hchg;
-    DBuf<int> hvalid;
-    bool huge_prefix = false;
+};
+
+// The recount bound's arrays (gx_cdlp, CdlpArgs::vlb / vchg / hvalid).
+struct CdlpBound {
+    int32_t *vlb, *vchg;
+    int *hvalid;
 };
 
 // Switches read at every call (tests flip them within one process); unset means `dflt`.
@@ -1625,14 +1661,6 @@ int cdlp_plan(const CdlpGraph &g, int64_t v0, int64_t v1, CdlpPlan &P, hipStream
         GX_TRY(P.d_hl.alloc(hl.size()));
         GX_TRY(P.d_hoff.alloc(hoff.size()));
         GX_TRY(P.gtab.alloc(total));
-        GX_TRY(P.hlb.alloc(hv.size()));
-        GX_TRY(P.hchg.alloc(hv.size()));
-        GX_TRY(P.hvalid.alloc(1));
-        GX_HIP_TRY(hipMemsetAsync(P.hlb.p, 0, hv.size() * 4, s));
-        GX_HIP_TRY(hipMemsetAsync(P.hchg.p, 0, hv.size() * 4, s));
-        GX_HIP_TRY(hipMemsetAsync(P.hvalid.p, 0, sizeof(int), s));
-        P.huge_prefix = true;
-        for (size_t i = 0; i < hv.size(); i++) P.huge_prefix = P.huge_prefix && hv[i] == (int32_t)i;
         GX_TRY(P.vkey.alloc(hv.size()));
         GX_HIP_TRY(hipMemsetAsync(P.vkey.p, 0, hv.size() * 8, s));
         GX_HIP_TRY(hipMemsetAsync(P.gtab.p, 0, (size_t)total * 8, s));   // epoch 0: every slot empty
@@ -1688,17 +1716,17 @@ struct SparseLists {
 int cdlp_iteration(const CdlpGraph &g, CdlpPlan &P, const int32_t *cur, int32_t *nxt, int *changed, hipStream_t s,
                    const int32_t *act = nullptr, int32_t stamp = 0, const int *dense = nullptr, bool first = false,
                    const SparseLists *sl = nullptr, int cshards = 1, const int *keep = nullptr,
-                   bool hbound = false) {
+                   const CdlpBound *bd = nullptr) {
     gx_ctx *ctx = g.ctx;
     const int64_t n = g.n;
     CdlpArgs a{g.rpA,  g.ciA,  g.rpT, g.ciT,  cur,        nxt,     n,        changed,
                P.v0,   P.v1,   act,   stamp,  dense,      first && !g.directed ? 1 : 0,
                sl ? 1 : 0,     cshards};
     a.keep = keep;
-    if (hbound) {
-        a.hlb = P.hlb.p;
-        a.hchg = P.hchg.p;
-        a.hvalid = P.hvalid.p;
+    if (bd) {
+        a.vlb = bd->vlb;
+        a.vchg = bd->vchg;
+        a.hvalid = bd->hvalid;
     }
     const bool tiers = !(sl && sl->only);   // sparse-only: the huge tier alone beside the sparse kernels
     if (sl) {
@@ -1857,6 +1885,8 @@ struct CdlpCache {
     // entries the check reads: with the hub-first copy (rows by total degree, descending) the
     // rows of degree <= kTiny, which it skips, hold every entry from here on
     int64_t keep_nnzA = 0, keep_nnzT = 0;
+    DBuf<int32_t> vlb, vchg;    // the recount bound (GX_CDLP_BOUND)
+    DBuf<int> hvalid;
     DBuf<int32_t> redo;         // k_cdlp_sparse_group's vertices for the 16K-slot instance
     DBuf<unsigned int> rcnt;    // one redo count per iteration
     ~CdlpCache() {
@@ -2201,9 +2231,21 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
         GX_HIP_TRY(hipMemsetAsync(C->ccount.p, 0, sizeof(unsigned int) * kCdlpLists * kCdlpSubs * kCntStride * iters, s));
         GX_HIP_TRY(hipMemsetAsync(C->rcnt.p, 0, sizeof(unsigned int) * iters, s));
     }
-    // the huge vertices' majority bound (GX_CDLP_HUGE_BOUND=0: off): the relabelled graph, whose
-    // huge vertices are [0, n_huge), so k_cdlp_mark can count their changed entries by id
-    const bool hbound = relabel && P.n_huge && P.huge_prefix && env_on("GX_CDLP_HUGE_BOUND");
+    // the recount bound (GX_CDLP_BOUND=0: off): an active iteration skips the vertices whose
+    // label provably keeps a strict majority
+    CdlpBound bound{nullptr, nullptr, nullptr};
+    if (env_on("GX_CDLP_BOUND")) {
+        if (C->vlb.n < (size_t)n) {
+            GX_TRY(C->vlb.alloc(n));
+            GX_TRY(C->vchg.alloc(n));
+            GX_TRY(C->hvalid.alloc(1));
+            GX_HIP_TRY(hipMemsetAsync(C->vlb.p, 0, (size_t)n * 4, s));
+            GX_HIP_TRY(hipMemsetAsync(C->vchg.p, 0, (size_t)n * 4, s));
+            GX_HIP_TRY(hipMemsetAsync(C->hvalid.p, 0, sizeof(int), s));
+        }
+        bound = CdlpBound{C->vlb.p, C->vchg.p, C->hvalid.p};
+    }
+    const CdlpBound *bd = bound.vlb ? &bound : nullptr;
     int32_t *cur = C->la.p, *nxt = C->lb.p;
     for (int it = 0; it < iters; it++) {
         int *changed = C->changed.p + (size_t)it * kFlagShards * kFlagStride;
@@ -2218,7 +2260,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                 // 32 waves per shard of the change list (the grid must be a multiple of kCdlpSubs waves)
                 hipLaunchKernelGGL(k_cdlp_mark, dim3(8 * kCdlpSubs), dim3(kCdlpSubs), 0, s, G.rpA, G.ciA, G.rpT, G.ciT,
                                    C->clist.p, sub, cnt, C->act.p, (int32_t)it, C->dense.p, C->al.p, C->asub,
-                                   hbound ? P.hchg.p : nullptr, (int32_t)P.n_huge, hbound ? P.hvalid.p : nullptr);
+                                   bd ? bd->vchg : nullptr, bd ? bd->hvalid : nullptr);
                 GX_TRY(check_launch("k_cdlp_mark"));
             }
             // sparse-only (no idle tier launches, ~60 us per iteration on SYN-7_5) when iteration
@@ -2259,14 +2301,14 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                 }
                 hipLaunchKernelGGL(k_cdlp_keep_apply, dim3(8 * kCdlpSubs), dim3(256), 0, s, G.rpA, G.rpT, (int64_t)0, n,
                                    C->kcnt.p, C->act.p, (int32_t)it, kf, cnt, C->al.p, C->asub, kf + 1,
-                                   hbound ? P.hlb.p : nullptr, hbound ? P.hchg.p : nullptr, (int32_t)P.n_huge);
+                                   bd ? bd->vlb : nullptr, bd ? bd->vchg : nullptr);
                 GX_TRY(check_launch("k_cdlp_keep_apply"));
                 hipLaunchKernelGGL(k_cdlp_keep_finish, dim3(1), dim3(1), 0, s, C->dense.p, kf, kf + 1);
                 GX_TRY(check_launch("k_cdlp_keep_finish"));
             }
             const SparseLists sl{C->al.p, C->asub, cnt, only, C->redo.p, C->rcnt.p + it};
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, C->act.p, (int32_t)it, C->dense.p, false,
-                                  use_sparse ? &sl : nullptr, kFlagShards, kf, hbound));
+                                  use_sparse ? &sl : nullptr, kFlagShards, kf, bd));
         } else if (it == 0 && C->rows_sorted && first_sorted) {
             // on the caller's graph and vertex order (whose rows the check found sorted)
             KTimer kt(ctx, "cdlp_first", s);
@@ -2284,7 +2326,7 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             // (`first`) assumes no row repeats a column; k_rows_sorted found the caller's rows
             // strictly ascending, i.e. duplicate-free (else the counting path runs).
             GX_TRY(cdlp_iteration(G, P, cur, nxt, changed, s, nullptr, 0, nullptr, it == 0 && C->rows_sorted, nullptr,
-                                  kFlagShards, nullptr, hbound));
+                                  kFlagShards, nullptr, bd));
         }
         hipLaunchKernelGGL(k_cdlp_flag_out, dim3(1), dim3(kWave), 0, s, changed, kFlagShards,
                            active && it >= 2 ? C->dense.p : nullptr, dflag + it);

@@ -490,15 +490,16 @@ def test_cdlp_huge_table_epochs(ctx, directed):
 
 
 @pytest.mark.parametrize("bound", ["1", "0"])
-def test_cdlp_huge_bound(ctx, monkeypatch, bound):
-    """Huge vertices (degree > 8192) whose label provably keeps a strict majority skip their
-    recount in sparse iterations (GX_CDLP_HUGE_BOUND, the default on the relabelled graph: the
-    last exact count minus the changed neighbour entries k_cdlp_mark counts).  Repeated calls
-    on one graph (the relabelled copy from the second), iteration counts through the sparse
-    phase, equal to the oracle's."""
+def test_cdlp_recount_bound(ctx, monkeypatch, bound):
+    """Vertices whose label provably keeps a strict majority skip their recount in active
+    iterations (GX_CDLP_BOUND, the default: the count when the label was last computed minus
+    the changed neighbour entries k_cdlp_mark counts since), in every sparse role and the huge
+    tier (degree > 8192).  Repeated calls on one graph (the relabelled copy from the second),
+    iteration counts through the sparse phase, equal to the oracle's."""
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
-    monkeypatch.setenv("GX_CDLP_HUGE_BOUND", bound)
-    for g in (_rmat(16, 48, 7), _G(_tier_graph(False), False), _rmat(15, 40, 5, undirected=False)):
+    monkeypatch.setenv("GX_CDLP_BOUND", bound)
+    for g in (_rmat(16, 48, 7), _G(_tier_graph(False), False), _rmat(15, 40, 5, undirected=False),
+              _rmat(14, 16, 4), _rmat(12, 4, 8)):
         deg = np.diff(g.csr.rowptr.astype(np.int64))
         G = A.Graph(ctx, g.csr, g.directed)
         try:
@@ -506,7 +507,7 @@ def test_cdlp_huge_bound(ctx, monkeypatch, bound):
                 np.testing.assert_array_equal(A.LA_CDLP(G, k), O.cdlp(g.csr, g.directed, k))
         finally:
             G.close()
-        assert g.directed or deg.max() > 8192
+        assert g.directed or deg.max() > 8192 or g.csr.n < 30000
 
 
 @pytest.mark.parametrize("keep,only,asub", [("1", "1", None), ("1", "2", None), ("1", "0", None), ("0", "1", None),
