@@ -19,7 +19,12 @@ with open(sys.argv[1]) as f:
 rows.sort()
 starts = [i for i, r in enumerate(rows) if r[2].startswith("k_cdlp_first_sorted")]
 if not starts:
-    sys.exit("no k_cdlp_first_sorted in the trace")
+    # directed graphs have no sorted first iteration: a call (relabelled) ends with the gather
+    # back to the caller's order, so the last call starts after the second-to-last gather
+    ends = [i for i, r in enumerate(rows) if r[2].startswith("k_cdlp_gather_i32")]
+    if len(ends) < 2:
+        sys.exit("no call boundary in the trace")
+    starts = [ends[-2] + 1]
 i0 = starts[-1]
 t0 = rows[i0][0]
 last_end = t0
