@@ -1493,6 +1493,98 @@ __global__ __launch_bounds__(256) void k_cdlp_first_sorted(const int64_t *__rest
     if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag_sharded(changed, cshards);
 }
 
+// First iteration of a directed graph whose rows (A and A') are strictly sorted: every label is
+// still its vertex id, a neighbour's label occurs once per direction, so the mode is the
+// smallest reciprocal neighbour (out and in: count 2) if there is one, else the smallest
+// neighbour of either direction.  Replaces the tiers' counting pass over every label (~0.45 ms
+// of SYN-cit's first iteration: a random label gather per entry).  A wave takes 64 consecutive
+// vertices: rows of at most kFirstSmall entries each are compared pair by pair in one lane's
+// registers, longer ones afterwards by the whole wave (first_dir_merge).  (A list of the long
+// rows for a second kernel cost 0.69 ms: one returning atomic per wave on one counter.)
+
+// Both rows of v merged 64 entries at a time (each out-entry looked up among the in-chunk by a
+// 6-step search over lanes), the chunk with the smaller last entry advanced.  Every common entry
+// is met in the round that retires its chunk, and chunks retire in ascending order, so the first
+// round with a hit holds the smallest one.  SYN-cit: at most 13 rounds, 1.4 per long row (a
+// reciprocal neighbour is usually near the front).  Wave-uniform: every lane calls it.
+__device__ __forceinline__ int32_t first_dir_merge(const int32_t *__restrict__ xr, int64_t od,
+                                                   const int32_t *__restrict__ yr, int64_t id, int lane) {
+    for (int64_t i = 0, j = 0; i < od && j < id;) {
+        const int32_t xa = i + lane < od ? xr[i + lane] : INT32_MAX;   // ids < n <= INT32_MAX
+        const int32_t yb = j + lane < id ? yr[j + lane] : INT32_MAX;
+        int pos = 0;   // entries of the in-chunk below xa
+#pragma unroll
+        for (int st = 32; st; st >>= 1) pos += __shfl(yb, pos + st - 1) < xa ? st : 0;
+        const int32_t at = __shfl(yb, pos & (kWave - 1));
+        const uint32_t h = wave_min_u32(pos < kWave && at == xa && xa != INT32_MAX ? (uint32_t)xa : 0xffffffffu);
+        if (h != 0xffffffffu) return (int32_t)h;
+        const int32_t xm = __shfl(xa, kWave - 1), ym = __shfl(yb, kWave - 1);
+        i += xm <= ym ? kWave : 0;
+        j += ym <= xm ? kWave : 0;
+    }
+    return INT32_MAX;
+}
+
+template <int kFirstSmall>
+__global__ __launch_bounds__(256) void k_cdlp_first_dir(const int64_t *__restrict__ rpA, const int32_t *__restrict__ ciA,
+                                                        const int64_t *__restrict__ rpT, const int32_t *__restrict__ ciT,
+                                                        int64_t n, int32_t *out, int *changed, int cshards) {
+    const int lane = threadIdx.x & (kWave - 1);
+    bool any = false;
+    // wave-uniform trips: v0 is the wave's first vertex
+    for (int64_t v0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~(kWave - 1)); v0 < n; v0 += (int64_t)gridDim.x * 256) {
+        const int64_t v = v0 + lane;
+        const bool in = v < n;
+        const int64_t ob = in ? rpA[v] : 0, od = in ? rpA[v + 1] - ob : 0;
+        const int64_t ib = in ? rpT[v] : 0, id = in ? rpT[v + 1] - ib : 0;
+        const bool lng = od > kFirstSmall || id > kFirstSmall;
+        if (in && !lng) {
+            // loads clamped into the row (or to entry 0: rows_sorted implies nnz > 0) and
+            // issued four at a time while any lane's rows reach that far
+            int32_t x[kFirstSmall], y[kFirstSmall];
+            const int64_t ra = od ? ob : 0, rb = id ? ib : 0, la = od ? od - 1 : 0, lb = id ? id - 1 : 0;
+            const int64_t wide = od > id ? od : id;
+#pragma unroll
+            for (int k = 0; k < kFirstSmall; k++) {
+                x[k] = -1;
+                y[k] = -2;   // the paddings match nothing
+            }
+#pragma unroll
+            for (int k0 = 0; k0 < kFirstSmall; k0 += 4) {
+                if (!__any(wide > k0)) break;
+#pragma unroll
+                for (int k = k0; k < k0 + 4; k++) {
+                    const int32_t a = ciA[ra + min((int64_t)k, la)], b = ciT[rb + min((int64_t)k, lb)];
+                    x[k] = k < od ? a : -1;
+                    y[k] = k < id ? b : -2;
+                }
+            }
+            int32_t m = INT32_MAX;
+#pragma unroll
+            for (int i = 0; i < kFirstSmall; i++)
+#pragma unroll
+                for (int j = 0; j < kFirstSmall; j++) m = x[i] == y[j] ? min(m, x[i]) : m;
+            const int32_t lo = min(od ? x[0] : INT32_MAX, id ? y[0] : INT32_MAX);
+            const int32_t l = m != INT32_MAX ? m : od + id ? lo : (int32_t)v;
+            out[v] = l;
+            any |= l != (int32_t)v;
+        }
+        // the long rows, one after the other, by the whole wave
+        for (uint64_t bal = __ballot(in && lng); bal; bal &= bal - 1) {
+            const int b = __builtin_ctzll(bal);
+            const int64_t u = v0 + b;
+            const int64_t uob = __shfl(ob, b), uod = __shfl(od, b), uib = __shfl(ib, b), uid = __shfl(id, b);
+            const int32_t m = first_dir_merge(ciA + uob, uod, ciT + uib, uid, lane);
+            const int32_t l = m != INT32_MAX ? m : min(uod ? ciA[uob] : INT32_MAX, uid ? ciT[uib] : INT32_MAX);
+            if (lane == 0) {
+                out[u] = l;
+                any |= l != (int32_t)u;
+            }
+        }
+    }
+    if (__ballot(any) && (threadIdx.x & (kWave - 1)) == 0) raise_flag_sharded(changed, cshards);
+}
+
 // Whether every row of a CSR is sorted by column (strictly: rows hold no duplicates): the row
 // starts as a bitmap over the entries, then one compare per entry.
 __global__ __launch_bounds__(256) void k_row_start_bits(const int64_t *__restrict__ rp, int64_t n, uint32_t *bits) {
@@ -1864,7 +1956,7 @@ struct CdlpCache {
     int *hflag = nullptr, *dflag = nullptr;
     int cap_iters = 0;
     int64_t sub = 0, asub = 0;
-    bool rows_sorted = false;   // A's rows sorted by column (k_rows_sorted)
+    bool rows_sorted = false;   // A's rows (and A''s, directed) sorted by column (k_rows_sorted)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     // the own-label check's edge-parallel layout of G's A (and A'), its counters and flags
     // (keep, kover); built by the first call that needs it
@@ -2125,27 +2217,38 @@ int cdlp_cache(gx_graph *g, int iters, bool relabel, CdlpCache **out, hipStream_
         GX_TRY(fresh->al.alloc((size_t)fresh->asub * kCdlpSubs * (kCdlpLists - 1)));
         GX_TRY(fresh->dense.alloc(1));
         GX_TRY(fresh->redo.alloc(std::max<size_t>(1, fresh->P.n_mid4 + fresh->P.n_mid)));
-        if (!g->directed && g->nnz > 0) {
-            // the caller's rows sorted: the first iteration is each row's first column
-            // (k_cdlp_first_sorted on the caller's graph, then moved to the relabelled order)
-            GX_TRY(fresh->tmp.alloc(n));
+        // the caller's rows sorted (A, and A' for a directed graph): the first iteration is each
+        // row's first column (undirected, k_cdlp_first_sorted) or the smallest reciprocal
+        // neighbour (directed, k_cdlp_first_dir), on the caller's graph, then moved to the
+        // relabelled order
+        auto sorted_rows = [&](const DevCSR &M, bool *ok) -> int {
+            const int64_t nnz = (int64_t)M.nnz;
+            *ok = true;
+            if (nnz == 0) return GX_SUCCESS;
             DBuf<uint32_t> bits;
             DBuf<int> flag;
-            const int64_t nnz = (int64_t)g->nnz;
             GX_TRY(bits.alloc((size_t)(nnz + 31) / 32));
             GX_TRY(flag.alloc(1));
             GX_HIP_TRY(hipMemsetAsync(bits.p, 0, (size_t)(nnz + 31) / 32 * 4, s));
             const int one = 1;
             GX_HIP_TRY(hipMemcpyAsync(flag.p, &one, sizeof(int), hipMemcpyHostToDevice, s));
-            hipLaunchKernelGGL(k_row_start_bits, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p, n, bits.p);
+            hipLaunchKernelGGL(k_row_start_bits, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, M.rp.p, n, bits.p);
             GX_TRY(check_launch("k_row_start_bits"));
-            hipLaunchKernelGGL(k_rows_sorted, dim3(grid_for(nnz, 256, 8192)), dim3(256), 0, s, g->A.ci.p, nnz, bits.p,
+            hipLaunchKernelGGL(k_rows_sorted, dim3(grid_for(nnz, 256, 8192)), dim3(256), 0, s, M.ci.p, nnz, bits.p,
                                flag.p);
             GX_TRY(check_launch("k_rows_sorted"));
             int sorted = 0;
             GX_HIP_TRY(hipMemcpyAsync(&sorted, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
             GX_HIP_TRY(hipStreamSynchronize(s));
-            fresh->rows_sorted = sorted != 0;
+            *ok = sorted != 0;
+            return GX_SUCCESS;
+        };
+        if (g->nnz > 0 && (!g->directed || g->AT.built)) {
+            GX_TRY(fresh->tmp.alloc(n));
+            bool okA = false, okT = true;
+            GX_TRY(sorted_rows(g->A, &okA));
+            if (g->directed && okA) GX_TRY(sorted_rows(g->AT, &okT));
+            fresh->rows_sorted = okA && okT;
         }
         for (hipEvent_t &e : fresh->ev) GX_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         g->cdlp = fresh;
@@ -2313,9 +2416,19 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             // on the caller's graph and vertex order (whose rows the check found sorted)
             KTimer kt(ctx, "cdlp_first", s);
             int32_t *out = relabel ? C->tmp.p : nxt;
-            hipLaunchKernelGGL(k_cdlp_first_sorted, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p,
-                               g->A.ci.p, (int64_t)0, n, out, changed, kFlagShards);
-            GX_TRY(check_launch("k_cdlp_first_sorted"));
+            if (g->directed) {
+                // GX_CDLP_FIRST_SMALL = 8 / 16 (default) / 32: the longest row one lane compares
+                const char *fs = std::getenv("GX_CDLP_FIRST_SMALL");
+                const int small = fs ? std::atoi(fs) : 16;
+                const auto kern = small == 8 ? k_cdlp_first_dir<8> : small == 32 ? k_cdlp_first_dir<32> : k_cdlp_first_dir<16>;
+                hipLaunchKernelGGL(kern, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p, g->A.ci.p, g->AT.rp.p,
+                                   g->AT.ci.p, n, out, changed, kFlagShards);
+                GX_TRY(check_launch("k_cdlp_first_dir"));
+            } else {
+                hipLaunchKernelGGL(k_cdlp_first_sorted, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p,
+                                   g->A.ci.p, (int64_t)0, n, out, changed, kFlagShards);
+                GX_TRY(check_launch("k_cdlp_first_sorted"));
+            }
             if (relabel) {   // nxt[p] = result of the caller's vertex order[p]
                 hipLaunchKernelGGL(k_cdlp_gather_i32, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, C->tmp.p,
                                    C->order.p, n, nxt);

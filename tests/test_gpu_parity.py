@@ -472,6 +472,72 @@ def test_cdlp_row_order_and_sparse(ctx, monkeypatch, first_sorted, sparse, only)
         np.testing.assert_array_equal(gpu_run(ctx, _G(t, True), "CDLP", iters=iters), O.cdlp(t, True, iters))
 
 
+def _reciprocal_graph():
+    """A directed graph for the first-iteration shortcut: short rows (one thread compares both
+    rows) with and without reciprocal edges, self loops, isolated vertices, vertices with only
+    in- or only out-edges, and long rows (more than 16 entries, one wave each) whose smallest
+    reciprocal neighbour sits past the first 64 entries of the shorter row or is absent."""
+    from ldbc_graphalytics_platforms_graphblas_amd.graphio import csr_from_edges
+    rng = np.random.default_rng(5)
+    n = 5000
+    src, dst = [rng.integers(0, n, 12000)], [rng.integers(0, n, 12000)]
+    r = rng.integers(0, n, 3000)                      # reciprocal pairs
+    src += [r, (r * 7 + 3) % n]
+    dst += [(r * 7 + 3) % n, r]
+    loops = rng.integers(0, n, 200)                   # self loops
+    src.append(loops)
+    dst.append(loops)
+    # vertex 10: 300 out-edges to 1000.., 250 in-edges from 900..; the in-row is the shorter
+    # one and its first reciprocal entry (1000) is its 101st
+    src += [np.full(300, 10), np.arange(900, 1150)]
+    dst += [np.arange(1000, 1300), np.full(250, 10)]
+    # vertex 11: 100 out, 90 in, no reciprocal neighbour
+    src += [np.full(100, 11), np.arange(2000, 2090)]
+    dst += [np.arange(3000, 3100), np.full(90, 11)]
+    # vertex 12: 17 out-edges, 2 in-edges, one reciprocal (4321): past every per-lane limit but 32
+    src += [np.full(17, 12), np.array([4321, 4000])]
+    dst += [np.arange(4310, 4327), np.full(2, 12)]
+    s, d = np.concatenate(src).astype(np.int64), np.concatenate(dst).astype(np.int64)
+    ok = ~np.isin(s, [10, 11, 12]) & ~np.isin(d, [10, 11, 12])
+    ok[-(300 + 250 + 100 + 90 + 17 + 2):] = True      # the crafted rows keep only their own edges
+    ok &= (s < 4990) | (d < 4990)                     # a few vertices isolated
+    ok &= ~np.isin(s, np.arange(4990, n)) & ~np.isin(d, np.arange(4990, n))
+    return csr_from_edges(n, s[ok], d[ok], None, symmetric=False)
+
+
+@pytest.mark.parametrize("first_sorted,small", [("1", "16"), ("1", "8"), ("1", "32"), ("0", "16")])
+def test_cdlp_first_directed(ctx, monkeypatch, first_sorted, small):
+    """The first iteration of a directed graph whose rows (A and A') are strictly sorted is the
+    smallest reciprocal neighbour, else the smallest neighbour of either direction
+    (k_cdlp_first_dir: rows up to GX_CDLP_FIRST_SMALL entries in one lane, longer ones merged by
+    the wave; GX_CDLP_FIRST_SORTED=0: the tier kernels' count); rows in random order take the
+    tier kernels.  Same labels as the oracle every time."""
+    from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
+    monkeypatch.setenv("GX_CDLP_FIRST_SORTED", first_sorted)
+    monkeypatch.setenv("GX_CDLP_FIRST_SMALL", small)
+    rc = _reciprocal_graph()
+    want1 = O.cdlp(rc, True, 1)
+    assert want1[10] == 1000 and want1[11] == 2000 and want1[12] == 4321
+    cases = [rc, _rmat(13, 8, 21, undirected=False).csr, _tier_graph(True), _shuffle_rows(rc)]
+    ctx.set_kernel_timing(True)
+    try:
+        for i, csr in enumerate(cases):
+            G = A.Graph(ctx, csr, True)
+            try:
+                for iters in (1, 2, 5):
+                    ctx.reset_kernel_stats()
+                    np.testing.assert_array_equal(A.LA_CDLP(G, iters), O.cdlp(csr, True, iters))
+                    ran = ctx.kernel_stats("cdlp_first")[0]
+                    if first_sorted == "0" or i == 3:
+                        assert ran == 0
+                    elif i == 0:
+                        assert ran == 1   # the crafted graph is duplicate-free, so its rows qualify
+            finally:
+                G.close()
+    finally:
+        ctx.set_kernel_timing(False)
+
+
 @pytest.mark.parametrize("directed", [False, True])
 def test_cdlp_huge_table_epochs(ctx, directed):
     """The huge tier's global tables are emptied by a new epoch per iteration, and cleared for
