@@ -1506,12 +1506,15 @@ __global__ __launch_bounds__(256) void k_cdlp_first_sorted(const int64_t *__rest
 // 6-step search over lanes), the chunk with the smaller last entry advanced.  Every common entry
 // is met in the round that retires its chunk, and chunks retire in ascending order, so the first
 // round with a hit holds the smallest one.  SYN-cit: at most 13 rounds, 1.4 per long row (a
-// reciprocal neighbour is usually near the front).  Wave-uniform: every lane calls it.
+// reciprocal neighbour is usually near the front).  Wave-uniform: every lane calls it.  Returns
+// the label: that entry, else the smallest entry of either row (from the first chunks).
 __device__ __forceinline__ int32_t first_dir_merge(const int32_t *__restrict__ xr, int64_t od,
                                                    const int32_t *__restrict__ yr, int64_t id, int lane) {
-    for (int64_t i = 0, j = 0; i < od && j < id;) {
-        const int32_t xa = i + lane < od ? xr[i + lane] : INT32_MAX;   // ids < n <= INT32_MAX
-        const int32_t yb = j + lane < id ? yr[j + lane] : INT32_MAX;
+    int64_t i = 0, j = 0;
+    int32_t xa = lane < od ? xr[lane] : INT32_MAX;   // ids < n <= INT32_MAX
+    int32_t yb = lane < id ? yr[lane] : INT32_MAX;
+    const int32_t lo = min(__shfl(xa, 0), __shfl(yb, 0));
+    while (i < od && j < id) {
         int pos = 0;   // entries of the in-chunk below xa
 #pragma unroll
         for (int st = 32; st; st >>= 1) pos += __shfl(yb, pos + st - 1) < xa ? st : 0;
@@ -1519,10 +1522,16 @@ __device__ __forceinline__ int32_t first_dir_merge(const int32_t *__restrict__ x
         const uint32_t h = wave_min_u32(pos < kWave && at == xa && xa != INT32_MAX ? (uint32_t)xa : 0xffffffffu);
         if (h != 0xffffffffu) return (int32_t)h;
         const int32_t xm = __shfl(xa, kWave - 1), ym = __shfl(yb, kWave - 1);
-        i += xm <= ym ? kWave : 0;
-        j += ym <= xm ? kWave : 0;
+        if (xm <= ym) {
+            i += kWave;
+            xa = i + lane < od ? xr[i + lane] : INT32_MAX;
+        }
+        if (ym <= xm) {
+            j += kWave;
+            yb = j + lane < id ? yr[j + lane] : INT32_MAX;
+        }
     }
-    return INT32_MAX;
+    return lo;
 }
 
 template <int kFirstSmall>
@@ -1574,8 +1583,7 @@ __global__ __launch_bounds__(256) void k_cdlp_first_dir(const int64_t *__restric
             const int b = __builtin_ctzll(bal);
             const int64_t u = v0 + b;
             const int64_t uob = __shfl(ob, b), uod = __shfl(od, b), uib = __shfl(ib, b), uid = __shfl(id, b);
-            const int32_t m = first_dir_merge(ciA + uob, uod, ciT + uib, uid, lane);
-            const int32_t l = m != INT32_MAX ? m : min(uod ? ciA[uob] : INT32_MAX, uid ? ciT[uib] : INT32_MAX);
+            const int32_t l = first_dir_merge(ciA + uob, uod, ciT + uib, uid, lane);
             if (lane == 0) {
                 out[u] = l;
                 any |= l != (int32_t)u;
@@ -2417,10 +2425,11 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
             KTimer kt(ctx, "cdlp_first", s);
             int32_t *out = relabel ? C->tmp.p : nxt;
             if (g->directed) {
-                // GX_CDLP_FIRST_SMALL = 8 / 16 (default) / 32: the longest row one lane compares
+                // GX_CDLP_FIRST_SMALL = 4 / 8 (default) / 16: the longest row one lane compares
+                // (SYN-cit: 32 ran 0.43 ms, 16 0.20, 8 0.185)
                 const char *fs = std::getenv("GX_CDLP_FIRST_SMALL");
-                const int small = fs ? std::atoi(fs) : 16;
-                const auto kern = small == 8 ? k_cdlp_first_dir<8> : small == 32 ? k_cdlp_first_dir<32> : k_cdlp_first_dir<16>;
+                const int small = fs ? std::atoi(fs) : 8;
+                const auto kern = small == 4 ? k_cdlp_first_dir<4> : small == 16 ? k_cdlp_first_dir<16> : k_cdlp_first_dir<8>;
                 hipLaunchKernelGGL(kern, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p, g->A.ci.p, g->AT.rp.p,
                                    g->AT.ci.p, n, out, changed, kFlagShards);
                 GX_TRY(check_launch("k_cdlp_first_dir"));

@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out/fs
 for r in 1 2; do
-for v in 8 16 32; do
+for v in 4 8 16; do
   GX_CDLP_FIRST_SMALL=$v timeout -k 10 180 python bench.py --algorithm cdlp --graph SYN-cit --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/fs/cit_$v.json 2>/dev/null || exit 1
   python -c "import json;d=json.load(open('gpurun_out/fs/cit_$v.json'));print('SYN-cit first_small=$v round $r', round(d['ms_per_step'],4), 'first', round(d['roofline']['kernels']['cdlp_first']['ms_per_run'],4))" | tee -a gpurun_out/fs/summary.txt
 done
