@@ -1499,36 +1499,45 @@ __global__ __launch_bounds__(256) void k_cdlp_first_sorted(const int64_t *__rest
 // neighbour of either direction.  Replaces the tiers' counting pass over every label (~0.45 ms
 // of SYN-cit's first iteration: a random label gather per entry).  A wave takes 64 consecutive
 // vertices: rows of at most kFirstSmall entries each are compared pair by pair in one lane's
-// registers, longer ones afterwards by the whole wave (first_dir_merge).  (A list of the long
-// rows for a second kernel cost 0.69 ms: one returning atomic per wave on one counter.)
+// registers, rows up to `medmax` entries afterwards by 16-lane groups (four rows at once), longer
+// ones by the whole wave (first_dir_merge).  (A list of the long rows for a second kernel cost
+// 0.69 ms: returning atomics on one counter.)  SYN-cit: 0.14 ms against the tiers' ~0.45.
 
-// Both rows of v merged 64 entries at a time (each out-entry looked up among the in-chunk by a
-// 6-step search over lanes), the chunk with the smaller last entry advanced.  Every common entry
-// is met in the round that retires its chunk, and chunks retire in ascending order, so the first
-// round with a hit holds the smallest one.  SYN-cit: at most 13 rounds, 1.4 per long row (a
-// reciprocal neighbour is usually near the front).  Wave-uniform: every lane calls it.  Returns
-// the label: that entry, else the smallest entry of either row (from the first chunks).
+// Both rows of v merged G entries at a time by G lanes (each out-entry looked up among the
+// in-chunk by a log2(G)-step search over the group's lanes), the chunk with the smaller last
+// entry advanced.  Every common entry is met in the round that retires its chunk, and chunks
+// retire in ascending order, so the first round with a hit holds the smallest one.  SYN-cit: at
+// most 13 rounds of 64, 1.4 per long row (a reciprocal neighbour is usually near the front).
+// Group-uniform: every lane of the group calls it (gl = lane within the group).  Returns the
+// label: that entry, else the smallest entry of either row (from the first chunks).
+template <int G>
 __device__ __forceinline__ int32_t first_dir_merge(const int32_t *__restrict__ xr, int64_t od,
-                                                   const int32_t *__restrict__ yr, int64_t id, int lane) {
+                                                   const int32_t *__restrict__ yr, int64_t id, int gl) {
     int64_t i = 0, j = 0;
-    int32_t xa = lane < od ? xr[lane] : INT32_MAX;   // ids < n <= INT32_MAX
-    int32_t yb = lane < id ? yr[lane] : INT32_MAX;
-    const int32_t lo = min(__shfl(xa, 0), __shfl(yb, 0));
+    int32_t xa = gl < od ? xr[gl] : INT32_MAX;   // ids < n <= INT32_MAX
+    int32_t yb = gl < id ? yr[gl] : INT32_MAX;
+    const int32_t lo = min(__shfl(xa, 0, G), __shfl(yb, 0, G));
     while (i < od && j < id) {
         int pos = 0;   // entries of the in-chunk below xa
 #pragma unroll
-        for (int st = 32; st; st >>= 1) pos += __shfl(yb, pos + st - 1) < xa ? st : 0;
-        const int32_t at = __shfl(yb, pos & (kWave - 1));
-        const uint32_t h = wave_min_u32(pos < kWave && at == xa && xa != INT32_MAX ? (uint32_t)xa : 0xffffffffu);
+        for (int st = G / 2; st; st >>= 1) pos += __shfl(yb, pos + st - 1, G) < xa ? st : 0;
+        const int32_t at = __shfl(yb, pos & (G - 1), G);
+        uint32_t h = pos < G && at == xa && xa != INT32_MAX ? (uint32_t)xa : 0xffffffffu;
+        if constexpr (G == kWave) {
+            h = wave_min_u32(h);
+        } else {
+#pragma unroll
+            for (int o = G / 2; o; o >>= 1) h = min(h, (uint32_t)__shfl_xor((int)h, o, G));
+        }
         if (h != 0xffffffffu) return (int32_t)h;
-        const int32_t xm = __shfl(xa, kWave - 1), ym = __shfl(yb, kWave - 1);
+        const int32_t xm = __shfl(xa, G - 1, G), ym = __shfl(yb, G - 1, G);
         if (xm <= ym) {
-            i += kWave;
-            xa = i + lane < od ? xr[i + lane] : INT32_MAX;
+            i += G;
+            xa = i + gl < od ? xr[i + gl] : INT32_MAX;
         }
         if (ym <= xm) {
-            j += kWave;
-            yb = j + lane < id ? yr[j + lane] : INT32_MAX;
+            j += G;
+            yb = j + gl < id ? yr[j + gl] : INT32_MAX;
         }
     }
     return lo;
@@ -1537,7 +1546,7 @@ __device__ __forceinline__ int32_t first_dir_merge(const int32_t *__restrict__ x
 template <int kFirstSmall>
 __global__ __launch_bounds__(256) void k_cdlp_first_dir(const int64_t *__restrict__ rpA, const int32_t *__restrict__ ciA,
                                                         const int64_t *__restrict__ rpT, const int32_t *__restrict__ ciT,
-                                                        int64_t n, int32_t *out, int *changed, int cshards) {
+                                                        int64_t n, int32_t *out, int *changed, int cshards, int medmax) {
     const int lane = threadIdx.x & (kWave - 1);
     bool any = false;
     // wave-uniform trips: v0 is the wave's first vertex
@@ -1546,13 +1555,13 @@ __global__ __launch_bounds__(256) void k_cdlp_first_dir(const int64_t *__restric
         const bool in = v < n;
         const int64_t ob = in ? rpA[v] : 0, od = in ? rpA[v + 1] - ob : 0;
         const int64_t ib = in ? rpT[v] : 0, id = in ? rpT[v + 1] - ib : 0;
-        const bool lng = od > kFirstSmall || id > kFirstSmall;
+        const int64_t wide = od > id ? od : id;
+        const bool lng = wide > kFirstSmall;
         if (in && !lng) {
             // loads clamped into the row (or to entry 0: rows_sorted implies nnz > 0) and
             // issued four at a time while any lane's rows reach that far
             int32_t x[kFirstSmall], y[kFirstSmall];
             const int64_t ra = od ? ob : 0, rb = id ? ib : 0, la = od ? od - 1 : 0, lb = id ? id - 1 : 0;
-            const int64_t wide = od > id ? od : id;
 #pragma unroll
             for (int k = 0; k < kFirstSmall; k++) {
                 x[k] = -1;
@@ -1578,12 +1587,30 @@ __global__ __launch_bounds__(256) void k_cdlp_first_dir(const int64_t *__restric
             out[v] = l;
             any |= l != (int32_t)v;
         }
-        // the long rows, one after the other, by the whole wave
-        for (uint64_t bal = __ballot(in && lng); bal; bal &= bal - 1) {
+        // rows of at most medmax entries each: four at a time, 16 lanes each; group g takes the
+        // wave's g-th, (g+4)-th, ... such row (the shuffles of the row extents run wave-wide)
+        const int grp = lane >> 4, gl = lane & 15;
+        uint64_t mb = __ballot(in && lng && wide <= medmax);
+        for (int k = 0; k < grp; k++) mb &= mb - 1;
+        while (__ballot(mb != 0)) {
+            const int b = mb ? __builtin_ctzll(mb) : 0;
+            const int64_t uob = __shfl(ob, b), uod = __shfl(od, b), uib = __shfl(ib, b), uid = __shfl(id, b);
+            if (mb) {
+                const int32_t l = first_dir_merge<16>(ciA + uob, uod, ciT + uib, uid, gl);
+                if (gl == 0) {
+                    out[v0 + b] = l;
+                    any |= l != (int32_t)(v0 + b);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) mb &= mb - 1;
+        }
+        // the longer rows, one after the other, by the whole wave
+        for (uint64_t bal = __ballot(in && lng && wide > medmax); bal; bal &= bal - 1) {
             const int b = __builtin_ctzll(bal);
             const int64_t u = v0 + b;
             const int64_t uob = __shfl(ob, b), uod = __shfl(od, b), uib = __shfl(ib, b), uid = __shfl(id, b);
-            const int32_t l = first_dir_merge(ciA + uob, uod, ciT + uib, uid, lane);
+            const int32_t l = first_dir_merge<kWave>(ciA + uob, uod, ciT + uib, uid, lane);
             if (lane == 0) {
                 out[u] = l;
                 any |= l != (int32_t)u;
@@ -2430,8 +2457,12 @@ extern "C" int gx_cdlp(gx_graph *g, int iters, uint64_t *labels) {
                 const char *fs = std::getenv("GX_CDLP_FIRST_SMALL");
                 const int small = fs ? std::atoi(fs) : 8;
                 const auto kern = small == 4 ? k_cdlp_first_dir<4> : small == 16 ? k_cdlp_first_dir<16> : k_cdlp_first_dir<8>;
+                // GX_CDLP_FIRST_MED: rows up to this many entries merged by 16-lane groups (0: off;
+                // SYN-cit first pass 0.174 ms off, 0.150 at 32, 0.158 at 64, 0.170 at 128)
+                const char *fm = std::getenv("GX_CDLP_FIRST_MED");
+                const int med = fm ? std::atoi(fm) : 32;
                 hipLaunchKernelGGL(kern, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p, g->A.ci.p, g->AT.rp.p,
-                                   g->AT.ci.p, n, out, changed, kFlagShards);
+                                   g->AT.ci.p, n, out, changed, kFlagShards, med);
                 GX_TRY(check_launch("k_cdlp_first_dir"));
             } else {
                 hipLaunchKernelGGL(k_cdlp_first_sorted, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, g->A.rp.p,

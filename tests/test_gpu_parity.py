@@ -505,16 +505,19 @@ def _reciprocal_graph():
     return csr_from_edges(n, s[ok], d[ok], None, symmetric=False)
 
 
-@pytest.mark.parametrize("first_sorted,small", [("1", "8"), ("1", "4"), ("1", "16"), ("0", "8")])
-def test_cdlp_first_directed(ctx, monkeypatch, first_sorted, small):
+@pytest.mark.parametrize("first_sorted,small,med", [("1", "8", "32"), ("1", "4", "64"), ("1", "16", "0"),
+                                                   ("1", "8", "100000"), ("0", "8", "32")])
+def test_cdlp_first_directed(ctx, monkeypatch, first_sorted, small, med):
     """The first iteration of a directed graph whose rows (A and A') are strictly sorted is the
     smallest reciprocal neighbour, else the smallest neighbour of either direction
-    (k_cdlp_first_dir: rows up to GX_CDLP_FIRST_SMALL entries in one lane, longer ones merged by
-    the wave; GX_CDLP_FIRST_SORTED=0: the tier kernels' count); rows in random order take the
-    tier kernels.  Same labels as the oracle every time."""
+    (k_cdlp_first_dir: rows up to GX_CDLP_FIRST_SMALL entries in one lane, up to
+    GX_CDLP_FIRST_MED merged by 16-lane groups, longer ones by the wave; GX_CDLP_FIRST_SORTED=0:
+    the tier kernels' count); rows in random order take the tier kernels.  Same labels as the
+    oracle every time."""
     from ldbc_graphalytics_platforms_graphblas_amd import algorithms as A
     monkeypatch.setenv("GX_CDLP_FIRST_SORTED", first_sorted)
     monkeypatch.setenv("GX_CDLP_FIRST_SMALL", small)
+    monkeypatch.setenv("GX_CDLP_FIRST_MED", med)
     rc = _reciprocal_graph()
     want1 = O.cdlp(rc, True, 1)
     assert want1[10] == 1000 and want1[11] == 2000 and want1[12] == 4321
