@@ -1,6 +1,6 @@
 """Per-iteration timeline of the last gx_cdlp call in a rocprofv3 kernel_trace.csv:
-python tools/cdlp_timeline.py kernel_trace.csv.  A call starts at k_cdlp_first_sorted (or the
-first tier kernel after a gather); iterations end at k_cdlp_flag_out."""
+python tools/cdlp_timeline.py kernel_trace.csv.  A call starts at k_cdlp_first_sorted or
+k_cdlp_first_dir (or the first tier kernel after a gather); iterations end at k_cdlp_flag_out."""
 import csv
 import re
 import sys
@@ -17,9 +17,9 @@ with open(sys.argv[1]) as f:
     for r in csv.DictReader(f):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
 rows.sort()
-starts = [i for i, r in enumerate(rows) if r[2].startswith("k_cdlp_first_sorted")]
+starts = [i for i, r in enumerate(rows) if r[2].startswith(("k_cdlp_first_sorted", "k_cdlp_first_dir"))]
 if not starts:
-    # directed graphs have no sorted first iteration: a call (relabelled) ends with the gather
+    # rows not sorted, or the shortcut off: a call (relabelled) ends with the gather
     # back to the caller's order, so the last call starts after the second-to-last gather
     ends = [i for i, r in enumerate(rows) if r[2].startswith("k_cdlp_gather_i32")]
     if len(ends) < 2:
